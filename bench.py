@@ -1,0 +1,206 @@
+#!/usr/bin/env python3
+"""Benchmark: outer RIPTRM iterations/sec on batched NonnegPCA n=4000 (BASELINE.json).
+
+One process per GPU (torchrun sets RANK/LOCAL_RANK/WORLD_SIZE); every rank owns 128 independent
+instances (global instance b -> rank b % WORLD_SIZE; weak scaling) generated on its own device.
+A "step" is one outer RIPTRM iteration of every instance of the batch (RIPTRM.py:931-968).
+``--warmup W`` outer iterations run untimed, then exactly ``--steps K`` outer iterations per
+instance are timed between barriers + device syncs; the max over ranks is the time.  The only
+collectives are the timing all_reduce and the final gather of per-instance results.
+
+The JSON line also carries:
+* roofline: the S-pass kernel (k_gemv) timed with HIP events on the stream it runs on, over the
+  timed region: algorithmic bytes (8 n^2 + 16 n per instance-pass) / summed kernel time,
+  against the 8 TB/s HBM3E peak; ``traffic`` from a committed rocprofv3 PMC summary if present;
+* cpu_baseline: the CPU oracle (vectorised NumPy "port", BLAS threads) on a bounded sample of
+  the same workload: one instance of the same n over the same outer-iteration window.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, "riemannian-interior-point-trust-region-method_amd")
+for p in (ROOT, PKG):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+METRIC = "outer RIPTRM iterations/sec, batched NonnegPCA n=4000, 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0
+
+
+def log(msg):
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
+def cpu_baseline(n: int, warmup: int, steps: int, budget_s: float):
+    """Oracle (vectorised NumPy) on one instance: outer iterations warmup+1..warmup+steps."""
+    import numpy as np
+    from oracle import nonnegpca_gen as G
+    from oracle import riptrm_oracle as O
+    try:
+        from threadpoolctl import threadpool_info
+        cores = max([d.get("num_threads", 1) for d in threadpool_info() if d.get("user_api") == "blas"] or [1])
+    except Exception:
+        cores = int(os.environ.get("OMP_NUM_THREADS", "1"))
+    Z, x0, y0 = G.generate_instance(n, G.SEED0)
+    t_start = time.time()
+    orc = O.RIPTRMOracle(dict(maxiter=warmup + steps, tolresid=0.0, maxtime=1e12, manviofun=O.sphere_manvio),
+                         deadline=t_start + budget_s)
+    P = O.NonnegPCAVectorized(Z)
+    complete = True
+    try:
+        orc.run(P, x0, y0)
+    except O.BudgetExceeded:
+        complete = False
+    heads = orc.outer_heads
+    if warmup not in heads:
+        return None
+    last = max(k for k in heads if k <= warmup + steps)
+    done = last - warmup
+    if done <= 0:
+        return None
+    el = heads[last] - heads[warmup]
+    return {"value": done / el, "unit": "outer iterations/s", "cores": int(cores), "kind": "port",
+            "sample": (f"oracle/riptrm_oracle.py NonnegPCAVectorized, 1 instance n={n} (reference generator "
+                       f"recipe, seed {G.SEED0}), outer iterations {warmup + 1}..{last} "
+                       f"({done} timed, {el:.1f} s, evaluation time excluded as RIPTRM.py:932-941; "
+                       f"{'complete' if complete else 'budget-truncated'} window), NumPy/OpenBLAS {cores} threads")}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10, help="timed outer iterations per instance")
+    ap.add_argument("--warmup", type=int, default=2, help="untimed outer iterations per instance")
+    ap.add_argument("--n", type=int, default=4000)
+    ap.add_argument("--batch", type=int, default=128, help="instances per GPU")
+    ap.add_argument("--cpu-budget", type=float, default=25.0, help="seconds of CPU-baseline sampling (0 = skip)")
+    ap.add_argument("--seed0", type=int, default=20251212)
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_gemv.json"))
+    args = ap.parse_args()
+
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", torch.cuda.current_device())
+
+    import engine
+    from problems import manviofun
+
+    n, B, W, K = args.n, args.batch, args.warmup, args.steps
+    eng = engine.NonnegPCABatch(n, B, log_capacity=2048)
+    log(f"rank {rank}/{world}: generating {B} instances n={n} ({B * eng.inst_stride * 8 / 1e9:.1f} GB S)")
+    # global instance ids owned by this rank: rank, rank+world, ... (seed seed0 + id)
+    gen_ids = [rank + world * i for i in range(B)]
+    xg, yg = eng.generate_synthetic(args.seed0, ids=gen_ids)
+    opt = {"TRS_solver": "tCG", "second_order_stationarity": False, "maxiter": W + K, "tolresid": 0.0,
+           "maxtime": math.inf, "manviofun": manviofun}
+    eng.begin(xg, yg, opt)
+    torch.cuda.synchronize(dev)
+    t0 = time.time()
+    eng.run_until(W)
+    torch.cuda.synchronize(dev)
+    log(f"rank {rank}: warmup ({W} outer iterations) {time.time() - t0:.2f}s")
+    st0 = eng.stats()
+    engine.profile_enable(eng, True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    eng.run_until(W + K)
+    torch.cuda.synchronize(dev)
+    el = time.perf_counter() - t0
+    if world > 1:
+        dist.barrier()
+    prof = engine.profile_read(eng)
+    engine.profile_enable(eng, False)
+    st1 = eng.stats()
+    C = engine.C
+    d = lambda f: float((st1[:, C[f"RIPTRM_STAT_{f}"]] - st0[:, C[f"RIPTRM_STAT_{f}"]]).sum())
+    outer = d("OUTER_ITERS")
+    passes, inner, tcg = d("PASSES"), d("INNER_ITERS"), d("TCG_ITERS")
+    counts = torch.tensor([outer, passes, inner, tcg, prof["gemv_ms"], prof["gemv_launches"]],
+                          dtype=torch.float64, device=dev)
+    tmax = torch.tensor([el], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(counts, op=dist.ReduceOp.SUM)
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+        # final gather of per-instance results (x, y, stats) over RCCL
+        res = eng.result()
+        gx = [torch.empty_like(res.x) for _ in range(world)]
+        dist.all_gather(gx, res.x.contiguous())
+    T = float(tmax.item())
+    outer_all, passes_all, inner_all, tcg_all, gemv_ms_all, gemv_n_all = [float(v) for v in counts.tolist()]
+
+    if rank == 0:
+        bytes_per_pass = 8.0 * n * n + 16.0 * n
+        # rank-0 kernel timing (every rank runs the same kernel on its own batch)
+        gemv_s = prof["gemv_ms"] / 1e3
+        passes_r0 = float((st1[:, C["RIPTRM_STAT_PASSES"]] - st0[:, C["RIPTRM_STAT_PASSES"]]).sum())
+        achieved = (passes_r0 * bytes_per_pass / gemv_s / 1e9) if gemv_s > 0 else None
+        nl = max(1, int(prof["gemv_launches"]))
+        traffic = None
+        if os.path.exists(args.traffic_json):
+            try:
+                tj = json.load(open(args.traffic_json))
+                if tj.get("n") == n:
+                    # per-launch HBM bytes scaled to this run's mean instances per launch
+                    traffic = tj["hbm_bytes_per_instance_pass"] * passes_r0 / nl
+            except Exception as e:  # pragma: no cover
+                log(f"traffic json unreadable: {e}")
+        cpu = None
+        if args.cpu_budget > 0 and world == 1:
+            log("CPU baseline (oracle) ...")
+            cpu = cpu_baseline(n, W, K, args.cpu_budget)
+        out = {
+            "metric": METRIC,
+            "value": outer_all / T,
+            "unit": "outer iterations/s",
+            "n_gpus": world,
+            "steps": K,
+            "warmup": W,
+            "ms_per_step": T / K * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (reference generator recipe src/NonnegPCA/generator.py:9-65, drawn on device)",
+            "config": {"workload": f"NonnegPCA n={n}, batch of {B} independent instances per GPU "
+                                   f"(BASELINE configs[2]; configs[3] at 8 GPUs)",
+                       "n": n, "batch_per_gpu": B, "global_batch": B * world,
+                       "outer_window": [W + 1, W + K], "parallelism": f"instance-sharded x{world}"},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
+                         "traffic": traffic,
+                         "kernel": "k_gemv (S-pass)",
+                         "bytes_per_launch": passes_r0 * bytes_per_pass / nl,
+                         "avg_launch_us": prof["gemv_ms"] * 1e3 / nl},
+            "cpu_baseline": cpu,
+            "detail": {"inner_iterations_per_s": inner_all / T, "tcg_iterations_per_s": tcg_all / T,
+                       "s_passes_per_s": passes_all / T, "gemv_time_frac": (prof["gemv_ms"] / 1e3) / T,
+                       "state_kernel_ms": prof["state_ms"], "state_launches": prof["state_launches"],
+                       "gemv_launches": prof["gemv_launches"]},
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

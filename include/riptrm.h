@@ -1,0 +1,195 @@
+/*
+ * riptrm.h — C-ABI of the MI355X (gfx950) RIPTRM tCG hot path.
+ *
+ * One shared library (libriptrm_hip.so) exports these symbols.  Every pointer argument is
+ * caller-owned DEVICE memory (fp64 unless stated, contiguous, row-major), every call enqueues
+ * on the hipStream_t bound to the context and never allocates device memory; only the calls
+ * documented as "synchronises" block the host.  Every function returns 0 on success and a
+ * negative RIPTRM_E_* code on failure; riptrm_last_error() returns the message.  Nothing
+ * throws across the ABI.
+ *
+ * Reference interfaces replaced (paths relative to the reference repository root):
+ *   riptrm_nonnegpca_hvp      HwCur(dx), src/solver/RIPTRM.py:729 = hessLagrangefun :491-523
+ *                             + Gxfun :525-551 ∘ (y ⊙ Gxajfun :553-571 ⊘ s), NonnegPCA callbacks
+ *                             src/NonnegPCA/coordinator.py:46-77 (egrad/ehess via autograd)
+ *   riptrm_tcg_*              truncated_conjugate_gradient, src/solver/RIPTRM.py:41-216, as
+ *                             called by compute_direction :445-452 (eta0 = 0, maxinner = dim)
+ *   riptrm_solve_*            RIPTRM.run :909-976 -> outer_step :866-896 -> inner_run :785-847
+ *                             -> inner_step :707-783 -> update_xy_TR_radius :631-705, with
+ *                             the KKT evaluation of src/solver/utils.py:269-368 for the log
+ *   riptrm_nonnegpca_symmetrize  S = Z + Z^T (the Hessian of -x^T Z x, coordinator.py:52-54)
+ */
+#ifndef RIPTRM_H
+#define RIPTRM_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RIPTRM_ABI_VERSION 1
+
+/* status codes */
+#define RIPTRM_OK 0
+#define RIPTRM_E_ARG -1      /* bad argument (null pointer, size, alignment) */
+#define RIPTRM_E_HIP -2      /* a HIP runtime call failed */
+#define RIPTRM_E_STATE -3    /* call out of order (e.g. solve before bind) */
+#define RIPTRM_E_NODEV -4    /* no usable gfx950 device */
+
+/* tCG stop codes (RIPTRM.py:95,143,145,164,188,190) */
+#define RIPTRM_TCG_MAX_INNER_ITER 0
+#define RIPTRM_TCG_NEGATIVE_CURVATURE 1
+#define RIPTRM_TCG_EXCEEDED_TR 2
+#define RIPTRM_TCG_MODEL_INCREASED 3
+#define RIPTRM_TCG_REACHED_TARGET_LINEAR 4
+#define RIPTRM_TCG_REACHED_TARGET_SUPERLINEAR 5
+
+/* inner_status codes (RIPTRM.py:763,770,678,698,829,837); 0 = None */
+#define RIPTRM_IS_NONE 0
+#define RIPTRM_IS_INITIAL 1
+#define RIPTRM_IS_CONVERGED 2
+#define RIPTRM_IS_PRIMAL_INFEASIBLE 3
+#define RIPTRM_IS_SUCCESSFUL 4
+#define RIPTRM_IS_UNSUCCESSFUL 5
+#define RIPTRM_IS_MAX_TIME_EXCEEDED 6
+#define RIPTRM_IS_MAX_ITER_EXCEEDED 7
+
+/* radius_update codes (RIPTRM.py:668,671,674); 0 = None */
+#define RIPTRM_RU_NONE 0
+#define RIPTRM_RU_REDUCED 1
+#define RIPTRM_RU_EXPANDED 2
+#define RIPTRM_RU_UNCHANGED 3
+
+/* stopping criterion codes (base_solver.py:94-105, RIPTRM.py:944) */
+#define RIPTRM_STOP_NONE 0
+#define RIPTRM_STOP_MAXTIME 1
+#define RIPTRM_STOP_MAXITER 2
+#define RIPTRM_STOP_TOLRESID 3
+
+/* manifold-violation kinds for the KKT residual (option 'manviofun') */
+#define RIPTRM_MANVIO_ZERO 0     /* RIPTRM.py:347 default: lambda problem, x: 0 */
+#define RIPTRM_MANVIO_SPHERE 1   /* src/NonnegPCA/simulator.py:12-14: ||x|| - 1 */
+
+/* Per-inner-iteration log record: RIPTRM_LOG_NFIELDS doubles, field order below.
+ * Columns = evaluation keys (utils.py:356-364) + solver_status keys (RIPTRM.py:986-1023). */
+enum riptrm_log_field {
+    RIPTRM_LOG_ITERATION = 0, RIPTRM_LOG_TIME, RIPTRM_LOG_COST, RIPTRM_LOG_DISTANCE,
+    RIPTRM_LOG_RESIDUAL, RIPTRM_LOG_GRADNORM, RIPTRM_LOG_COMPLVIOLATION, RIPTRM_LOG_DUALVIOLATION,
+    RIPTRM_LOG_MANVIOLATION, RIPTRM_LOG_MAXVIOLATION, RIPTRM_LOG_MEANVIOLATION, RIPTRM_LOG_MU,
+    RIPTRM_LOG_HAS_INFO, RIPTRM_LOG_NUM_INNER, RIPTRM_LOG_INNER_STATUS, RIPTRM_LOG_TR_RADIUS,
+    RIPTRM_LOG_DXTYPE, RIPTRM_LOG_NORMDX, RIPTRM_LOG_MINXFEASI, RIPTRM_LOG_MINYFEASI,
+    RIPTRM_LOG_COMPL, RIPTRM_LOG_HAS_RATIO, RIPTRM_LOG_ARED_PRED, RIPTRM_LOG_RADIUS_UPDATE,
+    RIPTRM_LOG_DUAL_CLIPPING, RIPTRM_LOG_MAXABSLAGMULT, RIPTRM_LOG_TCG_ITERS,
+    RIPTRM_LOG_NFIELDS_USED
+};
+#define RIPTRM_LOG_NFIELDS 32
+
+/* Per-instance result record: RIPTRM_STAT_NFIELDS doubles. */
+enum riptrm_stat_field {
+    RIPTRM_STAT_OUTER_ITERS = 0, RIPTRM_STAT_INNER_ITERS, RIPTRM_STAT_TCG_ITERS, RIPTRM_STAT_PASSES,
+    RIPTRM_STAT_STOP_CODE, RIPTRM_STAT_STOP_RUNTIME, RIPTRM_STAT_FINAL_RESIDUAL, RIPTRM_STAT_LOG_COUNT,
+    RIPTRM_STAT_LOG_OVERFLOW, RIPTRM_STAT_PHASE, RIPTRM_STAT_MU, RIPTRM_STAT_TR_RADIUS,
+    RIPTRM_STAT_TCG_LAST_J, RIPTRM_STAT_TCG_LAST_STOP, RIPTRM_STAT_ERROR,
+    RIPTRM_STAT_NFIELDS_USED
+};
+#define RIPTRM_STAT_NFIELDS 16
+
+/* Solver options: the tCG-path keys of the RIPTRM default_option (RIPTRM.py:305-358).
+ * Option callables (forcing functions, barrier schedule) are evaluated by the host into the
+ * per-outer-iteration tables passed to riptrm_solve_begin(). */
+typedef struct riptrm_options {
+    int32_t struct_size;              /* = sizeof(riptrm_options) */
+    int32_t maxiter;                  /* 'maxiter' */
+    int32_t inner_maxiter;            /* 'inner_maxiter', -1 = None */
+    int32_t tcg_mininner;             /* 'tCG_mininner' */
+    int32_t save_inner_iteration;     /* 'save_inner_iteration' (bool) */
+    int32_t manvio_kind;              /* RIPTRM_MANVIO_* */
+    int32_t log_capacity;             /* log records per instance (<= the bound capacity) */
+    int32_t reserved0;
+    double maxtime;                   /* 'maxtime' seconds (INFINITY allowed) */
+    double inner_maxtime;             /* 'inner_maxtime' seconds, < 0 = None */
+    double tolresid;                  /* 'tolresid' */
+    double initial_tr_radius;         /* 'initial_TR_radius' (host resolves None -> pi/8) */
+    double minimal_initial_tr_radius; /* 'minimal_initial_TR_radius' */
+    double maximal_tr_radius;         /* 'maximal_TR_radius' */
+    double rho;                       /* 'rho' */
+    double reduction_regularization;  /* 'reduction_regularization' */
+    double gamma;                     /* 'gamma' */
+    double tcg_theta;                 /* 'tCG_theta' */
+    double tcg_kappa;                 /* 'tCG_kappa' */
+    double const_left;                /* 'const_left' */
+    double const_right;               /* 'const_right' */
+} riptrm_options;
+
+typedef struct riptrm_ctx riptrm_ctx;
+
+int riptrm_abi_version(void);
+
+/* Create a context on `device` that enqueues on `stream` (a hipStream_t; NULL = default). */
+int riptrm_ctx_create(riptrm_ctx** out, int device, void* stream);
+int riptrm_ctx_destroy(riptrm_ctx* ctx);
+const char* riptrm_last_error(const riptrm_ctx* ctx);
+/* Rebind the stream (e.g. torch.cuda.current_stream()). */
+int riptrm_ctx_set_stream(riptrm_ctx* ctx, void* stream);
+
+/* ---- layout (pure functions, no device work) ---- */
+/* Leading dimension (doubles) of one padded row of S and of every state vector. */
+int64_t riptrm_nonnegpca_ld(int32_t n);
+/* Rows of one padded instance of S (multiple of the mat-vec row block). */
+int64_t riptrm_nonnegpca_rows(int32_t n);
+/* Device workspace bytes for a batch (state vectors, scalars, log, counters). */
+int64_t riptrm_workspace_bytes(int32_t n, int32_t batch, int32_t log_capacity);
+/* Byte offsets inside the workspace.  kind: 0 = x, 1 = y, 2 = eta (last dx), 3 = Heta,
+ * 4 = stats (batch x RIPTRM_STAT_NFIELDS doubles), 5 = log (batch x capacity x NFIELDS). */
+int64_t riptrm_workspace_offset(int32_t n, int32_t batch, int32_t log_capacity, int32_t kind);
+
+/* ---- data preparation ---- */
+/* In place: S_b <- Z_b + Z_b^T for b < batch, where each instance is a padded
+ * (riptrm_nonnegpca_rows(n) x ld) block starting at S + b*inst_stride holding Z_b in its
+ * leading n x n corner; padding rows/columns are zeroed. */
+int riptrm_nonnegpca_symmetrize(riptrm_ctx* ctx, double* S, int32_t n, int32_t batch,
+                                int64_t ld, int64_t inst_stride);
+
+/* ---- bind a batch of NonnegPCA instances sharing n (the hydra multi-run axis) ---- */
+int riptrm_nonnegpca_bind(riptrm_ctx* ctx, const double* S, int32_t n, int32_t batch,
+                          int64_t ld, int64_t inst_stride, void* workspace,
+                          int64_t workspace_bytes, int32_t log_capacity);
+
+/* ---- operator entry points (parity / building blocks) ---- */
+/* out_b = HwCur_b(v_b) at (x_b, y_b, mu), s = x (NonnegPCA slack).  x, y, v, out: batch x ldv. */
+int riptrm_nonnegpca_hvp(riptrm_ctx* ctx, const double* x, const double* y, double mu,
+                         const double* v, double* out, int64_t ldv);
+/* Batched tCG at (x_b, y_b, mu_b, Delta_b): eta/Heta written into the workspace vectors
+ * (offset kinds 2/3); iters_b = loop index j at exit (RIPTRM.py:216 returns j), stop_b code.
+ * x, y: batch x ldv; mu, delta: batch doubles; iters, stop: batch int32.  Synchronises. */
+int riptrm_tcg(riptrm_ctx* ctx, const double* x, const double* y, int64_t ldv,
+               const double* mu, const double* delta, int32_t* iters, int32_t* stop,
+               int32_t max_steps);
+
+/* ---- full solve ---- */
+/* Start a batched RIPTRM run from x0/y0 (batch x ldv).  mu_table[k] = barrier parameter of
+ * outer step k+1 (k = 0..table_len-1), tolL/tolC = the forcing functions of mu_table. */
+int riptrm_solve_begin(riptrm_ctx* ctx, const riptrm_options* opt, const double* x0,
+                       const double* y0, int64_t ldv, const double* mu_table,
+                       const double* tolL_table, const double* tolC_table, int32_t table_len);
+/* Enqueue up to `steps` lock-step iterations (one S-pass for every instance that still needs
+ * one + one state-machine advance).  Instances pause before starting outer iteration number
+ * `outer_target` + 1 (pass INT32_MAX to run to completion).  Synchronises and returns the
+ * number of instances still running in *n_active. */
+int riptrm_solve_advance(riptrm_ctx* ctx, int32_t steps, int32_t outer_target, int32_t* n_active);
+/* Device timestamps for timing windows: wall-clock ticks per second of the device clock. */
+double riptrm_device_clock_hz(riptrm_ctx* ctx);
+
+/* ---- measurement ---- */
+/* Enable/disable HIP-event timing of every S-pass (k_gemv) and state-machine (k_state) launch
+ * enqueued by riptrm_solve_advance / riptrm_tcg; enabling resets the totals.  Synchronises. */
+int riptrm_profile_enable(riptrm_ctx* ctx, int32_t on);
+/* Summed device time (ms) and launch counts since the last enable.  Synchronises. */
+int riptrm_profile_read(riptrm_ctx* ctx, double* gemv_ms, int64_t* gemv_launches, double* state_ms,
+                        int64_t* state_launches);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RIPTRM_H */

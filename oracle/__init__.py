@@ -1,0 +1,4 @@
+"""CPU oracle package — TEST INFRASTRUCTURE ONLY (see riptrm_oracle.py header).
+
+Importable only by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg.
+"""

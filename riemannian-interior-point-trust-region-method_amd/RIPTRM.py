@@ -1,0 +1,92 @@
+"""Drop-in ``RIPTRM`` solver plugin (MI355X / gfx950).
+
+Same plugin contract as the reference ``src/solver/RIPTRM.py``: the simulator imports the
+module named ``RIPTRM`` from its solver path and calls ``RIPTRM(option).run(problem)``
+(``src/base/base_simulator.py:51-67``), getting an ``Output(name, x, option, log, ineqLagmult,
+eqLagmult)`` whose ``log`` has the reference's columns, one row per inner iteration
+(``RIPTRM.py:812-818``).  Differences, all explicit errors rather than silent fallbacks:
+
+* only ``TRS_solver='tCG'`` (what every shipped config selects) — ``Exact_RepMat`` raises;
+* the problem is a structured descriptor (``problems.NonnegPCAProblem``) instead of a list of
+  autograd closures, because closures cannot execute on the GPU;
+* ``manviofun`` must be 0 or the NonnegPCA simulator's ``||x|| - 1``; ``callbackfun`` and
+  wandb are not supported.
+
+``run_batch(problems)`` solves many instances of the same size at once (the reference runs its
+Hydra multi-run axis one after another, ``config_simulation.yaml:35-42``).
+"""
+from __future__ import annotations
+
+import copy
+import warnings
+from typing import Any, Dict, List, Sequence
+
+import numpy as np
+import torch
+
+from engine import NonnegPCABatch, REFERENCE_DEFAULTS, resolve_options
+from problems import NonnegPCAProblem
+from solver_base import Output, Solver
+
+
+class RIPTRM(Solver):
+    """Riemannian interior point trust region method, tCG subproblem solver on the GPU."""
+
+    def __init__(self, option: Dict[str, Any]):
+        merged = dict(REFERENCE_DEFAULTS)
+        merged.update(option)
+        self.option = merged
+        self.excluded_time = 0
+        self.log: Dict[str, list] = {}
+        self.name = f"RIPTRM_{self.option['TRS_solver']}"
+        self.initialize_wandb()
+        resolve_options(self.option, np.pi, 1)  # validate early (raises on unsupported options)
+        self.last_batch = None
+
+    def run(self, problem) -> Output:
+        return self.run_batch([problem])[0]
+
+    def run_batch(self, problems: Sequence[Any], log_capacity: int = 8192) -> List[Output]:
+        problems = list(problems)
+        if not problems:
+            return []
+        for p in problems:
+            if not isinstance(p, NonnegPCAProblem):
+                raise NotImplementedError(
+                    f"RIPTRM (MI355X) needs a structured problem (problems.NonnegPCAProblem), got {type(p).__name__}")
+            if p.has_eqconstraints:
+                warnings.warn("Equality constraints detecred. Currently, RIPTRM does not support equality "
+                              "constraints and will completely ignore them.", Warning)
+        n = problems[0].n
+        if any(p.n != n for p in problems):
+            raise ValueError("run_batch needs instances of equal dimension n (group them by n)")
+        B = len(problems)
+        eng = NonnegPCABatch(n, B, log_capacity=log_capacity)
+        Z = np.stack([np.asarray(p.Z.cpu() if hasattr(p.Z, "cpu") else p.Z, dtype=np.float64) for p in problems])
+        eng.load_Z(Z)
+        x0 = np.stack([np.asarray(p.initialpoint, dtype=np.float64) for p in problems])
+        y0 = np.stack([np.asarray(p.initialineqLagmult, dtype=np.float64) for p in problems])
+        res = eng.solve(x0, y0, self.option)
+        self.last_batch = res
+        outs = []
+        xs = res.x.cpu().numpy()
+        ys = res.y.cpu().numpy()
+        for b in range(B):
+            opt = copy.copy(self.option)
+            reason = res.stopping_criterion(b)
+            if reason is not None:
+                opt["stoppingcriterion"] = reason
+            if int(res.stat(b, "LOG_OVERFLOW")) > 0:
+                warnings.warn(f"instance {b}: log capacity {log_capacity} exceeded; later rows dropped")
+            log = res.log(b)
+            if self.option.get("verbosity", 0) == 1:
+                for it, c, r, m, st in zip(log["iteration"], log["cost"], log["residual"], log["mu"],
+                                           log["inner_status"]):
+                    if st in (None, "converged", "max-time-exceeded", "max-iter-exceeded"):
+                        print(f"Outer iteration: {it}, Cost: {c}, KKT residual: {r}, mu: {m}")
+                if reason:
+                    print(reason)
+            outs.append(Output(name=self.name, x=xs[b].copy(), option=opt, log=log,
+                               ineqLagmult=ys[b].copy(), eqLagmult=[]))
+        self.log = outs[0].log if B == 1 else {}
+        return outs

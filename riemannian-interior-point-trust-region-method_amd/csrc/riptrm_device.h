@@ -1,0 +1,112 @@
+// riptrm_device.h — device-side layout shared by the kernels and the C-ABI host code.
+//
+// Workspace (one allocation, caller-owned, zeroed at bind):
+//   [vectors]  NVEC x batch x ld doubles          per-instance state vectors (SoA per kind)
+//   [state]    batch x ST_N doubles               per-instance scalars (see enum St)
+//   [stats]    batch x RIPTRM_STAT_NFIELDS        host-visible results
+//   [log]      batch x cap x RIPTRM_LOG_NFIELDS   per-inner-iteration log rows
+//   [lists]    2 x batch int32                    active-instance lists (ping-pong)
+//   [req]      batch int32                        right-hand sides wanted per instance (1|2)
+//   [counters] 4 int32                            list lengths (ping-pong) + spare
+#pragma once
+#include <stdint.h>
+#include "../../include/riptrm.h"
+
+namespace riptrm {
+
+// rows of S handled by one mat-vec workgroup (4 waves x GV_RW rows)
+constexpr int GV_THREADS = 256;
+constexpr int GV_RW = 4;
+constexpr int GV_RB = (GV_THREADS / 64) * GV_RW;
+// state-machine workgroup
+constexpr int ST_THREADS = 512;
+constexpr int ST_WAVES = ST_THREADS / 64;
+
+// state vector kinds
+enum Vec : int {
+  V_X = 0, V_Y, V_ETA, V_HETA,   // 0..3 fixed so riptrm_workspace_offset kinds 0..3 map here
+  V_SX, V_X0, V_Y0, V_SX0, V_XPREV, V_R, V_IN0, V_IN1, V_OUT0, V_OUT1, V_YNEW, V_C,
+  NVEC
+};
+
+// per-instance scalar slots (all stored as double; integers are exact below 2^53)
+enum St : int {
+  ST_PHASE = 0, ST_MODE, ST_OUTER_IT, ST_INNER_IT, ST_MU_IDX, ST_MU, ST_DELTA, ST_DELTA0,
+  ST_DELTA_STEP, ST_T_START, ST_T_INNER, ST_TOLL, ST_TOLC,
+  // hoisted per inner step
+  ST_XX, ST_XSX, ST_YX, ST_COEF, ST_FCUR,
+  // tCG
+  ST_EPE, ST_EPD, ST_DPD, ST_ZR, ST_NORMR0, ST_MODEL, ST_J, ST_TCG_STOP,
+  // trial
+  ST_NORMDX, ST_XDX, ST_MINX, ST_MINY, ST_COMPL, ST_XFEAS, ST_YFEAS,
+  ST_HOT_END,
+  // cold: thread-0-owned counters
+  ST_TCG_TOTAL = 40, ST_INNER_TOTAL, ST_PASSES, ST_LOG_COUNT, ST_LOG_OVERFLOW, ST_STOP_CODE,
+  ST_STOP_RUNTIME, ST_RESIDUAL,
+  // last inner_info (for save_inner_iteration == False rows)
+  ST_I_HAS, ST_I_NUM, ST_I_STATUS, ST_I_TR, ST_I_DXTYPE, ST_I_NORMDX, ST_I_MINX, ST_I_MINY,
+  ST_I_COMPL, ST_I_HASRATIO, ST_I_RATIO, ST_I_RU, ST_I_DC,
+  ST_ERROR,
+  ST_N_USED
+};
+constexpr int ST_N = 64;
+constexpr int ST_HOT = ST_HOT_END;
+static_assert(ST_HOT_END <= 40, "hot scalar slots overflow into cold ones");
+static_assert(ST_N_USED <= ST_N, "state slots overflow");
+
+enum Phase : int {
+  PH_IDLE = 0, PH_START, PH_AFTER_SX0, PH_TCG, PH_TRIAL, PH_PAUSED, PH_DONE,
+  PH_TCGO_START, PH_TCGO_SX, PH_ERROR
+};
+
+enum Mode : int { MODE_SOLVE = 0, MODE_TCG_ONLY = 1 };
+
+struct Layout {
+  int32_t n, batch, cap;
+  int64_t ld;
+  int64_t off_vec, off_state, off_stats, off_log, off_lists, off_req, off_cnt, total;
+};
+
+inline int64_t round_up(int64_t a, int64_t m) { return (a + m - 1) / m * m; }
+inline int64_t ld_of(int32_t n) { return round_up(n > 0 ? n : 1, 16); }
+inline int64_t rows_of(int32_t n) { return round_up(n > 0 ? n : 1, GV_RB); }
+
+inline Layout make_layout(int32_t n, int32_t batch, int32_t cap) {
+  Layout L;
+  L.n = n; L.batch = batch; L.cap = cap; L.ld = ld_of(n);
+  int64_t o = 0;
+  L.off_vec = o;   o += (int64_t)NVEC * batch * L.ld * 8;               o = round_up(o, 256);
+  L.off_state = o; o += (int64_t)batch * ST_N * 8;                       o = round_up(o, 256);
+  L.off_stats = o; o += (int64_t)batch * RIPTRM_STAT_NFIELDS * 8;        o = round_up(o, 256);
+  L.off_log = o;   o += (int64_t)batch * cap * RIPTRM_LOG_NFIELDS * 8;   o = round_up(o, 256);
+  L.off_lists = o; o += (int64_t)2 * batch * 4;                          o = round_up(o, 256);
+  L.off_req = o;   o += (int64_t)batch * 4;                              o = round_up(o, 256);
+  L.off_cnt = o;   o += 16;                                              o = round_up(o, 256);
+  L.total = o;
+  return L;
+}
+
+// Kernel parameter block (passed by value).
+struct DevParams {
+  const double* S;      // batch x rows x ld
+  int64_t inst_stride;  // doubles between instances of S
+  int64_t ld;
+  int32_t n, batch, cap;
+  int32_t nrb;          // row blocks per instance
+  double* vec;          // workspace vectors
+  double* st;           // workspace scalars
+  double* stats;
+  double* log;
+  int32_t* lists;       // 2 x batch
+  int32_t* req;
+  int32_t* cnt;
+  const double* mu_tab;
+  const double* tolL_tab;
+  const double* tolC_tab;
+  int32_t tab_len;
+  int32_t outer_target;
+  double clock_hz;
+  riptrm_options opt;
+};
+
+}  // namespace riptrm

@@ -1,0 +1,1328 @@
+// riptrm_kernels.hip — MI355X (gfx950) kernels for the RIPTRM tCG hot path + the C-ABI.
+//
+// Work per lock-step iteration of a batch of independent NonnegPCA instances:
+//   k_gemv   : one pass over every active instance's S = Z + Z^T (fp64, HBM-bound):
+//              out0 = S*in0 (and out1 = S*in1 for the trial point's 2-RHS pass).
+//   k_state  : one 1024-thread workgroup per active instance advances the RIPTRM state machine
+//              (barrier Hessian epilogue, tCG iteration, trial point, ratio test, dual clipping,
+//              inner/outer loop control, KKT evaluation + log row) until it needs the next S-pass.
+// Reference restated: src/solver/RIPTRM.py:41-216 (tCG), :491-571 + :729-730 (barrier Hessian
+// and gradient), :574-629 (inner stopping test), :631-705 (acceptance / TR radius), :707-896
+// (inner/outer loops), :909-976 (run), src/solver/utils.py:269-368 (KKT residual, evaluation).
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <string>
+#include <vector>
+#include <cstring>
+#include <cstdio>
+#include "riptrm_device.h"
+
+namespace riptrm {
+
+// Elementwise arithmetic must round exactly like NumPy (no contraction into FMA).
+#pragma clang fp contract(off)
+
+typedef double dbl2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ double* vp(const DevParams& P, int k, int b) {
+  return P.vec + ((int64_t)k * P.batch + b) * P.ld;
+}
+
+// ------------------------------------------------------------------------------------------
+// Workgroup reductions (ST_THREADS threads).  Every thread ends with the bitwise-identical
+// result, so all scalar control flow downstream is uniform across the workgroup.
+// op per slot: 0 = sum, 1 = min (NaN-ignoring), 2 = max (NaN-ignoring).
+// ------------------------------------------------------------------------------------------
+constexpr int RED_MAX = 10;
+struct Red {
+  double* buf;  // LDS [2][ST_WAVES][RED_MAX]
+  int parity;
+};
+
+// lane l <- lane (l ^ off) for one double: two ds_bpermute_b32, no bounds select (64 lanes)
+__device__ __forceinline__ double xor_lane(double v, int off) {
+  const int addr = ((int)__lane_id() ^ off) << 2;
+  const int lo = __builtin_amdgcn_ds_bpermute(addr, __double2loint(v));
+  const int hi = __builtin_amdgcn_ds_bpermute(addr, __double2hiint(v));
+  return __hiloint2double(hi, lo);
+}
+
+__device__ __forceinline__ double comb(int op, double a, double b) {
+  return op == 0 ? a + b : (op == 1 ? fmin(a, b) : fmax(a, b));
+}
+
+template <int K>
+__device__ __forceinline__ void bred(Red& R, double (&v)[K], const int (&op)[K]) {
+  static_assert(K <= RED_MAX, "too many reduction slots");
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    double a = v[k];
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) a = comb(op[k], a, xor_lane(a, off));
+    v[k] = a;
+  }
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  double* b = R.buf + R.parity * (ST_WAVES * RED_MAX);
+  if (lane == 0) {
+#pragma unroll
+    for (int k = 0; k < K; ++k) b[w * RED_MAX + k] = v[k];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    double s = b[k];
+    for (int i = 1; i < ST_WAVES; ++i) s = comb(op[k], s, b[i * RED_MAX + k]);
+    v[k] = s;
+  }
+  R.parity ^= 1;
+}
+
+template <int K>
+__device__ __forceinline__ void bsum(Red& R, double (&v)[K]) {
+  int op[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) op[k] = 0;
+  bred<K>(R, v, op);
+}
+
+// numpy.minimum / numpy.maximum (NaN-propagating) used by the dual clipping (RIPTRM.py:681-683)
+__device__ __forceinline__ double np_min(double a, double b) {
+  return (isnan(a) || isnan(b)) ? NAN : (b < a ? b : a);
+}
+__device__ __forceinline__ double np_max(double a, double b) {
+  return (isnan(a) || isnan(b)) ? NAN : (b > a ? b : a);
+}
+
+// ------------------------------------------------------------------------------------------
+// k_gemv: batched fp64 mat-vec over the active instances.  Workgroup = GV_RB rows of one
+// instance; each wave owns GV_RW rows and streams them in 1 KiB (64 lanes x 16 B) column
+// chunks, v read as 16 B per lane (L1/L2-resident, 32 KiB per instance at n = 4000), FMAs into
+// per-lane partials, then a 64-lane butterfly per row.  S is read exactly once per pass.
+// ------------------------------------------------------------------------------------------
+template <int NR>
+__device__ __forceinline__ void gemv_rows(const DevParams& P, int b, int rb) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int row0 = rb * GV_RB + w * GV_RW;
+  const int64_t ld = P.ld;
+  const double* __restrict__ Sb = P.S + (int64_t)b * P.inst_stride + (int64_t)row0 * ld;
+  const double* __restrict__ v0 = vp(P, V_IN0, b);
+  const double* __restrict__ v1 = vp(P, V_IN1, b);
+  double a0[GV_RW], a1[GV_RW];
+#pragma unroll
+  for (int k = 0; k < GV_RW; ++k) { a0[k] = 0.0; a1[k] = 0.0; }
+
+  int64_t col = 2 * lane;
+  // main loop: two 1 KiB chunks per row in flight per iteration
+  for (; col + 128 < ld; col += 256) {
+    dbl2 s[2][GV_RW];
+#pragma unroll
+    for (int k = 0; k < GV_RW; ++k) {
+      s[0][k] = __builtin_nontemporal_load((const dbl2*)(Sb + k * ld + col));
+      s[1][k] = __builtin_nontemporal_load((const dbl2*)(Sb + k * ld + col + 128));
+    }
+    const dbl2 x00 = *(const dbl2*)(v0 + col);
+    const dbl2 x01 = *(const dbl2*)(v0 + col + 128);
+    dbl2 x10 = dbl2{0.0, 0.0}, x11 = dbl2{0.0, 0.0};
+    if (NR == 2) {
+      x10 = *(const dbl2*)(v1 + col);
+      x11 = *(const dbl2*)(v1 + col + 128);
+    }
+#pragma unroll
+    for (int k = 0; k < GV_RW; ++k) {
+      a0[k] = __builtin_fma(s[0][k].x, x00.x, a0[k]);
+      a0[k] = __builtin_fma(s[0][k].y, x00.y, a0[k]);
+      a0[k] = __builtin_fma(s[1][k].x, x01.x, a0[k]);
+      a0[k] = __builtin_fma(s[1][k].y, x01.y, a0[k]);
+      if (NR == 2) {
+        a1[k] = __builtin_fma(s[0][k].x, x10.x, a1[k]);
+        a1[k] = __builtin_fma(s[0][k].y, x10.y, a1[k]);
+        a1[k] = __builtin_fma(s[1][k].x, x11.x, a1[k]);
+        a1[k] = __builtin_fma(s[1][k].y, x11.y, a1[k]);
+      }
+    }
+  }
+  if (col < ld) {  // last (possibly partial) chunk
+    dbl2 s[GV_RW];
+#pragma unroll
+    for (int k = 0; k < GV_RW; ++k) s[k] = __builtin_nontemporal_load((const dbl2*)(Sb + k * ld + col));
+    const dbl2 x0 = *(const dbl2*)(v0 + col);
+    dbl2 x1 = dbl2{0.0, 0.0};
+    if (NR == 2) x1 = *(const dbl2*)(v1 + col);
+#pragma unroll
+    for (int k = 0; k < GV_RW; ++k) {
+      a0[k] = __builtin_fma(s[k].x, x0.x, a0[k]);
+      a0[k] = __builtin_fma(s[k].y, x0.y, a0[k]);
+      if (NR == 2) {
+        a1[k] = __builtin_fma(s[k].x, x1.x, a1[k]);
+        a1[k] = __builtin_fma(s[k].y, x1.y, a1[k]);
+      }
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < GV_RW; ++k) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      a0[k] += xor_lane(a0[k], off);
+      if (NR == 2) a1[k] += xor_lane(a1[k], off);
+    }
+  }
+  if (lane == 0) {
+    double* o0 = vp(P, V_OUT0, b);
+    double* o1 = vp(P, V_OUT1, b);
+#pragma unroll
+    for (int k = 0; k < GV_RW; ++k) {
+      const int row = row0 + k;
+      if (row < P.n) {
+        o0[row] = a0[k];
+        if (NR == 2) o1[row] = a1[k];
+      }
+    }
+  }
+}
+
+// list_in: which ping-pong list holds the active instances; zero_cnt: counter to clear for the
+// state kernel that follows.
+__global__ void __launch_bounds__(GV_THREADS) k_gemv(DevParams P, int list_in, int zero_cnt) {
+  if (zero_cnt >= 0 && blockIdx.x == 0 && threadIdx.x == 0) P.cnt[zero_cnt] = 0;
+  const int nact = P.cnt[list_in];
+  const int slot = blockIdx.x / P.nrb;
+  if (slot >= nact) return;
+  const int b = P.lists[list_in * P.batch + slot];
+  const int rb = blockIdx.x - slot * P.nrb;
+  if (P.req[b] == 2) gemv_rows<2>(P, b, rb);
+  else gemv_rows<1>(P, b, rb);
+}
+
+// ------------------------------------------------------------------------------------------
+// S = Z + Z^T in place on the padded (Np x Np, Np = ld) layout, zeroing the padding.
+// One workgroup per 16x16 tile pair (I <= J): both tiles staged in LDS, both written.
+// ------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_symmetrize(double* S, int n, int64_t ld, int64_t inst_stride, int nt) {
+  const int I = blockIdx.x / nt, J = blockIdx.x % nt;
+  if (I > J) return;
+  double* Sb = S + (int64_t)blockIdx.y * inst_stride;
+  __shared__ double a[16][17], t[16][17];
+  const int r = threadIdx.x >> 4, c = threadIdx.x & 15;
+  const int i1 = I * 16 + r, j1 = J * 16 + c;  // element of tile (I,J)
+  const int i2 = J * 16 + r, j2 = I * 16 + c;  // element of tile (J,I)
+  a[r][c] = (i1 < n && j1 < n) ? Sb[(int64_t)i1 * ld + j1] : 0.0;
+  t[r][c] = (i2 < n && j2 < n) ? Sb[(int64_t)i2 * ld + j2] : 0.0;
+  __syncthreads();
+  // S_ij = Z_ij + Z_ji for (i,j) in tile (I,J); S_ji is the same double.
+  const double sij = a[r][c] + t[c][r];
+  const double sji = t[r][c] + a[c][r];
+  Sb[(int64_t)i1 * ld + j1] = (i1 < n && j1 < n) ? sij : 0.0;
+  if (I != J) Sb[(int64_t)i2 * ld + j2] = (i2 < n && j2 < n) ? sji : 0.0;
+}
+
+// ------------------------------------------------------------------------------------------
+// The per-instance state machine.
+// ------------------------------------------------------------------------------------------
+enum Act : int { ACT_YIELD = 0, ACT_DONE = 1, ACT_PAUSE = 2 };
+
+struct Machine {
+  const DevParams P;
+  const int b;
+  const int tid;
+  const int n;
+  const int out_list;
+  Red R;
+  double s[ST_HOT];   // hot scalars: identical in every thread, drive uniform control flow
+  double* cold;       // cold scalars (ST_HOT..ST_N): read and written by thread 0 only
+
+  __device__ __forceinline__ Machine(const DevParams& P_, int b_, int out_list_, double* redbuf)
+      : P(P_), b(b_), tid(threadIdx.x), n(P_.n), out_list(out_list_) {
+    R.buf = redbuf;
+    R.parity = 0;
+    const double* g = P.st + (int64_t)b * ST_N;
+#pragma unroll
+    for (int k = 0; k < ST_HOT; ++k) s[k] = g[k];
+    cold = P.st + (int64_t)b * ST_N;
+  }
+
+  // thread-0-owned counters / info fields
+  __device__ __forceinline__ void cadd(int k, double v) { if (tid == 0) cold[k] += v; }
+  __device__ __forceinline__ void cset(int k, double v) { if (tid == 0) cold[k] = v; }
+
+  // workgroup-uniform device clock (thread 0 reads it, max-reduction broadcasts it)
+  __device__ __forceinline__ double unow() {
+    double t[1] = {tid == 0 ? (double)wall_clock64() : -INFINITY};
+    const int op[1] = {2};
+    bred<1>(R, t, op);
+    return t[0];
+  }
+
+  __device__ __forceinline__ double* V(int k) const { return vp(P, k, b); }
+  __device__ __forceinline__ double elapsed_u(double t0) { return (unow() - t0) / P.clock_hz; }
+  __device__ __forceinline__ double mu_at(int idx) const {
+    const int i = idx < P.tab_len ? idx : P.tab_len - 1;
+    return P.mu_tab[i];
+  }
+
+  __device__ __forceinline__ void copy(int dst, int src) {
+    double* d = V(dst);
+    const double* a = V(src);
+    for (int i = tid; i < n; i += ST_THREADS) d[i] = a[i];
+  }
+
+  __device__ __forceinline__ int request(int nrhs) {
+    if (tid == 0) {
+      P.req[b] = nrhs;
+      const int slot = atomicAdd(&P.cnt[out_list], 1);
+      P.lists[out_list * P.batch + slot] = b;
+    }
+    cadd(ST_PASSES, 1.0);
+    return ACT_YIELD;
+  }
+
+  __device__ __forceinline__ void finish_write() {
+    if (tid == 0) {
+      double* g = cold;
+#pragma unroll
+      for (int k = 0; k < ST_HOT; ++k) g[k] = s[k];
+      double* o = P.stats + (int64_t)b * RIPTRM_STAT_NFIELDS;
+      o[RIPTRM_STAT_OUTER_ITERS] = s[ST_OUTER_IT];
+      o[RIPTRM_STAT_INNER_ITERS] = g[ST_INNER_TOTAL];
+      o[RIPTRM_STAT_TCG_ITERS] = g[ST_TCG_TOTAL];
+      o[RIPTRM_STAT_PASSES] = g[ST_PASSES];
+      o[RIPTRM_STAT_STOP_CODE] = g[ST_STOP_CODE];
+      o[RIPTRM_STAT_STOP_RUNTIME] = g[ST_STOP_RUNTIME];
+      o[RIPTRM_STAT_FINAL_RESIDUAL] = g[ST_RESIDUAL];
+      o[RIPTRM_STAT_LOG_COUNT] = g[ST_LOG_COUNT];
+      o[RIPTRM_STAT_LOG_OVERFLOW] = g[ST_LOG_OVERFLOW];
+      o[RIPTRM_STAT_PHASE] = s[ST_PHASE];
+      o[RIPTRM_STAT_MU] = s[ST_MU];
+      o[RIPTRM_STAT_TR_RADIUS] = s[ST_DELTA];
+      o[RIPTRM_STAT_TCG_LAST_J] = s[ST_J];
+      o[RIPTRM_STAT_TCG_LAST_STOP] = s[ST_TCG_STOP];
+      o[RIPTRM_STAT_ERROR] = g[ST_ERROR];
+    }
+  }
+
+  // ---- barrier Hessian HwCur(v) (RIPTRM.py:729; closed form SURVEY.md Appendix A) ----------
+  // u = S v.  Writes Hw(v) into dst (dst may alias u).  Needs ST_COEF at the current x.
+  // Hw(v) = P_x(-u) + coef v + G_x(q),  q = y (v - x (x.v)) / x,  G_x(w) = w - (x.w) x
+  __device__ __forceinline__ void hw_apply(const double* u, const double* v, double* dst) {
+    const double* X = V(V_X);
+    const double* Y = V(V_Y);
+    double r1[2] = {0.0, 0.0};
+    for (int i = tid; i < n; i += ST_THREADS) {
+      r1[0] += X[i] * u[i];
+      r1[1] += X[i] * v[i];
+    }
+    bsum<2>(R, r1);
+    const double xu = r1[0], xv = r1[1];
+    double r2[1] = {0.0};
+    for (int i = tid; i < n; i += ST_THREADS) {
+      const double q = (Y[i] * (v[i] - X[i] * xv)) / X[i];
+      r2[0] += X[i] * q;
+    }
+    bsum<1>(R, r2);
+    const double xq = r2[0];
+    const double coef = s[ST_COEF];
+    for (int i = tid; i < n; i += ST_THREADS) {
+      const double q = (Y[i] * (v[i] - X[i] * xv)) / X[i];
+      const double hf = -u[i] + xu * X[i];
+      dst[i] = (hf + coef * v[i]) + (q - xq * X[i]);
+    }
+  }
+
+  // ---- KKT evaluation, src/solver/utils.py:342-368 (+ compute_residual :269-340) ----------
+  // ev: cost, distance, residual, gradnorm, complvio, dualvio, manvio, maxvio, meanvio, maxabsy
+  __device__ __forceinline__ void evaluation(int xprev_kind, double (&ev)[10]) {
+    const double* X = V(V_X);
+    const double* Y = V(V_Y);
+    const double* SX = V(V_SX);
+    const double* XP = V(xprev_kind);
+    double a[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+    const int op[9] = {0, 0, 0, 0, 0, 0, 0, 2, 2};
+    a[7] = 0.0;
+    a[8] = -INFINITY;
+    for (int i = tid; i < n; i += ST_THREADS) {
+      const double x = X[i], y = Y[i];
+      a[0] += x * SX[i];                  // x.Sx
+      a[1] += XP[i] * x;                  // xPrev.x
+      a[2] += y * x;                      // y.x
+      a[3] += x * x;                      // x.x
+      const double cv = y * (-x);
+      a[4] += cv * cv;                    // sum (y_i g_i)^2
+      const double nv = fmax(-y, 0.0);
+      a[5] += nv * nv;                    // sum max(-y_i,0)^2
+      const double iv = fmax(-x, 0.0);
+      a[6] += iv * iv;                    // sum max(g_i,0)^2
+      a[7] = fmax(a[7], iv);              // max violation
+      a[8] = fmax(a[8], fabs(y));         // max |y_i|
+    }
+    bred<9>(R, a, op);
+    const double xSx = a[0], yx = a[2];
+    const double xg = -xSx;
+    double gg[2] = {0.0, 0.0};
+    for (int i = tid; i < n; i += ST_THREADS) {
+      const double x = X[i];
+      const double g = -SX[i];
+      const double gl = (g - xg * x) - (Y[i] - yx * x);
+      gg[0] += gl * gl;
+      gg[1] += fmax(-x, 0.0);
+    }
+    bsum<2>(R, gg);
+    const double gradnorm = sqrt(gg[0]);
+    double manvio = 0.0;
+    if (P.opt.manvio_kind == RIPTRM_MANVIO_SPHERE) manvio = sqrt(a[3]) - 1.0;
+    const double sq = gradnorm * gradnorm + a[4] + a[5] + a[6] + 0.0 + manvio * manvio;
+    double inner = a[1];
+    inner = inner > 1.0 ? 1.0 : inner;
+    inner = inner < -1.0 ? -1.0 : inner;
+    ev[0] = -0.5 * xSx;
+    ev[1] = acos(inner);
+    ev[2] = sqrt(sq);
+    ev[3] = gradnorm;
+    ev[4] = sqrt(a[4]);
+    ev[5] = sqrt(a[5]);
+    ev[6] = manvio;
+    ev[7] = a[7] > 0.0 ? a[7] : 0.0;
+    ev[8] = gg[1] / (double)n;
+    ev[9] = a[8];
+  }
+
+  // one log row; info == false -> solver_status(..., inner_info=None)
+  __device__ __forceinline__ void log_row(const double (&ev)[10], bool info, double t_now) {
+    if (tid == 0) {
+      const double* c = cold;
+      const int cnt = (int)c[ST_LOG_COUNT];
+      if (cnt < P.opt.log_capacity && cnt < P.cap) {
+        double* L = P.log + ((int64_t)b * P.cap + cnt) * RIPTRM_LOG_NFIELDS;
+        L[RIPTRM_LOG_ITERATION] = s[ST_OUTER_IT];
+        L[RIPTRM_LOG_TIME] = (cnt == 0) ? 0.0 : (t_now - s[ST_T_START]) / P.clock_hz;
+        L[RIPTRM_LOG_COST] = ev[0];
+        L[RIPTRM_LOG_DISTANCE] = ev[1];
+        L[RIPTRM_LOG_RESIDUAL] = ev[2];
+        L[RIPTRM_LOG_GRADNORM] = ev[3];
+        L[RIPTRM_LOG_COMPLVIOLATION] = ev[4];
+        L[RIPTRM_LOG_DUALVIOLATION] = ev[5];
+        L[RIPTRM_LOG_MANVIOLATION] = ev[6];
+        L[RIPTRM_LOG_MAXVIOLATION] = ev[7];
+        L[RIPTRM_LOG_MEANVIOLATION] = ev[8];
+        L[RIPTRM_LOG_MU] = s[ST_MU];
+        L[RIPTRM_LOG_HAS_INFO] = info ? c[ST_I_HAS] : 0.0;
+        L[RIPTRM_LOG_NUM_INNER] = c[ST_I_NUM];
+        L[RIPTRM_LOG_INNER_STATUS] = c[ST_I_STATUS];
+        L[RIPTRM_LOG_TR_RADIUS] = c[ST_I_TR];
+        L[RIPTRM_LOG_DXTYPE] = c[ST_I_DXTYPE];
+        L[RIPTRM_LOG_NORMDX] = c[ST_I_NORMDX];
+        L[RIPTRM_LOG_MINXFEASI] = c[ST_I_MINX];
+        L[RIPTRM_LOG_MINYFEASI] = c[ST_I_MINY];
+        L[RIPTRM_LOG_COMPL] = c[ST_I_COMPL];
+        L[RIPTRM_LOG_HAS_RATIO] = c[ST_I_HASRATIO];
+        L[RIPTRM_LOG_ARED_PRED] = c[ST_I_RATIO];
+        L[RIPTRM_LOG_RADIUS_UPDATE] = c[ST_I_RU];
+        L[RIPTRM_LOG_DUAL_CLIPPING] = c[ST_I_DC];
+        L[RIPTRM_LOG_MAXABSLAGMULT] = ev[9];
+        L[RIPTRM_LOG_TCG_ITERS] = s[ST_J] + 1.0;
+      } else {
+        cold[ST_LOG_OVERFLOW] += 1.0;
+      }
+      cold[ST_LOG_COUNT] += 1.0;
+    }
+  }
+
+  // ---- outer loop head: RIPTRM.py:931-959 + base_solver.check_stoppingcriterion ------------
+  __device__ __forceinline__ int outer_top() {
+    double ev[10];
+    evaluation(V_X0, ev);
+    const bool save_inner = P.opt.save_inner_iteration != 0;
+    const double tn = unow();
+    if (s[ST_OUTER_IT] == 0.0 || !save_inner) log_row(ev, s[ST_OUTER_IT] != 0.0, tn);
+    cset(ST_RESIDUAL, ev[2]);
+    const double rt = (tn - s[ST_T_START]) / P.clock_hz;
+    int stop = RIPTRM_STOP_NONE;
+    if (rt >= P.opt.maxtime) stop = RIPTRM_STOP_MAXTIME;
+    else if (s[ST_OUTER_IT] >= (double)P.opt.maxiter) stop = RIPTRM_STOP_MAXITER;
+    if (ev[2] <= P.opt.tolresid) stop = RIPTRM_STOP_TOLRESID;
+    if (stop != RIPTRM_STOP_NONE) {
+      cset(ST_STOP_CODE, stop);
+      cset(ST_STOP_RUNTIME, rt);
+      s[ST_PHASE] = PH_DONE;
+      return ACT_DONE;
+    }
+    if (s[ST_OUTER_IT] >= (double)P.outer_target) {
+      s[ST_PHASE] = PH_PAUSED;
+      return ACT_PAUSE;
+    }
+    return start_outer_step();
+  }
+
+  // RIPTRM.py:866-887 + inner_run :785-799
+  __device__ __forceinline__ int start_outer_step() {
+    s[ST_OUTER_IT] += 1.0;
+    const int mi = (int)s[ST_MU_IDX];
+    const int ti = mi < P.tab_len ? mi : P.tab_len - 1;
+    s[ST_TOLL] = P.tolL_tab[ti];
+    s[ST_TOLC] = P.tolC_tab[ti];
+    copy(V_X0, V_X);
+    copy(V_Y0, V_Y);
+    copy(V_SX0, V_SX);
+    copy(V_XPREV, V_X);
+    s[ST_DELTA0] = s[ST_DELTA];
+    s[ST_INNER_IT] = 0.0;
+    s[ST_T_INNER] = unow();
+    return inner_step_begin();
+  }
+
+  // RIPTRM.py:707-733: quantities at x, then tCG start (RIPTRM.py:46-96 with eta = 0)
+  __device__ __forceinline__ int inner_step_begin() {
+    s[ST_INNER_IT] += 1.0;
+    s[ST_DELTA_STEP] = s[ST_DELTA];
+    return tcg_begin();
+  }
+
+  __device__ __forceinline__ int tcg_begin() {
+    const double* X = V(V_X);
+    const double* Y = V(V_Y);
+    const double* SX = V(V_SX);
+    double* C = V(V_C);
+    double* Rv = V(V_R);
+    double* D = V(V_IN0);
+    double* E = V(V_ETA);
+    double* HE = V(V_HETA);
+    const double mu = s[ST_MU];
+    double h[4] = {0.0, 0.0, 0.0, 0.0};
+    for (int i = tid; i < n; i += ST_THREADS) {
+      const double x = X[i];
+      h[0] += x * x;
+      h[1] += x * SX[i];
+      h[2] += Y[i] * x;
+      h[3] += x * (mu / x);
+    }
+    bsum<4>(R, h);
+    const double xx = h[0], xSx = h[1], yx = h[2], xm = h[3];
+    s[ST_XX] = xx;
+    s[ST_XSX] = xSx;
+    s[ST_YX] = yx;
+    s[ST_COEF] = (xSx + yx) * xx;
+    s[ST_FCUR] = -0.5 * xSx;
+    const double xg = -xSx;
+    double rr[1] = {0.0};
+    for (int i = tid; i < n; i += ST_THREADS) {
+      const double x = X[i];
+      const double g = -SX[i];
+      const double m = mu / x;
+      const double c = (g - xg * x) - (m - xm * x);   // cxCur, RIPTRM.py:730
+      C[i] = c;
+      Rv[i] = c;
+      D[i] = -c;
+      E[i] = 0.0;
+      HE[i] = 0.0;
+      rr[0] += c * c;
+    }
+    bsum<1>(R, rr);
+    s[ST_NORMR0] = sqrt(rr[0]);
+    s[ST_ZR] = rr[0];
+    s[ST_DPD] = rr[0];
+    s[ST_EPE] = 0.0;
+    s[ST_EPD] = 0.0;
+    s[ST_MODEL] = 0.0;
+    s[ST_J] = 0.0;
+    if (n - 1 <= 0) {  // maxinner = manifold.dim = 0: no tCG iteration is possible
+      cset(ST_ERROR, 1.0);
+      s[ST_PHASE] = PH_ERROR;
+      return ACT_DONE;
+    }
+    s[ST_PHASE] = PH_TCG;
+    return request(1);
+  }
+
+  // one tCG iteration after Hdelta's S-pass: RIPTRM.py:100-214
+  __device__ __forceinline__ int tcg_step() {
+    double* U = V(V_OUT0);          // S delta, overwritten with Hdelta
+    const double* D = V(V_IN0);     // delta
+    hw_apply(U, D, U);
+    const double* X = V(V_X);
+    const double* C = V(V_C);
+    double* E = V(V_ETA);
+    double* HE = V(V_HETA);
+    double* Rv = V(V_R);
+    double* Dw = V(V_IN0);
+    double d1[1] = {0.0};
+    for (int i = tid; i < n; i += ST_THREADS) d1[0] += D[i] * U[i];
+    bsum<1>(R, d1);
+    const double d_Hd = d1[0];
+    const double z_r = s[ST_ZR], e_Pd = s[ST_EPD], d_Pd = s[ST_DPD], e_Pe = s[ST_EPE];
+    const double Delta = s[ST_DELTA];
+    double alpha = 0.0, e_Pe_new;
+    if (d_Hd != 0.0) {
+      alpha = z_r / d_Hd;
+      e_Pe_new = (e_Pe + 2.0 * alpha * e_Pd) + (alpha * alpha) * d_Pd;
+    } else {
+      e_Pe_new = e_Pe;
+    }
+    const double D2 = Delta * Delta;
+    if (d_Hd <= 0.0 || e_Pe_new >= D2) {
+      const double tau = (-e_Pd + sqrt(e_Pd * e_Pd + d_Pd * (D2 - e_Pe))) / d_Pd;
+      for (int i = tid; i < n; i += ST_THREADS) {
+        E[i] = E[i] + tau * D[i];
+        HE[i] = HE[i] + tau * U[i];
+      }
+      s[ST_TCG_STOP] = d_Hd <= 0.0 ? RIPTRM_TCG_NEGATIVE_CURVATURE : RIPTRM_TCG_EXCEEDED_TR;
+      return tcg_end();
+    }
+    s[ST_EPE] = e_Pe_new;
+    double m2[2] = {0.0, 0.0};
+    for (int i = tid; i < n; i += ST_THREADS) {
+      const double ne = E[i] + alpha * D[i];
+      const double nh = HE[i] + alpha * U[i];
+      m2[0] += ne * C[i];
+      m2[1] += ne * nh;
+    }
+    bsum<2>(R, m2);
+    const double new_model = m2[0] + 0.5 * m2[1];
+    if (new_model >= s[ST_MODEL]) {
+      s[ST_TCG_STOP] = RIPTRM_TCG_MODEL_INCREASED;
+      return tcg_end();
+    }
+    s[ST_MODEL] = new_model;
+    double r2[1] = {0.0};
+    for (int i = tid; i < n; i += ST_THREADS) {
+      E[i] = E[i] + alpha * D[i];
+      HE[i] = HE[i] + alpha * U[i];
+      const double r = Rv[i] + alpha * U[i];
+      Rv[i] = r;
+      r2[0] += r * r;
+    }
+    bsum<1>(R, r2);
+    const double r_r = r2[0];
+    const double norm_r = sqrt(r_r);
+    const double nr0 = s[ST_NORMR0];
+    const double th = P.opt.tcg_theta, ka = P.opt.tcg_kappa;
+    const double nr0t = pow(nr0, th);
+    const double j = s[ST_J];
+    if (j >= (double)P.opt.tcg_mininner && norm_r <= nr0 * fmin(nr0t, ka)) {
+      s[ST_TCG_STOP] = ka < nr0t ? RIPTRM_TCG_REACHED_TARGET_LINEAR : RIPTRM_TCG_REACHED_TARGET_SUPERLINEAR;
+      return tcg_end();
+    }
+    const double zold = z_r;
+    const double znew = r_r;
+    const double beta = znew / zold;
+    double p1[1] = {0.0};
+    for (int i = tid; i < n; i += ST_THREADS) {
+      const double dn = -Rv[i] + beta * D[i];
+      Dw[i] = dn;
+      p1[0] += X[i] * dn;
+    }
+    bsum<1>(R, p1);
+    const double xd = p1[0];
+    for (int i = tid; i < n; i += ST_THREADS) Dw[i] = Dw[i] - xd * X[i];  // to_tangent_space
+    s[ST_ZR] = znew;
+    s[ST_EPD] = beta * (e_Pd + alpha * d_Pd);
+    s[ST_DPD] = znew + (beta * beta) * d_Pd;
+    s[ST_J] = j + 1.0;
+    if (j + 1.0 >= (double)(n - 1)) {  // range(maxinner) exhausted; Python j stays maxinner-1
+      s[ST_J] = j;
+      s[ST_TCG_STOP] = RIPTRM_TCG_MAX_INNER_ITER;
+      return tcg_end();
+    }
+    return request(1);
+  }
+
+  // after tCG: RIPTRM.py:733-746 (direction, ||dx||, dy, retraction) + feasibility part of :591
+  __device__ __forceinline__ int tcg_end() {
+    cadd(ST_TCG_TOTAL, s[ST_J] + 1.0);
+    const double* X = V(V_X);
+    const double* Y = V(V_Y);
+    const double* E = V(V_ETA);
+    double e1[2] = {0.0, 0.0};
+    for (int i = tid; i < n; i += ST_THREADS) {
+      e1[0] += E[i] * E[i];
+      e1[1] += X[i] * E[i];
+    }
+    bsum<2>(R, e1);
+    const double normdx = sqrt(e1[0]);
+    const double xdx = e1[1];
+    s[ST_NORMDX] = normdx;
+    s[ST_XDX] = xdx;
+    if ((int)s[ST_MODE] == MODE_TCG_ONLY) {
+      s[ST_PHASE] = PH_DONE;
+      return ACT_DONE;
+    }
+    const double mu = s[ST_MU];
+    double* YN = V(V_YNEW);
+    double* XN = V(V_IN1);
+    double w2[1] = {0.0};
+    for (int i = tid; i < n; i += ST_THREADS) {
+      const double x = X[i], y = Y[i], dx = E[i];
+      const double dy = (-y + mu * (1.0 / x)) - (y * (dx - x * xdx)) / x;   // RIPTRM.py:743
+      YN[i] = y + dy;
+      const double w = x + dx;
+      w2[0] += w * w;
+    }
+    bsum<1>(R, w2);
+    const double nw = sqrt(w2[0]);
+    double* D = V(V_IN0);
+    double c3[5] = {INFINITY, INFINITY, 0.0, 0.0, 0.0};
+    const int op3[5] = {1, 1, 0, 0, 0};
+    for (int i = tid; i < n; i += ST_THREADS) {
+      const double dx = E[i];
+      const double xn = (X[i] + dx) / nw;   // retraction (x+dx)/||x+dx||
+      XN[i] = xn;
+      D[i] = dx;
+      const double yn = YN[i];
+      c3[0] = fmin(c3[0], xn);
+      c3[1] = fmin(c3[1], yn);
+      c3[2] += (xn > 0.0) ? 0.0 : 1.0;
+      c3[3] += (yn > 0.0) ? 0.0 : 1.0;
+      const double cv = yn * xn - mu;
+      c3[4] += cv * cv;
+    }
+    bred<5>(R, c3, op3);
+    s[ST_MINX] = c3[0];
+    s[ST_MINY] = c3[1];
+    s[ST_XFEAS] = (c3[2] == 0.0) ? 1.0 : 0.0;
+    s[ST_COMPL] = sqrt(c3[4]);
+    s[ST_YFEAS] = (c3[3] == 0.0) ? 1.0 : 0.0;
+    if (s[ST_XFEAS] != 0.0) {
+      s[ST_PHASE] = PH_TRIAL;
+      return request(2);
+    }
+    // primal infeasible: RIPTRM.py:769-775
+    set_info(RIPTRM_IS_PRIMAL_INFEASIBLE, false, 0.0, RIPTRM_RU_NONE, -1.0);
+    s[ST_DELTA] = P.opt.gamma * normdx;
+    return inner_loop_tail(false);
+  }
+
+  __device__ __forceinline__ void set_info(int status, bool has_ratio, double ratio, int ru, double dc) {
+    if (tid == 0) {
+      double* c = cold;
+      c[ST_I_HAS] = 1.0;
+      c[ST_I_NUM] = s[ST_INNER_IT];
+      c[ST_I_STATUS] = status;
+      c[ST_I_TR] = s[ST_DELTA_STEP];
+      c[ST_I_DXTYPE] = s[ST_TCG_STOP];
+      c[ST_I_NORMDX] = s[ST_NORMDX];
+      c[ST_I_MINX] = s[ST_MINX];
+      c[ST_I_MINY] = s[ST_MINY];
+      c[ST_I_COMPL] = s[ST_COMPL];
+      c[ST_I_HASRATIO] = has_ratio ? 1.0 : 0.0;
+      c[ST_I_RATIO] = ratio;
+      c[ST_I_RU] = ru;
+      c[ST_I_DC] = dc;
+    }
+  }
+
+  // after the 2-RHS pass (S dx, S x_new): RIPTRM.py:748-783 with :574-629 and :631-705
+  __device__ __forceinline__ int trial_eval() {
+    const double* X = V(V_X);
+    const double* XN = V(V_IN1);
+    const double* YN = V(V_YNEW);
+    const double* SXN = V(V_OUT1);
+    const double mu = s[ST_MU];
+    double a[4] = {0.0, 0.0, 0.0, 0.0};
+    for (int i = tid; i < n; i += ST_THREADS) {
+      const double xn = XN[i];
+      a[0] += xn * SXN[i];
+      a[1] += YN[i] * xn;
+      a[2] += log(X[i]);
+      a[3] += log(xn);
+    }
+    bsum<4>(R, a);
+    const double xnS = a[0], ynxn = a[1];
+    const double xg = -xnS;
+    double g2[1] = {0.0};
+    for (int i = tid; i < n; i += ST_THREADS) {
+      const double xn = XN[i];
+      const double gl = (-SXN[i] - xg * xn) - (YN[i] - ynxn * xn);   // gradLagrangefun
+      g2[0] += gl * gl;
+    }
+    bsum<1>(R, g2);
+    const double normgl = sqrt(g2[0]);
+    const bool yfeas = s[ST_YFEAS] != 0.0;
+    const bool conv = yfeas && normgl <= s[ST_TOLL] && s[ST_COMPL] <= s[ST_TOLC];
+    if (conv) {  // RIPTRM.py:762-766
+      copy(V_X, V_IN1);
+      copy(V_Y, V_YNEW);
+      copy(V_SX, V_OUT1);
+      set_info(RIPTRM_IS_CONVERGED, false, 0.0, RIPTRM_RU_NONE, -1.0);
+      return inner_loop_tail(true);
+    }
+    // update_xy_TR_radius, RIPTRM.py:631-705
+    const double lb_c = s[ST_FCUR] - mu * a[2];
+    const double lb_n = (-0.5 * xnS) - mu * a[3];
+    double ared = lb_c - lb_n;
+    double* HW = V(V_OUT0);
+    const double* DX = V(V_IN0);
+    hw_apply(HW, DX, HW);
+    const double* C = V(V_C);
+    double pp[2] = {0.0, 0.0};
+    for (int i = tid; i < n; i += ST_THREADS) {
+      pp[0] += HW[i] * DX[i];
+      pp[1] += C[i] * DX[i];
+    }
+    bsum<2>(R, pp);
+    double pred = (0.0 - 0.5 * pp[0]) - pp[1];
+    const double red_reg = fmax(1.0, fabs(lb_c)) * 2.220446049250313e-16 * P.opt.reduction_regularization;
+    ared = ared + red_reg;
+    pred = pred + red_reg;
+    const double ratio = ared / pred;
+    const double Delta = s[ST_DELTA];
+    double Dn;
+    int ru;
+    if (ared < 0.25 * pred) {
+      ru = RIPTRM_RU_REDUCED;
+      Dn = 0.25 * Delta;
+    } else if (ared >= 0.75 * pred && fabs(s[ST_NORMDX] - Delta) <= 1e-15) {
+      ru = RIPTRM_RU_EXPANDED;
+      const double d2 = 2.0 * Delta;
+      Dn = d2 < P.opt.maximal_tr_radius ? d2 : P.opt.maximal_tr_radius;
+    } else {
+      ru = RIPTRM_RU_UNCHANGED;
+      Dn = Delta;
+    }
+    if (ared > P.opt.rho * pred) {
+      const double cl = P.opt.const_left, cr = P.opt.const_right;
+      const double iright = np_max(cr, cr / mu);   // RIPTRM.py:682 (3-arg np.maximum quirk)
+      double* Xw = V(V_X);
+      double* Yw = V(V_Y);
+      double* SXw = V(V_SX);
+      double nd[1] = {0.0};
+      for (int i = tid; i < n; i += ST_THREADS) {
+        const double xn = XN[i], yn = YN[i];
+        const double il = cl * np_min(np_min(Yw[i], mu / xn), 1.0);
+        const double yc = np_min(np_max(yn, il), iright);
+        nd[0] += (yc != yn) ? 1.0 : 0.0;
+        Xw[i] = xn;
+        Yw[i] = yc;
+        SXw[i] = SXN[i];
+      }
+      bsum<1>(R, nd);
+      set_info(RIPTRM_IS_SUCCESSFUL, true, ratio, ru, nd[0] > 0.0 ? 1.0 : 0.0);
+    } else {
+      set_info(RIPTRM_IS_UNSUCCESSFUL, true, ratio, ru, -1.0);
+    }
+    s[ST_DELTA] = Dn;
+    return inner_loop_tail(false);
+  }
+
+  // inner_run after a step: log, time/iteration limits, exit -> outer update (RIPTRM.py:810-896)
+  __device__ __forceinline__ int inner_loop_tail(bool converged) {
+    cadd(ST_INNER_TOTAL, 1.0);
+    const double tn = unow();
+    if (P.opt.save_inner_iteration) {
+      double ev[10];
+      evaluation(V_XPREV, ev);
+      log_row(ev, true, tn);
+    }
+    copy(V_XPREV, V_X);
+    bool exitflag = converged;
+    double rt, lim;
+    if (P.opt.inner_maxtime < 0.0) {
+      lim = P.opt.maxtime;
+      rt = (tn - s[ST_T_START]) / P.clock_hz;
+    } else {
+      lim = P.opt.inner_maxtime;
+      rt = (tn - s[ST_T_INNER]) / P.clock_hz;
+    }
+    bool reset = false;
+    if (rt >= lim) reset = true;
+    if (P.opt.inner_maxiter >= 0 && s[ST_INNER_IT] >= (double)P.opt.inner_maxiter) reset = true;
+    if (reset) {
+      cset(ST_I_STATUS, s[ST_INNER_IT] * 0.0 + (rt >= lim && !(P.opt.inner_maxiter >= 0 && s[ST_INNER_IT] >= (double)P.opt.inner_maxiter) ? RIPTRM_IS_MAX_TIME_EXCEEDED : RIPTRM_IS_MAX_ITER_EXCEEDED));
+      exitflag = true;
+      copy(V_X, V_X0);
+      copy(V_Y, V_Y0);
+      copy(V_SX, V_SX0);
+      copy(V_XPREV, V_X0);
+      s[ST_DELTA] = s[ST_DELTA0];
+    }
+    if (!exitflag) return inner_step_begin();
+    // outer_step tail: RIPTRM.py:889-896
+    s[ST_MU_IDX] += 1.0;
+    s[ST_MU] = mu_at((int)s[ST_MU_IDX]);
+    const double mn = P.opt.minimal_initial_tr_radius;
+    s[ST_DELTA] = s[ST_DELTA] > mn ? s[ST_DELTA] : mn;
+    return outer_top();
+  }
+
+  __device__ __forceinline__ int dispatch() {
+    switch ((int)s[ST_PHASE]) {
+      case PH_START:
+        copy(V_IN0, V_X);
+        s[ST_PHASE] = PH_AFTER_SX0;
+        return request(1);
+      case PH_AFTER_SX0:
+        copy(V_SX, V_OUT0);
+        s[ST_T_START] = unow();
+        copy(V_X0, V_X);
+        return outer_top();
+      case PH_TCG:
+        return tcg_step();
+      case PH_TRIAL:
+        return trial_eval();
+      case PH_PAUSED:
+        return start_outer_step();
+      case PH_TCGO_START:
+        copy(V_IN0, V_X);
+        s[ST_PHASE] = PH_TCGO_SX;
+        return request(1);
+      case PH_TCGO_SX:
+        copy(V_SX, V_OUT0);
+        return tcg_begin();
+      default:
+        return ACT_DONE;
+    }
+  }
+};
+
+// full = 1: workgroup b serves instance b; else workgroup k serves lists[list_in][k].
+__global__ void __launch_bounds__(ST_THREADS) k_state(DevParams P, int full, int list_in, int list_out) {
+  __shared__ double redbuf[2 * ST_WAVES * RED_MAX];
+  int b;
+  if (full) {
+    b = blockIdx.x;
+    if (b >= P.batch) return;
+    // a full launch (solve start / resume) only (re)starts instances that wait for no S-pass
+    const double* g = P.st + (int64_t)b * ST_N;
+    const int ph = (int)g[ST_PHASE];
+    const bool startable = ph == PH_START || ph == PH_TCGO_START ||
+                           (ph == PH_PAUSED && (double)P.outer_target > g[ST_OUTER_IT]);
+    if (!startable) return;
+  } else {
+    if ((int)blockIdx.x >= P.cnt[list_in]) return;
+    b = P.lists[list_in * P.batch + blockIdx.x];
+  }
+  Machine M(P, b, list_out, redbuf);
+  const int ph = (int)M.s[ST_PHASE];
+  if (ph == PH_DONE || ph == PH_IDLE || ph == PH_ERROR) return;
+  M.dispatch();
+  M.finish_write();
+}
+
+// initialise a solve: x0/y0 -> X/Y, scalars
+__global__ void __launch_bounds__(256) k_init(DevParams P, const double* x0, const double* y0, int64_t ldv,
+                                              const double* mu, const double* delta, int mode) {
+  const int b = blockIdx.x;
+  double* X = vp(P, V_X, b);
+  double* Y = vp(P, V_Y, b);
+  for (int i = threadIdx.x; i < P.n; i += blockDim.x) {
+    X[i] = x0[(int64_t)b * ldv + i];
+    Y[i] = y0[(int64_t)b * ldv + i];
+  }
+  if (threadIdx.x == 0) {
+    double* s = P.st + (int64_t)b * ST_N;
+    for (int k = 0; k < ST_N; ++k) s[k] = 0.0;
+    s[ST_MODE] = mode;
+    if (mode == MODE_SOLVE) {
+      s[ST_PHASE] = PH_START;
+      s[ST_MU] = P.mu_tab[0];
+      s[ST_DELTA] = P.opt.initial_tr_radius;
+    } else {
+      s[ST_PHASE] = PH_TCGO_START;
+      s[ST_MU] = mu[b];
+      s[ST_DELTA] = delta[b];
+    }
+    s[ST_I_DC] = -1.0;
+    s[ST_T_START] = (double)wall_clock64();
+  }
+}
+
+// HVP entry: copy x, y, v into the workspace and queue all instances for a 2-RHS pass
+__global__ void __launch_bounds__(256) k_hvp_prep(DevParams P, const double* x, const double* y, const double* v, int64_t ldv) {
+  const int b = blockIdx.x;
+  double* X = vp(P, V_X, b);
+  double* Y = vp(P, V_Y, b);
+  double* I0 = vp(P, V_IN0, b);
+  double* I1 = vp(P, V_IN1, b);
+  for (int i = threadIdx.x; i < P.n; i += blockDim.x) {
+    X[i] = x[(int64_t)b * ldv + i];
+    Y[i] = y[(int64_t)b * ldv + i];
+    I0[i] = v[(int64_t)b * ldv + i];
+    I1[i] = X[i];
+  }
+  if (threadIdx.x == 0) {
+    P.req[b] = 2;
+    P.lists[b] = b;
+    if (b == 0) P.cnt[0] = P.batch;
+  }
+}
+
+__global__ void __launch_bounds__(ST_THREADS) k_hvp_epi(DevParams P, double mu, double* out, int64_t ldv) {
+  __shared__ double redbuf[2 * ST_WAVES * RED_MAX];
+  const int b = blockIdx.x;
+  Machine M(P, b, 0, redbuf);
+  const double* X = M.V(V_X);
+  const double* Y = M.V(V_Y);
+  const double* SX = M.V(V_OUT1);
+  double h[3] = {0.0, 0.0, 0.0};
+  for (int i = threadIdx.x; i < P.n; i += ST_THREADS) {
+    h[0] += X[i] * X[i];
+    h[1] += X[i] * SX[i];
+    h[2] += Y[i] * X[i];
+  }
+  bsum<3>(M.R, h);
+  M.s[ST_COEF] = (h[1] + h[2]) * h[0];
+  (void)mu;
+  double* U = M.V(V_OUT0);
+  M.hw_apply(U, M.V(V_IN0), U);
+  for (int i = threadIdx.x; i < P.n; i += ST_THREADS) out[(int64_t)b * ldv + i] = U[i];
+}
+
+}  // namespace riptrm
+
+// ==========================================================================================
+// C-ABI
+// ==========================================================================================
+using namespace riptrm;
+
+struct riptrm_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::string err;
+  bool bound = false, solving = false;
+  Layout L{};
+  const double* S = nullptr;
+  int64_t inst_stride = 0;
+  char* ws = nullptr;
+  DevParams P{};
+  int parity = 0;        // list written by the last state kernel
+  int active_bound = 0;  // upper bound of active instances (for the gemv grid)
+  double clock_hz = 1e8;
+  // optional HIP-event timing of every k_gemv / k_state launch (riptrm_profile_*)
+  bool prof = false;
+  std::vector<hipEvent_t> ev_pool;
+  std::vector<std::pair<int, int>> ev_gemv, ev_state;  // (start, end) indices into ev_pool
+  int ev_used = 0;
+  double gemv_ms = 0.0, state_ms = 0.0;
+  int64_t gemv_n = 0, state_n = 0;
+};
+
+static hipEvent_t prof_event(riptrm_ctx* c, int* idx) {
+  if (c->ev_used == (int)c->ev_pool.size()) {
+    hipEvent_t e;
+    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    c->ev_pool.push_back(e);
+  }
+  *idx = c->ev_used;
+  return c->ev_pool[c->ev_used++];
+}
+
+// after a stream sync: fold the recorded pairs into the running totals
+static void prof_collect(riptrm_ctx* c) {
+  for (auto& pr : c->ev_gemv) {
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, c->ev_pool[pr.first], c->ev_pool[pr.second]) == hipSuccess) c->gemv_ms += ms;
+    c->gemv_n++;
+  }
+  for (auto& pr : c->ev_state) {
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, c->ev_pool[pr.first], c->ev_pool[pr.second]) == hipSuccess) c->state_ms += ms;
+    c->state_n++;
+  }
+  c->ev_gemv.clear();
+  c->ev_state.clear();
+  c->ev_used = 0;
+}
+
+static int fail(riptrm_ctx* c, int code, const std::string& msg) {
+  if (c) c->err = msg;
+  return code;
+}
+
+#define HIPCHK(c, expr)                                                                    \
+  do {                                                                                     \
+    hipError_t e_ = (expr);                                                                \
+    if (e_ != hipSuccess) return fail((c), RIPTRM_E_HIP, std::string(#expr ": ") + hipGetErrorString(e_)); \
+  } while (0)
+
+extern "C" {
+
+int riptrm_abi_version(void) { return RIPTRM_ABI_VERSION; }
+
+int riptrm_ctx_create(riptrm_ctx** out, int device, void* stream) {
+  if (!out) return RIPTRM_E_ARG;
+  *out = nullptr;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return RIPTRM_E_NODEV;
+  if (device < 0 || device >= ndev) return RIPTRM_E_ARG;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) != hipSuccess) return RIPTRM_E_NODEV;
+  if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) return RIPTRM_E_NODEV;
+  riptrm_ctx* c = new riptrm_ctx();
+  c->device = device;
+  c->stream = (hipStream_t)stream;
+  int khz = 0;
+  if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device) == hipSuccess && khz > 0)
+    c->clock_hz = (double)khz * 1000.0;
+  *out = c;
+  return RIPTRM_OK;
+}
+
+int riptrm_ctx_destroy(riptrm_ctx* ctx) {
+  if (ctx)
+    for (auto e : ctx->ev_pool) (void)hipEventDestroy(e);
+  delete ctx;
+  return RIPTRM_OK;
+}
+
+const char* riptrm_last_error(const riptrm_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+int riptrm_ctx_set_stream(riptrm_ctx* ctx, void* stream) {
+  if (!ctx) return RIPTRM_E_ARG;
+  ctx->stream = (hipStream_t)stream;
+  return RIPTRM_OK;
+}
+
+double riptrm_device_clock_hz(riptrm_ctx* ctx) { return ctx ? ctx->clock_hz : 0.0; }
+
+int64_t riptrm_nonnegpca_ld(int32_t n) { return ld_of(n); }
+int64_t riptrm_nonnegpca_rows(int32_t n) { return rows_of(n); }
+int64_t riptrm_workspace_bytes(int32_t n, int32_t batch, int32_t cap) {
+  if (n <= 0 || batch <= 0 || cap < 0) return -1;
+  return make_layout(n, batch, cap).total;
+}
+int64_t riptrm_workspace_offset(int32_t n, int32_t batch, int32_t cap, int32_t kind) {
+  if (n <= 0 || batch <= 0 || cap < 0) return -1;
+  const Layout L = make_layout(n, batch, cap);
+  switch (kind) {
+    case 0: case 1: case 2: case 3:
+      return L.off_vec + (int64_t)kind * batch * L.ld * 8;
+    case 4: return L.off_stats;
+    case 5: return L.off_log;
+    default: return -1;
+  }
+}
+
+int riptrm_nonnegpca_symmetrize(riptrm_ctx* ctx, double* S, int32_t n, int32_t batch, int64_t ld, int64_t inst_stride) {
+  if (!ctx || !S || n <= 0 || batch <= 0) return fail(ctx, RIPTRM_E_ARG, "symmetrize: bad argument");
+  if (ld != ld_of(n) || inst_stride < rows_of(n) * ld)
+    return fail(ctx, RIPTRM_E_ARG, "symmetrize: S must use riptrm_nonnegpca_ld/rows layout");
+  HIPCHK(ctx, hipSetDevice(ctx->device));
+  const int nt = (int)(ld / 16);
+  dim3 grid((unsigned)(nt * nt), (unsigned)batch);
+  hipLaunchKernelGGL(k_symmetrize, grid, dim3(256), 0, ctx->stream, S, n, ld, inst_stride, nt);
+  HIPCHK(ctx, hipGetLastError());
+  return RIPTRM_OK;
+}
+
+int riptrm_nonnegpca_bind(riptrm_ctx* ctx, const double* S, int32_t n, int32_t batch, int64_t ld, int64_t inst_stride,
+                          void* workspace, int64_t workspace_bytes, int32_t cap) {
+  if (!ctx) return RIPTRM_E_ARG;
+  if (!S || !workspace || n < 2 || batch <= 0 || cap < 0)
+    return fail(ctx, RIPTRM_E_ARG, "bind: bad argument (need n >= 2, batch >= 1)");
+  if (ld != ld_of(n) || inst_stride < rows_of(n) * ld || (inst_stride % 2) != 0)
+    return fail(ctx, RIPTRM_E_ARG, "bind: S must use riptrm_nonnegpca_ld/rows layout");
+  if (((uintptr_t)S % 16) != 0 || ((uintptr_t)workspace % 256) != 0)
+    return fail(ctx, RIPTRM_E_ARG, "bind: S must be 16-byte and workspace 256-byte aligned");
+  const Layout L = make_layout(n, batch, cap);
+  if (workspace_bytes < L.total) return fail(ctx, RIPTRM_E_ARG, "bind: workspace too small");
+  HIPCHK(ctx, hipSetDevice(ctx->device));
+  HIPCHK(ctx, hipMemsetAsync(workspace, 0, (size_t)L.total, ctx->stream));
+  ctx->L = L;
+  ctx->S = S;
+  ctx->inst_stride = inst_stride;
+  ctx->ws = (char*)workspace;
+  DevParams& P = ctx->P;
+  std::memset(&P, 0, sizeof(P));
+  P.S = S;
+  P.inst_stride = inst_stride;
+  P.ld = L.ld;
+  P.n = n;
+  P.batch = batch;
+  P.cap = cap;
+  P.nrb = (int)(rows_of(n) / GV_RB);
+  P.vec = (double*)(ctx->ws + L.off_vec);
+  P.st = (double*)(ctx->ws + L.off_state);
+  P.stats = (double*)(ctx->ws + L.off_stats);
+  P.log = (double*)(ctx->ws + L.off_log);
+  P.lists = (int32_t*)(ctx->ws + L.off_lists);
+  P.req = (int32_t*)(ctx->ws + L.off_req);
+  P.cnt = (int32_t*)(ctx->ws + L.off_cnt);
+  P.clock_hz = ctx->clock_hz;
+  P.outer_target = INT32_MAX;
+  ctx->bound = true;
+  ctx->solving = false;
+  return RIPTRM_OK;
+}
+
+static int launch_gemv(riptrm_ctx* c, int list_in, int zero_cnt, int bound) {
+  if (bound <= 0) return RIPTRM_OK;
+  const int64_t blocks = (int64_t)bound * c->P.nrb;
+  int i0 = -1, i1 = -1;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  if (c->prof && (e0 = prof_event(c, &i0)) && (e1 = prof_event(c, &i1))) HIPCHK(c, hipEventRecord(e0, c->stream));
+  hipLaunchKernelGGL(k_gemv, dim3((unsigned)blocks), dim3(GV_THREADS), 0, c->stream, c->P, list_in, zero_cnt);
+  HIPCHK(c, hipGetLastError());
+  if (c->prof && e1) {
+    HIPCHK(c, hipEventRecord(e1, c->stream));
+    c->ev_gemv.push_back({i0, i1});
+  }
+  return RIPTRM_OK;
+}
+
+static int launch_state(riptrm_ctx* c, int full, int list_in, int list_out, int bound) {
+  const int blocks = full ? c->P.batch : bound;
+  if (blocks <= 0) return RIPTRM_OK;
+  int i0 = -1, i1 = -1;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  if (c->prof && (e0 = prof_event(c, &i0)) && (e1 = prof_event(c, &i1))) HIPCHK(c, hipEventRecord(e0, c->stream));
+  hipLaunchKernelGGL(k_state, dim3((unsigned)blocks), dim3(ST_THREADS), 0, c->stream, c->P, full, list_in, list_out);
+  HIPCHK(c, hipGetLastError());
+  if (c->prof && e1) {
+    HIPCHK(c, hipEventRecord(e1, c->stream));
+    c->ev_state.push_back({i0, i1});
+  }
+  return RIPTRM_OK;
+}
+
+int riptrm_nonnegpca_hvp(riptrm_ctx* ctx, const double* x, const double* y, double mu, const double* v, double* out, int64_t ldv) {
+  if (!ctx) return RIPTRM_E_ARG;
+  if (!ctx->bound) return fail(ctx, RIPTRM_E_STATE, "hvp: bind first");
+  if (!x || !y || !v || !out || ldv < ctx->P.n) return fail(ctx, RIPTRM_E_ARG, "hvp: bad argument");
+  HIPCHK(ctx, hipSetDevice(ctx->device));
+  const int B = ctx->P.batch;
+  hipLaunchKernelGGL(k_hvp_prep, dim3(B), dim3(256), 0, ctx->stream, ctx->P, x, y, v, ldv);
+  HIPCHK(ctx, hipGetLastError());
+  int rc = launch_gemv(ctx, 0, -1, B);
+  if (rc) return rc;
+  hipLaunchKernelGGL(k_hvp_epi, dim3(B), dim3(ST_THREADS), 0, ctx->stream, ctx->P, mu, out, ldv);
+  HIPCHK(ctx, hipGetLastError());
+  ctx->solving = false;
+  return RIPTRM_OK;
+}
+
+static int run_steps(riptrm_ctx* c, int steps, int* n_active) {
+  for (int s = 0; s < steps; ++s) {
+    const int lin = c->parity, lout = c->parity ^ 1;
+    int rc = launch_gemv(c, lin, lout, c->active_bound);
+    if (rc) return rc;
+    rc = launch_state(c, 0, lin, lout, c->active_bound);
+    if (rc) return rc;
+    c->parity = lout;
+  }
+  int32_t h = 0;
+  HIPCHK(c, hipMemcpyAsync(&h, c->P.cnt + c->parity, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (c->prof) prof_collect(c);
+  c->active_bound = h;
+  if (n_active) *n_active = h;
+  return RIPTRM_OK;
+}
+
+// (re)start instances that wait for no S-pass (START / raised-target PAUSED): a full state
+// launch that APPENDS their requests to list `parity`, the one the next k_gemv reads, so the
+// requests of instances already in flight stay queued.
+static int kick(riptrm_ctx* c) {
+  int rc = launch_state(c, 1, c->parity, c->parity, c->P.batch);
+  if (rc) return rc;
+  c->active_bound = c->P.batch;
+  return RIPTRM_OK;
+}
+
+int riptrm_tcg(riptrm_ctx* ctx, const double* x, const double* y, int64_t ldv, const double* mu, const double* delta,
+               int32_t* iters, int32_t* stop, int32_t max_steps) {
+  if (!ctx) return RIPTRM_E_ARG;
+  if (!ctx->bound) return fail(ctx, RIPTRM_E_STATE, "tcg: bind first");
+  if (!x || !y || !mu || !delta || ldv < ctx->P.n) return fail(ctx, RIPTRM_E_ARG, "tcg: bad argument");
+  HIPCHK(ctx, hipSetDevice(ctx->device));
+  DevParams& P = ctx->P;
+  if (P.opt.struct_size == 0) {  // tCG defaults (RIPTRM.py:330-332) when no solve options were set
+    P.opt.tcg_theta = 1.0;
+    P.opt.tcg_kappa = 0.1;
+    P.opt.tcg_mininner = 1;
+  }
+  hipLaunchKernelGGL(k_init, dim3(P.batch), dim3(256), 0, ctx->stream, P, x, y, ldv, mu, delta, (int)MODE_TCG_ONLY);
+  HIPCHK(ctx, hipGetLastError());
+  ctx->parity = 0;
+  HIPCHK(ctx, hipMemsetAsync(P.cnt, 0, 4 * sizeof(int32_t), ctx->stream));
+  int rc = kick(ctx);
+  if (rc) return rc;
+  int act = P.batch;
+  int total = 0;
+  int chunk = 4;
+  while (act > 0) {
+    if (max_steps > 0 && total >= max_steps) return fail(ctx, RIPTRM_E_STATE, "tcg: step limit reached");
+    rc = run_steps(ctx, chunk, &act);
+    if (rc) return rc;
+    total += chunk;
+    if (chunk < 256) chunk *= 2;
+  }
+  if (iters || stop) {
+    const int B = P.batch;
+    double* h = new double[(size_t)B * RIPTRM_STAT_NFIELDS];
+    hipError_t e = hipMemcpy(h, P.stats, (size_t)B * RIPTRM_STAT_NFIELDS * 8, hipMemcpyDeviceToHost);
+    if (e != hipSuccess) {
+      delete[] h;
+      return fail(ctx, RIPTRM_E_HIP, "tcg: stats copy failed");
+    }
+    for (int b = 0; b < B; ++b) {
+      if (iters) iters[b] = (int32_t)h[b * RIPTRM_STAT_NFIELDS + RIPTRM_STAT_TCG_LAST_J];
+      if (stop) stop[b] = (int32_t)h[b * RIPTRM_STAT_NFIELDS + RIPTRM_STAT_TCG_LAST_STOP];
+    }
+    delete[] h;
+  }
+  ctx->solving = false;
+  return RIPTRM_OK;
+}
+
+int riptrm_solve_begin(riptrm_ctx* ctx, const riptrm_options* opt, const double* x0, const double* y0, int64_t ldv,
+                       const double* mu_table, const double* tolL_table, const double* tolC_table, int32_t table_len) {
+  if (!ctx) return RIPTRM_E_ARG;
+  if (!ctx->bound) return fail(ctx, RIPTRM_E_STATE, "solve_begin: bind first");
+  if (!opt || opt->struct_size != (int32_t)sizeof(riptrm_options))
+    return fail(ctx, RIPTRM_E_ARG, "solve_begin: riptrm_options.struct_size mismatch");
+  if (!x0 || !y0 || ldv < ctx->P.n || !mu_table || !tolL_table || !tolC_table || table_len <= 0)
+    return fail(ctx, RIPTRM_E_ARG, "solve_begin: bad argument");
+  if (opt->log_capacity > ctx->L.cap) return fail(ctx, RIPTRM_E_ARG, "solve_begin: log_capacity exceeds bound capacity");
+  HIPCHK(ctx, hipSetDevice(ctx->device));
+  DevParams& P = ctx->P;
+  P.opt = *opt;
+  P.mu_tab = mu_table;
+  P.tolL_tab = tolL_table;
+  P.tolC_tab = tolC_table;
+  P.tab_len = table_len;
+  P.outer_target = INT32_MAX;
+  hipLaunchKernelGGL(k_init, dim3(P.batch), dim3(256), 0, ctx->stream, P, x0, y0, ldv, (const double*)nullptr,
+                     (const double*)nullptr, (int)MODE_SOLVE);
+  HIPCHK(ctx, hipGetLastError());
+  ctx->parity = 0;
+  HIPCHK(ctx, hipMemsetAsync(P.cnt, 0, 4 * sizeof(int32_t), ctx->stream));
+  ctx->solving = true;
+  ctx->active_bound = 0;
+  return kick(ctx);
+}
+
+int riptrm_profile_enable(riptrm_ctx* ctx, int32_t on) {
+  if (!ctx) return RIPTRM_E_ARG;
+  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  prof_collect(ctx);
+  ctx->prof = on != 0;
+  ctx->gemv_ms = ctx->state_ms = 0.0;
+  ctx->gemv_n = ctx->state_n = 0;
+  return RIPTRM_OK;
+}
+
+int riptrm_profile_read(riptrm_ctx* ctx, double* gemv_ms, int64_t* gemv_launches, double* state_ms,
+                        int64_t* state_launches) {
+  if (!ctx) return RIPTRM_E_ARG;
+  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  prof_collect(ctx);
+  if (gemv_ms) *gemv_ms = ctx->gemv_ms;
+  if (gemv_launches) *gemv_launches = ctx->gemv_n;
+  if (state_ms) *state_ms = ctx->state_ms;
+  if (state_launches) *state_launches = ctx->state_n;
+  return RIPTRM_OK;
+}
+
+int riptrm_solve_advance(riptrm_ctx* ctx, int32_t steps, int32_t outer_target, int32_t* n_active) {
+  if (!ctx) return RIPTRM_E_ARG;
+  if (!ctx->solving) return fail(ctx, RIPTRM_E_STATE, "solve_advance: call riptrm_solve_begin first");
+  if (steps < 0) return fail(ctx, RIPTRM_E_ARG, "solve_advance: steps < 0");
+  HIPCHK(ctx, hipSetDevice(ctx->device));
+  if (outer_target != ctx->P.outer_target) {
+    const bool raised = outer_target > ctx->P.outer_target;
+    ctx->P.outer_target = outer_target;
+    if (raised) {  // resume paused instances
+      int rc = kick(ctx);
+      if (rc) return rc;
+    }
+  }
+  return run_steps(ctx, steps, n_active);
+}
+
+}  // extern "C"

@@ -1,0 +1,444 @@
+"""Batched NonnegPCA RIPTRM engine on one MI355X: device memory + the C-ABI calls.
+
+PyTorch owns the device memory (S, workspace, tables) and the stream; every operation on the
+hot path is a HIP kernel in ``libriptrm_hip.so``.  Layout in HBM:
+
+* ``S``   (batch, rows, ld) fp64, ``S_b = Z_b + Z_b^T`` row-major, rows/ld padded to 16 with
+  zeros; 8 n^2 bytes per instance (128 MB at n = 4000, 16.4 GB for 128 instances).
+* workspace: 16 state vectors per instance (batch, ld) fp64, per-instance scalars, stats and the
+  per-inner-iteration log rows, active lists.
+
+Host-side option handling mirrors ``RIPTRM.__init__`` (``src/solver/RIPTRM.py:305-365``): the
+option callables (forcing functions, barrier schedule) are evaluated here into per-outer-
+iteration tables, so the device reproduces the reference's mu sequence bit-exactly.
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+import time
+from dataclasses import dataclass
+from typing import Any, Dict, List, Optional, Sequence
+
+import numpy as np
+import torch
+
+import riptrm_native as N
+
+C = N.CONST
+NLOG = C["RIPTRM_LOG_NFIELDS"]
+NSTAT = C["RIPTRM_STAT_NFIELDS"]
+
+TCG_NAMES = {C["RIPTRM_TCG_MAX_INNER_ITER"]: "MAX_INNER_ITER",
+             C["RIPTRM_TCG_NEGATIVE_CURVATURE"]: "NEGATIVE_CURVATURE",
+             C["RIPTRM_TCG_EXCEEDED_TR"]: "EXCEEDED_TR",
+             C["RIPTRM_TCG_MODEL_INCREASED"]: "MODEL_INCREASED",
+             C["RIPTRM_TCG_REACHED_TARGET_LINEAR"]: "REACHED_TARGET_LINEAR",
+             C["RIPTRM_TCG_REACHED_TARGET_SUPERLINEAR"]: "REACHED_TARGET_SUPERLINEAR"}
+STATUS_NAMES = {0: None, 1: "initial", 2: "converged", 3: "primal_infeasible", 4: "successful",
+                5: "unsuccessful", 6: "max-time-exceeded", 7: "max-iter-exceeded"}
+RU_NAMES = {0: None, 1: "reduced", 2: "expanded", 3: "unchanged"}
+
+# RIPTRM default_option (src/solver/RIPTRM.py:305-358)
+REFERENCE_DEFAULTS: Dict[str, Any] = {
+    'maxtime': 240, 'maxiter': 100, 'tolresid': 1e-15,
+    'inner_maxiter': None, 'inner_maxtime': None,
+    'initial_TR_radius': None, 'minimal_initial_TR_radius': 1e-15, 'maximal_TR_radius': 10,
+    'rho': 0.1, 'reduction_regularization': 1e3, 'gamma': 0.25,
+    'forcing_function_Lagrangian': lambda mu: max(mu, 1e-14),
+    'forcing_function_complementarity': lambda mu: max(1e-3 * mu, 1e-14),
+    'forcing_function_second_order': lambda mu: mu,
+    'min_barrier_parameter': 1e-15,
+    'TRS_solver': 'Exact_RepMat', 'second_order_stationarity': True,
+    'do_euclidean_lincomb': False, 'is_euclidean_embedded': False,
+    'TRS_tolresid': 1e-12, 'TRS_tolhardcase': 1e-8,
+    'tCG_theta': 1, 'tCG_kappa': 0.1, 'tCG_mininner': 1,
+    'checkTRSoptimality': False,
+    'initial_barrier_parameter': 0.1,
+    'barrier_parameter_update_r': 0.01, 'barrier_parameter_update_c': 0.5,
+    'barrier_parameter_update_b': 0.8, 'do_simple_barrier_parameter_update': True,
+    'const_left': 0.5, 'const_right': 1e+20,
+    'basisfun': None,
+    'verbosity': 0,
+    'manviofun': lambda problem, x: 0,
+    'callbackfun': None,
+    'save_inner_iteration': True, 'wandb_logging': False,
+    'do_exit_on_error': True,
+}
+
+
+def mu_schedule(o: Dict[str, Any], maxlen: int) -> List[float]:
+    """mu_0, mu_1, ... exactly as RIPTRM.py:852 and :890-893 compute them (Python floats),
+    truncated once the sequence reaches a fixed point (the device then repeats the last one)."""
+    mu = o['initial_barrier_parameter']
+    out = [mu]
+    while len(out) < maxlen:
+        if o['do_simple_barrier_parameter_update']:
+            nxt = max(o['min_barrier_parameter'],
+                      o['barrier_parameter_update_c'] * (mu ** (1 + o['barrier_parameter_update_r'])))
+        else:
+            nxt = max(o['min_barrier_parameter'],
+                      min(o['barrier_parameter_update_b'] * mu,
+                          o['barrier_parameter_update_c'] * (mu ** (1 + o['barrier_parameter_update_r']))))
+        out.append(nxt)
+        if nxt == mu:
+            break
+        mu = nxt
+    return out
+
+
+def manvio_kind(f) -> int:
+    """Classify the 'manviofun' option numerically: 0 (identically zero) or 1 (||x|| - 1)."""
+    if f is None:
+        return C["RIPTRM_MANVIO_ZERO"]
+    a = f(None, np.array([3.0, 4.0]))
+    b = f(None, np.array([0.6, 0.8]))
+    if abs(a) == 0 and abs(b) == 0:
+        return C["RIPTRM_MANVIO_ZERO"]
+    if abs(a - 4.0) < 1e-12 and abs(b) < 1e-12:
+        return C["RIPTRM_MANVIO_SPHERE"]
+    raise NotImplementedError("manviofun must be 0 or ||x||-1 (the NonnegPCA simulator's); "
+                              "arbitrary Python callables cannot run on the device")
+
+
+@dataclass
+class ResolvedOptions:
+    option: Dict[str, Any]
+    c_opt: N.RiptrmOptions
+    mu_tab: List[float]
+    tolL_tab: List[float]
+    tolC_tab: List[float]
+
+
+def resolve_options(option: Dict[str, Any], typical_dist: float, log_capacity: int) -> ResolvedOptions:
+    o = dict(REFERENCE_DEFAULTS)
+    o.update(option or {})
+    if o['TRS_solver'] != 'tCG':
+        raise NotImplementedError(
+            f"TRS_solver={o['TRS_solver']!r}: the MI355X path implements the tCG subproblem solver "
+            "(every shipped config selects TRS_solver='tCG', src/NonnegPCA/config_simulation.yaml:21)")
+    if o.get('use_rand'):
+        raise NotImplementedError("use_rand tCG start is not on the reference's path (RIPTRM.py:450)")
+    if o.get('callbackfun') is not None:
+        raise NotImplementedError("callbackfun cannot run on the device")
+    if o.get('wandb_logging'):
+        raise NotImplementedError("wandb logging is not available")
+    maxiter = int(o['maxiter'])
+    tab = mu_schedule(o, maxlen=max(2, maxiter + 2))
+    tolL = [float(o['forcing_function_Lagrangian'](m)) for m in tab]
+    tolC = [float(o['forcing_function_complementarity'](m)) for m in tab]
+    c = N.RiptrmOptions()
+    c.struct_size = ctypes.sizeof(N.RiptrmOptions)
+    c.maxiter = min(maxiter, 2 ** 31 - 2)
+    c.inner_maxiter = -1 if o['inner_maxiter'] is None else int(o['inner_maxiter'])
+    c.tcg_mininner = int(o['tCG_mininner'])
+    c.save_inner_iteration = 1 if o['save_inner_iteration'] else 0
+    c.manvio_kind = manvio_kind(o['manviofun'])
+    c.log_capacity = int(log_capacity)
+    c.maxtime = float(o['maxtime']) if o['maxtime'] is not None else math.inf
+    c.inner_maxtime = -1.0 if o['inner_maxtime'] is None else float(o['inner_maxtime'])
+    c.tolresid = float(o['tolresid'])
+    c.initial_tr_radius = (typical_dist / 8) if o['initial_TR_radius'] is None else float(o['initial_TR_radius'])
+    c.minimal_initial_tr_radius = float(o['minimal_initial_TR_radius'])
+    c.maximal_tr_radius = float(o['maximal_TR_radius'])
+    c.rho = float(o['rho'])
+    c.reduction_regularization = float(o['reduction_regularization'])
+    c.gamma = float(o['gamma'])
+    c.tcg_theta = float(o['tCG_theta'])
+    c.tcg_kappa = float(o['tCG_kappa'])
+    c.const_left = float(o['const_left'])
+    c.const_right = float(o['const_right'])
+    return ResolvedOptions(o, c, tab, tolL, tolC)
+
+
+def _stream_handle(device: torch.device) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+class NonnegPCABatch:
+    """A batch of NonnegPCA instances with a common n, resident on one GPU."""
+
+    def __init__(self, n: int, batch: int, device: Optional[int] = None, log_capacity: int = 4096):
+        if not torch.cuda.is_available():
+            raise RuntimeError("NonnegPCABatch needs a ROCm GPU (gfx950); there is no CPU fallback")
+        if n < 2 or batch < 1:
+            raise ValueError("need n >= 2 and batch >= 1")
+        self.lib = N.load()
+        self.device = torch.device("cuda", torch.cuda.current_device() if device is None else device)
+        self.n, self.batch, self.cap = int(n), int(batch), int(log_capacity)
+        self.ld = int(self.lib.riptrm_nonnegpca_ld(self.n))
+        self.rows = int(self.lib.riptrm_nonnegpca_rows(self.n))
+        self.inst_stride = self.rows * self.ld
+        self.ctx = N.Context(self.device.index, _stream_handle(self.device))
+        self.S = torch.zeros((self.batch, self.rows, self.ld), dtype=torch.float64, device=self.device)
+        nbytes = int(self.lib.riptrm_workspace_bytes(self.n, self.batch, self.cap))
+        self.ws = torch.zeros(nbytes + 256, dtype=torch.uint8, device=self.device)
+        base = self.ws.data_ptr()
+        self._ws_pad = (-base) % 256
+        self.ws_ptr = base + self._ws_pad
+        self.ws_bytes = nbytes
+        self.bound = False
+        self._keep: List[torch.Tensor] = []
+
+    # ---- views into the workspace -------------------------------------------------------
+    def _view(self, kind: int, shape, dtype=torch.float64):
+        off = int(self.lib.riptrm_workspace_offset(self.n, self.batch, self.cap, kind))
+        count = int(np.prod(shape))
+        start = self._ws_pad + off
+        return self.ws[start:start + count * 8].view(dtype).view(*shape)
+
+    def vec(self, kind: int) -> torch.Tensor:
+        """kind 0 = x, 1 = y, 2 = eta, 3 = Heta (batch, n) views (no copy)."""
+        return self._view(kind, (self.batch, self.ld))[:, :self.n]
+
+    def stats(self) -> np.ndarray:
+        return self._view(4, (self.batch, NSTAT)).cpu().numpy().copy()
+
+    def log_rows(self, count: int) -> np.ndarray:
+        lg = self._view(5, (self.batch, self.cap, NLOG))
+        return lg[:, :max(0, min(count, self.cap))].cpu().numpy()
+
+    # ---- data ---------------------------------------------------------------------------
+    def _sync_stream(self):
+        self.ctx.set_stream(_stream_handle(self.device))
+
+    def load_Z(self, Z) -> "NonnegPCABatch":
+        """Z: (batch, n, n) fp64 (numpy or torch).  S_b = Z_b + Z_b^T on the device."""
+        Zt = torch.as_tensor(Z, dtype=torch.float64)
+        if Zt.shape != (self.batch, self.n, self.n):
+            raise ValueError(f"Z must be {(self.batch, self.n, self.n)}, got {tuple(Zt.shape)}")
+        self.S.zero_()
+        for b in range(self.batch):
+            self.S[b, :self.n, :self.n].copy_(Zt[b].to(self.device, non_blocking=True))
+        return self.symmetrize()
+
+    def symmetrize(self) -> "NonnegPCABatch":
+        """In place S <- S + S^T on the device (the buffer holds Z in its leading n x n corner)."""
+        self._sync_stream()
+        self.ctx.check(self.lib.riptrm_nonnegpca_symmetrize(self.ctx.h, ctypes.c_void_p(self.S.data_ptr()),
+                                                            self.n, self.batch, self.ld, self.inst_stride),
+                       "riptrm_nonnegpca_symmetrize")
+        self.bind()
+        return self
+
+    def bind(self):
+        self._sync_stream()
+        self.ctx.check(self.lib.riptrm_nonnegpca_bind(self.ctx.h, ctypes.c_void_p(self.S.data_ptr()), self.n,
+                                                      self.batch, self.ld, self.inst_stride,
+                                                      ctypes.c_void_p(self.ws_ptr), self.ws_bytes, self.cap),
+                       "riptrm_nonnegpca_bind")
+        self.bound = True
+
+    def generate_synthetic(self, seed0: int = 20251212, snr: float = 0.5, delta: float = 0.7,
+                           ids: Optional[Sequence[int]] = None):
+        """Synthetic instances with the reference recipe's distribution
+        (src/NonnegPCA/generator.py:9-65) drawn on the device with torch's Philox generator:
+        Z = sqrt(snr) v v^T + N(0,1)/sqrt(n) with diagonal N(0,1)*2/sqrt(n), v = 1/sqrt(|S|) on a
+        random floor(delta n)-subset; feasible x0 = |u|/||u||, u ~ U[0,1)^n; y0 = 1.
+        Slot b uses seed ``seed0 + ids[b]`` (ids defaults to 0..batch-1, i.e. global instance
+        ids, so a sharded run draws the same instances as an unsharded one).
+        Returns (x0, y0) device tensors (batch, n)."""
+        n = self.n
+        k = int(np.floor(delta * n))
+        x0 = torch.empty((self.batch, n), dtype=torch.float64, device=self.device)
+        y0 = torch.ones((self.batch, n), dtype=torch.float64, device=self.device)
+        self.S.zero_()
+        ids = list(range(self.batch)) if ids is None else list(ids)
+        if len(ids) != self.batch:
+            raise ValueError("ids must have one entry per batch slot")
+        for b in range(self.batch):
+            g = torch.Generator(device=self.device)
+            g.manual_seed(int(seed0) + int(ids[b]))
+            idx = torch.randperm(n, generator=g, device=self.device)[:k]
+            v = torch.zeros(n, dtype=torch.float64, device=self.device)
+            v[idx] = 1.0 / math.sqrt(k)
+            Zb = self.S[b, :n, :n]
+            Zb.normal_(0.0, 1.0, generator=g).div_(math.sqrt(n))
+            dg = torch.randn(n, dtype=torch.float64, device=self.device, generator=g) * 2 / math.sqrt(n)
+            Zb.diagonal().copy_(dg)
+            Zb.add_(math.sqrt(snr) * torch.outer(v, v))
+            u = torch.rand(n, dtype=torch.float64, device=self.device, generator=g)
+            x0[b] = (u / torch.linalg.vector_norm(u)).abs()
+        self.symmetrize()
+        return x0, y0
+
+    # ---- operators ----------------------------------------------------------------------
+    def _padded(self, a) -> torch.Tensor:
+        t = torch.as_tensor(a, dtype=torch.float64)
+        if t.dim() == 1:
+            t = t.unsqueeze(0)
+        if t.shape != (self.batch, self.n):
+            raise ValueError(f"expected {(self.batch, self.n)}, got {tuple(t.shape)}")
+        out = torch.zeros((self.batch, self.ld), dtype=torch.float64, device=self.device)
+        out[:, :self.n] = t.to(self.device)
+        return out
+
+    def hvp(self, x, y, mu: float, v) -> torch.Tensor:
+        """HwCur(v) at (x, y, mu) for every instance (RIPTRM.py:729)."""
+        assert self.bound
+        X, Y, V = self._padded(x), self._padded(y), self._padded(v)
+        out = torch.zeros_like(X)
+        self._sync_stream()
+        self.ctx.check(self.lib.riptrm_nonnegpca_hvp(self.ctx.h, ctypes.c_void_p(X.data_ptr()),
+                                                     ctypes.c_void_p(Y.data_ptr()), float(mu),
+                                                     ctypes.c_void_p(V.data_ptr()), ctypes.c_void_p(out.data_ptr()),
+                                                     self.ld), "riptrm_nonnegpca_hvp")
+        torch.cuda.synchronize(self.device)
+        return out[:, :self.n]
+
+    def tcg(self, x, y, mu, Delta, max_steps: int = 0):
+        """truncated_conjugate_gradient at (x_b, y_b, mu_b, Delta_b) (RIPTRM.py:41-216 via
+        compute_direction :445-452).  Returns (eta, Heta, j, stop_names)."""
+        assert self.bound
+        X, Y = self._padded(x), self._padded(y)
+        mu_t = torch.as_tensor(np.broadcast_to(np.asarray(mu, dtype=np.float64), (self.batch,)).copy(),
+                               device=self.device)
+        de_t = torch.as_tensor(np.broadcast_to(np.asarray(Delta, dtype=np.float64), (self.batch,)).copy(),
+                               device=self.device)
+        it = (ctypes.c_int32 * self.batch)()
+        st = (ctypes.c_int32 * self.batch)()
+        self._sync_stream()
+        self.ctx.check(self.lib.riptrm_tcg(self.ctx.h, ctypes.c_void_p(X.data_ptr()), ctypes.c_void_p(Y.data_ptr()),
+                                           self.ld, ctypes.c_void_p(mu_t.data_ptr()), ctypes.c_void_p(de_t.data_ptr()),
+                                           it, st, int(max_steps)), "riptrm_tcg")
+        eta = self.vec(2).clone()
+        heta = self.vec(3).clone()
+        return eta, heta, np.array(list(it)), [TCG_NAMES[s] for s in st]
+
+    # ---- full solve ---------------------------------------------------------------------
+    def begin(self, x0, y0, option: Dict[str, Any]) -> ResolvedOptions:
+        assert self.bound
+        ro = resolve_options(option, math.pi, self.cap)
+        X, Y = self._padded(x0), self._padded(y0)
+        tabs = [torch.tensor(t, dtype=torch.float64, device=self.device) for t in (ro.mu_tab, ro.tolL_tab, ro.tolC_tab)]
+        self._keep = [X, Y] + tabs
+        self._sync_stream()
+        self.ctx.check(self.lib.riptrm_solve_begin(self.ctx.h, ctypes.byref(ro.c_opt), ctypes.c_void_p(X.data_ptr()),
+                                                   ctypes.c_void_p(Y.data_ptr()), self.ld,
+                                                   ctypes.c_void_p(tabs[0].data_ptr()), ctypes.c_void_p(tabs[1].data_ptr()),
+                                                   ctypes.c_void_p(tabs[2].data_ptr()), len(ro.mu_tab)),
+                       "riptrm_solve_begin")
+        self.ro = ro
+        self._target = 2 ** 31 - 1
+        return ro
+
+    def advance(self, steps: int, outer_target: Optional[int] = None) -> int:
+        tgt = 2 ** 31 - 1 if outer_target is None else int(outer_target)
+        act = ctypes.c_int32(0)
+        self._sync_stream()
+        self.ctx.check(self.lib.riptrm_solve_advance(self.ctx.h, int(steps), tgt, ctypes.byref(act)),
+                       "riptrm_solve_advance")
+        return int(act.value)
+
+    def run_until(self, outer_target: Optional[int] = None, max_chunk: int = 512, timeout_s: float = 1e9) -> int:
+        """Advance until every instance is finished or paused at ``outer_target``."""
+        chunk, t0 = 4, time.time()
+        act = self.advance(0, outer_target)
+        while act > 0:
+            act = self.advance(chunk, outer_target)
+            chunk = min(chunk * 2, max_chunk)
+            if time.time() - t0 > timeout_s:
+                raise TimeoutError("RIPTRM device solve exceeded the host timeout")
+        return act
+
+    def solve(self, x0, y0, option: Dict[str, Any]) -> "BatchResult":
+        self.begin(x0, y0, option)
+        self.run_until(None)
+        return self.result()
+
+    def result(self) -> "BatchResult":
+        torch.cuda.synchronize(self.device)
+        st = self.stats()
+        x = self.vec(0).clone()
+        y = self.vec(1).clone()
+        count = int(st[:, C["RIPTRM_STAT_LOG_COUNT"]].max()) if self.batch else 0
+        logs = self.log_rows(count)
+        return BatchResult(x=x, y=y, stats=st, raw_log=logs, ro=self.ro)
+
+
+@dataclass
+class BatchResult:
+    x: torch.Tensor
+    y: torch.Tensor
+    stats: np.ndarray
+    raw_log: np.ndarray
+    ro: ResolvedOptions
+
+    def stat(self, b: int, name: str) -> float:
+        return float(self.stats[b, C[f"RIPTRM_STAT_{name}"]])
+
+    def stopping_criterion(self, b: int) -> Optional[str]:
+        code = int(self.stat(b, "STOP_CODE"))
+        rt = self.stat(b, "STOP_RUNTIME")
+        o = self.ro.option
+        if code == C["RIPTRM_STOP_MAXTIME"]:
+            return f"Max time exceeded; runtime={rt:.2f} and maxtime={o['maxtime']}"
+        if code == C["RIPTRM_STOP_MAXITER"]:
+            return f"Max iteration count reached; maxiter={o['maxiter']} after {rt:.2f} seconds"
+        if code == C["RIPTRM_STOP_TOLRESID"]:
+            res = np.float64(self.stat(b, "FINAL_RESIDUAL"))
+            return ("KKT residual tolerance reached; current residual=" + str(res)
+                    + " and tolresid=" + str(o['tolresid']) + f" after {rt:.2f} seconds")
+        return None
+
+    def log(self, b: int) -> Dict[str, list]:
+        """Instance b's log in the reference's column schema (base_solver.py:58-76,
+        utils.py:356-364, RIPTRM.py:986-1023)."""
+        cnt = min(int(self.stat(b, "LOG_COUNT")), self.raw_log.shape[1])
+        save_inner = bool(self.ro.option['save_inner_iteration'])
+        cols: Dict[str, list] = {k: [] for k in (
+            "iteration", "time", "cost", "distance", "residual", "gradnorm", "complviolation",
+            "dualviolation", "manviolation", "maxviolation", "meanviolation", "mu", "num_inner",
+            "inner_status", "TR_radius")}
+        extra = ("dxtype", "normdx", "minxfeasi", "minyfeasi", "compl", "mineigvalHw", "ared/pred",
+                 "radius_update", "dual_clipping")
+        if save_inner:
+            for k in extra:
+                cols[k] = []
+        cols["maxabsLagmult"] = []
+        F = lambda name: C[f"RIPTRM_LOG_{name}"]
+        for r in self.raw_log[b, :cnt]:
+            it = int(r[F("ITERATION")])
+            cols["iteration"].append(it)
+            cols["time"].append(0 if len(cols["time"]) == 0 else float(r[F("TIME")]))
+            for k, f in (("cost", "COST"), ("distance", "DISTANCE"), ("residual", "RESIDUAL"),
+                         ("gradnorm", "GRADNORM"), ("complviolation", "COMPLVIOLATION"),
+                         ("dualviolation", "DUALVIOLATION"), ("manviolation", "MANVIOLATION"),
+                         ("maxviolation", "MAXVIOLATION"), ("meanviolation", "MEANVIOLATION"),
+                         ("mu", "MU")):
+                cols[k].append(np.float64(r[F(f)]))
+            has = r[F("HAS_INFO")] != 0
+            cols["num_inner"].append(int(r[F("NUM_INNER")]) if has else None)
+            cols["inner_status"].append(STATUS_NAMES[int(r[F("INNER_STATUS")])] if has else None)
+            cols["TR_radius"].append(np.float64(r[F("TR_RADIUS")]) if has else None)
+            if save_inner:
+                cols["dxtype"].append(f"tCG_{TCG_NAMES[int(r[F('DXTYPE')])]}" if has else None)
+                cols["normdx"].append(np.float64(r[F("NORMDX")]) if has else None)
+                cols["minxfeasi"].append(np.float64(r[F("MINXFEASI")]) if has else None)
+                cols["minyfeasi"].append(np.float64(r[F("MINYFEASI")]) if has else None)
+                cols["compl"].append(np.float64(r[F("COMPL")]) if has else None)
+                cols["mineigvalHw"].append(None)
+                hr = has and r[F("HAS_RATIO")] != 0
+                cols["ared/pred"].append(np.float64(r[F("ARED_PRED")]) if hr else None)
+                cols["radius_update"].append(RU_NAMES[int(r[F("RADIUS_UPDATE")])] if hr else None)
+                dc = int(r[F("DUAL_CLIPPING")])
+                cols["dual_clipping"].append(None if (not has or dc < 0) else bool(dc))
+            cols["maxabsLagmult"].append(np.float64(r[F("MAXABSLAGMULT")]))
+        return cols
+
+    def tcg_iters_per_row(self, b: int) -> List[int]:
+        cnt = min(int(self.stat(b, "LOG_COUNT")), self.raw_log.shape[1])
+        return [int(v) for v in self.raw_log[b, :cnt, C["RIPTRM_LOG_TCG_ITERS"]]]
+
+
+def profile_enable(batch: NonnegPCABatch, on: bool = True):
+    """HIP-event timing of every S-pass / state launch (riptrm_profile_enable)."""
+    batch.ctx.check(batch.lib.riptrm_profile_enable(batch.ctx.h, 1 if on else 0), "riptrm_profile_enable")
+
+
+def profile_read(batch: NonnegPCABatch) -> Dict[str, float]:
+    gm, sm = ctypes.c_double(0), ctypes.c_double(0)
+    gn, sn = ctypes.c_int64(0), ctypes.c_int64(0)
+    batch.ctx.check(batch.lib.riptrm_profile_read(batch.ctx.h, ctypes.byref(gm), ctypes.byref(gn),
+                                                  ctypes.byref(sm), ctypes.byref(sn)), "riptrm_profile_read")
+    return {"gemv_ms": gm.value, "gemv_launches": gn.value, "state_ms": sm.value, "state_launches": sn.value}

@@ -1,0 +1,219 @@
+"""GPU parity tests: the HIP path (through the C-ABI) against the CPU oracle on the same inputs.
+
+Tolerances (fp64 throughout; the only differences are reduction order and libm-vs-ocml log/acos):
+* operator level (S-pass, barrier Hessian, tCG step from the same state): rel 1e-12 / 1e-9;
+* trajectory level (whole solve): identical branch decisions (inner_status, dxtype, radius
+  updates) and residuals within rtol 1e-6 — the same bound the two CPU back-ends meet against
+  each other (tests/test_oracle.py::test_structured_matches_vectorized_fixture).
+"""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+from oracle import nonnegpca_gen as G
+from oracle import riptrm_oracle as O
+
+OPT = dict(tolresid=0.0, maxtime=1e9)
+
+
+def _engine(Z, cap=4096):
+    import engine
+    Z = np.asarray(Z)
+    if Z.ndim == 2:
+        Z = Z[None]
+    eng = engine.NonnegPCABatch(Z.shape[1], Z.shape[0], log_capacity=cap)
+    eng.load_Z(Z)
+    return eng
+
+
+def _gpu_opt(**kw):
+    from problems import manviofun
+    o = {"TRS_solver": "tCG", "second_order_stationarity": False, "manviofun": manviofun}
+    o.update(OPT)
+    o.update(kw)
+    return o
+
+
+def _oracle_opt(**kw):
+    o = dict(OPT, manviofun=O.sphere_manvio)
+    o.update(kw)
+    return o
+
+
+def _state(n, seed):
+    rs = np.random.RandomState(seed)
+    x = np.abs(rs.rand(n)) + 1e-3
+    x /= np.linalg.norm(x)
+    y = rs.rand(n) + 0.05
+    return x, y
+
+
+@pytest.mark.parametrize("n", [2, 17, 50, 333, 1000])
+def test_symmetrize_and_spass(n):
+    Z, _, _ = G.generate_instance(n, 3)
+    eng = _engine(np.stack([Z, Z.T * 0.5]))
+    S = eng.S[:, :n, :n].cpu().numpy()
+    np.testing.assert_array_equal(S[0], Z + Z.T)          # exact: one add per element
+    np.testing.assert_array_equal(S[0], S[0].T)
+    assert float(eng.S[:, n:, :].abs().sum()) == 0 and float(eng.S[:, :, n:].abs().sum()) == 0
+
+
+@pytest.mark.parametrize("n,B", [(17, 3), (50, 2), (1000, 3), (4000, 2)])
+def test_barrier_hessian_matches_oracle(n, B):
+    Zs, xs, ys, vs = [], [], [], []
+    for b in range(B):
+        Z, _, _ = G.generate_instance(n, 10 + b)
+        x, y = _state(n, 20 + b)
+        Zs.append(Z); xs.append(x); ys.append(y)
+        vs.append(np.random.RandomState(30 + b).randn(n))
+    eng = _engine(np.stack(Zs))
+    mu = 0.0123
+    out = eng.hvp(np.stack(xs), np.stack(ys), mu, np.stack(vs)).cpu().numpy()
+    for b in range(B):
+        P = O.NonnegPCAVectorized(Zs[b])
+        _, _, Hw, _ = P.begin_inner(xs[b], ys[b], mu)
+        ref = Hw(vs[b])
+        err = np.linalg.norm(out[b] - ref) / np.linalg.norm(ref)
+        assert err < 1e-12, (b, err)
+
+
+@pytest.mark.parametrize("n", [50, 200, 1000])
+def test_tcg_matches_oracle_teacher_forced(n):
+    """Same (x, y, mu, Delta) in -> same tCG exit (stop reason, j) and eta."""
+    B = 6
+    Zs, xs, ys = [], [], []
+    for b in range(B):
+        Z, x0, y0 = G.generate_instance(n, 40 + b)
+        Zs.append(Z); xs.append(x0); ys.append(y0)
+    mus = np.array([0.1, 0.05, 1e-2, 1e-3, 0.1, 0.02])
+    deltas = np.array([np.pi / 8, 1e-3, 0.05, 0.3, 5.0, 0.01])
+    eng = _engine(np.stack(Zs))
+    eta, heta, js, stops = eng.tcg(np.stack(xs), np.stack(ys), mus, deltas)
+    eta = eta.cpu().numpy()
+    heta = heta.cpu().numpy()
+    for b in range(B):
+        P = O.NonnegPCAVectorized(Zs[b])
+        _, _, Hw, c = P.begin_inner(xs[b], ys[b], mus[b])
+        e, he, j, stop = O.truncated_conjugate_gradient(P.manifold, Hw, xs[b], c, deltas[b], 1, 0.1, 1, n - 1)
+        assert stops[b] == stop, (b, stops[b], stop)
+        assert js[b] == j, (b, js[b], j)
+        assert np.linalg.norm(eta[b] - e) <= 1e-9 * max(np.linalg.norm(e), 1e-300), b
+        assert np.linalg.norm(heta[b] - he) <= 1e-8 * max(np.linalg.norm(he), 1e-300), b
+
+
+def _compare_logs(gl, rl, rtol=1e-6, atol=1e-13):
+    assert list(gl.keys()) == list(rl.keys())
+    assert len(gl["iteration"]) == len(rl["iteration"]), (len(gl["iteration"]), len(rl["iteration"]))
+    for k in ("iteration", "num_inner", "inner_status", "dxtype", "radius_update", "dual_clipping"):
+        if k in gl:
+            assert gl[k] == rl[k], k
+    for k in ("residual", "cost", "gradnorm", "complviolation", "mu", "normdx", "TR_radius"):
+        if k in gl:
+            g = np.array([np.nan if v is None else v for v in gl[k]], dtype=float)
+            r = np.array([np.nan if v is None else v for v in rl[k]], dtype=float)
+            np.testing.assert_allclose(g, r, rtol=rtol, atol=atol, equal_nan=True, err_msg=k)
+
+
+def test_full_solve_fixture_n50(fixture_n50):
+    from problems import NonnegPCAProblem
+    from RIPTRM import RIPTRM
+    Z, x0, y0 = fixture_n50
+    out = RIPTRM(_gpu_opt(maxiter=12)).run(NonnegPCAProblem(Z=Z, initialpoint=x0, initialineqLagmult=y0))
+    ref = O.solve(Z, x0, y0, _oracle_opt(maxiter=12))
+    assert f"{out.log['residual'][0]:.6e}" == "4.986888e+00"
+    _compare_logs(out.log, ref.log)
+    np.testing.assert_allclose(out.x, ref.x, atol=1e-7)
+    np.testing.assert_allclose(out.ineqLagmult, ref.y, rtol=1e-5, atol=1e-8)
+    assert out.option["stoppingcriterion"].startswith("Max iteration count reached; maxiter=12 after")
+    assert out.name == "RIPTRM_tCG"
+
+
+def test_fixture_reaches_published_residual_on_gpu(fixture_n50):
+    """analyzer.ipynb: RIPTRM (tCG) on dataset/NonnegPCA/1/a plateaus at ~1e-14."""
+    from problems import NonnegPCAProblem
+    from RIPTRM import RIPTRM
+    Z, x0, y0 = fixture_n50
+    out = RIPTRM(_gpu_opt(maxiter=45)).run(NonnegPCAProblem(Z=Z, initialpoint=x0, initialineqLagmult=y0))
+    res = np.array(out.log["residual"], float)
+    conv = [i for i, s in enumerate(out.log["inner_status"]) if s in (None, "converged")]
+    assert res[conv][-1] < 2e-14
+
+
+@pytest.mark.parametrize("n,B,K", [(37, 5, 10), (200, 4, 12), (1000, 2, 10)])
+def test_batched_solve_matches_oracle(n, B, K):
+    insts = [G.generate_instance(n, 100 + b) for b in range(B)]
+    eng = _engine(np.stack([z for z, _, _ in insts]))
+    res = eng.solve(np.stack([x for _, x, _ in insts]), np.stack([y for _, _, y in insts]), _gpu_opt(maxiter=K))
+    xs = res.x.cpu().numpy()
+    for b, (Z, x0, y0) in enumerate(insts):
+        ref = O.solve(Z, x0, y0, _oracle_opt(maxiter=K))
+        _compare_logs(res.log(b), ref.log)
+        np.testing.assert_allclose(xs[b], ref.x, atol=1e-6)
+        assert int(res.stat(b, "TCG_ITERS")) == ref.tcg_iterations
+        assert int(res.stat(b, "PASSES")) == ref.passes
+
+
+def test_edge_options_match_oracle():
+    Z, x0, y0 = G.generate_instance(9, 7)
+    cases = [dict(maxiter=0), dict(maxiter=4, tolresid=1e3), dict(maxiter=3, inner_maxiter=1),
+             dict(maxiter=4, save_inner_iteration=False), dict(maxiter=3, initial_TR_radius=1e-4),
+             dict(maxiter=5, do_simple_barrier_parameter_update=False)]
+    for kw in cases:
+        eng = _engine(Z)
+        res = eng.solve(x0[None], y0[None], _gpu_opt(**kw))
+        ref = O.solve(Z, x0, y0, _oracle_opt(**kw))
+        _compare_logs(res.log(0), ref.log)
+        assert (res.stopping_criterion(0) or "").split(" after")[0] == ref.stoppingcriterion.split(" after")[0], kw
+
+
+def test_tiny_n2():
+    Z, x0, y0 = G.generate_instance(2, 1)
+    eng = _engine(Z)
+    res = eng.solve(x0[None], y0[None], _gpu_opt(maxiter=6))
+    ref = O.solve(Z, x0, y0, _oracle_opt(maxiter=6))
+    _compare_logs(res.log(0), ref.log)
+
+
+def test_pause_resume_is_transparent():
+    """Stopping every instance at outer-iteration targets and resuming changes nothing."""
+    n, B = 120, 3
+    insts = [G.generate_instance(n, 300 + b) for b in range(B)]
+    Z = np.stack([z for z, _, _ in insts])
+    X0 = np.stack([x for _, x, _ in insts])
+    Y0 = np.stack([y for _, _, y in insts])
+    e1 = _engine(Z)
+    r1 = e1.solve(X0, Y0, _gpu_opt(maxiter=9))
+    e2 = _engine(Z)
+    e2.begin(X0, Y0, _gpu_opt(maxiter=9))
+    for tgt in (2, 5, 7, None):
+        e2.run_until(tgt)
+    r2 = e2.result()
+    for b in range(B):
+        a, c = r1.log(b), r2.log(b)
+        for k in a:
+            if k != "time":
+                assert a[k] == c[k] or np.allclose(np.array(a[k], float), np.array(c[k], float), rtol=0, atol=0), k
+    assert torch.equal(r1.x, r2.x)
+
+
+def test_large_n4000_properties():
+    """n = 4000 (BASELINE config 3's size): symmetric operator, tangent output, S-pass vs torch."""
+    n = 4000
+    Z, x0, y0 = G.generate_instance(n, 4242)
+    eng = _engine(Z)
+    S = eng.S[0, :n, :n]
+    rs = np.random.RandomState(1)
+    x = x0
+    y = rs.rand(n) + 0.1
+    u = rs.randn(n); u -= (x @ u) * x
+    v = rs.randn(n); v -= (x @ v) * x
+    Hu = eng.hvp(x, y, 0.01, u).cpu().numpy()[0]
+    Hv = eng.hvp(x, y, 0.01, v).cpu().numpy()[0]
+    assert abs(u @ Hv - v @ Hu) <= 1e-10 * np.linalg.norm(Hu) * np.linalg.norm(v)
+    P = O.NonnegPCAVectorized(Z)
+    _, _, Hw, _ = P.begin_inner(x, y, 0.01)
+    assert np.linalg.norm(Hu - Hw(u)) <= 1e-12 * np.linalg.norm(Hu)
+    Sx = (S @ torch.tensor(x, device=S.device)).cpu().numpy()
+    np.testing.assert_allclose(Sx, (Z + Z.T) @ x, rtol=1e-12, atol=1e-12)

@@ -1,0 +1,140 @@
+"""CPU-side checks of the C-ABI library and the host logic (no GPU compute calls)."""
+import ctypes
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from conftest import ROOT
+
+import riptrm_native as N
+
+
+def test_library_exports_every_header_symbol(built_lib):
+    syms = N.header_symbols()
+    assert len(syms) >= 15
+    missing = [s for s in syms if not hasattr(built_lib, s)]
+    assert not missing, missing
+    # and the ctypes signature table covers exactly the header
+    assert sorted(N.SIGNATURES) == syms
+
+
+def test_abi_version_and_no_device(built_lib):
+    assert built_lib.riptrm_abi_version() == N.CONST["RIPTRM_ABI_VERSION"]
+    try:
+        import torch
+        has_gpu = torch.cuda.is_available()
+    except Exception:
+        has_gpu = False
+    if has_gpu:
+        pytest.skip("a GPU is visible")
+    h = ctypes.c_void_p()
+    rc = built_lib.riptrm_ctx_create(ctypes.byref(h), 0, None)
+    assert rc == N.CONST["RIPTRM_E_NODEV"]
+    assert h.value is None
+
+
+def test_layout_functions(built_lib):
+    for n in (2, 17, 50, 1000, 4000, 4001):
+        ld = built_lib.riptrm_nonnegpca_ld(n)
+        rows = built_lib.riptrm_nonnegpca_rows(n)
+        assert ld >= n and ld % 16 == 0 and ld - n < 16
+        assert rows >= n and rows % 16 == 0
+        for B, cap in ((1, 0), (3, 10), (128, 4096)):
+            tot = built_lib.riptrm_workspace_bytes(n, B, cap)
+            offs = [built_lib.riptrm_workspace_offset(n, B, cap, k) for k in range(6)]
+            assert all(0 <= o < tot for o in offs[:5])
+            assert offs[0] == 0 and offs[1] == B * ld * 8
+            assert all(o % 256 == 0 or k < 4 for k, o in enumerate(offs))
+            assert offs[5] + B * cap * 32 * 8 <= tot
+    assert built_lib.riptrm_workspace_bytes(0, 1, 1) == -1
+    assert built_lib.riptrm_workspace_offset(10, 1, 1, 9) == -1
+
+
+def test_options_struct_layout_matches_c(tmp_path):
+    """ctypes RiptrmOptions == the C struct (sizeof and every offset), compiled with gcc."""
+    fields = [f for f, _ in N.RiptrmOptions._fields_]
+    src = tmp_path / "probe.c"
+    body = "\n".join(f'printf("%zu\\n", offsetof(riptrm_options, {f}));' for f in fields)
+    src.write_text(f'#include <stdio.h>\n#include <stddef.h>\n#include "riptrm.h"\n'
+                   f'int main(void){{printf("%zu\\n", sizeof(riptrm_options));\n{body}\nreturn 0;}}\n')
+    exe = tmp_path / "probe"
+    subprocess.run(["gcc", "-std=c99", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], check=True)
+    vals = [int(v) for v in subprocess.check_output([str(exe)]).split()]
+    assert vals[0] == ctypes.sizeof(N.RiptrmOptions)
+    for f, off in zip(fields, vals[1:]):
+        assert getattr(N.RiptrmOptions, f).offset == off, f
+
+
+def test_resolve_options_defaults_and_errors():
+    import engine
+    from problems import manviofun
+    with pytest.raises(NotImplementedError):
+        engine.resolve_options({}, np.pi, 16)  # reference default TRS_solver is Exact_RepMat
+    ro = engine.resolve_options({"TRS_solver": "tCG", "manviofun": manviofun, "maxiter": 50}, np.pi, 16)
+    c = ro.c_opt
+    assert c.struct_size == ctypes.sizeof(N.RiptrmOptions)
+    assert c.maxiter == 50 and c.inner_maxiter == -1 and c.inner_maxtime == -1.0
+    assert c.initial_tr_radius == np.pi / 8
+    assert c.manvio_kind == N.CONST["RIPTRM_MANVIO_SPHERE"]
+    assert c.rho == 0.1 and c.gamma == 0.25 and c.const_right == 1e20
+    assert ro.tolL_tab[0] == 0.1 and ro.tolC_tab[0] == 1e-4
+    assert ro.tolL_tab[-1] == 1e-14 and ro.tolC_tab[-1] == 1e-14
+    ro0 = engine.resolve_options({"TRS_solver": "tCG"}, np.pi, 16)
+    assert ro0.c_opt.manvio_kind == N.CONST["RIPTRM_MANVIO_ZERO"]
+    with pytest.raises(NotImplementedError):
+        engine.resolve_options({"TRS_solver": "tCG", "manviofun": lambda p, x: float(np.sum(x))}, np.pi, 16)
+    with pytest.raises(NotImplementedError):
+        engine.resolve_options({"TRS_solver": "tCG", "callbackfun": lambda *a: a[-1]}, np.pi, 16)
+
+
+def test_log_decoding_schema_matches_oracle(fixture_n50):
+    """A raw device log decodes into the reference's columns in the reference's order."""
+    import engine
+    from oracle import riptrm_oracle as O
+    C = N.CONST
+    Z, x0, y0 = fixture_n50
+    ref = O.solve(Z, x0, y0, dict(maxiter=2, tolresid=0.0, maxtime=1e9, manviofun=O.sphere_manvio))
+    ro = engine.resolve_options({"TRS_solver": "tCG", "maxiter": 2}, np.pi, 8)
+    raw = np.zeros((1, 3, C["RIPTRM_LOG_NFIELDS"]))
+    raw[0, 1, C["RIPTRM_LOG_HAS_INFO"]] = 1
+    raw[0, 1, C["RIPTRM_LOG_INNER_STATUS"]] = C["RIPTRM_IS_SUCCESSFUL"]
+    raw[0, 1, C["RIPTRM_LOG_HAS_RATIO"]] = 1
+    raw[0, 1, C["RIPTRM_LOG_RADIUS_UPDATE"]] = C["RIPTRM_RU_EXPANDED"]
+    raw[0, 1, C["RIPTRM_LOG_DUAL_CLIPPING"]] = 0
+    raw[0, 2, C["RIPTRM_LOG_HAS_INFO"]] = 1
+    raw[0, 2, C["RIPTRM_LOG_INNER_STATUS"]] = C["RIPTRM_IS_CONVERGED"]
+    raw[0, 2, C["RIPTRM_LOG_DUAL_CLIPPING"]] = -1
+    raw[0, 2, C["RIPTRM_LOG_DXTYPE"]] = C["RIPTRM_TCG_EXCEEDED_TR"]
+    stats = np.zeros((1, C["RIPTRM_STAT_NFIELDS"]))
+    stats[0, C["RIPTRM_STAT_LOG_COUNT"]] = 3
+    stats[0, C["RIPTRM_STAT_STOP_CODE"]] = C["RIPTRM_STOP_MAXITER"]
+    res = engine.BatchResult(x=None, y=None, stats=stats, raw_log=raw, ro=ro)
+    log = res.log(0)
+    assert list(log.keys()) == list(ref.log.keys())
+    assert log["inner_status"] == [None, "successful", "converged"]
+    assert log["radius_update"] == [None, "expanded", None]
+    assert log["dual_clipping"] == [None, False, None]
+    assert log["dxtype"][2] == "tCG_EXCEEDED_TR"
+    assert log["time"][0] == 0
+    assert res.stopping_criterion(0).startswith("Max iteration count reached; maxiter=2 after")
+
+
+def test_product_path_has_no_oracle_dependency():
+    """The shipped package must never import the oracle (no CPU fallback)."""
+    pkg = os.path.join(ROOT, "riemannian-interior-point-trust-region-method_amd")
+    for fn in os.listdir(pkg):
+        if fn.endswith(".py"):
+            txt = open(os.path.join(pkg, fn)).read()
+            assert "oracle" not in txt.replace("oracle/", ""), fn
+
+
+def test_engine_refuses_without_gpu():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is visible")
+    import engine
+    with pytest.raises(RuntimeError):
+        engine.NonnegPCABatch(10, 1)

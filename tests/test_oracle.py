@@ -1,0 +1,158 @@
+"""CPU tests of the oracle (the parity checker) against the reference's known answers and
+internal consistency.  No GPU needed."""
+import numpy as np
+import pytest
+
+from oracle import nonnegpca_gen as G
+from oracle import riptrm_oracle as O
+
+OPT = dict(tolresid=0.0, maxtime=1e9, manviofun=O.sphere_manvio)
+
+
+def _eval0(P, x0, y0):
+    orc = O.RIPTRMOracle(dict(OPT))
+    return orc.evaluation(P, x0, x0, y0)
+
+
+@pytest.mark.parametrize("structured", [False, True])
+def test_initial_residual_known_answer(fixture_n50, structured):
+    """src/NonnegPCA/analyzer.ipynb (cell 5 output): every solver's row 0 on dataset/NonnegPCA/1,
+    point a, has KKT residual 4.986888e+00."""
+    Z, x0, y0 = fixture_n50
+    P = O.NonnegPCAStructured(Z) if structured else O.NonnegPCAVectorized(Z)
+    ev = _eval0(P, x0, y0)
+    assert f"{ev['residual']:.6e}" == "4.986888e+00"
+
+
+def test_fixture_run_reaches_published_residual(fixture_n50):
+    """analyzer.ipynb cell 5 plot: RIPTRM (tCG) reaches ~1e-14 KKT residual and stays flat."""
+    Z, x0, y0 = fixture_n50
+    r = O.solve(Z, x0, y0, dict(OPT, maxiter=45))
+    res = np.array(r.log["residual"], dtype=float)
+    conv = [i for i, s in enumerate(r.log["inner_status"]) if s in (None, "converged")]
+    rc = res[conv]
+    assert rc[-1] < 2e-14
+    # the converged-row residual decreases over the first ~35 outer iterations
+    assert np.all(np.diff(np.log10(rc[:36])) < 0)
+    assert r.stoppingcriterion.startswith("Max iteration count reached; maxiter=45")
+
+
+def test_structured_matches_vectorized_fixture(fixture_n50):
+    Z, x0, y0 = fixture_n50
+    a = O.solve(Z, x0, y0, dict(OPT, maxiter=8), structured=True)
+    b = O.solve(Z, x0, y0, dict(OPT, maxiter=8), structured=False)
+    assert a.log["inner_status"] == b.log["inner_status"]
+    assert a.log["dxtype"] == b.log["dxtype"]
+    # trajectory-level: summation-order differences are amplified by tCG, ~1e-8 relative here
+    np.testing.assert_allclose(np.array(a.log["residual"], float), np.array(b.log["residual"], float),
+                               rtol=1e-6, atol=1e-14)
+    np.testing.assert_allclose(a.x, b.x, atol=1e-7)
+    np.testing.assert_allclose(a.y, b.y, rtol=1e-5, atol=1e-8)
+
+
+def test_barrier_hessian_closed_form_matches_structured():
+    rs = np.random.RandomState(3)
+    n = 23
+    Z = rs.randn(n, n)
+    x = np.abs(rs.rand(n)); x /= np.linalg.norm(x)
+    y = rs.rand(n) + 0.1
+    mu = 0.03
+    Ps, Pv = O.NonnegPCAStructured(Z), O.NonnegPCAVectorized(Z)
+    _, s1, H1, c1 = Ps.begin_inner(x, y, mu)
+    _, s2, H2, c2 = Pv.begin_inner(x, y, mu)
+    np.testing.assert_allclose(c1, c2, rtol=1e-12, atol=1e-13)
+    for _ in range(3):
+        v = Ps.manifold.projection(x, rs.randn(n))
+        np.testing.assert_allclose(H1(v), H2(v), rtol=1e-11, atol=1e-12)
+    np.testing.assert_allclose(Ps.gradlag(x, y), Pv.gradlag(x, y), rtol=1e-12, atol=1e-13)
+
+
+def test_gradient_matches_torch_autograd():
+    torch = pytest.importorskip("torch")
+    rs = np.random.RandomState(5)
+    n = 17
+    Z = rs.randn(n, n)
+    x = rs.randn(n)
+    xt = torch.tensor(x, requires_grad=True)
+    f = -(xt @ torch.tensor(Z) @ xt)
+    (g,) = torch.autograd.grad(f, xt, create_graph=True)
+    v = rs.randn(n)
+    (hv,) = torch.autograd.grad(g @ torch.tensor(v), xt)
+    P = O.NonnegPCAVectorized(Z)
+    np.testing.assert_allclose(-P.S @ x, g.detach().numpy(), rtol=1e-12, atol=1e-12)
+    np.testing.assert_allclose(-P.S @ v, hv.numpy(), rtol=1e-12, atol=1e-12)
+    np.testing.assert_allclose(O.NonnegPCAStructured(Z).euclidean_gradient(x), g.detach().numpy(), atol=1e-12)
+
+
+def test_riemannian_hessian_finite_difference():
+    """Hess f[v] = P(ehess[v]) + W(x, v, normal egrad) (pymanopt Sphere) vs a central difference
+    of the Riemannian gradient along the retraction curve (second-order accurate on the sphere)."""
+    rs = np.random.RandomState(11)
+    n = 12
+    Z = rs.randn(n, n)
+    P = O.NonnegPCAStructured(Z)
+    M = P.manifold
+    x = rs.randn(n); x /= np.linalg.norm(x)
+    v = M.projection(x, rs.randn(n))
+    h = 1e-5
+    gp = P.riemannian_gradient(M.retraction(x, h * v))
+    gm = P.riemannian_gradient(M.retraction(x, -h * v))
+    fd = M.projection(x, (gp - gm) / (2 * h))
+    np.testing.assert_allclose(P.riemannian_hessian(x, v), fd, rtol=1e-6, atol=1e-6)
+
+
+def test_tcg_invariants():
+    rs = np.random.RandomState(7)
+    n = 40
+    Z, x0, y0 = G.generate_instance(n, 99)
+    P = O.NonnegPCAVectorized(Z)
+    M = P.manifold
+    seen = set()
+    for Delta in (1e-3, 0.05, 0.4, 3.0):
+        for mu in (0.1, 1e-3):
+            _, s, Hw, c = P.begin_inner(x0, y0, mu)
+            eta, Heta, j, stop = O.truncated_conjugate_gradient(M, Hw, x0, c, Delta, 1, 0.1, 1, M.dim)
+            seen.add(stop)
+            assert np.linalg.norm(eta) <= Delta * (1 + 1e-10)
+            model = M.inner_product(x0, eta, c) + 0.5 * M.inner_product(x0, eta, Hw(eta))
+            assert model <= 1e-14
+            if stop in ("EXCEEDED_TR", "NEGATIVE_CURVATURE"):
+                assert abs(np.linalg.norm(eta) - Delta) <= 1e-9 * Delta
+            assert abs(x0 @ eta) < 1e-10  # tangent
+            assert 0 <= j < M.dim
+    assert "EXCEEDED_TR" in seen
+
+
+def test_mu_schedule_matches_engine_table():
+    import engine
+    o = dict(engine.REFERENCE_DEFAULTS)
+    tab = engine.mu_schedule(o, 100)
+    ref = O.mu_schedule({}, len(tab))
+    assert tab == ref                                  # bit-exact Python floats
+    assert tab[0] == 0.1 and tab[-1] == 1e-15
+    k20 = tab[20]
+    assert 1.3e-8 < k20 < 1.5e-8                       # mu_20 ~ 1.42e-8
+    assert 36 <= len(tab) <= 41                        # floor 1e-15 after ~38 updates
+
+
+def test_generator_recipe_properties():
+    Z1, x1, y1 = G.generate_instance(60, 5)
+    Z2, x2, y2 = G.generate_instance(60, 5)
+    np.testing.assert_array_equal(Z1, Z2)
+    assert np.all(x1 >= 0) and abs(np.linalg.norm(x1) - 1) < 1e-14
+    assert np.all(y1 == 1)
+    Z3, _, _ = G.generate_instance(60, 6)
+    assert not np.array_equal(Z1, Z3)
+
+
+def test_oracle_edge_paths():
+    """inner_maxiter reset path (RIPTRM.py:835-842), save_inner_iteration=False rows, tiny n."""
+    Z, x0, y0 = G.generate_instance(6, 1)
+    r = O.solve(Z, x0, y0, dict(OPT, maxiter=3, inner_maxiter=1))
+    assert r.outer_iterations == 3
+    r2 = O.solve(Z, x0, y0, dict(OPT, maxiter=4, save_inner_iteration=False))
+    assert r2.log["iteration"] == [0, 1, 2, 3, 4]
+    assert "dxtype" not in r2.log
+    Z, x0, y0 = G.generate_instance(2, 1)
+    r3 = O.solve(Z, x0, y0, dict(OPT, maxiter=5))
+    assert r3.outer_iterations == 5
