@@ -8,6 +8,11 @@ A "step" is one outer RIPTRM iteration of every instance of the batch (RIPTRM.py
 instance are timed between barriers + device syncs; the max over ranks is the time.  The only
 collectives are the timing all_reduce and the final gather of per-instance results.
 
+Window: the defaults (W=1, K=19) time outer iterations 2..20 of every instance, the BASELINE.md
+window (20 outer iterations, mu 0.1 -> 1.4e-8).  Each instance restarts its solve from
+(x0, y0, mu0, Delta0) after every 20 outer iterations (riptrm_options.restart_every), so any
+--warmup/--steps keeps measuring that same workload instead of running into the mu floor.
+
 The JSON line also carries:
 * roofline: the S-pass kernel (k_gemv) timed with HIP events on the stream it runs on, over the
   timed region: algorithmic bytes (8 n^2 + 16 n per instance-pass) / summed kernel time,
@@ -70,14 +75,16 @@ def cpu_baseline(n: int, warmup: int, steps: int, budget_s: float):
             "sample": (f"oracle/riptrm_oracle.py NonnegPCAVectorized, 1 instance n={n} (reference generator "
                        f"recipe, seed {G.SEED0}), outer iterations {warmup + 1}..{last} "
                        f"({done} timed, {el:.1f} s, evaluation time excluded as RIPTRM.py:932-941; "
-                       f"{'complete' if complete else 'budget-truncated'} window), NumPy/OpenBLAS {cores} threads")}
+                       f"{'complete' if complete else 'budget-truncated'} window), NumPy + OpenBLAS dsymv (one triangle of S), {cores} threads")}
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10, help="timed outer iterations per instance")
-    ap.add_argument("--warmup", type=int, default=2, help="untimed outer iterations per instance")
+    ap.add_argument("--steps", type=int, default=19, help="timed outer iterations per instance")
+    ap.add_argument("--warmup", type=int, default=1, help="untimed outer iterations per instance")
+    ap.add_argument("--layout", default="sym", choices=["sym", "full"], help="storage of S = Z + Z^T")
+    ap.add_argument("--cycle", type=int, default=20, help="outer iterations per solve before restart")
     ap.add_argument("--n", type=int, default=4000)
     ap.add_argument("--batch", type=int, default=128, help="instances per GPU")
     ap.add_argument("--cpu-budget", type=float, default=25.0, help="seconds of CPU-baseline sampling (0 = skip)")
@@ -104,14 +111,14 @@ def main():
     from problems import manviofun
 
     n, B, W, K = args.n, args.batch, args.warmup, args.steps
-    eng = engine.NonnegPCABatch(n, B, log_capacity=2048)
+    eng = engine.NonnegPCABatch(n, B, log_capacity=2048, layout=args.layout)
     log(f"rank {rank}/{world}: generating {B} instances n={n} ({B * eng.inst_stride * 8 / 1e9:.1f} GB S)")
     # global instance ids owned by this rank: rank, rank+world, ... (seed seed0 + id)
     gen_ids = [rank + world * i for i in range(B)]
     xg, yg = eng.generate_synthetic(args.seed0, ids=gen_ids)
     opt = {"TRS_solver": "tCG", "second_order_stationarity": False, "maxiter": W + K, "tolresid": 0.0,
            "maxtime": math.inf, "manviofun": manviofun}
-    eng.begin(xg, yg, opt)
+    eng.begin(xg, yg, opt, restart_every=args.cycle)
     torch.cuda.synchronize(dev)
     t0 = time.time()
     eng.run_until(W)
@@ -149,7 +156,10 @@ def main():
     outer_all, passes_all, inner_all, tcg_all, gemv_ms_all, gemv_n_all = [float(v) for v in counts.tolist()]
 
     if rank == 0:
-        bytes_per_pass = 8.0 * n * n + 16.0 * n
+        # algorithmic bytes of one instance-pass: the stored S (sym: upper-triangle tiles incl.
+        # padding, ~4 n^2; full: 8 n^2) + the vectors in/out
+        s_bytes = 8.0 * eng.inst_stride if args.layout == "sym" else 8.0 * n * n
+        bytes_per_pass = s_bytes + 16.0 * n
         # rank-0 kernel timing (every rank runs the same kernel on its own batch)
         gemv_s = prof["gemv_ms"] / 1e3
         passes_r0 = float((st1[:, C["RIPTRM_STAT_PASSES"]] - st0[:, C["RIPTRM_STAT_PASSES"]]).sum())
@@ -167,7 +177,7 @@ def main():
         cpu = None
         if args.cpu_budget > 0 and world == 1:
             log("CPU baseline (oracle) ...")
-            cpu = cpu_baseline(n, W, K, args.cpu_budget)
+            cpu = cpu_baseline(n, W, min(K, max(1, args.cycle - W)), args.cpu_budget)
         out = {
             "metric": METRIC,
             "value": outer_all / T,
@@ -184,11 +194,13 @@ def main():
             "config": {"workload": f"NonnegPCA n={n}, batch of {B} independent instances per GPU "
                                    f"(BASELINE configs[2]; configs[3] at 8 GPUs)",
                        "n": n, "batch_per_gpu": B, "global_batch": B * world,
-                       "outer_window": [W + 1, W + K], "parallelism": f"instance-sharded x{world}"},
+                       "outer_window": [W + 1, W + K], "restart_every": args.cycle, "layout": args.layout,
+                       "parallelism": f"instance-sharded x{world}"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
                          "traffic": traffic,
-                         "kernel": "k_gemv (S-pass)",
+                         "kernel": "k_spass_sym (S-pass, symmetric tiles)" if args.layout == "sym"
+                                   else "k_gemv (S-pass, full matrix)",
                          "bytes_per_launch": passes_r0 * bytes_per_pass / nl,
                          "avg_launch_us": prof["gemv_ms"] * 1e3 / nl},
             "cpu_baseline": cpu,

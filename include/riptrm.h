@@ -67,6 +67,11 @@ extern "C" {
 #define RIPTRM_STOP_MAXITER 2
 #define RIPTRM_STOP_TOLRESID 3
 
+/* storage layouts of S = Z + Z^T (one instance) */
+#define RIPTRM_LAYOUT_FULL 0      /* row-major, riptrm_nonnegpca_rows(n) rows of riptrm_nonnegpca_ld(n) */
+#define RIPTRM_LAYOUT_SYMTILE 1   /* upper triangle as 128x128 row-major tiles (I,J), I <= J, ordered
+                                   * row by row: tile t = I*nt - I*(I-1)/2 + (J-I), nt = ld/128 */
+
 /* manifold-violation kinds for the KKT residual (option 'manviofun') */
 #define RIPTRM_MANVIO_ZERO 0     /* RIPTRM.py:347 default: lambda problem, x: 0 */
 #define RIPTRM_MANVIO_SPHERE 1   /* src/NonnegPCA/simulator.py:12-14: ||x|| - 1 */
@@ -106,7 +111,9 @@ typedef struct riptrm_options {
     int32_t save_inner_iteration;     /* 'save_inner_iteration' (bool) */
     int32_t manvio_kind;              /* RIPTRM_MANVIO_* */
     int32_t log_capacity;             /* log records per instance (<= the bound capacity) */
-    int32_t reserved0;
+    int32_t restart_every;            /* 0 = off; k > 0: after outer iteration k, 2k, ... restart the
+                                       * instance from (x0, y0, mu_0, Delta_0) and keep counting
+                                       * (benchmark windows longer than one solve) */
     double maxtime;                   /* 'maxtime' seconds (INFINITY allowed) */
     double inner_maxtime;             /* 'inner_maxtime' seconds, < 0 = None */
     double tolresid;                  /* 'tolresid' */
@@ -134,26 +141,30 @@ const char* riptrm_last_error(const riptrm_ctx* ctx);
 int riptrm_ctx_set_stream(riptrm_ctx* ctx, void* stream);
 
 /* ---- layout (pure functions, no device work) ---- */
-/* Leading dimension (doubles) of one padded row of S and of every state vector. */
+/* Leading dimension (doubles) of every state vector and of a full-layout row of S
+ * (n rounded up to 128). */
 int64_t riptrm_nonnegpca_ld(int32_t n);
-/* Rows of one padded instance of S (multiple of the mat-vec row block). */
+/* Rows of one full-layout instance of S (multiple of the mat-vec row block). */
 int64_t riptrm_nonnegpca_rows(int32_t n);
-/* Device workspace bytes for a batch (state vectors, scalars, log, counters). */
-int64_t riptrm_workspace_bytes(int32_t n, int32_t batch, int32_t log_capacity);
+/* Doubles of one instance of S in `layout` (the minimum instance stride). */
+int64_t riptrm_nonnegpca_s_elems(int32_t n, int32_t layout);
+/* Device workspace bytes for a batch (state vectors, scalars, log, partial sums, counters). */
+int64_t riptrm_workspace_bytes(int32_t n, int32_t batch, int32_t log_capacity, int32_t layout);
 /* Byte offsets inside the workspace.  kind: 0 = x, 1 = y, 2 = eta (last dx), 3 = Heta,
  * 4 = stats (batch x RIPTRM_STAT_NFIELDS doubles), 5 = log (batch x capacity x NFIELDS). */
-int64_t riptrm_workspace_offset(int32_t n, int32_t batch, int32_t log_capacity, int32_t kind);
+int64_t riptrm_workspace_offset(int32_t n, int32_t batch, int32_t log_capacity, int32_t layout,
+                                int32_t kind);
 
 /* ---- data preparation ---- */
-/* In place: S_b <- Z_b + Z_b^T for b < batch, where each instance is a padded
- * (riptrm_nonnegpca_rows(n) x ld) block starting at S + b*inst_stride holding Z_b in its
- * leading n x n corner; padding rows/columns are zeroed. */
-int riptrm_nonnegpca_symmetrize(riptrm_ctx* ctx, double* S, int32_t n, int32_t batch,
-                                int64_t ld, int64_t inst_stride);
+/* S_b <- pack(Z_b + Z_b^T) for b < count: Z_b is n x n row-major with leading dimension ldz at
+ * Z + b*z_stride, S_b is written at S + b*s_stride in `layout` with zero padding.  Each
+ * element is the one rounding of Z_ij + Z_ji, so S is exactly symmetric. */
+int riptrm_nonnegpca_pack(riptrm_ctx* ctx, const double* Z, int64_t ldz, int64_t z_stride, int32_t n,
+                          int32_t count, double* S, int32_t layout, int64_t s_stride);
 
 /* ---- bind a batch of NonnegPCA instances sharing n (the hydra multi-run axis) ---- */
 int riptrm_nonnegpca_bind(riptrm_ctx* ctx, const double* S, int32_t n, int32_t batch,
-                          int64_t ld, int64_t inst_stride, void* workspace,
+                          int32_t layout, int64_t s_stride, void* workspace,
                           int64_t workspace_bytes, int32_t log_capacity);
 
 /* ---- operator entry points (parity / building blocks) ---- */

@@ -5,6 +5,7 @@
 //   [state]    batch x ST_N doubles               per-instance scalars (see enum St)
 //   [stats]    batch x RIPTRM_STAT_NFIELDS        host-visible results
 //   [log]      batch x cap x RIPTRM_LOG_NFIELDS   per-inner-iteration log rows
+//   [pbuf]     2 x batch x nt x nt x TS doubles   S-pass partial sums (symmetric-tile layout only)
 //   [lists]    2 x batch int32                    active-instance lists (ping-pong)
 //   [req]      batch int32                        right-hand sides wanted per instance (1|2)
 //   [counters] 4 int32                            list lengths (ping-pong) + spare
@@ -14,7 +15,10 @@
 
 namespace riptrm {
 
-// rows of S handled by one mat-vec workgroup (4 waves x GV_RW rows)
+// S layouts (RIPTRM_LAYOUT_*): full row-major, or the upper triangle in TS x TS tiles
+constexpr int TS = 128;            // tile edge of the symmetric-tile layout; vector padding unit
+constexpr int SP_THREADS = 256;    // 4 waves per tile workgroup, 32 rows each
+// rows of S handled by one full-layout mat-vec workgroup (4 waves x GV_RW rows)
 constexpr int GV_THREADS = 256;
 constexpr int GV_RW = 4;
 constexpr int GV_RB = (GV_THREADS / 64) * GV_RW;
@@ -26,6 +30,7 @@ constexpr int ST_WAVES = ST_THREADS / 64;
 enum Vec : int {
   V_X = 0, V_Y, V_ETA, V_HETA,   // 0..3 fixed so riptrm_workspace_offset kinds 0..3 map here
   V_SX, V_X0, V_Y0, V_SX0, V_XPREV, V_R, V_IN0, V_IN1, V_OUT0, V_OUT1, V_YNEW, V_C,
+  V_XI, V_YI, V_SXI,             // initial point (restart_every cycling)
   NVEC
 };
 
@@ -62,23 +67,32 @@ enum Phase : int {
 enum Mode : int { MODE_SOLVE = 0, MODE_TCG_ONLY = 1 };
 
 struct Layout {
-  int32_t n, batch, cap;
+  int32_t n, batch, cap, layout, nt;
   int64_t ld;
-  int64_t off_vec, off_state, off_stats, off_log, off_lists, off_req, off_cnt, total;
+  int64_t off_vec, off_state, off_stats, off_log, off_pbuf, off_lists, off_req, off_cnt, total;
 };
 
 inline int64_t round_up(int64_t a, int64_t m) { return (a + m - 1) / m * m; }
-inline int64_t ld_of(int32_t n) { return round_up(n > 0 ? n : 1, 16); }
-inline int64_t rows_of(int32_t n) { return round_up(n > 0 ? n : 1, GV_RB); }
+inline int64_t ld_of(int32_t n) { return round_up(n > 0 ? n : 1, TS); }
+inline int64_t rows_of(int32_t n) { return round_up(n > 0 ? n : 1, 32); }  // k_pack writes 32-row sub-tiles
+inline int32_t nt_of(int32_t n) { return (int32_t)(ld_of(n) / TS); }
+inline int64_t ntiles_of(int32_t n) { const int64_t t = nt_of(n); return t * (t + 1) / 2; }
+// doubles of one instance of S in a layout
+inline int64_t s_elems_of(int32_t n, int32_t layout) {
+  return layout == RIPTRM_LAYOUT_SYMTILE ? ntiles_of(n) * TS * TS : rows_of(n) * ld_of(n);
+}
 
-inline Layout make_layout(int32_t n, int32_t batch, int32_t cap) {
+inline Layout make_layout(int32_t n, int32_t batch, int32_t cap, int32_t layout) {
   Layout L;
-  L.n = n; L.batch = batch; L.cap = cap; L.ld = ld_of(n);
+  L.n = n; L.batch = batch; L.cap = cap; L.ld = ld_of(n); L.layout = layout; L.nt = nt_of(n);
   int64_t o = 0;
   L.off_vec = o;   o += (int64_t)NVEC * batch * L.ld * 8;               o = round_up(o, 256);
   L.off_state = o; o += (int64_t)batch * ST_N * 8;                       o = round_up(o, 256);
   L.off_stats = o; o += (int64_t)batch * RIPTRM_STAT_NFIELDS * 8;        o = round_up(o, 256);
   L.off_log = o;   o += (int64_t)batch * cap * RIPTRM_LOG_NFIELDS * 8;   o = round_up(o, 256);
+  L.off_pbuf = o;
+  if (layout == RIPTRM_LAYOUT_SYMTILE) o += (int64_t)2 * batch * L.nt * L.nt * TS * 8;
+  o = round_up(o, 256);
   L.off_lists = o; o += (int64_t)2 * batch * 4;                          o = round_up(o, 256);
   L.off_req = o;   o += (int64_t)batch * 4;                              o = round_up(o, 256);
   L.off_cnt = o;   o += 16;                                              o = round_up(o, 256);
@@ -88,11 +102,15 @@ inline Layout make_layout(int32_t n, int32_t batch, int32_t cap) {
 
 // Kernel parameter block (passed by value).
 struct DevParams {
-  const double* S;      // batch x rows x ld
+  const double* S;      // batch instances, inst_stride doubles apart (layout below)
   int64_t inst_stride;  // doubles between instances of S
   int64_t ld;
   int32_t n, batch, cap;
-  int32_t nrb;          // row blocks per instance
+  int32_t nrb;          // row blocks per instance (full layout)
+  int32_t layout;       // RIPTRM_LAYOUT_*
+  int32_t nt;           // tiles per dimension (symmetric-tile layout)
+  int32_t ntiles;       // nt (nt + 1) / 2
+  double* pbuf;         // 2 x batch x nt x nt x TS partial sums (symmetric-tile layout)
   double* vec;          // workspace vectors
   double* st;           // workspace scalars
   double* stats;

@@ -194,25 +194,183 @@ __global__ void __launch_bounds__(GV_THREADS) k_gemv(DevParams P, int list_in, i
 }
 
 // ------------------------------------------------------------------------------------------
-// S = Z + Z^T in place on the padded (Np x Np, Np = ld) layout, zeroing the padding.
-// One workgroup per 16x16 tile pair (I <= J): both tiles staged in LDS, both written.
+// Symmetric-tile S-pass.  S = Z + Z^T is stored as its upper triangle of 128 x 128 tiles; tile
+// (I, J), I <= J, gives y_I += S_IJ v_J ("row part") and, off the diagonal, y_J += S_IJ^T v_I
+// ("column part"), so every S byte is read once per pass for two output blocks: ~half the
+// HBM traffic of the full matrix.  One 4-wave workgroup per tile; lane l owns columns 2l, 2l+1
+// (16 B loads, 1 KiB per wave instruction), each wave 32 rows in four 8-row batches.  Row sums
+// use an 8-row reduce-scatter across the wave (~3.5 lane exchanges per row); column sums
+// accumulate per lane and are combined across the 4 waves through LDS.  Results go to a
+// partial-sum grid P[b][I][J][0..127] (every slot written exactly once per pass) that the
+// state kernel sums in fixed J order: deterministic, no atomics.
 // ------------------------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) k_symmetrize(double* S, int n, int64_t ld, int64_t inst_stride, int nt) {
-  const int I = blockIdx.x / nt, J = blockIdx.x % nt;
-  if (I > J) return;
-  double* Sb = S + (int64_t)blockIdx.y * inst_stride;
-  __shared__ double a[16][17], t[16][17];
-  const int r = threadIdx.x >> 4, c = threadIdx.x & 15;
-  const int i1 = I * 16 + r, j1 = J * 16 + c;  // element of tile (I,J)
-  const int i2 = J * 16 + r, j2 = I * 16 + c;  // element of tile (J,I)
-  a[r][c] = (i1 < n && j1 < n) ? Sb[(int64_t)i1 * ld + j1] : 0.0;
-  t[r][c] = (i2 < n && j2 < n) ? Sb[(int64_t)i2 * ld + j2] : 0.0;
+__device__ __forceinline__ void tile_ij(int t, int nt, int& I, int& J) {
+  int i = 0, rem = t, len = nt;
+  while (rem >= len) { rem -= len; ++i; --len; }
+  I = i;
+  J = i + rem;
+}
+
+// gfx950 half exchanges on one double: swap32 trades lanes 32-63 of a with lanes 0-31 of b,
+// swap16 trades the odd 16-lane rows of a with the even rows of b (v_permlane{32,16}_swap_b32).
+__device__ __forceinline__ void swap32(double& a, double& b) {
+  const auto lo = __builtin_amdgcn_permlane32_swap((unsigned)__double2loint(a), (unsigned)__double2loint(b), false, false);
+  const auto hi = __builtin_amdgcn_permlane32_swap((unsigned)__double2hiint(a), (unsigned)__double2hiint(b), false, false);
+  a = __hiloint2double((int)hi[0], (int)lo[0]);
+  b = __hiloint2double((int)hi[1], (int)lo[1]);
+}
+__device__ __forceinline__ void swap16(double& a, double& b) {
+  const auto lo = __builtin_amdgcn_permlane16_swap((unsigned)__double2loint(a), (unsigned)__double2loint(b), false, false);
+  const auto hi = __builtin_amdgcn_permlane16_swap((unsigned)__double2hiint(a), (unsigned)__double2hiint(b), false, false);
+  a = __hiloint2double((int)hi[0], (int)lo[0]);
+  b = __hiloint2double((int)hi[1], (int)lo[1]);
+}
+
+// Reduce-scatter of 8 per-lane row partials over the 64 lanes: afterwards lane l holds the
+// full sum of row rs_row(l) = 4 b5 + 2 b4 + b3 (b_k = bit k of l); the 8 lanes sharing bits
+// 3-5 agree.  8->4 rows by swap32 and 4->2 by swap16 (no lane selects), 2->1 by a lane
+// exchange with a per-lane choice of the kept half, then a butterfly over bits 0-2.
+__device__ __forceinline__ double reduce_scatter8(double (&a)[8]) {
+  const int lane = (int)__lane_id();
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {  // lanes 0-31 keep rows k, lanes 32-63 rows k+4
+    swap32(a[k], a[k + 4]);
+    a[k] = a[k] + a[k + 4];
+  }
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {  // even 16-lane rows keep k, odd rows k+2
+    swap16(a[k], a[k + 2]);
+    a[k] = a[k] + a[k + 2];
+  }
+  const double r0 = a[0], r1 = a[1];
+  const bool b3 = (lane & 8) != 0;
+  const double snd = b3 ? r0 : r1, kp = b3 ? r1 : r0;
+  double v = kp + xor_lane(snd, 8);
+  v += xor_lane(v, 4);
+  v += xor_lane(v, 2);
+  v += xor_lane(v, 1);
+  return v;
+}
+
+template <int NR>
+__device__ __forceinline__ void spass_tile(const DevParams& P, int b, int t) {
+  int I, J;
+  tile_ij(t, P.nt, I, J);
+  const int lane = (int)__lane_id();
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const double* __restrict__ T = P.S + (int64_t)b * P.inst_stride + (int64_t)t * TS * TS;
+  const double* __restrict__ v0 = vp(P, V_IN0, b);
+  const double* __restrict__ v1 = vp(P, V_IN1, b);
+  const dbl2 vj0 = *(const dbl2*)(v0 + J * TS + 2 * lane);
+  dbl2 vj1 = dbl2{0.0, 0.0};
+  if (NR == 2) vj1 = *(const dbl2*)(v1 + J * TS + 2 * lane);
+  const int64_t nn = (int64_t)P.nt * P.nt * TS;
+  double* __restrict__ pb0 = P.pbuf + (int64_t)b * nn;
+  double* __restrict__ pb1 = P.pbuf + ((int64_t)P.batch + b) * nn;
+  double c0x = 0.0, c0y = 0.0, c1x = 0.0, c1y = 0.0;
+  const int rrow = 4 * ((lane >> 5) & 1) + 2 * ((lane >> 4) & 1) + ((lane >> 3) & 1);
+#pragma unroll 1
+  for (int rb = 0; rb < 4; ++rb) {
+    const int r0 = w * 32 + rb * 8;
+    dbl2 sv[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) sv[k] = __builtin_nontemporal_load((const dbl2*)(T + (r0 + k) * TS + 2 * lane));
+    double a[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const double vi0 = v0[I * TS + r0 + k];
+      a[k] = __builtin_fma(sv[k].y, vj0.y, sv[k].x * vj0.x);
+      c0x = __builtin_fma(sv[k].x, vi0, c0x);
+      c0y = __builtin_fma(sv[k].y, vi0, c0y);
+    }
+    const double s0 = reduce_scatter8(a);
+    if ((lane & 7) == 0) pb0[((int64_t)I * P.nt + J) * TS + r0 + rrow] = s0;
+    if (NR == 2) {  // second right-hand side reuses the loaded tile rows
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const double vi1 = v1[I * TS + r0 + k];
+        a[k] = __builtin_fma(sv[k].y, vj1.y, sv[k].x * vj1.x);
+        c1x = __builtin_fma(sv[k].x, vi1, c1x);
+        c1y = __builtin_fma(sv[k].y, vi1, c1y);
+      }
+      const double s1 = reduce_scatter8(a);
+      if ((lane & 7) == 0) pb1[((int64_t)I * P.nt + J) * TS + r0 + rrow] = s1;
+    }
+  }
+  if (I != J) {
+    __shared__ double cs[2][4][TS];
+    cs[0][w][2 * lane] = c0x;
+    cs[0][w][2 * lane + 1] = c0y;
+    if (NR == 2) {
+      cs[1][w][2 * lane] = c1x;
+      cs[1][w][2 * lane + 1] = c1y;
+    }
+    __syncthreads();
+    if (threadIdx.x < TS) {
+      const int c = threadIdx.x;
+      pb0[((int64_t)J * P.nt + I) * TS + c] = ((cs[0][0][c] + cs[0][1][c]) + cs[0][2][c]) + cs[0][3][c];
+      if (NR == 2)
+        pb1[((int64_t)J * P.nt + I) * TS + c] = ((cs[1][0][c] + cs[1][1][c]) + cs[1][2][c]) + cs[1][3][c];
+    }
+  }
+}
+
+__global__ void __launch_bounds__(SP_THREADS, 4) k_spass_sym(DevParams P, int list_in, int zero_cnt) {
+  if (zero_cnt >= 0 && blockIdx.x == 0 && threadIdx.x == 0) P.cnt[zero_cnt] = 0;
+  const int nact = P.cnt[list_in];
+  const int slot = blockIdx.x / P.ntiles;
+  if (slot >= nact) return;
+  const int b = P.lists[list_in * P.batch + slot];
+  const int t = blockIdx.x - slot * P.ntiles;
+  if (P.req[b] == 2) spass_tile<2>(P, b, t);
+  else spass_tile<1>(P, b, t);
+}
+
+// ------------------------------------------------------------------------------------------
+// Packing: S = Z + Z^T from a row-major Z (leading dimension ldz) into either layout, zero
+// padded.  32x32 sub-tiles staged through LDS so both Z and Z^T are read coalesced; each
+// element is the single rounding of Z_ij + Z_ji (so S_ij == S_ji bit for bit).
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ void pack_sub32(const double* __restrict__ Zb, int64_t ldz, int n, int i0, int j0,
+                                           double* __restrict__ dst, int64_t dst_ld) {
+  __shared__ double a[32][33], bt[32][33];
+  const int c = threadIdx.x & 31, r8 = threadIdx.x >> 5;  // 256 threads: 32 x 8
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int r = r8 + 8 * k;
+    const int i = i0 + r, j = j0 + c;
+    a[r][c] = (i < n && j < n) ? Zb[(int64_t)i * ldz + j] : 0.0;
+    const int i2 = j0 + r, j2 = i0 + c;               // Z block (J, I)
+    bt[r][c] = (i2 < n && j2 < n) ? Zb[(int64_t)i2 * ldz + j2] : 0.0;
+  }
   __syncthreads();
-  // S_ij = Z_ij + Z_ji for (i,j) in tile (I,J); S_ji is the same double.
-  const double sij = a[r][c] + t[c][r];
-  const double sji = t[r][c] + a[c][r];
-  Sb[(int64_t)i1 * ld + j1] = (i1 < n && j1 < n) ? sij : 0.0;
-  if (I != J) Sb[(int64_t)i2 * ld + j2] = (i2 < n && j2 < n) ? sji : 0.0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int r = r8 + 8 * k;
+    const int i = i0 + r, j = j0 + c;
+    dst[(int64_t)r * dst_ld + c] = (i < n && j < n) ? a[r][c] + bt[c][r] : 0.0;
+  }
+  __syncthreads();
+}
+
+// grid.x = sub-tiles of the padded square, grid.y = instance
+__global__ void __launch_bounds__(256) k_pack(const double* Z, int64_t ldz, int64_t zs, int n, double* S,
+                                              int64_t ss, int layout, int64_t ld, int64_t rows) {
+  const double* Zb = Z + (int64_t)blockIdx.y * zs;
+  double* Sb = S + (int64_t)blockIdx.y * ss;
+  const int nsub = (int)(ld / 32);
+  const int si = blockIdx.x / nsub, sj = blockIdx.x % nsub;
+  const int i0 = si * 32, j0 = sj * 32;
+  if (layout == RIPTRM_LAYOUT_FULL) {
+    if (i0 >= rows) return;
+    pack_sub32(Zb, ldz, n, i0, j0, Sb + (int64_t)i0 * ld + j0, ld);
+  } else {
+    const int I = i0 / TS, J = j0 / TS;
+    if (I > J) return;
+    const int nt = (int)(ld / TS);
+    const int64_t t = (int64_t)I * nt - (int64_t)I * (I - 1) / 2 + (J - I);
+    pack_sub32(Zb, ldz, n, i0, j0, Sb + t * TS * TS + (int64_t)(i0 - I * TS) * TS + (j0 - J * TS), TS);
+  }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -263,6 +421,31 @@ struct Machine {
     double* d = V(dst);
     const double* a = V(src);
     for (int i = tid; i < n; i += ST_THREADS) d[i] = a[i];
+  }
+
+  // OUT_k = sum_J P_k[b][I][J] for the symmetric-tile layout, J in fixed order
+  __device__ __forceinline__ void gather_out(int nr) {
+    const int nt = P.nt;
+    const int64_t nn = (int64_t)nt * nt * TS;
+    for (int k = 0; k < nr; ++k) {
+      const double* pb = P.pbuf + ((int64_t)k * P.batch + b) * nn;
+      double* O = V(k == 0 ? V_OUT0 : V_OUT1);
+      for (int i = tid; i < n; i += ST_THREADS) {
+        const int I = i / TS, c = i - I * TS;
+        const double* q = pb + (int64_t)I * nt * TS + c;
+        double acc = q[0];
+        int J = 1;
+        for (; J + 8 <= nt; J += 8) {
+          double t[8];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) t[u] = q[(int64_t)(J + u) * TS];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) acc += t[u];
+        }
+        for (; J < nt; ++J) acc += q[(int64_t)J * TS];
+        O[i] = acc;
+      }
+    }
   }
 
   __device__ __forceinline__ int request(int nrhs) {
@@ -451,8 +634,22 @@ struct Machine {
     return start_outer_step();
   }
 
+  // restart_every cycling (benchmark windows only): back to (x0, y0, mu_0, Delta_0)
+  __device__ __forceinline__ void maybe_restart() {
+    const int k = P.opt.restart_every;
+    if (k > 0 && s[ST_OUTER_IT] > 0.0 && fmod(s[ST_OUTER_IT], (double)k) == 0.0) {
+      copy(V_X, V_XI);
+      copy(V_Y, V_YI);
+      copy(V_SX, V_SXI);
+      s[ST_MU_IDX] = 0.0;
+      s[ST_MU] = mu_at(0);
+      s[ST_DELTA] = P.opt.initial_tr_radius;
+    }
+  }
+
   // RIPTRM.py:866-887 + inner_run :785-799
   __device__ __forceinline__ int start_outer_step() {
+    maybe_restart();
     s[ST_OUTER_IT] += 1.0;
     const int mi = (int)s[ST_MU_IDX];
     const int ti = mi < P.tab_len ? mi : P.tab_len - 1;
@@ -850,6 +1047,9 @@ struct Machine {
         copy(V_SX, V_OUT0);
         s[ST_T_START] = unow();
         copy(V_X0, V_X);
+        copy(V_XI, V_X);
+        copy(V_YI, V_Y);
+        copy(V_SXI, V_SX);
         return outer_top();
       case PH_TCG:
         return tcg_step();
@@ -890,6 +1090,7 @@ __global__ void __launch_bounds__(ST_THREADS) k_state(DevParams P, int full, int
   Machine M(P, b, list_out, redbuf);
   const int ph = (int)M.s[ST_PHASE];
   if (ph == PH_DONE || ph == PH_IDLE || ph == PH_ERROR) return;
+  if (!full && P.layout == RIPTRM_LAYOUT_SYMTILE) M.gather_out(P.req[b]);
   M.dispatch();
   M.finish_write();
 }
@@ -946,6 +1147,7 @@ __global__ void __launch_bounds__(ST_THREADS) k_hvp_epi(DevParams P, double mu, 
   __shared__ double redbuf[2 * ST_WAVES * RED_MAX];
   const int b = blockIdx.x;
   Machine M(P, b, 0, redbuf);
+  if (P.layout == RIPTRM_LAYOUT_SYMTILE) M.gather_out(2);
   const double* X = M.V(V_X);
   const double* Y = M.V(V_Y);
   const double* SX = M.V(V_OUT1);
@@ -1070,15 +1272,20 @@ int riptrm_ctx_set_stream(riptrm_ctx* ctx, void* stream) {
 
 double riptrm_device_clock_hz(riptrm_ctx* ctx) { return ctx ? ctx->clock_hz : 0.0; }
 
-int64_t riptrm_nonnegpca_ld(int32_t n) { return ld_of(n); }
-int64_t riptrm_nonnegpca_rows(int32_t n) { return rows_of(n); }
-int64_t riptrm_workspace_bytes(int32_t n, int32_t batch, int32_t cap) {
-  if (n <= 0 || batch <= 0 || cap < 0) return -1;
-  return make_layout(n, batch, cap).total;
+static bool layout_ok(int32_t layout) { return layout == RIPTRM_LAYOUT_FULL || layout == RIPTRM_LAYOUT_SYMTILE; }
+
+int64_t riptrm_nonnegpca_ld(int32_t n) { return n > 0 ? ld_of(n) : -1; }
+int64_t riptrm_nonnegpca_rows(int32_t n) { return n > 0 ? rows_of(n) : -1; }
+int64_t riptrm_nonnegpca_s_elems(int32_t n, int32_t layout) {
+  return (n > 0 && layout_ok(layout)) ? s_elems_of(n, layout) : -1;
 }
-int64_t riptrm_workspace_offset(int32_t n, int32_t batch, int32_t cap, int32_t kind) {
-  if (n <= 0 || batch <= 0 || cap < 0) return -1;
-  const Layout L = make_layout(n, batch, cap);
+int64_t riptrm_workspace_bytes(int32_t n, int32_t batch, int32_t cap, int32_t layout) {
+  if (n <= 0 || batch <= 0 || cap < 0 || !layout_ok(layout)) return -1;
+  return make_layout(n, batch, cap, layout).total;
+}
+int64_t riptrm_workspace_offset(int32_t n, int32_t batch, int32_t cap, int32_t layout, int32_t kind) {
+  if (n <= 0 || batch <= 0 || cap < 0 || !layout_ok(layout)) return -1;
+  const Layout L = make_layout(n, batch, cap, layout);
   switch (kind) {
     case 0: case 1: case 2: case 3:
       return L.off_vec + (int64_t)kind * batch * L.ld * 8;
@@ -1088,28 +1295,33 @@ int64_t riptrm_workspace_offset(int32_t n, int32_t batch, int32_t cap, int32_t k
   }
 }
 
-int riptrm_nonnegpca_symmetrize(riptrm_ctx* ctx, double* S, int32_t n, int32_t batch, int64_t ld, int64_t inst_stride) {
-  if (!ctx || !S || n <= 0 || batch <= 0) return fail(ctx, RIPTRM_E_ARG, "symmetrize: bad argument");
-  if (ld != ld_of(n) || inst_stride < rows_of(n) * ld)
-    return fail(ctx, RIPTRM_E_ARG, "symmetrize: S must use riptrm_nonnegpca_ld/rows layout");
+int riptrm_nonnegpca_pack(riptrm_ctx* ctx, const double* Z, int64_t ldz, int64_t z_stride, int32_t n, int32_t count,
+                          double* S, int32_t layout, int64_t s_stride) {
+  if (!ctx) return RIPTRM_E_ARG;
+  if (!Z || !S || n <= 0 || count <= 0 || ldz < n || !layout_ok(layout))
+    return fail(ctx, RIPTRM_E_ARG, "pack: bad argument");
+  if (count > 1 && (z_stride < (int64_t)n * ldz || s_stride < s_elems_of(n, layout)))
+    return fail(ctx, RIPTRM_E_ARG, "pack: instance strides too small");
   HIPCHK(ctx, hipSetDevice(ctx->device));
-  const int nt = (int)(ld / 16);
-  dim3 grid((unsigned)(nt * nt), (unsigned)batch);
-  hipLaunchKernelGGL(k_symmetrize, grid, dim3(256), 0, ctx->stream, S, n, ld, inst_stride, nt);
+  const int64_t ld = ld_of(n);
+  const int64_t nsub = ld / 32;
+  dim3 grid((unsigned)(nsub * nsub), (unsigned)count);
+  hipLaunchKernelGGL(k_pack, grid, dim3(256), 0, ctx->stream, Z, ldz, z_stride, n, S, s_stride, layout, ld,
+                     rows_of(n));
   HIPCHK(ctx, hipGetLastError());
   return RIPTRM_OK;
 }
 
-int riptrm_nonnegpca_bind(riptrm_ctx* ctx, const double* S, int32_t n, int32_t batch, int64_t ld, int64_t inst_stride,
-                          void* workspace, int64_t workspace_bytes, int32_t cap) {
+int riptrm_nonnegpca_bind(riptrm_ctx* ctx, const double* S, int32_t n, int32_t batch, int32_t layout,
+                          int64_t inst_stride, void* workspace, int64_t workspace_bytes, int32_t cap) {
   if (!ctx) return RIPTRM_E_ARG;
-  if (!S || !workspace || n < 2 || batch <= 0 || cap < 0)
-    return fail(ctx, RIPTRM_E_ARG, "bind: bad argument (need n >= 2, batch >= 1)");
-  if (ld != ld_of(n) || inst_stride < rows_of(n) * ld || (inst_stride % 2) != 0)
-    return fail(ctx, RIPTRM_E_ARG, "bind: S must use riptrm_nonnegpca_ld/rows layout");
+  if (!S || !workspace || n < 2 || batch <= 0 || cap < 0 || !layout_ok(layout))
+    return fail(ctx, RIPTRM_E_ARG, "bind: bad argument (need n >= 2, batch >= 1, a known layout)");
+  if (inst_stride < s_elems_of(n, layout) || (inst_stride % 2) != 0)
+    return fail(ctx, RIPTRM_E_ARG, "bind: instance stride smaller than riptrm_nonnegpca_s_elems (or odd)");
   if (((uintptr_t)S % 16) != 0 || ((uintptr_t)workspace % 256) != 0)
     return fail(ctx, RIPTRM_E_ARG, "bind: S must be 16-byte and workspace 256-byte aligned");
-  const Layout L = make_layout(n, batch, cap);
+  const Layout L = make_layout(n, batch, cap, layout);
   if (workspace_bytes < L.total) return fail(ctx, RIPTRM_E_ARG, "bind: workspace too small");
   HIPCHK(ctx, hipSetDevice(ctx->device));
   HIPCHK(ctx, hipMemsetAsync(workspace, 0, (size_t)L.total, ctx->stream));
@@ -1126,6 +1338,10 @@ int riptrm_nonnegpca_bind(riptrm_ctx* ctx, const double* S, int32_t n, int32_t b
   P.batch = batch;
   P.cap = cap;
   P.nrb = (int)(rows_of(n) / GV_RB);
+  P.layout = layout;
+  P.nt = L.nt;
+  P.ntiles = (int)ntiles_of(n);
+  P.pbuf = (double*)(ctx->ws + L.off_pbuf);
   P.vec = (double*)(ctx->ws + L.off_vec);
   P.st = (double*)(ctx->ws + L.off_state);
   P.stats = (double*)(ctx->ws + L.off_stats);
@@ -1142,11 +1358,15 @@ int riptrm_nonnegpca_bind(riptrm_ctx* ctx, const double* S, int32_t n, int32_t b
 
 static int launch_gemv(riptrm_ctx* c, int list_in, int zero_cnt, int bound) {
   if (bound <= 0) return RIPTRM_OK;
-  const int64_t blocks = (int64_t)bound * c->P.nrb;
+  const bool sym = c->P.layout == RIPTRM_LAYOUT_SYMTILE;
+  const int64_t blocks = (int64_t)bound * (sym ? c->P.ntiles : c->P.nrb);
   int i0 = -1, i1 = -1;
   hipEvent_t e0 = nullptr, e1 = nullptr;
   if (c->prof && (e0 = prof_event(c, &i0)) && (e1 = prof_event(c, &i1))) HIPCHK(c, hipEventRecord(e0, c->stream));
-  hipLaunchKernelGGL(k_gemv, dim3((unsigned)blocks), dim3(GV_THREADS), 0, c->stream, c->P, list_in, zero_cnt);
+  if (sym)
+    hipLaunchKernelGGL(k_spass_sym, dim3((unsigned)blocks), dim3(SP_THREADS), 0, c->stream, c->P, list_in, zero_cnt);
+  else
+    hipLaunchKernelGGL(k_gemv, dim3((unsigned)blocks), dim3(GV_THREADS), 0, c->stream, c->P, list_in, zero_cnt);
   HIPCHK(c, hipGetLastError());
   if (c->prof && e1) {
     HIPCHK(c, hipEventRecord(e1, c->stream));

@@ -3,8 +3,10 @@
 PyTorch owns the device memory (S, workspace, tables) and the stream; every operation on the
 hot path is a HIP kernel in ``libriptrm_hip.so``.  Layout in HBM:
 
-* ``S``   (batch, rows, ld) fp64, ``S_b = Z_b + Z_b^T`` row-major, rows/ld padded to 16 with
-  zeros; 8 n^2 bytes per instance (128 MB at n = 4000, 16.4 GB for 128 instances).
+* ``S``   one flat fp64 buffer, ``S_b = Z_b + Z_b^T`` per instance in one of two layouts:
+  ``"sym"`` (default) = the upper triangle as 128 x 128 tiles, ~4 n^2 bytes per instance
+  (69 MB at n = 4000, 8.9 GB for 128 instances); ``"full"`` = row-major n x n padded to 128
+  columns, 8 n^2 bytes (131 MB at n = 4000).
 * workspace: 16 state vectors per instance (batch, ld) fp64, per-instance scalars, stats and the
   per-inner-iteration log rows, active lists.
 
@@ -110,7 +112,8 @@ class ResolvedOptions:
     tolC_tab: List[float]
 
 
-def resolve_options(option: Dict[str, Any], typical_dist: float, log_capacity: int) -> ResolvedOptions:
+def resolve_options(option: Dict[str, Any], typical_dist: float, log_capacity: int,
+                    restart_every: int = 0) -> ResolvedOptions:
     o = dict(REFERENCE_DEFAULTS)
     o.update(option or {})
     if o['TRS_solver'] != 'tCG':
@@ -135,6 +138,7 @@ def resolve_options(option: Dict[str, Any], typical_dist: float, log_capacity: i
     c.save_inner_iteration = 1 if o['save_inner_iteration'] else 0
     c.manvio_kind = manvio_kind(o['manviofun'])
     c.log_capacity = int(log_capacity)
+    c.restart_every = int(restart_every)
     c.maxtime = float(o['maxtime']) if o['maxtime'] is not None else math.inf
     c.inner_maxtime = -1.0 if o['inner_maxtime'] is None else float(o['inner_maxtime'])
     c.tolresid = float(o['tolresid'])
@@ -155,10 +159,14 @@ def _stream_handle(device: torch.device) -> int:
     return torch.cuda.current_stream(device).cuda_stream
 
 
+LAYOUTS = {"full": C["RIPTRM_LAYOUT_FULL"], "sym": C["RIPTRM_LAYOUT_SYMTILE"]}
+
+
 class NonnegPCABatch:
     """A batch of NonnegPCA instances with a common n, resident on one GPU."""
 
-    def __init__(self, n: int, batch: int, device: Optional[int] = None, log_capacity: int = 4096):
+    def __init__(self, n: int, batch: int, device: Optional[int] = None, log_capacity: int = 4096,
+                 layout: str = "sym"):
         if not torch.cuda.is_available():
             raise RuntimeError("NonnegPCABatch needs a ROCm GPU (gfx950); there is no CPU fallback")
         if n < 2 or batch < 1:
@@ -166,12 +174,16 @@ class NonnegPCABatch:
         self.lib = N.load()
         self.device = torch.device("cuda", torch.cuda.current_device() if device is None else device)
         self.n, self.batch, self.cap = int(n), int(batch), int(log_capacity)
+        if layout not in LAYOUTS:
+            raise ValueError(f"layout must be one of {sorted(LAYOUTS)}")
+        self.layout_name = layout
+        self.layout = LAYOUTS[layout]
         self.ld = int(self.lib.riptrm_nonnegpca_ld(self.n))
         self.rows = int(self.lib.riptrm_nonnegpca_rows(self.n))
-        self.inst_stride = self.rows * self.ld
+        self.inst_stride = int(self.lib.riptrm_nonnegpca_s_elems(self.n, self.layout))
         self.ctx = N.Context(self.device.index, _stream_handle(self.device))
-        self.S = torch.zeros((self.batch, self.rows, self.ld), dtype=torch.float64, device=self.device)
-        nbytes = int(self.lib.riptrm_workspace_bytes(self.n, self.batch, self.cap))
+        self.S = torch.zeros((self.batch, self.inst_stride), dtype=torch.float64, device=self.device)
+        nbytes = int(self.lib.riptrm_workspace_bytes(self.n, self.batch, self.cap, self.layout))
         self.ws = torch.zeros(nbytes + 256, dtype=torch.uint8, device=self.device)
         base = self.ws.data_ptr()
         self._ws_pad = (-base) % 256
@@ -182,7 +194,7 @@ class NonnegPCABatch:
 
     # ---- views into the workspace -------------------------------------------------------
     def _view(self, kind: int, shape, dtype=torch.float64):
-        off = int(self.lib.riptrm_workspace_offset(self.n, self.batch, self.cap, kind))
+        off = int(self.lib.riptrm_workspace_offset(self.n, self.batch, self.cap, self.layout, kind))
         count = int(np.prod(shape))
         start = self._ws_pad + off
         return self.ws[start:start + count * 8].view(dtype).view(*shape)
@@ -203,28 +215,48 @@ class NonnegPCABatch:
         self.ctx.set_stream(_stream_handle(self.device))
 
     def load_Z(self, Z) -> "NonnegPCABatch":
-        """Z: (batch, n, n) fp64 (numpy or torch).  S_b = Z_b + Z_b^T on the device."""
+        """Z: (batch, n, n) fp64 (numpy or torch).  S_b = Z_b + Z_b^T packed on the device."""
         Zt = torch.as_tensor(Z, dtype=torch.float64)
         if Zt.shape != (self.batch, self.n, self.n):
             raise ValueError(f"Z must be {(self.batch, self.n, self.n)}, got {tuple(Zt.shape)}")
-        self.S.zero_()
+        tmp = torch.empty((self.n, self.n), dtype=torch.float64, device=self.device)
         for b in range(self.batch):
-            self.S[b, :self.n, :self.n].copy_(Zt[b].to(self.device, non_blocking=True))
-        return self.symmetrize()
-
-    def symmetrize(self) -> "NonnegPCABatch":
-        """In place S <- S + S^T on the device (the buffer holds Z in its leading n x n corner)."""
-        self._sync_stream()
-        self.ctx.check(self.lib.riptrm_nonnegpca_symmetrize(self.ctx.h, ctypes.c_void_p(self.S.data_ptr()),
-                                                            self.n, self.batch, self.ld, self.inst_stride),
-                       "riptrm_nonnegpca_symmetrize")
+            tmp.copy_(Zt[b])
+            self.pack_one(tmp, b)
+        torch.cuda.synchronize(self.device)
         self.bind()
         return self
+
+    def pack_one(self, Zdev: torch.Tensor, slot: int):
+        """S[slot] <- pack(Z + Z^T) from a contiguous (n, n) device tensor (riptrm_nonnegpca_pack)."""
+        assert Zdev.is_contiguous() and Zdev.shape == (self.n, self.n) and Zdev.device == self.device
+        self._sync_stream()
+        self.ctx.check(self.lib.riptrm_nonnegpca_pack(self.ctx.h, ctypes.c_void_p(Zdev.data_ptr()), self.n,
+                                                      self.n * self.n, self.n, 1,
+                                                      ctypes.c_void_p(self.S[slot].data_ptr()), self.layout,
+                                                      self.inst_stride), "riptrm_nonnegpca_pack")
+
+    def unpack(self, slot: int) -> np.ndarray:
+        """Host copy of S[slot] as a dense n x n matrix (tests / inspection)."""
+        raw = self.S[slot].cpu().numpy()
+        n, ld = self.n, self.ld
+        if self.layout == LAYOUTS["full"]:
+            return raw[: self.rows * ld].reshape(self.rows, ld)[:n, :n].copy()
+        ts, nt = 128, ld // 128
+        full = np.zeros((ld, ld))
+        t = 0
+        for I in range(nt):
+            for J in range(I, nt):
+                blk = raw[t * ts * ts:(t + 1) * ts * ts].reshape(ts, ts)
+                full[I * ts:(I + 1) * ts, J * ts:(J + 1) * ts] = blk
+                full[J * ts:(J + 1) * ts, I * ts:(I + 1) * ts] = blk.T
+                t += 1
+        return full[:n, :n].copy()
 
     def bind(self):
         self._sync_stream()
         self.ctx.check(self.lib.riptrm_nonnegpca_bind(self.ctx.h, ctypes.c_void_p(self.S.data_ptr()), self.n,
-                                                      self.batch, self.ld, self.inst_stride,
+                                                      self.batch, self.layout, self.inst_stride,
                                                       ctypes.c_void_p(self.ws_ptr), self.ws_bytes, self.cap),
                        "riptrm_nonnegpca_bind")
         self.bound = True
@@ -242,24 +274,25 @@ class NonnegPCABatch:
         k = int(np.floor(delta * n))
         x0 = torch.empty((self.batch, n), dtype=torch.float64, device=self.device)
         y0 = torch.ones((self.batch, n), dtype=torch.float64, device=self.device)
-        self.S.zero_()
         ids = list(range(self.batch)) if ids is None else list(ids)
         if len(ids) != self.batch:
             raise ValueError("ids must have one entry per batch slot")
+        Zb = torch.empty((n, n), dtype=torch.float64, device=self.device)
         for b in range(self.batch):
             g = torch.Generator(device=self.device)
             g.manual_seed(int(seed0) + int(ids[b]))
             idx = torch.randperm(n, generator=g, device=self.device)[:k]
             v = torch.zeros(n, dtype=torch.float64, device=self.device)
             v[idx] = 1.0 / math.sqrt(k)
-            Zb = self.S[b, :n, :n]
             Zb.normal_(0.0, 1.0, generator=g).div_(math.sqrt(n))
             dg = torch.randn(n, dtype=torch.float64, device=self.device, generator=g) * 2 / math.sqrt(n)
             Zb.diagonal().copy_(dg)
             Zb.add_(math.sqrt(snr) * torch.outer(v, v))
             u = torch.rand(n, dtype=torch.float64, device=self.device, generator=g)
             x0[b] = (u / torch.linalg.vector_norm(u)).abs()
-        self.symmetrize()
+            self.pack_one(Zb, b)
+        torch.cuda.synchronize(self.device)
+        self.bind()
         return x0, y0
 
     # ---- operators ----------------------------------------------------------------------
@@ -306,9 +339,9 @@ class NonnegPCABatch:
         return eta, heta, np.array(list(it)), [TCG_NAMES[s] for s in st]
 
     # ---- full solve ---------------------------------------------------------------------
-    def begin(self, x0, y0, option: Dict[str, Any]) -> ResolvedOptions:
+    def begin(self, x0, y0, option: Dict[str, Any], restart_every: int = 0) -> ResolvedOptions:
         assert self.bound
-        ro = resolve_options(option, math.pi, self.cap)
+        ro = resolve_options(option, math.pi, self.cap, restart_every)
         X, Y = self._padded(x0), self._padded(y0)
         tabs = [torch.tensor(t, dtype=torch.float64, device=self.device) for t in (ro.mu_tab, ro.tolL_tab, ro.tolC_tab)]
         self._keep = [X, Y] + tabs

@@ -28,7 +28,7 @@ class RiptrmOptions(ctypes.Structure):
     _fields_ = [
         ("struct_size", c_int32), ("maxiter", c_int32), ("inner_maxiter", c_int32),
         ("tcg_mininner", c_int32), ("save_inner_iteration", c_int32), ("manvio_kind", c_int32),
-        ("log_capacity", c_int32), ("reserved0", c_int32),
+        ("log_capacity", c_int32), ("restart_every", c_int32),
         ("maxtime", c_double), ("inner_maxtime", c_double), ("tolresid", c_double),
         ("initial_tr_radius", c_double), ("minimal_initial_tr_radius", c_double),
         ("maximal_tr_radius", c_double), ("rho", c_double), ("reduction_regularization", c_double),
@@ -46,10 +46,12 @@ SIGNATURES: Dict[str, tuple] = {
     "riptrm_ctx_set_stream": (c_int32, [c_void_p, c_void_p]),
     "riptrm_nonnegpca_ld": (c_int64, [c_int32]),
     "riptrm_nonnegpca_rows": (c_int64, [c_int32]),
-    "riptrm_workspace_bytes": (c_int64, [c_int32, c_int32, c_int32]),
-    "riptrm_workspace_offset": (c_int64, [c_int32, c_int32, c_int32, c_int32]),
-    "riptrm_nonnegpca_symmetrize": (c_int32, [c_void_p, c_void_p, c_int32, c_int32, c_int64, c_int64]),
-    "riptrm_nonnegpca_bind": (c_int32, [c_void_p, c_void_p, c_int32, c_int32, c_int64, c_int64,
+    "riptrm_nonnegpca_s_elems": (c_int64, [c_int32, c_int32]),
+    "riptrm_workspace_bytes": (c_int64, [c_int32, c_int32, c_int32, c_int32]),
+    "riptrm_workspace_offset": (c_int64, [c_int32, c_int32, c_int32, c_int32, c_int32]),
+    "riptrm_nonnegpca_pack": (c_int32, [c_void_p, c_void_p, c_int64, c_int64, c_int32, c_int32, c_void_p,
+                                        c_int32, c_int64]),
+    "riptrm_nonnegpca_bind": (c_int32, [c_void_p, c_void_p, c_int32, c_int32, c_int32, c_int64,
                                         c_void_p, c_int64, c_int32]),
     "riptrm_nonnegpca_hvp": (c_int32, [c_void_p, c_void_p, c_void_p, c_double, c_void_p, c_void_p, c_int64]),
     "riptrm_tcg": (c_int32, [c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p, P_int32, P_int32, c_int32]),

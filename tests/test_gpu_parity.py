@@ -20,12 +20,12 @@ from oracle import riptrm_oracle as O
 OPT = dict(tolresid=0.0, maxtime=1e9)
 
 
-def _engine(Z, cap=4096):
+def _engine(Z, cap=4096, layout="sym"):
     import engine
     Z = np.asarray(Z)
     if Z.ndim == 2:
         Z = Z[None]
-    eng = engine.NonnegPCABatch(Z.shape[1], Z.shape[0], log_capacity=cap)
+    eng = engine.NonnegPCABatch(Z.shape[1], Z.shape[0], log_capacity=cap, layout=layout)
     eng.load_Z(Z)
     return eng
 
@@ -52,25 +52,31 @@ def _state(n, seed):
     return x, y
 
 
-@pytest.mark.parametrize("n", [2, 17, 50, 333, 1000])
-def test_symmetrize_and_spass(n):
+@pytest.mark.parametrize("layout", ["sym", "full"])
+@pytest.mark.parametrize("n", [2, 17, 40, 50, 129, 333, 1000])
+def test_pack_is_exact_symmetrization(n, layout):
     Z, _, _ = G.generate_instance(n, 3)
-    eng = _engine(np.stack([Z, Z.T * 0.5]))
-    S = eng.S[:, :n, :n].cpu().numpy()
-    np.testing.assert_array_equal(S[0], Z + Z.T)          # exact: one add per element
-    np.testing.assert_array_equal(S[0], S[0].T)
-    assert float(eng.S[:, n:, :].abs().sum()) == 0 and float(eng.S[:, :, n:].abs().sum()) == 0
+    Z2 = Z.T * 0.5
+    eng = _engine(np.stack([Z, Z2]), layout=layout)
+    np.testing.assert_array_equal(eng.unpack(0), Z + Z.T)          # exact: one add per element
+    np.testing.assert_array_equal(eng.unpack(1), Z2 + Z2.T)
+    S = eng.S.cpu().numpy()
+    assert np.isfinite(S).all()
+    if layout == "full":   # padding is zero
+        full = S[0][: eng.rows * eng.ld].reshape(eng.rows, eng.ld)
+        assert not full[n:, :].any() and not full[:, n:].any()
 
 
-@pytest.mark.parametrize("n,B", [(17, 3), (50, 2), (1000, 3), (4000, 2)])
-def test_barrier_hessian_matches_oracle(n, B):
+@pytest.mark.parametrize("layout", ["sym", "full"])
+@pytest.mark.parametrize("n,B", [(17, 3), (50, 2), (200, 2), (1000, 3), (4000, 2)])
+def test_barrier_hessian_matches_oracle(n, B, layout):
     Zs, xs, ys, vs = [], [], [], []
     for b in range(B):
         Z, _, _ = G.generate_instance(n, 10 + b)
         x, y = _state(n, 20 + b)
         Zs.append(Z); xs.append(x); ys.append(y)
         vs.append(np.random.RandomState(30 + b).randn(n))
-    eng = _engine(np.stack(Zs))
+    eng = _engine(np.stack(Zs), layout=layout)
     mu = 0.0123
     out = eng.hvp(np.stack(xs), np.stack(ys), mu, np.stack(vs)).cpu().numpy()
     for b in range(B):
@@ -211,7 +217,7 @@ def test_large_n4000_properties():
     n = 4000
     Z, x0, y0 = G.generate_instance(n, 4242)
     eng = _engine(Z)
-    S = eng.S[0, :n, :n]
+    S = torch.tensor(eng.unpack(0), device="cuda")
     rs = np.random.RandomState(1)
     x = x0
     y = rs.rand(n) + 0.1

@@ -37,20 +37,32 @@ def test_abi_version_and_no_device(built_lib):
 
 
 def test_layout_functions(built_lib):
+    C = N.CONST
     for n in (2, 17, 50, 1000, 4000, 4001):
         ld = built_lib.riptrm_nonnegpca_ld(n)
         rows = built_lib.riptrm_nonnegpca_rows(n)
-        assert ld >= n and ld % 16 == 0 and ld - n < 16
-        assert rows >= n and rows % 16 == 0
-        for B, cap in ((1, 0), (3, 10), (128, 4096)):
-            tot = built_lib.riptrm_workspace_bytes(n, B, cap)
-            offs = [built_lib.riptrm_workspace_offset(n, B, cap, k) for k in range(6)]
-            assert all(0 <= o < tot for o in offs[:5])
-            assert offs[0] == 0 and offs[1] == B * ld * 8
-            assert all(o % 256 == 0 or k < 4 for k, o in enumerate(offs))
-            assert offs[5] + B * cap * 32 * 8 <= tot
-    assert built_lib.riptrm_workspace_bytes(0, 1, 1) == -1
-    assert built_lib.riptrm_workspace_offset(10, 1, 1, 9) == -1
+        assert ld >= n and ld % 128 == 0 and ld - n < 128
+        assert rows >= n and rows % 32 == 0
+        nt = ld // 128
+        assert built_lib.riptrm_nonnegpca_s_elems(n, C["RIPTRM_LAYOUT_FULL"]) == rows * ld
+        sym = built_lib.riptrm_nonnegpca_s_elems(n, C["RIPTRM_LAYOUT_SYMTILE"])
+        assert sym == nt * (nt + 1) // 2 * 128 * 128
+        if n >= 1000:
+            assert sym < 0.6 * n * n  # about half the bytes of the full matrix
+        if n >= 4000:
+            assert sym < 0.55 * n * n
+        for layout in (C["RIPTRM_LAYOUT_FULL"], C["RIPTRM_LAYOUT_SYMTILE"]):
+            for B, cap in ((1, 0), (3, 10), (128, 4096)):
+                tot = built_lib.riptrm_workspace_bytes(n, B, cap, layout)
+                offs = [built_lib.riptrm_workspace_offset(n, B, cap, layout, k) for k in range(6)]
+                assert all(0 <= o < tot for o in offs[:5])
+                assert offs[0] == 0 and offs[1] == B * ld * 8
+                assert offs[4] % 256 == 0 and offs[5] % 256 == 0
+                assert offs[5] + B * cap * 32 * 8 <= tot
+    assert built_lib.riptrm_workspace_bytes(0, 1, 1, 0) == -1
+    assert built_lib.riptrm_workspace_bytes(10, 1, 1, 7) == -1
+    assert built_lib.riptrm_workspace_offset(10, 1, 1, 0, 9) == -1
+    assert built_lib.riptrm_nonnegpca_s_elems(10, 5) == -1
 
 
 def test_options_struct_layout_matches_c(tmp_path):
