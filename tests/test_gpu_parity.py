@@ -2,11 +2,9 @@
 
 Tolerances (fp64 throughout; the only differences are reduction order and libm-vs-ocml log/acos):
 * operator level (S-pass, barrier Hessian, tCG step from the same state): rel 1e-12 / 1e-9;
-* trajectory level (whole solve): identical branch decisions (inner_status, dxtype, radius
-  updates, dual clipping) and values within rtol 1e-6 on the outer iterates (log rows with
-  inner_status None/'converged') and 5e-2 on intermediate trial rows — CG amplifies rounding
-  there: the two CPU back-ends themselves differ by up to 0.6% on those rows
-  (tests/test_oracle.py::test_structured_matches_vectorized_fixture).
+* trajectory level (whole solve): identical branch decisions and per-row values within the
+  bounds of tests/parity.py, calibrated on the two CPU oracles against each other
+  (tests/test_oracle.py::test_comparator_calibration).
 """
 import numpy as np
 import pytest
@@ -111,23 +109,9 @@ def test_tcg_matches_oracle_teacher_forced(n):
         assert np.linalg.norm(heta[b] - he) <= 1e-8 * max(np.linalg.norm(he), 1e-300), b
 
 
-def _compare_logs(gl, rl, rtol=1e-6, atol=1e-13, rtol_trial=5e-2):
-    """Same branch decisions everywhere; values within rtol on the outer iterates (rows with
-    inner_status None/'converged') and within rtol_trial on intermediate trial rows, whose
-    residuals inherit CG's rounding sensitivity (the two CPU back-ends differ by up to ~0.6%
-    there on dataset/NonnegPCA/1, tests/test_oracle.py)."""
-    assert list(gl.keys()) == list(rl.keys())
-    assert len(gl["iteration"]) == len(rl["iteration"]), (len(gl["iteration"]), len(rl["iteration"]))
-    for k in ("iteration", "num_inner", "inner_status", "dxtype", "radius_update", "dual_clipping"):
-        if k in gl:
-            assert gl[k] == rl[k], k
-    outer = np.array([s in (None, "converged") for s in rl["inner_status"]])
-    for k in ("residual", "cost", "gradnorm", "complviolation", "mu", "normdx", "TR_radius"):
-        if k in gl:
-            g = np.array([np.nan if v is None else v for v in gl[k]], dtype=float)
-            r = np.array([np.nan if v is None else v for v in rl[k]], dtype=float)
-            np.testing.assert_allclose(g[outer], r[outer], rtol=rtol, atol=atol, equal_nan=True, err_msg=k)
-            np.testing.assert_allclose(g[~outer], r[~outer], rtol=rtol_trial, atol=atol, equal_nan=True, err_msg=k)
+def _compare_logs(gl, rl):
+    from parity import compare_logs
+    compare_logs(gl, rl)
 
 
 def test_full_solve_fixture_n50(fixture_n50):
@@ -138,8 +122,8 @@ def test_full_solve_fixture_n50(fixture_n50):
     ref = O.solve(Z, x0, y0, _oracle_opt(maxiter=12))
     assert f"{out.log['residual'][0]:.6e}" == "4.986888e+00"
     _compare_logs(out.log, ref.log)
-    np.testing.assert_allclose(out.x, ref.x, atol=1e-7)
-    np.testing.assert_allclose(out.ineqLagmult, ref.y, rtol=1e-5, atol=1e-8)
+    np.testing.assert_allclose(out.x, ref.x, atol=1e-6)
+    np.testing.assert_allclose(out.ineqLagmult, ref.y, rtol=1e-3, atol=1e-6)
     assert out.option["stoppingcriterion"].startswith("Max iteration count reached; maxiter=12 after")
     assert out.name == "RIPTRM_tCG"
 
@@ -179,7 +163,14 @@ def test_edge_options_match_oracle():
         res = eng.solve(x0[None], y0[None], _gpu_opt(**kw))
         ref = O.solve(Z, x0, y0, _oracle_opt(**kw))
         _compare_logs(res.log(0), ref.log)
-        assert (res.stopping_criterion(0) or "").split(" after")[0] == ref.stoppingcriterion.split(" after")[0], kw
+        gs, rs_ = (res.stopping_criterion(0) or ""), ref.stoppingcriterion
+        if rs_.startswith("KKT residual tolerance reached"):
+            assert gs.startswith("KKT residual tolerance reached; current residual="), kw
+            gv = float(gs.split("residual=")[1].split(" ")[0])
+            rv = float(rs_.split("residual=")[1].split(" ")[0])
+            assert abs(gv - rv) <= 1e-12 * abs(rv), kw
+        else:
+            assert gs.split(" after")[0] == rs_.split(" after")[0], kw
 
 
 def test_tiny_n2():

@@ -156,3 +156,14 @@ def test_oracle_edge_paths():
     Z, x0, y0 = G.generate_instance(2, 1)
     r3 = O.solve(Z, x0, y0, dict(OPT, maxiter=5))
     assert r3.outer_iterations == 5
+
+
+@pytest.mark.parametrize("n,seed,K", [(37, 100, 10), (37, 101, 10), (37, 104, 10), (200, 101, 12)])
+def test_comparator_calibration(n, seed, K):
+    """The GPU parity bar (tests/parity.py) is met by the two CPU oracles against each other:
+    it is the size of fp64 summation-order noise on these trajectories, not looser."""
+    from parity import compare_logs
+    Z, x0, y0 = G.generate_instance(n, seed)
+    a = O.solve(Z, x0, y0, dict(OPT, maxiter=K), structured=True)
+    b = O.solve(Z, x0, y0, dict(OPT, maxiter=K))
+    compare_logs(a.log, b.log)
