@@ -146,12 +146,15 @@ def main():
                           dtype=torch.float64, device=dev)
     tmax = torch.tensor([el], dtype=torch.float64, device=dev)
     if world > 1:
+        from distributed import gather_rows
         dist.all_reduce(counts, op=dist.ReduceOp.SUM)
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
-        # final gather of per-instance results (x, y, stats) over RCCL
+        # final gather of per-instance results (x, y, stats) over RCCL, in global instance order
         res = eng.result()
-        gx = [torch.empty_like(res.x) for _ in range(world)]
-        dist.all_gather(gx, res.x.contiguous())
+        total = B * world
+        gather_rows(res.x.contiguous(), total, world, rank)
+        gather_rows(res.y.contiguous(), total, world, rank)
+        gather_rows(torch.as_tensor(res.stats, device=dev), total, world, rank)
     T = float(tmax.item())
     outer_all, passes_all, inner_all, tcg_all, gemv_ms_all, gemv_n_all = [float(v) for v in counts.tolist()]
 
