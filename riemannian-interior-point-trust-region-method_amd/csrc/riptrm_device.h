@@ -17,7 +17,8 @@ namespace riptrm {
 
 // S layouts (RIPTRM_LAYOUT_*): full row-major, or the upper triangle in TS x TS tiles
 constexpr int TS = 128;            // tile edge of the symmetric-tile layout; vector padding unit
-constexpr int SP_THREADS = 256;    // 4 waves per tile workgroup, 32 rows each
+constexpr int SP_WAVES = 8;        // waves per tile workgroup, 16 rows each
+constexpr int SP_THREADS = SP_WAVES * 64;
 // rows of S handled by one full-layout mat-vec workgroup (4 waves x GV_RW rows)
 constexpr int GV_THREADS = 256;
 constexpr int GV_RW = 4;

@@ -197,8 +197,10 @@ __global__ void __launch_bounds__(GV_THREADS) k_gemv(DevParams P, int list_in, i
 // Symmetric-tile S-pass.  S = Z + Z^T is stored as its upper triangle of 128 x 128 tiles; tile
 // (I, J), I <= J, gives y_I += S_IJ v_J ("row part") and, off the diagonal, y_J += S_IJ^T v_I
 // ("column part"), so every S byte is read once per pass for two output blocks: ~half the
-// HBM traffic of the full matrix.  One 4-wave workgroup per tile; lane l owns columns 2l, 2l+1
-// (16 B loads, 1 KiB per wave instruction), each wave 32 rows in four 8-row batches.  Row sums
+// HBM traffic of the full matrix.  One 8-wave workgroup per tile; lane l owns columns 2l, 2l+1
+// (16 B non-temporal loads, 1 KiB per wave instruction), each wave 16 rows in two 8-row
+// batches (tools/spass_bench.hip: 8 waves 6.22 TB/s vs 4 waves 5.90, 16 waves 6.06, a pure
+// non-temporal streaming read of the same bytes 6.47; plain loads 10% slower).  Row sums
 // use an 8-row reduce-scatter across the wave (~3.5 lane exchanges per row); column sums
 // accumulate per lane and are combined across the 4 waves through LDS.  Results go to a
 // partial-sum grid P[b][I][J][0..127] (every slot written exactly once per pass) that the
@@ -269,9 +271,10 @@ __device__ __forceinline__ void spass_tile(const DevParams& P, int b, int t) {
   double* __restrict__ pb1 = P.pbuf + ((int64_t)P.batch + b) * nn;
   double c0x = 0.0, c0y = 0.0, c1x = 0.0, c1y = 0.0;
   const int rrow = 4 * ((lane >> 5) & 1) + 2 * ((lane >> 4) & 1) + ((lane >> 3) & 1);
+  constexpr int ROWS = TS / SP_WAVES;  // rows per wave
 #pragma unroll 1
-  for (int rb = 0; rb < 4; ++rb) {
-    const int r0 = w * 32 + rb * 8;
+  for (int rb = 0; rb < ROWS / 8; ++rb) {
+    const int r0 = w * ROWS + rb * 8;
     dbl2 sv[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) sv[k] = __builtin_nontemporal_load((const dbl2*)(T + (r0 + k) * TS + 2 * lane));
@@ -298,7 +301,7 @@ __device__ __forceinline__ void spass_tile(const DevParams& P, int b, int t) {
     }
   }
   if (I != J) {
-    __shared__ double cs[2][4][TS];
+    __shared__ double cs[2][SP_WAVES][TS];
     cs[0][w][2 * lane] = c0x;
     cs[0][w][2 * lane + 1] = c0y;
     if (NR == 2) {
@@ -308,9 +311,16 @@ __device__ __forceinline__ void spass_tile(const DevParams& P, int b, int t) {
     __syncthreads();
     if (threadIdx.x < TS) {
       const int c = threadIdx.x;
-      pb0[((int64_t)J * P.nt + I) * TS + c] = ((cs[0][0][c] + cs[0][1][c]) + cs[0][2][c]) + cs[0][3][c];
-      if (NR == 2)
-        pb1[((int64_t)J * P.nt + I) * TS + c] = ((cs[1][0][c] + cs[1][1][c]) + cs[1][2][c]) + cs[1][3][c];
+      double s0 = cs[0][0][c];
+#pragma unroll
+      for (int q = 1; q < SP_WAVES; ++q) s0 += cs[0][q][c];
+      pb0[((int64_t)J * P.nt + I) * TS + c] = s0;
+      if (NR == 2) {
+        double s1 = cs[1][0][c];
+#pragma unroll
+        for (int q = 1; q < SP_WAVES; ++q) s1 += cs[1][q][c];
+        pb1[((int64_t)J * P.nt + I) * TS + c] = s1;
+      }
     }
   }
 }
@@ -420,30 +430,48 @@ struct Machine {
   __device__ __forceinline__ void copy(int dst, int src) {
     double* d = V(dst);
     const double* a = V(src);
+    #pragma unroll 4
     for (int i = tid; i < n; i += ST_THREADS) d[i] = a[i];
   }
 
-  // OUT_k = sum_J P_k[b][I][J] for the symmetric-tile layout, J in fixed order
+  // OUT_k = sum_J P_k[b][I][J] for the symmetric-tile layout, J in fixed order.  Each thread
+  // sums GE elements at once with GJ partials per element in flight (GE*GJ loads per round),
+  // so the ~nt rounds of memory latency of a naive loop become ~nt/GJ.
   __device__ __forceinline__ void gather_out(int nr) {
+    constexpr int GE = 8, GJ = 4;
     const int nt = P.nt;
     const int64_t nn = (int64_t)nt * nt * TS;
     for (int k = 0; k < nr; ++k) {
       const double* pb = P.pbuf + ((int64_t)k * P.batch + b) * nn;
       double* O = V(k == 0 ? V_OUT0 : V_OUT1);
-      for (int i = tid; i < n; i += ST_THREADS) {
-        const int I = i / TS, c = i - I * TS;
-        const double* q = pb + (int64_t)I * nt * TS + c;
-        double acc = q[0];
-        int J = 1;
-        for (; J + 8 <= nt; J += 8) {
-          double t[8];
+      for (int base = tid; base < n; base += ST_THREADS * GE) {
+        const double* q[GE];
+        double acc[GE];
 #pragma unroll
-          for (int u = 0; u < 8; ++u) t[u] = q[(int64_t)(J + u) * TS];
-#pragma unroll
-          for (int u = 0; u < 8; ++u) acc += t[u];
+        for (int e = 0; e < GE; ++e) {
+          int i = base + e * ST_THREADS;
+          i = i < n ? i : n - 1;  // clamp: duplicate work, stored only if in range
+          const int I = i / TS, c = i - I * TS;
+          q[e] = pb + (int64_t)I * nt * TS + c;
+          acc[e] = q[e][0];
         }
-        for (; J < nt; ++J) acc += q[(int64_t)J * TS];
-        O[i] = acc;
+        for (int J = 1; J < nt; J += GJ) {
+          double t[GE][GJ];
+#pragma unroll
+          for (int e = 0; e < GE; ++e)
+#pragma unroll
+            for (int u = 0; u < GJ; ++u) t[e][u] = (J + u < nt) ? q[e][(int64_t)(J + u) * TS] : 0.0;
+#pragma unroll
+          for (int e = 0; e < GE; ++e)
+#pragma unroll
+            for (int u = 0; u < GJ; ++u)
+              if (J + u < nt) acc[e] += t[e][u];
+        }
+#pragma unroll
+        for (int e = 0; e < GE; ++e) {
+          const int i = base + e * ST_THREADS;
+          if (i < n) O[i] = acc[e];
+        }
       }
     }
   }
@@ -489,6 +517,7 @@ struct Machine {
     const double* X = V(V_X);
     const double* Y = V(V_Y);
     double r1[2] = {0.0, 0.0};
+    #pragma unroll 4
     for (int i = tid; i < n; i += ST_THREADS) {
       r1[0] += X[i] * u[i];
       r1[1] += X[i] * v[i];
@@ -496,6 +525,7 @@ struct Machine {
     bsum<2>(R, r1);
     const double xu = r1[0], xv = r1[1];
     double r2[1] = {0.0};
+    #pragma unroll 4
     for (int i = tid; i < n; i += ST_THREADS) {
       const double q = (Y[i] * (v[i] - X[i] * xv)) / X[i];
       r2[0] += X[i] * q;
@@ -503,6 +533,7 @@ struct Machine {
     bsum<1>(R, r2);
     const double xq = r2[0];
     const double coef = s[ST_COEF];
+    #pragma unroll 4
     for (int i = tid; i < n; i += ST_THREADS) {
       const double q = (Y[i] * (v[i] - X[i] * xv)) / X[i];
       const double hf = -u[i] + xu * X[i];
@@ -521,6 +552,7 @@ struct Machine {
     const int op[9] = {0, 0, 0, 0, 0, 0, 0, 2, 2};
     a[7] = 0.0;
     a[8] = -INFINITY;
+    #pragma unroll 4
     for (int i = tid; i < n; i += ST_THREADS) {
       const double x = X[i], y = Y[i];
       a[0] += x * SX[i];                  // x.Sx
@@ -540,6 +572,7 @@ struct Machine {
     const double xSx = a[0], yx = a[2];
     const double xg = -xSx;
     double gg[2] = {0.0, 0.0};
+    #pragma unroll 4
     for (int i = tid; i < n; i += ST_THREADS) {
       const double x = X[i];
       const double g = -SX[i];
@@ -683,6 +716,7 @@ struct Machine {
     double* HE = V(V_HETA);
     const double mu = s[ST_MU];
     double h[4] = {0.0, 0.0, 0.0, 0.0};
+    #pragma unroll 4
     for (int i = tid; i < n; i += ST_THREADS) {
       const double x = X[i];
       h[0] += x * x;
@@ -699,6 +733,7 @@ struct Machine {
     s[ST_FCUR] = -0.5 * xSx;
     const double xg = -xSx;
     double rr[1] = {0.0};
+    #pragma unroll 4
     for (int i = tid; i < n; i += ST_THREADS) {
       const double x = X[i];
       const double g = -SX[i];
@@ -740,6 +775,7 @@ struct Machine {
     double* Rv = V(V_R);
     double* Dw = V(V_IN0);
     double d1[1] = {0.0};
+    #pragma unroll 4
     for (int i = tid; i < n; i += ST_THREADS) d1[0] += D[i] * U[i];
     bsum<1>(R, d1);
     const double d_Hd = d1[0];
@@ -755,6 +791,7 @@ struct Machine {
     const double D2 = Delta * Delta;
     if (d_Hd <= 0.0 || e_Pe_new >= D2) {
       const double tau = (-e_Pd + sqrt(e_Pd * e_Pd + d_Pd * (D2 - e_Pe))) / d_Pd;
+      #pragma unroll 4
       for (int i = tid; i < n; i += ST_THREADS) {
         E[i] = E[i] + tau * D[i];
         HE[i] = HE[i] + tau * U[i];
@@ -764,6 +801,7 @@ struct Machine {
     }
     s[ST_EPE] = e_Pe_new;
     double m2[2] = {0.0, 0.0};
+    #pragma unroll 4
     for (int i = tid; i < n; i += ST_THREADS) {
       const double ne = E[i] + alpha * D[i];
       const double nh = HE[i] + alpha * U[i];
@@ -778,6 +816,7 @@ struct Machine {
     }
     s[ST_MODEL] = new_model;
     double r2[1] = {0.0};
+    #pragma unroll 4
     for (int i = tid; i < n; i += ST_THREADS) {
       E[i] = E[i] + alpha * D[i];
       HE[i] = HE[i] + alpha * U[i];
@@ -800,6 +839,7 @@ struct Machine {
     const double znew = r_r;
     const double beta = znew / zold;
     double p1[1] = {0.0};
+    #pragma unroll 4
     for (int i = tid; i < n; i += ST_THREADS) {
       const double dn = -Rv[i] + beta * D[i];
       Dw[i] = dn;
@@ -807,6 +847,7 @@ struct Machine {
     }
     bsum<1>(R, p1);
     const double xd = p1[0];
+    #pragma unroll 4
     for (int i = tid; i < n; i += ST_THREADS) Dw[i] = Dw[i] - xd * X[i];  // to_tangent_space
     s[ST_ZR] = znew;
     s[ST_EPD] = beta * (e_Pd + alpha * d_Pd);
@@ -827,6 +868,7 @@ struct Machine {
     const double* Y = V(V_Y);
     const double* E = V(V_ETA);
     double e1[2] = {0.0, 0.0};
+    #pragma unroll 4
     for (int i = tid; i < n; i += ST_THREADS) {
       e1[0] += E[i] * E[i];
       e1[1] += X[i] * E[i];
@@ -844,6 +886,7 @@ struct Machine {
     double* YN = V(V_YNEW);
     double* XN = V(V_IN1);
     double w2[1] = {0.0};
+    #pragma unroll 4
     for (int i = tid; i < n; i += ST_THREADS) {
       const double x = X[i], y = Y[i], dx = E[i];
       const double dy = (-y + mu * (1.0 / x)) - (y * (dx - x * xdx)) / x;   // RIPTRM.py:743
@@ -856,6 +899,7 @@ struct Machine {
     double* D = V(V_IN0);
     double c3[5] = {INFINITY, INFINITY, 0.0, 0.0, 0.0};
     const int op3[5] = {1, 1, 0, 0, 0};
+    #pragma unroll 4
     for (int i = tid; i < n; i += ST_THREADS) {
       const double dx = E[i];
       const double xn = (X[i] + dx) / nw;   // retraction (x+dx)/||x+dx||
@@ -912,6 +956,7 @@ struct Machine {
     const double* SXN = V(V_OUT1);
     const double mu = s[ST_MU];
     double a[4] = {0.0, 0.0, 0.0, 0.0};
+    #pragma unroll 4
     for (int i = tid; i < n; i += ST_THREADS) {
       const double xn = XN[i];
       a[0] += xn * SXN[i];
@@ -923,6 +968,7 @@ struct Machine {
     const double xnS = a[0], ynxn = a[1];
     const double xg = -xnS;
     double g2[1] = {0.0};
+    #pragma unroll 4
     for (int i = tid; i < n; i += ST_THREADS) {
       const double xn = XN[i];
       const double gl = (-SXN[i] - xg * xn) - (YN[i] - ynxn * xn);   // gradLagrangefun
@@ -948,6 +994,7 @@ struct Machine {
     hw_apply(HW, DX, HW);
     const double* C = V(V_C);
     double pp[2] = {0.0, 0.0};
+    #pragma unroll 4
     for (int i = tid; i < n; i += ST_THREADS) {
       pp[0] += HW[i] * DX[i];
       pp[1] += C[i] * DX[i];
@@ -979,6 +1026,7 @@ struct Machine {
       double* Yw = V(V_Y);
       double* SXw = V(V_SX);
       double nd[1] = {0.0};
+      #pragma unroll 4
       for (int i = tid; i < n; i += ST_THREADS) {
         const double xn = XN[i], yn = YN[i];
         const double il = cl * np_min(np_min(Yw[i], mu / xn), 1.0);
