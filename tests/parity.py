@@ -20,6 +20,11 @@ The bar therefore is:
 """
 import numpy as np
 
+
+class BranchFlip(AssertionError):
+    """The two trajectories took a different branch at some inner iteration."""
+
+
 BRANCH_KEYS = ("iteration", "num_inner", "inner_status", "dxtype", "radius_update", "dual_clipping")
 VALUE_KEYS = ("residual", "cost", "gradnorm", "complviolation", "dualviolation", "manviolation",
               "maxviolation", "meanviolation", "mu", "normdx", "TR_radius", "minxfeasi", "minyfeasi",
@@ -34,10 +39,11 @@ def _col(log, k):
 
 def compare_logs(gl, rl, rtol=1e-4, ascale=1e-5, trial_rtol=1.0, trial_ascale=1e-2, atol=1e-14):
     assert list(gl.keys()) == list(rl.keys()), (list(gl.keys()), list(rl.keys()))
-    assert len(gl["iteration"]) == len(rl["iteration"]), (len(gl["iteration"]), len(rl["iteration"]))
     for k in BRANCH_KEYS:
-        if k in gl:
-            assert gl[k] == rl[k], k
+        if k in gl and gl[k] != rl[k]:
+            m = min(len(gl[k]), len(rl[k]))
+            first = next((i for i in range(m) if gl[k][i] != rl[k][i]), m)
+            raise BranchFlip(f"{k} differs first at row {first}")
     outer = np.array([s in (None, "converged") for s in rl["inner_status"]])
     for k in VALUE_KEYS:
         if k not in gl:
@@ -54,3 +60,27 @@ def compare_logs(gl, rl, rtol=1e-4, ascale=1e-5, trial_rtol=1.0, trial_ascale=1e
         rows_outer = outer if k not in STEP_KEYS else np.zeros_like(outer)
         bad = m & np.where(rows_outer, ~ok_outer, ~ok_trial)
         assert not bad.any(), (k, np.nonzero(bad)[0][:5], g[bad][:5], r[bad][:5])
+
+
+def outer_rows(log):
+    """Row index of each outer iterate: row 0 and the last row of every outer iteration."""
+    it = log["iteration"]
+    rows = [0]
+    for r in range(1, len(it)):
+        if r == len(it) - 1 or it[r + 1] != it[r]:
+            rows.append(r)
+    return rows
+
+
+def compare_outer(gl, rl, rtol=1e-3, tol_mult=10.0):
+    """Outer-level agreement for trajectories whose inner branches differ (a rounding tie, as
+    the CPU oracles themselves show on some instances): same outer iterations, same end state of
+    each, and the KKT residual of every outer iterate within rtol or within tol_mult times the
+    inner stopping tolerance max(mu, 1e-14) of that outer iteration (RIPTRM.py:320)."""
+    go, ro = outer_rows(gl), outer_rows(rl)
+    assert [gl["iteration"][i] for i in go] == [rl["iteration"][i] for i in ro]
+    assert [gl["inner_status"][i] for i in go] == [rl["inner_status"][i] for i in ro]
+    for a, b in zip(go, ro):
+        g, r = float(gl["residual"][a]), float(rl["residual"][b])
+        tol = tol_mult * max(float(rl["mu"][b]), 1e-14)
+        assert abs(g - r) <= max(rtol * abs(r), tol), (rl["iteration"][b], g, r)

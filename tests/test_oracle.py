@@ -167,3 +167,16 @@ def test_comparator_calibration(n, seed, K):
     a = O.solve(Z, x0, y0, dict(OPT, maxiter=K), structured=True)
     b = O.solve(Z, x0, y0, dict(OPT, maxiter=K))
     compare_logs(a.log, b.log)
+
+
+@pytest.mark.parametrize("n,seed,K", [(37, 125, 10), (60, 115, 10)])
+def test_outer_comparator_on_branch_flips(n, seed, K):
+    """On instances where the two CPU oracles' inner branches differ, the outer-level comparator
+    (used for the same situation on the GPU) holds."""
+    from parity import BranchFlip, compare_logs, compare_outer
+    Z, x0, y0 = G.generate_instance(n, seed)
+    a = O.solve(Z, x0, y0, dict(OPT, maxiter=K), structured=True)
+    b = O.solve(Z, x0, y0, dict(OPT, maxiter=K))
+    with pytest.raises(BranchFlip):
+        compare_logs(a.log, b.log)
+    compare_outer(a.log, b.log)
