@@ -6,9 +6,9 @@
 //   [stats]    batch x RIPTRM_STAT_NFIELDS        host-visible results
 //   [log]      batch x cap x RIPTRM_LOG_NFIELDS   per-inner-iteration log rows
 //   [pbuf]     2 x batch x nt x nt x TS doubles   S-pass partial sums (symmetric-tile layout only)
-//   [lists]    2 x batch int32                    active-instance lists (ping-pong)
+//   [lists]    4 x batch int32                    active-instance lists (2 groups x ping-pong)
 //   [req]      batch int32                        right-hand sides wanted per instance (1|2)
-//   [counters] 4 int32                            list lengths (ping-pong) + spare
+//   [counters] 4 int32                            list lengths (2 groups x ping-pong)
 #pragma once
 #include <stdint.h>
 #include "../../include/riptrm.h"
@@ -94,7 +94,7 @@ inline Layout make_layout(int32_t n, int32_t batch, int32_t cap, int32_t layout)
   L.off_pbuf = o;
   if (layout == RIPTRM_LAYOUT_SYMTILE) o += (int64_t)2 * batch * L.nt * L.nt * TS * 8;
   o = round_up(o, 256);
-  L.off_lists = o; o += (int64_t)2 * batch * 4;                          o = round_up(o, 256);
+  L.off_lists = o; o += (int64_t)4 * batch * 4;                          o = round_up(o, 256);
   L.off_req = o;   o += (int64_t)batch * 4;                              o = round_up(o, 256);
   L.off_cnt = o;   o += 16;                                              o = round_up(o, 256);
   L.total = o;
@@ -116,7 +116,7 @@ struct DevParams {
   double* st;           // workspace scalars
   double* stats;
   double* log;
-  int32_t* lists;       // 2 x batch
+  int32_t* lists;       // 4 x batch: list id = group * 2 + parity
   int32_t* req;
   int32_t* cnt;
   const double* mu_tab;

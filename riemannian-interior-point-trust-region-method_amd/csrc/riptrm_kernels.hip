@@ -1118,12 +1118,15 @@ struct Machine {
   }
 };
 
-// full = 1: workgroup b serves instance b; else workgroup k serves lists[list_in][k].
-__global__ void __launch_bounds__(ST_THREADS) k_state(DevParams P, int full, int list_in, int list_out) {
+// full = 1: workgroup k serves instance full_base + k (k < full_count); else workgroup k
+// serves lists[list_in][k].  List ids are group * 2 + parity (two independent instance groups).
+__global__ void __launch_bounds__(ST_THREADS) k_state(DevParams P, int full, int list_in, int list_out,
+                                                      int full_base, int full_count) {
   __shared__ double redbuf[2 * ST_WAVES * RED_MAX];
   int b;
   if (full) {
-    b = blockIdx.x;
+    if ((int)blockIdx.x >= full_count) return;
+    b = full_base + blockIdx.x;
     if (b >= P.batch) return;
     // a full launch (solve start / resume) only (re)starts instances that wait for no S-pass
     const double* g = P.st + (int64_t)b * ST_N;
@@ -1230,8 +1233,15 @@ struct riptrm_ctx {
   int64_t inst_stride = 0;
   char* ws = nullptr;
   DevParams P{};
-  int parity = 0;        // list written by the last state kernel
-  int active_bound = 0;  // upper bound of active instances (for the gemv grid)
+  // two instance groups with independent lock-step pipelines on two streams: one group's
+  // latency-bound state kernel overlaps the other group's HBM-bound S-pass
+  int ngroups = 1;
+  int gbase[2] = {0, 0}, gsize[2] = {0, 0};
+  int parity[2] = {0, 0};        // list written by the group's last state kernel
+  int active_bound[2] = {0, 0};  // upper bound of the group's active instances
+  hipStream_t gstream[2] = {nullptr, nullptr};
+  hipStream_t own_stream = nullptr;  // created for group 1
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_pass[2] = {nullptr, nullptr};
   double clock_hz = 1e8;
   // optional HIP-event timing of every k_gemv / k_state launch (riptrm_profile_*)
   bool prof = false;
@@ -1299,13 +1309,25 @@ int riptrm_ctx_create(riptrm_ctx** out, int device, void* stream) {
   int khz = 0;
   if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device) == hipSuccess && khz > 0)
     c->clock_hz = (double)khz * 1000.0;
+  if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_pass[0], hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_pass[1], hipEventDisableTiming) != hipSuccess) {
+    riptrm_ctx_destroy(c);
+    return RIPTRM_E_HIP;
+  }
   *out = c;
   return RIPTRM_OK;
 }
 
 int riptrm_ctx_destroy(riptrm_ctx* ctx) {
-  if (ctx)
+  if (ctx) {
     for (auto e : ctx->ev_pool) (void)hipEventDestroy(e);
+    for (auto e : {ctx->ev_fork, ctx->ev_join, ctx->ev_pass[0], ctx->ev_pass[1]})
+      if (e) (void)hipEventDestroy(e);
+    if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);
+  }
   delete ctx;
   return RIPTRM_OK;
 }
@@ -1399,42 +1421,67 @@ int riptrm_nonnegpca_bind(riptrm_ctx* ctx, const double* S, int32_t n, int32_t b
   P.cnt = (int32_t*)(ctx->ws + L.off_cnt);
   P.clock_hz = ctx->clock_hz;
   P.outer_target = INT32_MAX;
+  ctx->ngroups = batch >= 8 ? 2 : 1;
+  ctx->gbase[0] = 0;
+  ctx->gsize[0] = ctx->ngroups == 2 ? (batch + 1) / 2 : batch;
+  ctx->gbase[1] = ctx->gsize[0];
+  ctx->gsize[1] = batch - ctx->gsize[0];
   ctx->bound = true;
   ctx->solving = false;
   return RIPTRM_OK;
 }
 
-static int launch_gemv(riptrm_ctx* c, int list_in, int zero_cnt, int bound) {
+static int launch_gemv(riptrm_ctx* c, hipStream_t st, int list_in, int zero_cnt, int bound) {
   if (bound <= 0) return RIPTRM_OK;
   const bool sym = c->P.layout == RIPTRM_LAYOUT_SYMTILE;
   const int64_t blocks = (int64_t)bound * (sym ? c->P.ntiles : c->P.nrb);
   int i0 = -1, i1 = -1;
   hipEvent_t e0 = nullptr, e1 = nullptr;
-  if (c->prof && (e0 = prof_event(c, &i0)) && (e1 = prof_event(c, &i1))) HIPCHK(c, hipEventRecord(e0, c->stream));
+  if (c->prof && (e0 = prof_event(c, &i0)) && (e1 = prof_event(c, &i1))) HIPCHK(c, hipEventRecord(e0, st));
   if (sym)
-    hipLaunchKernelGGL(k_spass_sym, dim3((unsigned)blocks), dim3(SP_THREADS), 0, c->stream, c->P, list_in, zero_cnt);
+    hipLaunchKernelGGL(k_spass_sym, dim3((unsigned)blocks), dim3(SP_THREADS), 0, st, c->P, list_in, zero_cnt);
   else
-    hipLaunchKernelGGL(k_gemv, dim3((unsigned)blocks), dim3(GV_THREADS), 0, c->stream, c->P, list_in, zero_cnt);
+    hipLaunchKernelGGL(k_gemv, dim3((unsigned)blocks), dim3(GV_THREADS), 0, st, c->P, list_in, zero_cnt);
   HIPCHK(c, hipGetLastError());
   if (c->prof && e1) {
-    HIPCHK(c, hipEventRecord(e1, c->stream));
+    HIPCHK(c, hipEventRecord(e1, st));
     c->ev_gemv.push_back({i0, i1});
   }
   return RIPTRM_OK;
 }
 
-static int launch_state(riptrm_ctx* c, int full, int list_in, int list_out, int bound) {
-  const int blocks = full ? c->P.batch : bound;
+static int launch_state(riptrm_ctx* c, hipStream_t st, int full, int list_in, int list_out, int bound,
+                        int full_base = 0) {
+  const int blocks = bound;
   if (blocks <= 0) return RIPTRM_OK;
   int i0 = -1, i1 = -1;
   hipEvent_t e0 = nullptr, e1 = nullptr;
-  if (c->prof && (e0 = prof_event(c, &i0)) && (e1 = prof_event(c, &i1))) HIPCHK(c, hipEventRecord(e0, c->stream));
-  hipLaunchKernelGGL(k_state, dim3((unsigned)blocks), dim3(ST_THREADS), 0, c->stream, c->P, full, list_in, list_out);
+  if (c->prof && (e0 = prof_event(c, &i0)) && (e1 = prof_event(c, &i1))) HIPCHK(c, hipEventRecord(e0, st));
+  hipLaunchKernelGGL(k_state, dim3((unsigned)blocks), dim3(ST_THREADS), 0, st, c->P, full, list_in, list_out,
+                     full_base, bound);
   HIPCHK(c, hipGetLastError());
   if (c->prof && e1) {
-    HIPCHK(c, hipEventRecord(e1, c->stream));
+    HIPCHK(c, hipEventRecord(e1, st));
     c->ev_state.push_back({i0, i1});
   }
+  return RIPTRM_OK;
+}
+
+// group 1's stream starts after everything already enqueued on the caller's stream
+static int fork_streams(riptrm_ctx* c) {
+  c->gstream[0] = c->stream;
+  c->gstream[1] = c->own_stream;
+  if (c->ngroups < 2) return RIPTRM_OK;
+  HIPCHK(c, hipEventRecord(c->ev_fork, c->stream));
+  HIPCHK(c, hipStreamWaitEvent(c->own_stream, c->ev_fork, 0));
+  return RIPTRM_OK;
+}
+
+// the caller's stream continues after group 1's work
+static int join_streams(riptrm_ctx* c) {
+  if (c->ngroups < 2) return RIPTRM_OK;
+  HIPCHK(c, hipEventRecord(c->ev_join, c->own_stream));
+  HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_join, 0));
   return RIPTRM_OK;
 }
 
@@ -1446,7 +1493,7 @@ int riptrm_nonnegpca_hvp(riptrm_ctx* ctx, const double* x, const double* y, doub
   const int B = ctx->P.batch;
   hipLaunchKernelGGL(k_hvp_prep, dim3(B), dim3(256), 0, ctx->stream, ctx->P, x, y, v, ldv);
   HIPCHK(ctx, hipGetLastError());
-  int rc = launch_gemv(ctx, 0, -1, B);
+  int rc = launch_gemv(ctx, ctx->stream, 0, -1, B);
   if (rc) return rc;
   hipLaunchKernelGGL(k_hvp_epi, dim3(B), dim3(ST_THREADS), 0, ctx->stream, ctx->P, mu, out, ldv);
   HIPCHK(ctx, hipGetLastError());
@@ -1454,32 +1501,59 @@ int riptrm_nonnegpca_hvp(riptrm_ctx* ctx, const double* x, const double* y, doub
   return RIPTRM_OK;
 }
 
+// `steps` lock-step iterations of every group.  Per step and group: S-pass then state kernel on
+// the group's stream.  The S-passes of the two groups are chained by events so they never run
+// concurrently (each gets the whole HBM; per-launch timing stays clean), while a group's state
+// kernel runs beside the other group's S-pass.
 static int run_steps(riptrm_ctx* c, int steps, int* n_active) {
+  int rc = fork_streams(c);
+  if (rc) return rc;
+  const int G = c->ngroups;
   for (int s = 0; s < steps; ++s) {
-    const int lin = c->parity, lout = c->parity ^ 1;
-    int rc = launch_gemv(c, lin, lout, c->active_bound);
-    if (rc) return rc;
-    rc = launch_state(c, 0, lin, lout, c->active_bound);
-    if (rc) return rc;
-    c->parity = lout;
+    for (int g = 0; g < G; ++g) {
+      if (c->active_bound[g] <= 0) continue;  // nothing queued: keep the list (and its count 0)
+      hipStream_t st = c->gstream[g];
+      const int lin = g * 2 + c->parity[g], lout = g * 2 + (c->parity[g] ^ 1);
+      if (G == 2) HIPCHK(c, hipStreamWaitEvent(st, c->ev_pass[g ^ 1], 0));
+      rc = launch_gemv(c, st, lin, lout, c->active_bound[g]);
+      if (rc) return rc;
+      if (G == 2) HIPCHK(c, hipEventRecord(c->ev_pass[g], st));
+      rc = launch_state(c, st, 0, lin, lout, c->active_bound[g]);
+      if (rc) return rc;
+      c->parity[g] ^= 1;
+    }
   }
-  int32_t h = 0;
-  HIPCHK(c, hipMemcpyAsync(&h, c->P.cnt + c->parity, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(c, hipStreamSynchronize(c->stream));
+  int32_t h[2] = {0, 0};
+  for (int g = 0; g < G; ++g)
+    HIPCHK(c, hipMemcpyAsync(&h[g], c->P.cnt + g * 2 + c->parity[g], sizeof(int32_t), hipMemcpyDeviceToHost,
+                             c->gstream[g]));
+  rc = join_streams(c);
+  if (rc) return rc;
+  for (int g = 0; g < G; ++g) HIPCHK(c, hipStreamSynchronize(c->gstream[g]));
   if (c->prof) prof_collect(c);
-  c->active_bound = h;
-  if (n_active) *n_active = h;
+  for (int g = 0; g < G; ++g) c->active_bound[g] = h[g];
+  if (n_active) *n_active = h[0] + (G == 2 ? h[1] : 0);
   return RIPTRM_OK;
 }
 
 // (re)start instances that wait for no S-pass (START / raised-target PAUSED): a full state
-// launch that APPENDS their requests to list `parity`, the one the next k_gemv reads, so the
-// requests of instances already in flight stay queued.
+// launch per group that APPENDS their requests to the group's list `parity`, the one its next
+// S-pass reads, so the requests of instances already in flight stay queued.
 static int kick(riptrm_ctx* c) {
-  int rc = launch_state(c, 1, c->parity, c->parity, c->P.batch);
+  int rc = fork_streams(c);
   if (rc) return rc;
-  c->active_bound = c->P.batch;
-  return RIPTRM_OK;
+  for (int g = 0; g < c->ngroups; ++g) {
+    const int l = g * 2 + c->parity[g];
+    rc = launch_state(c, c->gstream[g], 1, l, l, c->gsize[g], c->gbase[g]);
+    if (rc) return rc;
+    c->active_bound[g] = c->gsize[g];
+  }
+  return join_streams(c);
+}
+
+static void reset_groups(riptrm_ctx* c) {
+  c->parity[0] = c->parity[1] = 0;
+  c->active_bound[0] = c->active_bound[1] = 0;
 }
 
 int riptrm_tcg(riptrm_ctx* ctx, const double* x, const double* y, int64_t ldv, const double* mu, const double* delta,
@@ -1496,7 +1570,7 @@ int riptrm_tcg(riptrm_ctx* ctx, const double* x, const double* y, int64_t ldv, c
   }
   hipLaunchKernelGGL(k_init, dim3(P.batch), dim3(256), 0, ctx->stream, P, x, y, ldv, mu, delta, (int)MODE_TCG_ONLY);
   HIPCHK(ctx, hipGetLastError());
-  ctx->parity = 0;
+  reset_groups(ctx);
   HIPCHK(ctx, hipMemsetAsync(P.cnt, 0, 4 * sizeof(int32_t), ctx->stream));
   int rc = kick(ctx);
   if (rc) return rc;
@@ -1548,16 +1622,16 @@ int riptrm_solve_begin(riptrm_ctx* ctx, const riptrm_options* opt, const double*
   hipLaunchKernelGGL(k_init, dim3(P.batch), dim3(256), 0, ctx->stream, P, x0, y0, ldv, (const double*)nullptr,
                      (const double*)nullptr, (int)MODE_SOLVE);
   HIPCHK(ctx, hipGetLastError());
-  ctx->parity = 0;
+  reset_groups(ctx);
   HIPCHK(ctx, hipMemsetAsync(P.cnt, 0, 4 * sizeof(int32_t), ctx->stream));
   ctx->solving = true;
-  ctx->active_bound = 0;
   return kick(ctx);
 }
 
 int riptrm_profile_enable(riptrm_ctx* ctx, int32_t on) {
   if (!ctx) return RIPTRM_E_ARG;
   HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  HIPCHK(ctx, hipStreamSynchronize(ctx->own_stream));
   prof_collect(ctx);
   ctx->prof = on != 0;
   ctx->gemv_ms = ctx->state_ms = 0.0;
@@ -1569,6 +1643,7 @@ int riptrm_profile_read(riptrm_ctx* ctx, double* gemv_ms, int64_t* gemv_launches
                         int64_t* state_launches) {
   if (!ctx) return RIPTRM_E_ARG;
   HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  HIPCHK(ctx, hipStreamSynchronize(ctx->own_stream));
   prof_collect(ctx);
   if (gemv_ms) *gemv_ms = ctx->gemv_ms;
   if (gemv_launches) *gemv_launches = ctx->gemv_n;
