@@ -1421,7 +1421,9 @@ int riptrm_nonnegpca_bind(riptrm_ctx* ctx, const double* S, int32_t n, int32_t b
   P.cnt = (int32_t*)(ctx->ws + L.off_cnt);
   P.clock_hz = ctx->clock_hz;
   P.outer_target = INT32_MAX;
-  ctx->ngroups = batch >= 8 ? 2 : 1;
+  // two groups only when one group's S-pass is long enough (>= ~0.6 GB, ~100 us) to hide the
+  // other group's state kernel; small batches are launch/latency bound and lose from the split
+  ctx->ngroups = (batch >= 8 && (double)batch * s_elems_of(n, layout) * 8.0 >= 1.2e9) ? 2 : 1;
   ctx->gbase[0] = 0;
   ctx->gsize[0] = ctx->ngroups == 2 ? (batch + 1) / 2 : batch;
   ctx->gbase[1] = ctx->gsize[0];
