@@ -192,6 +192,11 @@ int riptrm_solve_advance(riptrm_ctx* ctx, int32_t steps, int32_t outer_target, i
 /* Device timestamps for timing windows: wall-clock ticks per second of the device clock. */
 double riptrm_device_clock_hz(riptrm_ctx* ctx);
 
+/* Lock-step pipelines: 0 = automatic (two instance groups on two streams when the batch's S is
+ * >= ~1.2 GB, so one group's state kernel overlaps the other's S-pass), 1 or 2 to force.
+ * Takes effect at the next riptrm_nonnegpca_bind.  Results do not depend on it. */
+int riptrm_set_stream_groups(riptrm_ctx* ctx, int32_t groups);
+
 /* ---- measurement ---- */
 /* Enable/disable HIP-event timing of every S-pass (k_gemv) and state-machine (k_state) launch
  * enqueued by riptrm_solve_advance / riptrm_tcg; enabling resets the totals.  Synchronises. */

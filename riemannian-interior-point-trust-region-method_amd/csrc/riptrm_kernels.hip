@@ -1236,6 +1236,7 @@ struct riptrm_ctx {
   // two instance groups with independent lock-step pipelines on two streams: one group's
   // latency-bound state kernel overlaps the other group's HBM-bound S-pass
   int ngroups = 1;
+  int groups_req = 0;  // riptrm_set_stream_groups: 0 = automatic
   int gbase[2] = {0, 0}, gsize[2] = {0, 0};
   int parity[2] = {0, 0};        // list written by the group's last state kernel
   int active_bound[2] = {0, 0};  // upper bound of the group's active instances
@@ -1424,6 +1425,7 @@ int riptrm_nonnegpca_bind(riptrm_ctx* ctx, const double* S, int32_t n, int32_t b
   // two groups only when one group's S-pass is long enough (>= ~0.6 GB, ~100 us) to hide the
   // other group's state kernel; small batches are launch/latency bound and lose from the split
   ctx->ngroups = (batch >= 8 && (double)batch * s_elems_of(n, layout) * 8.0 >= 1.2e9) ? 2 : 1;
+  if (ctx->groups_req > 0) ctx->ngroups = (ctx->groups_req >= 2 && batch >= 2) ? 2 : 1;
   ctx->gbase[0] = 0;
   ctx->gsize[0] = ctx->ngroups == 2 ? (batch + 1) / 2 : batch;
   ctx->gbase[1] = ctx->gsize[0];
@@ -1628,6 +1630,13 @@ int riptrm_solve_begin(riptrm_ctx* ctx, const riptrm_options* opt, const double*
   HIPCHK(ctx, hipMemsetAsync(P.cnt, 0, 4 * sizeof(int32_t), ctx->stream));
   ctx->solving = true;
   return kick(ctx);
+}
+
+int riptrm_set_stream_groups(riptrm_ctx* ctx, int32_t groups) {
+  if (!ctx || groups < 0 || groups > 2) return RIPTRM_E_ARG;
+  if (ctx->solving) return fail(ctx, RIPTRM_E_STATE, "set_stream_groups: call before riptrm_nonnegpca_bind");
+  ctx->groups_req = groups;
+  return RIPTRM_OK;
 }
 
 int riptrm_profile_enable(riptrm_ctx* ctx, int32_t on) {

@@ -166,7 +166,7 @@ class NonnegPCABatch:
     """A batch of NonnegPCA instances with a common n, resident on one GPU."""
 
     def __init__(self, n: int, batch: int, device: Optional[int] = None, log_capacity: int = 4096,
-                 layout: str = "sym"):
+                 layout: str = "sym", stream_groups: int = 0):
         if not torch.cuda.is_available():
             raise RuntimeError("NonnegPCABatch needs a ROCm GPU (gfx950); there is no CPU fallback")
         if n < 2 or batch < 1:
@@ -182,6 +182,7 @@ class NonnegPCABatch:
         self.rows = int(self.lib.riptrm_nonnegpca_rows(self.n))
         self.inst_stride = int(self.lib.riptrm_nonnegpca_s_elems(self.n, self.layout))
         self.ctx = N.Context(self.device.index, _stream_handle(self.device))
+        self.ctx.check(self.lib.riptrm_set_stream_groups(self.ctx.h, int(stream_groups)), "riptrm_set_stream_groups")
         self.S = torch.zeros((self.batch, self.inst_stride), dtype=torch.float64, device=self.device)
         nbytes = int(self.lib.riptrm_workspace_bytes(self.n, self.batch, self.cap, self.layout))
         self.ws = torch.zeros(nbytes + 256, dtype=torch.uint8, device=self.device)
