@@ -85,7 +85,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=1, help="untimed outer iterations per instance")
     ap.add_argument("--layout", default="sym", choices=["sym", "full"], help="storage of S = Z + Z^T")
     ap.add_argument("--cycle", type=int, default=20, help="outer iterations per solve before restart")
-    ap.add_argument("--n", type=int, default=4000)
+    ap.add_argument("--dim", type=int, default=4000, help="problem dimension n")
     ap.add_argument("--batch", type=int, default=128, help="instances per GPU")
     ap.add_argument("--cpu-budget", type=float, default=25.0, help="seconds of CPU-baseline sampling (0 = skip)")
     ap.add_argument("--seed0", type=int, default=20251212)
@@ -117,7 +117,7 @@ def main():
     import engine
     from problems import manviofun
 
-    n, B, W, K = args.n, args.batch, args.warmup, args.steps
+    n, B, W, K = args.dim, args.batch, args.warmup, args.steps
     eng = engine.NonnegPCABatch(n, B, log_capacity=2048, layout=args.layout)
     log(f"rank {rank}/{world}: generating {B} instances n={n} ({B * eng.inst_stride * 8 / 1e9:.1f} GB S)")
     # global instance ids owned by this rank: rank, rank+world, ... (seed seed0 + id)
