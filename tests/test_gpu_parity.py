@@ -253,3 +253,26 @@ def test_deterministic_and_batch_independent():
         for k in a:
             if k != "time":
                 assert a[k] == c[k] or np.array_equal(np.array(a[k], float), np.array(c[k], float)), k
+
+
+def test_simulator_end_to_end_fixture(tmp_path):
+    """cfg -> coordinator -> RIPTRM on the GPU -> CSVs in the reference layout."""
+    import os
+    import shutil
+    import pandas as pd
+    from conftest import GOLDEN
+    from simulator import Simulator
+    ds = tmp_path / "dataset" / "NonnegPCA" / "1"
+    ds.mkdir(parents=True)
+    for f in ("dim.csv", "Z.csv", "initx_a.csv", "initineqLagmult.csv"):
+        shutil.copy(os.path.join(GOLDEN, "nonnegpca_1", f), ds / f)
+    cfg = {"problem_name": "NonnegPCA", "problem_instance": 1, "problem_initialpoint": "a",
+           "problem_coordinator_name": "coordinator", "solver_name": ["RIPTRM"],
+           "solver_option": {"common": {"maxtime": 240, "maxiter": 6, "tolresid": 1e-16, "verbosity": 0},
+                             "RIPTRM": {"TRS_solver": "tCG", "second_order_stationarity": False}}}
+    outs = Simulator(cfg, root=str(tmp_path)).run()
+    d = tmp_path / "intermediate" / "NonnegPCA" / "1" / "a"
+    log = pd.read_csv(d / "RIPTRM_tCG_log.csv")
+    assert abs(log["residual"][0] - 4.986888432851817) < 1e-12
+    assert log["iteration"].max() == 6
+    assert np.allclose(np.loadtxt(d / "RIPTRM_tCG_x.csv"), outs[0].x)

@@ -150,3 +150,27 @@ def test_engine_refuses_without_gpu():
     import engine
     with pytest.raises(RuntimeError):
         engine.NonnegPCABatch(10, 1)
+
+
+def test_save_output_reference_layout(tmp_path):
+    """CSV files as base_simulator.Simulator.save_output writes them (no GPU needed)."""
+    import pandas as pd
+    from simulator import save_output
+    from solver_base import Output
+    log = {"iteration": [0, 1, 1], "time": [0, 0.1, 0.2], "residual": [4.9, 0.5, 0.1],
+           "inner_status": [None, "successful", "converged"], "dual_clipping": [None, False, None]}
+    out = Output(name="RIPTRM_tCG", x=np.array([0.6, 0.8]), option={"maxiter": 3, "tolresid": 1e-16},
+                 log=log, ineqLagmult=np.array([1.0, 2.0]), eqLagmult=[])
+    files = save_output(str(tmp_path), out.name, out)
+    names = sorted(os.path.basename(f) for f in files)
+    assert names == sorted(f"RIPTRM_tCG_{a}.csv" for a in ("name", "x", "option", "log", "ineqLagmult", "eqLagmult"))
+    np.testing.assert_array_equal(np.loadtxt(tmp_path / "RIPTRM_tCG_x.csv"), [0.6, 0.8])
+    df = pd.read_csv(tmp_path / "RIPTRM_tCG_log.csv")
+    assert list(df.columns) == list(log.keys())
+    conv = df[(df["inner_status"] == "converged") | (df["inner_status"].isna())]   # analyzer.ipynb filter
+    assert list(conv["residual"]) == [4.9, 0.1]
+    opt = pd.read_csv(tmp_path / "RIPTRM_tCG_option.csv")
+    assert opt["maxiter"][0] == 3
+    assert open(tmp_path / "RIPTRM_tCG_eqLagmult.csv").read() == ""
+    # csv.writerows on the name string: one character per row, as the reference writes it
+    assert open(tmp_path / "RIPTRM_tCG_name.csv").read().split() == list("RIPTRM_tCG")
