@@ -37,6 +37,7 @@ for p in (ROOT, PKG):
 
 METRIC = "outer RIPTRM iterations/sec, batched NonnegPCA n=4000, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0
+MFMA_F64_PEAK_TFS = 78.6  # MI355X dense FP64 matrix peak (spec); tools/mfma_bench.hip issue probe: 70 TFLOP/s
 
 
 def log(msg):
@@ -83,7 +84,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=19, help="timed outer iterations per instance")
     ap.add_argument("--warmup", type=int, default=1, help="untimed outer iterations per instance")
-    ap.add_argument("--layout", default="sym", choices=["sym", "full"], help="storage of S = Z + Z^T")
+    ap.add_argument("--layout", default="sym", choices=["sym", "full", "shared"],
+                    help="storage of S = Z + Z^T (shared: one Z, --batch initial points, MFMA S-pass)")
     ap.add_argument("--cycle", type=int, default=20, help="outer iterations per solve before restart")
     ap.add_argument("--dim", type=int, default=4000, help="problem dimension n")
     ap.add_argument("--batch", type=int, default=128, help="instances per GPU")
@@ -119,7 +121,8 @@ def main():
 
     n, B, W, K = args.dim, args.batch, args.warmup, args.steps
     eng = engine.NonnegPCABatch(n, B, log_capacity=2048, layout=args.layout)
-    log(f"rank {rank}/{world}: generating {B} instances n={n} ({B * eng.inst_stride * 8 / 1e9:.1f} GB S)")
+    nS = 1 if args.layout == "shared" else B
+    log(f"rank {rank}/{world}: generating {B} instances n={n} ({nS * eng.inst_stride * 8 / 1e9:.1f} GB S)")
     # global instance ids owned by this rank: rank, rank+world, ... (seed seed0 + id)
     gen_ids = [rank + world * i for i in range(B)]
     xg, yg = eng.generate_synthetic(args.seed0, ids=gen_ids)
@@ -176,7 +179,7 @@ def main():
         achieved = (passes_r0 * bytes_per_pass / gemv_s / 1e9) if gemv_s > 0 else None
         nl = max(1, int(prof["gemv_launches"]))
         traffic = None
-        if os.path.exists(args.traffic_json):
+        if os.path.exists(args.traffic_json) and args.layout == "sym":
             try:
                 tj = json.load(open(args.traffic_json))
                 if tj.get("n") == n:
@@ -184,6 +187,22 @@ def main():
                     traffic = tj["hbm_bytes_per_instance_pass"] * passes_r0 / nl
             except Exception as e:  # pragma: no cover
                 log(f"traffic json unreadable: {e}")
+        if args.layout == "shared":
+            # dense product on the fp64 matrix cores: 2 n^2 algorithmic flops per right-hand side
+            flops = passes_r0 * 2.0 * n * n
+            tf = flops / gemv_s / 1e12 if gemv_s > 0 else None
+            roofline = {"bound": "mfma", "achieved": tf, "peak": MFMA_F64_PEAK_TFS, "unit": "TFLOP/s",
+                        "frac": (tf / MFMA_F64_PEAK_TFS) if tf else None, "traffic": None,
+                        "kernel": "k_spass_mm (shared-S multi-start S-pass, v_mfma_f64_16x16x4_f64)",
+                        "flops_per_launch": flops / nl, "avg_launch_us": prof["gemv_ms"] * 1e3 / nl}
+        else:
+            roofline = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
+                        "traffic": traffic,
+                        "kernel": "k_spass_sym (S-pass, symmetric tiles)" if args.layout == "sym"
+                                  else "k_gemv (S-pass, full matrix)",
+                        "bytes_per_launch": passes_r0 * bytes_per_pass / nl,
+                        "avg_launch_us": prof["gemv_ms"] * 1e3 / nl}
         cpu = None
         if args.cpu_budget > 0 and world == 1:
             log("CPU baseline (oracle) ...")
@@ -201,18 +220,14 @@ def main():
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (reference generator recipe src/NonnegPCA/generator.py:9-65, drawn on device)",
-            "config": {"workload": f"NonnegPCA n={n}, batch of {B} independent instances per GPU "
-                                   f"(BASELINE configs[2]; configs[3] at 8 GPUs)",
+            "config": {"workload": (f"NonnegPCA n={n}, one Z with {B} initial points per GPU (multi-start, "
+                                    f"the problem_initialpoint axis; SURVEY 8d variant)") if args.layout == "shared"
+                                   else (f"NonnegPCA n={n}, batch of {B} independent instances per GPU "
+                                         f"(BASELINE configs[2]; configs[3] at 8 GPUs)"),
                        "n": n, "batch_per_gpu": B, "global_batch": B * world,
                        "outer_window": [W + 1, W + K], "restart_every": args.cycle, "layout": args.layout,
                        "parallelism": f"instance-sharded x{world}"},
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
-                         "traffic": traffic,
-                         "kernel": "k_spass_sym (S-pass, symmetric tiles)" if args.layout == "sym"
-                                   else "k_gemv (S-pass, full matrix)",
-                         "bytes_per_launch": passes_r0 * bytes_per_pass / nl,
-                         "avg_launch_us": prof["gemv_ms"] * 1e3 / nl},
+            "roofline": roofline,
             "cpu_baseline": cpu,
             "detail": {"inner_iterations_per_s": inner_all / T, "tcg_iterations_per_s": tcg_all / T,
                        "s_passes_per_s": passes_all / T, "gemv_time_frac": (prof["gemv_ms"] / 1e3) / T,

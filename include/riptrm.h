@@ -71,6 +71,10 @@ extern "C" {
 #define RIPTRM_LAYOUT_FULL 0      /* row-major, riptrm_nonnegpca_rows(n) rows of riptrm_nonnegpca_ld(n) */
 #define RIPTRM_LAYOUT_SYMTILE 1   /* upper triangle as 128x128 row-major tiles (I,J), I <= J, ordered
                                    * row by row: tile t = I*nt - I*(I-1)/2 + (J-I), nt = ld/128 */
+#define RIPTRM_LAYOUT_SHARED 2    /* multi-start: ONE full row-major S shared by every instance of the
+                                   * batch (same Z, different initial points: the reference's
+                                   * problem_initialpoint axis); bind with inst_stride = 0.  The S-pass
+                                   * is a fp64 MFMA product S [v_1 .. v_B] */
 
 /* manifold-violation kinds for the KKT residual (option 'manviofun') */
 #define RIPTRM_MANVIO_ZERO 0     /* RIPTRM.py:347 default: lambda problem, x: 0 */

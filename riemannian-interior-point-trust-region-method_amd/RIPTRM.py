@@ -61,9 +61,13 @@ class RIPTRM(Solver):
         if any(p.n != n for p in problems):
             raise ValueError("run_batch needs instances of equal dimension n (group them by n)")
         B = len(problems)
-        eng = NonnegPCABatch(n, B, log_capacity=log_capacity)
-        Z = np.stack([np.asarray(p.Z.cpu() if hasattr(p.Z, "cpu") else p.Z, dtype=np.float64) for p in problems])
-        eng.load_Z(Z)
+        Zs = [np.asarray(p.Z.cpu() if hasattr(p.Z, "cpu") else p.Z, dtype=np.float64) for p in problems]
+        # multi-start (the problem_initialpoint axis): one Z for every problem -> one shared S,
+        # S-pass on the matrix cores
+        shared = B > 1 and all(z is Zs[0] or np.array_equal(z, Zs[0]) for z in Zs[1:])
+        eng = NonnegPCABatch(n, B, log_capacity=log_capacity, layout="shared" if shared else "sym")
+        eng.load_Z(Zs[0] if shared else np.stack(Zs))
+        self.last_layout = eng.layout_name
         x0 = np.stack([np.asarray(p.initialpoint, dtype=np.float64) for p in problems])
         y0 = np.stack([np.asarray(p.initialineqLagmult, dtype=np.float64) for p in problems])
         res = eng.solve(x0, y0, self.option)

@@ -5,7 +5,8 @@
 //   [state]    batch x ST_N doubles               per-instance scalars (see enum St)
 //   [stats]    batch x RIPTRM_STAT_NFIELDS        host-visible results
 //   [log]      batch x cap x RIPTRM_LOG_NFIELDS   per-inner-iteration log rows
-//   [pbuf]     2 x batch x nt x nt x TS doubles   S-pass partial sums (symmetric-tile layout only)
+//   [pbuf]     2 x batch x nt x nt x TS doubles   S-pass partial sums (symmetric-tile layout)
+//              MM_KZ x 2 x batch x ld doubles    K-slice partial products (shared layout)
 //   [lists]    4 x batch int32                    active-instance lists (2 groups x ping-pong)
 //   [req]      batch int32                        right-hand sides wanted per instance (1|2)
 //   [counters] 4 int32                            list lengths (2 groups x ping-pong)
@@ -78,6 +79,10 @@ inline int64_t ld_of(int32_t n) { return round_up(n > 0 ? n : 1, TS); }
 inline int64_t rows_of(int32_t n) { return round_up(n > 0 ? n : 1, 32); }  // k_pack writes 32-row sub-tiles
 inline int32_t nt_of(int32_t n) { return (int32_t)(ld_of(n) / TS); }
 inline int64_t ntiles_of(int32_t n) { const int64_t t = nt_of(n); return t * (t + 1) / 2; }
+// shared-S MFMA S-pass: K is split over MM_KZ workgroup slices whose partial products land in
+// MM_KZ x 2 x batch x ld slabs, summed in slice order by the state kernel
+constexpr int MM_KZ = 4;
+
 // doubles of one instance of S in a layout
 inline int64_t s_elems_of(int32_t n, int32_t layout) {
   return layout == RIPTRM_LAYOUT_SYMTILE ? ntiles_of(n) * TS * TS : rows_of(n) * ld_of(n);
@@ -93,6 +98,7 @@ inline Layout make_layout(int32_t n, int32_t batch, int32_t cap, int32_t layout)
   L.off_log = o;   o += (int64_t)batch * cap * RIPTRM_LOG_NFIELDS * 8;   o = round_up(o, 256);
   L.off_pbuf = o;
   if (layout == RIPTRM_LAYOUT_SYMTILE) o += (int64_t)2 * batch * L.nt * L.nt * TS * 8;
+  if (layout == RIPTRM_LAYOUT_SHARED) o += (int64_t)MM_KZ * 2 * batch * L.ld * 8;
   o = round_up(o, 256);
   L.off_lists = o; o += (int64_t)4 * batch * 4;                          o = round_up(o, 256);
   L.off_req = o;   o += (int64_t)batch * 4;                              o = round_up(o, 256);
@@ -111,7 +117,8 @@ struct DevParams {
   int32_t layout;       // RIPTRM_LAYOUT_*
   int32_t nt;           // tiles per dimension (symmetric-tile layout)
   int32_t ntiles;       // nt (nt + 1) / 2
-  double* pbuf;         // 2 x batch x nt x nt x TS partial sums (symmetric-tile layout)
+  double* pbuf;         // S-pass partial sums: 2 x batch x nt x nt x TS (symmetric-tile layout),
+                        // MM_KZ x 2 x batch x ld (shared layout)
   double* vec;          // workspace vectors
   double* st;           // workspace scalars
   double* stats;

@@ -337,6 +337,125 @@ __global__ void __launch_bounds__(SP_THREADS, 4) k_spass_sym(DevParams P, int li
 }
 
 // ------------------------------------------------------------------------------------------
+// Shared-S (multi-start) S-pass on the fp64 matrix cores: every active instance multiplies the
+// SAME S, so one pass is the dense product Y^T = V^T S over the active right-hand sides
+// (column c = active slot for in0, bound + slot for in1 when the instance asked for two).
+// v_mfma_f64_16x16x4_f64: A = 16 right-hand sides x 4 k, B = 4 k x 16 rows of S (S is
+// symmetric, so row i of S is column i of S^T), D = 16 x 16 fp64 accumulators.  A wave holds
+// WM x WN such tiles and walks K in 32-wide chunks: lane l loads 8 consecutive k (64 B) of
+// right-hand side / S row (l & 15) at offset 8 (l >> 4) and MFMA m of the chunk consumes
+// element m — the same k permutation on both operands, so the sum is over every k exactly once.
+// KS waves of a workgroup take interleaved chunks of one K slice and are summed through LDS in
+// wave order; MM_KZ workgroup slices (grid.z) write partial slabs that the state kernel adds in
+// slice order (deterministic; tools/mfma_bench.hip: 8x2 tiles, 4 waves, 4 slices = 34 TFLOP/s
+// at n = 4000 and 128 right-hand sides, against a 70 TFLOP/s issue-rate probe).
+// ------------------------------------------------------------------------------------------
+typedef double dbl4 __attribute__((ext_vector_type(4)));
+
+template <int WM, int WN, int KS>
+__global__ void __launch_bounds__(64 * KS) k_spass_mm(DevParams P, int list_in, int zero_cnt, int bound) {
+  if (zero_cnt >= 0 && blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0 && threadIdx.x == 0) P.cnt[zero_cnt] = 0;
+  const int nact = P.cnt[list_in];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int r = lane & 15, q = lane >> 4;
+  constexpr int CT = 16 * WM;                     // right-hand sides per workgroup
+  const int t0 = (bound + CT - 1) / CT;           // column tiles of in0
+  const int which = (int)blockIdx.y >= t0 ? 1 : 0;
+  const int s0 = ((int)blockIdx.y - which * t0) * CT;
+  if (s0 >= nact) return;
+  if (which) {  // in1 tiles: skip unless some instance of the tile asked for two right-hand sides
+    __shared__ int any2;
+    if (threadIdx.x == 0) any2 = 0;
+    __syncthreads();
+    if (threadIdx.x < CT) {
+      const int sl = s0 + threadIdx.x;
+      if (sl < nact && P.req[P.lists[list_in * P.batch + sl]] == 2) any2 = 1;
+    }
+    __syncthreads();
+    if (!any2) return;
+  }
+  const int64_t ld = P.ld;
+  const int rows = (P.n + 31) / 32 * 32;  // rows_of(n)
+  const int i0 = blockIdx.x * 16 * WN;
+  const int vk = which ? V_IN1 : V_IN0;
+  const double* ap[WM];
+  const double* bp[WN];
+#pragma unroll
+  for (int a = 0; a < WM; ++a) {
+    int sl = s0 + 16 * a + r;
+    sl = sl < nact ? sl : nact - 1;
+    ap[a] = vp(P, vk, P.lists[list_in * P.batch + sl]) + 8 * q;
+  }
+#pragma unroll
+  for (int c = 0; c < WN; ++c) {
+    int i = i0 + 16 * c + r;
+    i = i < rows ? i : rows - 1;
+    bp[c] = P.S + (int64_t)i * ld + 8 * q;
+  }
+  dbl4 acc[WM][WN];
+#pragma unroll
+  for (int a = 0; a < WM; ++a)
+#pragma unroll
+    for (int c = 0; c < WN; ++c) acc[a][c] = dbl4{0.0, 0.0, 0.0, 0.0};
+  const int nch_all = (int)(ld / 32), per = (nch_all + MM_KZ - 1) / MM_KZ;
+  const int ch_lo = blockIdx.z * per, ch_hi = min(nch_all, ch_lo + per);
+  for (int ch = ch_lo + w; ch < ch_hi; ch += KS) {
+    const int64_t k0 = (int64_t)ch * 32;
+    dbl2 fa[WM][4], fb[WN][4];
+#pragma unroll
+    for (int a = 0; a < WM; ++a)
+#pragma unroll
+      for (int h = 0; h < 4; ++h) fa[a][h] = *(const dbl2*)(ap[a] + k0 + 2 * h);
+#pragma unroll
+    for (int c = 0; c < WN; ++c)
+#pragma unroll
+      for (int h = 0; h < 4; ++h) fb[c][h] = __builtin_nontemporal_load((const dbl2*)(bp[c] + k0 + 2 * h));
+#pragma unroll
+    for (int m = 0; m < 8; ++m)
+#pragma unroll
+      for (int a = 0; a < WM; ++a)
+#pragma unroll
+        for (int c = 0; c < WN; ++c) {
+          const double av = (m & 1) ? fa[a][m >> 1].y : fa[a][m >> 1].x;
+          const double bv = (m & 1) ? fb[c][m >> 1].y : fb[c][m >> 1].x;
+          acc[a][c] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc[a][c], 0, 0, 0);
+        }
+  }
+  if (KS > 1) {  // waves 1..KS-1 accumulate in turn into one LDS slab, wave 0 adds it last
+    __shared__ dbl4 red[WM][WN][64];
+    for (int s = 1; s < KS; ++s) {
+      if (w == s)
+#pragma unroll
+        for (int a = 0; a < WM; ++a)
+#pragma unroll
+          for (int c = 0; c < WN; ++c) red[a][c][lane] = s == 1 ? acc[a][c] : red[a][c][lane] + acc[a][c];
+      __syncthreads();
+    }
+    if (w != 0) return;
+#pragma unroll
+    for (int a = 0; a < WM; ++a)
+#pragma unroll
+      for (int c = 0; c < WN; ++c) acc[a][c] += red[a][c][lane];
+  }
+  // D (f64): column = lane & 15 -> row i of S, row = (lane >> 4) + 4 g -> right-hand side
+  double* slab = P.pbuf + ((int64_t)blockIdx.z * 2 + which) * P.batch * ld;
+#pragma unroll
+  for (int a = 0; a < WM; ++a)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int sl = s0 + 16 * a + q + 4 * g;
+      if (sl >= nact) continue;
+      const int bb = P.lists[list_in * P.batch + sl];
+      if (which && P.req[bb] != 2) continue;
+#pragma unroll
+      for (int c = 0; c < WN; ++c) {
+        const int i = i0 + 16 * c + r;
+        if (i < P.n) slab[(int64_t)bb * ld + i] = acc[a][c][g];
+      }
+    }
+}
+
+// ------------------------------------------------------------------------------------------
 // Packing: S = Z + Z^T from a row-major Z (leading dimension ldz) into either layout, zero
 // padded.  32x32 sub-tiles staged through LDS so both Z and Z^T are read coalesced; each
 // element is the single rounding of Z_ij + Z_ji (so S_ij == S_ji bit for bit).
@@ -371,7 +490,7 @@ __global__ void __launch_bounds__(256) k_pack(const double* Z, int64_t ldz, int6
   const int nsub = (int)(ld / 32);
   const int si = blockIdx.x / nsub, sj = blockIdx.x % nsub;
   const int i0 = si * 32, j0 = sj * 32;
-  if (layout == RIPTRM_LAYOUT_FULL) {
+  if (layout != RIPTRM_LAYOUT_SYMTILE) {  // full / shared: row-major
     if (i0 >= rows) return;
     pack_sub32(Zb, ldz, n, i0, j0, Sb + (int64_t)i0 * ld + j0, ld);
   } else {
@@ -437,6 +556,21 @@ struct Machine {
   // OUT_k = sum_J P_k[b][I][J] for the symmetric-tile layout, J in fixed order.  Each thread
   // sums GE elements at once with GJ partials per element in flight (GE*GJ loads per round),
   // so the ~nt rounds of memory latency of a naive loop become ~nt/GJ.
+  // shared layout: out_k[i] = sum over the MM_KZ K-slices, in slice order
+  __device__ __forceinline__ void gather_slices(int nr) {
+    const int64_t ld = P.ld, slab = (int64_t)P.batch * ld;
+    for (int k = 0; k < nr; ++k) {
+      const double* pb = P.pbuf + ((int64_t)k * P.batch + b) * ld;
+      double* O = V(k == 0 ? V_OUT0 : V_OUT1);
+      for (int i = tid; i < n; i += ST_THREADS) {
+        double acc = pb[i];
+#pragma unroll
+        for (int z = 1; z < MM_KZ; ++z) acc += pb[(int64_t)z * 2 * slab + i];
+        O[i] = acc;
+      }
+    }
+  }
+
   __device__ __forceinline__ void gather_out(int nr) {
     constexpr int GE = 8, GJ = 4;
     const int nt = P.nt;
@@ -1142,6 +1276,7 @@ __global__ void __launch_bounds__(ST_THREADS) k_state(DevParams P, int full, int
   const int ph = (int)M.s[ST_PHASE];
   if (ph == PH_DONE || ph == PH_IDLE || ph == PH_ERROR) return;
   if (!full && P.layout == RIPTRM_LAYOUT_SYMTILE) M.gather_out(P.req[b]);
+  if (!full && P.layout == RIPTRM_LAYOUT_SHARED) M.gather_slices(P.req[b]);
   M.dispatch();
   M.finish_write();
 }
@@ -1199,6 +1334,7 @@ __global__ void __launch_bounds__(ST_THREADS) k_hvp_epi(DevParams P, double mu, 
   const int b = blockIdx.x;
   Machine M(P, b, 0, redbuf);
   if (P.layout == RIPTRM_LAYOUT_SYMTILE) M.gather_out(2);
+  if (P.layout == RIPTRM_LAYOUT_SHARED) M.gather_slices(2);
   const double* X = M.V(V_X);
   const double* Y = M.V(V_Y);
   const double* SX = M.V(V_OUT1);
@@ -1343,7 +1479,9 @@ int riptrm_ctx_set_stream(riptrm_ctx* ctx, void* stream) {
 
 double riptrm_device_clock_hz(riptrm_ctx* ctx) { return ctx ? ctx->clock_hz : 0.0; }
 
-static bool layout_ok(int32_t layout) { return layout == RIPTRM_LAYOUT_FULL || layout == RIPTRM_LAYOUT_SYMTILE; }
+static bool layout_ok(int32_t layout) {
+  return layout == RIPTRM_LAYOUT_FULL || layout == RIPTRM_LAYOUT_SYMTILE || layout == RIPTRM_LAYOUT_SHARED;
+}
 
 int64_t riptrm_nonnegpca_ld(int32_t n) { return n > 0 ? ld_of(n) : -1; }
 int64_t riptrm_nonnegpca_rows(int32_t n) { return n > 0 ? rows_of(n) : -1; }
@@ -1388,8 +1526,11 @@ int riptrm_nonnegpca_bind(riptrm_ctx* ctx, const double* S, int32_t n, int32_t b
   if (!ctx) return RIPTRM_E_ARG;
   if (!S || !workspace || n < 2 || batch <= 0 || cap < 0 || !layout_ok(layout))
     return fail(ctx, RIPTRM_E_ARG, "bind: bad argument (need n >= 2, batch >= 1, a known layout)");
-  if (inst_stride < s_elems_of(n, layout) || (inst_stride % 2) != 0)
+  if (layout == RIPTRM_LAYOUT_SHARED) {
+    if (inst_stride != 0) return fail(ctx, RIPTRM_E_ARG, "bind: the shared layout needs inst_stride = 0");
+  } else if (inst_stride < s_elems_of(n, layout) || (inst_stride % 2) != 0) {
     return fail(ctx, RIPTRM_E_ARG, "bind: instance stride smaller than riptrm_nonnegpca_s_elems (or odd)");
+  }
   if (((uintptr_t)S % 16) != 0 || ((uintptr_t)workspace % 256) != 0)
     return fail(ctx, RIPTRM_E_ARG, "bind: S must be 16-byte and workspace 256-byte aligned");
   const Layout L = make_layout(n, batch, cap, layout);
@@ -1424,7 +1565,8 @@ int riptrm_nonnegpca_bind(riptrm_ctx* ctx, const double* S, int32_t n, int32_t b
   P.outer_target = INT32_MAX;
   // two groups only when one group's S-pass is long enough (>= ~0.6 GB, ~100 us) to hide the
   // other group's state kernel; small batches are launch/latency bound and lose from the split
-  ctx->ngroups = (batch >= 8 && (double)batch * s_elems_of(n, layout) * 8.0 >= 1.2e9) ? 2 : 1;
+  ctx->ngroups = (layout != RIPTRM_LAYOUT_SHARED && batch >= 8 &&
+                  (double)batch * s_elems_of(n, layout) * 8.0 >= 1.2e9) ? 2 : 1;
   if (ctx->groups_req > 0) ctx->ngroups = (ctx->groups_req >= 2 && batch >= 2) ? 2 : 1;
   ctx->gbase[0] = 0;
   ctx->gsize[0] = ctx->ngroups == 2 ? (batch + 1) / 2 : batch;
@@ -1442,7 +1584,19 @@ static int launch_gemv(riptrm_ctx* c, hipStream_t st, int list_in, int zero_cnt,
   int i0 = -1, i1 = -1;
   hipEvent_t e0 = nullptr, e1 = nullptr;
   if (c->prof && (e0 = prof_event(c, &i0)) && (e1 = prof_event(c, &i1))) HIPCHK(c, hipEventRecord(e0, st));
-  if (sym)
+  if (c->P.layout == RIPTRM_LAYOUT_SHARED) {
+    // 8 x 2 tiles (128 right-hand sides x 32 rows) for wide batches, 2 x 1 for narrow ones
+    const unsigned rows = (unsigned)rows_of(c->P.n);
+    if (bound > 32) {
+      const unsigned ct = (unsigned)((bound + 127) / 128);
+      hipLaunchKernelGGL((k_spass_mm<8, 2, 4>), dim3(rows / 32, 2 * ct, MM_KZ), dim3(256), 0, st, c->P, list_in,
+                         zero_cnt, bound);
+    } else {
+      const unsigned ct = (unsigned)((bound + 31) / 32);
+      hipLaunchKernelGGL((k_spass_mm<2, 1, 4>), dim3(rows / 16, 2 * ct, MM_KZ), dim3(256), 0, st, c->P, list_in,
+                         zero_cnt, bound);
+    }
+  } else if (sym)
     hipLaunchKernelGGL(k_spass_sym, dim3((unsigned)blocks), dim3(SP_THREADS), 0, st, c->P, list_in, zero_cnt);
   else
     hipLaunchKernelGGL(k_gemv, dim3((unsigned)blocks), dim3(GV_THREADS), 0, st, c->P, list_in, zero_cnt);

@@ -159,11 +159,15 @@ def _stream_handle(device: torch.device) -> int:
     return torch.cuda.current_stream(device).cuda_stream
 
 
-LAYOUTS = {"full": C["RIPTRM_LAYOUT_FULL"], "sym": C["RIPTRM_LAYOUT_SYMTILE"]}
+LAYOUTS = {"full": C["RIPTRM_LAYOUT_FULL"], "sym": C["RIPTRM_LAYOUT_SYMTILE"], "shared": C["RIPTRM_LAYOUT_SHARED"]}
 
 
 class NonnegPCABatch:
-    """A batch of NonnegPCA instances with a common n, resident on one GPU."""
+    """A batch of NonnegPCA instances with a common n, resident on one GPU.
+
+    layout "sym" (default) / "full": one S = Z + Z^T per instance.  layout "shared": ONE S for the
+    whole batch (multi-start: same Z, different initial points — the reference's
+    problem_initialpoint axis), S-pass on the fp64 matrix cores."""
 
     def __init__(self, n: int, batch: int, device: Optional[int] = None, log_capacity: int = 4096,
                  layout: str = "sym", stream_groups: int = 0):
@@ -180,10 +184,12 @@ class NonnegPCABatch:
         self.layout = LAYOUTS[layout]
         self.ld = int(self.lib.riptrm_nonnegpca_ld(self.n))
         self.rows = int(self.lib.riptrm_nonnegpca_rows(self.n))
+        self.shared = layout == "shared"
         self.inst_stride = int(self.lib.riptrm_nonnegpca_s_elems(self.n, self.layout))
         self.ctx = N.Context(self.device.index, _stream_handle(self.device))
         self.ctx.check(self.lib.riptrm_set_stream_groups(self.ctx.h, int(stream_groups)), "riptrm_set_stream_groups")
-        self.S = torch.zeros((self.batch, self.inst_stride), dtype=torch.float64, device=self.device)
+        self.S = torch.zeros((1 if self.shared else self.batch, self.inst_stride), dtype=torch.float64,
+                             device=self.device)
         nbytes = int(self.lib.riptrm_workspace_bytes(self.n, self.batch, self.cap, self.layout))
         self.ws = torch.zeros(nbytes + 256, dtype=torch.uint8, device=self.device)
         base = self.ws.data_ptr()
@@ -216,8 +222,18 @@ class NonnegPCABatch:
         self.ctx.set_stream(_stream_handle(self.device))
 
     def load_Z(self, Z) -> "NonnegPCABatch":
-        """Z: (batch, n, n) fp64 (numpy or torch).  S_b = Z_b + Z_b^T packed on the device."""
+        """Z: (batch, n, n) fp64 (numpy or torch).  S_b = Z_b + Z_b^T packed on the device.
+        Shared layout: one (n, n) (or (1, n, n)) Z for the whole batch."""
         Zt = torch.as_tensor(Z, dtype=torch.float64)
+        if self.shared:
+            if Zt.dim() == 3 and Zt.shape[0] == 1:
+                Zt = Zt[0]
+            if Zt.shape != (self.n, self.n):
+                raise ValueError(f"shared layout: Z must be {(self.n, self.n)}, got {tuple(Zt.shape)}")
+            self.pack_one(Zt.to(self.device).contiguous(), 0)
+            torch.cuda.synchronize(self.device)
+            self.bind()
+            return self
         if Zt.shape != (self.batch, self.n, self.n):
             raise ValueError(f"Z must be {(self.batch, self.n, self.n)}, got {tuple(Zt.shape)}")
         tmp = torch.empty((self.n, self.n), dtype=torch.float64, device=self.device)
@@ -241,7 +257,7 @@ class NonnegPCABatch:
         """Host copy of S[slot] as a dense n x n matrix (tests / inspection)."""
         raw = self.S[slot].cpu().numpy()
         n, ld = self.n, self.ld
-        if self.layout == LAYOUTS["full"]:
+        if self.layout != LAYOUTS["sym"]:
             return raw[: self.rows * ld].reshape(self.rows, ld)[:n, :n].copy()
         ts, nt = 128, ld // 128
         full = np.zeros((ld, ld))
@@ -257,7 +273,7 @@ class NonnegPCABatch:
     def bind(self):
         self._sync_stream()
         self.ctx.check(self.lib.riptrm_nonnegpca_bind(self.ctx.h, ctypes.c_void_p(self.S.data_ptr()), self.n,
-                                                      self.batch, self.layout, self.inst_stride,
+                                                      self.batch, self.layout, 0 if self.shared else self.inst_stride,
                                                       ctypes.c_void_p(self.ws_ptr), self.ws_bytes, self.cap),
                        "riptrm_nonnegpca_bind")
         self.bound = True
@@ -270,6 +286,8 @@ class NonnegPCABatch:
         random floor(delta n)-subset; feasible x0 = |u|/||u||, u ~ U[0,1)^n; y0 = 1.
         Slot b uses seed ``seed0 + ids[b]`` (ids defaults to 0..batch-1, i.e. global instance
         ids, so a sharded run draws the same instances as an unsharded one).
+        Shared layout: Z (and the first start) from ``seed0``; start b's x0 from its own
+        generator seeded ``seed0 + 1000003 * (ids[b] + 1)``.
         Returns (x0, y0) device tensors (batch, n)."""
         n = self.n
         k = int(np.floor(delta * n))
@@ -279,22 +297,38 @@ class NonnegPCABatch:
         if len(ids) != self.batch:
             raise ValueError("ids must have one entry per batch slot")
         Zb = torch.empty((n, n), dtype=torch.float64, device=self.device)
+        if self.shared:
+            self._draw_Z(Zb, int(seed0), k, snr)
+            self.pack_one(Zb, 0)
+            for b in range(self.batch):
+                g = torch.Generator(device=self.device)
+                g.manual_seed(int(seed0) + 1000003 * (int(ids[b]) + 1))
+                u = torch.rand(n, dtype=torch.float64, device=self.device, generator=g)
+                x0[b] = (u / torch.linalg.vector_norm(u)).abs()
+            torch.cuda.synchronize(self.device)
+            self.bind()
+            return x0, y0
         for b in range(self.batch):
-            g = torch.Generator(device=self.device)
-            g.manual_seed(int(seed0) + int(ids[b]))
-            idx = torch.randperm(n, generator=g, device=self.device)[:k]
-            v = torch.zeros(n, dtype=torch.float64, device=self.device)
-            v[idx] = 1.0 / math.sqrt(k)
-            Zb.normal_(0.0, 1.0, generator=g).div_(math.sqrt(n))
-            dg = torch.randn(n, dtype=torch.float64, device=self.device, generator=g) * 2 / math.sqrt(n)
-            Zb.diagonal().copy_(dg)
-            Zb.add_(math.sqrt(snr) * torch.outer(v, v))
+            g = self._draw_Z(Zb, int(seed0) + int(ids[b]), k, snr)
             u = torch.rand(n, dtype=torch.float64, device=self.device, generator=g)
             x0[b] = (u / torch.linalg.vector_norm(u)).abs()
             self.pack_one(Zb, b)
         torch.cuda.synchronize(self.device)
         self.bind()
         return x0, y0
+
+    def _draw_Z(self, Zb: torch.Tensor, seed: int, k: int, snr: float) -> torch.Generator:
+        n = self.n
+        g = torch.Generator(device=self.device)
+        g.manual_seed(seed)
+        idx = torch.randperm(n, generator=g, device=self.device)[:k]
+        v = torch.zeros(n, dtype=torch.float64, device=self.device)
+        v[idx] = 1.0 / math.sqrt(k)
+        Zb.normal_(0.0, 1.0, generator=g).div_(math.sqrt(n))
+        dg = torch.randn(n, dtype=torch.float64, device=self.device, generator=g) * 2 / math.sqrt(n)
+        Zb.diagonal().copy_(dg)
+        Zb.add_(math.sqrt(snr) * torch.outer(v, v))
+        return g
 
     # ---- operators ----------------------------------------------------------------------
     def _padded(self, a) -> torch.Tensor:

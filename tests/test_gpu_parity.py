@@ -276,3 +276,104 @@ def test_simulator_end_to_end_fixture(tmp_path):
     assert abs(log["residual"][0] - 4.986888432851817) < 1e-12
     assert log["iteration"].max() == 6
     assert np.allclose(np.loadtxt(d / "RIPTRM_tCG_x.csv"), outs[0].x)
+
+
+# ---- shared layout (multi-start: one Z, many initial points; fp64 MFMA S-pass) ----------------
+
+def _shared_engine(Z, B, cap=4096):
+    import engine
+    eng = engine.NonnegPCABatch(Z.shape[0], B, log_capacity=cap, layout="shared")
+    eng.load_Z(Z)
+    return eng
+
+
+@pytest.mark.parametrize("n", [2, 37, 129, 1000])
+def test_shared_pack_is_exact_symmetrization(n):
+    Z, _, _ = G.generate_instance(n, 5)
+    eng = _shared_engine(Z, 3)
+    np.testing.assert_array_equal(eng.unpack(0), Z + Z.T)
+    assert eng.S.shape[0] == 1
+
+
+@pytest.mark.parametrize("n,B", [(17, 3), (50, 33), (200, 130), (1000, 40), (4000, 20)])
+def test_shared_barrier_hessian_matches_oracle(n, B):
+    """Both MFMA tilings (<= 32 and > 32 right-hand sides), ragged n and B."""
+    Z, _, _ = G.generate_instance(n, 11)
+    xs, ys, vs = [], [], []
+    for b in range(B):
+        x, y = _state(n, 200 + b)
+        xs.append(x); ys.append(y)
+        vs.append(np.random.RandomState(300 + b).randn(n))
+    eng = _shared_engine(Z, B)
+    mu = 0.0123
+    out = eng.hvp(np.stack(xs), np.stack(ys), mu, np.stack(vs)).cpu().numpy()
+    P = O.NonnegPCAVectorized(Z)
+    for b in range(B):
+        _, _, Hw, _ = P.begin_inner(xs[b], ys[b], mu)
+        ref = Hw(vs[b])
+        err = np.linalg.norm(out[b] - ref) / np.linalg.norm(ref)
+        assert err < 1e-12, (b, err)
+
+
+@pytest.mark.parametrize("n,B", [(200, 6), (1000, 36)])
+def test_shared_tcg_matches_oracle_teacher_forced(n, B):
+    Z, _, _ = G.generate_instance(n, 41)
+    rs = np.random.RandomState(7)
+    xs, ys = [], []
+    for b in range(B):
+        x, y = _state(n, 400 + b)
+        xs.append(x); ys.append(y)
+    mus = rs.choice([0.1, 0.05, 1e-2, 1e-3], B)
+    deltas = rs.choice([np.pi / 8, 1e-3, 0.05, 0.3, 5.0], B)
+    eng = _shared_engine(Z, B)
+    eta, _, js, stops = eng.tcg(np.stack(xs), np.stack(ys), mus, deltas)
+    eta = eta.cpu().numpy()
+    P = O.NonnegPCAVectorized(Z)
+    for b in range(B):
+        _, _, Hw, c = P.begin_inner(xs[b], ys[b], mus[b])
+        e, _, j, stop = O.truncated_conjugate_gradient(P.manifold, Hw, xs[b], c, deltas[b], 1, 0.1, 1, n - 1)
+        assert stops[b] == stop and js[b] == j, (b, stops[b], stop, js[b], j)
+        # the MFMA product sums k in another order than dsymv (permuted 32-chunks, 4 K slices);
+        # CG amplifies that rounding over j iterations: 1e-8 here vs 1e-9 for the mat-vec layouts
+        err = np.linalg.norm(eta[b] - e) / max(np.linalg.norm(e), 1e-300)
+        assert err <= 1e-8, (b, j, err)
+
+
+@pytest.mark.parametrize("n,B,K", [(60, 40, 10), (1000, 5, 8)])
+def test_shared_multistart_solve_matches_oracle(n, B, K):
+    """One Z, B feasible starts: every start's trajectory against the oracle's."""
+    from parity import BranchFlip, compare_outer
+    Z, _, y0 = G.generate_instance(n, 500)
+    starts = []
+    for b in range(B):
+        x0 = np.abs(np.random.RandomState(600 + b).rand(n))
+        starts.append(x0 / np.linalg.norm(x0))
+    eng = _shared_engine(Z, B)
+    res = eng.solve(np.stack(starts), np.stack([y0] * B), _gpu_opt(maxiter=K))
+    xs = res.x.cpu().numpy()
+    flips = 0
+    for b in range(B):
+        ref = O.solve(Z, starts[b], y0, _oracle_opt(maxiter=K))
+        try:
+            _compare_logs(res.log(b), ref.log)
+        except BranchFlip:
+            flips += 1
+            compare_outer(res.log(b), ref.log)
+            continue
+        np.testing.assert_allclose(xs[b], ref.x, atol=1e-6)
+    assert flips <= B // 2, flips
+
+
+def test_run_batch_detects_shared_Z(fixture_n50):
+    """problem_initialpoint axis: problems that share Z run on one shared S."""
+    from problems import NonnegPCAProblem
+    from RIPTRM import RIPTRM
+    Z, x0, y0 = fixture_n50
+    x1 = np.abs(np.random.RandomState(1).rand(Z.shape[0]))
+    x1 /= np.linalg.norm(x1)
+    solver = RIPTRM(_gpu_opt(maxiter=6))
+    outs = solver.run_batch([NonnegPCAProblem(Z=Z, initialpoint=x0, initialineqLagmult=y0),
+                             NonnegPCAProblem(Z=Z, initialpoint=x1, initialineqLagmult=y0)])
+    assert solver.last_layout == "shared"
+    single = RIPTRM(_gpu_opt(maxiter=6)).run(NonnegPCAProblem(Z=Z, initialpoint=x0, initialineqLagmult=y0))
+    np.testing.assert_allclose(outs[0].log["residual"], single.log["residual"], rtol=1e-6, atol=1e-13)

@@ -51,7 +51,11 @@ def test_layout_functions(built_lib):
             assert sym < 0.6 * n * n  # about half the bytes of the full matrix
         if n >= 4000:
             assert sym < 0.55 * n * n
-        for layout in (C["RIPTRM_LAYOUT_FULL"], C["RIPTRM_LAYOUT_SYMTILE"]):
+        assert built_lib.riptrm_nonnegpca_s_elems(n, C["RIPTRM_LAYOUT_SHARED"]) == rows * ld
+        # shared layout: 4 K-slice slabs x 2 right-hand sides of partial products per instance
+        assert (built_lib.riptrm_workspace_bytes(n, 8, 0, C["RIPTRM_LAYOUT_SHARED"])
+                - built_lib.riptrm_workspace_bytes(n, 8, 0, C["RIPTRM_LAYOUT_FULL"])) >= 4 * 2 * 8 * ld * 8
+        for layout in (C["RIPTRM_LAYOUT_FULL"], C["RIPTRM_LAYOUT_SYMTILE"], C["RIPTRM_LAYOUT_SHARED"]):
             for B, cap in ((1, 0), (3, 10), (128, 4096)):
                 tot = built_lib.riptrm_workspace_bytes(n, B, cap, layout)
                 offs = [built_lib.riptrm_workspace_offset(n, B, cap, layout, k) for k in range(6)]

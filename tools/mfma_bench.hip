@@ -20,6 +20,7 @@ typedef double dbl4 __attribute__((ext_vector_type(4)));
 template <int WM, int WN, int KS>
 __global__ void __launch_bounds__(64 * KS) k_mm(const double* __restrict__ S, const double* __restrict__ V,
                                                 double* __restrict__ Y, int n, int rows, int64_t ld, int C) {
+  Y += (int64_t)blockIdx.z * C * ld;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int i0 = blockIdx.x * 16 * WN, c0 = blockIdx.y * 16 * WM;
   const int r = lane & 15, q = lane >> 4;
@@ -42,8 +43,9 @@ __global__ void __launch_bounds__(64 * KS) k_mm(const double* __restrict__ S, co
   for (int a = 0; a < WM; ++a)
 #pragma unroll
     for (int b = 0; b < WN; ++b) acc[a][b] = dbl4{0.0, 0.0, 0.0, 0.0};
-  const int nch = (int)(ld / 32);
-  for (int ch = w; ch < nch; ch += KS) {
+  const int nch_all = (int)(ld / 32), per = (nch_all + gridDim.z - 1) / gridDim.z;
+  const int ch_lo = blockIdx.z * per, nch = min(nch_all, ch_lo + per);
+  for (int ch = ch_lo + w; ch < nch; ch += KS) {
     const int64_t k0 = (int64_t)ch * 32;
     dbl2 fa[WM][4], fb[WN][4];
 #pragma unroll
@@ -65,20 +67,21 @@ __global__ void __launch_bounds__(64 * KS) k_mm(const double* __restrict__ S, co
           acc[a][b] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc[a][b], 0, 0, 0);
         }
   }
-  if (KS > 1) {
-    __shared__ dbl4 red[KS > 1 ? KS - 1 : 1][WM][WN][64];
-    if (w > 0)
+  if (KS > 1) {  // waves 1..KS-1 accumulate in turn into one LDS slab, wave 0 adds it last
+    __shared__ dbl4 red[WM][WN][64];
+    for (int s = 1; s < KS; ++s) {
+      if (w == s)
 #pragma unroll
-      for (int a = 0; a < WM; ++a)
+        for (int a = 0; a < WM; ++a)
 #pragma unroll
-        for (int b = 0; b < WN; ++b) red[w - 1][a][b][lane] = acc[a][b];
-    __syncthreads();
+          for (int b = 0; b < WN; ++b) red[a][b][lane] = s == 1 ? acc[a][b] : red[a][b][lane] + acc[a][b];
+      __syncthreads();
+    }
     if (w != 0) return;
-    for (int s = 0; s < KS - 1; ++s)
 #pragma unroll
-      for (int a = 0; a < WM; ++a)
+    for (int a = 0; a < WM; ++a)
 #pragma unroll
-        for (int b = 0; b < WN; ++b) acc[a][b] += red[s][a][b][lane];
+      for (int b = 0; b < WN; ++b) acc[a][b] += red[a][b][lane];
   }
   // D layout (f64): col = lane & 15 (-> i), row = (lane >> 4) + 4 * reg (-> c)
 #pragma unroll
@@ -94,15 +97,42 @@ __global__ void __launch_bounds__(64 * KS) k_mm(const double* __restrict__ S, co
     }
 }
 
+// sum of KZ partial slabs in fixed order into slab 0
+__global__ void k_red(double* Y, int64_t slab, int kz) {
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e >= slab) return;
+  double s = Y[e];
+  for (int z = 1; z < kz; ++z) s += Y[(int64_t)z * slab + e];
+  Y[e] = s;
+}
+
+// f64 MFMA issue-rate probe: independent accumulator chains, no memory
+template <int NACC>
+__global__ void k_peak(double* out, int iters) {
+  dbl4 acc[NACC];
+  for (int a = 0; a < NACC; ++a) acc[a] = dbl4{0.0, 0.0, 0.0, 0.0};
+  double x = threadIdx.x * 1e-3, y = 1.0 + threadIdx.x * 1e-4;
+  for (int it = 0; it < iters; ++it)
+#pragma unroll
+    for (int a = 0; a < NACC; ++a) acc[a] = __builtin_amdgcn_mfma_f64_16x16x4f64(x, y, acc[a], 0, 0, 0);
+  double s = 0;
+  for (int a = 0; a < NACC; ++a) s += acc[a][0] + acc[a][1] + acc[a][2] + acc[a][3];
+  if (s == 12345.678) out[0] = s;
+}
+
 struct Variant {
   std::string name;
   void (*launch)(const double*, const double*, double*, int, int, int64_t, int, hipStream_t);
 };
 
-template <int WM, int WN, int KS>
+template <int WM, int WN, int KS, int KZ = 1>
 void launch_mm(const double* S, const double* V, double* Y, int n, int rows, int64_t ld, int C, hipStream_t st) {
-  dim3 grid((rows + 16 * WN - 1) / (16 * WN), (C + 16 * WM - 1) / (16 * WM));
+  dim3 grid((rows + 16 * WN - 1) / (16 * WN), (C + 16 * WM - 1) / (16 * WM), KZ);
   hipLaunchKernelGGL((k_mm<WM, WN, KS>), grid, dim3(64 * KS), 0, st, S, V, Y, n, rows, ld, C);
+  if (KZ > 1) {
+    const int64_t slab = (int64_t)C * ld;
+    hipLaunchKernelGGL(k_red, dim3((unsigned)((slab + 255) / 256)), dim3(256), 0, st, Y, slab, KZ);
+  }
 }
 
 int main(int argc, char** argv) {
@@ -130,14 +160,35 @@ int main(int argc, char** argv) {
   double *S, *V, *Y;
   CHK(hipMalloc(&S, hS.size() * 8));
   CHK(hipMalloc(&V, hV.size() * 8));
-  CHK(hipMalloc(&Y, (size_t)C * ld * 8));
+  CHK(hipMalloc(&Y, (size_t)4 * C * ld * 8));
+  {
+    hipEvent_t a, b;
+    CHK(hipEventCreate(&a));
+    CHK(hipEventCreate(&b));
+    for (int waves : {1024, 2048, 4096}) {
+      const int iters = 4000;
+      hipLaunchKernelGGL(k_peak<4>, dim3(waves / 4), dim3(256), 0, 0, Y, 10);
+      CHK(hipEventRecord(a, 0));
+      hipLaunchKernelGGL(k_peak<4>, dim3(waves / 4), dim3(256), 0, 0, Y, iters);
+      CHK(hipEventRecord(b, 0));
+      CHK(hipEventSynchronize(b));
+      float ms = 0;
+      CHK(hipEventElapsedTime(&ms, a, b));
+      const double fl = (double)waves * iters * 4 * 2048.0;
+      printf("{\"variant\": \"mfma_f64_16x16x4 peak probe\", \"waves\": %d, \"TFLOPs\": %.2f}\n", waves, fl / (ms * 1e-3) / 1e12);
+    }
+  }
   CHK(hipMemcpy(S, hS.data(), hS.size() * 8, hipMemcpyHostToDevice));
   CHK(hipMemcpy(V, hV.data(), hV.size() * 8, hipMemcpyHostToDevice));
   std::vector<Variant> vs = {
-      {"wm2 wn2 ks4", launch_mm<2, 2, 4>}, {"wm2 wn2 ks2", launch_mm<2, 2, 2>}, {"wm2 wn2 ks8", launch_mm<2, 2, 8>},
-      {"wm2 wn4 ks4", launch_mm<2, 4, 4>}, {"wm4 wn2 ks4", launch_mm<4, 2, 4>}, {"wm4 wn4 ks4", launch_mm<4, 4, 4>},
-      {"wm1 wn4 ks4", launch_mm<1, 4, 4>}, {"wm2 wn1 ks4", launch_mm<2, 1, 4>}, {"wm4 wn4 ks2", launch_mm<4, 4, 2>},
-      {"wm8 wn2 ks4", launch_mm<8, 2, 4>}, {"wm2 wn8 ks4", launch_mm<2, 8, 4>},
+      {"wm8 wn2 ks4", launch_mm<8, 2, 4>},      {"wm8 wn2 ks8", launch_mm<8, 2, 8>},
+      {"wm8 wn2 ks16", launch_mm<8, 2, 16>},    {"wm4 wn4 ks8", launch_mm<4, 4, 8>},
+      {"wm4 wn4 ks16", launch_mm<4, 4, 16>},    {"wm4 wn2 ks8", launch_mm<4, 2, 8>},
+      {"wm4 wn2 ks16", launch_mm<4, 2, 16>},    {"wm2 wn2 ks16", launch_mm<2, 2, 16>},
+      {"wm8 wn2 ks4 kz4", launch_mm<8, 2, 4, 4>}, {"wm8 wn2 ks8 kz2", launch_mm<8, 2, 8, 2>},
+      {"wm4 wn4 ks4 kz4", launch_mm<4, 4, 4, 4>}, {"wm4 wn2 ks4 kz4", launch_mm<4, 2, 4, 4>},
+      {"wm2 wn1 ks4 kz4", launch_mm<2, 1, 4, 4>}, {"wm2 wn1 ks8", launch_mm<2, 1, 8>},
+      {"wm2 wn2 ks8 kz2", launch_mm<2, 2, 8, 2>}, {"wm1 wn2 ks8", launch_mm<1, 2, 8>},
   };
   hipEvent_t e0, e1;
   CHK(hipEventCreate(&e0));
