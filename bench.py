@@ -91,6 +91,8 @@ def main():
     ap.add_argument("--batch", type=int, default=128, help="instances per GPU")
     ap.add_argument("--cpu-budget", type=float, default=25.0, help="seconds of CPU-baseline sampling (0 = skip)")
     ap.add_argument("--seed0", type=int, default=20251212)
+    ap.add_argument("--stream-groups", type=int, default=0, choices=[0, 1, 2],
+                    help="instance groups on separate streams (0 = library default)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_gemv.json"))
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend (nccl = RCCL)")
     ap.add_argument("--same-device", action="store_true",
@@ -120,7 +122,7 @@ def main():
     from problems import manviofun
 
     n, B, W, K = args.dim, args.batch, args.warmup, args.steps
-    eng = engine.NonnegPCABatch(n, B, log_capacity=2048, layout=args.layout)
+    eng = engine.NonnegPCABatch(n, B, log_capacity=2048, layout=args.layout, stream_groups=args.stream_groups)
     nS = 1 if args.layout == "shared" else B
     log(f"rank {rank}/{world}: generating {B} instances n={n} ({nS * eng.inst_stride * 8 / 1e9:.1f} GB S)")
     # global instance ids owned by this rank: rank, rank+world, ... (seed seed0 + id)

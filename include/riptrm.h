@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define RIPTRM_ABI_VERSION 1
+#define RIPTRM_ABI_VERSION 2
 
 /* status codes */
 #define RIPTRM_OK 0
@@ -79,6 +79,8 @@ extern "C" {
 /* manifold-violation kinds for the KKT residual (option 'manviofun') */
 #define RIPTRM_MANVIO_ZERO 0     /* RIPTRM.py:347 default: lambda problem, x: 0 */
 #define RIPTRM_MANVIO_SPHERE 1   /* src/NonnegPCA/simulator.py:12-14: ||x|| - 1 */
+#define RIPTRM_MANVIO_SI 2       /* src/StableIdentification/simulator.py:11-32: ||J+J^T|| + ||R-R^T||
+                                  * + ||Q-Q^T||, inf when R or Q is not positive definite */
 
 /* Per-inner-iteration log record: RIPTRM_LOG_NFIELDS doubles, field order below.
  * Columns = evaluation keys (utils.py:356-364) + solver_status keys (RIPTRM.py:986-1023). */
@@ -208,6 +210,53 @@ int riptrm_profile_enable(riptrm_ctx* ctx, int32_t on);
 /* Summed device time (ms) and launch counts since the last enable.  Synchronises. */
 int riptrm_profile_read(riptrm_ctx* ctx, double* gemv_ms, int64_t* gemv_launches, double* state_ms,
                         int64_t* state_launches);
+
+/* ==== StableIdentification (src/StableIdentification/coordinator.py:13-152) ====================
+ * M = SkewSymmetric(d) x SPD(d) x SPD(d) (pymanopt Product, :38-44), points (J, R, Q) stored as
+ * 3 consecutive row-major d x d blocks; f = tr(E E^T)/N, E = XP - (I + h (J-R) Q) X (:92-98);
+ * m inequality constraints on entries of A = (J-R)Q (:102-152), one row of RIPTRM_SI_CONS_FIELDS
+ * doubles each: kind (0: -A_rc + p0, 1: A_rc - p0, 2: -(A_rc - p0)^2 + p1), r, c, p0, p1 — the
+ * reference's constset rows expanded in order (type 0/1 -> kinds 0 then 1; type 2 -> kind 2 with
+ * p1 = k^2).  One 64-lane workgroup runs one instance's whole RIPTRM solve in one launch. */
+#define RIPTRM_SI_DMAX 8
+#define RIPTRM_SI_MMAX 64
+#define RIPTRM_SI_CONS_FIELDS 5
+
+typedef struct riptrm_si_problem {
+    int32_t struct_size;     /* = sizeof(riptrm_si_problem) */
+    int32_t d;               /* 1 <= d <= RIPTRM_SI_DMAX */
+    int32_t N;               /* columns of X / XP (coordinator.py:54-90) */
+    int32_t m;               /* 1 <= m <= RIPTRM_SI_MMAX */
+    double h;                /* cfg.h */
+    const double* X;         /* device, d x N row-major */
+    const double* XP;        /* device, d x N row-major */
+    int64_t data_stride;     /* doubles between instances' X (and XP); 0 = one problem, many starts */
+    const double* cons;      /* device, m x RIPTRM_SI_CONS_FIELDS */
+    int64_t cons_stride;     /* doubles between instances' constraint tables; 0 = shared */
+} riptrm_si_problem;
+
+/* Workspace for a batch: points, multipliers, tCG outputs, residual scratch, stats and log. */
+int64_t riptrm_si_workspace_bytes(int32_t d, int32_t N, int32_t m, int32_t batch, int32_t log_capacity);
+/* kind: 0 = x (batch x 3 d d), 1 = y (batch x m), 2 = eta, 3 = Heta (batch x 3 d d),
+ * 4 = stats (batch x RIPTRM_STAT_NFIELDS), 5 = log (batch x capacity x RIPTRM_LOG_NFIELDS). */
+int64_t riptrm_si_workspace_offset(int32_t d, int32_t N, int32_t m, int32_t batch, int32_t log_capacity,
+                                   int32_t kind);
+/* Bind a batch of StableIdentification instances (the problem_initialpoint / instance axes). */
+int riptrm_si_bind(riptrm_ctx* ctx, const riptrm_si_problem* problem, int32_t batch, void* workspace,
+                   int64_t workspace_bytes, int32_t log_capacity);
+/* out_b = HwCur_b(v_b) (RIPTRM.py:729) at (x_b, y_b, mu_b).  x, v, out: batch x 3 d d; y: batch x m;
+ * mu: batch doubles.  Asynchronous. */
+int riptrm_si_hvp(riptrm_ctx* ctx, const double* x, const double* y, const double* mu, const double* v,
+                  double* out);
+/* tCG (RIPTRM.py:41-216) at (x_b, y_b, mu_b, Delta_b): eta / Heta into the workspace (kinds 2/3),
+ * stats TCG_LAST_J / TCG_LAST_STOP.  tCG options from opt (NULL = RIPTRM defaults).  Asynchronous. */
+int riptrm_si_tcg(riptrm_ctx* ctx, const riptrm_options* opt, const double* x, const double* y,
+                  const double* mu, const double* delta);
+/* Whole RIPTRM solves (RIPTRM.py:909-976) from x0 (batch x 3 d d), y0 (batch x m); tables as in
+ * riptrm_solve_begin.  One launch, asynchronous: synchronise the stream, then read the workspace. */
+int riptrm_si_solve(riptrm_ctx* ctx, const riptrm_options* opt, const double* x0, const double* y0,
+                    const double* mu_table, const double* tolL_table, const double* tolC_table,
+                    int32_t table_len);
 
 #ifdef __cplusplus
 }

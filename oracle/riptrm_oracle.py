@@ -583,7 +583,7 @@ class RIPTRMOracle:
         dy = P.dy(x, y, s, mu, dx)
         xNew = M.retraction(x, dx)
         yNew = y + dy
-        if np.all(xNew > 0):
+        if getattr(P, "gpu_pass_accounting", True) and np.all(xNew > 0):
             self.passes += 1   # GPU: one fused pass computes S.dx (pred) and S.x_new
         cr = self.inner_criteria(P, xNew, yNew, mu, inner_option)
         info["minxfeasi"] = cr["minxfeasi"]

@@ -7,10 +7,12 @@ eqLagmult)`` whose ``log`` has the reference's columns, one row per inner iterat
 (``RIPTRM.py:812-818``).  Differences, all explicit errors rather than silent fallbacks:
 
 * only ``TRS_solver='tCG'`` (what every shipped config selects) — ``Exact_RepMat`` raises;
-* the problem is a structured descriptor (``problems.NonnegPCAProblem``) instead of a list of
-  autograd closures, because closures cannot execute on the GPU;
-* ``manviofun`` must be 0 or the NonnegPCA simulator's ``||x|| - 1``; ``callbackfun`` and
-  wandb are not supported.
+* the problem is a structured descriptor (``problems.NonnegPCAProblem`` or
+  ``si.SIProblem`` for StableIdentification) instead of a list of autograd closures, because
+  closures cannot execute on the GPU;
+* ``manviofun`` must be 0 or the problem's simulator function (NonnegPCA ``||x|| - 1``,
+  StableIdentification's symmetry / definiteness violation); ``callbackfun`` and wandb are not
+  supported.
 
 ``run_batch(problems)`` solves many instances of the same size at once (the reference runs its
 Hydra multi-run axis one after another, ``config_simulation.yaml:35-42``).
@@ -24,9 +26,17 @@ from typing import Any, Dict, List, Sequence
 import numpy as np
 import torch
 
-from engine import NonnegPCABatch, REFERENCE_DEFAULTS, resolve_options
+from engine import NonnegPCABatch, REFERENCE_DEFAULTS, manvio_kind, resolve_options
 from problems import NonnegPCAProblem
+from si import SIBatch, SIProblem, si_manvio_kind
 from solver_base import Output, Solver
+
+
+def _any_manvio_kind(f):
+    try:
+        return manvio_kind(f)
+    except Exception:
+        return si_manvio_kind(f)
 
 
 class RIPTRM(Solver):
@@ -40,7 +50,8 @@ class RIPTRM(Solver):
         self.log: Dict[str, list] = {}
         self.name = f"RIPTRM_{self.option['TRS_solver']}"
         self.initialize_wandb()
-        resolve_options(self.option, np.pi, 1)  # validate early (raises on unsupported options)
+        # validate early (raises on unsupported options)
+        resolve_options(self.option, np.pi, 1, manvio_classifier=_any_manvio_kind)
         self.last_batch = None
 
     def run(self, problem) -> Output:
@@ -50,6 +61,8 @@ class RIPTRM(Solver):
         problems = list(problems)
         if not problems:
             return []
+        if all(isinstance(p, SIProblem) for p in problems):
+            return self._run_batch_si(problems, log_capacity)
         for p in problems:
             if not isinstance(p, NonnegPCAProblem):
                 raise NotImplementedError(
@@ -72,9 +85,45 @@ class RIPTRM(Solver):
         y0 = np.stack([np.asarray(p.initialineqLagmult, dtype=np.float64) for p in problems])
         res = eng.solve(x0, y0, self.option)
         self.last_batch = res
-        outs = []
         xs = res.x.cpu().numpy()
         ys = res.y.cpu().numpy()
+        return self._outputs(res, [xs[b].copy() for b in range(B)], ys, log_capacity)
+
+    def _run_batch_si(self, problems: List[SIProblem], log_capacity: int) -> List[Output]:
+        """StableIdentification (src/StableIdentification/coordinator.py): one workgroup per
+        problem, every solve of the batch in one launch."""
+        p0 = problems[0]
+        d, N_, m = p0.d, p0.N, p0.m
+        if any((p.d, p.N, p.m) != (d, N_, m) for p in problems):
+            raise ValueError("run_batch needs StableIdentification problems of equal (d, N, m)")
+        for p in problems:
+            if p.has_eqconstraints:
+                warnings.warn("Equality constraints detecred. Currently, RIPTRM does not support equality "
+                              "constraints and will completely ignore them.", Warning)
+        B = len(problems)
+        eng = SIBatch(d, N_, m, B, log_capacity=log_capacity)
+        same = all(p.X is p0.X or (np.array_equal(p.X, p0.X) and np.array_equal(p.XP, p0.XP)
+                                   and np.array_equal(p.cons, p0.cons) and p.h == p0.h) for p in problems)
+        if same:   # the problem_initialpoint axis: one data set, many starts
+            eng.load(p0.X, p0.XP, p0.h, p0.cons)
+        else:
+            if any(p.h != p0.h for p in problems):
+                raise ValueError("run_batch needs one h per batch")
+            eng.load(np.stack([p.X for p in problems]), np.stack([p.XP for p in problems]), p0.h,
+                     np.stack([p.cons for p in problems]))
+        self.last_layout = "si-shared" if same else "si"
+        x0 = np.stack([p.point_array() for p in problems])
+        y0 = np.stack([np.asarray(p.initialineqLagmult, dtype=np.float64) for p in problems])
+        res = eng.solve(x0, y0, self.option)
+        self.last_batch = res
+        xs = res.x.cpu().numpy()
+        ys = res.y.cpu().numpy()
+        return self._outputs(res, [[xs[b, 0].copy(), xs[b, 1].copy(), xs[b, 2].copy()] for b in range(B)], ys,
+                             log_capacity)
+
+    def _outputs(self, res, xs, ys, log_capacity) -> List[Output]:
+        outs = []
+        B = len(xs)
         for b in range(B):
             opt = copy.copy(self.option)
             reason = res.stopping_criterion(b)
@@ -90,7 +139,7 @@ class RIPTRM(Solver):
                         print(f"Outer iteration: {it}, Cost: {c}, KKT residual: {r}, mu: {m}")
                 if reason:
                     print(reason)
-            outs.append(Output(name=self.name, x=xs[b].copy(), option=opt, log=log,
+            outs.append(Output(name=self.name, x=xs[b], option=opt, log=log,
                                ineqLagmult=ys[b].copy(), eqLagmult=[]))
         self.log = outs[0].log if B == 1 else {}
         return outs

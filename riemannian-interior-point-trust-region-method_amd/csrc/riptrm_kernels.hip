@@ -16,6 +16,7 @@
 #include <cstring>
 #include <cstdio>
 #include "riptrm_device.h"
+#include "riptrm_ctx.h"
 
 namespace riptrm {
 
@@ -1359,36 +1360,6 @@ __global__ void __launch_bounds__(ST_THREADS) k_hvp_epi(DevParams P, double mu, 
 // ==========================================================================================
 using namespace riptrm;
 
-struct riptrm_ctx {
-  int device = 0;
-  hipStream_t stream = nullptr;
-  std::string err;
-  bool bound = false, solving = false;
-  Layout L{};
-  const double* S = nullptr;
-  int64_t inst_stride = 0;
-  char* ws = nullptr;
-  DevParams P{};
-  // two instance groups with independent lock-step pipelines on two streams: one group's
-  // latency-bound state kernel overlaps the other group's HBM-bound S-pass
-  int ngroups = 1;
-  int groups_req = 0;  // riptrm_set_stream_groups: 0 = automatic
-  int gbase[2] = {0, 0}, gsize[2] = {0, 0};
-  int parity[2] = {0, 0};        // list written by the group's last state kernel
-  int active_bound[2] = {0, 0};  // upper bound of the group's active instances
-  hipStream_t gstream[2] = {nullptr, nullptr};
-  hipStream_t own_stream = nullptr;  // created for group 1
-  hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_pass[2] = {nullptr, nullptr};
-  double clock_hz = 1e8;
-  // optional HIP-event timing of every k_gemv / k_state launch (riptrm_profile_*)
-  bool prof = false;
-  std::vector<hipEvent_t> ev_pool;
-  std::vector<std::pair<int, int>> ev_gemv, ev_state;  // (start, end) indices into ev_pool
-  int ev_used = 0;
-  double gemv_ms = 0.0, state_ms = 0.0;
-  int64_t gemv_n = 0, state_n = 0;
-};
-
 static hipEvent_t prof_event(riptrm_ctx* c, int* idx) {
   if (c->ev_used == (int)c->ev_pool.size()) {
     hipEvent_t e;
@@ -1415,17 +1386,6 @@ static void prof_collect(riptrm_ctx* c) {
   c->ev_state.clear();
   c->ev_used = 0;
 }
-
-static int fail(riptrm_ctx* c, int code, const std::string& msg) {
-  if (c) c->err = msg;
-  return code;
-}
-
-#define HIPCHK(c, expr)                                                                    \
-  do {                                                                                     \
-    hipError_t e_ = (expr);                                                                \
-    if (e_ != hipSuccess) return fail((c), RIPTRM_E_HIP, std::string(#expr ": ") + hipGetErrorString(e_)); \
-  } while (0)
 
 extern "C" {
 
@@ -1460,6 +1420,7 @@ int riptrm_ctx_create(riptrm_ctx** out, int device, void* stream) {
 
 int riptrm_ctx_destroy(riptrm_ctx* ctx) {
   if (ctx) {
+    if (ctx->si) riptrm_si_release(ctx->si);
     for (auto e : ctx->ev_pool) (void)hipEventDestroy(e);
     for (auto e : {ctx->ev_fork, ctx->ev_join, ctx->ev_pass[0], ctx->ev_pass[1]})
       if (e) (void)hipEventDestroy(e);

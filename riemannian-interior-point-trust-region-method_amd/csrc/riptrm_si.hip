@@ -1,0 +1,1089 @@
+// riptrm_si.hip — RIPTRM (tCG path) for StableIdentification on MI355X (gfx950).
+//
+// Problem (src/StableIdentification/coordinator.py:13-152): Product(SkewSymmetric(d), SPD(d),
+// SPD(d)) with f(J,R,Q) = tr(E E^T)/N, E = XP - (I + h A) X, A = (J-R)Q, and m box constraints on
+// entries of A.  Everything is d x d (d <= 8, the fixture has d = 5, m = 16, N = 95), so one
+// 64-lane workgroup runs one instance's WHOLE solve in one launch: lane l < d*d owns element
+// (l / d, l % d) of every d x d block; products go through LDS (one staging write + d reads per
+// operand), inner products / norms are wave butterflies, Cholesky / Jacobi eigenvalues for the
+// evaluation (dist, manifold violation) run serially on lane 0.  No S-pass, no host round trip.
+//
+// Math = oracle/si_oracle.py::SIVectorized (the Lagrangian aggregated through dL/dA), i.e.
+//   HessL[v]  = e2rh(x, chain(G_L), chain_hess(G_L, dG_L, v), v)        RIPTRM.py:491-523
+//   Gx(w)     = -e2rg(x, chain(sum_i w_i dg_i/dA))                        RIPTRM.py:525-551
+//   Gxaj(v)_i = -(dg_i/dA) : dA(v)                                        RIPTRM.py:553-571
+// with pymanopt's SPD (affine-invariant) and SkewSymmetric formulas restated.
+// Control flow = RIPTRM.py:41-216 (tCG), :574-629, :631-705, :707-896, :909-976 — the same as
+// the NonnegPCA state machine in riptrm_kernels.hip, written as plain loops.
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <cstring>
+#include <string>
+#include "riptrm_ctx.h"
+
+namespace riptrm_si {
+
+#pragma clang fp contract(off)
+
+constexpr int W = 64;
+constexpr int DMAX = RIPTRM_SI_DMAX;
+constexpr int MMAX = RIPTRM_SI_MMAX;
+constexpr int CF = RIPTRM_SI_CONS_FIELDS;
+
+enum Mode : int { MODE_SOLVE = 0, MODE_HVP = 1, MODE_TCG = 2 };
+
+struct SIParams {
+  int32_t d, N, m, batch, cap, mode, tab_len, pad;
+  double h, clock_hz;
+  const double* X;
+  const double* XP;
+  int64_t data_stride;
+  const double* cons;
+  int64_t cons_stride;
+  double* x;       // batch x 3dd   current point / result
+  double* y;       // batch x m
+  double* eta;     // batch x 3dd
+  double* heta;    // batch x 3dd
+  double* escr;    // batch x d x N residual scratch
+  double* stats;   // batch x RIPTRM_STAT_NFIELDS
+  double* log;     // batch x cap x RIPTRM_LOG_NFIELDS
+  const double* in_x;
+  const double* in_y;
+  const double* in_mu;
+  const double* in_delta;
+  const double* in_v;
+  double* out_v;
+  const double* mu_tab;
+  const double* tolL_tab;
+  const double* tolC_tab;
+  riptrm_options opt;
+};
+
+struct Layout {
+  int64_t off_x, off_y, off_eta, off_heta, off_escr, off_stats, off_log, total;
+};
+
+inline int64_t rup(int64_t a, int64_t m) { return (a + m - 1) / m * m; }
+
+inline Layout make_layout(int d, int N, int m, int batch, int cap) {
+  Layout L;
+  const int64_t v3 = 3LL * d * d;
+  int64_t o = 0;
+  L.off_x = o;     o = rup(o + 8 * batch * v3, 256);
+  L.off_y = o;     o = rup(o + 8LL * batch * m, 256);
+  L.off_eta = o;   o = rup(o + 8 * batch * v3, 256);
+  L.off_heta = o;  o = rup(o + 8 * batch * v3, 256);
+  L.off_escr = o;  o = rup(o + 8LL * batch * d * N, 256);
+  L.off_stats = o; o = rup(o + 8LL * batch * RIPTRM_STAT_NFIELDS, 256);
+  L.off_log = o;   o = rup(o + 8LL * batch * cap * RIPTRM_LOG_NFIELDS, 256);
+  L.total = o;
+  return L;
+}
+
+// numpy.minimum / numpy.maximum (NaN-propagating), RIPTRM.py:681-683
+__device__ __forceinline__ double np_min(double a, double b) { return (isnan(a) || isnan(b)) ? NAN : (b < a ? b : a); }
+__device__ __forceinline__ double np_max(double a, double b) { return (isnan(a) || isnan(b)) ? NAN : (b > a ? b : a); }
+
+// value of v on lane src.  A wave op: call it on every lane (never inside a lane-dependent
+// branch or ?:), inactive source lanes read as 0.
+__device__ __forceinline__ double lane_read(double v, int src) {
+  const int addr = src << 2;
+  const int lo = __builtin_amdgcn_ds_bpermute(addr, __double2loint(v));
+  const int hi = __builtin_amdgcn_ds_bpermute(addr, __double2hiint(v));
+  return __hiloint2double(hi, lo);
+}
+
+__device__ __forceinline__ double wsum(double v) {
+  const int l = (int)__lane_id();
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v = v + lane_read(v, l ^ off);
+  return v;
+}
+__device__ __forceinline__ double wmin(double v) {
+  const int l = (int)__lane_id();
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v = fmin(v, lane_read(v, l ^ off));
+  return v;
+}
+__device__ __forceinline__ double wmax(double v) {
+  const int l = (int)__lane_id();
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v = fmax(v, lane_read(v, l ^ off));
+  return v;
+}
+
+// a point / tangent vector of the product: this lane's element of J, R and Q
+struct PV {
+  double j, r, q;
+};
+__device__ __forceinline__ PV pv_add(PV a, PV b) { return PV{a.j + b.j, a.r + b.r, a.q + b.q}; }
+__device__ __forceinline__ PV pv_sub(PV a, PV b) { return PV{a.j - b.j, a.r - b.r, a.q - b.q}; }
+__device__ __forceinline__ PV pv_scale(double s, PV a) { return PV{s * a.j, s * a.r, s * a.q}; }
+__device__ __forceinline__ PV pv_neg(PV a) { return PV{-a.j, -a.r, -a.q}; }
+
+struct Info {  // inner-iteration record of solver_status (RIPTRM.py:986-1023)
+  double has, num, status, tr, dxtype, normdx, minx, miny, compl_, hasratio, ratio, ru, dc;
+};
+
+struct Eng {
+  const SIParams& P;
+  const int b, l, d, dd, m, N;
+  const int li, lj;
+  const bool act, cact;
+  double* sh;      // LDS staging: 2 x 64 doubles
+  double* ser;     // LDS serial scratch: 4 x 64 doubles (lane 0 only)
+  int* cr_s;       // LDS constraint rows / cols / kinds
+  int* cc_s;
+  // constraint of this lane (l < m)
+  int ck, cr, cc;
+  double cp0, cp1;
+  double M2;       // (X X^T)_{li,lj}
+  const double* Xd;
+  const double* XPd;
+  double* E;
+
+  __device__ Eng(const SIParams& P_, int b_, double* sh_, double* ser_, int* crs, int* ccs)
+      : P(P_), b(b_), l((int)threadIdx.x), d(P_.d), dd(P_.d * P_.d), m(P_.m), N(P_.N),
+        li((int)threadIdx.x / P_.d), lj((int)threadIdx.x % P_.d), act((int)threadIdx.x < P_.d * P_.d),
+        cact((int)threadIdx.x < P_.m), sh(sh_), ser(ser_), cr_s(crs), cc_s(ccs) {
+    Xd = P.X + (int64_t)b * P.data_stride;
+    XPd = P.XP + (int64_t)b * P.data_stride;
+    E = P.escr + (int64_t)b * d * N;
+    const double* cs = P.cons + (int64_t)b * P.cons_stride;
+    ck = 0; cr = 0; cc = 0; cp0 = 0.0; cp1 = 0.0;
+    if (cact) {
+      ck = (int)cs[l * CF + 0];
+      cr = (int)cs[l * CF + 1];
+      cc = (int)cs[l * CF + 2];
+      cp0 = cs[l * CF + 3];
+      cp1 = cs[l * CF + 4];
+      cr_s[l] = cr;
+      cc_s[l] = cc;
+    }
+    // X X^T (f's Hessian, coordinator.py:92-98)
+    double acc = 0.0;
+    if (act)
+      for (int t = 0; t < N; ++t) acc = acc + Xd[li * N + t] * Xd[lj * N + t];
+    M2 = acc;
+    __syncthreads();
+  }
+
+  // ---- d x d block primitives (one element per lane) ---------------------------------------
+  __device__ __forceinline__ double tr(double a) {
+    sh[l] = a;
+    __syncthreads();
+    const double v = act ? sh[lj * d + li] : 0.0;
+    __syncthreads();
+    return v;
+  }
+  // op(a) op(b), ta / tb transpose the operand
+  __device__ __forceinline__ double mm(double a, double b, bool ta = false, bool tb = false) {
+    sh[l] = a;
+    sh[W + l] = b;
+    __syncthreads();
+    double acc = 0.0;
+    if (act) {
+      for (int k = 0; k < d; ++k) {
+        const double av = ta ? sh[k * d + li] : sh[li * d + k];
+        const double bv = tb ? sh[W + lj * d + k] : sh[W + k * d + lj];
+        acc = acc + av * bv;
+      }
+    }
+    __syncthreads();
+    return acc;
+  }
+  __device__ __forceinline__ double sym(double a) { return 0.5 * (a + tr(a)); }
+  __device__ __forceinline__ double skew(double a) { return 0.5 * (a - tr(a)); }
+  __device__ __forceinline__ double elem(double a, int i, int j) { return lane_read(a, i * d + j); }
+
+  // inverse by Gauss-Jordan with partial pivoting (numpy.linalg.solve / inv analogue)
+  __device__ double inv(double a) {
+    double* g = ser;  // d x 2d augmented, row-major
+    if (act) {
+      g[li * 2 * d + lj] = a;
+      g[li * 2 * d + d + lj] = (li == lj) ? 1.0 : 0.0;
+    }
+    __syncthreads();
+    if (l == 0) {
+      for (int k = 0; k < d; ++k) {
+        int p = k;
+        double best = fabs(g[k * 2 * d + k]);
+        for (int r = k + 1; r < d; ++r) {
+          const double v = fabs(g[r * 2 * d + k]);
+          if (v > best) { best = v; p = r; }
+        }
+        if (p != k)
+          for (int c = 0; c < 2 * d; ++c) {
+            const double t = g[k * 2 * d + c];
+            g[k * 2 * d + c] = g[p * 2 * d + c];
+            g[p * 2 * d + c] = t;
+          }
+        const double piv = g[k * 2 * d + k];
+        for (int c = 0; c < 2 * d; ++c) g[k * 2 * d + c] = g[k * 2 * d + c] / piv;
+        for (int r = 0; r < d; ++r) {
+          if (r == k) continue;
+          const double f = g[r * 2 * d + k];
+          if (f != 0.0)
+            for (int c = 0; c < 2 * d; ++c) g[r * 2 * d + c] = g[r * 2 * d + c] - f * g[k * 2 * d + c];
+        }
+      }
+    }
+    __syncthreads();
+    const double v = act ? g[li * 2 * d + d + lj] : 0.0;
+    __syncthreads();
+    return v;
+  }
+
+  // eigenvalues of a symmetric d x d matrix (cyclic Jacobi on lane 0); result in ser[3*W + i]
+  __device__ void eigvalsh_lane0(double* a) {
+    for (int sweep = 0; sweep < 60; ++sweep) {
+      double off = 0.0, dg = 0.0;
+      for (int p = 0; p < d; ++p) {
+        dg += a[p * d + p] * a[p * d + p];
+        for (int q = p + 1; q < d; ++q) off += a[p * d + q] * a[p * d + q];
+      }
+      if (off <= 1e-36 * dg) break;   // converged to far below the eigenvalues' rounding
+      for (int p = 0; p < d; ++p)
+        for (int q = p + 1; q < d; ++q) {
+          const double apq = a[p * d + q];
+          if (apq == 0.0) continue;
+          const double app = a[p * d + p], aqq = a[q * d + q];
+          const double theta = (aqq - app) / (2.0 * apq);
+          const double t = (theta >= 0.0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
+          const double c = 1.0 / sqrt(t * t + 1.0), s = t * c;
+          for (int k = 0; k < d; ++k) {
+            const double akp = a[k * d + p], akq = a[k * d + q];
+            a[k * d + p] = c * akp - s * akq;
+            a[k * d + q] = s * akp + c * akq;
+          }
+          for (int k = 0; k < d; ++k) {
+            const double apk = a[p * d + k], aqk = a[q * d + k];
+            a[p * d + k] = c * apk - s * aqk;
+            a[q * d + k] = s * apk + c * aqk;
+          }
+        }
+    }
+  }
+
+  // ||logm(chol(a)^-1 b chol(a)^-T)||_F (pymanopt SPD dist), all lanes get the value
+  __device__ double spd_dist(double a, double bm) {
+    double* A = ser;
+    double* B = ser + W;
+    double* Cm = ser + 2 * W;
+    if (act) { A[l] = a; B[l] = bm; }
+    __syncthreads();
+    if (l == 0) {
+      // Cholesky a = C C^T (lower)
+      for (int i = 0; i < d * d; ++i) Cm[i] = 0.0;
+      bool ok = true;
+      for (int j = 0; j < d && ok; ++j) {
+        double s = A[j * d + j];
+        for (int k = 0; k < j; ++k) s -= Cm[j * d + k] * Cm[j * d + k];
+        if (!(s > 0.0)) { ok = false; break; }
+        const double cjj = sqrt(s);
+        Cm[j * d + j] = cjj;
+        for (int i = j + 1; i < d; ++i) {
+          double t = A[i * d + j];
+          for (int k = 0; k < j; ++k) t -= Cm[i * d + k] * Cm[j * d + k];
+          Cm[i * d + j] = t / cjj;
+        }
+      }
+      double res = NAN;
+      if (ok) {
+        // Ci = C^-1 (lower), stored in A
+        for (int i = 0; i < d * d; ++i) A[i] = 0.0;
+        for (int j = 0; j < d; ++j) {
+          A[j * d + j] = 1.0 / Cm[j * d + j];
+          for (int i = j + 1; i < d; ++i) {
+            double t = 0.0;
+            for (int k = j; k < i; ++k) t -= Cm[i * d + k] * A[k * d + j];
+            A[i * d + j] = t / Cm[i * d + i];
+          }
+        }
+        // M = Ci B Ci^T into Cm, symmetrised
+        for (int i = 0; i < d; ++i)
+          for (int j = 0; j < d; ++j) {
+            double t = 0.0;
+            for (int k = 0; k < d; ++k) {
+              double u = 0.0;
+              for (int q = 0; q < d; ++q) u += B[k * d + q] * A[j * d + q];
+              t += A[i * d + k] * u;
+            }
+            Cm[i * d + j] = t;
+          }
+        for (int i = 0; i < d; ++i)
+          for (int j = i + 1; j < d; ++j) {
+            const double s = 0.5 * (Cm[i * d + j] + Cm[j * d + i]);
+            Cm[i * d + j] = s;
+            Cm[j * d + i] = s;
+          }
+        eigvalsh_lane0(Cm);
+        double s2 = 0.0;
+        for (int i = 0; i < d; ++i) {
+          const double lg = log(Cm[i * d + i]);
+          s2 += lg * lg;
+        }
+        res = sqrt(s2);
+      }
+      ser[3 * W] = res;
+    }
+    __syncthreads();
+    const double v = ser[3 * W];
+    __syncthreads();
+    return v;
+  }
+
+  // all eigenvalues of symmetric a positive? (numpy.linalg.eigvalsh(a) > 0 for every value)
+  __device__ bool spd_pd(double a) {
+    double* A = ser;
+    if (act) A[l] = a;
+    __syncthreads();
+    if (l == 0) {
+      // eigvalsh reads the lower triangle
+      for (int i = 0; i < d; ++i)
+        for (int j = i + 1; j < d; ++j) A[i * d + j] = A[j * d + i];
+      eigvalsh_lane0(A);
+      bool pd = true;
+      for (int i = 0; i < d; ++i) pd = pd && (A[i * d + i] > 0.0);
+      ser[3 * W] = pd ? 1.0 : 0.0;
+    }
+    __syncthreads();
+    const bool v = ser[3 * W] != 0.0;
+    __syncthreads();
+    return v;
+  }
+
+  // ---- manifold (pymanopt Product(SkewSymmetric, SPD, SPD)) ---------------------------------
+  struct Metric {
+    double XiR, XiQ;  // R^-1, Q^-1 at the base point
+  };
+  __device__ __forceinline__ Metric metric(PV x) { return Metric{inv(x.r), inv(x.q)}; }
+  __device__ __forceinline__ double spd_inner(double Xi, double u, double v) {
+    const double pu = mm(Xi, u);
+    const double pv = mm(Xi, v);
+    return wsum(pu * tr(pv));
+  }
+  __device__ __forceinline__ double inner(const Metric& g, PV u, PV v) {
+    const double a = wsum(u.j * v.j);
+    const double br = spd_inner(g.XiR, u.r, v.r);
+    const double bq = spd_inner(g.XiQ, u.q, v.q);
+    return ((0.0 + a) + br) + bq;
+  }
+  __device__ __forceinline__ double norm(const Metric& g, PV u) { return sqrt(inner(g, u, u)); }
+  __device__ __forceinline__ PV proj(PV u) { return PV{skew(u.j), sym(u.r), sym(u.q)}; }
+  // euclidean_to_riemannian_gradient: (skew(gJ), R sym(gR) R, Q sym(gQ) Q)
+  __device__ __forceinline__ PV e2rg(PV x, PV g) {
+    return PV{skew(g.j), mm(mm(x.r, sym(g.r)), x.r), mm(mm(x.q, sym(g.q)), x.q)};
+  }
+  // SPD retraction sym(X + U + U X^-1 U / 2); skew retraction X + U
+  __device__ __forceinline__ PV retract(PV x, const Metric& g, PV u) {
+    const double ur = mm(u.r, mm(g.XiR, u.r));
+    const double uq = mm(u.q, mm(g.XiQ, u.q));
+    return PV{x.j + u.j, sym((x.r + u.r) + ur / 2.0), sym((x.q + u.q) + uq / 2.0)};
+  }
+
+  // ---- problem ------------------------------------------------------------------------------
+  __device__ __forceinline__ double Aof(PV x) { return mm(x.j - x.r, x.q); }
+  // chain rule of phi(A(J,R,Q)) from G = dphi/dA
+  __device__ __forceinline__ PV chain(PV x, double G) {
+    const double gq = mm(G, x.q, false, true);
+    return PV{gq, -gq, mm(x.j - x.r, G, true, false)};
+  }
+  // constraint value g_k(x) on constraint lanes from A (this lane's element)
+  __device__ __forceinline__ double cons_val(double A) {
+    const double a = lane_read(A, cr * d + cc);
+    if (!cact) return 0.0;
+    return ck == 0 ? (-a + cp0) : (ck == 1 ? (a - cp0) : (-((a - cp0) * (a - cp0)) + cp1));
+  }
+  __device__ __forceinline__ double cons_w(double A) {
+    const double a = lane_read(A, cr * d + cc);
+    if (!cact) return 0.0;
+    return ck == 0 ? -1.0 : (ck == 1 ? 1.0 : -2.0 * (a - cp0));
+  }
+  // element lane (i,j) <- sum over constraints k with (r_k, c_k) = (i, j) of v_k, k ascending
+  __device__ __forceinline__ double scatter(double v) {
+    sh[l] = cact ? v : 0.0;
+    __syncthreads();
+    double acc = 0.0;
+    if (act)
+      for (int k = 0; k < m; ++k)
+        if (cr_s[k] == li && cc_s[k] == lj) acc = acc + sh[k];
+    __syncthreads();
+    return act ? acc : 0.0;
+  }
+  // f(x) and G_f = df/dA = -(2h/N) E X^T (E kept in the instance's scratch)
+  __device__ void cost_grad(double A, double& f, double& Gf) {
+    const double At = ((li == lj) ? 1.0 : 0.0) + P.h * A;
+    sh[l] = act ? At : 0.0;
+    __syncthreads();
+    double part = 0.0;
+    const int tot = d * N;
+    for (int e = l; e < tot; e += W) {
+      const int i = e / N, t = e - i * N;
+      double s = 0.0;
+      for (int k = 0; k < d; ++k) s = s + sh[i * d + k] * Xd[k * N + t];
+      const double ev = XPd[i * N + t] - s;
+      E[e] = ev;
+      part = part + ev * ev;
+    }
+    __syncthreads();
+    f = wsum(part) / (double)N;
+    double g = 0.0;
+    if (act)
+      for (int t = 0; t < N; ++t) g = g + E[li * N + t] * Xd[lj * N + t];
+    Gf = act ? -(2.0 * P.h / (double)N) * g : 0.0;
+    __syncthreads();
+  }
+
+  // everything HwCur / cxCur need at (x, y, mu): RIPTRM.py:720-730
+  struct AtX {
+    PV x;
+    Metric g;
+    double A, Gf, GL, sgR, sgQ, f;
+    double s, w, y;  // constraint lanes
+    PV c;            // cxCur
+  };
+  __device__ void prepare(AtX& a, PV x, double y, double mu) {
+    a.x = x;
+    a.y = y;
+    a.g = metric(x);
+    a.A = Aof(x);
+    cost_grad(a.A, a.f, a.Gf);
+    const double g0 = cons_val(a.A);   // wave op: evaluate on every lane, then select
+    a.s = cact ? -g0 : 1.0;
+    a.w = cons_w(a.A);
+    a.GL = a.Gf + scatter(y * a.w);
+    const PV cg = chain(x, a.GL);
+    a.sgR = sym(cg.r);
+    a.sgQ = sym(cg.q);
+    // c = rgrad f - Gx(mu / s);  Gx(v) = e2rg(chain(scatter(-(v w))))
+    const PV rgf = e2rg(x, chain(x, a.Gf));
+    const double q = cact ? (mu / a.s) : 0.0;
+    const PV gx = e2rg(x, chain(x, scatter(-(q * a.w))));
+    a.c = pv_sub(rgf, gx);
+  }
+  __device__ __forceinline__ double dAof(const AtX& a, PV v) {
+    return mm(v.j - v.r, a.x.q) + mm(a.x.j - a.x.r, v.q);
+  }
+  // Gxaj(v) on constraint lanes from dA(v)
+  __device__ __forceinline__ double gxaj(const AtX& a, double dA) {
+    const double da = lane_read(dA, cr * d + cc);
+    return cact ? -(a.w * da) : 0.0;
+  }
+  // HwCur(v) = HessL[v] + Gx(y Gxaj(v) / s)
+  __device__ PV hw(const AtX& a, PV v) {
+    const PV x = a.x;
+    const double dA = dAof(a, v);
+    double dG = (2.0 * P.h * P.h / (double)N) * mm(dA, M2);
+    {  // two-box second derivatives, constraint order
+      const double da = lane_read(dA, cr * d + cc);
+      const double t = (cact && ck == 2) ? a.y * (-2.0 * da) : 0.0;
+      sh[l] = t;
+      __syncthreads();
+      double acc = dG;
+      if (act)
+        for (int k = 0; k < m; ++k)
+          if (cr_s[k] == li && cc_s[k] == lj) acc = acc + sh[k];
+      __syncthreads();
+      dG = act ? acc : 0.0;
+    }
+    // chain_hess(x, G_L, dG, v)
+    const double t = mm(dG, x.q, false, true) + mm(a.GL, v.q, false, true);
+    const PV h{t, -t, mm(v.j - v.r, a.GL, true, false) + mm(x.j - x.r, dG, true, false)};
+    // e2rh: (skew(hJ), R sym(hR) R + sym(vR sym(gR) R), Q sym(hQ) Q + sym(vQ sym(gQ) Q))
+    const double hr = mm(mm(x.r, sym(h.r)), x.r) + sym(mm(mm(v.r, a.sgR), x.r));
+    const double hq = mm(mm(x.q, sym(h.q)), x.q) + sym(mm(mm(v.q, a.sgQ), x.q));
+    const PV hl{skew(h.j), hr, hq};
+    const double gj = gxaj(a, dA);     // wave op outside the lane select
+    const double q = cact ? (a.y * gj) / a.s : 0.0;
+    const PV gx = e2rg(x, chain(x, scatter(-(q * a.w))));
+    return pv_add(hl, gx);
+  }
+  // gradLagrangefun (RIPTRM.py:475-489) and its norm at (x, y)
+  __device__ double gradlag_norm(PV x, double y, double& f_out, double& A_out) {
+    const Metric g = metric(x);
+    const double A = Aof(x);
+    double f, Gf;
+    cost_grad(A, f, Gf);
+    const double w = cons_w(A);
+    const double G = Gf + scatter(y * w);
+    const PV gl = e2rg(x, chain(x, G));
+    f_out = f;
+    A_out = A;
+    return norm(g, gl);
+  }
+
+  // ---- tCG, RIPTRM.py:41-216 (eta0 = 0, identity preconditioner) ----------------------------
+  __device__ int tcg(const AtX& a, double Delta, PV& eta, PV& Heta, int& jout, double& hvps) {
+    const double theta = P.opt.tcg_theta, kappa = P.opt.tcg_kappa;
+    const int mininner = P.opt.tcg_mininner;
+    const int maxinner = P.d * (P.d - 1) / 2 + P.d * (P.d + 1);  // manifold.dim
+    eta = PV{0.0, 0.0, 0.0};
+    Heta = PV{0.0, 0.0, 0.0};
+    PV r = a.c;
+    double e_Pe = 0.0;
+    double r_r = inner(a.g, r, r);
+    double norm_r = sqrt(r_r);
+    const double norm_r0 = norm_r;
+    PV z = r;
+    double z_r = inner(a.g, z, r);
+    double d_Pd = z_r;
+    PV delta = pv_neg(z);
+    double e_Pd = 0.0;
+    double model = 0.0;
+    int stop = RIPTRM_TCG_MAX_INNER_ITER;
+    int j = 0;
+    for (j = 0; j < maxinner; ++j) {
+      const PV Hd = hw(a, delta);
+      hvps += 1.0;
+      const double d_Hd = inner(a.g, delta, Hd);
+      double alpha = 0.0, e_Pe_new;
+      if (d_Hd != 0.0) {
+        alpha = z_r / d_Hd;
+        e_Pe_new = (e_Pe + 2.0 * alpha * e_Pd) + (alpha * alpha) * d_Pd;
+      } else {
+        e_Pe_new = e_Pe;
+      }
+      const double D2 = Delta * Delta;
+      if (d_Hd <= 0.0 || e_Pe_new >= D2) {
+        const double tau = (-e_Pd + sqrt(e_Pd * e_Pd + d_Pd * (D2 - e_Pe))) / d_Pd;
+        eta = pv_add(eta, pv_scale(tau, delta));
+        Heta = pv_add(Heta, pv_scale(tau, Hd));
+        stop = d_Hd <= 0.0 ? RIPTRM_TCG_NEGATIVE_CURVATURE : RIPTRM_TCG_EXCEEDED_TR;
+        break;
+      }
+      e_Pe = e_Pe_new;
+      const PV ne = pv_add(eta, pv_scale(alpha, delta));
+      const PV nh = pv_add(Heta, pv_scale(alpha, Hd));
+      const double nm = inner(a.g, ne, a.c) + 0.5 * inner(a.g, ne, nh);
+      if (nm >= model) {
+        stop = RIPTRM_TCG_MODEL_INCREASED;
+        break;
+      }
+      eta = ne;
+      Heta = nh;
+      model = nm;
+      r = pv_add(r, pv_scale(alpha, Hd));
+      r_r = inner(a.g, r, r);
+      norm_r = sqrt(r_r);
+      if (j >= mininner && norm_r <= norm_r0 * fmin(pow(norm_r0, theta), kappa)) {
+        stop = kappa < pow(norm_r0, theta) ? RIPTRM_TCG_REACHED_TARGET_LINEAR : RIPTRM_TCG_REACHED_TARGET_SUPERLINEAR;
+        break;
+      }
+      z = r;
+      const double zold = z_r;
+      z_r = r_r;   // inner(z, r) with z = r: pymanopt reuses solve(x, r) for both operands -> == r_r
+      const double beta = z_r / zold;
+      delta = pv_add(pv_neg(z), pv_scale(beta, delta));
+      delta = proj(delta);
+      e_Pd = beta * (e_Pd + alpha * d_Pd);
+      d_Pd = z_r + (beta * beta) * d_Pd;
+    }
+    if (j >= maxinner) j = maxinner - 1;  // Python's range loop variable after exhaustion
+    jout = j;
+    return stop;
+  }
+
+  // ---- evaluation, src/solver/utils.py:342-368 (+ compute_residual :269-340) ----------------
+  // ev: cost, distance, residual, gradnorm, complvio, dualvio, manvio, maxvio, meanvio, maxabsy
+  __device__ void evaluation(PV xprev, PV x, double y, double (&ev)[10]) {
+    double f, A;
+    const double gradnorm = gradlag_norm(x, y, f, A);
+    const double g = cons_val(A);
+    const double cv = cact ? y * g : 0.0;
+    const double sq_compl = wsum(cv * cv);
+    const double nv = cact ? fmax(-y, 0.0) : 0.0;
+    const double sq_nonneg = wsum(nv * nv);
+    const double iv = cact ? fmax(g, 0.0) : 0.0;
+    const double sq_ineq = wsum(iv * iv);
+    const double maxvio = wmax(cact ? iv : 0.0);
+    const double meanvio = wsum(iv) / (double)m;
+    const double maxy = wmax(cact ? fabs(y) : -INFINITY);
+    double manvio = 0.0;
+    if (P.opt.manvio_kind == RIPTRM_MANVIO_SI) {
+      const double aj = x.j + tr(x.j), ar = x.r - tr(x.r), aq = x.q - tr(x.q);
+      manvio = (sqrt(wsum(aj * aj)) + sqrt(wsum(ar * ar))) + sqrt(wsum(aq * aq));
+      const bool pr = spd_pd(x.r);
+      const bool pq = spd_pd(x.q);
+      if (!pr || !pq) manvio = INFINITY;
+    }
+    const double dj = x.j - xprev.j;
+    const double dJ = sqrt(wsum(dj * dj));
+    const double dR = spd_dist(xprev.r, x.r);
+    const double dQ = spd_dist(xprev.q, x.q);
+    ev[0] = f;
+    ev[1] = sqrt((dJ * dJ + dR * dR) + dQ * dQ);
+    ev[2] = sqrt(((((gradnorm * gradnorm + sq_compl) + sq_nonneg) + sq_ineq) + 0.0) + manvio * manvio);
+    ev[3] = gradnorm;
+    ev[4] = sqrt(sq_compl);
+    ev[5] = sqrt(sq_nonneg);
+    ev[6] = manvio;
+    ev[7] = maxvio;
+    ev[8] = meanvio;
+    ev[9] = maxy;
+  }
+
+  __device__ __forceinline__ double now() {
+    double t = (l == 0) ? (double)wall_clock64() : -INFINITY;
+    return wmax(t);
+  }
+
+  __device__ void log_row(const double (&ev)[10], double outer_it, double mu, const Info* inf, double tcg_iters,
+                          double t_now, double t_start, double& count, double& overflow) {
+    if (l == 0) {
+      const int cnt = (int)count;
+      if (cnt < P.opt.log_capacity && cnt < P.cap) {
+        double* L = P.log + ((int64_t)b * P.cap + cnt) * RIPTRM_LOG_NFIELDS;
+        for (int k = 0; k < RIPTRM_LOG_NFIELDS; ++k) L[k] = 0.0;
+        L[RIPTRM_LOG_ITERATION] = outer_it;
+        L[RIPTRM_LOG_TIME] = (cnt == 0) ? 0.0 : (t_now - t_start) / P.clock_hz;
+        L[RIPTRM_LOG_COST] = ev[0];
+        L[RIPTRM_LOG_DISTANCE] = ev[1];
+        L[RIPTRM_LOG_RESIDUAL] = ev[2];
+        L[RIPTRM_LOG_GRADNORM] = ev[3];
+        L[RIPTRM_LOG_COMPLVIOLATION] = ev[4];
+        L[RIPTRM_LOG_DUALVIOLATION] = ev[5];
+        L[RIPTRM_LOG_MANVIOLATION] = ev[6];
+        L[RIPTRM_LOG_MAXVIOLATION] = ev[7];
+        L[RIPTRM_LOG_MEANVIOLATION] = ev[8];
+        L[RIPTRM_LOG_MU] = mu;
+        L[RIPTRM_LOG_MAXABSLAGMULT] = ev[9];
+        L[RIPTRM_LOG_TCG_ITERS] = tcg_iters;
+        L[RIPTRM_LOG_DUAL_CLIPPING] = -1.0;
+        if (inf) {
+          L[RIPTRM_LOG_HAS_INFO] = inf->has;
+          L[RIPTRM_LOG_NUM_INNER] = inf->num;
+          L[RIPTRM_LOG_INNER_STATUS] = inf->status;
+          L[RIPTRM_LOG_TR_RADIUS] = inf->tr;
+          L[RIPTRM_LOG_DXTYPE] = inf->dxtype;
+          L[RIPTRM_LOG_NORMDX] = inf->normdx;
+          L[RIPTRM_LOG_MINXFEASI] = inf->minx;
+          L[RIPTRM_LOG_MINYFEASI] = inf->miny;
+          L[RIPTRM_LOG_COMPL] = inf->compl_;
+          L[RIPTRM_LOG_HAS_RATIO] = inf->hasratio;
+          L[RIPTRM_LOG_ARED_PRED] = inf->ratio;
+          L[RIPTRM_LOG_RADIUS_UPDATE] = inf->ru;
+          L[RIPTRM_LOG_DUAL_CLIPPING] = inf->dc;
+        }
+      } else {
+        overflow += 1.0;
+      }
+    }
+    count += 1.0;
+  }
+
+  __device__ __forceinline__ PV load_pv(const double* base) {
+    if (!act) return PV{0.0, 0.0, 0.0};
+    return PV{base[l], base[dd + l], base[2 * dd + l]};
+  }
+  __device__ __forceinline__ void store_pv(double* base, PV v) {
+    if (act) {
+      base[l] = v.j;
+      base[dd + l] = v.r;
+      base[2 * dd + l] = v.q;
+    }
+  }
+  __device__ __forceinline__ double mu_at(int idx) const {
+    const int i = idx < P.tab_len ? idx : P.tab_len - 1;
+    return P.mu_tab[i];
+  }
+
+  // ---- the whole run: RIPTRM.run / outer_step / inner_run / inner_step ----------------------
+  __device__ void solve() {
+    const int64_t v3 = 3LL * dd;
+    PV x = load_pv(P.in_x + b * v3);
+    double y = cact ? P.in_y[(int64_t)b * m + l] : 0.0;
+    const PV xI = x;
+    const double yI = y;
+    double outer_it = 0.0, mu_idx = 0.0, mu = mu_at(0), Delta = P.opt.initial_tr_radius;
+    double inner_total = 0.0, tcg_total = 0.0, hvps = 0.0, log_count = 0.0, log_over = 0.0;
+    double stop_code = RIPTRM_STOP_NONE, stop_rt = 0.0, residual = 0.0, last_j = 0.0, last_stop = 0.0;
+    const double t_start = now();
+    PV xPrev = x;   // inner_run's xPrev (RIPTRM.py:787)
+    PV xHead = x;   // run's xPrev: the point at the previous outer head (RIPTRM.py:929, :947)
+    Info info{};
+    bool have_info = false;
+    const bool save_inner = P.opt.save_inner_iteration != 0;
+    while (true) {
+      // outer loop head, RIPTRM.py:931-959
+      double ev[10];
+      evaluation(xHead, x, y, ev);
+      double tn = now();
+      if (outer_it == 0.0 || !save_inner)
+        log_row(ev, outer_it, mu, (outer_it != 0.0 && have_info) ? &info : nullptr, last_j + 1.0, tn, t_start,
+                log_count, log_over);
+      residual = ev[2];
+      xHead = x;
+      const double rt = (tn - t_start) / P.clock_hz;
+      int stop = RIPTRM_STOP_NONE;
+      if (rt >= P.opt.maxtime) stop = RIPTRM_STOP_MAXTIME;
+      else if (outer_it >= (double)P.opt.maxiter) stop = RIPTRM_STOP_MAXITER;
+      if (ev[2] <= P.opt.tolresid) stop = RIPTRM_STOP_TOLRESID;
+      if (stop != RIPTRM_STOP_NONE) {
+        stop_code = stop;
+        stop_rt = rt;
+        break;
+      }
+      // restart_every cycling (benchmark windows)
+      const int k = P.opt.restart_every;
+      if (k > 0 && outer_it > 0.0 && fmod(outer_it, (double)k) == 0.0) {
+        x = xI;
+        y = yI;
+        xPrev = x;
+        mu_idx = 0.0;
+        mu = mu_at(0);
+        Delta = P.opt.initial_tr_radius;
+      }
+      outer_it += 1.0;
+      const int ti = (int)mu_idx < P.tab_len ? (int)mu_idx : P.tab_len - 1;
+      const double tolL = P.tolL_tab[ti], tolC = P.tolC_tab[ti];
+      const PV x0 = x;
+      const double y0 = y;
+      const double Delta0 = Delta;
+      xPrev = x;
+      double inner_it = 0.0;
+      const double t_inner = now();
+      while (true) {  // inner_run, RIPTRM.py:785-847
+        inner_it += 1.0;
+        const double DeltaStep = Delta;
+        AtX a;
+        prepare(a, x, y, mu);
+        PV eta, Heta;
+        int jj = 0;
+        const int tstop = tcg(a, Delta, eta, Heta, jj, hvps);
+        tcg_total += (double)jj + 1.0;
+        last_j = jj;
+        last_stop = tstop;
+        const double normdx = norm(a.g, eta);
+        const double dA = dAof(a, eta);
+        const double gj = gxaj(a, dA);
+        const double dy = cact ? ((-y + mu * (1.0 / a.s)) - (y * gj) / a.s) : 0.0;
+        const PV xN = retract(x, a.g, eta);
+        const double yN = cact ? y + dy : 0.0;
+        const double AN = Aof(xN);
+        const double gN = cons_val(AN);
+        const double sN = cact ? -gN : 1.0;
+        const double minx = wmin(cact ? sN : INFINITY);
+        const double miny = wmin(cact ? yN : INFINITY);
+        const bool xfeas = minx > 0.0 && wmin(cact ? (sN > 0.0 ? 1.0 : 0.0) : 1.0) > 0.0;
+        const bool yfeas = wmin(cact ? (yN > 0.0 ? 1.0 : 0.0) : 1.0) > 0.0;
+        const double cvv = cact ? yN * sN - mu : 0.0;
+        const double compl_ = sqrt(wsum(cvv * cvv));
+        info = Info{1.0, inner_it, 0.0, DeltaStep, (double)tstop, normdx, minx, miny, compl_, 0.0, 0.0, 0.0, -1.0};
+        have_info = true;
+        bool converged = false;
+        double fN = 0.0, AN2 = 0.0;
+        if (xfeas) {
+          const double normgl = gradlag_norm(xN, yN, fN, AN2);
+          converged = yfeas && normgl <= tolL && compl_ <= tolC;
+        }
+        if (converged) {  // RIPTRM.py:762-766
+          x = xN;
+          y = yN;
+          info.status = RIPTRM_IS_CONVERGED;
+        } else if (!xfeas) {  // RIPTRM.py:769-775
+          info.status = RIPTRM_IS_PRIMAL_INFEASIBLE;
+          Delta = P.opt.gamma * normdx;
+        } else {  // update_xy_TR_radius, RIPTRM.py:631-705
+          const double ls = wsum(cact ? log(a.s) : 0.0);
+          const double lsN = wsum(cact ? log(sN) : 0.0);
+          const double lb_c = a.f - mu * ls;
+          const double lb_n = fN - mu * lsN;
+          double ared = lb_c - lb_n;
+          const PV Hdx = hw(a, eta);
+          hvps += 1.0;
+          double pred = (0.0 - 0.5 * inner(a.g, Hdx, eta)) - inner(a.g, a.c, eta);
+          const double red_reg = fmax(1.0, fabs(lb_c)) * 2.220446049250313e-16 * P.opt.reduction_regularization;
+          ared = ared + red_reg;
+          pred = pred + red_reg;
+          const double ratio = ared / pred;
+          double Dn;
+          int ru;
+          if (ared < 0.25 * pred) {
+            ru = RIPTRM_RU_REDUCED;
+            Dn = 0.25 * Delta;
+          } else if (ared >= 0.75 * pred && fabs(normdx - Delta) <= 1e-15) {
+            ru = RIPTRM_RU_EXPANDED;
+            const double d2 = 2.0 * Delta;
+            Dn = d2 < P.opt.maximal_tr_radius ? d2 : P.opt.maximal_tr_radius;
+          } else {
+            ru = RIPTRM_RU_UNCHANGED;
+            Dn = Delta;
+          }
+          info.hasratio = 1.0;
+          info.ratio = ratio;
+          info.ru = ru;
+          if (ared > P.opt.rho * pred) {
+            const double cl = P.opt.const_left, crr = P.opt.const_right;
+            const double iright = np_max(crr, crr / mu);   // RIPTRM.py:682 (3-arg np.maximum quirk)
+            double yc = 0.0;
+            if (cact) {
+              const double il = cl * np_min(np_min(y, mu / sN), 1.0);
+              yc = np_min(np_max(yN, il), iright);
+            }
+            const double nd = wsum((cact && yc != yN) ? 1.0 : 0.0);
+            x = xN;
+            y = yc;
+            info.status = RIPTRM_IS_SUCCESSFUL;
+            info.dc = nd > 0.0 ? 1.0 : 0.0;
+          } else {
+            info.status = RIPTRM_IS_UNSUCCESSFUL;
+          }
+          Delta = Dn;
+        }
+        // inner_run tail, RIPTRM.py:810-847
+        inner_total += 1.0;
+        tn = now();
+        if (save_inner) {
+          evaluation(xPrev, x, y, ev);
+          log_row(ev, outer_it, mu, &info, last_j + 1.0, tn, t_start, log_count, log_over);
+        }
+        xPrev = x;
+        bool exitflag = converged;
+        double rti, lim;
+        if (P.opt.inner_maxtime < 0.0) {
+          lim = P.opt.maxtime;
+          rti = (tn - t_start) / P.clock_hz;
+        } else {
+          lim = P.opt.inner_maxtime;
+          rti = (tn - t_inner) / P.clock_hz;
+        }
+        const bool tmo = rti >= lim;
+        const bool imax = P.opt.inner_maxiter >= 0 && inner_it >= (double)P.opt.inner_maxiter;
+        if (tmo || imax) {
+          info.status = imax ? RIPTRM_IS_MAX_ITER_EXCEEDED : RIPTRM_IS_MAX_TIME_EXCEEDED;
+          exitflag = true;
+          x = x0;
+          y = y0;
+          xPrev = x0;
+          Delta = Delta0;
+        }
+        if (exitflag) break;
+      }
+      // outer_step tail, RIPTRM.py:889-896
+      mu_idx += 1.0;
+      mu = mu_at((int)mu_idx);
+      const double mn = P.opt.minimal_initial_tr_radius;
+      Delta = Delta > mn ? Delta : mn;
+    }
+    store_pv(P.x + b * v3, x);
+    if (cact) P.y[(int64_t)b * m + l] = y;
+    if (l == 0) {
+      double* o = P.stats + (int64_t)b * RIPTRM_STAT_NFIELDS;
+      for (int k = 0; k < RIPTRM_STAT_NFIELDS; ++k) o[k] = 0.0;
+      o[RIPTRM_STAT_OUTER_ITERS] = outer_it;
+      o[RIPTRM_STAT_INNER_ITERS] = inner_total;
+      o[RIPTRM_STAT_TCG_ITERS] = tcg_total;
+      o[RIPTRM_STAT_PASSES] = hvps;
+      o[RIPTRM_STAT_STOP_CODE] = stop_code;
+      o[RIPTRM_STAT_STOP_RUNTIME] = stop_rt;
+      o[RIPTRM_STAT_FINAL_RESIDUAL] = residual;
+      o[RIPTRM_STAT_LOG_COUNT] = log_count;
+      o[RIPTRM_STAT_LOG_OVERFLOW] = log_over;
+      o[RIPTRM_STAT_PHASE] = riptrm::PH_DONE;
+      o[RIPTRM_STAT_MU] = mu;
+      o[RIPTRM_STAT_TR_RADIUS] = Delta;
+      o[RIPTRM_STAT_TCG_LAST_J] = last_j;
+      o[RIPTRM_STAT_TCG_LAST_STOP] = last_stop;
+    }
+  }
+
+  __device__ void op_hvp() {
+    const int64_t v3 = 3LL * dd;
+    const PV x = load_pv(P.in_x + b * v3);
+    const double y = cact ? P.in_y[(int64_t)b * m + l] : 0.0;
+    AtX a;
+    prepare(a, x, y, P.in_mu[b]);
+    const PV v = load_pv(P.in_v + b * v3);
+    const PV h = hw(a, v);
+    store_pv(P.out_v + b * v3, h);
+  }
+
+  __device__ void op_tcg() {
+    const int64_t v3 = 3LL * dd;
+    const PV x = load_pv(P.in_x + b * v3);
+    const double y = cact ? P.in_y[(int64_t)b * m + l] : 0.0;
+    AtX a;
+    prepare(a, x, y, P.in_mu[b]);
+    PV eta, Heta;
+    int j = 0;
+    double hv = 0.0;
+    const int stop = tcg(a, P.in_delta[b], eta, Heta, j, hv);
+    store_pv(P.eta + b * v3, eta);
+    store_pv(P.heta + b * v3, Heta);
+    if (l == 0) {
+      double* o = P.stats + (int64_t)b * RIPTRM_STAT_NFIELDS;
+      o[RIPTRM_STAT_TCG_LAST_J] = j;
+      o[RIPTRM_STAT_TCG_LAST_STOP] = stop;
+      o[RIPTRM_STAT_PASSES] = hv;
+    }
+  }
+};
+
+__global__ void __launch_bounds__(W) k_si(SIParams P) {
+  __shared__ double sh[2 * W];
+  __shared__ double ser[4 * W];
+  __shared__ int crs[MMAX], ccs[MMAX];
+  const int b = blockIdx.x;
+  if (b >= P.batch) return;
+  Eng e(P, b, sh, ser, crs, ccs);
+  if (P.mode == MODE_SOLVE) e.solve();
+  else if (P.mode == MODE_HVP) e.op_hvp();
+  else e.op_tcg();
+}
+
+struct Bound {
+  riptrm_si_problem prob;
+  int batch = 0, cap = 0;
+  Layout L{};
+  char* ws = nullptr;
+};
+
+}  // namespace riptrm_si
+
+using namespace riptrm_si;
+
+void riptrm_si_release(riptrm_si::Bound* s) { delete s; }
+
+static bool si_dims_ok(int32_t d, int32_t N, int32_t m, int32_t batch, int32_t cap) {
+  return d >= 1 && d <= DMAX && N >= 1 && m >= 1 && m <= MMAX && batch >= 1 && cap >= 0;
+}
+
+static SIParams si_params(riptrm_ctx* c, int mode) {
+  Bound* s = c->si;
+  SIParams P;
+  std::memset(&P, 0, sizeof(P));
+  P.d = s->prob.d;
+  P.N = s->prob.N;
+  P.m = s->prob.m;
+  P.batch = s->batch;
+  P.cap = s->cap;
+  P.mode = mode;
+  P.h = s->prob.h;
+  P.clock_hz = c->clock_hz;
+  P.X = s->prob.X;
+  P.XP = s->prob.XP;
+  P.data_stride = s->prob.data_stride;
+  P.cons = s->prob.cons;
+  P.cons_stride = s->prob.cons_stride;
+  P.x = (double*)(s->ws + s->L.off_x);
+  P.y = (double*)(s->ws + s->L.off_y);
+  P.eta = (double*)(s->ws + s->L.off_eta);
+  P.heta = (double*)(s->ws + s->L.off_heta);
+  P.escr = (double*)(s->ws + s->L.off_escr);
+  P.stats = (double*)(s->ws + s->L.off_stats);
+  P.log = (double*)(s->ws + s->L.off_log);
+  P.opt.struct_size = (int32_t)sizeof(riptrm_options);
+  P.opt.tcg_theta = 1.0;   // RIPTRM.py:330-332 defaults for the operator entry points
+  P.opt.tcg_kappa = 0.1;
+  P.opt.tcg_mininner = 1;
+  return P;
+}
+
+static int si_launch(riptrm_ctx* c, const SIParams& P) {
+  hipLaunchKernelGGL(k_si, dim3((unsigned)P.batch), dim3(W), 0, c->stream, P);
+  HIPCHK(c, hipGetLastError());
+  return RIPTRM_OK;
+}
+
+extern "C" {
+
+int64_t riptrm_si_workspace_bytes(int32_t d, int32_t N, int32_t m, int32_t batch, int32_t cap) {
+  if (!si_dims_ok(d, N, m, batch, cap)) return -1;
+  return make_layout(d, N, m, batch, cap).total;
+}
+
+int64_t riptrm_si_workspace_offset(int32_t d, int32_t N, int32_t m, int32_t batch, int32_t cap, int32_t kind) {
+  if (!si_dims_ok(d, N, m, batch, cap)) return -1;
+  const riptrm_si::Layout L = make_layout(d, N, m, batch, cap);
+  switch (kind) {
+    case 0: return L.off_x;
+    case 1: return L.off_y;
+    case 2: return L.off_eta;
+    case 3: return L.off_heta;
+    case 4: return L.off_stats;
+    case 5: return L.off_log;
+    default: return -1;
+  }
+}
+
+int riptrm_si_bind(riptrm_ctx* ctx, const riptrm_si_problem* prob, int32_t batch, void* ws, int64_t ws_bytes,
+                   int32_t cap) {
+  if (!ctx) return RIPTRM_E_ARG;
+  if (!prob || prob->struct_size != (int32_t)sizeof(riptrm_si_problem))
+    return fail(ctx, RIPTRM_E_ARG, "si_bind: riptrm_si_problem.struct_size mismatch");
+  if (!si_dims_ok(prob->d, prob->N, prob->m, batch, cap))
+    return fail(ctx, RIPTRM_E_ARG, "si_bind: need 1 <= d <= 8, N >= 1, 1 <= m <= 64, batch >= 1");
+  if (!prob->X || !prob->XP || !prob->cons || !ws || prob->data_stride < 0 || prob->cons_stride < 0)
+    return fail(ctx, RIPTRM_E_ARG, "si_bind: bad argument");
+  if (prob->data_stride != 0 && prob->data_stride < (int64_t)prob->d * prob->N)
+    return fail(ctx, RIPTRM_E_ARG, "si_bind: data_stride smaller than d*N");
+  if (prob->cons_stride != 0 && prob->cons_stride < (int64_t)prob->m * RIPTRM_SI_CONS_FIELDS)
+    return fail(ctx, RIPTRM_E_ARG, "si_bind: cons_stride smaller than m*RIPTRM_SI_CONS_FIELDS");
+  if (((uintptr_t)ws % 256) != 0) return fail(ctx, RIPTRM_E_ARG, "si_bind: workspace must be 256-byte aligned");
+  const riptrm_si::Layout L = make_layout(prob->d, prob->N, prob->m, batch, cap);
+  if (ws_bytes < L.total) return fail(ctx, RIPTRM_E_ARG, "si_bind: workspace too small");
+  HIPCHK(ctx, hipSetDevice(ctx->device));
+  HIPCHK(ctx, hipMemsetAsync(ws, 0, (size_t)L.total, ctx->stream));
+  if (!ctx->si) ctx->si = new Bound();
+  ctx->si->prob = *prob;
+  ctx->si->batch = batch;
+  ctx->si->cap = cap;
+  ctx->si->L = L;
+  ctx->si->ws = (char*)ws;
+  return RIPTRM_OK;
+}
+
+int riptrm_si_hvp(riptrm_ctx* ctx, const double* x, const double* y, const double* mu, const double* v, double* out) {
+  if (!ctx) return RIPTRM_E_ARG;
+  if (!ctx->si) return fail(ctx, RIPTRM_E_STATE, "si_hvp: riptrm_si_bind first");
+  if (!x || !y || !mu || !v || !out) return fail(ctx, RIPTRM_E_ARG, "si_hvp: bad argument");
+  HIPCHK(ctx, hipSetDevice(ctx->device));
+  SIParams P = si_params(ctx, MODE_HVP);
+  P.in_x = x;
+  P.in_y = y;
+  P.in_mu = mu;
+  P.in_v = v;
+  P.out_v = out;
+  return si_launch(ctx, P);
+}
+
+int riptrm_si_tcg(riptrm_ctx* ctx, const riptrm_options* opt, const double* x, const double* y, const double* mu,
+                  const double* delta) {
+  if (!ctx) return RIPTRM_E_ARG;
+  if (!ctx->si) return fail(ctx, RIPTRM_E_STATE, "si_tcg: riptrm_si_bind first");
+  if (!x || !y || !mu || !delta) return fail(ctx, RIPTRM_E_ARG, "si_tcg: bad argument");
+  if (opt && opt->struct_size != (int32_t)sizeof(riptrm_options))
+    return fail(ctx, RIPTRM_E_ARG, "si_tcg: riptrm_options.struct_size mismatch");
+  HIPCHK(ctx, hipSetDevice(ctx->device));
+  SIParams P = si_params(ctx, MODE_TCG);
+  if (opt) P.opt = *opt;
+  P.in_x = x;
+  P.in_y = y;
+  P.in_mu = mu;
+  P.in_delta = delta;
+  return si_launch(ctx, P);
+}
+
+int riptrm_si_solve(riptrm_ctx* ctx, const riptrm_options* opt, const double* x0, const double* y0,
+                    const double* mu_table, const double* tolL_table, const double* tolC_table, int32_t table_len) {
+  if (!ctx) return RIPTRM_E_ARG;
+  if (!ctx->si) return fail(ctx, RIPTRM_E_STATE, "si_solve: riptrm_si_bind first");
+  if (!opt || opt->struct_size != (int32_t)sizeof(riptrm_options))
+    return fail(ctx, RIPTRM_E_ARG, "si_solve: riptrm_options.struct_size mismatch");
+  if (!x0 || !y0 || !mu_table || !tolL_table || !tolC_table || table_len <= 0)
+    return fail(ctx, RIPTRM_E_ARG, "si_solve: bad argument");
+  if (opt->log_capacity > ctx->si->cap) return fail(ctx, RIPTRM_E_ARG, "si_solve: log_capacity exceeds bound capacity");
+  HIPCHK(ctx, hipSetDevice(ctx->device));
+  SIParams P = si_params(ctx, MODE_SOLVE);
+  P.opt = *opt;
+  P.in_x = x0;
+  P.in_y = y0;
+  P.mu_tab = mu_table;
+  P.tolL_tab = tolL_table;
+  P.tolC_tab = tolC_table;
+  P.tab_len = table_len;
+  return si_launch(ctx, P);
+}
+
+}  // extern "C"

@@ -113,7 +113,7 @@ class ResolvedOptions:
 
 
 def resolve_options(option: Dict[str, Any], typical_dist: float, log_capacity: int,
-                    restart_every: int = 0) -> ResolvedOptions:
+                    restart_every: int = 0, manvio_classifier=None) -> ResolvedOptions:
     o = dict(REFERENCE_DEFAULTS)
     o.update(option or {})
     if o['TRS_solver'] != 'tCG':
@@ -136,7 +136,7 @@ def resolve_options(option: Dict[str, Any], typical_dist: float, log_capacity: i
     c.inner_maxiter = -1 if o['inner_maxiter'] is None else int(o['inner_maxiter'])
     c.tcg_mininner = int(o['tCG_mininner'])
     c.save_inner_iteration = 1 if o['save_inner_iteration'] else 0
-    c.manvio_kind = manvio_kind(o['manviofun'])
+    c.manvio_kind = (manvio_classifier or manvio_kind)(o['manviofun'])
     c.log_capacity = int(log_capacity)
     c.restart_every = int(restart_every)
     c.maxtime = float(o['maxtime']) if o['maxtime'] is not None else math.inf

@@ -37,6 +37,15 @@ class RiptrmOptions(ctypes.Structure):
     ]
 
 
+class RiptrmSIProblem(ctypes.Structure):
+    """Mirror of ``riptrm_si_problem`` (include/riptrm.h)."""
+    _fields_ = [
+        ("struct_size", c_int32), ("d", c_int32), ("N", c_int32), ("m", c_int32), ("h", c_double),
+        ("X", c_void_p), ("XP", c_void_p), ("data_stride", c_int64), ("cons", c_void_p),
+        ("cons_stride", c_int64),
+    ]
+
+
 # (restype, argtypes) of every exported symbol
 SIGNATURES: Dict[str, tuple] = {
     "riptrm_abi_version": (c_int32, []),
@@ -63,6 +72,13 @@ SIGNATURES: Dict[str, tuple] = {
     "riptrm_profile_enable": (c_int32, [c_void_p, c_int32]),
     "riptrm_profile_read": (c_int32, [c_void_p, ctypes.POINTER(c_double), ctypes.POINTER(c_int64),
                                       ctypes.POINTER(c_double), ctypes.POINTER(c_int64)]),
+    "riptrm_si_workspace_bytes": (c_int64, [c_int32, c_int32, c_int32, c_int32, c_int32]),
+    "riptrm_si_workspace_offset": (c_int64, [c_int32, c_int32, c_int32, c_int32, c_int32, c_int32]),
+    "riptrm_si_bind": (c_int32, [c_void_p, ctypes.POINTER(RiptrmSIProblem), c_int32, c_void_p, c_int64, c_int32]),
+    "riptrm_si_hvp": (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "riptrm_si_tcg": (c_int32, [c_void_p, ctypes.POINTER(RiptrmOptions), c_void_p, c_void_p, c_void_p, c_void_p]),
+    "riptrm_si_solve": (c_int32, [c_void_p, ctypes.POINTER(RiptrmOptions), c_void_p, c_void_p, c_void_p, c_void_p,
+                                  c_void_p, c_int32]),
 }
 
 

@@ -69,19 +69,21 @@ def test_layout_functions(built_lib):
     assert built_lib.riptrm_nonnegpca_s_elems(10, 5) == -1
 
 
-def test_options_struct_layout_matches_c(tmp_path):
-    """ctypes RiptrmOptions == the C struct (sizeof and every offset), compiled with gcc."""
-    fields = [f for f, _ in N.RiptrmOptions._fields_]
+@pytest.mark.parametrize("cls,cname", [("RiptrmOptions", "riptrm_options"), ("RiptrmSIProblem", "riptrm_si_problem")])
+def test_options_struct_layout_matches_c(tmp_path, cls, cname):
+    """ctypes mirrors == the C structs (sizeof and every offset), compiled with gcc."""
+    S = getattr(N, cls)
+    fields = [f for f, _ in S._fields_]
     src = tmp_path / "probe.c"
-    body = "\n".join(f'printf("%zu\\n", offsetof(riptrm_options, {f}));' for f in fields)
+    body = "\n".join(f'printf("%zu\\n", offsetof({cname}, {f}));' for f in fields)
     src.write_text(f'#include <stdio.h>\n#include <stddef.h>\n#include "riptrm.h"\n'
-                   f'int main(void){{printf("%zu\\n", sizeof(riptrm_options));\n{body}\nreturn 0;}}\n')
+                   f'int main(void){{printf("%zu\\n", sizeof({cname}));\n{body}\nreturn 0;}}\n')
     exe = tmp_path / "probe"
     subprocess.run(["gcc", "-std=c99", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], check=True)
     vals = [int(v) for v in subprocess.check_output([str(exe)]).split()]
-    assert vals[0] == ctypes.sizeof(N.RiptrmOptions)
+    assert vals[0] == ctypes.sizeof(S)
     for f, off in zip(fields, vals[1:]):
-        assert getattr(N.RiptrmOptions, f).offset == off, f
+        assert getattr(S, f).offset == off, f
 
 
 def test_resolve_options_defaults_and_errors():

@@ -1,0 +1,152 @@
+"""CPU tests of the StableIdentification restatement (oracle/si_oracle.py) on the reference's
+fixture dataset/StableIdentification/1 (d = 5, N = 95, m = 16, starts a..t), and of the host-side
+SI plumbing (si.py) that needs no GPU.  pymanopt / autograd are absent: the manifold and
+derivative formulas are checked by identities (finite differences, metric compatibility,
+self-adjointness) and by the two back-ends against each other; the end-to-end pin is the
+published KKT residual level (src/StableIdentification/analyzer.ipynb: median log10 -12.37)."""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+from oracle import si_oracle as SI
+from oracle import riptrm_oracle as RO
+
+DS = os.path.join(GOLDEN, "si_1")
+
+
+@pytest.fixture(scope="module")
+def data():
+    return SI.SIData.load(DS)
+
+
+def _tangent(P, x, seed):
+    return P.manifold.projection(x, np.random.RandomState(seed).randn(3, 5, 5))
+
+
+def test_fixture_shapes(data):
+    assert (data.d, data.N, data.m) == (5, 95, 16)   # N = 95 after the hstack
+    x0, y0 = SI.load_start(DS, "a")
+    assert x0.shape == (3, 5, 5) and y0.shape == (16,)
+    M = SI.ProductSkewSPDSPD(5)
+    assert M.dim == 40 and np.isclose(M.typical_dist, np.sqrt(40))
+    assert np.allclose(x0[0], -x0[0].T) and np.all(np.linalg.eigvalsh(x0[1]) > 0)
+    assert SI.si_manvio(x0) < 1e-12
+
+
+def test_structured_and_vectorized_operators_agree(data):
+    Ps, Pv = SI.SIStructured(data), SI.SIVectorized(data)
+    for pt, seed in (("a", 1), ("f", 2), ("t", 3)):
+        x, y0 = SI.load_start(DS, pt)
+        y = y0 * (0.3 + np.random.RandomState(seed).rand(16))
+        v = _tangent(Pv, x, seed)
+        rel = lambda a, b: np.linalg.norm(a - b) / np.linalg.norm(b)
+        assert rel(Pv.gradlag(x, y), Ps.gradlag(x, y)) < 1e-13
+        assert rel(Pv.hesslag(x, y, v), Ps.hesslag(x, y, v)) < 1e-13
+        assert rel(Pv.Gx(x, y), Ps.Gx(x, y)) < 1e-13
+        assert rel(Pv.Gxaj(x, v), Ps.Gxaj(x, v)) < 1e-13
+        _, s1, H1, c1 = Pv.begin_inner(x, y, 0.01)
+        _, s2, H2, c2 = Ps.begin_inner(x, y, 0.01)
+        assert rel(c1, c2) < 1e-13 and rel(H1(v), H2(v)) < 1e-13
+        r1 = Pv.residual(x, y, SI.si_manvio)
+        r2 = Ps.residual(x, y, SI.si_manvio)
+        assert np.allclose(r1, r2, rtol=1e-13, atol=1e-15)
+
+
+def test_derivatives_by_finite_differences(data):
+    P = SI.SIStructured(data)
+    x, _ = SI.load_start(DS, "b")
+    u = np.random.RandomState(4).randn(3, 5, 5)
+    h = 1e-6
+    fd = (P.cost(x + h * u) - P.cost(x - h * u)) / (2 * h)
+    assert abs(fd - np.sum(P.euclidean_gradient(x) * u)) < 1e-7 * max(1, abs(fd))
+    w = np.random.RandomState(5).randn(3, 5, 5)
+    fdh = (P.euclidean_gradient(x + h * w) - P.euclidean_gradient(x - h * w)) / (2 * h)
+    assert np.linalg.norm(fdh - P.euclidean_hessian(x, w)) < 1e-6 * np.linalg.norm(fdh)
+    for i, g in enumerate(P.ineq):     # constraint gradients through rgrad + metric
+        v = _tangent(P, x, 10 + i)
+        fdg = (g(x + h * v) - g(x - h * v)) / (2 * h)
+        assert abs(P.manifold.inner_product(x, P.ineq_rgrad[i](x), v) - fdg) < 1e-6 * max(1, abs(fdg))
+
+
+def test_riemannian_hessian_is_self_adjoint(data):
+    """The affine-invariant SPD Hessian formula (pymanopt) is self-adjoint in the
+    metric; so is the barrier Hessian HwCur."""
+    P = SI.SIVectorized(data)
+    x, y = SI.load_start(DS, "c")
+    u, v = _tangent(P, x, 6), _tangent(P, x, 7)
+    M = P.manifold
+    a = M.inner_product(x, P.hesslag(x, y, u), v)
+    b = M.inner_product(x, u, P.hesslag(x, y, v))
+    assert abs(a - b) < 1e-10 * max(abs(a), 1)
+    _, _, Hw, _ = P.begin_inner(x, y, 0.05)
+    a = M.inner_product(x, Hw(u), v)
+    b = M.inner_product(x, u, Hw(v))
+    assert abs(a - b) < 1e-10 * max(abs(a), 1)
+
+
+def test_tcg_invariants(data):
+    P = SI.SIVectorized(data)
+    x, y = SI.load_start(DS, "d")
+    _, _, Hw, c = P.begin_inner(x, y, 0.1)
+    for Delta in (1e-3, 0.05, np.sqrt(40) / 8):
+        eta, Heta, j, stop = RO.truncated_conjugate_gradient(P.manifold, Hw, x, c, Delta, 1, 0.1, 1, P.manifold.dim)
+        assert P.manifold.norm(x, eta) <= Delta * (1 + 1e-12)
+        assert np.linalg.norm(Heta - Hw(eta)) < 1e-8 * max(np.linalg.norm(Heta), 1)
+        m = P.manifold.inner_product(x, eta, c) + 0.5 * P.manifold.inner_product(x, eta, Heta)
+        assert m < 0
+
+
+def test_comparator_calibration_on_oracle_pair(data):
+    """The flip-aware comparator used for the GPU holds between the two CPU oracles."""
+    import sys
+    sys.path.insert(0, os.path.dirname(__file__))
+    from parity import compare_until_flip
+    flips = 0
+    for pt in "aceg":
+        x0, y0 = SI.load_start(DS, pt)
+        o = dict(maxiter=8, tolresid=0, maxtime=1e9)
+        a = SI.solve(data, x0, y0, o).log
+        b = SI.solve(data, x0, y0, o, structured=True).log
+        flips += compare_until_flip(a, b) is not None
+    assert flips >= 1   # the radius-expansion tie does occur between fp64 implementations
+
+
+def test_oracle_reaches_published_residual_level(data):
+    """analyzer.ipynb: RIPTRM (tCG) on StableIdentification/1 reaches a median log10 KKT
+    residual of -12.37 (Q1 -12.44, Q3 -12.23).  The restatement gets there in ~33 outer
+    iterations (inner_maxiter bounds the last, unattainable inner tolerance 1e-14)."""
+    best = []
+    for pt in "ak":
+        x0, y0 = SI.load_start(DS, pt)
+        r = SI.solve(data, x0, y0, dict(maxiter=34, inner_maxiter=150, tolresid=0, maxtime=1e9))
+        res = np.array(r.log["residual"], float)
+        conv = [i for i, s in enumerate(r.log["inner_status"]) if s in (None, "converged")]
+        best.append(np.log10(res[conv].min()))
+    assert max(best) < -11.5 and min(best) > -14.0, best
+
+
+def test_host_si_helpers(tmp_path):
+    pytest.importorskip("torch")
+    import si
+    cons = si.expand_constset(np.loadtxt(os.path.join(DS, "constset.csv")))
+    assert cons.shape == (16, 5)
+    assert si.si_manvio_kind(si.si_manviofun) == si.C["RIPTRM_MANVIO_SI"]
+    assert si.si_manvio_kind(lambda p, x: 0) == si.C["RIPTRM_MANVIO_ZERO"]
+    with pytest.raises(NotImplementedError):
+        si.si_manvio_kind(lambda p, x: 1.0)
+    import shutil
+    d = tmp_path / "dataset" / "StableIdentification" / "1"
+    d.mkdir(parents=True)
+    for f in os.listdir(DS):
+        shutil.copy(os.path.join(DS, f), d / f)
+    prob = si.SICoordinator({"problem_name": "StableIdentification", "problem_instance": 1,
+                             "problem_initialpoint": "q"}, root=str(tmp_path)).run()
+    ref = SI.SIData.load(DS)
+    assert np.array_equal(prob.X, ref.X) and np.array_equal(prob.XP, ref.XP)
+    assert (prob.d, prob.N, prob.m, prob.manifold_dim) == (5, 95, 16, 40)
+    x0, y0 = SI.load_start(DS, "q")
+    assert np.array_equal(prob.point_array(), x0) and np.array_equal(prob.initialineqLagmult, y0)
+    with pytest.raises(RuntimeError):
+        si.SIBatch(5, 95, 16, 2)   # no GPU here: no CPU fallback
