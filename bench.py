@@ -91,6 +91,8 @@ def main():
     ap.add_argument("--batch", type=int, default=128, help="instances per GPU")
     ap.add_argument("--cpu-budget", type=float, default=25.0, help="seconds of CPU-baseline sampling (0 = skip)")
     ap.add_argument("--seed0", type=int, default=20251212)
+    ap.add_argument("--problem", default="nonnegpca", choices=["nonnegpca", "si"],
+                    help="si: StableIdentification (d=5 fixture, starts cycled + perturbed), one launch per solve")
     ap.add_argument("--stream-groups", type=int, default=0, choices=[0, 1, 2],
                     help="instance groups on separate streams (0 = library default)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_gemv.json"))
@@ -117,6 +119,12 @@ def main():
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
+
+    if args.problem == "si":
+        bench_si(args, world, rank, dev, dist)
+        if world > 1:
+            dist.destroy_process_group()
+        return
 
     import engine
     from problems import manviofun
@@ -239,6 +247,112 @@ def main():
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def si_starts(B: int, ids):
+    """StableIdentification batch: the fixture's 20 starts (dataset/StableIdentification/1, a..t)
+    cycled; copies beyond the first 20 perturbed (seeded by global id) so no two solves match:
+    J + 1e-3 skew noise, R and Q congruence-scaled by (I + 1e-3 sym noise), which keeps them SPD."""
+    import numpy as np
+    from oracle import si_oracle as SI
+    ds = os.path.join(ROOT, "tests", "golden", "si_1")
+    base = [SI.load_start(ds, p) for p in "abcdefghijklmnopqrst"]
+    xs, ys = [], []
+    for gid in ids:
+        x0, y0 = base[gid % 20]
+        x = x0.copy()
+        if gid >= 20:
+            rs = np.random.RandomState(1000 + gid)
+            a = rs.randn(5, 5) * 1e-3
+            x[0] = x[0] + (a - a.T) / 2
+            for k in (1, 2):
+                e = np.eye(5) + 1e-3 * (lambda b: (b + b.T) / 2)(rs.randn(5, 5))
+                x[k] = e @ x[k] @ e.T
+        xs.append(x)
+        ys.append(y0)
+    return np.stack(xs), np.stack(ys), SI.SIData.load(ds)
+
+
+def bench_si(args, world, rank, dev, dist):
+    """StableIdentification throughput: one HIP launch runs every instance's whole solve
+    (maxiter = warmup + steps); the timed launch is bracketed by barriers + syncs."""
+    import numpy as np
+    import torch
+    import si
+    B, W, K = args.batch, args.warmup, args.steps
+    ids = [rank + world * i for i in range(B)]
+    xs, ys, data = si_starts(B, ids)
+    cons = si.expand_constset(np.loadtxt(os.path.join(ROOT, "tests", "golden", "si_1", "constset.csv")))
+    eng = si.SIBatch(data.d, data.N, data.m, B, log_capacity=16)
+    eng.load(data.X, data.XP, data.h, cons)
+    opt = {"TRS_solver": "tCG", "manviofun": si.si_manviofun, "tolresid": 0.0, "maxtime": math.inf,
+           "maxiter": max(1, W), "save_inner_iteration": True}
+    eng.solve(xs, ys, opt)          # warmup launch (W outer iterations), untimed
+    opt["maxiter"] = K
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    e0.record()
+    eng.begin(xs, ys, opt)
+    e1.record()
+    torch.cuda.synchronize(dev)
+    el = time.perf_counter() - t0
+    if world > 1:
+        dist.barrier()
+    kern_s = e0.elapsed_time(e1) / 1e3
+    st = eng.stats()
+    # section breakdown from a second, instrumented launch (device clock per section)
+    eng.profile_enable(True)
+    eng.begin(xs, ys, opt)
+    sec = eng.profile_read()
+    eng.profile_enable(False)
+    secfrac = {k: (v / sec["total"] if sec["total"] > 0 else None) for k, v in sec.items() if k != "total"}
+    C = si.C
+    tot = lambda f: float(st[:, C[f"RIPTRM_STAT_{f}"]].sum())
+    counts = torch.tensor([tot("OUTER_ITERS"), tot("INNER_ITERS"), tot("TCG_ITERS"), tot("PASSES")],
+                          dtype=torch.float64, device=dev)
+    tmax = torch.tensor([el], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(counts, op=dist.ReduceOp.SUM)
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+    outer, inner, tcg, hvps = [float(v) for v in counts.tolist()]
+    T = float(tmax.item())
+    if rank != 0:
+        return
+    cpu = None
+    if args.cpu_budget > 0 and world == 1:
+        from oracle import riptrm_oracle as RO
+        from oracle import si_oracle as SI
+        orc = RO.RIPTRMOracle(dict(maxiter=K, tolresid=0.0, maxtime=1e12, manviofun=SI.si_manvio),
+                              deadline=time.time() + args.cpu_budget)
+        try:
+            orc.run(SI.SIVectorized(data), xs[0], ys[0])
+        except RO.BudgetExceeded:
+            pass
+        heads = orc.outer_heads
+        last = max(heads)
+        if last > 0:
+            cpu = {"value": last / heads[last], "unit": "outer iterations/s", "cores": 1, "kind": "port",
+                   "sample": f"oracle/si_oracle.py SIVectorized (NumPy, closed-form Lagrangian), start 'a', outer "
+                             f"iterations 1..{last} ({heads[last]:.1f} s, evaluation time excluded as RIPTRM.py:932-941)"}
+    print(json.dumps({
+        "metric": f"outer RIPTRM iterations/sec, StableIdentification d=5 (Product(Skew,SPD,SPD)), batch {B}/GPU",
+        "value": outer / T, "unit": "outer iterations/s", "n_gpus": world, "steps": K, "warmup": W,
+        "ms_per_step": T / K * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "f64",
+        "data": "reference fixture dataset/StableIdentification/1 (noisy X, 16 constraints), starts a..t cycled + perturbed",
+        "config": {"workload": f"StableIdentification d=5 N=95 m=16, {B} starts per GPU, outer iterations 1..{K}",
+                   "global_batch": B * world, "parallelism": f"instance-sharded x{world}"},
+        "roofline": {"bound": "latency", "achieved": hvps / kern_s / 1e6, "peak": None, "unit": "M HVP/s",
+                     "frac": None, "traffic": None,
+                     "kernel": "k_si (one 64-lane workgroup per instance, whole solve per launch)",
+                     "kernel_ms": kern_s * 1e3},
+        "cpu_baseline": cpu,
+        "detail": {"inner_iterations_per_s": inner / T, "tcg_iterations_per_s": tcg / T, "hvps_per_s": hvps / T,
+                   "section_fraction": secfrac, "us_per_hvp_per_instance": sec["hvp"] / max(1.0, tot("PASSES")) * 1e6},
+    }), flush=True)
 
 
 if __name__ == "__main__":

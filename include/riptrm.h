@@ -252,6 +252,18 @@ int riptrm_si_hvp(riptrm_ctx* ctx, const double* x, const double* y, const doubl
  * stats TCG_LAST_J / TCG_LAST_STOP.  tCG options from opt (NULL = RIPTRM defaults).  Asynchronous. */
 int riptrm_si_tcg(riptrm_ctx* ctx, const riptrm_options* opt, const double* x, const double* y,
                   const double* mu, const double* delta);
+/* Section timing of riptrm_si_solve (device clock, summed over the batch's instances). */
+enum riptrm_si_prof_field {
+    RIPTRM_SI_PROF_TOTAL = 0, RIPTRM_SI_PROF_PREPARE, RIPTRM_SI_PROF_TCG, RIPTRM_SI_PROF_HVP,
+    RIPTRM_SI_PROF_TRIAL, RIPTRM_SI_PROF_EVAL, RIPTRM_SI_PROF_NFIELDS_USED
+};
+#define RIPTRM_SI_PROF_NFIELDS 8
+/* Enable (allocates a batch x RIPTRM_SI_PROF_NFIELDS buffer, zeroed) or disable section timing of
+ * the following riptrm_si_solve launches. */
+int riptrm_si_profile_enable(riptrm_ctx* ctx, int32_t on);
+/* seconds[RIPTRM_SI_PROF_NFIELDS]: per-section device time summed over instances.  Synchronises. */
+int riptrm_si_profile_read(riptrm_ctx* ctx, double* seconds);
+
 /* Whole RIPTRM solves (RIPTRM.py:909-976) from x0 (batch x 3 d d), y0 (batch x m); tables as in
  * riptrm_solve_begin.  One launch, asynchronous: synchronise the stream, then read the workspace. */
 int riptrm_si_solve(riptrm_ctx* ctx, const riptrm_options* opt, const double* x0, const double* y0,

@@ -47,6 +47,7 @@ struct SIParams {
   double* escr;    // batch x d x N residual scratch
   double* stats;   // batch x RIPTRM_STAT_NFIELDS
   double* log;     // batch x cap x RIPTRM_LOG_NFIELDS
+  double* prof;    // optional: batch x RIPTRM_SI_PROF_NFIELDS device-clock ticks per section
   const double* in_x;
   const double* in_y;
   const double* in_mu;
@@ -125,13 +126,186 @@ struct Info {  // inner-iteration record of solver_status (RIPTRM.py:986-1023)
   double has, num, status, tr, dxtype, normdx, minx, miny, compl_, hasratio, ratio, ru, dc;
 };
 
+// ---- serial d x d linear algebra on ONE lane, register arrays, fully unrolled for D ---------
+// (numpy.linalg.solve / inv, cholesky and eigvalsh analogues; evaluation-only except inv)
+template <int D>
+__device__ __forceinline__ void inv_reg(const double (&a0)[D * D], double (&out)[D * D]) {
+  double a[D * D];
+#pragma unroll
+  for (int i = 0; i < D * D; ++i) { a[i] = a0[i]; out[i] = 0.0; }
+#pragma unroll
+  for (int i = 0; i < D; ++i) out[i * D + i] = 1.0;
+#pragma unroll
+  for (int k = 0; k < D; ++k) {  // Gauss-Jordan with partial pivoting
+    int p = k;
+    double best = fabs(a[k * D + k]);
+#pragma unroll
+    for (int r = k + 1; r < D; ++r) {
+      const double v = fabs(a[r * D + k]);
+      if (v > best) { best = v; p = r; }
+    }
+#pragma unroll
+    for (int r = k + 1; r < D; ++r)
+      if (r == p) {
+#pragma unroll
+        for (int c = 0; c < D; ++c) {
+          double t = a[k * D + c]; a[k * D + c] = a[r * D + c]; a[r * D + c] = t;
+          t = out[k * D + c]; out[k * D + c] = out[r * D + c]; out[r * D + c] = t;
+        }
+      }
+    const double piv = a[k * D + k];
+#pragma unroll
+    for (int c = 0; c < D; ++c) { a[k * D + c] = a[k * D + c] / piv; out[k * D + c] = out[k * D + c] / piv; }
+#pragma unroll
+    for (int r = 0; r < D; ++r) {
+      if (r == k) continue;
+      const double f = a[r * D + k];
+#pragma unroll
+      for (int c = 0; c < D; ++c) {
+        a[r * D + c] = a[r * D + c] - f * a[k * D + c];
+        out[r * D + c] = out[r * D + c] - f * out[k * D + c];
+      }
+    }
+  }
+}
+
+// cyclic Jacobi: eigenvalues of symmetric a end on its diagonal
+template <int D>
+__device__ __forceinline__ void jacobi_reg(double (&a)[D * D]) {
+  for (int sweep = 0; sweep < 60; ++sweep) {
+    double off = 0.0, dg = 0.0;
+#pragma unroll
+    for (int p = 0; p < D; ++p) {
+      dg += a[p * D + p] * a[p * D + p];
+#pragma unroll
+      for (int q = p + 1; q < D; ++q) off += a[p * D + q] * a[p * D + q];
+    }
+    if (off <= 1e-36 * dg) break;   // converged far below the eigenvalues' rounding
+#pragma unroll
+    for (int p = 0; p < D; ++p)
+#pragma unroll
+      for (int q = p + 1; q < D; ++q) {
+        const double apq = a[p * D + q];
+        if (apq != 0.0) {
+          const double app = a[p * D + p], aqq = a[q * D + q];
+          const double theta = (aqq - app) / (2.0 * apq);
+          const double t = (theta >= 0.0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
+          const double c = 1.0 / sqrt(t * t + 1.0), s = t * c;
+#pragma unroll
+          for (int k = 0; k < D; ++k) {
+            const double akp = a[k * D + p], akq = a[k * D + q];
+            a[k * D + p] = c * akp - s * akq;
+            a[k * D + q] = s * akp + c * akq;
+          }
+#pragma unroll
+          for (int k = 0; k < D; ++k) {
+            const double apk = a[p * D + k], aqk = a[q * D + k];
+            a[p * D + k] = c * apk - s * aqk;
+            a[q * D + k] = s * apk + c * aqk;
+          }
+        }
+      }
+  }
+}
+
+// all eigenvalues of symmetric a > 0 (numpy.linalg.eigvalsh reads the lower triangle)
+template <int D>
+__device__ __forceinline__ bool pd_reg(double (&a)[D * D]) {
+#pragma unroll
+  for (int i = 0; i < D; ++i)
+#pragma unroll
+    for (int j = i + 1; j < D; ++j) a[i * D + j] = a[j * D + i];
+  jacobi_reg<D>(a);
+  bool pd = true;
+#pragma unroll
+  for (int i = 0; i < D; ++i) pd = pd && (a[i * D + i] > 0.0);
+  return pd;
+}
+
+// pymanopt SPD dist: ||logm(C^-1 B C^-T)||_F, C = cholesky(A); NaN if A is not PD
+template <int D>
+__device__ __forceinline__ double spd_dist_reg(const double (&A)[D * D], const double (&B)[D * D]) {
+  double Cm[D * D];
+#pragma unroll
+  for (int i = 0; i < D * D; ++i) Cm[i] = 0.0;
+  bool ok = true;
+#pragma unroll
+  for (int j = 0; j < D; ++j) {
+    double s = A[j * D + j];
+#pragma unroll
+    for (int k = 0; k < j; ++k) s -= Cm[j * D + k] * Cm[j * D + k];
+    ok = ok && (s > 0.0);
+    const double cjj = sqrt(s > 0.0 ? s : 1.0);
+    Cm[j * D + j] = cjj;
+#pragma unroll
+    for (int i = j + 1; i < D; ++i) {
+      double t = A[i * D + j];
+#pragma unroll
+      for (int k = 0; k < j; ++k) t -= Cm[i * D + k] * Cm[j * D + k];
+      Cm[i * D + j] = t / cjj;
+    }
+  }
+  double Ci[D * D];  // C^-1, lower triangular
+#pragma unroll
+  for (int i = 0; i < D * D; ++i) Ci[i] = 0.0;
+#pragma unroll
+  for (int j = 0; j < D; ++j) {
+    Ci[j * D + j] = 1.0 / Cm[j * D + j];
+#pragma unroll
+    for (int i = j + 1; i < D; ++i) {
+      double t = 0.0;
+#pragma unroll
+      for (int k = j; k < i; ++k) t -= Cm[i * D + k] * Ci[k * D + j];
+      Ci[i * D + j] = t / Cm[i * D + i];
+    }
+  }
+  double T[D * D];   // B Ci^T
+#pragma unroll
+  for (int i = 0; i < D; ++i)
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+      double t = 0.0;
+#pragma unroll
+      for (int k = 0; k < D; ++k) t += B[i * D + k] * Ci[j * D + k];
+      T[i * D + j] = t;
+    }
+  double M[D * D];   // Ci (B Ci^T)
+#pragma unroll
+  for (int i = 0; i < D; ++i)
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+      double t = 0.0;
+#pragma unroll
+      for (int k = 0; k < D; ++k) t += Ci[i * D + k] * T[k * D + j];
+      M[i * D + j] = t;
+    }
+#pragma unroll
+  for (int i = 0; i < D; ++i)
+#pragma unroll
+    for (int j = i + 1; j < D; ++j) {
+      const double sm = 0.5 * (M[i * D + j] + M[j * D + i]);
+      M[i * D + j] = sm;
+      M[j * D + i] = sm;
+    }
+  jacobi_reg<D>(M);
+  double s2 = 0.0;
+#pragma unroll
+  for (int i = 0; i < D; ++i) {
+    const double lg = log(M[i * D + i]);
+    s2 += lg * lg;
+  }
+  return ok ? sqrt(s2) : NAN;
+}
+
+template <int D>
 struct Eng {
+  static constexpr int d = D, dd = D * D;
   const SIParams& P;
-  const int b, l, d, dd, m, N;
+  const int b, l, m, N;
   const int li, lj;
   const bool act, cact;
   double* sh;      // LDS staging: 2 x 64 doubles
-  double* ser;     // LDS serial scratch: 4 x 64 doubles (lane 0 only)
+  double* ser;     // LDS scratch for the per-lane serial solvers: 8 x 64 doubles
   int* cr_s;       // LDS constraint rows / cols / kinds
   int* cc_s;
   // constraint of this lane (l < m)
@@ -141,10 +315,12 @@ struct Eng {
   const double* Xd;
   const double* XPd;
   double* E;
+  double pt[RIPTRM_SI_PROF_NFIELDS];   // section tick totals (riptrm_si_profile_*)
+  __device__ __forceinline__ double tick() const { return P.prof ? (double)wall_clock64() : 0.0; }
 
-  __device__ Eng(const SIParams& P_, int b_, double* sh_, double* ser_, int* crs, int* ccs)
-      : P(P_), b(b_), l((int)threadIdx.x), d(P_.d), dd(P_.d * P_.d), m(P_.m), N(P_.N),
-        li((int)threadIdx.x / P_.d), lj((int)threadIdx.x % P_.d), act((int)threadIdx.x < P_.d * P_.d),
+  __device__ __forceinline__ Eng(const SIParams& P_, int b_, double* sh_, double* ser_, int* crs, int* ccs)
+      : P(P_), b(b_), l((int)threadIdx.x), m(P_.m), N(P_.N),
+        li((int)threadIdx.x / D), lj((int)threadIdx.x % D), act((int)threadIdx.x < D * D),
         cact((int)threadIdx.x < P_.m), sh(sh_), ser(ser_), cr_s(crs), cc_s(ccs) {
     Xd = P.X + (int64_t)b * P.data_stride;
     XPd = P.XP + (int64_t)b * P.data_stride;
@@ -165,6 +341,8 @@ struct Eng {
     if (act)
       for (int t = 0; t < N; ++t) acc = acc + Xd[li * N + t] * Xd[lj * N + t];
     M2 = acc;
+#pragma unroll
+    for (int k = 0; k < RIPTRM_SI_PROF_NFIELDS; ++k) pt[k] = 0.0;
     __syncthreads();
   }
 
@@ -183,7 +361,8 @@ struct Eng {
     __syncthreads();
     double acc = 0.0;
     if (act) {
-      for (int k = 0; k < d; ++k) {
+#pragma unroll
+      for (int k = 0; k < D; ++k) {
         const double av = ta ? sh[k * d + li] : sh[li * d + k];
         const double bv = tb ? sh[W + lj * d + k] : sh[W + k * d + lj];
         acc = acc + av * bv;
@@ -196,168 +375,69 @@ struct Eng {
   __device__ __forceinline__ double skew(double a) { return 0.5 * (a - tr(a)); }
   __device__ __forceinline__ double elem(double a, int i, int j) { return lane_read(a, i * d + j); }
 
-  // inverse by Gauss-Jordan with partial pivoting (numpy.linalg.solve / inv analogue)
-  __device__ double inv(double a) {
-    double* g = ser;  // d x 2d augmented, row-major
-    if (act) {
-      g[li * 2 * d + lj] = a;
-      g[li * 2 * d + d + lj] = (li == lj) ? 1.0 : 0.0;
-    }
-    __syncthreads();
-    if (l == 0) {
-      for (int k = 0; k < d; ++k) {
-        int p = k;
-        double best = fabs(g[k * 2 * d + k]);
-        for (int r = k + 1; r < d; ++r) {
-          const double v = fabs(g[r * 2 * d + k]);
-          if (v > best) { best = v; p = r; }
-        }
-        if (p != k)
-          for (int c = 0; c < 2 * d; ++c) {
-            const double t = g[k * 2 * d + c];
-            g[k * 2 * d + c] = g[p * 2 * d + c];
-            g[p * 2 * d + c] = t;
-          }
-        const double piv = g[k * 2 * d + k];
-        for (int c = 0; c < 2 * d; ++c) g[k * 2 * d + c] = g[k * 2 * d + c] / piv;
-        for (int r = 0; r < d; ++r) {
-          if (r == k) continue;
-          const double f = g[r * 2 * d + k];
-          if (f != 0.0)
-            for (int c = 0; c < 2 * d; ++c) g[r * 2 * d + c] = g[r * 2 * d + c] - f * g[k * 2 * d + c];
-        }
-      }
-    }
-    __syncthreads();
-    const double v = act ? g[li * 2 * d + d + lj] : 0.0;
-    __syncthreads();
-    return v;
+  // stage blocks into LDS slots (slot k = ser + k*W), every lane
+  __device__ __forceinline__ void stage(int slot, double a) {
+    if (act) ser[slot * W + l] = a;
   }
-
-  // eigenvalues of a symmetric d x d matrix (cyclic Jacobi on lane 0); result in ser[3*W + i]
-  __device__ void eigvalsh_lane0(double* a) {
-    for (int sweep = 0; sweep < 60; ++sweep) {
-      double off = 0.0, dg = 0.0;
-      for (int p = 0; p < d; ++p) {
-        dg += a[p * d + p] * a[p * d + p];
-        for (int q = p + 1; q < d; ++q) off += a[p * d + q] * a[p * d + q];
-      }
-      if (off <= 1e-36 * dg) break;   // converged to far below the eigenvalues' rounding
-      for (int p = 0; p < d; ++p)
-        for (int q = p + 1; q < d; ++q) {
-          const double apq = a[p * d + q];
-          if (apq == 0.0) continue;
-          const double app = a[p * d + p], aqq = a[q * d + q];
-          const double theta = (aqq - app) / (2.0 * apq);
-          const double t = (theta >= 0.0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
-          const double c = 1.0 / sqrt(t * t + 1.0), s = t * c;
-          for (int k = 0; k < d; ++k) {
-            const double akp = a[k * d + p], akq = a[k * d + q];
-            a[k * d + p] = c * akp - s * akq;
-            a[k * d + q] = s * akp + c * akq;
-          }
-          for (int k = 0; k < d; ++k) {
-            const double apk = a[p * d + k], aqk = a[q * d + k];
-            a[p * d + k] = c * apk - s * aqk;
-            a[q * d + k] = s * apk + c * aqk;
-          }
-        }
-    }
+  __device__ __forceinline__ void load_reg(int slot, double (&r)[D * D]) {
+#pragma unroll
+    for (int i = 0; i < D * D; ++i) r[i] = ser[slot * W + i];
   }
-
-  // ||logm(chol(a)^-1 b chol(a)^-T)||_F (pymanopt SPD dist), all lanes get the value
-  __device__ double spd_dist(double a, double bm) {
-    double* A = ser;
-    double* B = ser + W;
-    double* Cm = ser + 2 * W;
-    if (act) { A[l] = a; B[l] = bm; }
+  // R^-1 and Q^-1 at once: lane 0 inverts slot 0, lane 1 slot 1 (Gauss-Jordan, partial pivoting)
+  __device__ __forceinline__ void inv2(double r, double q, double& ri, double& qi) {
+    stage(0, r);
+    stage(1, q);
     __syncthreads();
-    if (l == 0) {
-      // Cholesky a = C C^T (lower)
-      for (int i = 0; i < d * d; ++i) Cm[i] = 0.0;
-      bool ok = true;
-      for (int j = 0; j < d && ok; ++j) {
-        double s = A[j * d + j];
-        for (int k = 0; k < j; ++k) s -= Cm[j * d + k] * Cm[j * d + k];
-        if (!(s > 0.0)) { ok = false; break; }
-        const double cjj = sqrt(s);
-        Cm[j * d + j] = cjj;
-        for (int i = j + 1; i < d; ++i) {
-          double t = A[i * d + j];
-          for (int k = 0; k < j; ++k) t -= Cm[i * d + k] * Cm[j * d + k];
-          Cm[i * d + j] = t / cjj;
-        }
-      }
-      double res = NAN;
-      if (ok) {
-        // Ci = C^-1 (lower), stored in A
-        for (int i = 0; i < d * d; ++i) A[i] = 0.0;
-        for (int j = 0; j < d; ++j) {
-          A[j * d + j] = 1.0 / Cm[j * d + j];
-          for (int i = j + 1; i < d; ++i) {
-            double t = 0.0;
-            for (int k = j; k < i; ++k) t -= Cm[i * d + k] * A[k * d + j];
-            A[i * d + j] = t / Cm[i * d + i];
-          }
-        }
-        // M = Ci B Ci^T into Cm, symmetrised
-        for (int i = 0; i < d; ++i)
-          for (int j = 0; j < d; ++j) {
-            double t = 0.0;
-            for (int k = 0; k < d; ++k) {
-              double u = 0.0;
-              for (int q = 0; q < d; ++q) u += B[k * d + q] * A[j * d + q];
-              t += A[i * d + k] * u;
-            }
-            Cm[i * d + j] = t;
-          }
-        for (int i = 0; i < d; ++i)
-          for (int j = i + 1; j < d; ++j) {
-            const double s = 0.5 * (Cm[i * d + j] + Cm[j * d + i]);
-            Cm[i * d + j] = s;
-            Cm[j * d + i] = s;
-          }
-        eigvalsh_lane0(Cm);
-        double s2 = 0.0;
-        for (int i = 0; i < d; ++i) {
-          const double lg = log(Cm[i * d + i]);
-          s2 += lg * lg;
-        }
-        res = sqrt(s2);
-      }
-      ser[3 * W] = res;
+    if (l < 2) {
+      double a[D * D], o[D * D];
+      load_reg(l, a);
+      inv_reg<D>(a, o);
+#pragma unroll
+      for (int i = 0; i < D * D; ++i) ser[(2 + l) * W + i] = o[i];
     }
     __syncthreads();
-    const double v = ser[3 * W];
+    ri = act ? ser[2 * W + l] : 0.0;
+    qi = act ? ser[3 * W + l] : 0.0;
     __syncthreads();
-    return v;
   }
-
-  // all eigenvalues of symmetric a positive? (numpy.linalg.eigvalsh(a) > 0 for every value)
-  __device__ bool spd_pd(double a) {
-    double* A = ser;
-    if (act) A[l] = a;
+  // evaluation's dense solvers, four lanes in parallel: PD(R), PD(Q), dist(Rp,R), dist(Qp,Q)
+  __device__ __forceinline__ void eval_solvers(double rp, double r, double qp, double q, bool& pdr, bool& pdq, double& dR, double& dQ) {
+    stage(0, r);
+    stage(1, q);
+    stage(2, rp);
+    stage(3, qp);
     __syncthreads();
-    if (l == 0) {
-      // eigvalsh reads the lower triangle
-      for (int i = 0; i < d; ++i)
-        for (int j = i + 1; j < d; ++j) A[i * d + j] = A[j * d + i];
-      eigvalsh_lane0(A);
-      bool pd = true;
-      for (int i = 0; i < d; ++i) pd = pd && (A[i * d + i] > 0.0);
-      ser[3 * W] = pd ? 1.0 : 0.0;
+    if (l < 4) {
+      double a[D * D];
+      double res;
+      if (l < 2) {
+        load_reg(l, a);
+        res = pd_reg<D>(a) ? 1.0 : 0.0;
+      } else {
+        double bm[D * D];
+        load_reg(l, a);        // previous point (Cholesky factor side)
+        load_reg(l - 2, bm);   // current point
+        res = spd_dist_reg<D>(a, bm);
+      }
+      ser[4 * W + l] = res;
     }
     __syncthreads();
-    const bool v = ser[3 * W] != 0.0;
+    pdr = ser[4 * W + 0] != 0.0;
+    pdq = ser[4 * W + 1] != 0.0;
+    dR = ser[4 * W + 2];
+    dQ = ser[4 * W + 3];
     __syncthreads();
-    return v;
   }
 
   // ---- manifold (pymanopt Product(SkewSymmetric, SPD, SPD)) ---------------------------------
   struct Metric {
     double XiR, XiQ;  // R^-1, Q^-1 at the base point
   };
-  __device__ __forceinline__ Metric metric(PV x) { return Metric{inv(x.r), inv(x.q)}; }
+  __device__ __forceinline__ Metric metric(PV x) {
+    Metric g;
+    inv2(x.r, x.q, g.XiR, g.XiQ);
+    return g;
+  }
   __device__ __forceinline__ double spd_inner(double Xi, double u, double v) {
     const double pu = mm(Xi, u);
     const double pv = mm(Xi, v);
@@ -412,7 +492,7 @@ struct Eng {
     return act ? acc : 0.0;
   }
   // f(x) and G_f = df/dA = -(2h/N) E X^T (E kept in the instance's scratch)
-  __device__ void cost_grad(double A, double& f, double& Gf) {
+  __device__ __forceinline__ void cost_grad(double A, double& f, double& Gf) {
     const double At = ((li == lj) ? 1.0 : 0.0) + P.h * A;
     sh[l] = act ? At : 0.0;
     __syncthreads();
@@ -443,7 +523,7 @@ struct Eng {
     double s, w, y;  // constraint lanes
     PV c;            // cxCur
   };
-  __device__ void prepare(AtX& a, PV x, double y, double mu) {
+  __device__ __forceinline__ void prepare(AtX& a, PV x, double y, double mu) {
     a.x = x;
     a.y = y;
     a.g = metric(x);
@@ -471,7 +551,7 @@ struct Eng {
     return cact ? -(a.w * da) : 0.0;
   }
   // HwCur(v) = HessL[v] + Gx(y Gxaj(v) / s)
-  __device__ PV hw(const AtX& a, PV v) {
+  __device__ __forceinline__ PV hw(const AtX& a, PV v) {
     const PV x = a.x;
     const double dA = dAof(a, v);
     double dG = (2.0 * P.h * P.h / (double)N) * mm(dA, M2);
@@ -500,7 +580,7 @@ struct Eng {
     return pv_add(hl, gx);
   }
   // gradLagrangefun (RIPTRM.py:475-489) and its norm at (x, y)
-  __device__ double gradlag_norm(PV x, double y, double& f_out, double& A_out) {
+  __device__ __forceinline__ double gradlag_norm(PV x, double y, double& f_out, double& A_out) {
     const Metric g = metric(x);
     const double A = Aof(x);
     double f, Gf;
@@ -514,7 +594,7 @@ struct Eng {
   }
 
   // ---- tCG, RIPTRM.py:41-216 (eta0 = 0, identity preconditioner) ----------------------------
-  __device__ int tcg(const AtX& a, double Delta, PV& eta, PV& Heta, int& jout, double& hvps) {
+  __device__ __forceinline__ int tcg(const AtX& a, double Delta, PV& eta, PV& Heta, int& jout, double& hvps) {
     const double theta = P.opt.tcg_theta, kappa = P.opt.tcg_kappa;
     const int mininner = P.opt.tcg_mininner;
     const int maxinner = P.d * (P.d - 1) / 2 + P.d * (P.d + 1);  // manifold.dim
@@ -534,7 +614,9 @@ struct Eng {
     int stop = RIPTRM_TCG_MAX_INNER_ITER;
     int j = 0;
     for (j = 0; j < maxinner; ++j) {
+      const double th0 = tick();
       const PV Hd = hw(a, delta);
+      pt[RIPTRM_SI_PROF_HVP] += tick() - th0;
       hvps += 1.0;
       const double d_Hd = inner(a.g, delta, Hd);
       double alpha = 0.0, e_Pe_new;
@@ -586,7 +668,7 @@ struct Eng {
 
   // ---- evaluation, src/solver/utils.py:342-368 (+ compute_residual :269-340) ----------------
   // ev: cost, distance, residual, gradnorm, complvio, dualvio, manvio, maxvio, meanvio, maxabsy
-  __device__ void evaluation(PV xprev, PV x, double y, double (&ev)[10]) {
+  __device__ __forceinline__ void evaluation(PV xprev, PV x, double y, double (&ev)[10]) {
     double f, A;
     const double gradnorm = gradlag_norm(x, y, f, A);
     const double g = cons_val(A);
@@ -603,14 +685,13 @@ struct Eng {
     if (P.opt.manvio_kind == RIPTRM_MANVIO_SI) {
       const double aj = x.j + tr(x.j), ar = x.r - tr(x.r), aq = x.q - tr(x.q);
       manvio = (sqrt(wsum(aj * aj)) + sqrt(wsum(ar * ar))) + sqrt(wsum(aq * aq));
-      const bool pr = spd_pd(x.r);
-      const bool pq = spd_pd(x.q);
-      if (!pr || !pq) manvio = INFINITY;
     }
+    bool pr, pq;
+    double dR, dQ;
+    eval_solvers(xprev.r, x.r, xprev.q, x.q, pr, pq, dR, dQ);
+    if (P.opt.manvio_kind == RIPTRM_MANVIO_SI && (!pr || !pq)) manvio = INFINITY;
     const double dj = x.j - xprev.j;
     const double dJ = sqrt(wsum(dj * dj));
-    const double dR = spd_dist(xprev.r, x.r);
-    const double dQ = spd_dist(xprev.q, x.q);
     ev[0] = f;
     ev[1] = sqrt((dJ * dJ + dR * dR) + dQ * dQ);
     ev[2] = sqrt(((((gradnorm * gradnorm + sq_compl) + sq_nonneg) + sq_ineq) + 0.0) + manvio * manvio);
@@ -628,7 +709,7 @@ struct Eng {
     return wmax(t);
   }
 
-  __device__ void log_row(const double (&ev)[10], double outer_it, double mu, const Info* inf, double tcg_iters,
+  __device__ __forceinline__ void log_row(const double (&ev)[10], double outer_it, double mu, const Info* inf, double tcg_iters,
                           double t_now, double t_start, double& count, double& overflow) {
     if (l == 0) {
       const int cnt = (int)count;
@@ -689,7 +770,7 @@ struct Eng {
   }
 
   // ---- the whole run: RIPTRM.run / outer_step / inner_run / inner_step ----------------------
-  __device__ void solve() {
+  __device__ __forceinline__ void solve() {
     const int64_t v3 = 3LL * dd;
     PV x = load_pv(P.in_x + b * v3);
     double y = cact ? P.in_y[(int64_t)b * m + l] : 0.0;
@@ -699,6 +780,7 @@ struct Eng {
     double inner_total = 0.0, tcg_total = 0.0, hvps = 0.0, log_count = 0.0, log_over = 0.0;
     double stop_code = RIPTRM_STOP_NONE, stop_rt = 0.0, residual = 0.0, last_j = 0.0, last_stop = 0.0;
     const double t_start = now();
+    const double t_tick0 = (double)wall_clock64();
     PV xPrev = x;   // inner_run's xPrev (RIPTRM.py:787)
     PV xHead = x;   // run's xPrev: the point at the previous outer head (RIPTRM.py:929, :947)
     Info info{};
@@ -746,11 +828,16 @@ struct Eng {
       while (true) {  // inner_run, RIPTRM.py:785-847
         inner_it += 1.0;
         const double DeltaStep = Delta;
+        double tq = tick();
         AtX a;
         prepare(a, x, y, mu);
+        pt[RIPTRM_SI_PROF_PREPARE] += tick() - tq;
+        tq = tick();
         PV eta, Heta;
         int jj = 0;
         const int tstop = tcg(a, Delta, eta, Heta, jj, hvps);
+        pt[RIPTRM_SI_PROF_TCG] += tick() - tq;
+        tq = tick();
         tcg_total += (double)jj + 1.0;
         last_j = jj;
         last_stop = tstop;
@@ -832,12 +919,15 @@ struct Eng {
           Delta = Dn;
         }
         // inner_run tail, RIPTRM.py:810-847
+        pt[RIPTRM_SI_PROF_TRIAL] += tick() - tq;
+        tq = tick();
         inner_total += 1.0;
         tn = now();
         if (save_inner) {
           evaluation(xPrev, x, y, ev);
           log_row(ev, outer_it, mu, &info, last_j + 1.0, tn, t_start, log_count, log_over);
         }
+        pt[RIPTRM_SI_PROF_EVAL] += tick() - tq;
         xPrev = x;
         bool exitflag = converged;
         double rti, lim;
@@ -885,10 +975,14 @@ struct Eng {
       o[RIPTRM_STAT_TR_RADIUS] = Delta;
       o[RIPTRM_STAT_TCG_LAST_J] = last_j;
       o[RIPTRM_STAT_TCG_LAST_STOP] = last_stop;
+      if (P.prof) {
+        pt[RIPTRM_SI_PROF_TOTAL] = (double)wall_clock64() - t_tick0;
+        for (int k = 0; k < RIPTRM_SI_PROF_NFIELDS; ++k) P.prof[(int64_t)b * RIPTRM_SI_PROF_NFIELDS + k] = pt[k];
+      }
     }
   }
 
-  __device__ void op_hvp() {
+  __device__ __forceinline__ void op_hvp() {
     const int64_t v3 = 3LL * dd;
     const PV x = load_pv(P.in_x + b * v3);
     const double y = cact ? P.in_y[(int64_t)b * m + l] : 0.0;
@@ -899,7 +993,7 @@ struct Eng {
     store_pv(P.out_v + b * v3, h);
   }
 
-  __device__ void op_tcg() {
+  __device__ __forceinline__ void op_tcg() {
     const int64_t v3 = 3LL * dd;
     const PV x = load_pv(P.in_x + b * v3);
     const double y = cact ? P.in_y[(int64_t)b * m + l] : 0.0;
@@ -920,13 +1014,14 @@ struct Eng {
   }
 };
 
+template <int D>
 __global__ void __launch_bounds__(W) k_si(SIParams P) {
   __shared__ double sh[2 * W];
-  __shared__ double ser[4 * W];
+  __shared__ double ser[8 * W];
   __shared__ int crs[MMAX], ccs[MMAX];
   const int b = blockIdx.x;
   if (b >= P.batch) return;
-  Eng e(P, b, sh, ser, crs, ccs);
+  Eng<D> e(P, b, sh, ser, crs, ccs);
   if (P.mode == MODE_SOLVE) e.solve();
   else if (P.mode == MODE_HVP) e.op_hvp();
   else e.op_tcg();
@@ -937,13 +1032,18 @@ struct Bound {
   int batch = 0, cap = 0;
   Layout L{};
   char* ws = nullptr;
+  double* prof = nullptr;   // device, batch x RIPTRM_SI_PROF_NFIELDS (riptrm_si_profile_enable)
+  bool prof_on = false;
 };
 
 }  // namespace riptrm_si
 
 using namespace riptrm_si;
 
-void riptrm_si_release(riptrm_si::Bound* s) { delete s; }
+void riptrm_si_release(riptrm_si::Bound* s) {
+  if (s && s->prof) (void)hipFree(s->prof);
+  delete s;
+}
 
 static bool si_dims_ok(int32_t d, int32_t N, int32_t m, int32_t batch, int32_t cap) {
   return d >= 1 && d <= DMAX && N >= 1 && m >= 1 && m <= MMAX && batch >= 1 && cap >= 0;
@@ -973,6 +1073,7 @@ static SIParams si_params(riptrm_ctx* c, int mode) {
   P.escr = (double*)(s->ws + s->L.off_escr);
   P.stats = (double*)(s->ws + s->L.off_stats);
   P.log = (double*)(s->ws + s->L.off_log);
+  P.prof = s->prof_on ? s->prof : nullptr;
   P.opt.struct_size = (int32_t)sizeof(riptrm_options);
   P.opt.tcg_theta = 1.0;   // RIPTRM.py:330-332 defaults for the operator entry points
   P.opt.tcg_kappa = 0.1;
@@ -981,7 +1082,17 @@ static SIParams si_params(riptrm_ctx* c, int mode) {
 }
 
 static int si_launch(riptrm_ctx* c, const SIParams& P) {
-  hipLaunchKernelGGL(k_si, dim3((unsigned)P.batch), dim3(W), 0, c->stream, P);
+  const dim3 g((unsigned)P.batch), t(W);
+  switch (P.d) {  // the block size is a template parameter: unrolled products, register solvers
+    case 1: hipLaunchKernelGGL(k_si<1>, g, t, 0, c->stream, P); break;
+    case 2: hipLaunchKernelGGL(k_si<2>, g, t, 0, c->stream, P); break;
+    case 3: hipLaunchKernelGGL(k_si<3>, g, t, 0, c->stream, P); break;
+    case 4: hipLaunchKernelGGL(k_si<4>, g, t, 0, c->stream, P); break;
+    case 5: hipLaunchKernelGGL(k_si<5>, g, t, 0, c->stream, P); break;
+    case 6: hipLaunchKernelGGL(k_si<6>, g, t, 0, c->stream, P); break;
+    case 7: hipLaunchKernelGGL(k_si<7>, g, t, 0, c->stream, P); break;
+    default: hipLaunchKernelGGL(k_si<8>, g, t, 0, c->stream, P); break;
+  }
   HIPCHK(c, hipGetLastError());
   return RIPTRM_OK;
 }
@@ -1026,6 +1137,11 @@ int riptrm_si_bind(riptrm_ctx* ctx, const riptrm_si_problem* prob, int32_t batch
   HIPCHK(ctx, hipSetDevice(ctx->device));
   HIPCHK(ctx, hipMemsetAsync(ws, 0, (size_t)L.total, ctx->stream));
   if (!ctx->si) ctx->si = new Bound();
+  if (ctx->si->prof && ctx->si->batch != batch) {
+    (void)hipFree(ctx->si->prof);
+    ctx->si->prof = nullptr;
+    ctx->si->prof_on = false;
+  }
   ctx->si->prob = *prob;
   ctx->si->batch = batch;
   ctx->si->cap = cap;
@@ -1084,6 +1200,34 @@ int riptrm_si_solve(riptrm_ctx* ctx, const riptrm_options* opt, const double* x0
   P.tolC_tab = tolC_table;
   P.tab_len = table_len;
   return si_launch(ctx, P);
+}
+
+int riptrm_si_profile_enable(riptrm_ctx* ctx, int32_t on) {
+  if (!ctx) return RIPTRM_E_ARG;
+  if (!ctx->si) return fail(ctx, RIPTRM_E_STATE, "si_profile_enable: riptrm_si_bind first");
+  HIPCHK(ctx, hipSetDevice(ctx->device));
+  Bound* s = ctx->si;
+  if (on && !s->prof) HIPCHK(ctx, hipMalloc(&s->prof, (size_t)s->batch * RIPTRM_SI_PROF_NFIELDS * 8));
+  if (on) HIPCHK(ctx, hipMemsetAsync(s->prof, 0, (size_t)s->batch * RIPTRM_SI_PROF_NFIELDS * 8, ctx->stream));
+  s->prof_on = on != 0;
+  return RIPTRM_OK;
+}
+
+int riptrm_si_profile_read(riptrm_ctx* ctx, double* seconds) {
+  if (!ctx || !seconds) return RIPTRM_E_ARG;
+  if (!ctx->si || !ctx->si->prof) return fail(ctx, RIPTRM_E_STATE, "si_profile_read: riptrm_si_profile_enable first");
+  HIPCHK(ctx, hipSetDevice(ctx->device));
+  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  const int B = ctx->si->batch;
+  std::string buf((size_t)B * RIPTRM_SI_PROF_NFIELDS * 8, '\0');
+  HIPCHK(ctx, hipMemcpy(&buf[0], ctx->si->prof, buf.size(), hipMemcpyDeviceToHost));
+  const double* h = (const double*)buf.data();
+  for (int k = 0; k < RIPTRM_SI_PROF_NFIELDS; ++k) {
+    double t = 0.0;
+    for (int b = 0; b < B; ++b) t += h[(size_t)b * RIPTRM_SI_PROF_NFIELDS + k];
+    seconds[k] = t / ctx->clock_hz;
+  }
+  return RIPTRM_OK;
 }
 
 }  // extern "C"

@@ -276,6 +276,15 @@ class SIBatch:
         self.ro = ro
         return ro
 
+    def profile_enable(self, on: bool = True):
+        self.ctx.check(self.lib.riptrm_si_profile_enable(self.ctx.h, 1 if on else 0), "riptrm_si_profile_enable")
+
+    def profile_read(self) -> Dict[str, float]:
+        out = (ctypes.c_double * C["RIPTRM_SI_PROF_NFIELDS"])()
+        self.ctx.check(self.lib.riptrm_si_profile_read(self.ctx.h, out), "riptrm_si_profile_read")
+        names = ("total", "prepare", "tcg", "hvp", "trial", "eval")
+        return {k: float(out[i]) for i, k in enumerate(names)}
+
     def solve(self, x0, y0, option: Dict[str, Any], restart_every: int = 0) -> BatchResult:
         self.begin(x0, y0, option, restart_every)
         return self.result()
