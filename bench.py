@@ -91,8 +91,9 @@ def main():
     ap.add_argument("--batch", type=int, default=128, help="instances per GPU")
     ap.add_argument("--cpu-budget", type=float, default=25.0, help="seconds of CPU-baseline sampling (0 = skip)")
     ap.add_argument("--seed0", type=int, default=20251212)
-    ap.add_argument("--problem", default="nonnegpca", choices=["nonnegpca", "si"],
+    ap.add_argument("--problem", default="nonnegpca", choices=["nonnegpca", "si", "stiefel"],
                     help="si: StableIdentification (d=5 fixture, starts cycled + perturbed), one launch per solve")
+    ap.add_argument("--stiefel-p", type=int, default=50, help="p of Stiefel(n, p) for --problem stiefel")
     ap.add_argument("--stream-groups", type=int, default=0, choices=[0, 1, 2],
                     help="instance groups on separate streams (0 = library default)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_gemv.json"))
@@ -120,6 +121,11 @@ def main():
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
 
+    if args.problem == "stiefel":
+        bench_stiefel(args, world, rank, dev, dist)
+        if world > 1:
+            dist.destroy_process_group()
+        return
     if args.problem == "si":
         bench_si(args, world, rank, dev, dist)
         if world > 1:
@@ -247,6 +253,55 @@ def main():
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def bench_stiefel(args, world, rank, dev, dist):
+    """Stiefel(n, p) kernels (BASELINE configs[4] size (200, 50) x 256 per GPU):
+    --steps projections and retractions of the whole batch, HIP-event timed on the stream."""
+    import numpy as np
+    import torch
+    from stiefel import StiefelBatch
+    n, p, B = args.dim, args.stiefel_p, args.batch
+    g = torch.Generator(device=dev)
+    g.manual_seed(args.seed0 + rank)
+    X = torch.linalg.qr(torch.randn(B, n, p, dtype=torch.float64, device=dev, generator=g))[0].contiguous()
+    W = torch.randn(B, n, p, dtype=torch.float64, device=dev, generator=g)
+    st = StiefelBatch(n, p)
+    U = (0.1 * st.projection(X, W)).contiguous()
+    res = {}
+    for name, fn in (("projection", lambda: st.projection(X, W)), ("retraction", lambda: st.retraction(X, U))):
+        for _ in range(max(1, args.warmup)):
+            fn()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(args.steps):
+            fn()
+        e1.record()
+        torch.cuda.synchronize(dev)
+        res[name] = e0.elapsed_time(e1) / 1e3 / args.steps
+    t = torch.tensor([res["projection"], res["retraction"]], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    tp, tr = [float(v) for v in t.tolist()]
+    if rank != 0:
+        return
+    gbs = 3.0 * n * p * 8 * B / tp / 1e9    # read X, U; write the result
+    print(json.dumps({
+        "metric": f"Stiefel({n},{p}) projections/sec, batch {B}/GPU",
+        "value": B * world / tp, "unit": "projections/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": tp * 1e3, "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "f64", "data": "synthetic (random orthonormal X, Gaussian U)",
+        "config": {"workload": f"Stiefel(n={n}, p={p}) x {B} per GPU (BASELINE configs[4] size)",
+                   "global_batch": B * world, "parallelism": f"instance-sharded x{world}"},
+        "roofline": {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS,
+                     "traffic": None, "kernel": "k_st_proj (U - X sym(X^T U), one workgroup per point)"},
+        "cpu_baseline": None,
+        "detail": {"retractions_per_s": B * world / tr, "retraction_ms": tr * 1e3,
+                   "retraction_note": "CholeskyQR2, latency-bound (p Cholesky steps per point)"},
+    }), flush=True)
 
 
 def si_starts(B: int, ids):

@@ -270,6 +270,25 @@ int riptrm_si_solve(riptrm_ctx* ctx, const riptrm_options* opt, const double* x0
                     const double* mu_table, const double* tolL_table, const double* tolC_table,
                     int32_t table_len);
 
+/* ==== Stiefel(n, p) manifold operations =========================================
+ * Not in the reference (north_star / BASELINE configs[4] ask for them): pymanopt 2.x formulas,
+ * oracle/stiefel_oracle.py, parity unpinned.  Batched over `batch` instances, each an n x p
+ * row-major matrix at base + b * stride doubles (stride >= n p), 1 <= p <= RIPTRM_STIEFEL_PMAX,
+ * p <= n.  Device pointers, asynchronous on the context's stream. */
+#define RIPTRM_STIEFEL_PMAX 64
+/* out_b = tr(U_b^T V_b)  (pymanopt Stiefel.inner_product; X unused, kept for the signature) */
+int riptrm_stiefel_inner(riptrm_ctx* ctx, int32_t n, int32_t p, int32_t batch, int64_t stride, const double* X,
+                         const double* U, const double* V, double* out);
+/* out_b = U_b - X_b sym(X_b^T U_b)  (projection = to_tangent_space = euclidean_to_riemannian_gradient) */
+int riptrm_stiefel_proj(riptrm_ctx* ctx, int32_t n, int32_t p, int32_t batch, int64_t stride, const double* X,
+                        const double* U, double* out);
+/* out_b = qf(X_b + U_b), the Q factor with diag(R) > 0 (pymanopt Stiefel.retraction); CholeskyQR2 */
+int riptrm_stiefel_retr(riptrm_ctx* ctx, int32_t n, int32_t p, int32_t batch, int64_t stride, const double* X,
+                        const double* U, double* out);
+/* out_b = P_X(H_b - U_b sym(X_b^T G_b))  (euclidean_to_riemannian_hessian) */
+int riptrm_stiefel_ehess2rhess(riptrm_ctx* ctx, int32_t n, int32_t p, int32_t batch, int64_t stride,
+                               const double* X, const double* G, const double* H, const double* U, double* out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,320 @@
+// riptrm_stiefel.hip — batched Stiefel(n, p) manifold operations on MI355X (gfx950).
+//
+// north_star asks for "the Sphere/Stiefel projection+retraction from
+// pymanopt re-implemented as HIP kernels"; the reference itself has no Stiefel problem, so the
+// formulas are pymanopt 2.x's (oracle/stiefel_oracle.py, parity unpinned):
+//   projection  P_X(U) = U - X sym(X^T U)              (= euclidean_to_riemannian_gradient)
+//   retraction  qf(X + U), the QR factor with diag(R) > 0
+//   e2rh        P_X(H - U sym(X^T G))
+//   inner       tr(U^T V)
+// One 256-thread workgroup per instance.  Both products of a projection run on the fp64 matrix
+// cores: the p x p Gram X^T U as 16 x 16 blocks over K = n, the n x p update X sym(.) with the
+// p x p factor in LDS; per projection 3 n p doubles of HBM traffic (read X, U, write the result).  The retraction is CholeskyQR2 (Q = A R^-1
+// with R = chol(A^T A), twice): diag(R) > 0 by construction, so it is pymanopt's qf up to
+// rounding for full-rank A.
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include "riptrm_ctx.h"
+
+namespace riptrm_stiefel {
+
+#pragma clang fp contract(off)
+
+constexpr int T = 256;         // threads per workgroup
+constexpr int PMAX = RIPTRM_STIEFEL_PMAX;
+constexpr int OUT_PER = (PMAX * PMAX + T - 1) / T;
+
+constexpr int RT = 32;                      // rows per streamed Gram tile
+constexpr int PER = (RT * PMAX + T - 1) / T;  // tile elements per thread
+
+struct Smem {
+  double tA[RT * PMAX];
+  double tB[RT * PMAX];
+  double M[PMAX * PMAX];   // p x p (Gram / sym / R^-1)
+  double L[PMAX * PMAX];   // Cholesky factor
+  double red[T / 64];
+};
+
+typedef double dbl4 __attribute__((ext_vector_type(4)));
+
+// Small p x p matrices live in LDS with the padded row stride PS = 16 ceil(p / 16) and zeros
+// outside p x p, so the MFMA loops read operands without bounds tests (no divergent branches).
+__device__ __forceinline__ int pstride(int p) { return ((p + 15) / 16) * 16; }
+
+// M <- A^T B (p x p) for n x p row-major A, B on the fp64 matrix cores: 16 x 16 output blocks
+// (<= 16 at p <= 64) dealt to the 4 waves, K = n walked 4 rows per v_mfma_f64_16x16x4_f64.
+// Operands stream through LDS in 32-row tiles (zero padded to PS columns); the next tile's loads
+// are issued into registers before the current tile's MFMAs (one memory latency per tile).
+__device__ __forceinline__ void gram(Smem& sm, const double* __restrict__ A, const double* __restrict__ B, int n, int p) {
+  const int t = threadIdx.x, l = t & 63, w = t >> 6;
+  const int P16 = (p + 15) / 16, nb = P16 * P16, PS = P16 * 16;
+  const int c = l & 15, kk = l >> 4;
+  const int te = RT * PS;
+  dbl4 acc[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) acc[q] = dbl4{0.0, 0.0, 0.0, 0.0};
+  double ra[PER], rb[PER];
+  auto fetch = [&](int r0) {
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int e = t + i * T;
+      const int rr = e / PS, cc = e - (e / PS) * PS;
+      const bool ok = e < te && cc < p && r0 + rr < n;
+      const int64_t g = ok ? (int64_t)(r0 + rr) * p + cc : 0;
+      const double va = A[g], vb = B[g];
+      ra[i] = ok ? va : 0.0;
+      rb[i] = ok ? vb : 0.0;
+    }
+  };
+  fetch(0);
+  for (int r0 = 0; r0 < n; r0 += RT) {
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int e = t + i * T;
+      if (e < te) { sm.tA[e] = ra[i]; sm.tB[e] = rb[i]; }
+    }
+    __syncthreads();
+    if (r0 + RT < n) fetch(r0 + RT);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int blk = w + 4 * q;
+      if (blk < nb) {
+        const int I = blk / P16, J = blk - (blk / P16) * P16;
+        const double* pa = sm.tA + kk * PS + I * 16 + c;
+        const double* pb = sm.tB + kk * PS + J * 16 + c;
+#pragma unroll
+        for (int k4 = 0; k4 < RT / 4; ++k4)
+          acc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(pa[k4 * 4 * PS], pb[k4 * 4 * PS], acc[q], 0, 0, 0);
+      }
+    }
+    __syncthreads();
+  }
+  for (int e = t; e < PS * PS; e += T) sm.M[e] = 0.0;
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int blk = w + 4 * q;
+    if (blk < nb) {
+      const int I = blk / P16, J = blk - (blk / P16) * P16;
+      const int j = J * 16 + c;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int i = I * 16 + kk + 4 * g;
+        if (i < p && j < p) sm.M[i * PS + j] = acc[q][g];
+      }
+    }
+  }
+  __syncthreads();
+}
+
+__device__ __forceinline__ void symmetrize(Smem& sm, int p) {
+  const int t = threadIdx.x, PS = pstride(p);
+  double v[OUT_PER];
+#pragma unroll
+  for (int k = 0; k < OUT_PER; ++k) {
+    const int o = t + k * T;
+    v[k] = 0.0;
+    if (o < PS * PS) {
+      const int i = o / PS, j = o - i * PS;
+      v[k] = 0.5 * (sm.M[o] + sm.M[j * PS + i]);
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < OUT_PER; ++k) {
+    const int o = t + k * T;
+    if (o < PS * PS) sm.M[o] = v[k];
+  }
+  __syncthreads();
+}
+
+// out = C + sgn * A K (K = sm.M, p x p, padded) on the matrix cores.  A wave owns 16-row blocks
+// of the output and computes ALL their column blocks before writing, reading its A rows only:
+// out may alias A or C.  C = nullptr gives out = A K.
+__device__ __forceinline__ void update(Smem& sm, const double* A, const double* C, double sgn, double* out,
+                                       int n, int p) {
+  const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int P16 = (p + 15) / 16, R16 = (n + 15) / 16, PS = P16 * 16;
+  const int c = l & 15, kk = l >> 4;
+  const int P4 = (p + 3) / 4;
+  for (int I = w; I < R16; I += 4) {
+    dbl4 acc[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) acc[q] = dbl4{0.0, 0.0, 0.0, 0.0};
+    const int arow = I * 16 + c;
+    double ar[PMAX / 4];   // this lane's A operands for every k step, loaded at once
+#pragma unroll
+    for (int k4 = 0; k4 < PMAX / 4; ++k4) {
+      const int k = k4 * 4 + kk;
+      const bool ok = k4 < P4 && arow < n && k < p;
+      const double v = A[ok ? (int64_t)arow * p + k : 0];
+      ar[k4] = ok ? v : 0.0;
+    }
+#pragma unroll
+    for (int J = 0; J < 4; ++J) {
+      if (J < P16) {
+        const double* pb = sm.M + kk * PS + J * 16 + c;
+#pragma unroll
+        for (int k4 = 0; k4 < PMAX / 4; ++k4)
+          if (k4 < P4) acc[J] = __builtin_amdgcn_mfma_f64_16x16x4f64(ar[k4], pb[k4 * 4 * PS], acc[J], 0, 0, 0);
+      }
+    }
+    // every lane of the wave has read its A rows before any lane writes them
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int J = 0; J < 4; ++J) {
+      if (J < P16) {
+        const int j = J * 16 + c;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int i = I * 16 + kk + 4 * g;
+          if (i < n && j < p) {
+            const int64_t e = (int64_t)i * p + j;
+            out[e] = C ? C[e] + sgn * acc[J][g] : acc[J][g];
+          }
+        }
+      }
+    }
+  }
+  __syncthreads();
+}
+
+// sm.M (SPD p x p, stride PS) -> sm.M = (L^-1)^T = R^-1 for A^T A = R^T R, R = L^T (upper,
+// diag > 0), zero padded
+__device__ __forceinline__ void chol_rinv(Smem& sm, int p) {
+  const int t = threadIdx.x, PS = pstride(p);
+  double* G = sm.M;
+  double* L = sm.L;
+  for (int e = t; e < PS * PS; e += T) L[e] = 0.0;
+  __syncthreads();
+  for (int k = 0; k < p; ++k) {
+    if (t == 0) L[k * PS + k] = sqrt(G[k * PS + k]);
+    __syncthreads();
+    const double lkk = L[k * PS + k];
+    for (int i = k + 1 + t; i < p; i += T) L[i * PS + k] = G[i * PS + k] / lkk;
+    __syncthreads();
+    const int m = p - k - 1;
+    for (int e = t; e < m * m; e += T) {
+      const int i = k + 1 + e / m, j = k + 1 + (e - (e / m) * m);
+      if (j <= i) G[i * PS + j] = G[i * PS + j] - L[i * PS + k] * L[j * PS + k];
+    }
+    __syncthreads();
+  }
+  // column c of L^-1 by forward substitution; R^-1 = (L^-1)^T -> M[c][i] = (L^-1)[i][c]
+  for (int e = t; e < PS * PS; e += T) G[e] = 0.0;
+  __syncthreads();
+  if (t < p) {
+    const int c = t;
+    for (int i = c; i < p; ++i) {
+      double s = (i == c) ? 1.0 : 0.0;
+      for (int k = c; k < i; ++k) s = s - L[i * PS + k] * G[c * PS + k];
+      G[c * PS + i] = s / L[i * PS + i];
+    }
+  }
+  __syncthreads();
+}
+
+__global__ void __launch_bounds__(T) k_st_proj(int n, int p, int64_t stride, const double* X, const double* U, double* out) {
+  __shared__ Smem sm;
+  const int64_t o = (int64_t)blockIdx.x * stride;
+  gram(sm, X + o, U + o, n, p);
+  symmetrize(sm, p);
+  update(sm, X + o, U + o, -1.0, out + o, n, p);
+}
+
+__global__ void __launch_bounds__(T) k_st_e2rh(int n, int p, int64_t stride, const double* X, const double* G,
+                                               const double* H, const double* U, double* out) {
+  __shared__ Smem sm;
+  const int64_t o = (int64_t)blockIdx.x * stride;
+  gram(sm, X + o, G + o, n, p);            // X^T G
+  symmetrize(sm, p);
+  update(sm, U + o, H + o, -1.0, out + o, n, p);   // W = H - U sym(X^T G) into out
+  gram(sm, X + o, out + o, n, p);          // X^T W
+  symmetrize(sm, p);
+  update(sm, X + o, out + o, -1.0, out + o, n, p);  // P_X(W)
+}
+
+__global__ void __launch_bounds__(T) k_st_retr(int n, int p, int64_t stride, const double* X, const double* U, double* out) {
+  __shared__ Smem sm;
+  const int64_t o = (int64_t)blockIdx.x * stride;
+  double* A = out + o;
+  for (int e = threadIdx.x; e < n * p; e += T) A[e] = X[o + e] + U[o + e];
+  __syncthreads();
+  for (int pass = 0; pass < 2; ++pass) {   // CholeskyQR2
+    gram(sm, A, A, n, p);
+    chol_rinv(sm, p);
+    update(sm, A, nullptr, 0.0, A, n, p);
+  }
+}
+
+__global__ void __launch_bounds__(T) k_st_inner(int n, int p, int64_t stride, const double* U, const double* V, double* out) {
+  __shared__ double red[T / 64];
+  const int64_t o = (int64_t)blockIdx.x * stride;
+  double s = 0.0;
+  for (int e = threadIdx.x; e < n * p; e += T) s = s + U[o + e] * V[o + e];
+  for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) out[blockIdx.x] = ((red[0] + red[1]) + red[2]) + red[3];
+}
+
+}  // namespace riptrm_stiefel
+
+using namespace riptrm_stiefel;
+
+static int st_check(riptrm_ctx* c, int32_t n, int32_t p, int32_t batch, int64_t stride) {
+  if (n < 1 || p < 1 || p > PMAX || p > n || batch < 1 || stride < (int64_t)n * p)
+    return fail(c, RIPTRM_E_ARG, "stiefel: need 1 <= p <= min(n, 64), batch >= 1, stride >= n*p");
+  HIPCHK(c, hipSetDevice(c->device));
+  return RIPTRM_OK;
+}
+
+extern "C" {
+
+int riptrm_stiefel_inner(riptrm_ctx* ctx, int32_t n, int32_t p, int32_t batch, int64_t stride, const double* X,
+                         const double* U, const double* V, double* out) {
+  if (!ctx) return RIPTRM_E_ARG;
+  if (!U || !V || !out) return fail(ctx, RIPTRM_E_ARG, "stiefel_inner: null pointer");
+  (void)X;
+  int rc = st_check(ctx, n, p, batch, stride);
+  if (rc) return rc;
+  hipLaunchKernelGGL(k_st_inner, dim3(batch), dim3(T), 0, ctx->stream, n, p, stride, U, V, out);
+  HIPCHK(ctx, hipGetLastError());
+  return RIPTRM_OK;
+}
+
+int riptrm_stiefel_proj(riptrm_ctx* ctx, int32_t n, int32_t p, int32_t batch, int64_t stride, const double* X,
+                        const double* U, double* out) {
+  if (!ctx) return RIPTRM_E_ARG;
+  if (!X || !U || !out || out == X) return fail(ctx, RIPTRM_E_ARG, "stiefel_proj: bad pointer (out must not alias X)");
+  int rc = st_check(ctx, n, p, batch, stride);
+  if (rc) return rc;
+  hipLaunchKernelGGL(k_st_proj, dim3(batch), dim3(T), 0, ctx->stream, n, p, stride, X, U, out);
+  HIPCHK(ctx, hipGetLastError());
+  return RIPTRM_OK;
+}
+
+int riptrm_stiefel_retr(riptrm_ctx* ctx, int32_t n, int32_t p, int32_t batch, int64_t stride, const double* X,
+                        const double* U, double* out) {
+  if (!ctx) return RIPTRM_E_ARG;
+  if (!X || !U || !out) return fail(ctx, RIPTRM_E_ARG, "stiefel_retr: null pointer");
+  int rc = st_check(ctx, n, p, batch, stride);
+  if (rc) return rc;
+  hipLaunchKernelGGL(k_st_retr, dim3(batch), dim3(T), 0, ctx->stream, n, p, stride, X, U, out);
+  HIPCHK(ctx, hipGetLastError());
+  return RIPTRM_OK;
+}
+
+int riptrm_stiefel_ehess2rhess(riptrm_ctx* ctx, int32_t n, int32_t p, int32_t batch, int64_t stride, const double* X,
+                               const double* G, const double* H, const double* U, double* out) {
+  if (!ctx) return RIPTRM_E_ARG;
+  if (!X || !G || !H || !U || !out || out == X || out == U)
+    return fail(ctx, RIPTRM_E_ARG, "stiefel_ehess2rhess: bad pointer (out must not alias X or U)");
+  int rc = st_check(ctx, n, p, batch, stride);
+  if (rc) return rc;
+  hipLaunchKernelGGL(k_st_e2rh, dim3(batch), dim3(T), 0, ctx->stream, n, p, stride, X, G, H, U, out);
+  HIPCHK(ctx, hipGetLastError());
+  return RIPTRM_OK;
+}
+
+}  // extern "C"

@@ -79,6 +79,12 @@ SIGNATURES: Dict[str, tuple] = {
     "riptrm_si_tcg": (c_int32, [c_void_p, ctypes.POINTER(RiptrmOptions), c_void_p, c_void_p, c_void_p, c_void_p]),
     "riptrm_si_profile_enable": (c_int32, [c_void_p, c_int32]),
     "riptrm_si_profile_read": (c_int32, [c_void_p, ctypes.POINTER(c_double)]),
+    "riptrm_stiefel_inner": (c_int32, [c_void_p, c_int32, c_int32, c_int32, c_int64, c_void_p, c_void_p, c_void_p,
+                                       c_void_p]),
+    "riptrm_stiefel_proj": (c_int32, [c_void_p, c_int32, c_int32, c_int32, c_int64, c_void_p, c_void_p, c_void_p]),
+    "riptrm_stiefel_retr": (c_int32, [c_void_p, c_int32, c_int32, c_int32, c_int64, c_void_p, c_void_p, c_void_p]),
+    "riptrm_stiefel_ehess2rhess": (c_int32, [c_void_p, c_int32, c_int32, c_int32, c_int64, c_void_p, c_void_p, c_void_p,
+                                             c_void_p, c_void_p]),
     "riptrm_si_solve": (c_int32, [c_void_p, ctypes.POINTER(RiptrmOptions), c_void_p, c_void_p, c_void_p, c_void_p,
                                   c_void_p, c_int32]),
 }

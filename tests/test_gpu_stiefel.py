@@ -1,0 +1,56 @@
+"""GPU checks of the batched Stiefel kernels (csrc/riptrm_stiefel.hip) against the pymanopt
+restatement (oracle/stiefel_oracle.py).  SURVEY.md A14: not in the reference -> parity unpinned;
+bar: 1e-12 relative for projection / e2rh / inner (summation order), 1e-12 absolute for the
+retraction's orthonormal factor (CholeskyQR2 vs Householder QR)."""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+from oracle.stiefel_oracle import Stiefel
+
+
+def _data(n, p, B, seed=0):
+    M = Stiefel(n, p)
+    rs = np.random.RandomState(seed)
+    X = np.stack([M.random_point(rs) for _ in range(B)])
+    U = np.stack([M.random_tangent_vector(X[b], rs) for b in range(B)])
+    W = rs.randn(B, n, p)
+    return M, X, U, W
+
+
+def _t(a):
+    return torch.as_tensor(np.ascontiguousarray(a), device="cuda")
+
+
+@pytest.mark.parametrize("n,p,B", [(5, 1, 3), (37, 7, 5), (200, 50, 16), (257, 64, 3), (64, 64, 2)])
+def test_stiefel_ops_match_oracle(n, p, B):
+    from stiefel import StiefelBatch
+    M, X, U, W = _data(n, p, B, seed=n)
+    st = StiefelBatch(n, p)
+    Xt, Ut, Wt = _t(X), _t(U), _t(W)
+    P = st.projection(Xt, Wt).cpu().numpy()
+    R = st.retraction(Xt, 0.3 * Ut).cpu().numpy()
+    G, H = np.random.RandomState(1).randn(B, n, p), np.random.RandomState(2).randn(B, n, p)
+    E = st.euclidean_to_riemannian_hessian(Xt, _t(G), _t(H), Ut).cpu().numpy()
+    ip = st.inner_product(Xt, Ut, Wt).cpu().numpy()
+    for b in range(B):
+        ref = M.projection(X[b], W[b])
+        assert np.linalg.norm(P[b] - ref) <= 1e-12 * np.linalg.norm(ref)
+        ref = M.retraction(X[b], 0.3 * U[b])
+        assert np.abs(R[b] - ref).max() <= 1e-12
+        assert np.abs(R[b].T @ R[b] - np.eye(p)).max() <= 1e-13
+        ref = M.euclidean_to_riemannian_hessian(X[b], G[b], H[b], U[b])
+        assert np.linalg.norm(E[b] - ref) <= 1e-12 * np.linalg.norm(ref)
+        assert abs(ip[b] - M.inner_product(X[b], U[b], W[b])) <= 1e-12 * max(1.0, abs(ip[b]))
+
+
+def test_stiefel_rejects_bad_shapes():
+    from stiefel import StiefelBatch
+    with pytest.raises(ValueError):
+        StiefelBatch(4, 5)
+    st = StiefelBatch(8, 2)
+    with pytest.raises(ValueError):
+        st.projection(torch.zeros(2, 8, 3, dtype=torch.float64, device="cuda"),
+                      torch.zeros(2, 8, 3, dtype=torch.float64, device="cuda"))
