@@ -203,6 +203,11 @@ double riptrm_device_clock_hz(riptrm_ctx* ctx);
  * Takes effect at the next riptrm_nonnegpca_bind.  Results do not depend on it. */
 int riptrm_set_stream_groups(riptrm_ctx* ctx, int32_t groups);
 
+/* Small batches (S of the batch < 200 MB, or the shared layout) replay a captured hipGraph of 8
+ * lock-step iterations (16 kernels) per host submission instead of 2 launches per iteration,
+ * unless profiling is on.  on = 0 disables it (default 1).  Results do not depend on it. */
+int riptrm_set_graphs(riptrm_ctx* ctx, int32_t on);
+
 /* ---- measurement ---- */
 /* Enable/disable HIP-event timing of every S-pass (k_gemv) and state-machine (k_state) launch
  * enqueued by riptrm_solve_advance / riptrm_tcg; enabling resets the totals.  Synchronises. */

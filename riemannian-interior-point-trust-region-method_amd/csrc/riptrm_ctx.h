@@ -40,6 +40,13 @@ struct riptrm_ctx {
   int ev_used = 0;
   double gemv_ms = 0.0, state_ms = 0.0;
   int64_t gemv_n = 0, state_n = 0;
+  // hipGraph of GRAPH_STEPS lock-step iterations (single group, no profiling): replayed instead of
+  // 2 launches per step when the kernels are short enough for host launch cost to matter
+  hipGraphExec_t gexec = nullptr;
+  int g_bound = -1, g_parity = -1;
+  uint64_t g_pver = ~0ull;
+  uint64_t pver = 0;          // bumped whenever P (kernel parameters) changes
+  int graphs = 1;             // riptrm_set_graphs
   // StableIdentification binding (riptrm_si.hip)
   riptrm_si::Bound* si = nullptr;
 };

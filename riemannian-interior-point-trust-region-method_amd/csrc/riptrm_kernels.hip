@@ -17,6 +17,7 @@
 #include <cstdio>
 #include "riptrm_device.h"
 #include "riptrm_ctx.h"
+#include "riptrm_wave.h"
 
 namespace riptrm {
 
@@ -56,11 +57,9 @@ template <int K>
 __device__ __forceinline__ void bred(Red& R, double (&v)[K], const int (&op)[K]) {
   static_assert(K <= RED_MAX, "too many reduction slots");
 #pragma unroll
-  for (int k = 0; k < K; ++k) {
-    double a = v[k];
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) a = comb(op[k], a, xor_lane(a, off));
-    v[k] = a;
+  for (int k = 0; k < K; ++k) {  // in-wave: DPP / permlane reduction (riptrm_wave.h), no LDS
+    v[k] = op[k] == 0 ? riptrm_wave::wave_sum(v[k])
+                      : (op[k] == 1 ? riptrm_wave::wave_min(v[k]) : riptrm_wave::wave_max(v[k]));
   }
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   double* b = R.buf + R.parity * (ST_WAVES * RED_MAX);
@@ -1420,6 +1419,7 @@ int riptrm_ctx_create(riptrm_ctx** out, int device, void* stream) {
 
 int riptrm_ctx_destroy(riptrm_ctx* ctx) {
   if (ctx) {
+    if (ctx->gexec) (void)hipGraphExecDestroy(ctx->gexec);
     if (ctx->si) riptrm_si_release(ctx->si);
     for (auto e : ctx->ev_pool) (void)hipEventDestroy(e);
     for (auto e : {ctx->ev_fork, ctx->ev_join, ctx->ev_pass[0], ctx->ev_pass[1]})
@@ -1535,6 +1535,7 @@ int riptrm_nonnegpca_bind(riptrm_ctx* ctx, const double* S, int32_t n, int32_t b
   ctx->gsize[1] = batch - ctx->gsize[0];
   ctx->bound = true;
   ctx->solving = false;
+  ctx->pver++;
   return RIPTRM_OK;
 }
 
@@ -1624,7 +1625,61 @@ int riptrm_nonnegpca_hvp(riptrm_ctx* ctx, const double* x, const double* y, doub
 // the group's stream.  The S-passes of the two groups are chained by events so they never run
 // concurrently (each gets the whole HBM; per-launch timing stays clean), while a group's state
 // kernel runs beside the other group's S-pass.
+constexpr int GRAPH_STEPS = 8;   // even: the ping-pong lists are back at the same parity
+
+// (re)capture GRAPH_STEPS lock-step iterations of group 0 on the private stream
+static int capture_graph(riptrm_ctx* c, int bound) {
+  if (c->gexec) {
+    (void)hipGraphExecDestroy(c->gexec);
+    c->gexec = nullptr;
+  }
+  hipStream_t st = c->own_stream;
+  HIPCHK(c, hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
+  int par = c->parity[0];
+  int rc = RIPTRM_OK;
+  for (int s = 0; s < GRAPH_STEPS && rc == RIPTRM_OK; ++s) {
+    const int lin = par, lout = par ^ 1;
+    rc = launch_gemv(c, st, lin, lout, bound);
+    if (rc == RIPTRM_OK) rc = launch_state(c, st, 0, lin, lout, bound);
+    par ^= 1;
+  }
+  hipGraph_t g = nullptr;
+  const hipError_t e = hipStreamEndCapture(st, &g);
+  if (rc) {
+    if (g) (void)hipGraphDestroy(g);
+    return rc;
+  }
+  if (e != hipSuccess) return fail(c, RIPTRM_E_HIP, std::string("hipStreamEndCapture: ") + hipGetErrorString(e));
+  const hipError_t e2 = hipGraphInstantiate(&c->gexec, g, nullptr, nullptr, 0);
+  (void)hipGraphDestroy(g);
+  if (e2 != hipSuccess) return fail(c, RIPTRM_E_HIP, std::string("hipGraphInstantiate: ") + hipGetErrorString(e2));
+  c->g_bound = bound;
+  c->g_parity = c->parity[0];
+  c->g_pver = c->pver;
+  return RIPTRM_OK;
+}
+
 static int run_steps(riptrm_ctx* c, int steps, int* n_active) {
+  // short kernels (small n x batch): replay a captured graph of GRAPH_STEPS iterations instead of
+  // launching 2 kernels per step from the host
+  const bool small = (double)c->P.batch * (double)s_elems_of(c->P.n, c->P.layout) * 8.0 < 2.0e8 ||
+                     c->P.layout == RIPTRM_LAYOUT_SHARED;
+  if (c->graphs && !c->prof && c->ngroups == 1 && c->active_bound[0] > 0 && small && steps > 0) {
+    int bound = 1;
+    while (bound < c->active_bound[0]) bound *= 2;
+    if (bound > c->P.batch) bound = c->P.batch;
+    if (!c->gexec || c->g_bound != bound || c->g_parity != c->parity[0] || c->g_pver != c->pver) {
+      const int rc = capture_graph(c, bound);
+      if (rc) return rc;
+    }
+    for (int s = 0; s < steps; s += GRAPH_STEPS) HIPCHK(c, hipGraphLaunch(c->gexec, c->stream));
+    int32_t h = 0;
+    HIPCHK(c, hipMemcpyAsync(&h, c->P.cnt + c->parity[0], sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    c->active_bound[0] = h;
+    if (n_active) *n_active = h;
+    return RIPTRM_OK;
+  }
   int rc = fork_streams(c);
   if (rc) return rc;
   const int G = c->ngroups;
@@ -1686,6 +1741,7 @@ int riptrm_tcg(riptrm_ctx* ctx, const double* x, const double* y, int64_t ldv, c
     P.opt.tcg_theta = 1.0;
     P.opt.tcg_kappa = 0.1;
     P.opt.tcg_mininner = 1;
+    ctx->pver++;
   }
   hipLaunchKernelGGL(k_init, dim3(P.batch), dim3(256), 0, ctx->stream, P, x, y, ldv, mu, delta, (int)MODE_TCG_ONLY);
   HIPCHK(ctx, hipGetLastError());
@@ -1738,6 +1794,7 @@ int riptrm_solve_begin(riptrm_ctx* ctx, const riptrm_options* opt, const double*
   P.tolC_tab = tolC_table;
   P.tab_len = table_len;
   P.outer_target = INT32_MAX;
+  ctx->pver++;
   hipLaunchKernelGGL(k_init, dim3(P.batch), dim3(256), 0, ctx->stream, P, x0, y0, ldv, (const double*)nullptr,
                      (const double*)nullptr, (int)MODE_SOLVE);
   HIPCHK(ctx, hipGetLastError());
@@ -1751,6 +1808,12 @@ int riptrm_set_stream_groups(riptrm_ctx* ctx, int32_t groups) {
   if (!ctx || groups < 0 || groups > 2) return RIPTRM_E_ARG;
   if (ctx->solving) return fail(ctx, RIPTRM_E_STATE, "set_stream_groups: call before riptrm_nonnegpca_bind");
   ctx->groups_req = groups;
+  return RIPTRM_OK;
+}
+
+int riptrm_set_graphs(riptrm_ctx* ctx, int32_t on) {
+  if (!ctx || on < 0 || on > 1) return RIPTRM_E_ARG;
+  ctx->graphs = on;
   return RIPTRM_OK;
 }
 
@@ -1786,6 +1849,7 @@ int riptrm_solve_advance(riptrm_ctx* ctx, int32_t steps, int32_t outer_target, i
   if (outer_target != ctx->P.outer_target) {
     const bool raised = outer_target > ctx->P.outer_target;
     ctx->P.outer_target = outer_target;
+    ctx->pver++;
     if (raised) {  // resume paused instances
       int rc = kick(ctx);
       if (rc) return rc;

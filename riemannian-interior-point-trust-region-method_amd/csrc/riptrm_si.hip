@@ -20,6 +20,7 @@
 #include <cstring>
 #include <string>
 #include "riptrm_ctx.h"
+#include "riptrm_wave.h"
 
 namespace riptrm_si {
 
@@ -94,24 +95,9 @@ __device__ __forceinline__ double lane_read(double v, int src) {
   return __hiloint2double(hi, lo);
 }
 
-__device__ __forceinline__ double wsum(double v) {
-  const int l = (int)__lane_id();
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) v = v + lane_read(v, l ^ off);
-  return v;
-}
-__device__ __forceinline__ double wmin(double v) {
-  const int l = (int)__lane_id();
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) v = fmin(v, lane_read(v, l ^ off));
-  return v;
-}
-__device__ __forceinline__ double wmax(double v) {
-  const int l = (int)__lane_id();
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) v = fmax(v, lane_read(v, l ^ off));
-  return v;
-}
+__device__ __forceinline__ double wsum(double v) { return riptrm_wave::wave_sum(v); }
+__device__ __forceinline__ double wmin(double v) { return riptrm_wave::wave_min(v); }
+__device__ __forceinline__ double wmax(double v) { return riptrm_wave::wave_max(v); }
 
 // a point / tangent vector of the product: this lane's element of J, R and Q
 struct PV {
