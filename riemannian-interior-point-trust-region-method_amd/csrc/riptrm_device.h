@@ -83,9 +83,25 @@ inline int64_t ntiles_of(int32_t n) { const int64_t t = nt_of(n); return t * (t 
 // MM_KZ x 2 x batch x ld slabs, summed in slice order by the state kernel
 constexpr int MM_KZ = 4;
 
+// Symmetric-tile layout: tiles (I, J), I <= J, row by row; full TS x TS tiles except the last
+// tile column (J = nt - 1), which keeps only the wl = round_up(n - (nt - 1) TS, 32) columns that
+// hold data (row stride wl), and the corner tile (nt - 1, nt - 1), wl x wl.  wl = TS when n is a
+// multiple of TS.  Offset of tile (I, J) = base(I) + (J - I) TS^2.
+inline int32_t edge_w_of(int32_t n) {
+  return (int32_t)round_up((int64_t)(n > 0 ? n : 1) - (int64_t)(nt_of(n) - 1) * TS, 32);
+}
+__host__ __device__ inline int64_t sym_off(int I, int J, int nt, int wl) {
+  const int64_t F = (int64_t)TS * TS;
+  return F * ((int64_t)I * (nt - 1) - (int64_t)I * (I - 1) / 2) + (int64_t)I * TS * wl + (int64_t)(J - I) * F;
+}
+
 // doubles of one instance of S in a layout
 inline int64_t s_elems_of(int32_t n, int32_t layout) {
-  return layout == RIPTRM_LAYOUT_SYMTILE ? ntiles_of(n) * TS * TS : rows_of(n) * ld_of(n);
+  if (layout == RIPTRM_LAYOUT_SYMTILE) {
+    const int nt = nt_of(n), wl = edge_w_of(n);
+    return sym_off(nt - 1, nt - 1, nt, wl) + (int64_t)wl * wl;
+  }
+  return rows_of(n) * ld_of(n);
 }
 
 inline Layout make_layout(int32_t n, int32_t batch, int32_t cap, int32_t layout) {
@@ -117,6 +133,7 @@ struct DevParams {
   int32_t layout;       // RIPTRM_LAYOUT_*
   int32_t nt;           // tiles per dimension (symmetric-tile layout)
   int32_t ntiles;       // nt (nt + 1) / 2
+  int32_t wl;           // stored columns of the last tile column (symmetric-tile layout)
   double* pbuf;         // S-pass partial sums: 2 x batch x nt x nt x TS (symmetric-tile layout),
                         // MM_KZ x 2 x batch x ld (shared layout)
   double* vec;          // workspace vectors

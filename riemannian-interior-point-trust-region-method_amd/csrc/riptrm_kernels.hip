@@ -260,7 +260,11 @@ __device__ __forceinline__ void spass_tile(const DevParams& P, int b, int t) {
   tile_ij(t, P.nt, I, J);
   const int lane = (int)__lane_id();
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const double* __restrict__ T = P.S + (int64_t)b * P.inst_stride + (int64_t)t * TS * TS;
+  const int nt = P.nt, wl = P.wl;
+  const int rowsT = (I == nt - 1) ? wl : TS;   // stored rows / columns of this tile
+  const int colsT = (J == nt - 1) ? wl : TS;
+  const bool cl = 2 * lane < colsT;            // this lane's two columns are stored
+  const double* __restrict__ T = P.S + (int64_t)b * P.inst_stride + sym_off(I, J, nt, wl);
   const double* __restrict__ v0 = vp(P, V_IN0, b);
   const double* __restrict__ v1 = vp(P, V_IN1, b);
   const dbl2 vj0 = *(const dbl2*)(v0 + J * TS + 2 * lane);
@@ -275,9 +279,11 @@ __device__ __forceinline__ void spass_tile(const DevParams& P, int b, int t) {
 #pragma unroll 1
   for (int rb = 0; rb < ROWS / 8; ++rb) {
     const int r0 = w * ROWS + rb * 8;
+    if (r0 >= rowsT) break;   // corner tile: rows beyond wl are not stored (wave-uniform)
     dbl2 sv[8];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) sv[k] = __builtin_nontemporal_load((const dbl2*)(T + (r0 + k) * TS + 2 * lane));
+    for (int k = 0; k < 8; ++k)
+      sv[k] = cl ? __builtin_nontemporal_load((const dbl2*)(T + (r0 + k) * colsT + 2 * lane)) : dbl2{0.0, 0.0};
     double a[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
@@ -497,8 +503,11 @@ __global__ void __launch_bounds__(256) k_pack(const double* Z, int64_t ldz, int6
     const int I = i0 / TS, J = j0 / TS;
     if (I > J) return;
     const int nt = (int)(ld / TS);
-    const int64_t t = (int64_t)I * nt - (int64_t)I * (I - 1) / 2 + (J - I);
-    pack_sub32(Zb, ldz, n, i0, j0, Sb + t * TS * TS + (int64_t)(i0 - I * TS) * TS + (j0 - J * TS), TS);
+    const int wl = (int)(((int64_t)n - (int64_t)(nt - 1) * TS + 31) / 32 * 32);
+    const int rowsT = (I == nt - 1) ? wl : TS, colsT = (J == nt - 1) ? wl : TS;
+    if (i0 - I * TS >= rowsT || j0 - J * TS >= colsT) return;   // outside the stored part
+    pack_sub32(Zb, ldz, n, i0, j0, Sb + sym_off(I, J, nt, wl) + (int64_t)(i0 - I * TS) * colsT + (j0 - J * TS),
+               colsT);
   }
 }
 
@@ -995,6 +1004,209 @@ struct Machine {
     return request(1);
   }
 
+  // ---- register-resident tCG iteration (n <= RT_EPT * ST_THREADS) ------------------------------
+  // Same arithmetic, element order and reductions as gather_out + tcg_step (bitwise identical),
+  // but every vector is read from memory once and kept in registers across the iteration's six
+  // reductions (element i = tid + k * ST_THREADS, k < RT_EPT): one load phase, one store phase.
+  static constexpr int RT_EPT = 8;
+
+  __device__ __forceinline__ void load_reg(int kind, double (&r)[RT_EPT]) const {
+    const double* a = V(kind);
+#pragma unroll
+    for (int k = 0; k < RT_EPT; ++k) {
+      const int i = tid + k * ST_THREADS;
+      r[k] = i < n ? a[i] : 0.0;
+    }
+  }
+  __device__ __forceinline__ void store_reg(int kind, const double (&r)[RT_EPT]) const {
+    double* a = V(kind);
+#pragma unroll
+    for (int k = 0; k < RT_EPT; ++k) {
+      const int i = tid + k * ST_THREADS;
+      if (i < n) a[i] = r[k];
+    }
+  }
+  // S delta of the last S-pass into registers (the layouts' partial sums, in gather_out's order)
+  __device__ __forceinline__ void gather_reg(double (&u)[RT_EPT]) {
+    if (P.layout == RIPTRM_LAYOUT_SYMTILE) {
+      const int nt = P.nt;
+      const int64_t nn = (int64_t)nt * nt * TS;
+      const double* pb = P.pbuf + (int64_t)b * nn;
+      const double* q[RT_EPT];
+#pragma unroll
+      for (int e = 0; e < RT_EPT; ++e) {
+        int i = tid + e * ST_THREADS;
+        i = i < n ? i : n - 1;
+        const int I = i / TS, c = i - I * TS;
+        q[e] = pb + (int64_t)I * nt * TS + c;
+        u[e] = q[e][0];
+      }
+      constexpr int GJ = 2;
+      for (int J = 1; J < nt; J += GJ) {
+        double t[RT_EPT][GJ];
+#pragma unroll
+        for (int e = 0; e < RT_EPT; ++e)
+#pragma unroll
+          for (int v = 0; v < GJ; ++v) t[e][v] = (J + v < nt) ? q[e][(int64_t)(J + v) * TS] : 0.0;
+#pragma unroll
+        for (int e = 0; e < RT_EPT; ++e)
+#pragma unroll
+          for (int v = 0; v < GJ; ++v)
+            if (J + v < nt) u[e] += t[e][v];
+      }
+#pragma unroll
+      for (int e = 0; e < RT_EPT; ++e)
+        if (tid + e * ST_THREADS >= n) u[e] = 0.0;
+    } else if (P.layout == RIPTRM_LAYOUT_SHARED) {
+      const int64_t ld = P.ld, slab = (int64_t)P.batch * ld;
+      const double* pb = P.pbuf + (int64_t)b * ld;
+#pragma unroll
+      for (int e = 0; e < RT_EPT; ++e) {
+        const int i = tid + e * ST_THREADS;
+        double acc = 0.0;
+        if (i < n) {
+          acc = pb[i];
+#pragma unroll
+          for (int z = 1; z < MM_KZ; ++z) acc += pb[(int64_t)z * 2 * slab + i];
+        }
+        u[e] = acc;
+      }
+    } else {
+      load_reg(V_OUT0, u);
+    }
+  }
+
+  __device__ __forceinline__ int tcg_step_reg() {
+    constexpr int K = RT_EPT;
+    double u[K], d[K], x[K], y[K];
+    gather_reg(u);
+    load_reg(V_IN0, d);
+    load_reg(V_X, x);
+    load_reg(V_Y, y);
+    // hw_apply(U, D, U)
+    double r1[2] = {0.0, 0.0};
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      r1[0] += x[k] * u[k];
+      r1[1] += x[k] * d[k];
+    }
+    bsum<2>(R, r1);
+    const double xu = r1[0], xv = r1[1];
+    double r2[1] = {0.0};
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const bool ok = tid + k * ST_THREADS < n;
+      const double q = ok ? (y[k] * (d[k] - x[k] * xv)) / x[k] : 0.0;
+      r2[0] += ok ? x[k] * q : 0.0;
+    }
+    bsum<1>(R, r2);
+    const double xq = r2[0];
+    const double coef = s[ST_COEF];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {   // q recomputed, as hw_apply does
+      const bool ok = tid + k * ST_THREADS < n;
+      const double q = ok ? (y[k] * (d[k] - x[k] * xv)) / x[k] : 0.0;
+      const double hf = -u[k] + xu * x[k];
+      u[k] = (hf + coef * d[k]) + (q - xq * x[k]);
+    }
+    double c[K], e[K], he[K];
+    load_reg(V_C, c);
+    load_reg(V_ETA, e);
+    load_reg(V_HETA, he);
+    double d1[1] = {0.0};
+#pragma unroll
+    for (int k = 0; k < K; ++k) d1[0] += d[k] * u[k];
+    bsum<1>(R, d1);
+    const double d_Hd = d1[0];
+    const double z_r = s[ST_ZR], e_Pd = s[ST_EPD], d_Pd = s[ST_DPD], e_Pe = s[ST_EPE];
+    const double Delta = s[ST_DELTA];
+    double alpha = 0.0, e_Pe_new;
+    if (d_Hd != 0.0) {
+      alpha = z_r / d_Hd;
+      e_Pe_new = (e_Pe + 2.0 * alpha * e_Pd) + (alpha * alpha) * d_Pd;
+    } else {
+      e_Pe_new = e_Pe;
+    }
+    const double D2 = Delta * Delta;
+    if (d_Hd <= 0.0 || e_Pe_new >= D2) {
+      const double tau = (-e_Pd + sqrt(e_Pd * e_Pd + d_Pd * (D2 - e_Pe))) / d_Pd;
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        e[k] = e[k] + tau * d[k];
+        he[k] = he[k] + tau * u[k];
+      }
+      store_reg(V_ETA, e);
+      store_reg(V_HETA, he);
+      s[ST_TCG_STOP] = d_Hd <= 0.0 ? RIPTRM_TCG_NEGATIVE_CURVATURE : RIPTRM_TCG_EXCEEDED_TR;
+      return tcg_end();
+    }
+    s[ST_EPE] = e_Pe_new;
+    double m2[2] = {0.0, 0.0};
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const double ne = e[k] + alpha * d[k];
+      const double nh = he[k] + alpha * u[k];
+      m2[0] += ne * c[k];
+      m2[1] += ne * nh;
+    }
+    bsum<2>(R, m2);
+    const double new_model = m2[0] + 0.5 * m2[1];
+    if (new_model >= s[ST_MODEL]) {
+      s[ST_TCG_STOP] = RIPTRM_TCG_MODEL_INCREASED;
+      return tcg_end();
+    }
+    s[ST_MODEL] = new_model;
+    double rv[K];
+    load_reg(V_R, rv);
+    double r2b[1] = {0.0};
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      e[k] = e[k] + alpha * d[k];
+      he[k] = he[k] + alpha * u[k];
+      const double r = rv[k] + alpha * u[k];
+      rv[k] = r;
+      r2b[0] += r * r;
+    }
+    store_reg(V_ETA, e);
+    store_reg(V_HETA, he);
+    store_reg(V_R, rv);
+    bsum<1>(R, r2b);
+    const double r_r = r2b[0];
+    const double norm_r = sqrt(r_r);
+    const double nr0 = s[ST_NORMR0];
+    const double th = P.opt.tcg_theta, ka = P.opt.tcg_kappa;
+    const double nr0t = pow(nr0, th);
+    const double j = s[ST_J];
+    if (j >= (double)P.opt.tcg_mininner && norm_r <= nr0 * fmin(nr0t, ka)) {
+      s[ST_TCG_STOP] = ka < nr0t ? RIPTRM_TCG_REACHED_TARGET_LINEAR : RIPTRM_TCG_REACHED_TARGET_SUPERLINEAR;
+      return tcg_end();
+    }
+    const double znew = r_r;
+    const double beta = znew / z_r;
+    double p1[1] = {0.0};
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const double dn = -rv[k] + beta * d[k];
+      d[k] = dn;
+      p1[0] += x[k] * dn;
+    }
+    bsum<1>(R, p1);
+    const double xd = p1[0];
+#pragma unroll
+    for (int k = 0; k < K; ++k) d[k] = d[k] - xd * x[k];  // to_tangent_space
+    store_reg(V_IN0, d);
+    s[ST_ZR] = znew;
+    s[ST_EPD] = beta * (e_Pd + alpha * d_Pd);
+    s[ST_DPD] = znew + (beta * beta) * d_Pd;
+    s[ST_J] = j + 1.0;
+    if (j + 1.0 >= (double)(n - 1)) {  // range(maxinner) exhausted; Python j stays maxinner-1
+      s[ST_J] = j;
+      s[ST_TCG_STOP] = RIPTRM_TCG_MAX_INNER_ITER;
+      return tcg_end();
+    }
+    return request(1);
+  }
+
   // after tCG: RIPTRM.py:733-746 (direction, ||dx||, dy, retraction) + feasibility part of :591
   __device__ __forceinline__ int tcg_end() {
     cadd(ST_TCG_TOTAL, s[ST_J] + 1.0);
@@ -1275,9 +1487,13 @@ __global__ void __launch_bounds__(ST_THREADS) k_state(DevParams P, int full, int
   Machine M(P, b, list_out, redbuf);
   const int ph = (int)M.s[ST_PHASE];
   if (ph == PH_DONE || ph == PH_IDLE || ph == PH_ERROR) return;
-  if (!full && P.layout == RIPTRM_LAYOUT_SYMTILE) M.gather_out(P.req[b]);
-  if (!full && P.layout == RIPTRM_LAYOUT_SHARED) M.gather_slices(P.req[b]);
-  M.dispatch();
+  if (!full && ph == PH_TCG && P.n <= Machine::RT_EPT * ST_THREADS) {
+    M.tcg_step_reg();   // gathers S delta itself, vectors register-resident
+  } else {
+    if (!full && P.layout == RIPTRM_LAYOUT_SYMTILE) M.gather_out(P.req[b]);
+    if (!full && P.layout == RIPTRM_LAYOUT_SHARED) M.gather_slices(P.req[b]);
+    M.dispatch();
+  }
   M.finish_write();
 }
 
@@ -1514,6 +1730,7 @@ int riptrm_nonnegpca_bind(riptrm_ctx* ctx, const double* S, int32_t n, int32_t b
   P.layout = layout;
   P.nt = L.nt;
   P.ntiles = (int)ntiles_of(n);
+  P.wl = edge_w_of(n);
   P.pbuf = (double*)(ctx->ws + L.off_pbuf);
   P.vec = (double*)(ctx->ws + L.off_vec);
   P.st = (double*)(ctx->ws + L.off_state);

@@ -260,14 +260,18 @@ class NonnegPCABatch:
         if self.layout != LAYOUTS["sym"]:
             return raw[: self.rows * ld].reshape(self.rows, ld)[:n, :n].copy()
         ts, nt = 128, ld // 128
+        wl = -(-(n - (nt - 1) * ts) // 32) * 32     # stored columns of the last tile column
         full = np.zeros((ld, ld))
-        t = 0
+        F = ts * ts
         for I in range(nt):
+            base = F * (I * (nt - 1) - I * (I - 1) // 2) + I * ts * wl
             for J in range(I, nt):
-                blk = raw[t * ts * ts:(t + 1) * ts * ts].reshape(ts, ts)
-                full[I * ts:(I + 1) * ts, J * ts:(J + 1) * ts] = blk
-                full[J * ts:(J + 1) * ts, I * ts:(I + 1) * ts] = blk.T
-                t += 1
+                off = base + (J - I) * F
+                rT = wl if I == nt - 1 else ts
+                cT = wl if J == nt - 1 else ts
+                blk = raw[off:off + rT * cT].reshape(rT, cT)
+                full[I * ts:I * ts + rT, J * ts:J * ts + cT] = blk
+                full[J * ts:J * ts + cT, I * ts:I * ts + rT] = blk.T
         return full[:n, :n].copy()
 
     def bind(self):

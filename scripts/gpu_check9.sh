@@ -14,4 +14,6 @@ timeout -k 10 300 python bench.py --dim 1000 --batch 1 --steps 10 --warmup 2 --c
 timeout -k 10 300 python bench.py --layout shared --cpu-budget 0 > gpurun_out/b_shared.json 2>/dev/null; rc=$?; echo "shared rc=$rc"; cat gpurun_out/b_shared.json
 [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python bench.py --problem si --batch 256 --steps 20 --cpu-budget 0 > gpurun_out/b_si.json 2>/dev/null; rc=$?; echo "si rc=$rc"; cat gpurun_out/b_si.json
+[ $rc -eq 0 ] || exit $rc
+timeout -k 10 600 python bench.py --cpu-budget 0 > gpurun_out/b_head.json 2>/dev/null; rc=$?; echo "headline rc=$rc"; cat gpurun_out/b_head.json
 exit $rc

@@ -41,7 +41,8 @@ def main():
     fetch, write = load(a.fetch, "FETCH_SIZE"), load(a.write, "WRITE_SIZE")
     ts = 128
     nt = (a.n + ts - 1) // ts
-    inst_stride = nt * (nt + 1) // 2 * ts * ts
+    wl = -(-(a.n - (nt - 1) * ts) // 32) * 32
+    inst_stride = (nt - 1) * nt // 2 * ts * ts + (nt - 1) * ts * wl + wl * wl
     alg_pass = 8 * inst_stride + 16 * a.n           # S tiles once + x read + y write
     out = {"source": a.source,
            "correction": "FETCH_SIZE/WRITE_SIZE in KiB; hbm_read = 2*FETCH_SIZE*1024 (gfx950 wide-read undercount); "

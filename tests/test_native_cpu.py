@@ -46,7 +46,9 @@ def test_layout_functions(built_lib):
         nt = ld // 128
         assert built_lib.riptrm_nonnegpca_s_elems(n, C["RIPTRM_LAYOUT_FULL"]) == rows * ld
         sym = built_lib.riptrm_nonnegpca_s_elems(n, C["RIPTRM_LAYOUT_SYMTILE"])
-        assert sym == nt * (nt + 1) // 2 * 128 * 128
+        wl = -(-(n - (nt - 1) * 128) // 32) * 32     # last tile column keeps its stored width
+        assert sym == (nt - 1) * nt // 2 * 128 * 128 + (nt - 1) * 128 * wl + wl * wl
+        assert sym >= n * (n + 1) // 2
         if n >= 1000:
             assert sym < 0.6 * n * n  # about half the bytes of the full matrix
         if n >= 4000:
