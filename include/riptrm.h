@@ -177,6 +177,12 @@ int riptrm_nonnegpca_bind(riptrm_ctx* ctx, const double* S, int32_t n, int32_t b
 /* out_b = HwCur_b(v_b) at (x_b, y_b, mu), s = x (NonnegPCA slack).  x, y, v, out: batch x ldv. */
 int riptrm_nonnegpca_hvp(riptrm_ctx* ctx, const double* x, const double* y, double mu,
                          const double* v, double* out, int64_t ldv);
+/* RIPM's condensed Newton operator OperatorAw (src/solver/RIPM.py:485-487, do_euclidean_lincomb
+ * False): out_b = hessLagrangian(x_b, z_b)[v_b] + Gx(x_b, Gxaj(x_b, v_b) * z_b / s_b) for NonnegPCA
+ * (constraints -x_i <= 0, multipliers z, slacks s) = the barrier-Hessian structure of HwCur with
+ * (y, s) -> (z, s).  x, z, s, v, out: batch x ldv. */
+int riptrm_nonnegpca_operator_aw(riptrm_ctx* ctx, const double* x, const double* z, const double* s,
+                                 const double* v, double* out, int64_t ldv);
 /* Batched tCG at (x_b, y_b, mu_b, Delta_b): eta/Heta written into the workspace vectors
  * (offset kinds 2/3); iters_b = loop index j at exit (RIPTRM.py:216 returns j), stop_b code.
  * x, y: batch x ldv; mu, delta: batch doubles; iters, stop: batch int32.  Synchronises. */

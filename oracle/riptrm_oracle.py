@@ -705,6 +705,37 @@ class RIPTRMOracle:
                             trace=self.trace)
 
 
+def ripm_operator_aw(P, x, z, s, v):
+    """RIPM's condensed Newton operator OperatorAw (src/solver/RIPM.py:485-487) with
+    do_euclidean_lincomb=False (RIPM.py:149 default; :399-409): hessLagrangian(x, y, z, dx) =
+    rhess f[dx] + sum_i z_i rhess g_i[dx] (:123-132, no equality constraints) plus
+    Gx(x, Gxaj(x, dx) * (z / s)) with Gx(x, c) = sum_i c_i rgrad g_i(x) (:12-17) and
+    Gxaj(x, dx)_i = <rgrad g_i(x), dx> (:19-24).  RIPM's constraints are the problem's g_i <= 0
+    (NonnegPCA: g_i = -x_i) with a separate slack s.  P = NonnegPCAStructured (per-constraint)."""
+    vec = P.riemannian_hessian(x, v)
+    for i in range(len(z)):
+        vec = vec + z[i] * P.ineq_rhess[i](x, v)
+    gxaj = np.array([P.manifold.inner_product(x, P.ineq_rgrad[i](x), v) for i in range(len(z))])
+    c = gxaj * (z / s)
+    theta = P.manifold.zero_vector(x)
+    for i in range(len(z)):
+        theta = theta + c[i] * P.ineq_rgrad[i](x)
+    return vec + theta
+
+
+def ripm_operator_aw_vectorized(Z, x, z, s, v):
+    """Closed form of ripm_operator_aw for NonnegPCA (the HIP kernel's formula):
+    Aw(v) = P_x(-S v) + (x^T S x + z^T x)(x^T x) v + P_x((z / s) (v - x (x^T v)))."""
+    S = Z + Z.T
+    Sx, Sv = S @ x, S @ v
+    xx, xSx, zx = x @ x, x @ Sx, z @ x
+    coef = (xSx + zx) * xx
+    xu, xv = x @ Sv, x @ v
+    q = (v - x * xv) * (z / s)
+    xq = x @ q
+    return ((-Sv + xu * x) + coef * v) + (q - xq * x)
+
+
 def solve(Z, x0, y0, option=None, structured=False, clock=time.time) -> OracleResult:
     P = NonnegPCAStructured(Z) if structured else NonnegPCAVectorized(Z)
     return RIPTRMOracle(option, clock=clock).run(P, x0, y0)

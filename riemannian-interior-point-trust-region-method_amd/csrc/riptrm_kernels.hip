@@ -1568,6 +1568,46 @@ __global__ void __launch_bounds__(ST_THREADS) k_hvp_epi(DevParams P, double mu, 
   for (int i = threadIdx.x; i < P.n; i += ST_THREADS) out[(int64_t)b * ldv + i] = U[i];
 }
 
+// RIPM's condensed Newton operator (src/solver/RIPM.py:485-487) after an HVP-style 2-RHS pass
+// (k_hvp_prep with y := z):  Aw(v) = P_x(-Sv) + (x^T S x + z^T x)(x^T x) v + P_x(w (v - x x^T v)),
+// w = z / s — HwCur's structure with RIPM's multipliers z and separate slacks s.
+__global__ void __launch_bounds__(ST_THREADS) k_aw_epi(DevParams P, const double* sl, double* out, int64_t ldv) {
+  __shared__ double redbuf[2 * ST_WAVES * RED_MAX];
+  const int b = blockIdx.x;
+  Machine M(P, b, 0, redbuf);
+  if (P.layout == RIPTRM_LAYOUT_SYMTILE) M.gather_out(2);
+  if (P.layout == RIPTRM_LAYOUT_SHARED) M.gather_slices(2);
+  const int n = P.n;
+  const double* X = M.V(V_X);
+  const double* Zm = M.V(V_Y);
+  const double* SX = M.V(V_OUT1);
+  const double* U = M.V(V_OUT0);
+  const double* Vv = M.V(V_IN0);
+  const double* Sl = sl + (int64_t)b * ldv;
+  double h[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
+  for (int i = threadIdx.x; i < n; i += ST_THREADS) {
+    h[0] += X[i] * X[i];
+    h[1] += X[i] * SX[i];
+    h[2] += Zm[i] * X[i];
+    h[3] += X[i] * U[i];
+    h[4] += X[i] * Vv[i];
+  }
+  bsum<5>(M.R, h);
+  const double coef = (h[1] + h[2]) * h[0];
+  const double xu = h[3], xv = h[4];
+  double r2[1] = {0.0};
+  for (int i = threadIdx.x; i < n; i += ST_THREADS) {
+    const double q = (Vv[i] - X[i] * xv) * (Zm[i] / Sl[i]);
+    r2[0] += X[i] * q;
+  }
+  bsum<1>(M.R, r2);
+  const double xq = r2[0];
+  for (int i = threadIdx.x; i < n; i += ST_THREADS) {
+    const double q = (Vv[i] - X[i] * xv) * (Zm[i] / Sl[i]);
+    out[(int64_t)b * ldv + i] = ((-U[i] + xu * X[i]) + coef * Vv[i]) + (q - xq * X[i]);
+  }
+}
+
 }  // namespace riptrm
 
 // ==========================================================================================
@@ -1833,6 +1873,23 @@ int riptrm_nonnegpca_hvp(riptrm_ctx* ctx, const double* x, const double* y, doub
   int rc = launch_gemv(ctx, ctx->stream, 0, -1, B);
   if (rc) return rc;
   hipLaunchKernelGGL(k_hvp_epi, dim3(B), dim3(ST_THREADS), 0, ctx->stream, ctx->P, mu, out, ldv);
+  HIPCHK(ctx, hipGetLastError());
+  ctx->solving = false;
+  return RIPTRM_OK;
+}
+
+int riptrm_nonnegpca_operator_aw(riptrm_ctx* ctx, const double* x, const double* z, const double* s, const double* v,
+                                 double* out, int64_t ldv) {
+  if (!ctx) return RIPTRM_E_ARG;
+  if (!ctx->bound) return fail(ctx, RIPTRM_E_STATE, "operator_aw: bind first");
+  if (!x || !z || !s || !v || !out || ldv < ctx->P.n) return fail(ctx, RIPTRM_E_ARG, "operator_aw: bad argument");
+  HIPCHK(ctx, hipSetDevice(ctx->device));
+  const int B = ctx->P.batch;
+  hipLaunchKernelGGL(k_hvp_prep, dim3(B), dim3(256), 0, ctx->stream, ctx->P, x, z, v, ldv);
+  HIPCHK(ctx, hipGetLastError());
+  int rc = launch_gemv(ctx, ctx->stream, 0, -1, B);
+  if (rc) return rc;
+  hipLaunchKernelGGL(k_aw_epi, dim3(B), dim3(ST_THREADS), 0, ctx->stream, ctx->P, s, out, ldv);
   HIPCHK(ctx, hipGetLastError());
   ctx->solving = false;
   return RIPTRM_OK;

@@ -358,6 +358,19 @@ class NonnegPCABatch:
         torch.cuda.synchronize(self.device)
         return out[:, :self.n]
 
+    def operator_aw(self, x, z, s, v) -> torch.Tensor:
+        """RIPM's OperatorAw(v) at (x, z, s) for every instance (src/solver/RIPM.py:485-487)."""
+        assert self.bound
+        X, Zt, St, V = self._padded(x), self._padded(z), self._padded(s), self._padded(v)
+        out = torch.zeros_like(X)
+        self._sync_stream()
+        self.ctx.check(self.lib.riptrm_nonnegpca_operator_aw(self.ctx.h, ctypes.c_void_p(X.data_ptr()),
+                                                             ctypes.c_void_p(Zt.data_ptr()), ctypes.c_void_p(St.data_ptr()),
+                                                             ctypes.c_void_p(V.data_ptr()), ctypes.c_void_p(out.data_ptr()),
+                                                             self.ld), "riptrm_nonnegpca_operator_aw")
+        torch.cuda.synchronize(self.device)
+        return out[:, :self.n]
+
     def tcg(self, x, y, mu, Delta, max_steps: int = 0):
         """truncated_conjugate_gradient at (x_b, y_b, mu_b, Delta_b) (RIPTRM.py:41-216 via
         compute_direction :445-452).  Returns (eta, Heta, j, stop_names)."""

@@ -63,6 +63,7 @@ SIGNATURES: Dict[str, tuple] = {
     "riptrm_nonnegpca_bind": (c_int32, [c_void_p, c_void_p, c_int32, c_int32, c_int32, c_int64,
                                         c_void_p, c_int64, c_int32]),
     "riptrm_nonnegpca_hvp": (c_int32, [c_void_p, c_void_p, c_void_p, c_double, c_void_p, c_void_p, c_int64]),
+    "riptrm_nonnegpca_operator_aw": (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64]),
     "riptrm_tcg": (c_int32, [c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p, P_int32, P_int32, c_int32]),
     "riptrm_solve_begin": (c_int32, [c_void_p, ctypes.POINTER(RiptrmOptions), c_void_p, c_void_p, c_int64,
                                      c_void_p, c_void_p, c_void_p, c_int32]),

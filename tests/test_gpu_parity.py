@@ -377,3 +377,25 @@ def test_run_batch_detects_shared_Z(fixture_n50):
     assert solver.last_layout == "shared"
     single = RIPTRM(_gpu_opt(maxiter=6)).run(NonnegPCAProblem(Z=Z, initialpoint=x0, initialineqLagmult=y0))
     np.testing.assert_allclose(outs[0].log["residual"], single.log["residual"], rtol=1e-6, atol=1e-13)
+
+
+@pytest.mark.parametrize("layout", ["sym", "full"])
+@pytest.mark.parametrize("n,B", [(23, 3), (1000, 2), (4000, 2)])
+def test_ripm_operator_aw_matches_oracle(n, B, layout):
+    """RIPM OperatorAw (RIPM.py:485-487) through the same S-pass as HwCur."""
+    Zs, xs, zs, ss, vs = [], [], [], [], []
+    for b in range(B):
+        Z, _, _ = G.generate_instance(n, 60 + b)
+        x, _ = _state(n, 70 + b)
+        rs = np.random.RandomState(80 + b)
+        Zs.append(Z); xs.append(x); zs.append(rs.rand(n) + 0.1); ss.append(rs.rand(n) + 0.2)
+        vs.append(rs.randn(n))
+    eng = _engine(np.stack(Zs), layout=layout)
+    out = eng.operator_aw(np.stack(xs), np.stack(zs), np.stack(ss), np.stack(vs)).cpu().numpy()
+    for b in range(B):
+        ref = O.ripm_operator_aw_vectorized(Zs[b], xs[b], zs[b], ss[b], vs[b])
+        assert np.linalg.norm(out[b] - ref) <= 1e-12 * np.linalg.norm(ref), b
+    if n <= 100:   # the reference's per-constraint wiring too
+        P = O.NonnegPCAStructured(Zs[0])
+        ref = O.ripm_operator_aw(P, xs[0], zs[0], ss[0], vs[0])
+        assert np.linalg.norm(out[0] - ref) <= 1e-12 * np.linalg.norm(ref)

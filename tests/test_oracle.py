@@ -180,3 +180,23 @@ def test_outer_comparator_on_branch_flips(n, seed, K):
     with pytest.raises(BranchFlip):
         compare_logs(a.log, b.log)
     compare_outer(a.log, b.log)
+
+
+def test_ripm_operator_aw_closed_form():
+    """RIPM OperatorAw (RIPM.py:485-487): per-constraint wiring == closed form,
+    and the operator is self-adjoint on the tangent space."""
+    from oracle import nonnegpca_gen as G2
+    Z, x0, _ = G2.generate_instance(23, 77)
+    rs = np.random.RandomState(1)
+    x = x0 / np.linalg.norm(x0)
+    z = rs.rand(23) + 0.1
+    s = rs.rand(23) + 0.2
+    P = O.NonnegPCAStructured(Z)
+    u = P.manifold.projection(x, rs.randn(23))
+    w = P.manifold.projection(x, rs.randn(23))
+    a = O.ripm_operator_aw(P, x, z, s, u)
+    b = O.ripm_operator_aw_vectorized(Z, x, z, s, u)
+    assert np.linalg.norm(a - b) <= 1e-12 * np.linalg.norm(a)
+    l = P.manifold.inner_product(x, O.ripm_operator_aw(P, x, z, s, u), w)
+    r = P.manifold.inner_product(x, u, O.ripm_operator_aw(P, x, z, s, w))
+    assert abs(l - r) <= 1e-11 * max(1.0, abs(l))
