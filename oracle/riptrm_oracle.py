@@ -49,6 +49,7 @@ from dataclasses import dataclass, field
 from typing import Any, Callable, Dict, List, Optional
 
 import numpy as np
+import scipy.linalg
 from scipy.linalg.blas import dsymv as _dsymv
 
 SPACING1 = np.spacing(1)  # RIPTRM.py:660 np.spacing(1)
@@ -402,7 +403,7 @@ def default_option() -> Dict[str, Any]:
         'forcing_function_complementarity': lambda mu: max(1e-3 * mu, 1e-14),
         'forcing_function_second_order': lambda mu: mu,
         'min_barrier_parameter': 1e-15,
-        'TRS_solver': 'tCG', 'second_order_stationarity': False,
+        'TRS_solver': 'tCG', 'second_order_stationarity': False, 'TRS_tolhardcase': 1e-8,
         'tCG_theta': 1, 'tCG_kappa': 0.1, 'tCG_mininner': 1,
         'initial_barrier_parameter': 0.1,
         'barrier_parameter_update_r': 0.01, 'barrier_parameter_update_c': 0.5,
@@ -523,6 +524,17 @@ class RIPTRMOracle:
         out["minyfeasi"] = min(yNew)
         out["compl"] = compl
         out["sNew"] = sNew
+        o = self.option
+        if o['TRS_solver'] == 'Exact_RepMat' and o['second_order_stationarity']:   # RIPTRM.py:599-617
+            from .trs_oracle import selfadj_operator2matrix
+            _, _, HwNew, _ = P.begin_inner(xNew, yNew, mu)
+            try:
+                Hm = selfadj_operator2matrix(P.manifold, xNew, HwNew, P.tangent_basis(xNew))
+                mineig = scipy.linalg.eigh(Hm, eigvals_only=True)[0]
+            except np.linalg.LinAlgError:
+                mineig = np.nan
+            out["mineigvalHw"] = mineig
+            out["mineigval_criterion"] = bool(mineig >= -o['forcing_function_second_order'](mu))
         return out
 
     # RIPTRM.py:631-705
@@ -572,12 +584,18 @@ class RIPTRMOracle:
         info = self.initial_inner_info(inner_iteration, Delta)
         M = P.manifold
         cx, s, Hw, c = P.begin_inner(x, y, mu)
-        dx, _, j, stop = truncated_conjugate_gradient(M, Hw, x, c, Delta, o['tCG_theta'], o['tCG_kappa'],
-                                                      o['tCG_mininner'], M.dim)
+        if o['TRS_solver'] == 'Exact_RepMat':   # RIPTRM.py:433-444 (trs_oracle)
+            from .trs_oracle import exact_repmat_direction
+            dx, _, kind, _ = exact_repmat_direction(M, x, Hw, c, Delta, P.tangent_basis(x), o['TRS_tolhardcase'])
+            j, stop = -1, None
+            info["dxtype"] = kind
+        else:
+            dx, _, j, stop = truncated_conjugate_gradient(M, Hw, x, c, Delta, o['tCG_theta'], o['tCG_kappa'],
+                                                          o['tCG_mininner'], M.dim)
+            info["dxtype"] = f"tCG_{stop}"
         # Hessian-vector products performed inside tCG = j + 1 (loop index at exit)
         self.tcg_total += j + 1
         self.passes += j + 1
-        info["dxtype"] = f"tCG_{stop}"
         normdx = M.norm(x, dx)
         info["normdx"] = normdx
         dy = P.dy(x, y, s, mu, dx)
@@ -589,9 +607,10 @@ class RIPTRMOracle:
         info["minxfeasi"] = cr["minxfeasi"]
         info["minyfeasi"] = cr["minyfeasi"]
         info["compl"] = cr["compl"]
+        info["mineigvalHw"] = cr.get("mineigvalHw")
         rec = {"tcg_iters": j + 1, "tcg_stop": stop, "normdx": normdx, "Delta": Delta, "mu": mu}
         if (cr["xfeasi_criterion"] and cr["yfeasi_criterion"] and cr["normgradLagfun_criterion"]
-                and cr["complementary_criterion"]):
+                and cr["complementary_criterion"] and cr.get("mineigval_criterion", True)):
             info["inner_status"] = "converged"
             rec["status"] = "converged"
             self.trace.append(rec)

@@ -269,6 +269,10 @@ class _SIBase:
     def slack(self, x):
         return -self.ineq_values(x)
 
+    def tangent_basis(self, x):
+        from .trs_oracle import si_tangent_basis
+        return si_tangent_basis(x)
+
     def maxmeanviolations(self, x):
         mx, mean = 0, 0
         for g in self.ineq_values(x):
