@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define RIPTRM_ABI_VERSION 2
+#define RIPTRM_ABI_VERSION 3
 
 /* status codes */
 #define RIPTRM_OK 0
@@ -44,6 +44,17 @@ extern "C" {
 #define RIPTRM_TCG_MODEL_INCREASED 3
 #define RIPTRM_TCG_REACHED_TARGET_LINEAR 4
 #define RIPTRM_TCG_REACHED_TARGET_SUPERLINEAR 5
+/* Exact_RepMat direction types (TRSgep's `type`, RIPTRM.py:263,270,280,297), same log field */
+#define RIPTRM_TRS_BOUNDARY 6
+#define RIPTRM_TRS_INTERIOR 7
+#define RIPTRM_TRS_HARDCASE_1 8
+
+/* TRS_solver option (RIPTRM.py:325) */
+#define RIPTRM_TRS_SOLVER_TCG 0
+#define RIPTRM_TRS_SOLVER_EXACT_REPMAT 1
+/* Exact_RepMat works on the dim x dim matrix of HwCur in LDS: manifold.dim <= this
+ * (NonnegPCA n <= 97, StableIdentification d <= 7) */
+#define RIPTRM_TRS_DIM_MAX 96
 
 /* inner_status codes (RIPTRM.py:763,770,678,698,829,837); 0 = None */
 #define RIPTRM_IS_NONE 0
@@ -92,6 +103,7 @@ enum riptrm_log_field {
     RIPTRM_LOG_DXTYPE, RIPTRM_LOG_NORMDX, RIPTRM_LOG_MINXFEASI, RIPTRM_LOG_MINYFEASI,
     RIPTRM_LOG_COMPL, RIPTRM_LOG_HAS_RATIO, RIPTRM_LOG_ARED_PRED, RIPTRM_LOG_RADIUS_UPDATE,
     RIPTRM_LOG_DUAL_CLIPPING, RIPTRM_LOG_MAXABSLAGMULT, RIPTRM_LOG_TCG_ITERS,
+    RIPTRM_LOG_HAS_MINEIG, RIPTRM_LOG_MINEIGVALHW,
     RIPTRM_LOG_NFIELDS_USED
 };
 #define RIPTRM_LOG_NFIELDS 32
@@ -133,6 +145,9 @@ typedef struct riptrm_options {
     double tcg_kappa;                 /* 'tCG_kappa' */
     double const_left;                /* 'const_left' */
     double const_right;               /* 'const_right' */
+    int32_t trs_solver;               /* 'TRS_solver': RIPTRM_TRS_SOLVER_* */
+    int32_t second_order_stationarity;/* 'second_order_stationarity' (bool; Exact_RepMat only) */
+    double trs_tolhardcase;           /* 'TRS_tolhardcase' */
 } riptrm_options;
 
 typedef struct riptrm_ctx riptrm_ctx;
@@ -280,6 +295,16 @@ int riptrm_si_profile_read(riptrm_ctx* ctx, double* seconds);
 int riptrm_si_solve(riptrm_ctx* ctx, const riptrm_options* opt, const double* x0, const double* y0,
                     const double* mu_table, const double* tolL_table, const double* tolC_table,
                     int32_t table_len);
+
+/* ==== Exact_RepMat trust-region subproblem ==============================
+ * TRSgep(A, a, B = I, Delta, tolhardcase) (src/solver/RIPTRM.py:218-299) for a batch of dense
+ * symmetric dim x dim matrices: instance b's A at A + b*a_stride (row-major, leading dimension
+ * lda), a / x at a + b*ldv, x + b*ldv; Delta, lam1, mineig: batch doubles; kind: batch int32
+ * (RIPTRM_TRS_*).  mineig (may be NULL) = the smallest eigenvalue of A (RIPTRM.py:611).
+ * 1 <= dim <= RIPTRM_TRS_DIM_MAX.  One workgroup per instance.  Asynchronous. */
+int riptrm_trs_gep(riptrm_ctx* ctx, int32_t dim, int32_t batch, const double* A, int64_t lda, int64_t a_stride,
+                   const double* a, int64_t ldv, const double* Delta, double tolhardcase, double* x,
+                   double* lam1, int32_t* kind, double* mineig);
 
 /* ==== Stiefel(n, p) manifold operations =========================================
  * Not in the reference (north_star / BASELINE configs[4] ask for them): pymanopt 2.x formulas,

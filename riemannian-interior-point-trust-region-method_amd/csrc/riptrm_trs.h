@@ -1,0 +1,438 @@
+// riptrm_trs.h — the Exact_RepMat trust-region subproblem solve on one workgroup (gfx950).
+//
+// Reference: TRSgep (src/solver/RIPTRM.py:218-299), called by compute_direction's Exact_RepMat
+// branch (RIPTRM.py:433-444) with B = I on the matrix of HwCur in an orthonormal tangent basis
+// (selfadj_operator2matrix, src/solver/utils.py:565-573), and the second-order stationarity test
+// (RIPTRM.py:599-617: smallest eigenvalue of the same matrix at the trial point).
+//
+//   minimize x^T A x / 2 + a^T x   s.t.  ||x|| <= Delta
+//
+// The reference takes the rightmost eigenpair of the 2n x 2n pencil (MM0, -MM1) (Adachi et al.
+// 2017).  Its rightmost eigenvalue is the rightmost root lam1 of ||(A + lam I)^-1 a|| = Delta on
+// (-lam_min, inf), so the device solves the same three-candidate problem from the symmetric
+// eigendecomposition A = Q diag(lam) Q^T (restated in oracle/trs_oracle.py::trs_eigh):
+//   * interior candidate p1: SciPy's CG on A p = -a (RIPTRM.py:245-251, loop for loop as
+//     scipy.sparse.linalg.cg 1.15: x0 = 0, rtol 1e-5, maxiter 10 n), kept iff
+//     ||A p1 + a|| / ||a|| < 1e-5 and p1^T p1 < Delta^2;
+//   * hard case (a orthogonal to the lam_min eigenspace and ||x2|| < Delta): lam1 = -lam_min,
+//     x = x2 + alp q_min (RIPTRM.py:266-291);
+//   * boundary: safeguarded Newton on 1/||x(lam)|| - 1/Delta from lam = -lam_min + ||a||/Delta,
+//     x = -(A + lam1 I)^-1 a rescaled to ||x|| = Delta (RIPTRM.py:262);
+//   * interior wins if its model value is <= the boundary one (RIPTRM.py:294-298).
+// The eigendecomposition is a parallel two-sided cyclic Jacobi (round-robin pair ordering: all
+// dim/2 rotations of a round are disjoint and applied at once by the whole workgroup) on the
+// matrix held in LDS — eigenvalues to high relative accuracy, no library call, no host round trip.
+//
+// Every thread of the NT-thread workgroup must call every function here (they synchronise).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include "riptrm_wave.h"
+
+namespace riptrm_trs {
+
+#pragma clang fp contract(off)
+
+constexpr int DIM_MAX = 96;   // LDS: 2 * 96 * 97 doubles = 146 KiB (matrix + eigenvectors)
+
+enum Kind : int { K_BOUNDARY = 0, K_INTERIOR = 1, K_HARDCASE_1 = 2 };
+
+// odd row stride: column walks of the Jacobi rotations spread over the LDS banks
+__host__ __device__ constexpr int lda_of(int dim) { return dim | 1; }
+
+// LDS doubles of a Work area for dim (matrix, eigenvectors, vectors, rotation table)
+__host__ __device__ constexpr int work_doubles(int dim) {
+  return 2 * dim * lda_of(dim) + 8 * DIM_MAX + 5 * (DIM_MAX / 2 + 1);
+}
+
+struct Work {
+  double* A;    // dim x lda  (destroyed: eigenvalues end on the diagonal)
+  double* V;    // dim x lda  eigenvectors (columns)
+  double* a;    // dim   linear term
+  double* x;    // dim   solution
+  double* p;    // dim   CG direction / scratch
+  double* r;    // dim   CG residual / scratch
+  double* q;    // dim   CG A p / scratch
+  double* cgx;  // dim   CG iterate (the interior candidate p1)
+  double* g;    // dim   Q^T a
+  double* ev;   // dim   eigenvalues (copied off the diagonal)
+  double* rot;  // 5 x (DIM_MAX/2 + 1)  (c, s, t, a_pp, a_qq) per pair
+  int dim, lda;
+};
+
+// carve a Work out of an LDS area of work_doubles(dim) doubles
+__device__ __forceinline__ Work make_work(double* base, int dim) {
+  Work w;
+  w.dim = dim;
+  w.lda = lda_of(dim);
+  const int mat = dim * w.lda;
+  w.A = base;
+  w.V = base + mat;
+  double* v = base + 2 * mat;
+  w.a = v;
+  w.x = v + DIM_MAX;
+  w.p = v + 2 * DIM_MAX;
+  w.r = v + 3 * DIM_MAX;
+  w.q = v + 4 * DIM_MAX;
+  w.cgx = v + 5 * DIM_MAX;
+  w.g = v + 6 * DIM_MAX;
+  w.ev = v + 7 * DIM_MAX;
+  w.rot = v + 8 * DIM_MAX;
+  return w;
+}
+
+// Workgroup reductions for NT threads: in-wave DPP/permlane reduction (riptrm_wave.h), then the
+// NW wave partials through LDS in wave order.  Every thread gets the bitwise-identical value.
+template <int NT>
+struct Blk {
+  static constexpr int NW = NT / 64;
+  double* red;  // LDS, 2 * NW doubles (unused when NW == 1)
+  int par;
+  __device__ __forceinline__ explicit Blk(double* red_) : red(red_), par(0) {}
+  template <int OP>
+  __device__ __forceinline__ double reduce(double v) {
+    v = riptrm_wave::wave_reduce<OP>(v);
+    if constexpr (NW == 1) {
+      return v;
+    } else {
+      double* b = red + par * NW;
+      par ^= 1;
+      if ((threadIdx.x & 63) == 0) b[threadIdx.x >> 6] = v;
+      __syncthreads();
+      double s = b[0];
+#pragma unroll
+      for (int i = 1; i < NW; ++i) s = riptrm_wave::comb<OP>(s, b[i]);
+      return s;
+    }
+  }
+  __device__ __forceinline__ double sum(double v) { return reduce<0>(v); }
+  __device__ __forceinline__ double min(double v) { return reduce<1>(v); }
+  __device__ __forceinline__ double max(double v) { return reduce<2>(v); }
+};
+
+// round-robin tournament: pair k of round r among me (even) players, p < q
+__device__ __forceinline__ void pair_of(int r, int k, int me, int& p, int& q) {
+  const int m1 = me - 1;
+  int u, v;
+  if (k == 0) {
+    u = 0;
+    v = 1 + r % m1;
+  } else {
+    u = 1 + (r + k) % m1;
+    v = 1 + (r + m1 - k) % m1;
+  }
+  p = u < v ? u : v;
+  q = u < v ? v : u;
+}
+
+// Parallel cyclic Jacobi on the symmetric dim x dim matrix w.A (LDS).  On return w.ev holds the
+// eigenvalues (diagonal order) and, if want_v, w.V the eigenvectors as columns (A0 = V diag V^T).
+// Rotation formulas: Numerical Recipes' (same as the serial jacobi_reg of riptrm_si.hip).
+template <int NT>
+__device__ void jacobi(Blk<NT>& B, Work& w, bool want_v) {
+  const int tid = threadIdx.x;
+  const int m = w.dim, lda = w.lda;
+  double* A = w.A;
+  double* V = w.V;
+  double* rot = w.rot;
+  if (want_v)
+    for (int e = tid; e < m * m; e += NT) {
+      const int i = e / m, j = e - i * m;
+      V[i * lda + j] = (i == j) ? 1.0 : 0.0;
+    }
+  const int me = m + (m & 1);
+  const int np = me / 2;
+  __syncthreads();
+  for (int sweep = 0; sweep < 40 && m > 1; ++sweep) {
+    double off = 0.0, dg = 0.0;
+    for (int e = tid; e < m * m; e += NT) {
+      const int i = e / m, j = e - i * m;
+      const double v = A[i * lda + j];
+      if (j > i) off += v * v;
+      else if (j == i) dg += v * v;
+    }
+    off = B.sum(off);
+    dg = B.sum(dg);
+    if (off <= 1e-36 * dg) break;   // off-diagonal far below the eigenvalues' rounding
+    for (int r = 0; r < me - 1; ++r) {
+      for (int k = tid; k < np; k += NT) {
+        int p, q;
+        pair_of(r, k, me, p, q);
+        double c = 1.0, s = 0.0, t = 0.0, app = 0.0, aqq = 0.0;
+        if (q < m) {
+          const double apq = A[p * lda + q];
+          app = A[p * lda + p];
+          aqq = A[q * lda + q];
+          if (apq != 0.0) {
+            const double theta = (aqq - app) / (2.0 * apq);
+            t = (theta >= 0.0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
+            c = 1.0 / sqrt(t * t + 1.0);
+            s = t * c;
+            app = app - t * apq;
+            aqq = aqq + t * apq;
+          }
+        }
+        rot[5 * k + 0] = c;
+        rot[5 * k + 1] = s;
+        rot[5 * k + 2] = t;
+        rot[5 * k + 3] = app;
+        rot[5 * k + 4] = aqq;
+      }
+      __syncthreads();
+      // columns p, q of A (and V): A <- A J
+      for (int e = tid; e < m * np; e += NT) {
+        const int k = e / m, i = e - k * m;
+        const double s = rot[5 * k + 1];
+        if (s == 0.0) continue;
+        int p, q;
+        pair_of(r, k, me, p, q);
+        const double c = rot[5 * k];
+        const double aip = A[i * lda + p], aiq = A[i * lda + q];
+        A[i * lda + p] = c * aip - s * aiq;
+        A[i * lda + q] = s * aip + c * aiq;
+        if (want_v) {
+          const double vip = V[i * lda + p], viq = V[i * lda + q];
+          V[i * lda + p] = c * vip - s * viq;
+          V[i * lda + q] = s * vip + c * viq;
+        }
+      }
+      __syncthreads();
+      // rows p, q: A <- J^T A
+      for (int e = tid; e < m * np; e += NT) {
+        const int k = e / m, j = e - k * m;
+        const double s = rot[5 * k + 1];
+        if (s == 0.0) continue;
+        int p, q;
+        pair_of(r, k, me, p, q);
+        const double c = rot[5 * k];
+        const double apj = A[p * lda + j], aqj = A[q * lda + j];
+        A[p * lda + j] = c * apj - s * aqj;
+        A[q * lda + j] = s * apj + c * aqj;
+      }
+      __syncthreads();
+      // the rotated 2 x 2 block exactly: a_pq = 0, a_pp / a_qq by the stable update
+      for (int k = tid; k < np; k += NT) {
+        if (rot[5 * k + 1] == 0.0) continue;
+        int p, q;
+        pair_of(r, k, me, p, q);
+        A[p * lda + q] = 0.0;
+        A[q * lda + p] = 0.0;
+        A[p * lda + p] = rot[5 * k + 3];
+        A[q * lda + q] = rot[5 * k + 4];
+      }
+      __syncthreads();
+    }
+  }
+  for (int i = tid; i < m; i += NT) w.ev[i] = A[i * lda + i];
+  __syncthreads();
+}
+
+// smallest eigenvalue of w.A (destroys w.A): RIPTRM.py:611-612
+template <int NT>
+__device__ double min_eig(Blk<NT>& B, Work& w) {
+  jacobi<NT>(B, w, false);
+  double v = INFINITY;
+  for (int i = threadIdx.x; i < w.dim; i += NT) v = fmin(v, w.ev[i]);
+  return B.min(v);
+}
+
+// y = A v over the LDS matrix, one thread per row (row sums in column order)
+template <int NT>
+__device__ __forceinline__ void matvec(const Work& w, const double* v, double* y) {
+  const int m = w.dim, lda = w.lda;
+  for (int i = threadIdx.x; i < m; i += NT) {
+    const double* row = w.A + i * lda;
+    double acc = 0.0;
+    for (int k = 0; k < m; ++k) acc += row[k] * v[k];
+    y[i] = acc;
+  }
+}
+
+struct Result {
+  double lam1;
+  int kind;
+};
+
+// TRSgep(A, a, I, Delta, tolhardcase): w.A, w.a filled by the caller (A symmetric).  Writes the
+// solution into w.x; w.A is destroyed.
+template <int NT>
+__device__ Result trs_solve(Blk<NT>& B, Work& w, double Delta, double tolhardcase) {
+  const int tid = threadIdx.x;
+  const int m = w.dim;
+  const double D2 = Delta * Delta;
+  // ---- interior candidate: scipy.sparse.linalg.cg(A, -a) (RIPTRM.py:245) -----------------
+  double an = 0.0;
+  for (int i = tid; i < m; i += NT) {
+    const double b = -w.a[i];
+    w.cgx[i] = 0.0;
+    w.r[i] = b;
+    an += b * b;
+  }
+  an = sqrt(B.sum(an));   // ||b|| = ||a||
+  __syncthreads();
+  bool cg_ok = false;
+  double p1obj = 0.0;
+  if (an == 0.0) {
+    // cg returns b itself (= -a = 0); the residual test divides by ||a|| = 0 -> not eligible
+    cg_ok = false;
+  } else {
+    const double atol = 1e-5 * an;
+    double rho_prev = 1.0;
+    for (int it = 0; it < 10 * m; ++it) {
+      double rr = 0.0;
+      for (int i = tid; i < m; i += NT) rr += w.r[i] * w.r[i];
+      rr = B.sum(rr);
+      if (sqrt(rr) < atol) break;
+      const double rho = rr;   // dot(r, z) with z = r (no preconditioner)
+      const double beta = it > 0 ? rho / rho_prev : 0.0;
+      for (int i = tid; i < m; i += NT) w.p[i] = it > 0 ? w.p[i] * beta + w.r[i] : w.r[i];
+      __syncthreads();
+      matvec<NT>(w, w.p, w.q);
+      __syncthreads();
+      double pq = 0.0;
+      for (int i = tid; i < m; i += NT) pq += w.p[i] * w.q[i];
+      pq = B.sum(pq);
+      const double alpha = rho / pq;
+      for (int i = tid; i < m; i += NT) {
+        w.cgx[i] += alpha * w.p[i];
+        w.r[i] -= alpha * w.q[i];
+      }
+      rho_prev = rho;
+      __syncthreads();
+    }
+    // ||A p1 + a|| / ||a|| < 1e-5 and p1^T p1 < Delta^2 (RIPTRM.py:246-251)
+    matvec<NT>(w, w.cgx, w.q);
+    __syncthreads();
+    double v3[3] = {0.0, 0.0, 0.0};
+    for (int i = tid; i < m; i += NT) {
+      const double res = w.q[i] + w.a[i];
+      v3[0] += res * res;
+      v3[1] += w.cgx[i] * w.cgx[i];
+      v3[2] += w.cgx[i] * w.q[i];
+    }
+    const double res2 = B.sum(v3[0]);
+    const double pp = B.sum(v3[1]);
+    const double pAp = B.sum(v3[2]);
+    double ap = 0.0;
+    for (int i = tid; i < m; i += NT) ap += w.a[i] * w.cgx[i];
+    ap = B.sum(ap);
+    cg_ok = (sqrt(res2) / an < 1e-5) && (pp < D2);
+    p1obj = 0.5 * pAp + ap;
+  }
+  // ---- eigendecomposition ------------------------------------------------------------------
+  jacobi<NT>(B, w, true);
+  const int lda = w.lda;
+  double lmin = INFINITY, lmax_abs = 0.0;
+  for (int i = tid; i < m; i += NT) {
+    lmin = fmin(lmin, w.ev[i]);
+    lmax_abs = fmax(lmax_abs, fabs(w.ev[i]));
+  }
+  lmin = B.min(lmin);
+  lmax_abs = B.max(lmax_abs);
+  // index of lmin (the lowest such index) and g = Q^T a
+  double imin = INFINITY;
+  for (int i = tid; i < m; i += NT) {
+    if (w.ev[i] == lmin) imin = fmin(imin, (double)i);
+    double acc = 0.0;
+    for (int k = 0; k < m; ++k) acc += w.V[k * lda + i] * w.a[k];
+    w.g[i] = acc;
+  }
+  const int kmin = (int)B.min(imin);
+  __syncthreads();
+  const double hard_tol = 1e-12 * fmax(1.0, lmax_abs);
+  double gh = 0.0, gg = 0.0;
+  for (int i = tid; i < m; i += NT) {
+    const double gi = w.g[i];
+    gg += gi * gi;
+    if (fabs(w.ev[i] - lmin) <= hard_tol) gh += gi * gi;
+  }
+  const double ghard = sqrt(B.sum(gh));
+  const double gn = sqrt(B.sum(gg));
+  const double lo = -lmin;
+  Result res{0.0, K_BOUNDARY};
+  bool have = false;
+  double xobj = 0.0;
+  if (ghard <= tolhardcase * gn) {
+    // hard case candidate: x2 = -(A - lmin I)^+ a on the non-hard eigenvectors
+    double x2 = 0.0;
+    for (int i = tid; i < m; i += NT) {
+      const bool hs = fabs(w.ev[i] - lmin) <= hard_tol;
+      const double c = hs ? 0.0 : -w.g[i] / (w.ev[i] - lmin);
+      w.p[i] = c;   // eigen coordinates
+      x2 += c * c;
+    }
+    x2 = B.sum(x2);
+    if (x2 < D2) {
+      const double alp = sqrt(D2 - x2);
+      __syncthreads();
+      if (tid == 0) w.p[kmin] += alp;   // x = Q (x2c + alp e_kmin)
+      __syncthreads();
+      res.lam1 = lo;
+      res.kind = K_HARDCASE_1;
+      have = true;
+    }
+  }
+  if (!have) {
+    // boundary: Newton on phi(l) = 1/||x(l)|| - 1/Delta, x(l) = -(Lam + l)^-1 g
+    double l1 = lo + gn / Delta;
+    for (int itn = 0; itn < 100; ++itn) {
+      double s2 = 0.0, s3 = 0.0;
+      for (int i = tid; i < m; i += NT) {
+        const double den = w.ev[i] + l1;
+        const double gi = w.g[i];
+        s2 += (gi / den) * (gi / den);
+        s3 += (gi * gi) / (den * den * den);
+      }
+      s2 = B.sum(s2);
+      s3 = B.sum(s3);
+      const double xn = sqrt(s2);
+      const double f = 1.0 / xn - 1.0 / Delta;
+      const double fp = s3 / (xn * xn * xn);
+      double nl = l1 - f / fp;
+      if (nl <= lo) nl = 0.5 * (lo + l1);
+      if (fabs(nl - l1) <= 1e-15 * fmax(1.0, fabs(l1))) {
+        l1 = nl;
+        break;
+      }
+      l1 = nl;
+    }
+    double s2 = 0.0;
+    for (int i = tid; i < m; i += NT) {
+      const double c = -w.g[i] / (w.ev[i] + l1);
+      w.p[i] = c;
+      s2 += c * c;
+    }
+    const double sc = Delta / sqrt(B.sum(s2));   // x / ||x|| * Delta (RIPTRM.py:262)
+    __syncthreads();
+    for (int i = tid; i < m; i += NT) w.p[i] = w.p[i] * sc;
+    res.lam1 = l1;
+    res.kind = K_BOUNDARY;
+  }
+  __syncthreads();
+  // model value of the eigen-coordinate candidate: sum lam c^2 / 2 + g.c
+  double o2[2] = {0.0, 0.0};
+  for (int i = tid; i < m; i += NT) {
+    const double c = w.p[i];
+    o2[0] += w.ev[i] * c * c;
+    o2[1] += w.g[i] * c;
+  }
+  xobj = 0.5 * B.sum(o2[0]) + B.sum(o2[1]);
+  const bool interior = cg_ok && p1obj <= xobj;   // RIPTRM.py:294-298
+  for (int i = tid; i < m; i += NT) {
+    if (interior) {
+      w.x[i] = w.cgx[i];
+    } else {
+      double acc = 0.0;
+      for (int k = 0; k < m; ++k) acc += w.V[i * lda + k] * w.p[k];
+      w.x[i] = acc;
+    }
+  }
+  if (interior) {
+    res.lam1 = 0.0;
+    res.kind = K_INTERIOR;
+  }
+  __syncthreads();
+  return res;
+}
+
+}  // namespace riptrm_trs

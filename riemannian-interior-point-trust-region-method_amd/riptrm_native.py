@@ -34,6 +34,7 @@ class RiptrmOptions(ctypes.Structure):
         ("maximal_tr_radius", c_double), ("rho", c_double), ("reduction_regularization", c_double),
         ("gamma", c_double), ("tcg_theta", c_double), ("tcg_kappa", c_double),
         ("const_left", c_double), ("const_right", c_double),
+        ("trs_solver", c_int32), ("second_order_stationarity", c_int32), ("trs_tolhardcase", c_double),
     ]
 
 
@@ -87,6 +88,8 @@ SIGNATURES: Dict[str, tuple] = {
     "riptrm_stiefel_retr": (c_int32, [c_void_p, c_int32, c_int32, c_int32, c_int64, c_void_p, c_void_p, c_void_p]),
     "riptrm_stiefel_ehess2rhess": (c_int32, [c_void_p, c_int32, c_int32, c_int32, c_int64, c_void_p, c_void_p, c_void_p,
                                              c_void_p, c_void_p]),
+    "riptrm_trs_gep": (c_int32, [c_void_p, c_int32, c_int32, c_void_p, c_int64, c_int64, c_void_p, c_int64, c_void_p,
+                                 c_double, c_void_p, c_void_p, c_void_p, c_void_p]),
     "riptrm_si_solve": (c_int32, [c_void_p, ctypes.POINTER(RiptrmOptions), c_void_p, c_void_p, c_void_p, c_void_p,
                                   c_void_p, c_int32]),
 }

@@ -1,0 +1,73 @@
+"""Exact_RepMat trust-region subproblem solver on the MI355X (csrc/riptrm_trs.hip, riptrm_trs.h).
+
+``TRSgep(A, a, B, Del, tolhardcase)`` keeps the reference's signature and return value
+(src/solver/RIPTRM.py:218-299: ``(x, lam1, type)``); ``trs_gep_batched`` solves a batch of
+subproblems held as torch tensors on the GPU in one launch.  Only B = I is supported — the one
+call site passes ``np.eye(xdim)`` (RIPTRM.py:441).  No CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Tuple
+
+import numpy as np
+import torch
+
+import riptrm_native as N
+from engine import _stream_handle
+
+C = N.CONST
+KIND_NAMES = {C["RIPTRM_TRS_BOUNDARY"]: "boundary", C["RIPTRM_TRS_INTERIOR"]: "interior",
+              C["RIPTRM_TRS_HARDCASE_1"]: "hardcase_1"}
+DIM_MAX = C["RIPTRM_TRS_DIM_MAX"]
+
+_ctx = {}
+
+
+def _context(device: torch.device) -> N.Context:
+    c = _ctx.get(device.index)
+    if c is None:
+        c = _ctx[device.index] = N.Context(device.index, _stream_handle(device))
+    c.set_stream(_stream_handle(device))
+    return c
+
+
+def trs_gep_batched(A: torch.Tensor, a: torch.Tensor, Delta: torch.Tensor, tolhardcase: float = 1e-8
+                    ) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor, torch.Tensor]:
+    """A: (batch, dim, dim) symmetric, a: (batch, dim), Delta: (batch,), fp64 contiguous on one GPU.
+    Returns (x (batch, dim), lam1 (batch,), kind (batch,) int32 RIPTRM_TRS_*, mineig (batch,))."""
+    if not torch.cuda.is_available():
+        raise RuntimeError("trs_gep_batched needs a ROCm GPU (gfx950); there is no CPU fallback")
+    if A.dim() != 3 or A.shape[1] != A.shape[2] or a.shape != A.shape[:2] or Delta.shape != A.shape[:1]:
+        raise ValueError("expected A (batch, dim, dim), a (batch, dim), Delta (batch,)")
+    dev = A.device
+    for t in (A, a, Delta):
+        if t.dtype != torch.float64 or t.device != dev or not t.is_contiguous():
+            raise ValueError("expected contiguous float64 tensors on one GPU")
+    B, dim = A.shape[0], A.shape[1]
+    if not 1 <= dim <= DIM_MAX:
+        raise ValueError(f"Exact_RepMat on the GPU supports 1 <= dim <= {DIM_MAX} (got {dim})")
+    ctx = _context(dev)
+    x = torch.empty((B, dim), dtype=torch.float64, device=dev)
+    lam1 = torch.empty(B, dtype=torch.float64, device=dev)
+    kind = torch.empty(B, dtype=torch.int32, device=dev)
+    mineig = torch.empty(B, dtype=torch.float64, device=dev)
+    p = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    ctx.check(ctx.lib.riptrm_trs_gep(ctx.h, dim, B, p(A), dim, dim * dim, p(a), dim, p(Delta), float(tolhardcase),
+                                     p(x), p(lam1), p(kind), p(mineig)), "riptrm_trs_gep")
+    return x, lam1, kind, mineig
+
+
+def TRSgep(A, a, B, Del, tolhardcase=1e-4):
+    """RIPTRM.py:218-299 on the GPU: returns (x, lam1, type) as numpy / float / str."""
+    A = np.asarray(A, dtype=np.float64)
+    if B is not None and not np.array_equal(np.asarray(B), np.eye(A.shape[0])):
+        raise NotImplementedError("TRSgep on the GPU supports B = I only (the call site RIPTRM.py:441)")
+    dev = torch.device("cuda", torch.cuda.current_device())
+    At = torch.as_tensor(A, device=dev).reshape(1, *A.shape).contiguous()
+    at = torch.as_tensor(np.asarray(a, dtype=np.float64), device=dev).reshape(1, -1).contiguous()
+    Dt = torch.tensor([float(Del)], dtype=torch.float64, device=dev)
+    x, lam1, kind, _ = trs_gep_batched(At, at, Dt, tolhardcase)
+    torch.cuda.synchronize(dev)
+    k = int(kind[0])
+    return x[0].cpu().numpy(), (0 if k == C["RIPTRM_TRS_INTERIOR"] else float(lam1[0])), KIND_NAMES[k]

@@ -1,0 +1,103 @@
+"""GPU parity of the Exact_RepMat subproblem solver (csrc/riptrm_trs.hip) against the reference's
+own formulation restated in oracle/trs_oracle.py::trs_gep (RIPTRM.py:218-299: the 2n x 2n pencil
+(MM0, -MM1) + SciPy CG interior candidate + hard-case refinement).
+
+Bar: same `type`; x within 1e-8 relative (the pencil's QZ and the device's Jacobi + secular Newton
+agree to that level: tests/test_trs_oracle.py pins the same bound between the two CPU forms).  The
+interior candidate is a CG iterate stopped at rtol 1e-5 whose value moves with the mat-vec summation
+order (up to ~1e-5 relative at dim 77, cond ~1e3): there both must pass the reference's acceptance
+test ||A p1 + a|| / ||a|| < 1e-5 (RIPTRM.py:246), agree to 1e-4 and in model value to 1e-8;
+lam1 within 1e-8; the smallest eigenvalue (RIPTRM.py:611) within 1e-11 relative to ||A||.  Hard
+case: the sign of the q_min component is arbitrary in both, so the model values are compared."""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+from oracle import trs_oracle as T
+
+
+def _obj(A, a, x):
+    return 0.5 * x @ A @ x + a @ x
+
+
+def _cases(seed, count, dims):
+    rs = np.random.RandomState(seed)
+    out = []
+    for t in range(count):
+        n = dims[t % len(dims)]
+        M = rs.randn(n, n)
+        kind = t % 4
+        if kind == 0:                 # positive definite, small radius -> boundary
+            A = M @ M.T + 0.1 * np.eye(n)
+            Del = 10 ** rs.uniform(-2, -0.5)
+        elif kind == 1:               # positive definite, large radius -> interior
+            A = M @ M.T + np.eye(n)
+            Del = 100.0
+        else:                         # indefinite -> boundary
+            A = M + M.T
+            Del = 10 ** rs.uniform(-2, 1)
+        out.append((A, rs.randn(n), Del))
+    return out
+
+
+def _solve(cases, tol=1e-8):
+    from trs import trs_gep_batched
+    dim = cases[0][0].shape[0]
+    A = torch.tensor(np.stack([c[0] for c in cases]), device="cuda")
+    a = torch.tensor(np.stack([c[1] for c in cases]), device="cuda")
+    D = torch.tensor([c[2] for c in cases], dtype=torch.float64, device="cuda")
+    x, lam1, kind, mineig = trs_gep_batched(A, a, D, tol)
+    torch.cuda.synchronize()
+    return x.cpu().numpy(), lam1.cpu().numpy(), kind.cpu().numpy(), mineig.cpu().numpy()
+
+
+@pytest.mark.parametrize("dim", [1, 2, 5, 17, 40, 49, 64, 77, 96])
+def test_trs_gep_matches_pencil_oracle(dim):
+    from trs import KIND_NAMES
+    cases = _cases(dim, 12, [dim])
+    x, lam1, kind, mineig = _solve(cases)
+    for b, (A, a, Del) in enumerate(cases):
+        xr, lr, kr = T.trs_gep(A, a, Del, 1e-8)
+        assert KIND_NAMES[int(kind[b])] == kr, (b, KIND_NAMES[int(kind[b])], kr)
+        if kr == "interior":   # both are CG iterates meeting the reference's own acceptance test
+            assert np.linalg.norm(x[b] - xr) <= 1e-4 * np.linalg.norm(xr), b
+            assert np.linalg.norm(A @ x[b] + a) / np.linalg.norm(a) < 1e-5, b
+            assert abs(_obj(A, a, x[b]) - _obj(A, a, xr)) <= 1e-8 * abs(_obj(A, a, xr)), b
+        else:
+            assert np.linalg.norm(x[b] - xr) <= 1e-8 * max(np.linalg.norm(xr), 1e-300), (b, kr)
+        assert abs(lam1[b] - lr) <= 1e-8 * max(1.0, abs(lr)), (b, lam1[b], lr)
+        ev = np.linalg.eigvalsh(A)[0]
+        assert abs(mineig[b] - ev) <= 1e-11 * max(1.0, np.abs(A).max() * dim), (b, mineig[b], ev)
+
+
+def test_trs_gep_hard_case():
+    rs = np.random.RandomState(7)
+    cases = []
+    for _ in range(6):
+        n = 9
+        Q, _ = np.linalg.qr(rs.randn(n, n))
+        lam = np.sort(rs.randn(n))
+        lam[0] = -3.0
+        A = Q @ np.diag(lam) @ Q.T
+        g = rs.randn(n)
+        g[0] = 0.0
+        cases.append((A, Q @ g, 5.0))
+    x, lam1, kind, _ = _solve(cases)
+    for b, (A, a, Del) in enumerate(cases):
+        xr, lr, kr = T.trs_gep(A, a, Del, 1e-8)
+        assert kr == "hardcase_1" and int(kind[b]) == 8
+        assert np.isclose(lam1[b], lr, rtol=1e-8)
+        assert np.isclose(np.linalg.norm(x[b]), Del, rtol=1e-12)
+        assert np.isclose(_obj(A, a, x[b]), _obj(A, a, xr), rtol=1e-10)
+
+
+def test_trs_gep_reference_signature():
+    from trs import TRSgep
+    A, a, Del = _cases(3, 1, [12])[0]
+    x, lam1, kind = TRSgep(A, a, np.eye(12), Del, 1e-8)
+    xr, lr, kr = T.trs_gep(A, a, Del, 1e-8)
+    assert kind == kr and np.allclose(x, xr, rtol=1e-8, atol=1e-12)
+    with pytest.raises(NotImplementedError):
+        TRSgep(A, a, 2 * np.eye(12), Del, 1e-8)
