@@ -148,6 +148,8 @@ typedef struct riptrm_options {
     int32_t trs_solver;               /* 'TRS_solver': RIPTRM_TRS_SOLVER_* */
     int32_t second_order_stationarity;/* 'second_order_stationarity' (bool; Exact_RepMat only) */
     double trs_tolhardcase;           /* 'TRS_tolhardcase' */
+    const double* tol2_table;         /* device, table_len doubles: forcing_function_second_order of the
+                                       * mu table (RIPTRM.py:884); NULL = mu itself (the default) */
 } riptrm_options;
 
 typedef struct riptrm_ctx riptrm_ctx;

@@ -6,7 +6,9 @@ module named ``RIPTRM`` from its solver path and calls ``RIPTRM(option).run(prob
 eqLagmult)`` whose ``log`` has the reference's columns, one row per inner iteration
 (``RIPTRM.py:812-818``).  Differences, all explicit errors rather than silent fallbacks:
 
-* only ``TRS_solver='tCG'`` (what every shipped config selects) — ``Exact_RepMat`` raises;
+* ``TRS_solver='tCG'`` (what every shipped config selects) at any size; ``'Exact_RepMat'`` (the
+  class default, with ``second_order_stationarity``) while ``manifold.dim <= 96`` — the matrix of
+  HwCur lives in LDS (csrc/riptrm_trs.h); larger problems raise;
 * the problem is a structured descriptor (``problems.NonnegPCAProblem`` or
   ``si.SIProblem`` for StableIdentification) instead of a list of autograd closures, because
   closures cannot execute on the GPU;

@@ -2057,6 +2057,8 @@ int riptrm_solve_begin(riptrm_ctx* ctx, const riptrm_options* opt, const double*
   if (!ctx->bound) return fail(ctx, RIPTRM_E_STATE, "solve_begin: bind first");
   if (!opt || opt->struct_size != (int32_t)sizeof(riptrm_options))
     return fail(ctx, RIPTRM_E_ARG, "solve_begin: riptrm_options.struct_size mismatch");
+  if (opt->trs_solver != RIPTRM_TRS_SOLVER_TCG)
+    return fail(ctx, RIPTRM_E_ARG, "solve_begin: Exact_RepMat is not implemented for NonnegPCA yet");
   if (!x0 || !y0 || ldv < ctx->P.n || !mu_table || !tolL_table || !tolC_table || table_len <= 0)
     return fail(ctx, RIPTRM_E_ARG, "solve_begin: bad argument");
   if (opt->log_capacity > ctx->L.cap) return fail(ctx, RIPTRM_E_ARG, "solve_begin: log_capacity exceeds bound capacity");

@@ -21,6 +21,7 @@
 #include <string>
 #include "riptrm_ctx.h"
 #include "riptrm_wave.h"
+#include "riptrm_trs.h"
 
 namespace riptrm_si {
 
@@ -109,7 +110,7 @@ __device__ __forceinline__ PV pv_scale(double s, PV a) { return PV{s * a.j, s * 
 __device__ __forceinline__ PV pv_neg(PV a) { return PV{-a.j, -a.r, -a.q}; }
 
 struct Info {  // inner-iteration record of solver_status (RIPTRM.py:986-1023)
-  double has, num, status, tr, dxtype, normdx, minx, miny, compl_, hasratio, ratio, ru, dc;
+  double has, num, status, tr, dxtype, normdx, minx, miny, compl_, hasratio, ratio, ru, dc, hasmin, mineig;
 };
 
 // ---- serial d x d linear algebra on ONE lane, register arrays, fully unrolled for D ---------
@@ -208,6 +209,39 @@ __device__ __forceinline__ bool pd_reg(double (&a)[D * D]) {
   return pd;
 }
 
+// lower Cholesky factor L of A (NaN entries if A is not PD) and L^-1 (Exact_RepMat tangent frame)
+template <int D>
+__device__ __forceinline__ void chol_inv_reg(const double (&A)[D * D], double (&Lm)[D * D], double (&Li)[D * D]) {
+#pragma unroll
+  for (int i = 0; i < D * D; ++i) { Lm[i] = 0.0; Li[i] = 0.0; }
+#pragma unroll
+  for (int j = 0; j < D; ++j) {
+    double s = A[j * D + j];
+#pragma unroll
+    for (int k = 0; k < j; ++k) s -= Lm[j * D + k] * Lm[j * D + k];
+    const double cjj = sqrt(s);
+    Lm[j * D + j] = cjj;
+#pragma unroll
+    for (int i = j + 1; i < D; ++i) {
+      double t = A[i * D + j];
+#pragma unroll
+      for (int k = 0; k < j; ++k) t -= Lm[i * D + k] * Lm[j * D + k];
+      Lm[i * D + j] = t / cjj;
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < D; ++j) {
+    Li[j * D + j] = 1.0 / Lm[j * D + j];
+#pragma unroll
+    for (int i = j + 1; i < D; ++i) {
+      double t = 0.0;
+#pragma unroll
+      for (int k = j; k < i; ++k) t -= Lm[i * D + k] * Li[k * D + j];
+      Li[i * D + j] = t / Lm[i * D + i];
+    }
+  }
+}
+
 // pymanopt SPD dist: ||logm(C^-1 B C^-T)||_F, C = cholesky(A); NaN if A is not PD
 template <int D>
 __device__ __forceinline__ double spd_dist_reg(const double (&A)[D * D], const double (&B)[D * D]) {
@@ -294,6 +328,7 @@ struct Eng {
   double* ser;     // LDS scratch for the per-lane serial solvers: 8 x 64 doubles
   int* cr_s;       // LDS constraint rows / cols / kinds
   int* cc_s;
+  double* tl;      // LDS work area of the Exact_RepMat subproblem (riptrm_trs.h), null for tCG
   // constraint of this lane (l < m)
   int ck, cr, cc;
   double cp0, cp1;
@@ -304,10 +339,10 @@ struct Eng {
   double pt[RIPTRM_SI_PROF_NFIELDS];   // section tick totals (riptrm_si_profile_*)
   __device__ __forceinline__ double tick() const { return P.prof ? (double)wall_clock64() : 0.0; }
 
-  __device__ __forceinline__ Eng(const SIParams& P_, int b_, double* sh_, double* ser_, int* crs, int* ccs)
+  __device__ __forceinline__ Eng(const SIParams& P_, int b_, double* sh_, double* ser_, int* crs, int* ccs, double* tl_)
       : P(P_), b(b_), l((int)threadIdx.x), m(P_.m), N(P_.N),
         li((int)threadIdx.x / D), lj((int)threadIdx.x % D), act((int)threadIdx.x < D * D),
-        cact((int)threadIdx.x < P_.m), sh(sh_), ser(ser_), cr_s(crs), cc_s(ccs) {
+        cact((int)threadIdx.x < P_.m), sh(sh_), ser(ser_), cr_s(crs), cc_s(ccs), tl(tl_) {
     Xd = P.X + (int64_t)b * P.data_stride;
     XPd = P.XP + (int64_t)b * P.data_stride;
     E = P.escr + (int64_t)b * d * N;
@@ -652,6 +687,109 @@ struct Eng {
     return stop;
   }
 
+  // ---- Exact_RepMat, RIPTRM.py:433-444 (+ the second-order test :599-617) ---------------------
+  // Tangent basis of T_x(Skew x SPD x SPD), orthonormal in the product metric (oracle/trs_oracle.py
+  // ::si_tangent_basis): skew pairs (E_ij - E_ji)/sqrt2 (i < j), then for R and Q the images
+  // L B_k L^T of the Frobenius-orthonormal symmetric basis (E_ii, (E_ij + E_ji)/sqrt2, i <= j) under
+  // the Cholesky factor L of the point: <L B L^T, L C L^T>_X = tr(B C).  The reference draws a random
+  // basis (utils.py:388-397); the subproblem's solution does not depend on the basis.
+  static constexpr int NS = D * (D - 1) / 2, NY = D * (D + 1) / 2, DIMM = NS + 2 * NY;
+  static constexpr double RS2 = 0.7071067811865475;   // 1 / np.sqrt(2)
+  __device__ __forceinline__ static int skew_idx(int i, int j) { return i * (2 * D - i - 1) / 2 + (j - i - 1); }
+  __device__ __forceinline__ static int sym_idx(int i, int j) { return i * D - i * (i - 1) / 2 + (j - i); }
+  struct Frame {
+    double Lr, Lq, Lri, Lqi;   // this lane's element of chol(R), chol(Q) and their inverses
+  };
+  __device__ __forceinline__ Frame frame(PV x) {
+    stage(0, x.r);
+    stage(1, x.q);
+    __syncthreads();
+    if (l < 2) {
+      double a[D * D], Lm[D * D], Li[D * D];
+      load_reg(l, a);
+      chol_inv_reg<D>(a, Lm, Li);
+#pragma unroll
+      for (int i = 0; i < D * D; ++i) {
+        ser[(2 + l) * W + i] = Lm[i];
+        ser[(4 + l) * W + i] = Li[i];
+      }
+    }
+    __syncthreads();
+    Frame F;
+    F.Lr = act ? ser[2 * W + l] : 0.0;
+    F.Lq = act ? ser[3 * W + l] : 0.0;
+    F.Lri = act ? ser[4 * W + l] : 0.0;
+    F.Lqi = act ? ser[5 * W + l] : 0.0;
+    __syncthreads();
+    return F;
+  }
+  // sum_k c_k b_k (c in LDS, DIMM entries)
+  __device__ __forceinline__ PV from_coords(const Frame& F, const double* c) {
+    double vj = 0.0, cr = 0.0, cq = 0.0;
+    if (act) {
+      if (li < lj) vj = c[skew_idx(li, lj)] * RS2;
+      else if (li > lj) vj = -(c[skew_idx(lj, li)] * RS2);
+      const int i0 = li < lj ? li : lj, j0 = li < lj ? lj : li;
+      const double f = li == lj ? 1.0 : RS2;
+      cr = c[NS + sym_idx(i0, j0)] * f;
+      cq = c[NS + NY + sym_idx(i0, j0)] * f;
+    }
+    const double r = mm(mm(F.Lr, cr), F.Lr, false, true);
+    const double q = mm(mm(F.Lq, cq), F.Lq, false, true);
+    return PV{vj, r, q};
+  }
+  // out_k = <b_k, w>_x  (SPD part: <B_k, L^-1 W L^-T>_F)
+  __device__ __forceinline__ void to_coords(const Frame& F, PV w, double* out) {
+    const double jt = tr(w.j);
+    const double wr = mm(mm(F.Lri, w.r), F.Lri, false, true);
+    const double wq = mm(mm(F.Lqi, w.q), F.Lqi, false, true);
+    const double wrt = tr(wr), wqt = tr(wq);
+    if (act && li < lj) out[skew_idx(li, lj)] = (w.j - jt) * RS2;
+    if (act && li <= lj) {
+      out[NS + sym_idx(li, lj)] = li == lj ? wr : (wr + wrt) * RS2;
+      out[NS + NY + sym_idx(li, lj)] = li == lj ? wq : (wq + wqt) * RS2;
+    }
+    __syncthreads();
+  }
+  // selfadj_operator2matrix (utils.py:565-573): A[i][j] = <b_i, Hw(b_j)> for i <= j, mirrored;
+  // and the coordinates of cxCur (RIPTRM.py:438-440)
+  __device__ __forceinline__ riptrm_trs::Work repmat(const AtX& a, const Frame& F, double& hvps) {
+    riptrm_trs::Work w = riptrm_trs::make_work(tl, DIMM);
+    for (int j = 0; j < DIMM; ++j) {
+      for (int k = l; k < DIMM; k += W) w.p[k] = (k == j) ? 1.0 : 0.0;
+      __syncthreads();
+      const PV bj = from_coords(F, w.p);
+      const PV h = hw(a, bj);
+      hvps += 1.0;
+      to_coords(F, h, w.q);
+      for (int k = l; k <= j; k += W) {
+        w.A[k * w.lda + j] = w.q[k];
+        w.A[j * w.lda + k] = w.q[k];
+      }
+      __syncthreads();
+    }
+    to_coords(F, a.c, w.a);
+    return w;
+  }
+  // compute_direction's Exact_RepMat branch: returns the RIPTRM_TRS_* type
+  __device__ __forceinline__ int trs_direction(const AtX& a, double Delta, PV& eta, double& hvps) {
+    const Frame F = frame(a.x);
+    riptrm_trs::Work w = repmat(a, F, hvps);
+    riptrm_trs::Blk<W> B(nullptr);
+    const riptrm_trs::Result r = riptrm_trs::trs_solve<W>(B, w, Delta, P.opt.trs_tolhardcase);
+    eta = from_coords(F, w.x);
+    return RIPTRM_TRS_BOUNDARY + r.kind;
+  }
+  // smallest eigenvalue of HwNew's matrix at (xN, yN, mu) (RIPTRM.py:599-613)
+  __device__ __forceinline__ double mineig_at(PV xN, double yN, double mu, double& hvps) {
+    AtX aN;
+    prepare(aN, xN, yN, mu);
+    const Frame F = frame(xN);
+    riptrm_trs::Work w = repmat(aN, F, hvps);
+    riptrm_trs::Blk<W> B(nullptr);
+    return riptrm_trs::min_eig<W>(B, w);
+  }
+
   // ---- evaluation, src/solver/utils.py:342-368 (+ compute_residual :269-340) ----------------
   // ev: cost, distance, residual, gradnorm, complvio, dualvio, manvio, maxvio, meanvio, maxabsy
   __device__ __forceinline__ void evaluation(PV xprev, PV x, double y, double (&ev)[10]) {
@@ -731,6 +869,8 @@ struct Eng {
           L[RIPTRM_LOG_ARED_PRED] = inf->ratio;
           L[RIPTRM_LOG_RADIUS_UPDATE] = inf->ru;
           L[RIPTRM_LOG_DUAL_CLIPPING] = inf->dc;
+          L[RIPTRM_LOG_HAS_MINEIG] = inf->hasmin;
+          L[RIPTRM_LOG_MINEIGVALHW] = inf->mineig;
         }
       } else {
         overflow += 1.0;
@@ -821,7 +961,9 @@ struct Eng {
         tq = tick();
         PV eta, Heta;
         int jj = 0;
-        const int tstop = tcg(a, Delta, eta, Heta, jj, hvps);
+        const bool exact = P.opt.trs_solver == RIPTRM_TRS_SOLVER_EXACT_REPMAT;
+        const int tstop = exact ? trs_direction(a, Delta, eta, hvps) : tcg(a, Delta, eta, Heta, jj, hvps);
+        if (exact) jj = -1;   // no tCG iterations
         pt[RIPTRM_SI_PROF_TCG] += tick() - tq;
         tq = tick();
         tcg_total += (double)jj + 1.0;
@@ -842,13 +984,22 @@ struct Eng {
         const bool yfeas = wmin(cact ? (yN > 0.0 ? 1.0 : 0.0) : 1.0) > 0.0;
         const double cvv = cact ? yN * sN - mu : 0.0;
         const double compl_ = sqrt(wsum(cvv * cvv));
-        info = Info{1.0, inner_it, 0.0, DeltaStep, (double)tstop, normdx, minx, miny, compl_, 0.0, 0.0, 0.0, -1.0};
+        info = Info{1.0, inner_it, 0.0, DeltaStep, (double)tstop, normdx, minx, miny, compl_, 0.0, 0.0, 0.0, -1.0,
+                    0.0, 0.0};
         have_info = true;
+        bool mineig_ok = true;
+        if (exact && P.opt.second_order_stationarity) {   // RIPTRM.py:599-613
+          const double me = mineig_at(xN, yN, mu, hvps);
+          const double tol2 = P.opt.tol2_table ? P.opt.tol2_table[ti] : mu;
+          mineig_ok = me >= -tol2;
+          info.hasmin = 1.0;
+          info.mineig = me;
+        }
         bool converged = false;
         double fN = 0.0, AN2 = 0.0;
         if (xfeas) {
           const double normgl = gradlag_norm(xN, yN, fN, AN2);
-          converged = yfeas && normgl <= tolL && compl_ <= tolC;
+          converged = yfeas && normgl <= tolL && compl_ <= tolC && mineig_ok;
         }
         if (converged) {  // RIPTRM.py:762-766
           x = xN;
@@ -1005,9 +1156,10 @@ __global__ void __launch_bounds__(W) k_si(SIParams P) {
   __shared__ double sh[2 * W];
   __shared__ double ser[8 * W];
   __shared__ int crs[MMAX], ccs[MMAX];
+  extern __shared__ double trs_lds[];   // Exact_RepMat only (dynamic size 0 otherwise)
   const int b = blockIdx.x;
   if (b >= P.batch) return;
-  Eng<D> e(P, b, sh, ser, crs, ccs);
+  Eng<D> e(P, b, sh, ser, crs, ccs, trs_lds);
   if (P.mode == MODE_SOLVE) e.solve();
   else if (P.mode == MODE_HVP) e.op_hvp();
   else e.op_tcg();
@@ -1067,20 +1219,29 @@ static SIParams si_params(riptrm_ctx* c, int mode) {
   return P;
 }
 
-static int si_launch(riptrm_ctx* c, const SIParams& P) {
-  const dim3 g((unsigned)P.batch), t(W);
-  switch (P.d) {  // the block size is a template parameter: unrolled products, register solvers
-    case 1: hipLaunchKernelGGL(k_si<1>, g, t, 0, c->stream, P); break;
-    case 2: hipLaunchKernelGGL(k_si<2>, g, t, 0, c->stream, P); break;
-    case 3: hipLaunchKernelGGL(k_si<3>, g, t, 0, c->stream, P); break;
-    case 4: hipLaunchKernelGGL(k_si<4>, g, t, 0, c->stream, P); break;
-    case 5: hipLaunchKernelGGL(k_si<5>, g, t, 0, c->stream, P); break;
-    case 6: hipLaunchKernelGGL(k_si<6>, g, t, 0, c->stream, P); break;
-    case 7: hipLaunchKernelGGL(k_si<7>, g, t, 0, c->stream, P); break;
-    default: hipLaunchKernelGGL(k_si<8>, g, t, 0, c->stream, P); break;
-  }
+static int si_manifold_dim(int d) { return d * (d - 1) / 2 + d * (d + 1); }
+
+template <int D>
+static int si_launch_d(riptrm_ctx* c, const SIParams& P) {
+  const bool exact = P.mode == MODE_SOLVE && P.opt.trs_solver == RIPTRM_TRS_SOLVER_EXACT_REPMAT;
+  const size_t shm = exact ? (size_t)riptrm_trs::work_doubles(si_manifold_dim(D)) * sizeof(double) : 0;
+  if (shm) HIPCHK(c, hipFuncSetAttribute((const void*)k_si<D>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm));
+  hipLaunchKernelGGL(k_si<D>, dim3((unsigned)P.batch), dim3(W), shm, c->stream, P);
   HIPCHK(c, hipGetLastError());
   return RIPTRM_OK;
+}
+
+static int si_launch(riptrm_ctx* c, const SIParams& P) {
+  switch (P.d) {  // the block size is a template parameter: unrolled products, register solvers
+    case 1: return si_launch_d<1>(c, P);
+    case 2: return si_launch_d<2>(c, P);
+    case 3: return si_launch_d<3>(c, P);
+    case 4: return si_launch_d<4>(c, P);
+    case 5: return si_launch_d<5>(c, P);
+    case 6: return si_launch_d<6>(c, P);
+    case 7: return si_launch_d<7>(c, P);
+    default: return si_launch_d<8>(c, P);
+  }
 }
 
 extern "C" {
@@ -1176,6 +1337,10 @@ int riptrm_si_solve(riptrm_ctx* ctx, const riptrm_options* opt, const double* x0
   if (!x0 || !y0 || !mu_table || !tolL_table || !tolC_table || table_len <= 0)
     return fail(ctx, RIPTRM_E_ARG, "si_solve: bad argument");
   if (opt->log_capacity > ctx->si->cap) return fail(ctx, RIPTRM_E_ARG, "si_solve: log_capacity exceeds bound capacity");
+  if (opt->trs_solver != RIPTRM_TRS_SOLVER_TCG && opt->trs_solver != RIPTRM_TRS_SOLVER_EXACT_REPMAT)
+    return fail(ctx, RIPTRM_E_ARG, "si_solve: unknown trs_solver");
+  if (opt->trs_solver == RIPTRM_TRS_SOLVER_EXACT_REPMAT && si_manifold_dim(ctx->si->prob.d) > RIPTRM_TRS_DIM_MAX)
+    return fail(ctx, RIPTRM_E_ARG, "si_solve: Exact_RepMat needs manifold.dim <= RIPTRM_TRS_DIM_MAX (d <= 7)");
   HIPCHK(ctx, hipSetDevice(ctx->device));
   SIParams P = si_params(ctx, MODE_SOLVE);
   P.opt = *opt;

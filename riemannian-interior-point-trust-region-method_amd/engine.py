@@ -31,6 +31,8 @@ C = N.CONST
 NLOG = C["RIPTRM_LOG_NFIELDS"]
 NSTAT = C["RIPTRM_STAT_NFIELDS"]
 
+TRS_NAMES = {C["RIPTRM_TRS_BOUNDARY"]: "boundary", C["RIPTRM_TRS_INTERIOR"]: "interior",
+             C["RIPTRM_TRS_HARDCASE_1"]: "hardcase_1"}
 TCG_NAMES = {C["RIPTRM_TCG_MAX_INNER_ITER"]: "MAX_INNER_ITER",
              C["RIPTRM_TCG_NEGATIVE_CURVATURE"]: "NEGATIVE_CURVATURE",
              C["RIPTRM_TCG_EXCEEDED_TR"]: "EXCEEDED_TR",
@@ -40,6 +42,11 @@ TCG_NAMES = {C["RIPTRM_TCG_MAX_INNER_ITER"]: "MAX_INNER_ITER",
 STATUS_NAMES = {0: None, 1: "initial", 2: "converged", 3: "primal_infeasible", 4: "successful",
                 5: "unsuccessful", 6: "max-time-exceeded", 7: "max-iter-exceeded"}
 RU_NAMES = {0: None, 1: "reduced", 2: "expanded", 3: "unchanged"}
+
+def dxtype_name(code: int) -> str:
+    """inner_info['dxtype'] (RIPTRM.py:734): TRSgep's type or f"tCG_{stop_tCG}"."""
+    return TRS_NAMES[code] if code in TRS_NAMES else f"tCG_{TCG_NAMES[code]}"
+
 
 # RIPTRM default_option (src/solver/RIPTRM.py:305-358)
 REFERENCE_DEFAULTS: Dict[str, Any] = {
@@ -110,16 +117,33 @@ class ResolvedOptions:
     mu_tab: List[float]
     tolL_tab: List[float]
     tolC_tab: List[float]
+    tol2_tab: List[float]
+
+    @property
+    def exact(self) -> bool:
+        return self.c_opt.trs_solver == C["RIPTRM_TRS_SOLVER_EXACT_REPMAT"]
+
+    def device_tables(self, device) -> List[torch.Tensor]:
+        """(mu, tolL, tolC[, tol2]) tables on the device; tol2's pointer goes into c_opt.  The
+        caller keeps the tensors alive while the solve runs."""
+        tabs = [torch.tensor(t, dtype=torch.float64, device=device) for t in (self.mu_tab, self.tolL_tab, self.tolC_tab)]
+        if self.exact and self.c_opt.second_order_stationarity:
+            t2 = torch.tensor(self.tol2_tab, dtype=torch.float64, device=device)
+            tabs.append(t2)
+            self.c_opt.tol2_table = t2.data_ptr()
+        else:
+            self.c_opt.tol2_table = None
+        return tabs
 
 
 def resolve_options(option: Dict[str, Any], typical_dist: float, log_capacity: int,
                     restart_every: int = 0, manvio_classifier=None) -> ResolvedOptions:
     o = dict(REFERENCE_DEFAULTS)
     o.update(option or {})
-    if o['TRS_solver'] != 'tCG':
-        raise NotImplementedError(
-            f"TRS_solver={o['TRS_solver']!r}: the MI355X path implements the tCG subproblem solver "
-            "(every shipped config selects TRS_solver='tCG', src/NonnegPCA/config_simulation.yaml:21)")
+    if o['TRS_solver'] not in ('tCG', 'Exact_RepMat'):
+        raise ValueError(f"TRS_solver {o['TRS_solver']} is not supported.")   # RIPTRM.py:453-454
+    if o.get('checkTRSoptimality'):
+        raise NotImplementedError("checkTRSoptimality (a diagnostic print, RIPTRM.py:367-391) is not on the device path")
     if o.get('use_rand'):
         raise NotImplementedError("use_rand tCG start is not on the reference's path (RIPTRM.py:450)")
     if o.get('callbackfun') is not None:
@@ -130,6 +154,9 @@ def resolve_options(option: Dict[str, Any], typical_dist: float, log_capacity: i
     tab = mu_schedule(o, maxlen=max(2, maxiter + 2))
     tolL = [float(o['forcing_function_Lagrangian'](m)) for m in tab]
     tolC = [float(o['forcing_function_complementarity'](m)) for m in tab]
+    exact = o['TRS_solver'] == 'Exact_RepMat'
+    sos = bool(exact and o['second_order_stationarity'])
+    tol2 = [float(o['forcing_function_second_order'](m)) for m in tab] if sos else []
     c = N.RiptrmOptions()
     c.struct_size = ctypes.sizeof(N.RiptrmOptions)
     c.maxiter = min(maxiter, 2 ** 31 - 2)
@@ -152,7 +179,10 @@ def resolve_options(option: Dict[str, Any], typical_dist: float, log_capacity: i
     c.tcg_kappa = float(o['tCG_kappa'])
     c.const_left = float(o['const_left'])
     c.const_right = float(o['const_right'])
-    return ResolvedOptions(o, c, tab, tolL, tolC)
+    c.trs_solver = C["RIPTRM_TRS_SOLVER_EXACT_REPMAT"] if exact else C["RIPTRM_TRS_SOLVER_TCG"]
+    c.second_order_stationarity = 1 if sos else 0
+    c.trs_tolhardcase = float(o['TRS_tolhardcase'])
+    return ResolvedOptions(o, c, tab, tolL, tolC, tol2)
 
 
 def _stream_handle(device: torch.device) -> int:
@@ -394,8 +424,11 @@ class NonnegPCABatch:
     def begin(self, x0, y0, option: Dict[str, Any], restart_every: int = 0) -> ResolvedOptions:
         assert self.bound
         ro = resolve_options(option, math.pi, self.cap, restart_every)
+        if ro.exact and self.n - 1 > C["RIPTRM_TRS_DIM_MAX"]:
+            raise NotImplementedError(f"TRS_solver='Exact_RepMat' on the GPU needs manifold.dim = n - 1 <= "
+                                      f"{C['RIPTRM_TRS_DIM_MAX']} (got n = {self.n}); use TRS_solver='tCG'")
         X, Y = self._padded(x0), self._padded(y0)
-        tabs = [torch.tensor(t, dtype=torch.float64, device=self.device) for t in (ro.mu_tab, ro.tolL_tab, ro.tolC_tab)]
+        tabs = ro.device_tables(self.device)
         self._keep = [X, Y] + tabs
         self._sync_stream()
         self.ctx.check(self.lib.riptrm_solve_begin(self.ctx.h, ctypes.byref(ro.c_opt), ctypes.c_void_p(X.data_ptr()),
@@ -497,12 +530,12 @@ class BatchResult:
             cols["inner_status"].append(STATUS_NAMES[int(r[F("INNER_STATUS")])] if has else None)
             cols["TR_radius"].append(np.float64(r[F("TR_RADIUS")]) if has else None)
             if save_inner:
-                cols["dxtype"].append(f"tCG_{TCG_NAMES[int(r[F('DXTYPE')])]}" if has else None)
+                cols["dxtype"].append(dxtype_name(int(r[F('DXTYPE')])) if has else None)
                 cols["normdx"].append(np.float64(r[F("NORMDX")]) if has else None)
                 cols["minxfeasi"].append(np.float64(r[F("MINXFEASI")]) if has else None)
                 cols["minyfeasi"].append(np.float64(r[F("MINYFEASI")]) if has else None)
                 cols["compl"].append(np.float64(r[F("COMPL")]) if has else None)
-                cols["mineigvalHw"].append(None)
+                cols["mineigvalHw"].append(np.float64(r[F("MINEIGVALHW")]) if has and r[F("HAS_MINEIG")] != 0 else None)
                 hr = has and r[F("HAS_RATIO")] != 0
                 cols["ared/pred"].append(np.float64(r[F("ARED_PRED")]) if hr else None)
                 cols["radius_update"].append(RU_NAMES[int(r[F("RADIUS_UPDATE")])] if hr else None)

@@ -35,6 +35,7 @@ class RiptrmOptions(ctypes.Structure):
         ("gamma", c_double), ("tcg_theta", c_double), ("tcg_kappa", c_double),
         ("const_left", c_double), ("const_right", c_double),
         ("trs_solver", c_int32), ("second_order_stationarity", c_int32), ("trs_tolhardcase", c_double),
+        ("tol2_table", c_void_p),
     ]
 
 

@@ -266,7 +266,10 @@ class SIBatch:
         ro = resolve_options(option, typical, self.cap, restart_every, manvio_classifier=si_manvio_kind)
         X = self._dev(x0, (self.batch, 3, d, d))
         Y = self._dev(y0, (self.batch, self.m))
-        tabs = [torch.tensor(t, dtype=torch.float64, device=self.device) for t in (ro.mu_tab, ro.tolL_tab, ro.tolC_tab)]
+        if ro.exact and d * (d - 1) // 2 + d * (d + 1) > C["RIPTRM_TRS_DIM_MAX"]:
+            raise NotImplementedError(f"TRS_solver='Exact_RepMat' on the GPU needs manifold.dim <= "
+                                      f"{C['RIPTRM_TRS_DIM_MAX']} (d <= 7)")
+        tabs = ro.device_tables(self.device)
         self._keep = [X, Y] + tabs
         self.ctx.set_stream(_stream_handle(self.device))
         self.ctx.check(self.lib.riptrm_si_solve(self.ctx.h, ctypes.byref(ro.c_opt), ctypes.c_void_p(X.data_ptr()),

@@ -28,9 +28,9 @@ class BranchFlip(AssertionError):
 BRANCH_KEYS = ("iteration", "num_inner", "inner_status", "dxtype", "radius_update", "dual_clipping")
 VALUE_KEYS = ("residual", "cost", "gradnorm", "complviolation", "dualviolation", "manviolation",
               "maxviolation", "meanviolation", "mu", "normdx", "TR_radius", "minxfeasi", "minyfeasi",
-              "compl", "ared/pred", "maxabsLagmult")
+              "compl", "ared/pred", "maxabsLagmult", "mineigvalHw")
 # properties of the tCG step / trial point rather than of the iterate: trial bounds on every row
-STEP_KEYS = ("normdx", "minxfeasi", "minyfeasi", "compl", "ared/pred")
+STEP_KEYS = ("normdx", "minxfeasi", "minyfeasi", "compl", "ared/pred", "mineigvalHw")
 
 
 def _col(log, k):

@@ -195,3 +195,42 @@ def test_si_deterministic(data):
     a = _batch(data, 4).solve(xs, ys, _gpu_opt(maxiter=5))
     b = _batch(data, 4).solve(xs[::-1].copy(), ys[::-1].copy(), _gpu_opt(maxiter=5))
     np.testing.assert_array_equal(a.x.cpu().numpy(), b.x.cpu().numpy()[::-1])
+
+
+@pytest.mark.parametrize("sos", [True, False])
+def test_si_exact_repmat_matches_oracle(data, sos):
+    """TRS_solver = 'Exact_RepMat' (RIPTRM.py:433-444): the matrix of HwCur in a tangent basis (40 HVPs
+    in-kernel), TRSgep on the device (csrc/riptrm_trs.h), and with second_order_stationarity the
+    smallest eigenvalue of HwNew's matrix at every trial point (RIPTRM.py:599-617) against the oracle
+    (trs_oracle: the reference's 2n x 2n pencil).  Same bar as the tCG trajectories."""
+    from parity import compare_until_flip
+    xs, ys = _starts("abc")
+    K = 4
+    opt = dict(TRS_solver="Exact_RepMat", second_order_stationarity=sos, maxiter=K)
+    res = _batch(data, 3).solve(xs, ys, _gpu_opt(**opt))
+    for b in range(3):
+        ref = SI.solve(data, xs[b], ys[b], _oracle_opt(**opt))
+        gl = res.log(b)
+        kinds = [k for k in gl["dxtype"] if k is not None]
+        assert kinds and all(k in ("boundary", "interior", "hardcase_1") for k in kinds), kinds
+        mins = [v for v in gl["mineigvalHw"] if v is not None]
+        assert (len(mins) > 0) == sos
+        compare_until_flip(gl, ref.log)
+
+
+def test_si_reference_default_options_use_exact_repmat(tmp_path):
+    """RIPTRM's class defaults (RIPTRM.py:325-326): Exact_RepMat with the second-order test."""
+    from si import SICoordinator
+    from RIPTRM import RIPTRM
+    import shutil
+    d = tmp_path / "dataset" / "StableIdentification" / "1"
+    d.mkdir(parents=True)
+    for f in os.listdir(DS):
+        shutil.copy(os.path.join(DS, f), d / f)
+    cfg = {"problem_name": "StableIdentification", "problem_instance": 1, "problem_initialpoint": "a",
+           "is_X_noisy": True, "Xset": [1, 2, 3, 4, 5], "h": 0.02}
+    prob = SICoordinator(cfg, root=str(tmp_path)).run()
+    import si
+    out = RIPTRM({"maxiter": 2, "tolresid": 0.0, "maxtime": 1e9, "manviofun": si.si_manviofun}).run(prob)
+    assert out.name == "RIPTRM_Exact_RepMat"
+    assert any(v is not None for v in out.log["mineigvalHw"])
