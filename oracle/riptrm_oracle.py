@@ -104,6 +104,30 @@ class Sphere:
 # ---------------------------------------------------------------------------------------------
 # Problem back-ends
 # ---------------------------------------------------------------------------------------------
+def sphere_tangent_basis(x, rs=None):
+    """Orthonormal basis of T_x Sphere(n) for Exact_RepMat (RIPTRM.py:436 basisfun).
+    rs=None: the columns 1..n-1 of the Householder reflector H = I - tau w w^T, w = x + sign(x_0)
+    ||x|| e_0 (what the device uses).  rs = RandomState: the reference's tangentorthobasis
+    (utils.py:388-397) — random tangent vectors, Gram-Schmidt in the manifold metric (utils.py:
+    375-386).  The subproblem's solution does not depend on the choice."""
+    x = np.asarray(x, dtype=np.float64)
+    n = len(x)
+    if rs is None:
+        w = x.copy()
+        w[0] += (1.0 if x[0] >= 0 else -1.0) * np.sqrt(x @ x)
+        tau = 2.0 / (w @ w)
+        return [np.eye(n)[k] - tau * w * w[k] for k in range(1, n)]
+    Q = []
+    for _ in range(n - 1):
+        v = rs.randn(n)
+        v = v - (x @ v) * x
+        v = v / np.linalg.norm(v)
+        for q in Q:
+            v = v - (q @ v) * q
+        Q.append(v / np.linalg.norm(v))
+    return Q
+
+
 class NonnegPCAStructured:
     """Per-constraint restatement of NonnegPCA + NonlinearProblem + RIPTRM's G/H helpers.
 
@@ -155,6 +179,9 @@ class NonnegPCAStructured:
         self.ineq_rhess = [c[4] for c in cons]
 
     # RIPTRM.py:721 costineqconstvecfun
+    def tangent_basis(self, x):
+        return sphere_tangent_basis(x)
+
     def slack(self, x):
         return np.array([-g(x) for g in self.ineq])
 
@@ -270,6 +297,9 @@ class NonnegPCAVectorized:
 
     def cost(self, x):
         return -0.5 * (x @ self.Sx(x))
+
+    def tangent_basis(self, x):
+        return sphere_tangent_basis(x)
 
     def slack(self, x):
         return x.copy()

@@ -46,13 +46,15 @@ enum St : int {
   ST_EPE, ST_EPD, ST_DPD, ST_ZR, ST_NORMR0, ST_MODEL, ST_J, ST_TCG_STOP,
   // trial
   ST_NORMDX, ST_XDX, ST_MINX, ST_MINY, ST_COMPL, ST_XFEAS, ST_YFEAS,
+  // Exact_RepMat second-order test at the trial point (RIPTRM.py:599-613)
+  ST_HASMIN, ST_MINEIG, ST_MINEIG_OK,
   ST_HOT_END,
   // cold: thread-0-owned counters
   ST_TCG_TOTAL = 40, ST_INNER_TOTAL, ST_PASSES, ST_LOG_COUNT, ST_LOG_OVERFLOW, ST_STOP_CODE,
   ST_STOP_RUNTIME, ST_RESIDUAL,
   // last inner_info (for save_inner_iteration == False rows)
   ST_I_HAS, ST_I_NUM, ST_I_STATUS, ST_I_TR, ST_I_DXTYPE, ST_I_NORMDX, ST_I_MINX, ST_I_MINY,
-  ST_I_COMPL, ST_I_HASRATIO, ST_I_RATIO, ST_I_RU, ST_I_DC,
+  ST_I_COMPL, ST_I_HASRATIO, ST_I_RATIO, ST_I_RU, ST_I_DC, ST_I_HASMIN, ST_I_MINEIG,
   ST_ERROR,
   ST_N_USED
 };

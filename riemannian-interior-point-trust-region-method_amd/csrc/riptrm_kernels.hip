@@ -18,6 +18,7 @@
 #include "riptrm_device.h"
 #include "riptrm_ctx.h"
 #include "riptrm_wave.h"
+#include "riptrm_trs.h"
 
 namespace riptrm {
 
@@ -516,7 +517,11 @@ __global__ void __launch_bounds__(256) k_pack(const double* Z, int64_t ldz, int6
 // ------------------------------------------------------------------------------------------
 enum Act : int { ACT_YIELD = 0, ACT_DONE = 1, ACT_PAUSE = 2 };
 
-struct Machine {
+// EXACT = false: the tCG machine (every shipped config); EXACT = true adds the Exact_RepMat
+// branches (a separate k_state instantiation, so the tCG kernel carries none of its code or
+// register / scratch pressure).
+template <bool EXACT>
+struct MachineT {
   const DevParams P;
   const int b;
   const int tid;
@@ -525,9 +530,10 @@ struct Machine {
   Red R;
   double s[ST_HOT];   // hot scalars: identical in every thread, drive uniform control flow
   double* cold;       // cold scalars (ST_HOT..ST_N): read and written by thread 0 only
+  double* tl;         // LDS of the Exact_RepMat subproblem (dynamic; Exact_RepMat solves only)
 
-  __device__ __forceinline__ Machine(const DevParams& P_, int b_, int out_list_, double* redbuf)
-      : P(P_), b(b_), tid(threadIdx.x), n(P_.n), out_list(out_list_) {
+  __device__ __forceinline__ MachineT(const DevParams& P_, int b_, int out_list_, double* redbuf, double* tl_ = nullptr)
+      : P(P_), b(b_), tid(threadIdx.x), n(P_.n), out_list(out_list_), tl(tl_) {
     R.buf = redbuf;
     R.parity = 0;
     const double* g = P.st + (int64_t)b * ST_N;
@@ -775,6 +781,8 @@ struct Machine {
         L[RIPTRM_LOG_ARED_PRED] = c[ST_I_RATIO];
         L[RIPTRM_LOG_RADIUS_UPDATE] = c[ST_I_RU];
         L[RIPTRM_LOG_DUAL_CLIPPING] = c[ST_I_DC];
+        L[RIPTRM_LOG_HAS_MINEIG] = c[ST_I_HASMIN];
+        L[RIPTRM_LOG_MINEIGVALHW] = c[ST_I_MINEIG];
         L[RIPTRM_LOG_MAXABSLAGMULT] = ev[9];
         L[RIPTRM_LOG_TCG_ITERS] = s[ST_J] + 1.0;
       } else {
@@ -897,6 +905,12 @@ struct Machine {
     s[ST_EPD] = 0.0;
     s[ST_MODEL] = 0.0;
     s[ST_J] = 0.0;
+    s[ST_HASMIN] = 0.0;
+    s[ST_MINEIG] = 0.0;
+    s[ST_MINEIG_OK] = 1.0;
+    if constexpr (EXACT) {
+      if (P.opt.trs_solver == RIPTRM_TRS_SOLVER_EXACT_REPMAT && (int)s[ST_MODE] == MODE_SOLVE) return trs_direction();
+    }
     if (n - 1 <= 0) {  // maxinner = manifold.dim = 0: no tCG iteration is possible
       cset(ST_ERROR, 1.0);
       s[ST_PHASE] = PH_ERROR;
@@ -1207,6 +1221,119 @@ struct Machine {
     return request(1);
   }
 
+  // ---- Exact_RepMat (RIPTRM.py:433-444, :599-617), n - 1 <= RIPTRM_TRS_DIM_MAX ---------------
+  // Tangent basis of x^perp: b_k = H e_k (k = 1..n-1) with the Householder reflector
+  // H = I - tau w w^T, w = x + sign(x_0) ||x|| e_0 (H x = -sign(x_0) ||x|| e_0, so the b_k are
+  // orthonormal and orthogonal to x).  For tangent b_i, b_j the closed form of HwCur
+  //  gives <b_i, Hw b_j> = b_i^T (-S + diag(y/x)) b_j + coef delta_ij, so the
+  // represented matrix (selfadj_operator2matrix, utils.py:565-573) is the trailing block of
+  // H M H = M - tau (w u^T + u w^T) + tau^2 (w^T u) w w^T, u = M w, M = -S + diag(y/x): O(n^2)
+  // instead of n HVPs.  The reference's basis is random (utils.py:388-397); the subproblem's
+  // solution and the eigenvalues do not depend on it.
+  __device__ __forceinline__ double s_at(int i, int j) const {
+    const double* Sb = P.S + (int64_t)b * P.inst_stride;
+    if (P.layout == RIPTRM_LAYOUT_SYMTILE) {
+      int I = i / TS, J = j / TS;
+      if (I > J) {
+        const int t = i; i = j; j = t;
+        const int u = I; I = J; J = u;
+      }
+      const int colsT = (J == P.nt - 1) ? P.wl : TS;
+      return Sb[sym_off(I, J, P.nt, P.wl) + (int64_t)(i - I * TS) * colsT + (j - J * TS)];
+    }
+    return Sb[(int64_t)i * P.ld + j];
+  }
+  // LDS: [Work of dim n-1][w: n][u: n][Blk scratch]
+  __device__ __forceinline__ double* trs_wvec() const { return tl + riptrm_trs::work_doubles(n - 1); }
+  __device__ __forceinline__ double* trs_uvec() const { return trs_wvec() + riptrm_trs::DIM_MAX + 1; }
+  __device__ __forceinline__ double* trs_red() const { return trs_uvec() + riptrm_trs::DIM_MAX + 1; }
+
+  // A <- (H M H)[1:, 1:] + coef I at (X, Y); returns tau (w in trs_wvec)
+  __device__ __noinline__ double repmat(riptrm_trs::Blk<ST_THREADS>& B, riptrm_trs::Work& w, const double* X,
+                                           const double* Y, double xx, double coef) {
+    double* Wv = trs_wvec();
+    double* Uv = trs_uvec();
+    const double sg = X[0] >= 0.0 ? 1.0 : -1.0;
+    double ww = 0.0;
+    for (int i = tid; i < n; i += ST_THREADS) {
+      const double wi = i == 0 ? X[0] + sg * sqrt(xx) : X[i];
+      Wv[i] = wi;
+      ww += wi * wi;
+    }
+    ww = B.sum(ww);
+    const double tau = 2.0 / ww;
+    __syncthreads();
+    double wu = 0.0;
+    for (int i = tid; i < n; i += ST_THREADS) {
+      double acc = 0.0;
+      for (int j = 0; j < n; ++j) acc += s_at(i, j) * Wv[j];
+      const double ui = -acc + (Y[i] / X[i]) * Wv[i];
+      Uv[i] = ui;
+      wu += Wv[i] * ui;
+    }
+    const double gam = B.sum(wu);
+    __syncthreads();
+    const int m = n - 1;
+    const double t2g = (tau * tau) * gam;
+    for (int e = tid; e < m * m; e += ST_THREADS) {
+      const int i = e / m + 1, j = e - (i - 1) * m + 1;
+      double mij = -s_at(i, j);
+      if (i == j) mij += Y[i] / X[i];
+      double v = (mij - tau * (Wv[i] * Uv[j] + Uv[i] * Wv[j])) + t2g * (Wv[i] * Wv[j]);
+      if (i == j) v += coef;
+      w.A[(i - 1) * w.lda + (j - 1)] = v;
+    }
+    __syncthreads();
+    return tau;
+  }
+
+  // compute_direction's Exact_RepMat branch: eta <- argmin of the model over the ball, then the
+  // rest of the inner step as after tCG
+  __device__ __noinline__ int trs_direction() {
+    riptrm_trs::Blk<ST_THREADS> B(trs_red());
+    riptrm_trs::Work w = riptrm_trs::make_work(tl, n - 1);
+    const double* X = V(V_X);
+    const double* Y = V(V_Y);
+    const double* Cv = V(V_C);
+    const double tau = repmat(B, w, X, Y, s[ST_XX], s[ST_COEF]);
+    const double* Wv = trs_wvec();
+    double wc = 0.0;   // cxCurvector_k = <c, b_k> = (H c)_k (RIPTRM.py:438-440)
+    for (int i = tid; i < n; i += ST_THREADS) wc += Wv[i] * Cv[i];
+    wc = B.sum(wc);
+    for (int k = tid + 1; k < n; k += ST_THREADS) w.a[k - 1] = Cv[k] - tau * Wv[k] * wc;
+    __syncthreads();
+    const riptrm_trs::Result r = riptrm_trs::trs_solve<ST_THREADS>(B, w, s[ST_DELTA], P.opt.trs_tolhardcase);
+    double wz = 0.0;   // dx = sum_k coeff_k b_k = H [0; coeff] (RIPTRM.py:442-444)
+    for (int k = tid + 1; k < n; k += ST_THREADS) wz += Wv[k] * w.x[k - 1];
+    wz = B.sum(wz);
+    double* E = V(V_ETA);
+    for (int i = tid; i < n; i += ST_THREADS) E[i] = (i == 0 ? 0.0 : w.x[i - 1]) - tau * Wv[i] * wz;
+    __syncthreads();
+    s[ST_TCG_STOP] = RIPTRM_TRS_BOUNDARY + r.kind;
+    s[ST_J] = -1.0;   // no tCG iterations
+    return tcg_end();
+  }
+
+  // smallest eigenvalue of HwNew's matrix at (x_new, y_new) = (IN1, YNEW) (RIPTRM.py:599-612);
+  // S x_new directly from S (n <= 97)
+  __device__ __noinline__ double trial_mineig() {
+    riptrm_trs::Blk<ST_THREADS> B(trs_red());
+    riptrm_trs::Work w = riptrm_trs::make_work(tl, n - 1);
+    const double* XN = V(V_IN1);
+    const double* YN = V(V_YNEW);
+    double h3[3] = {0.0, 0.0, 0.0};
+    for (int i = tid; i < n; i += ST_THREADS) {
+      double acc = 0.0;
+      for (int j = 0; j < n; ++j) acc += s_at(i, j) * XN[j];
+      h3[0] += XN[i] * XN[i];
+      h3[1] += XN[i] * acc;
+      h3[2] += YN[i] * XN[i];
+    }
+    const double xx = B.sum(h3[0]), xSx = B.sum(h3[1]), yx = B.sum(h3[2]);
+    repmat(B, w, XN, YN, xx, (xSx + yx) * xx);
+    return riptrm_trs::min_eig<ST_THREADS>(B, w);
+  }
+
   // after tCG: RIPTRM.py:733-746 (direction, ||dx||, dy, retraction) + feasibility part of :591
   __device__ __forceinline__ int tcg_end() {
     cadd(ST_TCG_TOTAL, s[ST_J] + 1.0);
@@ -1265,6 +1392,16 @@ struct Machine {
     s[ST_XFEAS] = (c3[2] == 0.0) ? 1.0 : 0.0;
     s[ST_COMPL] = sqrt(c3[4]);
     s[ST_YFEAS] = (c3[3] == 0.0) ? 1.0 : 0.0;
+    if (EXACT && P.opt.trs_solver == RIPTRM_TRS_SOLVER_EXACT_REPMAT && P.opt.second_order_stationarity) {
+      // compute_inner_stoppingcriteria's eigen-check at (x_new, y_new), RIPTRM.py:599-613
+      double me = 0.0;
+      if constexpr (EXACT) me = trial_mineig();
+      const int mi = (int)s[ST_MU_IDX];
+      const double tol2 = P.opt.tol2_table ? P.opt.tol2_table[mi < P.tab_len ? mi : P.tab_len - 1] : mu;
+      s[ST_HASMIN] = 1.0;
+      s[ST_MINEIG] = me;
+      s[ST_MINEIG_OK] = (me >= -tol2) ? 1.0 : 0.0;
+    }
     if (s[ST_XFEAS] != 0.0) {
       s[ST_PHASE] = PH_TRIAL;
       return request(2);
@@ -1291,6 +1428,8 @@ struct Machine {
       c[ST_I_RATIO] = ratio;
       c[ST_I_RU] = ru;
       c[ST_I_DC] = dc;
+      c[ST_I_HASMIN] = s[ST_HASMIN];
+      c[ST_I_MINEIG] = s[ST_MINEIG];
     }
   }
 
@@ -1323,7 +1462,7 @@ struct Machine {
     bsum<1>(R, g2);
     const double normgl = sqrt(g2[0]);
     const bool yfeas = s[ST_YFEAS] != 0.0;
-    const bool conv = yfeas && normgl <= s[ST_TOLL] && s[ST_COMPL] <= s[ST_TOLC];
+    const bool conv = yfeas && normgl <= s[ST_TOLL] && s[ST_COMPL] <= s[ST_TOLC] && s[ST_MINEIG_OK] != 0.0;
     if (conv) {  // RIPTRM.py:762-766
       copy(V_X, V_IN1);
       copy(V_Y, V_YNEW);
@@ -1463,12 +1602,15 @@ struct Machine {
     }
   }
 };
+using Machine = MachineT<false>;
 
 // full = 1: workgroup k serves instance full_base + k (k < full_count); else workgroup k
 // serves lists[list_in][k].  List ids are group * 2 + parity (two independent instance groups).
+template <bool EXACT>
 __global__ void __launch_bounds__(ST_THREADS) k_state(DevParams P, int full, int list_in, int list_out,
                                                       int full_base, int full_count) {
   __shared__ double redbuf[2 * ST_WAVES * RED_MAX];
+  extern __shared__ double trs_lds[];   // Exact_RepMat only (dynamic size 0 otherwise)
   int b;
   if (full) {
     if ((int)blockIdx.x >= full_count) return;
@@ -1484,7 +1626,7 @@ __global__ void __launch_bounds__(ST_THREADS) k_state(DevParams P, int full, int
     if ((int)blockIdx.x >= P.cnt[list_in]) return;
     b = P.lists[list_in * P.batch + blockIdx.x];
   }
-  Machine M(P, b, list_out, redbuf);
+  MachineT<EXACT> M(P, b, list_out, redbuf, trs_lds);
   const int ph = (int)M.s[ST_PHASE];
   if (ph == PH_DONE || ph == PH_IDLE || ph == PH_ERROR) return;
   if (!full && ph == PH_TCG && P.n <= Machine::RT_EPT * ST_THREADS) {
@@ -1827,6 +1969,12 @@ static int launch_gemv(riptrm_ctx* c, hipStream_t st, int list_in, int zero_cnt,
   return RIPTRM_OK;
 }
 
+// dynamic LDS of k_state: the Exact_RepMat work area (Machine::trs_wvec / trs_uvec / trs_red)
+static size_t state_lds_bytes(const DevParams& P) {
+  if (P.opt.trs_solver != RIPTRM_TRS_SOLVER_EXACT_REPMAT) return 0;
+  return ((size_t)riptrm_trs::work_doubles(P.n - 1) + 2 * (riptrm_trs::DIM_MAX + 1) + 2 * ST_WAVES) * sizeof(double);
+}
+
 static int launch_state(riptrm_ctx* c, hipStream_t st, int full, int list_in, int list_out, int bound,
                         int full_base = 0) {
   const int blocks = bound;
@@ -1834,8 +1982,12 @@ static int launch_state(riptrm_ctx* c, hipStream_t st, int full, int list_in, in
   int i0 = -1, i1 = -1;
   hipEvent_t e0 = nullptr, e1 = nullptr;
   if (c->prof && (e0 = prof_event(c, &i0)) && (e1 = prof_event(c, &i1))) HIPCHK(c, hipEventRecord(e0, st));
-  hipLaunchKernelGGL(k_state, dim3((unsigned)blocks), dim3(ST_THREADS), 0, st, c->P, full, list_in, list_out,
-                     full_base, bound);
+  if (c->P.opt.trs_solver == RIPTRM_TRS_SOLVER_EXACT_REPMAT)
+    hipLaunchKernelGGL(k_state<true>, dim3((unsigned)blocks), dim3(ST_THREADS), state_lds_bytes(c->P), st, c->P, full,
+                       list_in, list_out, full_base, bound);
+  else
+    hipLaunchKernelGGL(k_state<false>, dim3((unsigned)blocks), dim3(ST_THREADS), 0, st, c->P, full, list_in, list_out,
+                       full_base, bound);
   HIPCHK(c, hipGetLastError());
   if (c->prof && e1) {
     HIPCHK(c, hipEventRecord(e1, st));
@@ -2057,14 +2209,18 @@ int riptrm_solve_begin(riptrm_ctx* ctx, const riptrm_options* opt, const double*
   if (!ctx->bound) return fail(ctx, RIPTRM_E_STATE, "solve_begin: bind first");
   if (!opt || opt->struct_size != (int32_t)sizeof(riptrm_options))
     return fail(ctx, RIPTRM_E_ARG, "solve_begin: riptrm_options.struct_size mismatch");
-  if (opt->trs_solver != RIPTRM_TRS_SOLVER_TCG)
-    return fail(ctx, RIPTRM_E_ARG, "solve_begin: Exact_RepMat is not implemented for NonnegPCA yet");
+  if (opt->trs_solver != RIPTRM_TRS_SOLVER_TCG && opt->trs_solver != RIPTRM_TRS_SOLVER_EXACT_REPMAT)
+    return fail(ctx, RIPTRM_E_ARG, "solve_begin: unknown trs_solver");
+  if (opt->trs_solver == RIPTRM_TRS_SOLVER_EXACT_REPMAT && (ctx->P.n < 2 || ctx->P.n - 1 > RIPTRM_TRS_DIM_MAX))
+    return fail(ctx, RIPTRM_E_ARG, "solve_begin: Exact_RepMat needs 2 <= n <= RIPTRM_TRS_DIM_MAX + 1");
   if (!x0 || !y0 || ldv < ctx->P.n || !mu_table || !tolL_table || !tolC_table || table_len <= 0)
     return fail(ctx, RIPTRM_E_ARG, "solve_begin: bad argument");
   if (opt->log_capacity > ctx->L.cap) return fail(ctx, RIPTRM_E_ARG, "solve_begin: log_capacity exceeds bound capacity");
   HIPCHK(ctx, hipSetDevice(ctx->device));
   DevParams& P = ctx->P;
   P.opt = *opt;
+  if (const size_t shm = state_lds_bytes(P))
+    HIPCHK(ctx, hipFuncSetAttribute((const void*)k_state<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm));
   P.mu_tab = mu_table;
   P.tolL_tab = tolL_table;
   P.tolC_tab = tolC_table;

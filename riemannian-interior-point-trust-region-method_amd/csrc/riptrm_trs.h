@@ -129,7 +129,7 @@ __device__ __forceinline__ void pair_of(int r, int k, int me, int& p, int& q) {
 // eigenvalues (diagonal order) and, if want_v, w.V the eigenvectors as columns (A0 = V diag V^T).
 // Rotation formulas: Numerical Recipes' (same as the serial jacobi_reg of riptrm_si.hip).
 template <int NT>
-__device__ void jacobi(Blk<NT>& B, Work& w, bool want_v) {
+__device__ __noinline__ void jacobi(Blk<NT>& B, Work& w, bool want_v) {
   const int tid = threadIdx.x;
   const int m = w.dim, lda = w.lda;
   double* A = w.A;
@@ -229,7 +229,7 @@ __device__ void jacobi(Blk<NT>& B, Work& w, bool want_v) {
 
 // smallest eigenvalue of w.A (destroys w.A): RIPTRM.py:611-612
 template <int NT>
-__device__ double min_eig(Blk<NT>& B, Work& w) {
+__device__ __noinline__ double min_eig(Blk<NT>& B, Work& w) {
   jacobi<NT>(B, w, false);
   double v = INFINITY;
   for (int i = threadIdx.x; i < w.dim; i += NT) v = fmin(v, w.ev[i]);
@@ -256,7 +256,7 @@ struct Result {
 // TRSgep(A, a, I, Delta, tolhardcase): w.A, w.a filled by the caller (A symmetric).  Writes the
 // solution into w.x; w.A is destroyed.
 template <int NT>
-__device__ Result trs_solve(Blk<NT>& B, Work& w, double Delta, double tolhardcase) {
+__device__ __noinline__ Result trs_solve(Blk<NT>& B, Work& w, double Delta, double tolhardcase) {
   const int tid = threadIdx.x;
   const int m = w.dim;
   const double D2 = Delta * Delta;

@@ -399,3 +399,50 @@ def test_ripm_operator_aw_matches_oracle(n, B, layout):
         P = O.NonnegPCAStructured(Zs[0])
         ref = O.ripm_operator_aw(P, xs[0], zs[0], ss[0], vs[0])
         assert np.linalg.norm(out[0] - ref) <= 1e-12 * np.linalg.norm(ref)
+
+
+@pytest.mark.parametrize("sos", [True, False])
+@pytest.mark.parametrize("layout", ["sym", "full"])
+def test_exact_repmat_fixture_n50_matches_oracle(fixture_n50, sos, layout):
+    """TRS_solver = 'Exact_RepMat' (RIPTRM.py:433-444) on dataset/NonnegPCA/1 point a: HwCur's
+    matrix in the Householder frame of x^perp, TRSgep on the device (csrc/riptrm_trs.h), and with
+    second_order_stationarity the eigen-check at every trial point (RIPTRM.py:599-617), against the
+    oracle (the reference's 2n x 2n pencil, trs_oracle.trs_gep).  Same trajectory bar as tCG."""
+    from parity import compare_until_flip
+    Z, x0, y0 = fixture_n50
+    K = 6
+    opt = dict(TRS_solver="Exact_RepMat", second_order_stationarity=sos, maxiter=K)
+    eng = _engine(Z, layout=layout)
+    res = eng.solve(x0[None], y0[None], _gpu_opt(**opt))
+    ref = O.solve(Z, x0, y0, _oracle_opt(**opt))
+    gl = res.log(0)
+    assert f"{gl['residual'][0]:.6e}" == "4.986888e+00"
+    kinds = [k for k in gl["dxtype"] if k is not None]
+    assert kinds and all(k in ("boundary", "interior", "hardcase_1") for k in kinds), kinds
+    assert any(v is not None for v in gl["mineigvalHw"]) == sos
+    compare_until_flip(gl, ref.log)
+
+
+def test_exact_repmat_batch_matches_oracle():
+    """A batch of instances (n = 33) with the class defaults (Exact_RepMat + second-order test)."""
+    from parity import compare_until_flip
+    insts = [G.generate_instance(33, 300 + b) for b in range(3)]
+    eng = _engine(np.stack([z for z, _, _ in insts]))
+    opt = dict(TRS_solver="Exact_RepMat", second_order_stationarity=True, maxiter=8)
+    res = eng.solve(np.stack([x for _, x, _ in insts]), np.stack([y for _, _, y in insts]), _gpu_opt(**opt))
+    for b, (Z, x0, y0) in enumerate(insts):
+        compare_until_flip(res.log(b), O.solve(Z, x0, y0, _oracle_opt(**opt)).log)
+
+
+def test_exact_repmat_reference_defaults_drop_in(fixture_n50):
+    """RIPTRM(option) without TRS_solver runs the class default Exact_RepMat (RIPTRM.py:325)."""
+    from problems import NonnegPCAProblem, manviofun
+    from RIPTRM import RIPTRM
+    Z, x0, y0 = fixture_n50
+    out = RIPTRM({"maxiter": 3, "tolresid": 0.0, "maxtime": 1e9, "manviofun": manviofun}).run(
+        NonnegPCAProblem(Z=Z, initialpoint=x0, initialineqLagmult=y0))
+    assert out.name == "RIPTRM_Exact_RepMat"
+    assert any(v is not None for v in out.log["mineigvalHw"])
+    with pytest.raises(NotImplementedError):
+        Zb, xb, yb = G.generate_instance(120, 1)
+        RIPTRM({"maxiter": 1}).run(NonnegPCAProblem(Z=Zb, initialpoint=xb, initialineqLagmult=yb))

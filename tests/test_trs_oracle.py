@@ -103,3 +103,35 @@ def test_si_exact_repmat_oracle_short_run():
     assert kinds and all(k in ("boundary", "interior") or k.startswith("hardcase") for k in kinds)
     mins = [v for v in r.log["mineigvalHw"] if v is not None]
     assert mins and all(np.isfinite(mins))
+
+
+def test_sphere_basis_and_direction_are_basis_independent(fixture_n50):
+    """NonnegPCA: the Householder frame (device) and the reference's random Gram-Schmidt frame
+    (utils.py:388-397) give the same Exact_RepMat direction and the same smallest eigenvalue."""
+    from oracle import riptrm_oracle as O
+    Z, x0, y0 = fixture_n50
+    P = O.NonnegPCAVectorized(Z)
+    M = P.manifold
+    _, _, Hw, c = P.begin_inner(x0 / np.linalg.norm(x0), y0, 0.1)
+    x = x0 / np.linalg.norm(x0)
+    Bh = O.sphere_tangent_basis(x)
+    Br = O.sphere_tangent_basis(x, np.random.RandomState(0))
+    for B in (Bh, Br):
+        G = np.array([[bi @ bj for bj in B] for bi in B])
+        assert np.allclose(G, np.eye(len(B)), atol=1e-12)
+        assert max(abs(b @ x) for b in B) < 1e-12
+    d1, _, k1, H1 = T.exact_repmat_direction(M, x, Hw, c, 0.3, Bh, 1e-8)
+    d2, _, k2, H2 = T.exact_repmat_direction(M, x, Hw, c, 0.3, Br, 1e-8)
+    assert k1 == k2
+    assert np.linalg.norm(d1 - d2) <= 1e-8 * np.linalg.norm(d1)
+    assert abs(np.linalg.eigvalsh(H1)[0] - np.linalg.eigvalsh(H2)[0]) <= 1e-10 * np.abs(H1).max()
+
+
+def test_nonnegpca_exact_repmat_oracle_short_run(fixture_n50):
+    from oracle import riptrm_oracle as O
+    Z, x0, y0 = fixture_n50
+    r = O.solve(Z, x0, y0, dict(maxiter=3, tolresid=0, maxtime=1e9, TRS_solver="Exact_RepMat",
+                                second_order_stationarity=True, manviofun=O.sphere_manvio))
+    kinds = [k for k in r.log["dxtype"] if k is not None]
+    assert kinds and all(k in ("boundary", "interior") or k.startswith("hardcase") for k in kinds)
+    assert r.log["residual"][-1] < r.log["residual"][0]
