@@ -44,7 +44,15 @@ def log(msg):
     print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
 
 
-def cpu_baseline(n: int, warmup: int, steps: int, budget_s: float):
+def trs_options(trs: str) -> dict:
+    """--trs: the reference's shipped path (tCG, config_simulation.yaml:21-22) or its class
+    default (Exact_RepMat + second-order stationarity, RIPTRM.py:325-326)."""
+    if trs == "Exact_RepMat":
+        return {"TRS_solver": "Exact_RepMat", "second_order_stationarity": True}
+    return {"TRS_solver": "tCG", "second_order_stationarity": False}
+
+
+def cpu_baseline(n: int, warmup: int, steps: int, budget_s: float, trs: str = "tCG"):
     """Oracle (vectorised NumPy) on one instance: outer iterations warmup+1..warmup+steps."""
     import numpy as np
     from oracle import nonnegpca_gen as G
@@ -56,8 +64,8 @@ def cpu_baseline(n: int, warmup: int, steps: int, budget_s: float):
         cores = int(os.environ.get("OMP_NUM_THREADS", "1"))
     Z, x0, y0 = G.generate_instance(n, G.SEED0)
     t_start = time.time()
-    orc = O.RIPTRMOracle(dict(maxiter=warmup + steps, tolresid=0.0, maxtime=1e12, manviofun=O.sphere_manvio),
-                         deadline=t_start + budget_s)
+    orc = O.RIPTRMOracle(dict(maxiter=warmup + steps, tolresid=0.0, maxtime=1e12, manviofun=O.sphere_manvio,
+                              **trs_options(trs)), deadline=t_start + budget_s)
     P = O.NonnegPCAVectorized(Z)
     complete = True
     try:
@@ -76,7 +84,8 @@ def cpu_baseline(n: int, warmup: int, steps: int, budget_s: float):
             "sample": (f"oracle/riptrm_oracle.py NonnegPCAVectorized, 1 instance n={n} (reference generator "
                        f"recipe, seed {G.SEED0}), outer iterations {warmup + 1}..{last} "
                        f"({done} timed, {el:.1f} s, evaluation time excluded as RIPTRM.py:932-941; "
-                       f"{'complete' if complete else 'budget-truncated'} window), NumPy + OpenBLAS dsymv (one triangle of S), {cores} threads")}
+                       f"{'complete' if complete else 'budget-truncated'} window), NumPy + OpenBLAS dsymv (one triangle of S), {cores} threads"
+                       + (", TRS_solver=Exact_RepMat (trs_oracle: 2n x 2n pencil, scipy.linalg.eig)" if trs != "tCG" else ""))}
 
 
 def main():
@@ -94,6 +103,8 @@ def main():
     ap.add_argument("--problem", default="nonnegpca", choices=["nonnegpca", "si", "stiefel"],
                     help="si: StableIdentification (d=5 fixture, starts cycled + perturbed), one launch per solve")
     ap.add_argument("--stiefel-p", type=int, default=50, help="p of Stiefel(n, p) for --problem stiefel")
+    ap.add_argument("--trs", default="tCG", choices=["tCG", "Exact_RepMat"],
+                    help="subproblem solver (Exact_RepMat: manifold.dim <= 96, with the second-order test)")
     ap.add_argument("--stream-groups", type=int, default=0, choices=[0, 1, 2],
                     help="instance groups on separate streams (0 = library default)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_gemv.json"))
@@ -142,8 +153,7 @@ def main():
     # global instance ids owned by this rank: rank, rank+world, ... (seed seed0 + id)
     gen_ids = [rank + world * i for i in range(B)]
     xg, yg = eng.generate_synthetic(args.seed0, ids=gen_ids)
-    opt = {"TRS_solver": "tCG", "second_order_stationarity": False, "maxiter": W + 2 * K, "tolresid": 0.0,
-           "maxtime": math.inf, "manviofun": manviofun}
+    opt = {"maxiter": W + 2 * K, "tolresid": 0.0, "maxtime": math.inf, "manviofun": manviofun, **trs_options(args.trs)}
     eng.begin(xg, yg, opt, restart_every=args.cycle)
     torch.cuda.synchronize(dev)
     t0 = time.time()
@@ -235,7 +245,7 @@ def main():
         cpu = None
         if args.cpu_budget > 0 and world == 1:
             log("CPU baseline (oracle) ...")
-            cpu = cpu_baseline(n, W, min(K, max(1, args.cycle - W)), args.cpu_budget)
+            cpu = cpu_baseline(n, W, min(K, max(1, args.cycle - W)), args.cpu_budget, args.trs)
         out = {
             "metric": METRIC,
             "value": outer_all / T,
@@ -252,7 +262,9 @@ def main():
             "config": {"workload": (f"NonnegPCA n={n}, one Z with {B} initial points per GPU (multi-start, "
                                     f"the problem_initialpoint axis; SURVEY 8d variant)") if args.layout == "shared"
                                    else (f"NonnegPCA n={n}, batch of {B} independent instances per GPU "
-                                         f"(BASELINE configs[2]; configs[3] at 8 GPUs)"),
+                                         f"(BASELINE configs[2]; configs[3] at 8 GPUs)")
+                                   + ("" if args.trs == "tCG" else ", TRS_solver=Exact_RepMat + second-order test"),
+                       "trs_solver": args.trs,
                        "n": n, "batch_per_gpu": B, "global_batch": B * world,
                        "outer_window": [W + 1, W + K], "restart_every": args.cycle, "layout": args.layout,
                        "parallelism": f"instance-sharded x{world}"},
@@ -357,8 +369,8 @@ def bench_si(args, world, rank, dev, dist):
     cons = si.expand_constset(np.loadtxt(os.path.join(ROOT, "tests", "golden", "si_1", "constset.csv")))
     eng = si.SIBatch(data.d, data.N, data.m, B, log_capacity=16)
     eng.load(data.X, data.XP, data.h, cons)
-    opt = {"TRS_solver": "tCG", "manviofun": si.si_manviofun, "tolresid": 0.0, "maxtime": math.inf,
-           "maxiter": max(1, W), "save_inner_iteration": True}
+    opt = {"manviofun": si.si_manviofun, "tolresid": 0.0, "maxtime": math.inf,
+           "maxiter": max(1, W), "save_inner_iteration": True, **trs_options(args.trs)}
     eng.solve(xs, ys, opt)          # warmup launch (W outer iterations), untimed
     opt["maxiter"] = K
     if world > 1:
@@ -397,8 +409,8 @@ def bench_si(args, world, rank, dev, dist):
     if args.cpu_budget > 0 and world == 1:
         from oracle import riptrm_oracle as RO
         from oracle import si_oracle as SI
-        orc = RO.RIPTRMOracle(dict(maxiter=K, tolresid=0.0, maxtime=1e12, manviofun=SI.si_manvio),
-                              deadline=time.time() + args.cpu_budget)
+        orc = RO.RIPTRMOracle(dict(maxiter=K, tolresid=0.0, maxtime=1e12, manviofun=SI.si_manvio,
+                                   **trs_options(args.trs)), deadline=time.time() + args.cpu_budget)
         try:
             orc.run(SI.SIVectorized(data), xs[0], ys[0])
         except RO.BudgetExceeded:
@@ -415,7 +427,9 @@ def bench_si(args, world, rank, dev, dist):
         "ms_per_step": T / K * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
         "dtype": "f64",
         "data": "reference fixture dataset/StableIdentification/1 (noisy X, 16 constraints), starts a..t cycled + perturbed",
-        "config": {"workload": f"StableIdentification d=5 N=95 m=16, {B} starts per GPU, outer iterations 1..{K}",
+        "config": {"workload": f"StableIdentification d=5 N=95 m=16, {B} starts per GPU, outer iterations 1..{K}"
+                               + ("" if args.trs == "tCG" else ", TRS_solver=Exact_RepMat + second-order test"),
+                   "trs_solver": args.trs,
                    "global_batch": B * world, "parallelism": f"instance-sharded x{world}"},
         "roofline": {"bound": "latency", "achieved": hvps / kern_s / 1e6, "peak": None, "unit": "M HVP/s",
                      "frac": None, "traffic": None,

@@ -65,7 +65,8 @@ static_assert(ST_N_USED <= ST_N, "state slots overflow");
 
 enum Phase : int {
   PH_IDLE = 0, PH_START, PH_AFTER_SX0, PH_TCG, PH_TRIAL, PH_PAUSED, PH_DONE,
-  PH_TCGO_START, PH_TCGO_SX, PH_ERROR
+  PH_TCGO_START, PH_TCGO_SX, PH_ERROR,
+  PH_TRS, PH_TRS_END   // Exact_RepMat: subproblem solve / rest of the inner step (no S-pass between)
 };
 
 enum Mode : int { MODE_SOLVE = 0, MODE_TCG_ONLY = 1 };

@@ -515,7 +515,9 @@ __global__ void __launch_bounds__(256) k_pack(const double* Z, int64_t ldz, int6
 // ------------------------------------------------------------------------------------------
 // The per-instance state machine.
 // ------------------------------------------------------------------------------------------
-enum Act : int { ACT_YIELD = 0, ACT_DONE = 1, ACT_PAUSE = 2 };
+// ACT_CONTINUE: the next phase needs no S-pass; k_state<true> dispatches it in a loop (a direct
+// call would recurse through the inner loop whenever trial points are infeasible)
+enum Act : int { ACT_YIELD = 0, ACT_DONE = 1, ACT_PAUSE = 2, ACT_CONTINUE = 3 };
 
 // EXACT = false: the tCG machine (every shipped config); EXACT = true adds the Exact_RepMat
 // branches (a separate k_state instantiation, so the tCG kernel carries none of its code or
@@ -909,7 +911,10 @@ struct MachineT {
     s[ST_MINEIG] = 0.0;
     s[ST_MINEIG_OK] = 1.0;
     if constexpr (EXACT) {
-      if (P.opt.trs_solver == RIPTRM_TRS_SOLVER_EXACT_REPMAT && (int)s[ST_MODE] == MODE_SOLVE) return trs_direction();
+      if (P.opt.trs_solver == RIPTRM_TRS_SOLVER_EXACT_REPMAT && (int)s[ST_MODE] == MODE_SOLVE) {
+        s[ST_PHASE] = PH_TRS;
+        return ACT_CONTINUE;
+      }
     }
     if (n - 1 <= 0) {  // maxinner = manifold.dim = 0: no tCG iteration is possible
       cset(ST_ERROR, 1.0);
@@ -1311,7 +1316,8 @@ struct MachineT {
     __syncthreads();
     s[ST_TCG_STOP] = RIPTRM_TRS_BOUNDARY + r.kind;
     s[ST_J] = -1.0;   // no tCG iterations
-    return tcg_end();
+    s[ST_PHASE] = PH_TRS_END;
+    return ACT_CONTINUE;
   }
 
   // smallest eigenvalue of HwNew's matrix at (x_new, y_new) = (IN1, YNEW) (RIPTRM.py:599-612);
@@ -1597,6 +1603,11 @@ struct MachineT {
       case PH_TCGO_SX:
         copy(V_SX, V_OUT0);
         return tcg_begin();
+      case PH_TRS:
+        if constexpr (EXACT) return trs_direction();
+        return ACT_DONE;
+      case PH_TRS_END:
+        return tcg_end();
       default:
         return ACT_DONE;
     }
@@ -1634,7 +1645,12 @@ __global__ void __launch_bounds__(ST_THREADS) k_state(DevParams P, int full, int
   } else {
     if (!full && P.layout == RIPTRM_LAYOUT_SYMTILE) M.gather_out(P.req[b]);
     if (!full && P.layout == RIPTRM_LAYOUT_SHARED) M.gather_slices(P.req[b]);
-    M.dispatch();
+    if constexpr (EXACT) {
+      while (M.dispatch() == ACT_CONTINUE) {
+      }
+    } else {
+      M.dispatch();
+    }
   }
   M.finish_write();
 }
@@ -2090,7 +2106,11 @@ static int run_steps(riptrm_ctx* c, int steps, int* n_active) {
   // launching 2 kernels per step from the host
   const bool small = (double)c->P.batch * (double)s_elems_of(c->P.n, c->P.layout) * 8.0 < 2.0e8 ||
                      c->P.layout == RIPTRM_LAYOUT_SHARED;
-  if (c->graphs && !c->prof && c->ngroups == 1 && c->active_bound[0] > 0 && small && steps > 0) {
+  // Exact_RepMat's k_state needs up to 156 KiB of dynamic LDS: raised by hipFuncSetAttribute for
+  // direct launches, but a replayed graph's kernel node ran without it (LDS accesses past 64 KiB
+  // faulted, n = 97) -> direct launches whenever the state kernel needs more than the default
+  const bool graph_ok = state_lds_bytes(c->P) <= 64 * 1024;
+  if (c->graphs && !c->prof && c->ngroups == 1 && c->active_bound[0] > 0 && small && steps > 0 && graph_ok) {
     int bound = 1;
     while (bound < c->active_bound[0]) bound *= 2;
     if (bound > c->P.batch) bound = c->P.batch;

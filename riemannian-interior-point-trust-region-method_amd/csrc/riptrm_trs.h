@@ -337,7 +337,8 @@ __device__ __noinline__ Result trs_solve(Blk<NT>& B, Work& w, double Delta, doub
     for (int k = 0; k < m; ++k) acc += w.V[k * lda + i] * w.a[k];
     w.g[i] = acc;
   }
-  const int kmin = (int)B.min(imin);
+  const double kd = B.min(imin);   // no index when every eigenvalue is NaN: never form one from inf
+  const int kmin = (kd >= 0.0 && kd < (double)m) ? (int)kd : 0;
   __syncthreads();
   const double hard_tol = 1e-12 * fmax(1.0, lmax_abs);
   double gh = 0.0, gg = 0.0;
