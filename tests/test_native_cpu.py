@@ -91,10 +91,16 @@ def test_options_struct_layout_matches_c(tmp_path, cls, cname):
 def test_resolve_options_defaults_and_errors():
     import engine
     from problems import manviofun
+    ro_d = engine.resolve_options({}, np.pi, 16)   # reference defaults: Exact_RepMat + second-order test
+    assert ro_d.exact and ro_d.c_opt.second_order_stationarity == 1 and ro_d.c_opt.trs_tolhardcase == 1e-8
+    assert ro_d.tol2_tab == ro_d.mu_tab                # forcing_function_second_order = mu (RIPTRM.py:322)
+    with pytest.raises(ValueError):
+        engine.resolve_options({"TRS_solver": "Lanczos"}, np.pi, 16)   # RIPTRM.py:453-454
     with pytest.raises(NotImplementedError):
-        engine.resolve_options({}, np.pi, 16)  # reference default TRS_solver is Exact_RepMat
+        engine.resolve_options({"checkTRSoptimality": True}, np.pi, 16)
     ro = engine.resolve_options({"TRS_solver": "tCG", "manviofun": manviofun, "maxiter": 50}, np.pi, 16)
     c = ro.c_opt
+    assert not ro.exact and c.trs_solver == N.CONST["RIPTRM_TRS_SOLVER_TCG"] and c.second_order_stationarity == 0
     assert c.struct_size == ctypes.sizeof(N.RiptrmOptions)
     assert c.maxiter == 50 and c.inner_maxiter == -1 and c.inner_maxtime == -1.0
     assert c.initial_tr_radius == np.pi / 8
