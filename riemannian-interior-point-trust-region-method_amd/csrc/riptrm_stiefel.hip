@@ -7,9 +7,14 @@
 //   retraction  qf(X + U), the QR factor with diag(R) > 0
 //   e2rh        P_X(H - U sym(X^T G))
 //   inner       tr(U^T V)
-// One 256-thread workgroup per instance.  Both products of a projection run on the fp64 matrix
-// cores: the p x p Gram X^T U as 16 x 16 blocks over K = n, the n x p update X sym(.) with the
-// p x p factor in LDS; per projection 3 n p doubles of HBM traffic (read X, U, write the result).  The retraction is CholeskyQR2 (Q = A R^-1
+// One 512-thread workgroup (8 waves) per instance.  Both products of a projection run on the fp64
+// matrix cores: the symmetric Gram sym(X^T U) streamed row-chunk-wise into registers by all eight
+// waves at once (gram_sym), the n x p update X sym(.) with the p x p factor in LDS; per projection
+// 3 n p doubles of HBM traffic (read X, U, write the result; the update's re-reads hit L2).
+// At p = 50 the two products are ~4 n p^2 flops against 24 n p bytes (p / 6 flop/B, the fp64
+// ridge is 78.6 TFLOP/s / 8 TB/s ~ 10): v_mfma_f64_16x16x4_f64 keeps its SIMD busy 64 cycles
+// (SQ_VALU_MFMA_BUSY_CYCLES / SQ_INSTS_VALU_MFMA_F64 measured), so one point per CU is
+// latency-bound on its chain of loads, MFMAs and barriers.  The retraction is CholeskyQR2 (Q = A R^-1
 // with R = chol(A^T A), twice): diag(R) > 0 by construction, so it is pymanopt's qf up to
 // rounding for full-rank A.
 #include <hip/hip_runtime.h>
@@ -20,20 +25,24 @@ namespace riptrm_stiefel {
 
 #pragma clang fp contract(off)
 
-constexpr int T = 256;         // threads per workgroup
+constexpr int NW = 8;          // waves per workgroup (one workgroup per point)
+constexpr int T = NW * 64;     // threads per workgroup
 constexpr int PMAX = RIPTRM_STIEFEL_PMAX;
-constexpr int OUT_PER = (PMAX * PMAX + T - 1) / T;
+constexpr int GMAX = 8;        // 4-row groups per wave per streamed chunk (8 waves x 32 rows = 256 rows)
+constexpr int NBLK = 10;       // upper-triangular 16 x 16 blocks of a p x p matrix at p <= 64
 
-constexpr int RT = 32;                      // rows per streamed Gram tile
-constexpr int PER = (RT * PMAX + T - 1) / T;  // tile elements per thread
-
+// LDS (dynamic): M and L are p x p (padded stride PS <= 64), red holds the wave partials of the
+// Gram reduction tree (NW / 2 waves x NBLK blocks x 256 doubles).
 struct Smem {
-  double tA[RT * PMAX];
-  double tB[RT * PMAX];
-  double M[PMAX * PMAX];   // p x p (Gram / sym / R^-1)
-  double L[PMAX * PMAX];   // Cholesky factor
-  double red[T / 64];
+  double* M;     // p x p (Gram / sym / R^-1)
+  double* L;     // Cholesky factor
+  double* red;
 };
+constexpr int LDS_DOUBLES = 2 * PMAX * PMAX + (NW / 2) * NBLK * 256;
+
+__device__ __forceinline__ Smem smem_of(double* base) {
+  return Smem{base, base + PMAX * PMAX, base + 2 * PMAX * PMAX};
+}
 
 typedef double dbl4 __attribute__((ext_vector_type(4)));
 
@@ -41,89 +50,92 @@ typedef double dbl4 __attribute__((ext_vector_type(4)));
 // outside p x p, so the MFMA loops read operands without bounds tests (no divergent branches).
 __device__ __forceinline__ int pstride(int p) { return ((p + 15) / 16) * 16; }
 
-// M <- A^T B (p x p) for n x p row-major A, B on the fp64 matrix cores: 16 x 16 output blocks
-// (<= 16 at p <= 64) dealt to the 4 waves, K = n walked 4 rows per v_mfma_f64_16x16x4_f64.
-// Operands stream through LDS in 32-row tiles (zero padded to PS columns); the next tile's loads
-// are issued into registers before the current tile's MFMAs (one memory latency per tile).
-__device__ __forceinline__ void gram(Smem& sm, const double* __restrict__ A, const double* __restrict__ B, int n, int p) {
+// sm.M <- sym(A^T B) = (A^T B + B^T A) / 2 for n x p row-major A, B, exactly symmetric, on the fp64
+// matrix cores.  Every wave streams its own rows straight into registers — each lane loads the
+// 4 x 16 operand fragments of v_mfma_f64_16x16x4_f64 for GMAX 4-row groups and all p columns at
+// once (one memory latency per 256-row chunk, all loads of the workgroup in flight together) —
+// and accumulates the upper-triangular blocks S_IJ = A_I^T B_J + B_I^T A_J (I <= J).  The eight
+// wave partials meet in a fixed LDS tree (bitwise deterministic); wave 0 writes S / 2.
+__device__ __forceinline__ void gram_sym(Smem& sm, const double* __restrict__ A, const double* __restrict__ B,
+                                         int n, int p) {
   const int t = threadIdx.x, l = t & 63, w = t >> 6;
-  const int P16 = (p + 15) / 16, nb = P16 * P16, PS = P16 * 16;
   const int c = l & 15, kk = l >> 4;
-  const int te = RT * PS;
-  dbl4 acc[4];
+  const int P16 = (p + 15) / 16, PS = P16 * 16;
+  dbl4 acc[NBLK];
 #pragma unroll
-  for (int q = 0; q < 4; ++q) acc[q] = dbl4{0.0, 0.0, 0.0, 0.0};
-  double ra[PER], rb[PER];
-  auto fetch = [&](int r0) {
+  for (int b = 0; b < NBLK; ++b) acc[b] = dbl4{0.0, 0.0, 0.0, 0.0};
+  for (int r0 = 0; r0 < n; r0 += NW * GMAX * 4) {
+    double ar[GMAX][4], br[GMAX][4];
 #pragma unroll
-    for (int i = 0; i < PER; ++i) {
-      const int e = t + i * T;
-      const int rr = e / PS, cc = e - (e / PS) * PS;
-      const bool ok = e < te && cc < p && r0 + rr < n;
-      const int64_t g = ok ? (int64_t)(r0 + rr) * p + cc : 0;
-      const double va = A[g], vb = B[g];
-      ra[i] = ok ? va : 0.0;
-      rb[i] = ok ? vb : 0.0;
+    for (int g = 0; g < GMAX; ++g) {
+      const int row = r0 + (w * GMAX + g) * 4 + kk;
+#pragma unroll
+      for (int I = 0; I < 4; ++I) {
+        const int col = 16 * I + c;
+        const bool ok = row < n && col < p;
+        const int64_t e = ok ? (int64_t)row * p + col : 0;
+        const double va = A[e], vb = B[e];
+        ar[g][I] = ok ? va : 0.0;
+        br[g][I] = ok ? vb : 0.0;
+      }
     }
-  };
-  fetch(0);
-  for (int r0 = 0; r0 < n; r0 += RT) {
 #pragma unroll
-    for (int i = 0; i < PER; ++i) {
-      const int e = t + i * T;
-      if (e < te) { sm.tA[e] = ra[i]; sm.tB[e] = rb[i]; }
+    for (int g = 0; g < GMAX; ++g) {
+      if (r0 + (w * GMAX + g) * 4 >= n) break;   // wave-uniform: rows past n are all zero
+      int b = 0;
+#pragma unroll
+      for (int I = 0; I < 4; ++I)
+#pragma unroll
+        for (int J = I; J < 4; ++J) {
+          if (J < P16) {
+            acc[b] = __builtin_amdgcn_mfma_f64_16x16x4f64(ar[g][I], br[g][J], acc[b], 0, 0, 0);
+            acc[b] = __builtin_amdgcn_mfma_f64_16x16x4f64(br[g][I], ar[g][J], acc[b], 0, 0, 0);
+          }
+          ++b;
+        }
+    }
+  }
+  // tree over the waves: upper half writes, lower half adds (4 -> 2 -> 1)
+#pragma unroll
+  for (int h = NW / 2; h >= 1; h >>= 1) {
+    if (w >= h && w < 2 * h) {
+      double* r = sm.red + (int64_t)(w - h) * NBLK * 256;
+#pragma unroll
+      for (int b = 0; b < NBLK; ++b)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) r[b * 256 + q * 64 + l] = acc[b][q];
     }
     __syncthreads();
-    if (r0 + RT < n) fetch(r0 + RT);
+    if (w < h) {
+      const double* r = sm.red + (int64_t)w * NBLK * 256;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int blk = w + 4 * q;
-      if (blk < nb) {
-        const int I = blk / P16, J = blk - (blk / P16) * P16;
-        const double* pa = sm.tA + kk * PS + I * 16 + c;
-        const double* pb = sm.tB + kk * PS + J * 16 + c;
+      for (int b = 0; b < NBLK; ++b)
 #pragma unroll
-        for (int k4 = 0; k4 < RT / 4; ++k4)
-          acc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(pa[k4 * 4 * PS], pb[k4 * 4 * PS], acc[q], 0, 0, 0);
-      }
+        for (int q = 0; q < 4; ++q) acc[b][q] = acc[b][q] + r[b * 256 + q * 64 + l];
     }
     __syncthreads();
   }
   for (int e = t; e < PS * PS; e += T) sm.M[e] = 0.0;
   __syncthreads();
+  if (w == 0) {
+    int b = 0;
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int blk = w + 4 * q;
-    if (blk < nb) {
-      const int I = blk / P16, J = blk - (blk / P16) * P16;
-      const int j = J * 16 + c;
+    for (int I = 0; I < 4; ++I)
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int i = I * 16 + kk + 4 * g;
-        if (i < p && j < p) sm.M[i * PS + j] = acc[q][g];
+      for (int J = I; J < 4; ++J) {
+        if (J < P16) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int i = I * 16 + kk + 4 * q, j = J * 16 + c;
+            if (i < p && j < p && (I < J || i <= j)) {   // one writer per symmetric pair
+              const double v = 0.5 * acc[b][q];
+              sm.M[i * PS + j] = v;
+              sm.M[j * PS + i] = v;
+            }
+          }
+        }
+        ++b;
       }
-    }
-  }
-  __syncthreads();
-}
-
-__device__ __forceinline__ void symmetrize(Smem& sm, int p) {
-  const int t = threadIdx.x, PS = pstride(p);
-  double v[OUT_PER];
-#pragma unroll
-  for (int k = 0; k < OUT_PER; ++k) {
-    const int o = t + k * T;
-    v[k] = 0.0;
-    if (o < PS * PS) {
-      const int i = o / PS, j = o - i * PS;
-      v[k] = 0.5 * (sm.M[o] + sm.M[j * PS + i]);
-    }
-  }
-  __syncthreads();
-#pragma unroll
-  for (int k = 0; k < OUT_PER; ++k) {
-    const int o = t + k * T;
-    if (o < PS * PS) sm.M[o] = v[k];
   }
   __syncthreads();
 }
@@ -137,7 +149,7 @@ __device__ __forceinline__ void update(Smem& sm, const double* A, const double* 
   const int P16 = (p + 15) / 16, R16 = (n + 15) / 16, PS = P16 * 16;
   const int c = l & 15, kk = l >> 4;
   const int P4 = (p + 3) / 4;
-  for (int I = w; I < R16; I += 4) {
+  for (int I = w; I < R16; I += NW) {
     dbl4 acc[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) acc[q] = dbl4{0.0, 0.0, 0.0, 0.0};
@@ -215,33 +227,33 @@ __device__ __forceinline__ void chol_rinv(Smem& sm, int p) {
 }
 
 __global__ void __launch_bounds__(T) k_st_proj(int n, int p, int64_t stride, const double* X, const double* U, double* out) {
-  __shared__ Smem sm;
+  extern __shared__ double lds[];
+  Smem sm = smem_of(lds);
   const int64_t o = (int64_t)blockIdx.x * stride;
-  gram(sm, X + o, U + o, n, p);
-  symmetrize(sm, p);
+  gram_sym(sm, X + o, U + o, n, p);
   update(sm, X + o, U + o, -1.0, out + o, n, p);
 }
 
 __global__ void __launch_bounds__(T) k_st_e2rh(int n, int p, int64_t stride, const double* X, const double* G,
                                                const double* H, const double* U, double* out) {
-  __shared__ Smem sm;
+  extern __shared__ double lds[];
+  Smem sm = smem_of(lds);
   const int64_t o = (int64_t)blockIdx.x * stride;
-  gram(sm, X + o, G + o, n, p);            // X^T G
-  symmetrize(sm, p);
+  gram_sym(sm, X + o, G + o, n, p);                // sym(X^T G)
   update(sm, U + o, H + o, -1.0, out + o, n, p);   // W = H - U sym(X^T G) into out
-  gram(sm, X + o, out + o, n, p);          // X^T W
-  symmetrize(sm, p);
+  gram_sym(sm, X + o, out + o, n, p);              // sym(X^T W)
   update(sm, X + o, out + o, -1.0, out + o, n, p);  // P_X(W)
 }
 
 __global__ void __launch_bounds__(T) k_st_retr(int n, int p, int64_t stride, const double* X, const double* U, double* out) {
-  __shared__ Smem sm;
+  extern __shared__ double lds[];
+  Smem sm = smem_of(lds);
   const int64_t o = (int64_t)blockIdx.x * stride;
   double* A = out + o;
   for (int e = threadIdx.x; e < n * p; e += T) A[e] = X[o + e] + U[o + e];
   __syncthreads();
   for (int pass = 0; pass < 2; ++pass) {   // CholeskyQR2
-    gram(sm, A, A, n, p);
+    gram_sym(sm, A, A, n, p);                // (A^T A + A^T A) / 2 = A^T A exactly
     chol_rinv(sm, p);
     update(sm, A, nullptr, 0.0, A, n, p);
   }
@@ -255,7 +267,11 @@ __global__ void __launch_bounds__(T) k_st_inner(int n, int p, int64_t stride, co
   for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
   __syncthreads();
-  if (threadIdx.x == 0) out[blockIdx.x] = ((red[0] + red[1]) + red[2]) + red[3];
+  if (threadIdx.x == 0) {
+    double r = red[0];
+    for (int i = 1; i < T / 64; ++i) r = r + red[i];
+    out[blockIdx.x] = r;
+  }
 }
 
 }  // namespace riptrm_stiefel
@@ -266,8 +282,18 @@ static int st_check(riptrm_ctx* c, int32_t n, int32_t p, int32_t batch, int64_t 
   if (n < 1 || p < 1 || p > PMAX || p > n || batch < 1 || stride < (int64_t)n * p)
     return fail(c, RIPTRM_E_ARG, "stiefel: need 1 <= p <= min(n, 64), batch >= 1, stride >= n*p");
   HIPCHK(c, hipSetDevice(c->device));
+  static bool attr[64] = {};   // per device: dynamic LDS above the 64 KiB default
+  if (c->device < 0 || c->device >= 64 || !attr[c->device]) {
+    const int shm = (int)(LDS_DOUBLES * sizeof(double));
+    HIPCHK(c, hipFuncSetAttribute((const void*)k_st_proj, hipFuncAttributeMaxDynamicSharedMemorySize, shm));
+    HIPCHK(c, hipFuncSetAttribute((const void*)k_st_e2rh, hipFuncAttributeMaxDynamicSharedMemorySize, shm));
+    HIPCHK(c, hipFuncSetAttribute((const void*)k_st_retr, hipFuncAttributeMaxDynamicSharedMemorySize, shm));
+    if (c->device >= 0 && c->device < 64) attr[c->device] = true;
+  }
   return RIPTRM_OK;
 }
+
+constexpr size_t SHM = LDS_DOUBLES * sizeof(double);
 
 extern "C" {
 
@@ -289,7 +315,7 @@ int riptrm_stiefel_proj(riptrm_ctx* ctx, int32_t n, int32_t p, int32_t batch, in
   if (!X || !U || !out || out == X) return fail(ctx, RIPTRM_E_ARG, "stiefel_proj: bad pointer (out must not alias X)");
   int rc = st_check(ctx, n, p, batch, stride);
   if (rc) return rc;
-  hipLaunchKernelGGL(k_st_proj, dim3(batch), dim3(T), 0, ctx->stream, n, p, stride, X, U, out);
+  hipLaunchKernelGGL(k_st_proj, dim3(batch), dim3(T), SHM, ctx->stream, n, p, stride, X, U, out);
   HIPCHK(ctx, hipGetLastError());
   return RIPTRM_OK;
 }
@@ -300,7 +326,7 @@ int riptrm_stiefel_retr(riptrm_ctx* ctx, int32_t n, int32_t p, int32_t batch, in
   if (!X || !U || !out) return fail(ctx, RIPTRM_E_ARG, "stiefel_retr: null pointer");
   int rc = st_check(ctx, n, p, batch, stride);
   if (rc) return rc;
-  hipLaunchKernelGGL(k_st_retr, dim3(batch), dim3(T), 0, ctx->stream, n, p, stride, X, U, out);
+  hipLaunchKernelGGL(k_st_retr, dim3(batch), dim3(T), SHM, ctx->stream, n, p, stride, X, U, out);
   HIPCHK(ctx, hipGetLastError());
   return RIPTRM_OK;
 }
@@ -312,7 +338,7 @@ int riptrm_stiefel_ehess2rhess(riptrm_ctx* ctx, int32_t n, int32_t p, int32_t ba
     return fail(ctx, RIPTRM_E_ARG, "stiefel_ehess2rhess: bad pointer (out must not alias X or U)");
   int rc = st_check(ctx, n, p, batch, stride);
   if (rc) return rc;
-  hipLaunchKernelGGL(k_st_e2rh, dim3(batch), dim3(T), 0, ctx->stream, n, p, stride, X, G, H, U, out);
+  hipLaunchKernelGGL(k_st_e2rh, dim3(batch), dim3(T), SHM, ctx->stream, n, p, stride, X, G, H, U, out);
   HIPCHK(ctx, hipGetLastError());
   return RIPTRM_OK;
 }
