@@ -40,9 +40,11 @@ enum Kind : int { K_BOUNDARY = 0, K_INTERIOR = 1, K_HARDCASE_1 = 2 };
 // odd row stride: column walks of the Jacobi rotations spread over the LDS banks
 __host__ __device__ constexpr int lda_of(int dim) { return dim | 1; }
 
+constexpr int ROT_FIELDS = 7;   // per pair of a Jacobi round: c, s, t, a_pp', a_qq', p, q
+
 // LDS doubles of a Work area for dim (matrix, eigenvectors, vectors, rotation table)
 __host__ __device__ constexpr int work_doubles(int dim) {
-  return 2 * dim * lda_of(dim) + 8 * DIM_MAX + 5 * (DIM_MAX / 2 + 1);
+  return 2 * dim * lda_of(dim) + 8 * DIM_MAX + ROT_FIELDS * (DIM_MAX / 2 + 1);
 }
 
 struct Work {
@@ -56,7 +58,7 @@ struct Work {
   double* cgx;  // dim   CG iterate (the interior candidate p1)
   double* g;    // dim   Q^T a
   double* ev;   // dim   eigenvalues (copied off the diagonal)
-  double* rot;  // 5 x (DIM_MAX/2 + 1)  (c, s, t, a_pp, a_qq) per pair
+  double* rot;  // ROT_FIELDS x (DIM_MAX/2 + 1)  (c, s, t, a_pp, a_qq, p, q) per pair
   int dim, lda;
 };
 
@@ -130,27 +132,27 @@ __device__ __forceinline__ void pair_of(int r, int k, int me, int& p, int& q) {
 // Rotation formulas: Numerical Recipes' (same as the serial jacobi_reg of riptrm_si.hip).
 template <int NT>
 __device__ __noinline__ void jacobi(Blk<NT>& B, Work& w, bool want_v) {
-  const int tid = threadIdx.x;
+  constexpr int NWV = NT / 64;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int m = w.dim, lda = w.lda;
   double* A = w.A;
   double* V = w.V;
   double* rot = w.rot;
+  // rows are walked by waves and columns by lanes: no integer division on the hot loops
   if (want_v)
-    for (int e = tid; e < m * m; e += NT) {
-      const int i = e / m, j = e - i * m;
-      V[i * lda + j] = (i == j) ? 1.0 : 0.0;
-    }
+    for (int i = wv; i < m; i += NWV)
+      for (int j = lane; j < m; j += 64) V[i * lda + j] = (i == j) ? 1.0 : 0.0;
   const int me = m + (m & 1);
   const int np = me / 2;
   __syncthreads();
   for (int sweep = 0; sweep < 40 && m > 1; ++sweep) {
     double off = 0.0, dg = 0.0;
-    for (int e = tid; e < m * m; e += NT) {
-      const int i = e / m, j = e - i * m;
-      const double v = A[i * lda + j];
-      if (j > i) off += v * v;
-      else if (j == i) dg += v * v;
-    }
+    for (int i = wv; i < m; i += NWV)
+      for (int j = lane; j < m; j += 64) {
+        const double v = A[i * lda + j];
+        if (j > i) off += v * v;
+        else if (j == i) dg += v * v;
+      }
     off = B.sum(off);
     dg = B.sum(dg);
     if (off <= 1e-36 * dg) break;   // off-diagonal far below the eigenvalues' rounding
@@ -172,53 +174,58 @@ __device__ __noinline__ void jacobi(Blk<NT>& B, Work& w, bool want_v) {
             aqq = aqq + t * apq;
           }
         }
-        rot[5 * k + 0] = c;
-        rot[5 * k + 1] = s;
-        rot[5 * k + 2] = t;
-        rot[5 * k + 3] = app;
-        rot[5 * k + 4] = aqq;
+        double* R = rot + ROT_FIELDS * k;
+        R[0] = c;
+        R[1] = s;
+        R[2] = t;
+        R[3] = app;
+        R[4] = aqq;
+        R[5] = (double)p;
+        R[6] = (double)q;
       }
       __syncthreads();
-      // columns p, q of A (and V): A <- A J
-      for (int e = tid; e < m * np; e += NT) {
-        const int k = e / m, i = e - k * m;
-        const double s = rot[5 * k + 1];
+      // columns p, q of A (and V): A <- A J; wave per pair, lane per row
+      for (int k = wv; k < np; k += NWV) {
+        const double* R = rot + ROT_FIELDS * k;
+        const double s = R[1];
         if (s == 0.0) continue;
-        int p, q;
-        pair_of(r, k, me, p, q);
-        const double c = rot[5 * k];
-        const double aip = A[i * lda + p], aiq = A[i * lda + q];
-        A[i * lda + p] = c * aip - s * aiq;
-        A[i * lda + q] = s * aip + c * aiq;
-        if (want_v) {
-          const double vip = V[i * lda + p], viq = V[i * lda + q];
-          V[i * lda + p] = c * vip - s * viq;
-          V[i * lda + q] = s * vip + c * viq;
+        const double c = R[0];
+        const int p = (int)R[5], q = (int)R[6];
+        for (int i = lane; i < m; i += 64) {
+          const double aip = A[i * lda + p], aiq = A[i * lda + q];
+          A[i * lda + p] = c * aip - s * aiq;
+          A[i * lda + q] = s * aip + c * aiq;
+          if (want_v) {
+            const double vip = V[i * lda + p], viq = V[i * lda + q];
+            V[i * lda + p] = c * vip - s * viq;
+            V[i * lda + q] = s * vip + c * viq;
+          }
         }
       }
       __syncthreads();
-      // rows p, q: A <- J^T A
-      for (int e = tid; e < m * np; e += NT) {
-        const int k = e / m, j = e - k * m;
-        const double s = rot[5 * k + 1];
+      // rows p, q: A <- J^T A; wave per pair, lane per column (contiguous)
+      for (int k = wv; k < np; k += NWV) {
+        const double* R = rot + ROT_FIELDS * k;
+        const double s = R[1];
         if (s == 0.0) continue;
-        int p, q;
-        pair_of(r, k, me, p, q);
-        const double c = rot[5 * k];
-        const double apj = A[p * lda + j], aqj = A[q * lda + j];
-        A[p * lda + j] = c * apj - s * aqj;
-        A[q * lda + j] = s * apj + c * aqj;
+        const double c = R[0];
+        const int p = (int)R[5], q = (int)R[6];
+        for (int j = lane; j < m; j += 64) {
+          const double apj = A[p * lda + j], aqj = A[q * lda + j];
+          A[p * lda + j] = c * apj - s * aqj;
+          A[q * lda + j] = s * apj + c * aqj;
+        }
       }
       __syncthreads();
       // the rotated 2 x 2 block exactly: a_pq = 0, a_pp / a_qq by the stable update
       for (int k = tid; k < np; k += NT) {
-        if (rot[5 * k + 1] == 0.0) continue;
-        int p, q;
-        pair_of(r, k, me, p, q);
+        const double* R = rot + ROT_FIELDS * k;
+        if (R[1] == 0.0) continue;
+        const int p = (int)R[5], q = (int)R[6];
         A[p * lda + q] = 0.0;
         A[q * lda + p] = 0.0;
-        A[p * lda + p] = rot[5 * k + 3];
-        A[q * lda + q] = rot[5 * k + 4];
+        A[p * lda + p] = R[3];
+        A[q * lda + q] = R[4];
       }
       __syncthreads();
     }
