@@ -1029,58 +1029,81 @@ struct MachineT {
   // reductions (element i = tid + k * ST_THREADS, k < RT_EPT): one load phase, one store phase.
   static constexpr int RT_EPT = 8;
 
-  __device__ __forceinline__ void load_reg(int kind, double (&r)[RT_EPT]) const {
+  template <int K>
+  __device__ __forceinline__ void load_reg(int kind, double (&r)[K]) const {
     const double* a = V(kind);
 #pragma unroll
-    for (int k = 0; k < RT_EPT; ++k) {
+    for (int k = 0; k < K; ++k) {
       const int i = tid + k * ST_THREADS;
       r[k] = i < n ? a[i] : 0.0;
     }
   }
-  __device__ __forceinline__ void store_reg(int kind, const double (&r)[RT_EPT]) const {
+  template <int K>
+  __device__ __forceinline__ void store_reg(int kind, const double (&r)[K]) const {
     double* a = V(kind);
 #pragma unroll
-    for (int k = 0; k < RT_EPT; ++k) {
+    for (int k = 0; k < K; ++k) {
       const int i = tid + k * ST_THREADS;
       if (i < n) a[i] = r[k];
     }
   }
-  // S delta of the last S-pass into registers (the layouts' partial sums, in gather_out's order)
-  __device__ __forceinline__ void gather_reg(double (&u)[RT_EPT]) {
+  // S delta of the last S-pass into registers (the layouts' partial sums, in gather_out's order).
+  // K <= 2 (n <= 1024, nt <= 8): every partial of the element issued at once — one memory round
+  // trip instead of one per tile column (the partials come from S-pass workgroups on every XCD,
+  // so they are L2 misses).
+  template <int K>
+  __device__ __forceinline__ void gather_reg(double (&u)[K]) {
     if (P.layout == RIPTRM_LAYOUT_SYMTILE) {
       const int nt = P.nt;
       const int64_t nn = (int64_t)nt * nt * TS;
       const double* pb = P.pbuf + (int64_t)b * nn;
-      const double* q[RT_EPT];
+      const double* q[K];
 #pragma unroll
-      for (int e = 0; e < RT_EPT; ++e) {
+      for (int e = 0; e < K; ++e) {
         int i = tid + e * ST_THREADS;
         i = i < n ? i : n - 1;
         const int I = i / TS, c = i - I * TS;
         q[e] = pb + (int64_t)I * nt * TS + c;
-        u[e] = q[e][0];
       }
-      constexpr int GJ = 2;
-      for (int J = 1; J < nt; J += GJ) {
-        double t[RT_EPT][GJ];
+      if constexpr (K <= 2) {
+        constexpr int NTS = 8;
+        double t[K][NTS];
 #pragma unroll
-        for (int e = 0; e < RT_EPT; ++e)
+        for (int e = 0; e < K; ++e)
 #pragma unroll
-          for (int v = 0; v < GJ; ++v) t[e][v] = (J + v < nt) ? q[e][(int64_t)(J + v) * TS] : 0.0;
+          for (int J = 0; J < NTS; ++J) t[e][J] = (J < nt) ? q[e][(int64_t)J * TS] : 0.0;
 #pragma unroll
-        for (int e = 0; e < RT_EPT; ++e)
+        for (int e = 0; e < K; ++e) {
+          u[e] = t[e][0];
 #pragma unroll
-          for (int v = 0; v < GJ; ++v)
-            if (J + v < nt) u[e] += t[e][v];
+          for (int J = 1; J < NTS; ++J)
+            if (J < nt) u[e] += t[e][J];
+        }
+      } else {
+#pragma unroll
+        for (int e = 0; e < K; ++e) u[e] = q[e][0];
+        constexpr int GJ = 2;
+        for (int J = 1; J < nt; J += GJ) {
+          double t[K][GJ];
+#pragma unroll
+          for (int e = 0; e < K; ++e)
+#pragma unroll
+            for (int v = 0; v < GJ; ++v) t[e][v] = (J + v < nt) ? q[e][(int64_t)(J + v) * TS] : 0.0;
+#pragma unroll
+          for (int e = 0; e < K; ++e)
+#pragma unroll
+            for (int v = 0; v < GJ; ++v)
+              if (J + v < nt) u[e] += t[e][v];
+        }
       }
 #pragma unroll
-      for (int e = 0; e < RT_EPT; ++e)
+      for (int e = 0; e < K; ++e)
         if (tid + e * ST_THREADS >= n) u[e] = 0.0;
     } else if (P.layout == RIPTRM_LAYOUT_SHARED) {
       const int64_t ld = P.ld, slab = (int64_t)P.batch * ld;
       const double* pb = P.pbuf + (int64_t)b * ld;
 #pragma unroll
-      for (int e = 0; e < RT_EPT; ++e) {
+      for (int e = 0; e < K; ++e) {
         const int i = tid + e * ST_THREADS;
         double acc = 0.0;
         if (i < n) {
@@ -1091,17 +1114,22 @@ struct MachineT {
         u[e] = acc;
       }
     } else {
-      load_reg(V_OUT0, u);
+      load_reg<K>(V_OUT0, u);
     }
   }
 
+  template <int K>
   __device__ __forceinline__ int tcg_step_reg() {
-    constexpr int K = RT_EPT;
-    double u[K], d[K], x[K], y[K];
-    gather_reg(u);
-    load_reg(V_IN0, d);
-    load_reg(V_X, x);
-    load_reg(V_Y, y);
+    // every operand of the iteration is loaded up front (independent loads, one round trip)
+    double u[K], d[K], x[K], y[K], c[K], e[K], he[K], rv[K];
+    gather_reg<K>(u);
+    load_reg<K>(V_IN0, d);
+    load_reg<K>(V_X, x);
+    load_reg<K>(V_Y, y);
+    load_reg<K>(V_C, c);
+    load_reg<K>(V_ETA, e);
+    load_reg<K>(V_HETA, he);
+    load_reg<K>(V_R, rv);
     // hw_apply(U, D, U)
     double r1[2] = {0.0, 0.0};
 #pragma unroll
@@ -1128,10 +1156,6 @@ struct MachineT {
       const double hf = -u[k] + xu * x[k];
       u[k] = (hf + coef * d[k]) + (q - xq * x[k]);
     }
-    double c[K], e[K], he[K];
-    load_reg(V_C, c);
-    load_reg(V_ETA, e);
-    load_reg(V_HETA, he);
     double d1[1] = {0.0};
 #pragma unroll
     for (int k = 0; k < K; ++k) d1[0] += d[k] * u[k];
@@ -1175,8 +1199,6 @@ struct MachineT {
       return tcg_end();
     }
     s[ST_MODEL] = new_model;
-    double rv[K];
-    load_reg(V_R, rv);
     double r2b[1] = {0.0};
 #pragma unroll
     for (int k = 0; k < K; ++k) {
@@ -1641,7 +1663,9 @@ __global__ void __launch_bounds__(ST_THREADS) k_state(DevParams P, int full, int
   const int ph = (int)M.s[ST_PHASE];
   if (ph == PH_DONE || ph == PH_IDLE || ph == PH_ERROR) return;
   if (!full && ph == PH_TCG && P.n <= Machine::RT_EPT * ST_THREADS) {
-    M.tcg_step_reg();   // gathers S delta itself, vectors register-resident
+    // gathers S delta itself, vectors register-resident (2 elements per thread up to n = 1024)
+    if (P.n <= 2 * ST_THREADS) M.template tcg_step_reg<2>();
+    else M.template tcg_step_reg<Machine::RT_EPT>();
   } else {
     if (!full && P.layout == RIPTRM_LAYOUT_SYMTILE) M.gather_out(P.req[b]);
     if (!full && P.layout == RIPTRM_LAYOUT_SHARED) M.gather_slices(P.req[b]);
