@@ -31,6 +31,14 @@ __device__ __forceinline__ double* vp(const DevParams& P, int k, int b) {
   return P.vec + ((int64_t)k * P.batch + b) * P.ld;
 }
 
+// An active-list entry carries the instance and its right-hand-side count (1 or 2), so a consumer
+// learns both from ONE load, issued together with the list-count load (slot < grid bound <= batch
+// keeps the read in bounds): one dependent memory round trip less at the head of every S-pass and
+// state-kernel workgroup.
+__device__ __forceinline__ int32_t le_make(int b, int nrhs) { return b * 2 + (nrhs - 1); }
+__device__ __forceinline__ int le_b(int32_t e) { return e >> 1; }
+__device__ __forceinline__ int le_nrhs(int32_t e) { return (e & 1) + 1; }
+
 // ------------------------------------------------------------------------------------------
 // Workgroup reductions (ST_THREADS threads).  Every thread ends with the bitwise-identical
 // result, so all scalar control flow downstream is uniform across the workgroup.
@@ -185,12 +193,13 @@ __device__ __forceinline__ void gemv_rows(const DevParams& P, int b, int rb) {
 // state kernel that follows.
 __global__ void __launch_bounds__(GV_THREADS) k_gemv(DevParams P, int list_in, int zero_cnt) {
   if (zero_cnt >= 0 && blockIdx.x == 0 && threadIdx.x == 0) P.cnt[zero_cnt] = 0;
-  const int nact = P.cnt[list_in];
   const int slot = blockIdx.x / P.nrb;
+  const int nact = P.cnt[list_in];
+  const int32_t e = P.lists[list_in * P.batch + slot];
   if (slot >= nact) return;
-  const int b = P.lists[list_in * P.batch + slot];
+  const int b = le_b(e);
   const int rb = blockIdx.x - slot * P.nrb;
-  if (P.req[b] == 2) gemv_rows<2>(P, b, rb);
+  if (le_nrhs(e) == 2) gemv_rows<2>(P, b, rb);
   else gemv_rows<1>(P, b, rb);
 }
 
@@ -334,12 +343,13 @@ __device__ __forceinline__ void spass_tile(const DevParams& P, int b, int t) {
 
 __global__ void __launch_bounds__(SP_THREADS, 4) k_spass_sym(DevParams P, int list_in, int zero_cnt) {
   if (zero_cnt >= 0 && blockIdx.x == 0 && threadIdx.x == 0) P.cnt[zero_cnt] = 0;
-  const int nact = P.cnt[list_in];
   const int slot = blockIdx.x / P.ntiles;
+  const int nact = P.cnt[list_in];
+  const int32_t e = P.lists[list_in * P.batch + slot];
   if (slot >= nact) return;
-  const int b = P.lists[list_in * P.batch + slot];
+  const int b = le_b(e);
   const int t = blockIdx.x - slot * P.ntiles;
-  if (P.req[b] == 2) spass_tile<2>(P, b, t);
+  if (le_nrhs(e) == 2) spass_tile<2>(P, b, t);
   else spass_tile<1>(P, b, t);
 }
 
@@ -376,7 +386,7 @@ __global__ void __launch_bounds__(64 * KS) k_spass_mm(DevParams P, int list_in, 
     __syncthreads();
     if (threadIdx.x < CT) {
       const int sl = s0 + threadIdx.x;
-      if (sl < nact && P.req[P.lists[list_in * P.batch + sl]] == 2) any2 = 1;
+      if (sl < nact && le_nrhs(P.lists[list_in * P.batch + sl]) == 2) any2 = 1;
     }
     __syncthreads();
     if (!any2) return;
@@ -391,7 +401,7 @@ __global__ void __launch_bounds__(64 * KS) k_spass_mm(DevParams P, int list_in, 
   for (int a = 0; a < WM; ++a) {
     int sl = s0 + 16 * a + r;
     sl = sl < nact ? sl : nact - 1;
-    ap[a] = vp(P, vk, P.lists[list_in * P.batch + sl]) + 8 * q;
+    ap[a] = vp(P, vk, le_b(P.lists[list_in * P.batch + sl])) + 8 * q;
   }
 #pragma unroll
   for (int c = 0; c < WN; ++c) {
@@ -452,8 +462,9 @@ __global__ void __launch_bounds__(64 * KS) k_spass_mm(DevParams P, int list_in, 
     for (int g = 0; g < 4; ++g) {
       const int sl = s0 + 16 * a + q + 4 * g;
       if (sl >= nact) continue;
-      const int bb = P.lists[list_in * P.batch + sl];
-      if (which && P.req[bb] != 2) continue;
+      const int32_t eb = P.lists[list_in * P.batch + sl];
+      const int bb = le_b(eb);
+      if (which && le_nrhs(eb) != 2) continue;
 #pragma unroll
       for (int c = 0; c < WN; ++c) {
         const int i = i0 + 16 * c + r;
@@ -631,7 +642,7 @@ struct MachineT {
     if (tid == 0) {
       P.req[b] = nrhs;
       const int slot = atomicAdd(&P.cnt[out_list], 1);
-      P.lists[out_list * P.batch + slot] = b;
+      P.lists[out_list * P.batch + slot] = le_make(b, nrhs);
     }
     cadd(ST_PASSES, 1.0);
     return ACT_YIELD;
@@ -1656,8 +1667,10 @@ __global__ void __launch_bounds__(ST_THREADS) k_state(DevParams P, int full, int
                            (ph == PH_PAUSED && (double)P.outer_target > g[ST_OUTER_IT]);
     if (!startable) return;
   } else {
-    if ((int)blockIdx.x >= P.cnt[list_in]) return;
-    b = P.lists[list_in * P.batch + blockIdx.x];
+    const int nact = P.cnt[list_in];
+    const int32_t e = P.lists[list_in * P.batch + blockIdx.x];
+    if ((int)blockIdx.x >= nact) return;
+    b = le_b(e);
   }
   MachineT<EXACT> M(P, b, list_out, redbuf, trs_lds);
   const int ph = (int)M.s[ST_PHASE];
@@ -1722,7 +1735,7 @@ __global__ void __launch_bounds__(256) k_hvp_prep(DevParams P, const double* x, 
   }
   if (threadIdx.x == 0) {
     P.req[b] = 2;
-    P.lists[b] = b;
+    P.lists[b] = le_make(b, 2);
     if (b == 0) P.cnt[0] = P.batch;
   }
 }
