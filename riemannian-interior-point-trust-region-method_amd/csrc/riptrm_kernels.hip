@@ -530,6 +530,118 @@ __global__ void __launch_bounds__(256) k_pack(const double* Z, int64_t ldz, int6
 // call would recurse through the inner loop whenever trial points are infeasible)
 enum Act : int { ACT_YIELD = 0, ACT_DONE = 1, ACT_PAUSE = 2, ACT_CONTINUE = 3 };
 
+// ---- register-path operand loads (free functions: k_state prefetches them before the machine's
+// scalars arrive) --------------------------------------------------------------------------------
+template <int K>
+__device__ __forceinline__ void rl_load(const DevParams& P, int b, int kind, double (&r)[K]) {
+  const int tid = threadIdx.x, n = P.n;
+  const double* a = vp(P, kind, b);
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const int i = tid + k * ST_THREADS;
+    r[k] = i < n ? a[i] : 0.0;
+  }
+}
+template <int K>
+__device__ __forceinline__ void rl_store(const DevParams& P, int b, int kind, const double (&r)[K]) {
+  const int tid = threadIdx.x, n = P.n;
+  double* a = vp(P, kind, b);
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const int i = tid + k * ST_THREADS;
+    if (i < n) a[i] = r[k];
+  }
+}
+// S delta of the last S-pass into registers (the layouts' partial sums, in gather_out's order).
+// K <= 2 (n <= 1024, nt <= 8): every partial of the element issued at once — one memory round
+// trip instead of one per tile column (the partials come from S-pass workgroups on every XCD,
+// so they are L2 misses).
+template <int K>
+__device__ __forceinline__ void rl_gather(const DevParams& P, int b, double (&u)[K]) {
+  const int tid = threadIdx.x, n = P.n;
+  if (P.layout == RIPTRM_LAYOUT_SYMTILE) {
+    const int nt = P.nt;
+    const int64_t nn = (int64_t)nt * nt * TS;
+    const double* pb = P.pbuf + (int64_t)b * nn;
+    const double* q[K];
+#pragma unroll
+    for (int e = 0; e < K; ++e) {
+      int i = tid + e * ST_THREADS;
+      i = i < n ? i : n - 1;
+      const int I = i / TS, c = i - I * TS;
+      q[e] = pb + (int64_t)I * nt * TS + c;
+    }
+    if constexpr (K <= 2) {
+      constexpr int NTS = 8;
+      double t[K][NTS];
+#pragma unroll
+      for (int e = 0; e < K; ++e)
+#pragma unroll
+        for (int J = 0; J < NTS; ++J) t[e][J] = (J < nt) ? q[e][(int64_t)J * TS] : 0.0;
+#pragma unroll
+      for (int e = 0; e < K; ++e) {
+        u[e] = t[e][0];
+#pragma unroll
+        for (int J = 1; J < NTS; ++J)
+          if (J < nt) u[e] += t[e][J];
+      }
+    } else {
+#pragma unroll
+      for (int e = 0; e < K; ++e) u[e] = q[e][0];
+      constexpr int GJ = 2;
+      for (int J = 1; J < nt; J += GJ) {
+        double t[K][GJ];
+#pragma unroll
+        for (int e = 0; e < K; ++e)
+#pragma unroll
+          for (int v = 0; v < GJ; ++v) t[e][v] = (J + v < nt) ? q[e][(int64_t)(J + v) * TS] : 0.0;
+#pragma unroll
+        for (int e = 0; e < K; ++e)
+#pragma unroll
+          for (int v = 0; v < GJ; ++v)
+            if (J + v < nt) u[e] += t[e][v];
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < K; ++e)
+      if (tid + e * ST_THREADS >= n) u[e] = 0.0;
+  } else if (P.layout == RIPTRM_LAYOUT_SHARED) {
+    const int64_t ld = P.ld, slab = (int64_t)P.batch * ld;
+    const double* pb = P.pbuf + (int64_t)b * ld;
+#pragma unroll
+    for (int e = 0; e < K; ++e) {
+      const int i = tid + e * ST_THREADS;
+      double acc = 0.0;
+      if (i < n) {
+        acc = pb[i];
+#pragma unroll
+        for (int z = 1; z < MM_KZ; ++z) acc += pb[(int64_t)z * 2 * slab + i];
+      }
+      u[e] = acc;
+    }
+  } else {
+    rl_load<K>(P, b, V_OUT0, u);
+  }
+}
+
+
+// every operand of one register-path tCG iteration (independent loads, one round trip)
+template <int K>
+struct TcgOps {
+  double u[K], d[K], x[K], y[K], c[K], e[K], he[K], rv[K];
+};
+template <int K>
+__device__ __forceinline__ void load_tcg_ops(const DevParams& P, int b, TcgOps<K>& o) {
+  rl_gather<K>(P, b, o.u);
+  rl_load<K>(P, b, V_IN0, o.d);
+  rl_load<K>(P, b, V_X, o.x);
+  rl_load<K>(P, b, V_Y, o.y);
+  rl_load<K>(P, b, V_C, o.c);
+  rl_load<K>(P, b, V_ETA, o.e);
+  rl_load<K>(P, b, V_HETA, o.he);
+  rl_load<K>(P, b, V_R, o.rv);
+}
+
 // EXACT = false: the tCG machine (every shipped config); EXACT = true adds the Exact_RepMat
 // branches (a separate k_state instantiation, so the tCG kernel carries none of its code or
 // register / scratch pressure).
@@ -1041,106 +1153,27 @@ struct MachineT {
   static constexpr int RT_EPT = 8;
 
   template <int K>
-  __device__ __forceinline__ void load_reg(int kind, double (&r)[K]) const {
-    const double* a = V(kind);
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-      const int i = tid + k * ST_THREADS;
-      r[k] = i < n ? a[i] : 0.0;
-    }
-  }
+  __device__ __forceinline__ void load_reg(int kind, double (&r)[K]) const { rl_load<K>(P, b, kind, r); }
   template <int K>
-  __device__ __forceinline__ void store_reg(int kind, const double (&r)[K]) const {
-    double* a = V(kind);
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-      const int i = tid + k * ST_THREADS;
-      if (i < n) a[i] = r[k];
-    }
-  }
-  // S delta of the last S-pass into registers (the layouts' partial sums, in gather_out's order).
-  // K <= 2 (n <= 1024, nt <= 8): every partial of the element issued at once — one memory round
-  // trip instead of one per tile column (the partials come from S-pass workgroups on every XCD,
-  // so they are L2 misses).
+  __device__ __forceinline__ void store_reg(int kind, const double (&r)[K]) const { rl_store<K>(P, b, kind, r); }
   template <int K>
-  __device__ __forceinline__ void gather_reg(double (&u)[K]) {
-    if (P.layout == RIPTRM_LAYOUT_SYMTILE) {
-      const int nt = P.nt;
-      const int64_t nn = (int64_t)nt * nt * TS;
-      const double* pb = P.pbuf + (int64_t)b * nn;
-      const double* q[K];
-#pragma unroll
-      for (int e = 0; e < K; ++e) {
-        int i = tid + e * ST_THREADS;
-        i = i < n ? i : n - 1;
-        const int I = i / TS, c = i - I * TS;
-        q[e] = pb + (int64_t)I * nt * TS + c;
-      }
-      if constexpr (K <= 2) {
-        constexpr int NTS = 8;
-        double t[K][NTS];
-#pragma unroll
-        for (int e = 0; e < K; ++e)
-#pragma unroll
-          for (int J = 0; J < NTS; ++J) t[e][J] = (J < nt) ? q[e][(int64_t)J * TS] : 0.0;
-#pragma unroll
-        for (int e = 0; e < K; ++e) {
-          u[e] = t[e][0];
-#pragma unroll
-          for (int J = 1; J < NTS; ++J)
-            if (J < nt) u[e] += t[e][J];
-        }
-      } else {
-#pragma unroll
-        for (int e = 0; e < K; ++e) u[e] = q[e][0];
-        constexpr int GJ = 2;
-        for (int J = 1; J < nt; J += GJ) {
-          double t[K][GJ];
-#pragma unroll
-          for (int e = 0; e < K; ++e)
-#pragma unroll
-            for (int v = 0; v < GJ; ++v) t[e][v] = (J + v < nt) ? q[e][(int64_t)(J + v) * TS] : 0.0;
-#pragma unroll
-          for (int e = 0; e < K; ++e)
-#pragma unroll
-            for (int v = 0; v < GJ; ++v)
-              if (J + v < nt) u[e] += t[e][v];
-        }
-      }
-#pragma unroll
-      for (int e = 0; e < K; ++e)
-        if (tid + e * ST_THREADS >= n) u[e] = 0.0;
-    } else if (P.layout == RIPTRM_LAYOUT_SHARED) {
-      const int64_t ld = P.ld, slab = (int64_t)P.batch * ld;
-      const double* pb = P.pbuf + (int64_t)b * ld;
-#pragma unroll
-      for (int e = 0; e < K; ++e) {
-        const int i = tid + e * ST_THREADS;
-        double acc = 0.0;
-        if (i < n) {
-          acc = pb[i];
-#pragma unroll
-          for (int z = 1; z < MM_KZ; ++z) acc += pb[(int64_t)z * 2 * slab + i];
-        }
-        u[e] = acc;
-      }
-    } else {
-      load_reg<K>(V_OUT0, u);
-    }
-  }
+  __device__ __forceinline__ void gather_reg(double (&u)[K]) { rl_gather<K>(P, b, u); }
 
   template <int K>
   __device__ __forceinline__ int tcg_step_reg() {
-    // every operand of the iteration is loaded up front (independent loads, one round trip)
+    // K <= 2 (n <= 1024): every operand loaded up front, one memory round trip (few registers);
+    // K = 8: c / e / he / rv loaded where first needed, so fewer vectors are live at once
     double u[K], d[K], x[K], y[K], c[K], e[K], he[K], rv[K];
     gather_reg<K>(u);
     load_reg<K>(V_IN0, d);
     load_reg<K>(V_X, x);
     load_reg<K>(V_Y, y);
-    load_reg<K>(V_C, c);
-    load_reg<K>(V_ETA, e);
-    load_reg<K>(V_HETA, he);
-    load_reg<K>(V_R, rv);
+    if constexpr (K <= 2) {
+      load_reg<K>(V_C, c);
+      load_reg<K>(V_ETA, e);
+      load_reg<K>(V_HETA, he);
+      load_reg<K>(V_R, rv);
+    }
     // hw_apply(U, D, U)
     double r1[2] = {0.0, 0.0};
 #pragma unroll
@@ -1166,6 +1199,11 @@ struct MachineT {
       const double q = ok ? (y[k] * (d[k] - x[k] * xv)) / x[k] : 0.0;
       const double hf = -u[k] + xu * x[k];
       u[k] = (hf + coef * d[k]) + (q - xq * x[k]);
+    }
+    if constexpr (K > 2) {
+      load_reg<K>(V_C, c);
+      load_reg<K>(V_ETA, e);
+      load_reg<K>(V_HETA, he);
     }
     double d1[1] = {0.0};
 #pragma unroll
@@ -1210,6 +1248,7 @@ struct MachineT {
       return tcg_end();
     }
     s[ST_MODEL] = new_model;
+    if constexpr (K > 2) load_reg<K>(V_R, rv);
     double r2b[1] = {0.0};
 #pragma unroll
     for (int k = 0; k < K; ++k) {
@@ -1656,7 +1695,10 @@ __global__ void __launch_bounds__(ST_THREADS) k_state(DevParams P, int full, int
   __shared__ double redbuf[2 * ST_WAVES * RED_MAX];
   extern __shared__ double trs_lds[];   // Exact_RepMat only (dynamic size 0 otherwise)
   int b;
-  if (full) {
+  // full = 1: (re)start launch; full = 2: direct lock-step launch, workgroup k = instance
+  // full_base + k, active iff it waits for the S-pass that just ran (its phase says so: every
+  // instance in that state was queued by request()); full = 0: workgroup k = lists[list_in][k]
+  if (full == 1) {
     if ((int)blockIdx.x >= full_count) return;
     b = full_base + blockIdx.x;
     if (b >= P.batch) return;
@@ -1666,6 +1708,10 @@ __global__ void __launch_bounds__(ST_THREADS) k_state(DevParams P, int full, int
     const bool startable = ph == PH_START || ph == PH_TCGO_START ||
                            (ph == PH_PAUSED && (double)P.outer_target > g[ST_OUTER_IT]);
     if (!startable) return;
+  } else if (full == 2) {
+    if ((int)blockIdx.x >= full_count) return;
+    b = full_base + blockIdx.x;
+    if (b >= P.batch) return;
   } else {
     const int nact = P.cnt[list_in];
     const int32_t e = P.lists[list_in * P.batch + blockIdx.x];
@@ -1675,13 +1721,14 @@ __global__ void __launch_bounds__(ST_THREADS) k_state(DevParams P, int full, int
   MachineT<EXACT> M(P, b, list_out, redbuf, trs_lds);
   const int ph = (int)M.s[ST_PHASE];
   if (ph == PH_DONE || ph == PH_IDLE || ph == PH_ERROR) return;
-  if (!full && ph == PH_TCG && P.n <= Machine::RT_EPT * ST_THREADS) {
+  if (full == 2 && !(ph == PH_TCG || ph == PH_TRIAL || ph == PH_AFTER_SX0 || ph == PH_TCGO_SX)) return;
+  if (full != 1 && ph == PH_TCG && P.n <= Machine::RT_EPT * ST_THREADS) {
     // gathers S delta itself, vectors register-resident (2 elements per thread up to n = 1024)
     if (P.n <= 2 * ST_THREADS) M.template tcg_step_reg<2>();
     else M.template tcg_step_reg<Machine::RT_EPT>();
   } else {
-    if (!full && P.layout == RIPTRM_LAYOUT_SYMTILE) M.gather_out(P.req[b]);
-    if (!full && P.layout == RIPTRM_LAYOUT_SHARED) M.gather_slices(P.req[b]);
+    if (full != 1 && P.layout == RIPTRM_LAYOUT_SYMTILE) M.gather_out(P.req[b]);
+    if (full != 1 && P.layout == RIPTRM_LAYOUT_SHARED) M.gather_slices(P.req[b]);
     if constexpr (EXACT) {
       while (M.dispatch() == ACT_CONTINUE) {
       }
@@ -2119,7 +2166,7 @@ static int capture_graph(riptrm_ctx* c, int bound) {
   for (int s = 0; s < GRAPH_STEPS && rc == RIPTRM_OK; ++s) {
     const int lin = par, lout = par ^ 1;
     rc = launch_gemv(c, st, lin, lout, bound);
-    if (rc == RIPTRM_OK) rc = launch_state(c, st, 0, lin, lout, bound);
+    if (rc == RIPTRM_OK) rc = launch_state(c, st, 2, lin, lout, c->gsize[0], c->gbase[0]);
     par ^= 1;
   }
   hipGraph_t g = nullptr;
@@ -2175,7 +2222,7 @@ static int run_steps(riptrm_ctx* c, int steps, int* n_active) {
       rc = launch_gemv(c, st, lin, lout, c->active_bound[g]);
       if (rc) return rc;
       if (G == 2) HIPCHK(c, hipEventRecord(c->ev_pass[g], st));
-      rc = launch_state(c, st, 0, lin, lout, c->active_bound[g]);
+      rc = launch_state(c, st, 2, lin, lout, c->gsize[g], c->gbase[g]);
       if (rc) return rc;
       c->parity[g] ^= 1;
     }
