@@ -1321,15 +1321,17 @@ struct MachineT {
     return Sb[(int64_t)i * P.ld + j];
   }
   // LDS: [Work of dim n-1][w: n][u: n][Blk scratch]
-  __device__ __forceinline__ double* trs_wvec() const { return tl + riptrm_trs::work_doubles(n - 1); }
-  __device__ __forceinline__ double* trs_uvec() const { return trs_wvec() + riptrm_trs::DIM_MAX + 1; }
-  __device__ __forceinline__ double* trs_red() const { return trs_uvec() + riptrm_trs::DIM_MAX + 1; }
+  __device__ __forceinline__ riptrm_trs::lds_f64* trs_wvec() const {
+    return (riptrm_trs::lds_f64*)tl + riptrm_trs::work_doubles(n - 1);
+  }
+  __device__ __forceinline__ riptrm_trs::lds_f64* trs_uvec() const { return trs_wvec() + riptrm_trs::DIM_MAX + 1; }
+  __device__ __forceinline__ double* trs_red() const { return (double*)(trs_uvec() + riptrm_trs::DIM_MAX + 1); }
 
   // A <- (H M H)[1:, 1:] + coef I at (X, Y); returns tau (w in trs_wvec)
   __device__ __noinline__ double repmat(riptrm_trs::Blk<ST_THREADS>& B, riptrm_trs::Work& w, const double* X,
                                            const double* Y, double xx, double coef) {
-    double* Wv = trs_wvec();
-    double* Uv = trs_uvec();
+    riptrm_trs::lds_f64* Wv = trs_wvec();
+    riptrm_trs::lds_f64* Uv = trs_uvec();
     const double sg = X[0] >= 0.0 ? 1.0 : -1.0;
     double ww = 0.0;
     for (int i = tid; i < n; i += ST_THREADS) {
@@ -1373,7 +1375,7 @@ struct MachineT {
     const double* Y = V(V_Y);
     const double* Cv = V(V_C);
     const double tau = repmat(B, w, X, Y, s[ST_XX], s[ST_COEF]);
-    const double* Wv = trs_wvec();
+    const riptrm_trs::lds_f64* Wv = trs_wvec();
     double wc = 0.0;   // cxCurvector_k = <c, b_k> = (H c)_k (RIPTRM.py:438-440)
     for (int i = tid; i < n; i += ST_THREADS) wc += Wv[i] * Cv[i];
     wc = B.sum(wc);

@@ -758,17 +758,17 @@ struct Eng {
     for (int j = 0; j < DIMM; ++j) {
       for (int k = l; k < DIMM; k += W) w.p[k] = (k == j) ? 1.0 : 0.0;
       __syncthreads();
-      const PV bj = from_coords(F, w.p);
+      const PV bj = from_coords(F, (const double*)w.p);
       const PV h = hw(a, bj);
       hvps += 1.0;
-      to_coords(F, h, w.q);
+      to_coords(F, h, (double*)w.q);
       for (int k = l; k <= j; k += W) {
         w.A[k * w.lda + j] = w.q[k];
         w.A[j * w.lda + k] = w.q[k];
       }
       __syncthreads();
     }
-    to_coords(F, a.c, w.a);
+    to_coords(F, a.c, (double*)w.a);
     return w;
   }
   // compute_direction's Exact_RepMat branch: returns the RIPTRM_TRS_* type
@@ -777,7 +777,7 @@ struct Eng {
     riptrm_trs::Work w = repmat(a, F, hvps);
     riptrm_trs::Blk<W> B(nullptr);
     const riptrm_trs::Result r = riptrm_trs::trs_solve<W>(B, w, Delta, P.opt.trs_tolhardcase);
-    eta = from_coords(F, w.x);
+    eta = from_coords(F, (const double*)w.x);
     return RIPTRM_TRS_BOUNDARY + r.kind;
   }
   // smallest eigenvalue of HwNew's matrix at (xN, yN, mu) (RIPTRM.py:599-613)

@@ -33,7 +33,17 @@ namespace riptrm_trs {
 
 #pragma clang fp contract(off)
 
-constexpr int DIM_MAX = 96;   // LDS: 2 * 96 * 97 doubles = 146 KiB (matrix + eigenvectors)
+#ifdef RIPTRM_TRS_PROBE
+__device__ double g_probe[96];   // tools/trs_probe.hip only: per-sweep off / diag norms
+#endif
+
+constexpr int DIM_MAX = 96;
+
+// Everything below lives in LDS and is reached through these address-space-3 pointers, so the
+// (noinline) solver bodies compile to ds_read / ds_write — through generic pointers they became
+// flat loads/stores at several times the latency (measured: 5.7k cycles per Jacobi column stage
+// at dim 16).
+typedef __attribute__((address_space(3))) double lds_f64;   // LDS: 2 * 96 * 97 doubles = 146 KiB (matrix + eigenvectors)
 
 enum Kind : int { K_BOUNDARY = 0, K_INTERIOR = 1, K_HARDCASE_1 = 2 };
 
@@ -48,29 +58,30 @@ __host__ __device__ constexpr int work_doubles(int dim) {
 }
 
 struct Work {
-  double* A;    // dim x lda  (destroyed: eigenvalues end on the diagonal)
-  double* V;    // dim x lda  eigenvectors (columns)
-  double* a;    // dim   linear term
-  double* x;    // dim   solution
-  double* p;    // dim   CG direction / scratch
-  double* r;    // dim   CG residual / scratch
-  double* q;    // dim   CG A p / scratch
-  double* cgx;  // dim   CG iterate (the interior candidate p1)
-  double* g;    // dim   Q^T a
-  double* ev;   // dim   eigenvalues (copied off the diagonal)
-  double* rot;  // ROT_FIELDS x (DIM_MAX/2 + 1)  (c, s, t, a_pp, a_qq, p, q) per pair
+  lds_f64* A;    // dim x lda  (destroyed: eigenvalues end on the diagonal)
+  lds_f64* V;    // dim x lda  eigenvectors (columns)
+  lds_f64* a;    // dim   linear term
+  lds_f64* x;    // dim   solution
+  lds_f64* p;    // dim   CG direction / scratch
+  lds_f64* r;    // dim   CG residual / scratch
+  lds_f64* q;    // dim   CG A p / scratch
+  lds_f64* cgx;  // dim   CG iterate (the interior candidate p1)
+  lds_f64* g;    // dim   Q^T a
+  lds_f64* ev;   // dim   eigenvalues (copied off the diagonal)
+  lds_f64* rot;  // ROT_FIELDS x (DIM_MAX/2 + 1)  (c, s, t, a_pp, a_qq, p, q) per pair
   int dim, lda;
 };
 
 // carve a Work out of an LDS area of work_doubles(dim) doubles
-__device__ __forceinline__ Work make_work(double* base, int dim) {
+__device__ __forceinline__ Work make_work(double* base_generic, int dim) {
+  lds_f64* base = (lds_f64*)base_generic;
   Work w;
   w.dim = dim;
   w.lda = lda_of(dim);
   const int mat = dim * w.lda;
   w.A = base;
   w.V = base + mat;
-  double* v = base + 2 * mat;
+  lds_f64* v = base + 2 * mat;
   w.a = v;
   w.x = v + DIM_MAX;
   w.p = v + 2 * DIM_MAX;
@@ -88,16 +99,16 @@ __device__ __forceinline__ Work make_work(double* base, int dim) {
 template <int NT>
 struct Blk {
   static constexpr int NW = NT / 64;
-  double* red;  // LDS, 2 * NW doubles (unused when NW == 1)
+  lds_f64* red;  // LDS, 2 * NW doubles (unused when NW == 1)
   int par;
-  __device__ __forceinline__ explicit Blk(double* red_) : red(red_), par(0) {}
+  __device__ __forceinline__ explicit Blk(double* red_) : red((lds_f64*)red_), par(0) {}
   template <int OP>
   __device__ __forceinline__ double reduce(double v) {
     v = riptrm_wave::wave_reduce<OP>(v);
     if constexpr (NW == 1) {
       return v;
     } else {
-      double* b = red + par * NW;
+      lds_f64* b = red + par * NW;
       par ^= 1;
       if ((threadIdx.x & 63) == 0) b[threadIdx.x >> 6] = v;
       __syncthreads();
@@ -131,13 +142,14 @@ __device__ __forceinline__ void pair_of(int r, int k, int me, int& p, int& q) {
 // eigenvalues (diagonal order) and, if want_v, w.V the eigenvectors as columns (A0 = V diag V^T).
 // Rotation formulas: Numerical Recipes' (same as the serial jacobi_reg of riptrm_si.hip).
 template <int NT>
-__device__ __noinline__ void jacobi(Blk<NT>& B, Work& w, bool want_v) {
+__device__ __forceinline__ void jacobi(Blk<NT>& B, Work& w, bool want_v) {
   constexpr int NWV = NT / 64;
+  constexpr int CH = 4;   // pairs per wave per load/store batch
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int m = w.dim, lda = w.lda;
-  double* A = w.A;
-  double* V = w.V;
-  double* rot = w.rot;
+  lds_f64* A = w.A;
+  lds_f64* V = w.V;
+  lds_f64* rot = w.rot;
   // rows are walked by waves and columns by lanes: no integer division on the hot loops
   if (want_v)
     for (int i = wv; i < m; i += NWV)
@@ -155,8 +167,14 @@ __device__ __noinline__ void jacobi(Blk<NT>& B, Work& w, bool want_v) {
       }
     off = B.sum(off);
     dg = B.sum(dg);
+#ifdef RIPTRM_TRS_PROBE
+    if (tid == 0 && sweep < 40) { g_probe[2 * sweep] = off; g_probe[2 * sweep + 1] = dg; g_probe[80] = sweep; }
+#endif
     if (off <= 1e-36 * dg) break;   // off-diagonal far below the eigenvalues' rounding
     for (int r = 0; r < me - 1; ++r) {
+#ifdef RIPTRM_TRS_PROBE
+      long long pc0 = clock64();
+#endif
       for (int k = tid; k < np; k += NT) {
         int p, q;
         pair_of(r, k, me, p, q);
@@ -174,7 +192,7 @@ __device__ __noinline__ void jacobi(Blk<NT>& B, Work& w, bool want_v) {
             aqq = aqq + t * apq;
           }
         }
-        double* R = rot + ROT_FIELDS * k;
+        lds_f64* R = rot + ROT_FIELDS * k;
         R[0] = c;
         R[1] = s;
         R[2] = t;
@@ -184,42 +202,91 @@ __device__ __noinline__ void jacobi(Blk<NT>& B, Work& w, bool want_v) {
         R[6] = (double)q;
       }
       __syncthreads();
-      // columns p, q of A (and V): A <- A J; wave per pair, lane per row
-      for (int k = wv; k < np; k += NWV) {
-        const double* R = rot + ROT_FIELDS * k;
-        const double s = R[1];
-        if (s == 0.0) continue;
-        const double c = R[0];
-        const int p = (int)R[5], q = (int)R[6];
+#ifdef RIPTRM_TRS_PROBE
+      long long pc1 = clock64();
+#endif
+      // columns p, q of A (and V): A <- A J, then rows p, q: A <- J^T A.  A wave takes CH of its
+      // pairs at once: every LDS load of the chunk is issued before any store (the pairs of a
+      // round touch disjoint columns / rows), so a chunk costs two LDS round trips, not 2 CH.
+      for (int k0 = wv; k0 < np; k0 += NWV * CH) {
+        double cc[CH], ss[CH];
+        int pp[CH], qq[CH];
+#pragma unroll
+        for (int u = 0; u < CH; ++u) {
+          const int k = k0 + u * NWV;
+          const lds_f64* R = rot + ROT_FIELDS * (k < np ? k : 0);
+          cc[u] = R[0];
+          ss[u] = k < np ? R[1] : 0.0;
+          pp[u] = (int)R[5];
+          qq[u] = (int)R[6];
+        }
         for (int i = lane; i < m; i += 64) {
-          const double aip = A[i * lda + p], aiq = A[i * lda + q];
-          A[i * lda + p] = c * aip - s * aiq;
-          A[i * lda + q] = s * aip + c * aiq;
-          if (want_v) {
-            const double vip = V[i * lda + p], viq = V[i * lda + q];
-            V[i * lda + p] = c * vip - s * viq;
-            V[i * lda + q] = s * vip + c * viq;
+          double ap[CH], aq[CH], vp[CH], vq[CH];
+#pragma unroll
+          for (int u = 0; u < CH; ++u) {
+            if (ss[u] != 0.0) {
+              ap[u] = A[i * lda + pp[u]];
+              aq[u] = A[i * lda + qq[u]];
+              if (want_v) {
+                vp[u] = V[i * lda + pp[u]];
+                vq[u] = V[i * lda + qq[u]];
+              }
+            }
+          }
+#pragma unroll
+          for (int u = 0; u < CH; ++u) {
+            if (ss[u] != 0.0) {
+              A[i * lda + pp[u]] = cc[u] * ap[u] - ss[u] * aq[u];
+              A[i * lda + qq[u]] = ss[u] * ap[u] + cc[u] * aq[u];
+              if (want_v) {
+                V[i * lda + pp[u]] = cc[u] * vp[u] - ss[u] * vq[u];
+                V[i * lda + qq[u]] = ss[u] * vp[u] + cc[u] * vq[u];
+              }
+            }
           }
         }
       }
       __syncthreads();
-      // rows p, q: A <- J^T A; wave per pair, lane per column (contiguous)
-      for (int k = wv; k < np; k += NWV) {
-        const double* R = rot + ROT_FIELDS * k;
-        const double s = R[1];
-        if (s == 0.0) continue;
-        const double c = R[0];
-        const int p = (int)R[5], q = (int)R[6];
+#ifdef RIPTRM_TRS_PROBE
+      long long pc2 = clock64();
+#endif
+      for (int k0 = wv; k0 < np; k0 += NWV * CH) {
+        double cc[CH], ss[CH];
+        int pp[CH], qq[CH];
+#pragma unroll
+        for (int u = 0; u < CH; ++u) {
+          const int k = k0 + u * NWV;
+          const lds_f64* R = rot + ROT_FIELDS * (k < np ? k : 0);
+          cc[u] = R[0];
+          ss[u] = k < np ? R[1] : 0.0;
+          pp[u] = (int)R[5];
+          qq[u] = (int)R[6];
+        }
         for (int j = lane; j < m; j += 64) {
-          const double apj = A[p * lda + j], aqj = A[q * lda + j];
-          A[p * lda + j] = c * apj - s * aqj;
-          A[q * lda + j] = s * apj + c * aqj;
+          double ap[CH], aq[CH];
+#pragma unroll
+          for (int u = 0; u < CH; ++u) {
+            if (ss[u] != 0.0) {
+              ap[u] = A[pp[u] * lda + j];
+              aq[u] = A[qq[u] * lda + j];
+            }
+          }
+#pragma unroll
+          for (int u = 0; u < CH; ++u) {
+            if (ss[u] != 0.0) {
+              A[pp[u] * lda + j] = cc[u] * ap[u] - ss[u] * aq[u];
+              A[qq[u] * lda + j] = ss[u] * ap[u] + cc[u] * aq[u];
+            }
+          }
         }
       }
       __syncthreads();
+#ifdef RIPTRM_TRS_PROBE
+      long long pc3 = clock64();
+#endif
       // the rotated 2 x 2 block exactly: a_pq = 0, a_pp / a_qq by the stable update
       for (int k = tid; k < np; k += NT) {
-        const double* R = rot + ROT_FIELDS * k;
+        const lds_f64* R = rot + ROT_FIELDS * k;
         if (R[1] == 0.0) continue;
         const int p = (int)R[5], q = (int)R[6];
         A[p * lda + q] = 0.0;
@@ -228,6 +295,10 @@ __device__ __noinline__ void jacobi(Blk<NT>& B, Work& w, bool want_v) {
         A[q * lda + q] = R[4];
       }
       __syncthreads();
+#ifdef RIPTRM_TRS_PROBE
+      long long pc4 = clock64();
+      if (tid == 0) { g_probe[84] += pc1 - pc0; g_probe[85] += pc2 - pc1; g_probe[86] += pc3 - pc2; g_probe[87] += pc4 - pc3; g_probe[88] += 1; }
+#endif
     }
   }
   for (int i = tid; i < m; i += NT) w.ev[i] = A[i * lda + i];
@@ -236,7 +307,7 @@ __device__ __noinline__ void jacobi(Blk<NT>& B, Work& w, bool want_v) {
 
 // smallest eigenvalue of w.A (destroys w.A): RIPTRM.py:611-612
 template <int NT>
-__device__ __noinline__ double min_eig(Blk<NT>& B, Work& w) {
+__device__ __forceinline__ double min_eig(Blk<NT>& B, Work& w) {
   jacobi<NT>(B, w, false);
   double v = INFINITY;
   for (int i = threadIdx.x; i < w.dim; i += NT) v = fmin(v, w.ev[i]);
@@ -245,10 +316,10 @@ __device__ __noinline__ double min_eig(Blk<NT>& B, Work& w) {
 
 // y = A v over the LDS matrix, one thread per row (row sums in column order)
 template <int NT>
-__device__ __forceinline__ void matvec(const Work& w, const double* v, double* y) {
+__device__ __forceinline__ void matvec(const Work& w, const lds_f64* v, lds_f64* y) {
   const int m = w.dim, lda = w.lda;
   for (int i = threadIdx.x; i < m; i += NT) {
-    const double* row = w.A + i * lda;
+    const lds_f64* row = w.A + i * lda;
     double acc = 0.0;
     for (int k = 0; k < m; ++k) acc += row[k] * v[k];
     y[i] = acc;
@@ -263,7 +334,7 @@ struct Result {
 // TRSgep(A, a, I, Delta, tolhardcase): w.A, w.a filled by the caller (A symmetric).  Writes the
 // solution into w.x; w.A is destroyed.
 template <int NT>
-__device__ __noinline__ Result trs_solve(Blk<NT>& B, Work& w, double Delta, double tolhardcase) {
+__device__ __forceinline__ Result trs_solve(Blk<NT>& B, Work& w, double Delta, double tolhardcase) {
   const int tid = threadIdx.x;
   const int m = w.dim;
   const double D2 = Delta * Delta;
