@@ -33,14 +33,17 @@ constexpr int NBLK = 10;       // upper-triangular 16 x 16 blocks of a p x p mat
 
 // LDS (dynamic): M and L are p x p (padded stride PS <= 64), red holds the wave partials of the
 // Gram reduction tree (NW / 2 waves x NBLK blocks x 256 doubles).
+// address-space-3 pointers: ds_read / ds_write, not flat accesses through generic pointers
+typedef __attribute__((address_space(3))) double lds_f64;
 struct Smem {
-  double* M;     // p x p (Gram / sym / R^-1)
-  double* L;     // Cholesky factor
-  double* red;
+  lds_f64* M;     // p x p (Gram / sym / R^-1)
+  lds_f64* L;     // Cholesky factor
+  lds_f64* red;
 };
 constexpr int LDS_DOUBLES = 2 * PMAX * PMAX + (NW / 2) * NBLK * 256;
 
-__device__ __forceinline__ Smem smem_of(double* base) {
+__device__ __forceinline__ Smem smem_of(double* base_generic) {
+  lds_f64* base = (lds_f64*)base_generic;
   return Smem{base, base + PMAX * PMAX, base + 2 * PMAX * PMAX};
 }
 
@@ -99,7 +102,7 @@ __device__ __forceinline__ void gram_sym(Smem& sm, const double* __restrict__ A,
 #pragma unroll
   for (int h = NW / 2; h >= 1; h >>= 1) {
     if (w >= h && w < 2 * h) {
-      double* r = sm.red + (int64_t)(w - h) * NBLK * 256;
+      lds_f64* r = sm.red + (int64_t)(w - h) * NBLK * 256;
 #pragma unroll
       for (int b = 0; b < NBLK; ++b)
 #pragma unroll
@@ -107,7 +110,7 @@ __device__ __forceinline__ void gram_sym(Smem& sm, const double* __restrict__ A,
     }
     __syncthreads();
     if (w < h) {
-      const double* r = sm.red + (int64_t)w * NBLK * 256;
+      const lds_f64* r = sm.red + (int64_t)w * NBLK * 256;
 #pragma unroll
       for (int b = 0; b < NBLK; ++b)
 #pragma unroll
@@ -165,7 +168,7 @@ __device__ __forceinline__ void update(Smem& sm, const double* A, const double* 
 #pragma unroll
     for (int J = 0; J < 4; ++J) {
       if (J < P16) {
-        const double* pb = sm.M + kk * PS + J * 16 + c;
+        const lds_f64* pb = sm.M + kk * PS + J * 16 + c;
 #pragma unroll
         for (int k4 = 0; k4 < PMAX / 4; ++k4)
           if (k4 < P4) acc[J] = __builtin_amdgcn_mfma_f64_16x16x4f64(ar[k4], pb[k4 * 4 * PS], acc[J], 0, 0, 0);
@@ -195,8 +198,8 @@ __device__ __forceinline__ void update(Smem& sm, const double* A, const double* 
 // diag > 0), zero padded
 __device__ __forceinline__ void chol_rinv(Smem& sm, int p) {
   const int t = threadIdx.x, PS = pstride(p);
-  double* G = sm.M;
-  double* L = sm.L;
+  lds_f64* G = sm.M;
+  lds_f64* L = sm.L;
   for (int e = t; e < PS * PS; e += T) L[e] = 0.0;
   __syncthreads();
   for (int k = 0; k < p; ++k) {
