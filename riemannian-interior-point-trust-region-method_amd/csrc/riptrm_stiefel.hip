@@ -194,41 +194,6 @@ __device__ __forceinline__ void update(Smem& sm, const double* A, const double* 
   __syncthreads();
 }
 
-// sm.M (SPD p x p, stride PS) -> sm.M = (L^-1)^T = R^-1 for A^T A = R^T R, R = L^T (upper,
-// diag > 0), zero padded
-__device__ __forceinline__ void chol_rinv(Smem& sm, int p) {
-  const int t = threadIdx.x, PS = pstride(p);
-  lds_f64* G = sm.M;
-  lds_f64* L = sm.L;
-  for (int e = t; e < PS * PS; e += T) L[e] = 0.0;
-  __syncthreads();
-  for (int k = 0; k < p; ++k) {
-    if (t == 0) L[k * PS + k] = sqrt(G[k * PS + k]);
-    __syncthreads();
-    const double lkk = L[k * PS + k];
-    for (int i = k + 1 + t; i < p; i += T) L[i * PS + k] = G[i * PS + k] / lkk;
-    __syncthreads();
-    const int m = p - k - 1;
-    for (int e = t; e < m * m; e += T) {
-      const int i = k + 1 + e / m, j = k + 1 + (e - (e / m) * m);
-      if (j <= i) G[i * PS + j] = G[i * PS + j] - L[i * PS + k] * L[j * PS + k];
-    }
-    __syncthreads();
-  }
-  // column c of L^-1 by forward substitution; R^-1 = (L^-1)^T -> M[c][i] = (L^-1)[i][c]
-  for (int e = t; e < PS * PS; e += T) G[e] = 0.0;
-  __syncthreads();
-  if (t < p) {
-    const int c = t;
-    for (int i = c; i < p; ++i) {
-      double s = (i == c) ? 1.0 : 0.0;
-      for (int k = c; k < i; ++k) s = s - L[i * PS + k] * G[c * PS + k];
-      G[c * PS + i] = s / L[i * PS + i];
-    }
-  }
-  __syncthreads();
-}
-
 __global__ void __launch_bounds__(T) k_st_proj(int n, int p, int64_t stride, const double* X, const double* U, double* out) {
   extern __shared__ double lds[];
   Smem sm = smem_of(lds);
@@ -248,6 +213,51 @@ __global__ void __launch_bounds__(T) k_st_e2rh(int n, int p, int64_t stride, con
   update(sm, X + o, out + o, -1.0, out + o, n, p);  // P_X(W)
 }
 
+// sm.M (SPD p x p, stride PS) -> sm.L = lower Cholesky factor (A^T A = L L^T, diag > 0)
+__device__ __forceinline__ void chol_lower(Smem& sm, int p) {
+  const int t = threadIdx.x, PS = pstride(p);
+  lds_f64* G = sm.M;
+  lds_f64* L = sm.L;
+  for (int e = t; e < PS * PS; e += T) L[e] = 0.0;
+  __syncthreads();
+  for (int k = 0; k < p; ++k) {
+    const double lkk = sqrt(G[k * PS + k]);   // final since step k - 1; every thread takes it
+    if (t == 0) L[k * PS + k] = lkk;
+    for (int i = k + 1 + t; i < p; i += T) L[i * PS + k] = G[i * PS + k] / lkk;
+    __syncthreads();
+    const int m = p - k - 1;
+    for (int e = t; e < m * m; e += T) {
+      const int i = k + 1 + e / m, j = k + 1 + (e - (e / m) * m);
+      if (j <= i) G[i * PS + j] = G[i * PS + j] - L[i * PS + k] * L[j * PS + k];
+    }
+    __syncthreads();
+  }
+}
+
+// A <- A R^-1 (R = L^T) row by row: row a_i solves q R = a_i by forward substitution, all n rows in
+// parallel with the row in registers and L read as LDS broadcasts — no serial p^2 inverse.
+__device__ __forceinline__ void rows_solve(const Smem& sm, double* A, int n, int p) {
+  const int PS = pstride(p);
+  for (int i = threadIdx.x; i < n; i += T) {
+    double q[PMAX];
+#pragma unroll
+    for (int j = 0; j < PMAX; ++j) q[j] = (j < p) ? A[(int64_t)i * p + j] : 0.0;
+#pragma unroll
+    for (int j = 0; j < PMAX; ++j) {
+      if (j < p) {
+        double s = q[j];
+#pragma unroll
+        for (int k = 0; k < j; ++k) s = s - q[k] * sm.L[j * PS + k];
+        q[j] = s / sm.L[j * PS + j];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < PMAX; ++j)
+      if (j < p) A[(int64_t)i * p + j] = q[j];
+  }
+  __syncthreads();
+}
+
 __global__ void __launch_bounds__(T) k_st_retr(int n, int p, int64_t stride, const double* X, const double* U, double* out) {
   extern __shared__ double lds[];
   Smem sm = smem_of(lds);
@@ -257,8 +267,8 @@ __global__ void __launch_bounds__(T) k_st_retr(int n, int p, int64_t stride, con
   __syncthreads();
   for (int pass = 0; pass < 2; ++pass) {   // CholeskyQR2
     gram_sym(sm, A, A, n, p);                // (A^T A + A^T A) / 2 = A^T A exactly
-    chol_rinv(sm, p);
-    update(sm, A, nullptr, 0.0, A, n, p);
+    chol_lower(sm, p);
+    rows_solve(sm, A, n, p);                 // A R^-1
   }
 }
 
