@@ -164,6 +164,9 @@ def main():
                     help="subproblem solver (Exact_RepMat: manifold.dim <= 96, with the second-order test)")
     ap.add_argument("--stream-groups", type=int, default=0, choices=[0, 1, 2],
                     help="instance groups on separate streams (0 = library default)")
+    ap.add_argument("--spass-kind", type=int, default=1, choices=[0, 1, 2],
+                    help="sym layout S-pass: 1 = automatic (persistent super-tile kernel at >= 4 units per CU), "
+                         "0 = per-tile kernel only, 2 = super-tile kernel always")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_gemv.json"))
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend (nccl = RCCL)")
     ap.add_argument("--same-device", action="store_true",
@@ -204,7 +207,8 @@ def main():
     from problems import manviofun
 
     n, B, W, K = args.dim, args.batch, args.warmup, args.steps
-    eng = engine.NonnegPCABatch(n, B, log_capacity=2048, layout=args.layout, stream_groups=args.stream_groups)
+    eng = engine.NonnegPCABatch(n, B, log_capacity=2048, layout=args.layout, stream_groups=args.stream_groups,
+                                spass_kind=args.spass_kind)
     nS = 1 if args.layout == "shared" else B
     log(f"rank {rank}/{world}: generating {B} instances n={n} ({nS * eng.inst_stride * 8 / 1e9:.1f} GB S)")
     # global instance ids owned by this rank: rank, rank+world, ... (seed seed0 + id)
@@ -275,10 +279,14 @@ def main():
         achieved = (passes_r0 * bytes_per_pass / gemv_s / 1e9) if gemv_s > 0 else None
         nl = max(1, int(prof["gemv_launches"]))
         traffic = None
+        spass_kernel = "k_spass_sym" if args.spass_kind == 0 else "k_spass_sup"
+        spass_label = ("k_spass_sym (S-pass, one workgroup per symmetric 128x128 tile)" if args.spass_kind == 0 else
+                       "k_spass_sup (S-pass, persistent: one workgroup per CU over 2x2-tile units, partial sums "
+                       "written in bursts; k_spass_sym when a launch has < 4 units per CU)")
         if os.path.exists(args.traffic_json) and args.layout == "sym":
             try:
                 tj = json.load(open(args.traffic_json))
-                if tj.get("n") == n:
+                if tj.get("n") == n and tj.get("kernel", "k_spass_sym") == spass_kernel:
                     # per-launch HBM bytes scaled to this run's mean instances per launch
                     traffic = tj["hbm_bytes_per_instance_pass"] * passes_r0 / nl
             except Exception as e:  # pragma: no cover
@@ -295,8 +303,7 @@ def main():
             roofline = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
                         "traffic": traffic,
-                        "kernel": "k_spass_sym (S-pass, symmetric tiles)" if args.layout == "sym"
-                                  else "k_gemv (S-pass, full matrix)",
+                        "kernel": spass_label if args.layout == "sym" else "k_gemv (S-pass, full matrix)",
                         "bytes_per_launch": passes_r0 * bytes_per_pass / nl,
                         "avg_launch_us": prof["gemv_ms"] * 1e3 / nl}
         cpu = None

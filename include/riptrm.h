@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define RIPTRM_ABI_VERSION 3
+#define RIPTRM_ABI_VERSION 4
 
 /* status codes */
 #define RIPTRM_OK 0
@@ -230,6 +230,13 @@ int riptrm_set_stream_groups(riptrm_ctx* ctx, int32_t groups);
  * lock-step iterations (16 kernels) per host submission instead of 2 launches per iteration,
  * unless profiling is on.  on = 0 disables it (default 1).  Results do not depend on it. */
 int riptrm_set_graphs(riptrm_ctx* ctx, int32_t on);
+
+/* S-pass kernel of the symmetric-tile layout: 1 = automatic (default: the persistent super-tile
+ * kernel, whose partial-sum writes leave the HBM read stream in bursts, once every compute unit
+ * gets >= 4 units of 2 x 2 tiles; the per-tile kernel below that), 0 = per-tile kernel only,
+ * 2 = super-tile kernel always.  Results agree to rounding (the partial sums are added in a
+ * different, still fixed, order). */
+int riptrm_set_spass_kind(riptrm_ctx* ctx, int32_t kind);
 
 /* ---- measurement ---- */
 /* Enable/disable HIP-event timing of every S-pass (k_gemv) and state-machine (k_state) launch

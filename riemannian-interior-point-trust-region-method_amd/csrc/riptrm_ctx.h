@@ -33,6 +33,8 @@ struct riptrm_ctx {
   hipStream_t own_stream = nullptr;  // created for group 1
   hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_pass[2] = {nullptr, nullptr};
   double clock_hz = 1e8;
+  int ncu = 256;              // compute units (persistent S-pass grid)
+  int sup_req = 1;            // riptrm_set_spass_kind: 0 = tile S-pass only, 1 = automatic, 2 = super-tile always
   // optional HIP-event timing of every k_gemv / k_state launch (riptrm_profile_*)
   bool prof = false;
   std::vector<hipEvent_t> ev_pool;

@@ -82,6 +82,18 @@ inline int64_t ld_of(int32_t n) { return round_up(n > 0 ? n : 1, TS); }
 inline int64_t rows_of(int32_t n) { return round_up(n > 0 ? n : 1, 32); }  // k_pack writes 32-row sub-tiles
 inline int32_t nt_of(int32_t n) { return (int32_t)(ld_of(n) / TS); }
 inline int64_t ntiles_of(int32_t n) { const int64_t t = nt_of(n); return t * (t + 1) / 2; }
+// Persistent super-tile S-pass (k_spass_sup): work units of SB x SB stored tiles, partial sums
+// of SW = SB TS elements per unit side; nst super-blocks per dimension
+constexpr int SB = 2;
+constexpr int SW = SB * TS;
+inline int32_t nst_of(int32_t n) { return (nt_of(n) + SB - 1) / SB; }
+inline int64_t nsup_of(int32_t n) { const int64_t t = nst_of(n); return t * (t + 1) / 2; }
+// doubles of one instance's S-pass partial grid (one right-hand side): the larger of the tile
+// grid [nt][nt][TS] and the super-tile grid [nst][nst][SW]
+inline int64_t pgrid_of(int32_t n) {
+  const int64_t a = (int64_t)nt_of(n) * nt_of(n) * TS, b = (int64_t)nst_of(n) * nst_of(n) * SW;
+  return a > b ? a : b;
+}
 // shared-S MFMA S-pass: K is split over MM_KZ workgroup slices whose partial products land in
 // MM_KZ x 2 x batch x ld slabs, summed in slice order by the state kernel
 constexpr int MM_KZ = 4;
@@ -116,7 +128,7 @@ inline Layout make_layout(int32_t n, int32_t batch, int32_t cap, int32_t layout)
   L.off_stats = o; o += (int64_t)batch * RIPTRM_STAT_NFIELDS * 8;        o = round_up(o, 256);
   L.off_log = o;   o += (int64_t)batch * cap * RIPTRM_LOG_NFIELDS * 8;   o = round_up(o, 256);
   L.off_pbuf = o;
-  if (layout == RIPTRM_LAYOUT_SYMTILE) o += (int64_t)2 * batch * L.nt * L.nt * TS * 8;
+  if (layout == RIPTRM_LAYOUT_SYMTILE) o += (int64_t)2 * batch * pgrid_of(n) * 8;
   if (layout == RIPTRM_LAYOUT_SHARED) o += (int64_t)MM_KZ * 2 * batch * L.ld * 8;
   o = round_up(o, 256);
   L.off_lists = o; o += (int64_t)4 * batch * 4;                          o = round_up(o, 256);
@@ -137,7 +149,9 @@ struct DevParams {
   int32_t nt;           // tiles per dimension (symmetric-tile layout)
   int32_t ntiles;       // nt (nt + 1) / 2
   int32_t wl;           // stored columns of the last tile column (symmetric-tile layout)
-  double* pbuf;         // S-pass partial sums: 2 x batch x nt x nt x TS (symmetric-tile layout),
+  int32_t nst, nsup;    // super-blocks per dimension, super-tile units per instance
+  int32_t smode;        // per launch: 0 = tile S-pass (grid [nt][nt][TS]), 1 = super-tile ([nst][nst][SW])
+  double* pbuf;         // S-pass partial sums: 2 x batch x pgrid_of(n) (symmetric-tile layout),
                         // MM_KZ x 2 x batch x ld (shared layout)
   double* vec;          // workspace vectors
   double* st;           // workspace scalars

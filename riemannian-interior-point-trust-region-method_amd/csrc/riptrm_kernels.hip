@@ -354,6 +354,178 @@ __global__ void __launch_bounds__(SP_THREADS, 4) k_spass_sym(DevParams P, int li
 }
 
 // ------------------------------------------------------------------------------------------
+// Persistent super-tile S-pass (P.smode = 1; batches with >= 4 units per CU).  Same arithmetic
+// per stored tile as spass_tile, but one 8-wave workgroup per CU walks units u = g, g + G, ... of
+// SB x SB stored tiles: row sums accumulate over a unit's tile columns, column sums over its
+// tile rows (8 waves, then LDS across waves in wave order), and each unit's two SW-element
+// partial vectors are kept in LDS and written in bursts of up to SUP_OCAP doubles.  Why: the
+// partial-sum writes of the per-tile kernel, 1.5% of the bytes, cost 13% of its streaming rate
+// when they trickle out between the reads (tools/spass_glds_bench.hip: 6.15 TB/s with the writes,
+// 7.15 without, 6.79-6.82 for this kernel on the same box).  Partial grid [b][P][Q][SW]: slot
+// (P, Q) holds unit (P, Q)'s row part (P <= Q; the whole symmetric block on the diagonal) and
+// slot (Q, P) its column part; every slot is written by exactly one unit: deterministic.
+// ------------------------------------------------------------------------------------------
+constexpr int SUP_OCAP = 15360;                 // doubles of buffered unit results (120 KiB)
+constexpr int SUP_MAXU = SUP_OCAP / (2 * SW);   // units per burst at one right-hand side
+
+typedef double (*sup_red_t)[SP_WAVES][SW];
+
+template <int NR>
+__device__ __forceinline__ void sup_unit(const DevParams& P, int b, int Pq, int Qq, sup_red_t red, double* out) {
+  const int lane = (int)__lane_id();
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int nt = P.nt, wl = P.wl;
+  constexpr int ROWS = TS / SP_WAVES;
+  const double* __restrict__ Sb = P.S + (int64_t)b * P.inst_stride;
+  const double* __restrict__ v0 = vp(P, V_IN0, b);
+  const double* __restrict__ v1 = vp(P, V_IN1, b);
+  const int rrow = 4 * ((lane >> 5) & 1) + 2 * ((lane >> 4) & 1) + ((lane >> 3) & 1);
+  double racc[NR][SB][2];
+#pragma unroll
+  for (int k = 0; k < NR; ++k)
+#pragma unroll
+    for (int i = 0; i < SB; ++i) racc[k][i][0] = racc[k][i][1] = 0.0;
+#pragma unroll
+  for (int k = 0; k < NR; ++k)
+    for (int jl = 0; jl < SB; ++jl) {
+      red[k][w][jl * TS + 2 * lane] = 0.0;
+      red[k][w][jl * TS + 2 * lane + 1] = 0.0;
+    }
+#pragma unroll
+  for (int il = 0; il < SB; ++il) {
+    const int I = SB * Pq + il;
+    if (I >= nt) break;
+    const int rowsT = (I == nt - 1) ? wl : TS;
+#pragma unroll 1
+    for (int jl = 0; jl < SB; ++jl) {
+      const int J = SB * Qq + jl;
+      if (J >= nt || J < I) continue;
+      const int colsT = (J == nt - 1) ? wl : TS;
+      const bool cl = 2 * lane < colsT;
+      const double* __restrict__ T = Sb + sym_off(I, J, nt, wl);
+      const dbl2 vj0 = *(const dbl2*)(v0 + J * TS + 2 * lane);
+      dbl2 vj1 = dbl2{0.0, 0.0};
+      if (NR == 2) vj1 = *(const dbl2*)(v1 + J * TS + 2 * lane);
+      double c0x = 0.0, c0y = 0.0, c1x = 0.0, c1y = 0.0;
+#pragma unroll 1
+      for (int rb = 0; rb < ROWS / 8; ++rb) {
+        const int r0 = w * ROWS + rb * 8;
+        if (r0 >= rowsT) break;   // corner tiles: rows beyond wl are not stored (wave-uniform)
+        dbl2 sv[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+          sv[k] = cl ? __builtin_nontemporal_load((const dbl2*)(T + (r0 + k) * colsT + 2 * lane)) : dbl2{0.0, 0.0};
+        double a[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const double vi0 = v0[I * TS + r0 + k];
+          a[k] = __builtin_fma(sv[k].y, vj0.y, sv[k].x * vj0.x);
+          c0x = __builtin_fma(sv[k].x, vi0, c0x);
+          c0y = __builtin_fma(sv[k].y, vi0, c0y);
+        }
+        const double s0 = reduce_scatter8(a);
+        if (rb == 0) racc[0][il][0] += s0;
+        else racc[0][il][1] += s0;
+        if (NR == 2) {
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            const double vi1 = v1[I * TS + r0 + k];
+            a[k] = __builtin_fma(sv[k].y, vj1.y, sv[k].x * vj1.x);
+            c1x = __builtin_fma(sv[k].x, vi1, c1x);
+            c1y = __builtin_fma(sv[k].y, vi1, c1y);
+          }
+          const double s1 = reduce_scatter8(a);
+          if (rb == 0) racc[NR - 1][il][0] += s1;
+          else racc[NR - 1][il][1] += s1;
+        }
+      }
+      if (I != J) {   // column part (the diagonal tile is stored whole: row part only)
+        red[0][w][jl * TS + 2 * lane] += c0x;
+        red[0][w][jl * TS + 2 * lane + 1] += c0y;
+        if (NR == 2) {
+          red[NR - 1][w][jl * TS + 2 * lane] += c1x;
+          red[NR - 1][w][jl * TS + 2 * lane + 1] += c1y;
+        }
+      }
+    }
+  }
+  // unit result out[k][0] = rows of super-block Pq, out[k][1] = columns of super-block Qq
+  if ((lane & 7) == 0) {
+#pragma unroll
+    for (int k = 0; k < NR; ++k)
+#pragma unroll
+      for (int il = 0; il < SB; ++il) {
+        out[(2 * k) * SW + il * TS + w * ROWS + rrow] = racc[k][il][0];
+        out[(2 * k) * SW + il * TS + w * ROWS + 8 + rrow] = racc[k][il][1];
+      }
+  }
+  __syncthreads();
+  for (int t = threadIdx.x; t < NR * SW; t += SP_THREADS) {
+    const int k = t / SW, c = t - k * SW;
+    double cs = red[k][0][c];
+#pragma unroll
+    for (int q = 1; q < SP_WAVES; ++q) cs += red[k][q][c];
+    if (Pq == Qq) out[(2 * k) * SW + c] += cs;   // diagonal unit: both parts land in block Pq
+    else out[(2 * k + 1) * SW + c] = cs;
+  }
+  __syncthreads();
+}
+
+__device__ __forceinline__ void sup_flush(const DevParams& P, const double* outb, const int (*meta)[2], int nslot,
+                                          int list_in) {
+  __syncthreads();
+  const int64_t nn = (int64_t)P.nst * P.nst * SW;
+  int off = 0;
+  for (int s = 0; s < nslot; ++s) {
+    const int u = meta[s][0], nr = meta[s][1];
+    const int slot = u / P.nsup;
+    const int b = le_b(P.lists[list_in * P.batch + slot]);
+    int Pq, Qq;
+    tile_ij(u - slot * P.nsup, P.nst, Pq, Qq);
+    const int t = threadIdx.x, side = t / SW, c = t - side * SW;   // 512 threads: row side, column side
+    for (int k = 0; k < nr; ++k) {
+      double* pb = P.pbuf + ((int64_t)k * P.batch + b) * nn;
+      if (side == 0) pb[((int64_t)Pq * P.nst + Qq) * SW + c] = outb[off + (2 * k) * SW + c];
+      else if (Pq != Qq) pb[((int64_t)Qq * P.nst + Pq) * SW + c] = outb[off + (2 * k + 1) * SW + c];
+    }
+    off += nr * 2 * SW;
+  }
+  __syncthreads();
+}
+
+__global__ void __launch_bounds__(SP_THREADS, 1) k_spass_sup(DevParams P, int list_in, int zero_cnt) {
+  static_assert(SP_THREADS == 2 * SW, "sup_flush: one thread per element of the two sides");
+  __shared__ double red[2][SP_WAVES][SW];
+  __shared__ double outb[SUP_OCAP];
+  __shared__ int meta[SUP_MAXU][2];
+  if (zero_cnt >= 0 && blockIdx.x == 0 && threadIdx.x == 0) P.cnt[zero_cnt] = 0;
+  const int nact = P.cnt[list_in];
+  const int total = nact * P.nsup;
+  int used = 0, nslot = 0;
+  for (int u = blockIdx.x; u < total; u += gridDim.x) {
+    const int slot = u / P.nsup;
+    const int32_t e = P.lists[list_in * P.batch + slot];
+    const int b = le_b(e), nr = le_nrhs(e);
+    int Pq, Qq;
+    tile_ij(u - slot * P.nsup, P.nst, Pq, Qq);
+    if (used + nr * 2 * SW > SUP_OCAP) {
+      sup_flush(P, outb, meta, nslot, list_in);
+      used = 0;
+      nslot = 0;
+    }
+    if (nr == 2) sup_unit<2>(P, b, Pq, Qq, red, outb + used);
+    else sup_unit<1>(P, b, Pq, Qq, red, outb + used);
+    if (threadIdx.x == 0) {
+      meta[nslot][0] = u;
+      meta[nslot][1] = nr;
+    }
+    used += nr * 2 * SW;
+    ++nslot;
+  }
+  if (nslot > 0) sup_flush(P, outb, meta, nslot, list_in);
+}
+
+// ------------------------------------------------------------------------------------------
 // Shared-S (multi-start) S-pass on the fp64 matrix cores: every active instance multiplies the
 // SAME S, so one pass is the dense product Y^T = V^T S over the active right-hand sides
 // (column c = active slot for in0, bound + slot for in1 when the instance asked for two).
@@ -560,16 +732,19 @@ template <int K>
 __device__ __forceinline__ void rl_gather(const DevParams& P, int b, double (&u)[K]) {
   const int tid = threadIdx.x, n = P.n;
   if (P.layout == RIPTRM_LAYOUT_SYMTILE) {
-    const int nt = P.nt;
-    const int64_t nn = (int64_t)nt * nt * TS;
+    // tile grid [nt][nt][TS] or super-tile grid [nst][nst][SW] (P.smode), summed in block order
+    const int nt = P.smode ? P.nst : P.nt;
+    const int sh = P.smode ? 8 : 7, wd = 1 << sh;
+    static_assert(SW == 256 && TS == 128, "partial-grid shifts");
+    const int64_t nn = (int64_t)nt * nt * wd;
     const double* pb = P.pbuf + (int64_t)b * nn;
     const double* q[K];
 #pragma unroll
     for (int e = 0; e < K; ++e) {
       int i = tid + e * ST_THREADS;
       i = i < n ? i : n - 1;
-      const int I = i / TS, c = i - I * TS;
-      q[e] = pb + (int64_t)I * nt * TS + c;
+      const int I = i >> sh, c = i - (I << sh);
+      q[e] = pb + (int64_t)I * nt * wd + c;
     }
     if constexpr (K <= 2) {
       constexpr int NTS = 8;
@@ -577,7 +752,7 @@ __device__ __forceinline__ void rl_gather(const DevParams& P, int b, double (&u)
 #pragma unroll
       for (int e = 0; e < K; ++e)
 #pragma unroll
-        for (int J = 0; J < NTS; ++J) t[e][J] = (J < nt) ? q[e][(int64_t)J * TS] : 0.0;
+        for (int J = 0; J < NTS; ++J) t[e][J] = (J < nt) ? q[e][(int64_t)J * wd] : 0.0;
 #pragma unroll
       for (int e = 0; e < K; ++e) {
         u[e] = t[e][0];
@@ -594,7 +769,7 @@ __device__ __forceinline__ void rl_gather(const DevParams& P, int b, double (&u)
 #pragma unroll
         for (int e = 0; e < K; ++e)
 #pragma unroll
-          for (int v = 0; v < GJ; ++v) t[e][v] = (J + v < nt) ? q[e][(int64_t)(J + v) * TS] : 0.0;
+          for (int v = 0; v < GJ; ++v) t[e][v] = (J + v < nt) ? q[e][(int64_t)(J + v) * wd] : 0.0;
 #pragma unroll
         for (int e = 0; e < K; ++e)
 #pragma unroll
@@ -713,8 +888,9 @@ struct MachineT {
 
   __device__ __forceinline__ void gather_out(int nr) {
     constexpr int GE = 8, GJ = 4;
-    const int nt = P.nt;
-    const int64_t nn = (int64_t)nt * nt * TS;
+    const int nt = P.smode ? P.nst : P.nt;   // tile or super-tile partial grid
+    const int sh = P.smode ? 8 : 7, wd = 1 << sh;
+    const int64_t nn = (int64_t)nt * nt * wd;
     for (int k = 0; k < nr; ++k) {
       const double* pb = P.pbuf + ((int64_t)k * P.batch + b) * nn;
       double* O = V(k == 0 ? V_OUT0 : V_OUT1);
@@ -725,8 +901,8 @@ struct MachineT {
         for (int e = 0; e < GE; ++e) {
           int i = base + e * ST_THREADS;
           i = i < n ? i : n - 1;  // clamp: duplicate work, stored only if in range
-          const int I = i / TS, c = i - I * TS;
-          q[e] = pb + (int64_t)I * nt * TS + c;
+          const int I = i >> sh, c = i - (I << sh);
+          q[e] = pb + (int64_t)I * nt * wd + c;
           acc[e] = q[e][0];
         }
         for (int J = 1; J < nt; J += GJ) {
@@ -734,7 +910,7 @@ struct MachineT {
 #pragma unroll
           for (int e = 0; e < GE; ++e)
 #pragma unroll
-            for (int u = 0; u < GJ; ++u) t[e][u] = (J + u < nt) ? q[e][(int64_t)(J + u) * TS] : 0.0;
+            for (int u = 0; u < GJ; ++u) t[e][u] = (J + u < nt) ? q[e][(int64_t)(J + u) * wd] : 0.0;
 #pragma unroll
           for (int e = 0; e < GE; ++e)
 #pragma unroll
@@ -1905,6 +2081,8 @@ int riptrm_ctx_create(riptrm_ctx** out, int device, void* stream) {
   int khz = 0;
   if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device) == hipSuccess && khz > 0)
     c->clock_hz = (double)khz * 1000.0;
+  int ncu = 0;
+  if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && ncu > 0) c->ncu = ncu;
   if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess ||
@@ -2015,6 +2193,9 @@ int riptrm_nonnegpca_bind(riptrm_ctx* ctx, const double* S, int32_t n, int32_t b
   P.nt = L.nt;
   P.ntiles = (int)ntiles_of(n);
   P.wl = edge_w_of(n);
+  P.nst = nst_of(n);
+  P.nsup = (int32_t)nsup_of(n);
+  P.smode = 0;
   P.pbuf = (double*)(ctx->ws + L.off_pbuf);
   P.vec = (double*)(ctx->ws + L.off_vec);
   P.st = (double*)(ctx->ws + L.off_state);
@@ -2040,7 +2221,21 @@ int riptrm_nonnegpca_bind(riptrm_ctx* ctx, const double* S, int32_t n, int32_t b
   return RIPTRM_OK;
 }
 
-static int launch_gemv(riptrm_ctx* c, hipStream_t st, int list_in, int zero_cnt, int bound) {
+// S-pass kind for a launch over at most `bound` instances: the persistent super-tile kernel once
+// every CU gets >= 4 units of work; below that the per-tile kernel spreads the few instances'
+// tiles over more workgroups (latency).  The state kernel that gathers the pass gets the same mode.
+static int spass_mode(const riptrm_ctx* c, int bound) {
+  if (c->P.layout != RIPTRM_LAYOUT_SYMTILE || c->sup_req == 0) return 0;
+  return ((int64_t)bound * c->P.nsup >= (int64_t)4 * c->ncu || c->sup_req == 2) ? 1 : 0;
+}
+
+static DevParams params_for(const riptrm_ctx* c, int smode) {
+  DevParams P = c->P;
+  P.smode = smode;
+  return P;
+}
+
+static int launch_gemv(riptrm_ctx* c, hipStream_t st, int list_in, int zero_cnt, int bound, int smode) {
   if (bound <= 0) return RIPTRM_OK;
   const bool sym = c->P.layout == RIPTRM_LAYOUT_SYMTILE;
   const int64_t blocks = (int64_t)bound * (sym ? c->P.ntiles : c->P.nrb);
@@ -2059,6 +2254,10 @@ static int launch_gemv(riptrm_ctx* c, hipStream_t st, int list_in, int zero_cnt,
       hipLaunchKernelGGL((k_spass_mm<2, 1, 4>), dim3(rows / 16, 2 * ct, MM_KZ), dim3(256), 0, st, c->P, list_in,
                          zero_cnt, bound);
     }
+  } else if (sym && smode) {
+    const int64_t units = (int64_t)bound * c->P.nsup;
+    const unsigned grid = (unsigned)(units < c->ncu ? units : c->ncu);
+    hipLaunchKernelGGL(k_spass_sup, dim3(grid), dim3(SP_THREADS), 0, st, params_for(c, 1), list_in, zero_cnt);
   } else if (sym)
     hipLaunchKernelGGL(k_spass_sym, dim3((unsigned)blocks), dim3(SP_THREADS), 0, st, c->P, list_in, zero_cnt);
   else
@@ -2078,17 +2277,19 @@ static size_t state_lds_bytes(const DevParams& P) {
 }
 
 static int launch_state(riptrm_ctx* c, hipStream_t st, int full, int list_in, int list_out, int bound,
-                        int full_base = 0) {
+                        int full_base, int smode) {
   const int blocks = bound;
   if (blocks <= 0) return RIPTRM_OK;
   int i0 = -1, i1 = -1;
   hipEvent_t e0 = nullptr, e1 = nullptr;
   if (c->prof && (e0 = prof_event(c, &i0)) && (e1 = prof_event(c, &i1))) HIPCHK(c, hipEventRecord(e0, st));
   if (c->P.opt.trs_solver == RIPTRM_TRS_SOLVER_EXACT_REPMAT)
-    hipLaunchKernelGGL(k_state<true>, dim3((unsigned)blocks), dim3(ST_THREADS), state_lds_bytes(c->P), st, c->P, full,
+    hipLaunchKernelGGL(k_state<true>, dim3((unsigned)blocks), dim3(ST_THREADS), state_lds_bytes(c->P), st,
+                       params_for(c, smode), full,
                        list_in, list_out, full_base, bound);
   else
-    hipLaunchKernelGGL(k_state<false>, dim3((unsigned)blocks), dim3(ST_THREADS), 0, st, c->P, full, list_in, list_out,
+    hipLaunchKernelGGL(k_state<false>, dim3((unsigned)blocks), dim3(ST_THREADS), 0, st, params_for(c, smode), full,
+                       list_in, list_out,
                        full_base, bound);
   HIPCHK(c, hipGetLastError());
   if (c->prof && e1) {
@@ -2124,9 +2325,10 @@ int riptrm_nonnegpca_hvp(riptrm_ctx* ctx, const double* x, const double* y, doub
   const int B = ctx->P.batch;
   hipLaunchKernelGGL(k_hvp_prep, dim3(B), dim3(256), 0, ctx->stream, ctx->P, x, y, v, ldv);
   HIPCHK(ctx, hipGetLastError());
-  int rc = launch_gemv(ctx, ctx->stream, 0, -1, B);
+  const int sm = spass_mode(ctx, B);
+  int rc = launch_gemv(ctx, ctx->stream, 0, -1, B, sm);
   if (rc) return rc;
-  hipLaunchKernelGGL(k_hvp_epi, dim3(B), dim3(ST_THREADS), 0, ctx->stream, ctx->P, mu, out, ldv);
+  hipLaunchKernelGGL(k_hvp_epi, dim3(B), dim3(ST_THREADS), 0, ctx->stream, params_for(ctx, sm), mu, out, ldv);
   HIPCHK(ctx, hipGetLastError());
   ctx->solving = false;
   return RIPTRM_OK;
@@ -2141,9 +2343,10 @@ int riptrm_nonnegpca_operator_aw(riptrm_ctx* ctx, const double* x, const double*
   const int B = ctx->P.batch;
   hipLaunchKernelGGL(k_hvp_prep, dim3(B), dim3(256), 0, ctx->stream, ctx->P, x, z, v, ldv);
   HIPCHK(ctx, hipGetLastError());
-  int rc = launch_gemv(ctx, ctx->stream, 0, -1, B);
+  const int sm = spass_mode(ctx, B);
+  int rc = launch_gemv(ctx, ctx->stream, 0, -1, B, sm);
   if (rc) return rc;
-  hipLaunchKernelGGL(k_aw_epi, dim3(B), dim3(ST_THREADS), 0, ctx->stream, ctx->P, s, out, ldv);
+  hipLaunchKernelGGL(k_aw_epi, dim3(B), dim3(ST_THREADS), 0, ctx->stream, params_for(ctx, sm), s, out, ldv);
   HIPCHK(ctx, hipGetLastError());
   ctx->solving = false;
   return RIPTRM_OK;
@@ -2167,8 +2370,9 @@ static int capture_graph(riptrm_ctx* c, int bound) {
   int rc = RIPTRM_OK;
   for (int s = 0; s < GRAPH_STEPS && rc == RIPTRM_OK; ++s) {
     const int lin = par, lout = par ^ 1;
-    rc = launch_gemv(c, st, lin, lout, bound);
-    if (rc == RIPTRM_OK) rc = launch_state(c, st, 2, lin, lout, c->gsize[0], c->gbase[0]);
+    const int sm = spass_mode(c, bound);
+    rc = launch_gemv(c, st, lin, lout, bound, sm);
+    if (rc == RIPTRM_OK) rc = launch_state(c, st, 2, lin, lout, c->gsize[0], c->gbase[0], sm);
     par ^= 1;
   }
   hipGraph_t g = nullptr;
@@ -2221,10 +2425,11 @@ static int run_steps(riptrm_ctx* c, int steps, int* n_active) {
       hipStream_t st = c->gstream[g];
       const int lin = g * 2 + c->parity[g], lout = g * 2 + (c->parity[g] ^ 1);
       if (G == 2) HIPCHK(c, hipStreamWaitEvent(st, c->ev_pass[g ^ 1], 0));
-      rc = launch_gemv(c, st, lin, lout, c->active_bound[g]);
+      const int sm = spass_mode(c, c->active_bound[g]);
+      rc = launch_gemv(c, st, lin, lout, c->active_bound[g], sm);
       if (rc) return rc;
       if (G == 2) HIPCHK(c, hipEventRecord(c->ev_pass[g], st));
-      rc = launch_state(c, st, 2, lin, lout, c->gsize[g], c->gbase[g]);
+      rc = launch_state(c, st, 2, lin, lout, c->gsize[g], c->gbase[g], sm);
       if (rc) return rc;
       c->parity[g] ^= 1;
     }
@@ -2250,7 +2455,7 @@ static int kick(riptrm_ctx* c) {
   if (rc) return rc;
   for (int g = 0; g < c->ngroups; ++g) {
     const int l = g * 2 + c->parity[g];
-    rc = launch_state(c, c->gstream[g], 1, l, l, c->gsize[g], c->gbase[g]);
+    rc = launch_state(c, c->gstream[g], 1, l, l, c->gsize[g], c->gbase[g], 0);
     if (rc) return rc;
     c->active_bound[g] = c->gsize[g];
   }
@@ -2346,6 +2551,13 @@ int riptrm_set_stream_groups(riptrm_ctx* ctx, int32_t groups) {
   if (!ctx || groups < 0 || groups > 2) return RIPTRM_E_ARG;
   if (ctx->solving) return fail(ctx, RIPTRM_E_STATE, "set_stream_groups: call before riptrm_nonnegpca_bind");
   ctx->groups_req = groups;
+  return RIPTRM_OK;
+}
+
+int riptrm_set_spass_kind(riptrm_ctx* ctx, int32_t kind) {
+  if (!ctx || kind < 0 || kind > 2) return RIPTRM_E_ARG;
+  ctx->sup_req = kind;
+  ctx->pver++;   // a captured graph holds the old kernel
   return RIPTRM_OK;
 }
 

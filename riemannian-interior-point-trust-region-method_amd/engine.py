@@ -200,7 +200,7 @@ class NonnegPCABatch:
     problem_initialpoint axis), S-pass on the fp64 matrix cores."""
 
     def __init__(self, n: int, batch: int, device: Optional[int] = None, log_capacity: int = 4096,
-                 layout: str = "sym", stream_groups: int = 0):
+                 layout: str = "sym", stream_groups: int = 0, spass_kind: int = 1):
         if not torch.cuda.is_available():
             raise RuntimeError("NonnegPCABatch needs a ROCm GPU (gfx950); there is no CPU fallback")
         if n < 2 or batch < 1:
@@ -218,6 +218,7 @@ class NonnegPCABatch:
         self.inst_stride = int(self.lib.riptrm_nonnegpca_s_elems(self.n, self.layout))
         self.ctx = N.Context(self.device.index, _stream_handle(self.device))
         self.ctx.check(self.lib.riptrm_set_stream_groups(self.ctx.h, int(stream_groups)), "riptrm_set_stream_groups")
+        self.ctx.check(self.lib.riptrm_set_spass_kind(self.ctx.h, int(spass_kind)), "riptrm_set_spass_kind")
         self.S = torch.zeros((1 if self.shared else self.batch, self.inst_stride), dtype=torch.float64,
                              device=self.device)
         nbytes = int(self.lib.riptrm_workspace_bytes(self.n, self.batch, self.cap, self.layout))

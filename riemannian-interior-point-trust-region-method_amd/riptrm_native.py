@@ -73,6 +73,7 @@ SIGNATURES: Dict[str, tuple] = {
     "riptrm_device_clock_hz": (c_double, [c_void_p]),
     "riptrm_set_stream_groups": (c_int32, [c_void_p, c_int32]),
     "riptrm_set_graphs": (c_int32, [c_void_p, c_int32]),
+    "riptrm_set_spass_kind": (c_int32, [c_void_p, c_int32]),
     "riptrm_profile_enable": (c_int32, [c_void_p, c_int32]),
     "riptrm_profile_read": (c_int32, [c_void_p, ctypes.POINTER(c_double), ctypes.POINTER(c_int64),
                                       ctypes.POINTER(c_double), ctypes.POINTER(c_int64)]),

@@ -1,16 +1,10 @@
-# Round-1 evidence: default bench line, rocprofv3 kernel stats of the same command, PMC traffic passes.
+# Round-1 evidence: PMC traffic passes of the S-pass, the default bench line (with that traffic),
+# rocprofv3 kernel stats of the same command, and a same-box A/B against the per-tile S-pass.
 set -u
 cd "$GRAFT_REPO_ROOT"
-mkdir -p gpurun_out/r1b
+mkdir -p gpurun_out/r1c
 export TMPDIR=/tmp
-O=gpurun_out/r1b
-true
-timeout -k 10 600 python bench.py > $O/bench.json 2> $O/bench.err; rc=$?
-echo "bench rc=$rc"; cat $O/bench.json
-[ $rc -eq 0 ] || exit $rc
-timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o bench -- python bench.py --cpu-budget 0 > $O/prof_bench.json 2> $O/prof.log; rc=$?
-echo "rocprof rc=$rc"; cat $O/prof_bench.json
-[ $rc -eq 0 ] || exit $rc
+O=gpurun_out/r1c
 timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_fetch -o fetch -- python bench.py --cpu-budget 0 --steps 8 --warmup 1 > $O/pmc_fetch.json 2> $O/pmc_fetch.log; rc=$?
 echo "pmc fetch rc=$rc"
 [ $rc -eq 0 ] || exit $rc
@@ -18,5 +12,14 @@ timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_write
 echo "pmc write rc=$rc"
 [ $rc -eq 0 ] || exit $rc
 python scripts/pmc_summarize.py $O/pmc_fetch/fetch_counter_collection.csv $O/pmc_write/write_counter_collection.csv \
-  $O/pmc_summary.json $O/pmc_gemv.json --n 4000 --batch 128 \
+  $O/pmc_summary.json $O/pmc_gemv.json --n 4000 --batch 128 --instances 64 \
   --source "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes) of python bench.py --cpu-budget 0 --steps 8 --warmup 1"
+timeout -k 10 600 python bench.py --traffic-json $O/pmc_gemv.json > $O/bench.json 2> $O/bench.err; rc=$?
+echo "bench rc=$rc"; cat $O/bench.json
+[ $rc -eq 0 ] || exit $rc
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o bench -- python bench.py --cpu-budget 0 --traffic-json $O/pmc_gemv.json > $O/prof_bench.json 2> $O/prof.log; rc=$?
+echo "rocprof rc=$rc"; cat $O/prof_bench.json
+[ $rc -eq 0 ] || exit $rc
+timeout -k 10 600 python bench.py --cpu-budget 0 --spass-kind 0 > $O/bench_tile_kernel.json 2> $O/bench_tile_kernel.err; rc=$?
+echo "bench (per-tile S-pass) rc=$rc"; cat $O/bench_tile_kernel.json
+exit $rc

@@ -5,7 +5,8 @@ Usage: python scripts/pmc_summarize.py FETCH_CSV WRITE_CSV OUT_SUMMARY OUT_TRAFF
 gfx950 correction (MI355X_MICROARCH.md, HBM/rocprofv3 section): FETCH_SIZE and WRITE_SIZE are KiB;
 FETCH_SIZE counts half the bytes of wide coalesced streaming reads, so hbm_read = 2*FETCH_SIZE*1024.
 The S-pass traffic figure is taken from the launch with the largest fetch (every instance active),
-divided by its instance count (grid / (tiles x threads)), and compared with the algorithmic bytes of one instance pass.
+divided by its instance count (k_spass_sym: grid / (tiles x threads); k_spass_sup, a persistent grid:
+--instances, the group size), and compared with the algorithmic bytes of one instance pass.
 """
 import argparse
 import csv
@@ -36,6 +37,8 @@ def main():
     ap.add_argument("--n", type=int, default=4000)
     ap.add_argument("--batch", type=int, default=128)
     ap.add_argument("--threads", type=int, default=512, help="k_spass_sym workgroup size (instances = grid/(tiles*threads))")
+    ap.add_argument("--instances", type=int, default=64,
+                    help="instances in the max-traffic k_spass_sup launch (persistent grid: not derivable from it)")
     ap.add_argument("--source", default="")
     a = ap.parse_args()
     fetch, write = load(a.fetch, "FETCH_SIZE"), load(a.write, "WRITE_SIZE")
@@ -54,22 +57,23 @@ def main():
         e = {"launches": len(fetch.get(k, [])), "grid": f[1],
              "max_launch_FETCH_SIZE_KiB": f[2], "max_launch_WRITE_SIZE_KiB": w[2],
              "hbm_read_bytes_corrected": 2 * f[2] * 1024, "hbm_write_bytes": w[2] * 1024}
-        if k == "riptrm::k_spass_sym":
-            inst = f[1] // (nt * (nt + 1) // 2 * a.threads)
+        if k in ("riptrm::k_spass_sym", "riptrm::k_spass_sup"):
+            inst = f[1] // (nt * (nt + 1) // 2 * a.threads) if k.endswith("sym") else a.instances
             e["instances_in_launch"] = inst
             e["algorithmic_bytes_per_launch"] = alg_pass * inst
             e["traffic_over_algorithmic"] = (e["hbm_read_bytes_corrected"] + e["hbm_write_bytes"]) / (alg_pass * inst)
         out["kernels"][k] = e
     with open(a.summary, "w") as fh:
         json.dump(out, fh, indent=1)
-    sp = out["kernels"].get("riptrm::k_spass_sym")
+    kname = "k_spass_sup" if "riptrm::k_spass_sup" in out["kernels"] else "k_spass_sym"
+    sp = out["kernels"].get("riptrm::" + kname)
     if sp:
         with open(a.traffic, "w") as fh:
-            json.dump({"n": a.n, "layout": "sym", "kernel": "k_spass_sym",
+            json.dump({"n": a.n, "layout": "sym", "kernel": kname,
                        "hbm_bytes_per_instance_pass": (sp["hbm_read_bytes_corrected"] + sp["hbm_write_bytes"])
                        / sp["instances_in_launch"],
                        "source": f"{a.summary} (max-traffic launch, {sp['instances_in_launch']} instances)"}, fh, indent=1)
-    print(json.dumps(out["kernels"].get("riptrm::k_spass_sym", {})))
+    print(json.dumps(sp or {}))
 
 
 if __name__ == "__main__":

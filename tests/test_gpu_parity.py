@@ -19,11 +19,14 @@ OPT = dict(tolresid=0.0, maxtime=1e9)
 
 
 def _engine(Z, cap=4096, layout="sym", groups=0):
+    """layout "sym2": the symmetric-tile layout with the super-tile S-pass forced (spass_kind 2)."""
     import engine
     Z = np.asarray(Z)
     if Z.ndim == 2:
         Z = Z[None]
-    eng = engine.NonnegPCABatch(Z.shape[1], Z.shape[0], log_capacity=cap, layout=layout, stream_groups=groups)
+    kind = 2 if layout == "sym2" else 1
+    eng = engine.NonnegPCABatch(Z.shape[1], Z.shape[0], log_capacity=cap, layout=layout.rstrip("2"),
+                                stream_groups=groups, spass_kind=kind)
     eng.load_Z(Z)
     return eng
 
@@ -65,8 +68,8 @@ def test_pack_is_exact_symmetrization(n, layout):
         assert not full[n:, :].any() and not full[:, n:].any()
 
 
-@pytest.mark.parametrize("layout", ["sym", "full"])
-@pytest.mark.parametrize("n,B", [(17, 3), (50, 2), (200, 2), (1000, 3), (4000, 2)])
+@pytest.mark.parametrize("layout", ["sym", "sym2", "full"])
+@pytest.mark.parametrize("n,B", [(17, 3), (50, 2), (200, 2), (300, 3), (1000, 3), (4000, 2)])
 def test_barrier_hessian_matches_oracle(n, B, layout):
     Zs, xs, ys, vs = [], [], [], []
     for b in range(B):
@@ -139,14 +142,15 @@ def test_fixture_reaches_published_residual_on_gpu(fixture_n50):
     assert res[conv][-1] < 2e-14
 
 
-@pytest.mark.parametrize("n,B,K", [(37, 5, 10), (200, 4, 12), (1000, 2, 10)])
-def test_batched_solve_matches_oracle(n, B, K):
+@pytest.mark.parametrize("n,B,K,layout", [(37, 5, 10, "sym"), (200, 4, 12, "sym"), (1000, 2, 10, "sym"),
+                                          (300, 3, 10, "sym2"), (1000, 2, 10, "sym2")])
+def test_batched_solve_matches_oracle(n, B, K, layout):
     """Per instance: identical branches + tests/parity.py values; an instance whose inner
     branches flip at a rounding tie (the CPU oracles show such flips against each other too)
     must still agree at the outer level (parity.compare_outer)."""
     from parity import BranchFlip, compare_outer
     insts = [G.generate_instance(n, 100 + b) for b in range(B)]
-    eng = _engine(np.stack([z for z, _, _ in insts]))
+    eng = _engine(np.stack([z for z, _, _ in insts]), layout=layout)
     res = eng.solve(np.stack([x for _, x, _ in insts]), np.stack([y for _, _, y in insts]), _gpu_opt(maxiter=K))
     xs = res.x.cpu().numpy()
     flips = 0
@@ -379,7 +383,7 @@ def test_run_batch_detects_shared_Z(fixture_n50):
     np.testing.assert_allclose(outs[0].log["residual"], single.log["residual"], rtol=1e-6, atol=1e-13)
 
 
-@pytest.mark.parametrize("layout", ["sym", "full"])
+@pytest.mark.parametrize("layout", ["sym", "sym2", "full"])
 @pytest.mark.parametrize("n,B", [(23, 3), (1000, 2), (4000, 2)])
 def test_ripm_operator_aw_matches_oracle(n, B, layout):
     """RIPM OperatorAw (RIPM.py:485-487) through the same S-pass as HwCur."""
@@ -402,7 +406,7 @@ def test_ripm_operator_aw_matches_oracle(n, B, layout):
 
 
 @pytest.mark.parametrize("sos", [True, False])
-@pytest.mark.parametrize("layout", ["sym", "full"])
+@pytest.mark.parametrize("layout", ["sym", "sym2", "full"])
 def test_exact_repmat_fixture_n50_matches_oracle(fixture_n50, sos, layout):
     """TRS_solver = 'Exact_RepMat' (RIPTRM.py:433-444) on dataset/NonnegPCA/1 point a: HwCur's
     matrix in the Householder frame of x^perp, TRSgep on the device (csrc/riptrm_trs.h), and with
@@ -446,3 +450,43 @@ def test_exact_repmat_reference_defaults_drop_in(fixture_n50):
     with pytest.raises(NotImplementedError):
         Zb, xb, yb = G.generate_instance(120, 1)
         RIPTRM({"maxiter": 1}).run(NonnegPCAProblem(Z=Zb, initialpoint=xb, initialineqLagmult=yb))
+
+
+@pytest.mark.parametrize("n,B", [(2, 3), (129, 4), (300, 5), (1000, 3), (4000, 9)])
+def test_spass_kinds_agree(n, B):
+    """The persistent super-tile S-pass (2 x 2 tiles per unit, partials written in bursts) and the
+    per-tile S-pass give the same S v to rounding (they add the same products in a different,
+    fixed order).  n = 4000, B = 9 is large enough for the automatic choice to pick the super-tile
+    kernel (>= 4 units per CU), n = 300 has a partial last super-block, n = 129 a 32-wide edge."""
+    Zs, xs, ys, vs = [], [], [], []
+    for b in range(B):
+        Z, _, _ = G.generate_instance(n, 40 + b)
+        x, y = _state(n, 50 + b)
+        Zs.append(Z); xs.append(x); ys.append(y)
+        vs.append(np.random.RandomState(60 + b).randn(n))
+    outs = {}
+    for layout in ("sym", "sym2"):
+        eng = _engine(np.stack(Zs), layout=layout)
+        eng.lib.riptrm_set_spass_kind(eng.ctx.h, 0 if layout == "sym" else 2)
+        outs[layout] = eng.hvp(np.stack(xs), np.stack(ys), 0.0123, np.stack(vs)).cpu().numpy()
+        if n == 4000:   # automatic choice
+            eng.lib.riptrm_set_spass_kind(eng.ctx.h, 1)
+            auto = eng.hvp(np.stack(xs), np.stack(ys), 0.0123, np.stack(vs)).cpu().numpy()
+            if layout == "sym2":
+                np.testing.assert_array_equal(auto, outs["sym2"])
+    a, b2 = outs["sym"], outs["sym2"]
+    scale = np.abs(a).max(axis=1, keepdims=True)
+    assert np.max(np.abs(a - b2) / scale) < 1e-13
+    if n > 256:   # more than one super-block: a different summation order really ran
+        assert not np.array_equal(a, b2)
+
+
+def test_super_spass_solve_is_deterministic():
+    """Two solves with the super-tile S-pass give bitwise identical results (no atomics)."""
+    insts = [G.generate_instance(300, 200 + b) for b in range(3)]
+    xs = []
+    for _ in range(2):
+        eng = _engine(np.stack([z for z, _, _ in insts]), layout="sym2")
+        res = eng.solve(np.stack([x for _, x, _ in insts]), np.stack([y for _, _, y in insts]), _gpu_opt(maxiter=6))
+        xs.append(res.x.cpu().numpy())
+    np.testing.assert_array_equal(xs[0], xs[1])
