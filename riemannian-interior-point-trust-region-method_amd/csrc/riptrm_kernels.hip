@@ -371,7 +371,10 @@ constexpr int SUP_MAXU = SUP_OCAP / (2 * SW);   // units per burst at one right-
 typedef double (*sup_red_t)[SP_WAVES][SW];
 
 template <int NR>
-__device__ __forceinline__ void sup_unit(const DevParams& P, int b, int Pq, int Qq, sup_red_t red, double* out) {
+// red: column-sum scratch; one right-hand side uses red[rsel] (alternating between units, so a
+// unit's cross-wave column reduction needs no trailing barrier: the next unit zeroes the other
+// buffer), two use red[0] and red[1] between a leading and a trailing barrier
+__device__ __forceinline__ void sup_unit(const DevParams& P, int b, int Pq, int Qq, sup_red_t red, double* out, int rsel) {
   const int lane = (int)__lane_id();
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int nt = P.nt, wl = P.wl;
@@ -385,11 +388,13 @@ __device__ __forceinline__ void sup_unit(const DevParams& P, int b, int Pq, int 
   for (int k = 0; k < NR; ++k)
 #pragma unroll
     for (int i = 0; i < SB; ++i) racc[k][i][0] = racc[k][i][1] = 0.0;
+  if (NR == 2) __syncthreads();   // the previous unit's reduction may still read either buffer
+  const int r0sel = NR == 2 ? 0 : rsel;
 #pragma unroll
   for (int k = 0; k < NR; ++k)
     for (int jl = 0; jl < SB; ++jl) {
-      red[k][w][jl * TS + 2 * lane] = 0.0;
-      red[k][w][jl * TS + 2 * lane + 1] = 0.0;
+      red[r0sel + k][w][jl * TS + 2 * lane] = 0.0;
+      red[r0sel + k][w][jl * TS + 2 * lane + 1] = 0.0;
     }
 #pragma unroll
   for (int il = 0; il < SB; ++il) {
@@ -440,8 +445,8 @@ __device__ __forceinline__ void sup_unit(const DevParams& P, int b, int Pq, int 
         }
       }
       if (I != J) {   // column part (the diagonal tile is stored whole: row part only)
-        red[0][w][jl * TS + 2 * lane] += c0x;
-        red[0][w][jl * TS + 2 * lane + 1] += c0y;
+        red[r0sel][w][jl * TS + 2 * lane] += c0x;
+        red[r0sel][w][jl * TS + 2 * lane + 1] += c0y;
         if (NR == 2) {
           red[NR - 1][w][jl * TS + 2 * lane] += c1x;
           red[NR - 1][w][jl * TS + 2 * lane + 1] += c1y;
@@ -462,13 +467,13 @@ __device__ __forceinline__ void sup_unit(const DevParams& P, int b, int Pq, int 
   __syncthreads();
   for (int t = threadIdx.x; t < NR * SW; t += SP_THREADS) {
     const int k = t / SW, c = t - k * SW;
-    double cs = red[k][0][c];
+    double cs = red[r0sel + k][0][c];
 #pragma unroll
-    for (int q = 1; q < SP_WAVES; ++q) cs += red[k][q][c];
+    for (int q = 1; q < SP_WAVES; ++q) cs += red[r0sel + k][q][c];
     if (Pq == Qq) out[(2 * k) * SW + c] += cs;   // diagonal unit: both parts land in block Pq
     else out[(2 * k + 1) * SW + c] = cs;
   }
-  __syncthreads();
+  if (NR == 2) __syncthreads();
 }
 
 __device__ __forceinline__ void sup_flush(const DevParams& P, const double* outb, const int (*meta)[2], int nslot,
@@ -501,7 +506,7 @@ __global__ void __launch_bounds__(SP_THREADS, 1) k_spass_sup(DevParams P, int li
   if (zero_cnt >= 0 && blockIdx.x == 0 && threadIdx.x == 0) P.cnt[zero_cnt] = 0;
   const int nact = P.cnt[list_in];
   const int total = nact * P.nsup;
-  int used = 0, nslot = 0;
+  int used = 0, nslot = 0, rsel = 0;
   for (int u = blockIdx.x; u < total; u += gridDim.x) {
     const int slot = u / P.nsup;
     const int32_t e = P.lists[list_in * P.batch + slot];
@@ -513,8 +518,12 @@ __global__ void __launch_bounds__(SP_THREADS, 1) k_spass_sup(DevParams P, int li
       used = 0;
       nslot = 0;
     }
-    if (nr == 2) sup_unit<2>(P, b, Pq, Qq, red, outb + used);
-    else sup_unit<1>(P, b, Pq, Qq, red, outb + used);
+    if (nr == 2) {
+      sup_unit<2>(P, b, Pq, Qq, red, outb + used, 0);
+    } else {
+      sup_unit<1>(P, b, Pq, Qq, red, outb + used, rsel);
+      rsel ^= 1;
+    }
     if (threadIdx.x == 0) {
       meta[nslot][0] = u;
       meta[nslot][1] = nr;
