@@ -165,7 +165,7 @@ def main():
     ap.add_argument("--stream-groups", type=int, default=0, choices=[0, 1, 2],
                     help="instance groups on separate streams (0 = library default)")
     ap.add_argument("--spass-kind", type=int, default=1, choices=[0, 1, 2],
-                    help="sym layout S-pass: 1 = automatic (persistent super-tile kernel at >= 4 units per CU), "
+                    help="sym layout S-pass: 1 = automatic (bind-time calibrated: persistent super-tile kernel or per-tile kernel), "
                          "0 = per-tile kernel only, 2 = super-tile kernel always")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_gemv.json"))
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend (nccl = RCCL)")
@@ -279,10 +279,11 @@ def main():
         achieved = (passes_r0 * bytes_per_pass / gemv_s / 1e9) if gemv_s > 0 else None
         nl = max(1, int(prof["gemv_launches"]))
         traffic = None
-        spass_kernel = "k_spass_sym" if args.spass_kind == 0 else "k_spass_sup"
-        spass_label = ("k_spass_sym (S-pass, one workgroup per symmetric 128x128 tile)" if args.spass_kind == 0 else
+        cal = eng.spass_calibration() if args.layout == "sym" else {}
+        spass_kernel = cal.get("kernel", "k_spass_sym")
+        spass_label = ("k_spass_sym (S-pass, one workgroup per symmetric 128x128 tile)" if spass_kernel == "k_spass_sym" else
                        "k_spass_sup (S-pass, persistent: one workgroup per CU over 2x2-tile units, partial sums "
-                       "written in bursts; k_spass_sym when a launch has < 4 units per CU)")
+                       "written in bursts; k_spass_sym when a launch has fewer units than CUs)")
         if os.path.exists(args.traffic_json) and args.layout == "sym":
             try:
                 tj = json.load(open(args.traffic_json))
@@ -351,7 +352,8 @@ def main():
                                          f"{W + K + 1}..{W + 2 * K} (the timed window replays hipGraphs)")
                        if graph_mode else "HIP events inside the timed window",
                        "state_kernel_ms": prof["state_ms"], "state_launches": prof["state_launches"],
-                       "gemv_launches": prof["gemv_launches"]},
+                       "gemv_launches": prof["gemv_launches"],
+                       "spass_calibration": cal or None},
         }
         print(json.dumps(out), flush=True)
     if world > 1:

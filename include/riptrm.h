@@ -231,12 +231,17 @@ int riptrm_set_stream_groups(riptrm_ctx* ctx, int32_t groups);
  * unless profiling is on.  on = 0 disables it (default 1).  Results do not depend on it. */
 int riptrm_set_graphs(riptrm_ctx* ctx, int32_t on);
 
-/* S-pass kernel of the symmetric-tile layout: 1 = automatic (default: the persistent super-tile
- * kernel, whose partial-sum writes leave the HBM read stream in bursts, once every compute unit
- * gets >= 4 units of 2 x 2 tiles; the per-tile kernel below that), 0 = per-tile kernel only,
- * 2 = super-tile kernel always.  Results agree to rounding (the partial sums are added in a
- * different, still fixed, order). */
+/* S-pass kernel of the symmetric-tile layout: 1 = automatic (default: once every compute unit
+ * gets a unit of 2 x 2 tiles, the persistent super-tile kernel — whose partial-sum writes leave
+ * the HBM read stream in bursts — or the per-tile kernel, whichever streamed faster when
+ * riptrm_nonnegpca_bind timed both on one instance group; the per-tile kernel below that),
+ * 0 = per-tile kernel only, 2 = super-tile kernel always.  Set before riptrm_nonnegpca_bind.
+ * Results agree to rounding (the partial sums are added in a different, still fixed, order). */
 int riptrm_set_spass_kind(riptrm_ctx* ctx, int32_t kind);
+/* Bind-time calibration of the automatic choice: ms per S-pass launch over one instance group of
+ * the per-tile and the super-tile kernel (0 when not calibrated) and the kind in use for large
+ * launches (0 per-tile, 1 super-tile). */
+int riptrm_get_spass_calibration(riptrm_ctx* ctx, double* ms_tile, double* ms_super, int32_t* chosen);
 
 /* ---- measurement ---- */
 /* Enable/disable HIP-event timing of every S-pass (k_gemv) and state-machine (k_state) launch

@@ -35,6 +35,8 @@ struct riptrm_ctx {
   double clock_hz = 1e8;
   int ncu = 256;              // compute units (persistent S-pass grid)
   int sup_req = 1;            // riptrm_set_spass_kind: 0 = tile S-pass only, 1 = automatic, 2 = super-tile always
+  int sup_auto = 1;           // automatic: the super-tile kernel won the bind-time calibration
+  float spass_cal_ms[2] = {0.0f, 0.0f};   // calibration: ms per launch of the per-tile / super-tile kernel
   // optional HIP-event timing of every k_gemv / k_state launch (riptrm_profile_*)
   bool prof = false;
   std::vector<hipEvent_t> ev_pool;

@@ -354,7 +354,7 @@ __global__ void __launch_bounds__(SP_THREADS, 4) k_spass_sym(DevParams P, int li
 }
 
 // ------------------------------------------------------------------------------------------
-// Persistent super-tile S-pass (P.smode = 1; batches with >= 4 units per CU).  Same arithmetic
+// Persistent super-tile S-pass (P.smode = 1; launches with >= 1 unit per CU).  Same arithmetic
 // per stored tile as spass_tile, but one 8-wave workgroup per CU walks units u = g, g + G, ... of
 // SB x SB stored tiles: row sums accumulate over a unit's tile columns, column sums over its
 // tile rows (8 waves, then LDS across waves in wave order), and each unit's two SW-element
@@ -2169,6 +2169,51 @@ int riptrm_nonnegpca_pack(riptrm_ctx* ctx, const double* Z, int64_t ldz, int64_t
   return RIPTRM_OK;
 }
 
+// list 0 = instances [base, base + count), one right-hand side each (S-pass calibration)
+__global__ void k_list_range(DevParams P, int base, int count) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k < count) P.lists[k] = le_make(base + k, 1);
+  if (k == 0) P.cnt[0] = count;
+}
+
+// Which S-pass kernel streams faster on this device for this batch: the two kinds' HBM rates
+// differ by box (the per-tile kernel ran at 5.9-6.7 TB/s in the bench on different boxes of the
+// pool, the super-tile kernel at 6.4-6.5 on all of them), so `automatic` times both once at bind
+// on a full instance group (3 timed launches each after a warm-up) and keeps the faster.
+static int launch_gemv(riptrm_ctx* c, hipStream_t st, int list_in, int zero_cnt, int bound, int smode);
+
+static int calibrate_spass(riptrm_ctx* c) {
+  c->sup_auto = 1;
+  c->spass_cal_ms[0] = c->spass_cal_ms[1] = 0.0f;
+  const int count = c->gsize[0];
+  if (c->P.layout != RIPTRM_LAYOUT_SYMTILE || c->sup_req != 1 || (int64_t)count * c->P.nsup < (int64_t)4 * c->ncu)
+    return RIPTRM_OK;   // calibrated on groups of >= 4 units per CU (the bench's and the headline's case)
+  hipLaunchKernelGGL(k_list_range, dim3((unsigned)((count + 255) / 256)), dim3(256), 0, c->stream, c->P, c->gbase[0], count);
+  HIPCHK(c, hipGetLastError());
+  hipEvent_t ev[4];
+  for (auto& e : ev) HIPCHK(c, hipEventCreate(&e));
+  float ms[2] = {0.0f, 0.0f};
+  int rc = RIPTRM_OK;
+  const bool prof = c->prof;
+  c->prof = false;   // not part of any measured window
+  for (int kind = 0; kind < 2 && rc == RIPTRM_OK; ++kind) {
+    rc = launch_gemv(c, c->stream, 0, -1, count, kind);   // warm-up
+    if (rc == RIPTRM_OK) rc = hipEventRecord(ev[2 * kind], c->stream) == hipSuccess ? RIPTRM_OK : RIPTRM_E_HIP;
+    for (int r = 0; r < 3 && rc == RIPTRM_OK; ++r) rc = launch_gemv(c, c->stream, 0, -1, count, kind);
+    if (rc == RIPTRM_OK) rc = hipEventRecord(ev[2 * kind + 1], c->stream) == hipSuccess ? RIPTRM_OK : RIPTRM_E_HIP;
+  }
+  if (rc == RIPTRM_OK && hipEventSynchronize(ev[3]) == hipSuccess && hipEventElapsedTime(&ms[0], ev[0], ev[1]) == hipSuccess &&
+      hipEventElapsedTime(&ms[1], ev[2], ev[3]) == hipSuccess)
+    c->sup_auto = ms[1] <= ms[0] ? 1 : 0;
+  c->spass_cal_ms[0] = ms[0] / 3.0f;
+  c->spass_cal_ms[1] = ms[1] / 3.0f;
+  c->prof = prof;
+  for (auto& e : ev) (void)hipEventDestroy(e);
+  if (rc) return rc;
+  HIPCHK(c, hipMemsetAsync(c->P.cnt, 0, 4 * sizeof(int32_t), c->stream));
+  return RIPTRM_OK;
+}
+
 int riptrm_nonnegpca_bind(riptrm_ctx* ctx, const double* S, int32_t n, int32_t batch, int32_t layout,
                           int64_t inst_stride, void* workspace, int64_t workspace_bytes, int32_t cap) {
   if (!ctx) return RIPTRM_E_ARG;
@@ -2227,15 +2272,17 @@ int riptrm_nonnegpca_bind(riptrm_ctx* ctx, const double* S, int32_t n, int32_t b
   ctx->bound = true;
   ctx->solving = false;
   ctx->pver++;
-  return RIPTRM_OK;
+  return calibrate_spass(ctx);
 }
 
 // S-pass kind for a launch over at most `bound` instances: the persistent super-tile kernel once
-// every CU gets >= 4 units of work; below that the per-tile kernel spreads the few instances'
-// tiles over more workgroups (latency).  The state kernel that gathers the pass gets the same mode.
+// every CU gets a unit of work (and the bind-time calibration preferred it); below that the
+// per-tile kernel spreads the few instances' tiles over more workgroups (latency).  The state
+// kernel that gathers the pass gets the same mode.
 static int spass_mode(const riptrm_ctx* c, int bound) {
   if (c->P.layout != RIPTRM_LAYOUT_SYMTILE || c->sup_req == 0) return 0;
-  return ((int64_t)bound * c->P.nsup >= (int64_t)4 * c->ncu || c->sup_req == 2) ? 1 : 0;
+  if (c->sup_req == 2) return 1;
+  return ((int64_t)bound * c->P.nsup >= (int64_t)c->ncu && c->sup_auto) ? 1 : 0;
 }
 
 static DevParams params_for(const riptrm_ctx* c, int smode) {
@@ -2560,6 +2607,14 @@ int riptrm_set_stream_groups(riptrm_ctx* ctx, int32_t groups) {
   if (!ctx || groups < 0 || groups > 2) return RIPTRM_E_ARG;
   if (ctx->solving) return fail(ctx, RIPTRM_E_STATE, "set_stream_groups: call before riptrm_nonnegpca_bind");
   ctx->groups_req = groups;
+  return RIPTRM_OK;
+}
+
+int riptrm_get_spass_calibration(riptrm_ctx* ctx, double* ms_tile, double* ms_super, int32_t* chosen) {
+  if (!ctx || !ms_tile || !ms_super || !chosen) return RIPTRM_E_ARG;
+  *ms_tile = ctx->spass_cal_ms[0];
+  *ms_super = ctx->spass_cal_ms[1];
+  *chosen = ctx->P.layout != RIPTRM_LAYOUT_SYMTILE || ctx->sup_req == 0 ? 0 : (ctx->sup_req == 2 ? 1 : ctx->sup_auto);
   return RIPTRM_OK;
 }
 

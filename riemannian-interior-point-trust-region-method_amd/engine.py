@@ -376,6 +376,14 @@ class NonnegPCABatch:
         out[:, :self.n] = t.to(self.device)
         return out
 
+    def spass_calibration(self) -> Dict[str, Any]:
+        """riptrm_get_spass_calibration: the bind-time timing behind the automatic S-pass choice."""
+        t, u, k = ctypes.c_double(), ctypes.c_double(), ctypes.c_int32()
+        self.ctx.check(self.lib.riptrm_get_spass_calibration(self.ctx.h, ctypes.byref(t), ctypes.byref(u),
+                                                             ctypes.byref(k)), "riptrm_get_spass_calibration")
+        return {"ms_per_launch_tile": t.value, "ms_per_launch_super": u.value,
+                "kernel": "k_spass_sup" if k.value == 1 else "k_spass_sym"}
+
     def hvp(self, x, y, mu: float, v) -> torch.Tensor:
         """HwCur(v) at (x, y, mu) for every instance (RIPTRM.py:729)."""
         assert self.bound

@@ -74,6 +74,7 @@ SIGNATURES: Dict[str, tuple] = {
     "riptrm_set_stream_groups": (c_int32, [c_void_p, c_int32]),
     "riptrm_set_graphs": (c_int32, [c_void_p, c_int32]),
     "riptrm_set_spass_kind": (c_int32, [c_void_p, c_int32]),
+    "riptrm_get_spass_calibration": (c_int32, [c_void_p, ctypes.POINTER(c_double), ctypes.POINTER(c_double), P_int32]),
     "riptrm_profile_enable": (c_int32, [c_void_p, c_int32]),
     "riptrm_profile_read": (c_int32, [c_void_p, ctypes.POINTER(c_double), ctypes.POINTER(c_int64),
                                       ctypes.POINTER(c_double), ctypes.POINTER(c_int64)]),
