@@ -408,40 +408,53 @@ __device__ __forceinline__ void sup_unit(const DevParams& P, int b, int Pq, int 
       const int colsT = (J == nt - 1) ? wl : TS;
       const bool cl = 2 * lane < colsT;
       const double* __restrict__ T = Sb + sym_off(I, J, nt, wl);
+      // vector entries first, then the wave's 16 S rows (both 8-row batches) with no branches
+      // (clamped addresses + selects), so the compiler can wait for batch 0 while batch 1 is
+      // still in flight (one workgroup per CU has no sibling workgroups to cover its latency)
       const dbl2 vj0 = *(const dbl2*)(v0 + J * TS + 2 * lane);
       dbl2 vj1 = dbl2{0.0, 0.0};
       if (NR == 2) vj1 = *(const dbl2*)(v1 + J * TS + 2 * lane);
+      double vi0[ROWS], vi1[ROWS];
+#pragma unroll
+      for (int k = 0; k < ROWS; ++k) {
+        vi0[k] = v0[I * TS + w * ROWS + k];
+        vi1[k] = NR == 2 ? v1[I * TS + w * ROWS + k] : 0.0;
+      }
+      __builtin_amdgcn_sched_barrier(0);   // keep the vector loads ahead of the S rows
       double c0x = 0.0, c0y = 0.0, c1x = 0.0, c1y = 0.0;
-#pragma unroll 1
+      dbl2 sv2[ROWS / 8][8];
+#pragma unroll
+      for (int rb = 0; rb < ROWS / 8; ++rb)
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const int row = w * ROWS + rb * 8 + k;
+          const bool ok = cl && row < rowsT;   // corner / narrow tiles: not stored
+          const dbl2 x = __builtin_nontemporal_load((const dbl2*)(T + (row < rowsT ? row : 0) * colsT + (cl ? 2 * lane : 0)));
+          sv2[rb][k] = ok ? x : dbl2{0.0, 0.0};
+        }
+#pragma unroll
       for (int rb = 0; rb < ROWS / 8; ++rb) {
         const int r0 = w * ROWS + rb * 8;
-        if (r0 >= rowsT) break;   // corner tiles: rows beyond wl are not stored (wave-uniform)
-        dbl2 sv[8];
-#pragma unroll
-        for (int k = 0; k < 8; ++k)
-          sv[k] = cl ? __builtin_nontemporal_load((const dbl2*)(T + (r0 + k) * colsT + 2 * lane)) : dbl2{0.0, 0.0};
+        if (r0 >= rowsT) break;   // wave-uniform
+        const dbl2 (&sv)[8] = sv2[rb];
         double a[8];
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
-          const double vi0 = v0[I * TS + r0 + k];
+          const double vi = vi0[rb * 8 + k];
           a[k] = __builtin_fma(sv[k].y, vj0.y, sv[k].x * vj0.x);
-          c0x = __builtin_fma(sv[k].x, vi0, c0x);
-          c0y = __builtin_fma(sv[k].y, vi0, c0y);
+          c0x = __builtin_fma(sv[k].x, vi, c0x);
+          c0y = __builtin_fma(sv[k].y, vi, c0y);
         }
-        const double s0 = reduce_scatter8(a);
-        if (rb == 0) racc[0][il][0] += s0;
-        else racc[0][il][1] += s0;
+        racc[0][il][rb] += reduce_scatter8(a);
         if (NR == 2) {
 #pragma unroll
           for (int k = 0; k < 8; ++k) {
-            const double vi1 = v1[I * TS + r0 + k];
+            const double vi = vi1[rb * 8 + k];
             a[k] = __builtin_fma(sv[k].y, vj1.y, sv[k].x * vj1.x);
-            c1x = __builtin_fma(sv[k].x, vi1, c1x);
-            c1y = __builtin_fma(sv[k].y, vi1, c1y);
+            c1x = __builtin_fma(sv[k].x, vi, c1x);
+            c1y = __builtin_fma(sv[k].y, vi, c1y);
           }
-          const double s1 = reduce_scatter8(a);
-          if (rb == 0) racc[NR - 1][il][0] += s1;
-          else racc[NR - 1][il][1] += s1;
+          racc[NR - 1][il][rb] += reduce_scatter8(a);
         }
       }
       if (I != J) {   // column part (the diagonal tile is stored whole: row part only)
