@@ -164,9 +164,9 @@ def main():
                     help="subproblem solver (Exact_RepMat: manifold.dim <= 96, with the second-order test)")
     ap.add_argument("--stream-groups", type=int, default=0, choices=[0, 1, 2],
                     help="instance groups on separate streams (0 = library default)")
-    ap.add_argument("--spass-kind", type=int, default=1, choices=[0, 1, 2, 3],
+    ap.add_argument("--spass-kind", type=int, default=1, choices=[0, 1, 2],
                     help="sym layout S-pass: 1 = automatic (bind-time calibrated: persistent super-tile kernel or per-tile kernel), "
-                         "0 = per-tile kernel only, 2 = super-tile kernel always, 3 = super-tile with the earlier unit body (A/B)")
+                         "0 = per-tile kernel only, 2 = super-tile kernel always")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_gemv.json"))
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend (nccl = RCCL)")
     ap.add_argument("--same-device", action="store_true",

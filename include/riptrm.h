@@ -235,8 +235,7 @@ int riptrm_set_graphs(riptrm_ctx* ctx, int32_t on);
  * gets a unit of 2 x 2 tiles, the persistent super-tile kernel — whose partial-sum writes leave
  * the HBM read stream in bursts — or the per-tile kernel, whichever streamed faster when
  * riptrm_nonnegpca_bind timed both on one instance group; the per-tile kernel below that),
- * 0 = per-tile kernel only, 2 = super-tile kernel always, 3 = super-tile kernel with the earlier
- * batched-row unit body (kept for A/B timing).  Set before riptrm_nonnegpca_bind.
+ * 0 = per-tile kernel only, 2 = super-tile kernel always.  Set before riptrm_nonnegpca_bind.
  * Results agree to rounding (the partial sums are added in a different, still fixed, order). */
 int riptrm_set_spass_kind(riptrm_ctx* ctx, int32_t kind);
 /* Bind-time calibration of the automatic choice: ms per S-pass launch over one instance group of

@@ -489,96 +489,6 @@ __device__ __forceinline__ void sup_unit(const DevParams& P, int b, int Pq, int 
   if (NR == 2) __syncthreads();
 }
 
-// One right-hand side (every tCG pass): the unit's SB x SB tiles fully unrolled, the next tile's
-// vector entries and 16 S rows issued before the current tile is reduced (two register sets), and
-// no branches between them (absent tiles / rows / columns read one clamped 16-byte address and are
-// zeroed by selects), so the compiler's vmcnt waits let the next tile stream behind the current
-// tile's arithmetic.
-struct SupTile {
-  dbl2 sv[TS / SP_WAVES];
-  dbl2 vj;
-  double vi[TS / SP_WAVES];
-  double fo;   // 1: off-diagonal tile (column part counts), 0: diagonal or absent
-};
-
-__device__ __forceinline__ void sup_unit1(const DevParams& P, int b, int Pq, int Qq, sup_red_t red, double* out, int rsel) {
-  const int lane = (int)__lane_id();
-  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int nt = P.nt, wl = P.wl;
-  constexpr int ROWS = TS / SP_WAVES;
-  const double* __restrict__ Sb = P.S + (int64_t)b * P.inst_stride;
-  const double* __restrict__ v0 = vp(P, V_IN0, b);
-  const int rrow = 4 * ((lane >> 5) & 1) + 2 * ((lane >> 4) & 1) + ((lane >> 3) & 1);
-  auto fetch = [&](int t, SupTile& R) {
-    const int I = SB * Pq + t / SB, J = SB * Qq + t % SB;
-    const bool tv = I < nt && J < nt && J >= I;
-    const int Ic = tv ? I : 0, Jc = tv ? J : 0;
-    const int colsT = (Jc == nt - 1) ? wl : TS;
-    const int rowsT = tv ? ((Ic == nt - 1) ? wl : TS) : 0;
-    const bool cl = 2 * lane < colsT;
-    const double* __restrict__ T = Sb + sym_off(Ic, Jc, nt, wl);
-    R.vj = *(const dbl2*)(v0 + Jc * TS + 2 * lane);
-#pragma unroll
-    for (int k = 0; k < ROWS; ++k) R.vi[k] = v0[Ic * TS + w * ROWS + k];
-    R.fo = (tv && I != J) ? 1.0 : 0.0;
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int k = 0; k < ROWS; ++k) {
-      const int row = w * ROWS + k;
-      const bool ok = cl && row < rowsT;
-      const dbl2 x = __builtin_nontemporal_load((const dbl2*)(T + (ok ? row * colsT + 2 * lane : 0)));
-      R.sv[k] = ok ? x : dbl2{0.0, 0.0};
-    }
-  };
-  double racc[SB][2], cax[SB], cay[SB];
-#pragma unroll
-  for (int i = 0; i < SB; ++i) racc[i][0] = racc[i][1] = cax[i] = cay[i] = 0.0;
-  SupTile R[2];
-  fetch(0, R[0]);
-#pragma unroll
-  for (int t = 0; t < SB * SB; ++t) {
-    if (t + 1 < SB * SB) fetch(t + 1, R[(t + 1) & 1]);
-    const SupTile& C = R[t & 1];
-    const int il = t / SB, jl = t % SB;
-    double cx = 0.0, cy = 0.0;
-#pragma unroll
-    for (int rb = 0; rb < ROWS / 8; ++rb) {
-      double a[8];
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const dbl2 sv = C.sv[rb * 8 + k];
-        const double vi = C.vi[rb * 8 + k];
-        a[k] = __builtin_fma(sv.y, C.vj.y, sv.x * C.vj.x);
-        cx = __builtin_fma(sv.x, vi, cx);
-        cy = __builtin_fma(sv.y, vi, cy);
-      }
-      racc[il][rb] += reduce_scatter8(a);
-    }
-    cax[jl] += C.fo * cx;
-    cay[jl] += C.fo * cy;
-  }
-#pragma unroll
-  for (int jl = 0; jl < SB; ++jl) {
-    red[rsel][w][jl * TS + 2 * lane] = cax[jl];
-    red[rsel][w][jl * TS + 2 * lane + 1] = cay[jl];
-  }
-  if ((lane & 7) == 0) {
-#pragma unroll
-    for (int il = 0; il < SB; ++il) {
-      out[il * TS + w * ROWS + rrow] = racc[il][0];
-      out[il * TS + w * ROWS + 8 + rrow] = racc[il][1];
-    }
-  }
-  __syncthreads();
-  for (int t = threadIdx.x; t < SW; t += SP_THREADS) {
-    double cs = red[rsel][0][t];
-#pragma unroll
-    for (int q = 1; q < SP_WAVES; ++q) cs += red[rsel][q][t];
-    if (Pq == Qq) out[t] += cs;   // diagonal unit: both parts land in block Pq
-    else out[SW + t] = cs;
-  }
-}
-
 __device__ __forceinline__ void sup_flush(const DevParams& P, const double* outb, const int (*meta)[2], int nslot,
                                           int list_in) {
   __syncthreads();
@@ -624,8 +534,7 @@ __global__ void __launch_bounds__(SP_THREADS, 1) k_spass_sup(DevParams P, int li
     if (nr == 2) {
       sup_unit<2>(P, b, Pq, Qq, red, outb + used, 0);
     } else {
-      if (P.smode == 2) sup_unit<1>(P, b, Pq, Qq, red, outb + used, rsel);   // A/B: previous unit code
-      else sup_unit1(P, b, Pq, Qq, red, outb + used, rsel);
+      sup_unit<1>(P, b, Pq, Qq, red, outb + used, rsel);
       rsel ^= 1;
     }
     if (threadIdx.x == 0) {
@@ -2385,7 +2294,7 @@ int riptrm_nonnegpca_bind(riptrm_ctx* ctx, const double* S, int32_t n, int32_t b
 // kernel that gathers the pass gets the same mode.
 static int spass_mode(const riptrm_ctx* c, int bound) {
   if (c->P.layout != RIPTRM_LAYOUT_SYMTILE || c->sup_req == 0) return 0;
-  if (c->sup_req >= 2) return 1;
+  if (c->sup_req == 2) return 1;
   return ((int64_t)bound * c->P.nsup >= (int64_t)c->ncu && c->sup_auto) ? 1 : 0;
 }
 
@@ -2417,8 +2326,7 @@ static int launch_gemv(riptrm_ctx* c, hipStream_t st, int list_in, int zero_cnt,
   } else if (sym && smode) {
     const int64_t units = (int64_t)bound * c->P.nsup;
     const unsigned grid = (unsigned)(units < c->ncu ? units : c->ncu);
-    hipLaunchKernelGGL(k_spass_sup, dim3(grid), dim3(SP_THREADS), 0, st, params_for(c, c->sup_req == 3 ? 2 : 1), list_in,
-                       zero_cnt);
+    hipLaunchKernelGGL(k_spass_sup, dim3(grid), dim3(SP_THREADS), 0, st, params_for(c, 1), list_in, zero_cnt);
   } else if (sym)
     hipLaunchKernelGGL(k_spass_sym, dim3((unsigned)blocks), dim3(SP_THREADS), 0, st, c->P, list_in, zero_cnt);
   else
@@ -2724,7 +2632,7 @@ int riptrm_get_spass_calibration(riptrm_ctx* ctx, double* ms_tile, double* ms_su
 }
 
 int riptrm_set_spass_kind(riptrm_ctx* ctx, int32_t kind) {
-  if (!ctx || kind < 0 || kind > 3) return RIPTRM_E_ARG;
+  if (!ctx || kind < 0 || kind > 2) return RIPTRM_E_ARG;
   ctx->sup_req = kind;
   ctx->pver++;   // a captured graph holds the old kernel
   return RIPTRM_OK;
