@@ -20,10 +20,12 @@ def load(path, counter):
         for r in csv.DictReader(fh):
             if r["Counter_Name"] != counter:
                 continue
-            name = r["Kernel_Name"]
+            name = r["Kernel_Name"].split("(")[0]
+            if name.startswith("void "):
+                name = name[5:]
+            name = name.split("<")[0]   # template instantiations count under their kernel's name
             if not name.startswith("riptrm::"):
                 continue
-            name = name.split("(")[0]
             rows[name].append((int(r["Dispatch_Id"]), int(r["Grid_Size"]), float(r["Counter_Value"])))
     return rows
 
