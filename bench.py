@@ -53,91 +53,134 @@ def trs_options(trs: str) -> dict:
     return {"TRS_solver": "tCG", "second_order_stationarity": False}
 
 
-def cpu_baseline(n: int, warmup: int, steps: int, budget_s: float, trs: str = "tCG"):
-    """Oracle (vectorised NumPy) on one instance: outer iterations warmup+1..warmup+steps."""
-    import numpy as np
+def window_positions(warmup: int, steps: int, cycle: int):
+    """Solve positions (1..cycle) of the timed outer iterations warmup+1..warmup+steps: instances
+    restart after every `cycle` outer iterations (riptrm_options.restart_every), so iteration k of
+    the GPU window is outer iteration ((k - 1) mod cycle) + 1 of a solve."""
+    c = cycle if cycle > 0 else warmup + steps
+    return [((k - 1) % c) + 1 for k in range(warmup + 1, warmup + steps + 1)]
+
+
+def _oracle_positions(n: int, seed: int, pmax: int, budget_s: float, trs: str, structured: bool = False):
+    """Run the oracle on one instance through outer iteration pmax (or until the budget ends);
+    returns the solver time of every completed outer iteration (evaluation excluded, as
+    RIPTRM.py:932-941) keyed by its position 1..pmax."""
     from oracle import nonnegpca_gen as G
     from oracle import riptrm_oracle as O
-    try:
-        from threadpoolctl import threadpool_info
-        cores = max([d.get("num_threads", 1) for d in threadpool_info() if d.get("user_api") == "blas"] or [1])
-    except Exception:
-        cores = int(os.environ.get("OMP_NUM_THREADS", "1"))
-    Z, x0, y0 = G.generate_instance(n, G.SEED0)
-    t_start = time.time()
-    orc = O.RIPTRMOracle(dict(maxiter=warmup + steps, tolresid=0.0, maxtime=1e12, manviofun=O.sphere_manvio,
-                              **trs_options(trs)), deadline=t_start + budget_s)
-    P = O.NonnegPCAVectorized(Z)
-    complete = True
+    Z, x0, y0 = G.generate_instance(n, seed)
+    orc = O.RIPTRMOracle(dict(maxiter=pmax, tolresid=0.0, maxtime=1e12, manviofun=O.sphere_manvio,
+                              **trs_options(trs)), deadline=time.time() + budget_s)
+    P = O.NonnegPCAStructured(Z) if structured else O.NonnegPCAVectorized(Z)
     try:
         orc.run(P, x0, y0)
     except O.BudgetExceeded:
-        complete = False
-    heads = orc.outer_heads
-    if warmup not in heads:
+        pass
+    h = orc.outer_heads
+    return {p: h[p] - h[p - 1] for p in range(1, pmax + 1) if p in h and p - 1 in h}
+
+
+def _window_rate(durs, positions):
+    """outer iterations/s over exactly the GPU window's multiset of positions (None if incomplete)."""
+    if any(p not in durs for p in positions):
         return None
-    last = max(k for k in heads if k <= warmup + steps)
-    done = last - warmup
-    if done <= 0:
+    t = sum(durs[p] for p in positions)
+    return len(positions) / t if t > 0 else None
+
+
+def _blas_threads():
+    try:
+        from threadpoolctl import threadpool_info
+        return max([d.get("num_threads", 1) for d in threadpool_info() if d.get("user_api") == "blas"] or [1])
+    except Exception:
+        return int(os.environ.get("OMP_NUM_THREADS", "1"))
+
+
+def cpu_baseline(n: int, positions, budget_s: float, trs: str = "tCG"):
+    """SURVEY.md §8d variant (V), one process with all BLAS threads: the oracle (vectorised NumPy +
+    OpenBLAS dsymv) on one instance, timed over the GPU window's own outer iterations."""
+    from oracle import nonnegpca_gen as G
+    durs = _oracle_positions(n, G.SEED0, max(positions), budget_s, trs)
+    rate = _window_rate(durs, positions)
+    if rate is None:
         return None
-    el = heads[last] - heads[warmup]
-    return {"value": done / el, "unit": "outer iterations/s", "cores": int(cores), "kind": "port",
-            "sample": (f"oracle/riptrm_oracle.py NonnegPCAVectorized, 1 instance n={n} (reference generator "
-                       f"recipe, seed {G.SEED0}), outer iterations {warmup + 1}..{last} "
-                       f"({done} timed, {el:.1f} s, evaluation time excluded as RIPTRM.py:932-941; "
-                       f"{'complete' if complete else 'budget-truncated'} window), NumPy + OpenBLAS dsymv (one triangle of S), {cores} threads"
+    cores = _blas_threads()
+    return {"value": rate, "unit": "outer iterations/s", "cores": int(cores), "kind": "port",
+            "sample": (f"oracle/riptrm_oracle.py NonnegPCAVectorized, 1 instance n={n} (reference generator recipe, "
+                       f"seed {G.SEED0}), timed over the GPU window's own outer-iteration positions "
+                       f"{_pos_text(positions)} (evaluation time excluded as RIPTRM.py:932-941), NumPy + OpenBLAS dsymv "
+                       f"(one triangle of S), {cores} threads"
                        + (", TRS_solver=Exact_RepMat (trs_oracle: 2n x 2n pencil, scipy.linalg.eig)" if trs != "tCG" else ""))}
+
+
+def _pos_text(positions):
+    """Compact text of a position multiset, e.g. '6..20 + 1..5'."""
+    runs, start, prev = [], positions[0], positions[0]
+    for p in positions[1:]:
+        if p == prev + 1:
+            prev = p
+            continue
+        runs.append((start, prev))
+        start = prev = p
+    runs.append((start, prev))
+    return " + ".join(f"{a}..{b}" if a != b else f"{a}" for a, b in runs)
 
 
 def _cpu_worker(argv):
     """One single-threaded oracle instance (run in its own process by cpu_baseline_pool)."""
-    n, seed, warmup, steps, budget, trs = int(argv[0]), int(argv[1]), int(argv[2]), int(argv[3]), float(argv[4]), argv[5]
-    from oracle import nonnegpca_gen as G
-    from oracle import riptrm_oracle as O
-    Z, x0, y0 = G.generate_instance(n, seed)
-    orc = O.RIPTRMOracle(dict(maxiter=warmup + steps, tolresid=0.0, maxtime=1e12, manviofun=O.sphere_manvio,
-                              **trs_options(trs)), deadline=time.time() + budget)
-    try:
-        orc.run(O.NonnegPCAVectorized(Z), x0, y0)
-    except O.BudgetExceeded:
-        pass
-    heads = orc.outer_heads
-    out = {"done": 0, "el": 0.0, "complete": False}
-    if warmup in heads:
-        last = max(k for k in heads if k <= warmup + steps)
-        out = {"done": last - warmup, "el": heads[last] - heads[warmup], "complete": last == warmup + steps}
-    print(json.dumps(out), flush=True)
+    n, seed, pmax, budget, trs = int(argv[0]), int(argv[1]), int(argv[2]), float(argv[3]), argv[4]
+    durs = _oracle_positions(n, seed, pmax, budget, trs)
+    print(json.dumps({str(k): v for k, v in durs.items()}), flush=True)
 
 
-def cpu_baseline_pool(n: int, warmup: int, steps: int, budget_s: float, procs: int, trs: str = "tCG"):
-    """SURVEY.md §8d's other CPU variant: `procs` single-threaded oracle processes, one instance each
-    (seeds SEED0 + i), run concurrently; aggregate = sum over processes of (outer iterations done /
-    their own elapsed time) over the same window."""
+def cpu_baseline_pool(n: int, positions, budget_s: float, procs: int, trs: str = "tCG"):
+    """SURVEY.md §8d variant (V) as a pool: `procs` single-threaded oracle processes, one instance
+    each (seeds SEED0 + i), run concurrently, each timed over the GPU window's own positions;
+    aggregate = sum of the per-process rates, over processes that completed the whole window."""
     import subprocess
     from oracle import nonnegpca_gen as G
     env = dict(os.environ, OMP_NUM_THREADS="1", OPENBLAS_NUM_THREADS="1", MKL_NUM_THREADS="1")
     ps = [subprocess.Popen([sys.executable, os.path.abspath(__file__), "--cpu-worker", str(n), str(G.SEED0 + i),
-                            str(warmup), str(steps), str(budget_s), trs], stdout=subprocess.PIPE,
+                            str(max(positions)), str(budget_s), trs], stdout=subprocess.PIPE,
                            stderr=subprocess.DEVNULL, env=env, text=True) for i in range(procs)]
-    rates, done_all, complete = [], 0, 0
+    rates = []
     for p in ps:
         out, _ = p.communicate(timeout=budget_s + 600)
         try:
-            r = json.loads(out.strip().splitlines()[-1])
+            durs = {int(k): v for k, v in json.loads(out.strip().splitlines()[-1]).items()}
         except Exception:
             continue
-        if r["done"] > 0 and r["el"] > 0:
-            rates.append(r["done"] / r["el"])
-            done_all += r["done"]
-            complete += 1 if r.get("complete") else 0
+        r = _window_rate(durs, positions)
+        if r is not None:
+            rates.append(r)
     if not rates:
         return None
-    return {"value": sum(rates), "unit": "outer iterations/s", "cores": int(procs), "kind": "port",
+    # every process runs the same amount of work, so the complete ones are a fair sample; scale the
+    # aggregate to all `procs` cores (incomplete processes ran on cores too)
+    agg = sum(rates) / len(rates) * procs
+    return {"value": agg, "unit": "outer iterations/s", "cores": int(procs), "kind": "port",
             "sample": (f"oracle/riptrm_oracle.py NonnegPCAVectorized, {procs} single-threaded processes, one instance n={n} "
-                       f"each (seeds {G.SEED0}..{G.SEED0 + procs - 1}), outer iterations {warmup + 1}..{warmup + steps} within a "
-                       f"{budget_s:.0f} s budget ({done_all} outer iterations in all, {complete}/{procs} complete windows; a "
-                       f"truncated window misses its most expensive last iterations, so the rate is an upper bound), "
-                       f"aggregate of per-process rates, evaluation time excluded as RIPTRM.py:932-941")}
+                       f"each (seeds {G.SEED0}..{G.SEED0 + procs - 1}), each timed over the GPU window's own positions "
+                       f"{_pos_text(positions)} within a {budget_s:.0f} s budget; {len(rates)}/{procs} processes completed the "
+                       f"window, aggregate = mean complete per-process rate x {procs}, evaluation time excluded as "
+                       f"RIPTRM.py:932-941")}
+
+
+def cpu_reference_structured(n: int, budget_s: float):
+    """SURVEY.md §8d variant (R): the oracle's per-constraint restatement of the reference's wiring
+    (NonnegPCAStructured: n constraint closures, per-constraint Gx/Gxaj/hessLagrangian loops as
+    RIPTRM.py:475-571 runs them; no autograd, so a lower bound on the reference's own cost), one
+    instance, outer iterations 1..k completed within the budget.  A stated extra, not the
+    like-for-like baseline."""
+    from oracle import nonnegpca_gen as G
+    durs = _oracle_positions(n, G.SEED0, 20, budget_s, "tCG", structured=True)
+    if not durs:
+        return None
+    k = max(durs)
+    t = sum(durs[p] for p in range(1, k + 1))
+    return {"value": k / t, "unit": "outer iterations/s", "cores": 1, "kind": "port",
+            "sample": (f"oracle/riptrm_oracle.py NonnegPCAStructured (reference-structured, per-constraint loops), "
+                       f"1 instance n={n} seed {G.SEED0}, outer iterations 1..{k} ({t:.1f} s) within a {budget_s:.0f} s "
+                       f"budget")}
 
 
 def main():
@@ -153,7 +196,13 @@ def main():
     ap.add_argument("--cycle", type=int, default=20, help="outer iterations per solve before restart")
     ap.add_argument("--dim", type=int, default=4000, help="problem dimension n")
     ap.add_argument("--batch", type=int, default=128, help="instances per GPU")
-    ap.add_argument("--cpu-budget", type=float, default=25.0, help="seconds of CPU-baseline sampling (0 = skip)")
+    ap.add_argument("--cpu-budget", type=float, default=60.0,
+                    help="seconds allowed for the BLAS-threaded CPU baseline (0 = skip every CPU leg)")
+    ap.add_argument("--cpu-pool-budget", type=float, default=150.0,
+                    help="seconds allowed for each single-threaded pool process to complete the window")
+    ap.add_argument("--ref-structured-dim", type=int, default=1000,
+                    help="n of the reference-structured CPU variant (R) reported as an extra (0 = skip)")
+    ap.add_argument("--ref-structured-budget", type=float, default=20.0)
     ap.add_argument("--cpu-procs", type=int, default=16,
                     help="also time this many single-threaded oracle processes (0 = only the BLAS-threaded one)")
     ap.add_argument("--seed0", type=int, default=20251212)
@@ -164,9 +213,10 @@ def main():
                     help="subproblem solver (Exact_RepMat: manifold.dim <= 96, with the second-order test)")
     ap.add_argument("--stream-groups", type=int, default=0, choices=[0, 1, 2],
                     help="instance groups on separate streams (0 = library default)")
-    ap.add_argument("--spass-kind", type=int, default=1, choices=[0, 1, 2],
-                    help="sym layout S-pass: 1 = automatic (bind-time calibrated: persistent super-tile kernel or per-tile kernel), "
-                         "0 = per-tile kernel only, 2 = super-tile kernel always")
+    ap.add_argument("--spass-kind", type=int, default=1, choices=[0, 1, 2, 3],
+                    help="sym layout S-pass: 1 = automatic (rule on n alone: persistent super-tile kernel for n >= 2561, "
+                         "per-tile kernel below; batch-independent bits), 0 = per-tile kernel only, 2 = super-tile kernel "
+                         "always, 3 = super-tile for launches with >= 1 unit per CU if a bind-time timing preferred it")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_gemv.json"))
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend (nccl = RCCL)")
     ap.add_argument("--same-device", action="store_true",
@@ -208,7 +258,7 @@ def main():
 
     n, B, W, K = args.dim, args.batch, args.warmup, args.steps
     eng = engine.NonnegPCABatch(n, B, log_capacity=2048, layout=args.layout, stream_groups=args.stream_groups,
-                                spass_kind=args.spass_kind)
+                                spass_kind=args.spass_kind, drain_logs=False)
     nS = 1 if args.layout == "shared" else B
     log(f"rank {rank}/{world}: generating {B} instances n={n} ({nS * eng.inst_stride * 8 / 1e9:.1f} GB S)")
     # global instance ids owned by this rank: rank, rank+world, ... (seed seed0 + id)
@@ -283,7 +333,7 @@ def main():
         spass_kernel = cal.get("kernel", "k_spass_sym")
         spass_label = ("k_spass_sym (S-pass, one workgroup per symmetric 128x128 tile)" if spass_kernel == "k_spass_sym" else
                        "k_spass_sup (S-pass, persistent: one workgroup per CU over 2x2-tile units, partial sums "
-                       "written in bursts; k_spass_sym when a launch has fewer units than CUs)")
+                       "written in bursts)")
         if os.path.exists(args.traffic_json) and args.layout == "sym":
             try:
                 tj = json.load(open(args.traffic_json))
@@ -301,26 +351,42 @@ def main():
                         "kernel": "k_spass_mm (shared-S multi-start S-pass, v_mfma_f64_16x16x4_f64)",
                         "flops_per_launch": flops / nl, "avg_launch_us": prof["gemv_ms"] * 1e3 / nl}
         else:
+            # the same launches priced with the bytes symmetry strictly requires (one triangle incl. the
+            # diagonal + the vectors): what a layout without padded diagonal / edge tiles would move
+            min_bytes = 8.0 * n * (n + 1) / 2 + 16.0 * n
+            ach_min = (passes_r0 * min_bytes / gemv_s / 1e9) if gemv_s > 0 else None
             roofline = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
                         "traffic": traffic,
+                        "bytes_definition": ("stored S per instance-pass in the symmetric-tile layout (upper-triangle "
+                                             "128x128 tiles incl. the whole diagonal tiles and the 32-column-padded "
+                                             f"edge: {s_bytes / 1e6:.2f} MB at n={n}) + 16 n vector bytes")
+                        if args.layout == "sym" else "8 n^2 (full S) + 16 n vector bytes per instance-pass",
+                        "frac_min_bytes": (ach_min / HBM_PEAK_GBS) if ach_min else None,
+                        "min_bytes_definition": "n(n+1)/2 * 8 (one triangle incl. the diagonal) + 16 n per instance-pass",
                         "kernel": spass_label if args.layout == "sym" else "k_gemv (S-pass, full matrix)",
                         "bytes_per_launch": passes_r0 * bytes_per_pass / nl,
                         "avg_launch_us": prof["gemv_ms"] * 1e3 / nl}
         cpu = None
         if args.cpu_budget > 0 and world == 1:
-            log("CPU baseline (oracle) ...")
-            cpu = cpu_baseline(n, W, min(K, max(1, args.cycle - W)), args.cpu_budget, args.trs)
+            positions = window_positions(W, K, args.cycle)
+            log(f"CPU baseline (oracle) over positions {_pos_text(positions)} ...")
+            cpu = cpu_baseline(n, positions, args.cpu_budget, args.trs)
             if args.cpu_procs > 0:
                 log(f"CPU baseline, {args.cpu_procs} single-threaded processes ...")
-                pool = cpu_baseline_pool(n, W, min(K, max(1, args.cycle - W)), max(args.cpu_budget, 40.0),
-                                         args.cpu_procs, args.trs)
+                pool = cpu_baseline_pool(n, positions, args.cpu_pool_budget, args.cpu_procs, args.trs)
                 if pool is not None:
                     alt = cpu
                     if cpu is None or pool["value"] > cpu["value"]:
                         cpu, alt = pool, cpu
                     if alt is not None:   # report the better variant, name the other
                         cpu["other_variant"] = {"value": alt["value"], "cores": alt["cores"], "sample": alt["sample"]}
+            if cpu is not None:
+                cpu["gpu_over_cpu"] = (outer_all / T) / cpu["value"]
+                if args.ref_structured_dim > 0:
+                    log(f"CPU reference-structured variant (R), n={args.ref_structured_dim} ...")
+                    cpu["extra_reference_structured"] = cpu_reference_structured(args.ref_structured_dim,
+                                                                                 args.ref_structured_budget)
         out = {
             "metric": METRIC,
             "value": outer_all / T,
@@ -336,8 +402,9 @@ def main():
             "data": "synthetic (reference generator recipe src/NonnegPCA/generator.py:9-65, drawn on device)",
             "config": {"workload": (f"NonnegPCA n={n}, one Z with {B} initial points per GPU (multi-start, "
                                     f"the problem_initialpoint axis; SURVEY 8d variant)") if args.layout == "shared"
-                                   else (f"NonnegPCA n={n}, batch of {B} independent instances per GPU "
-                                         f"(BASELINE configs[2]; configs[3] at 8 GPUs)")
+                                   else (f"NonnegPCA n={n}, batch of {B} independent instances per GPU"
+                                         + (" (BASELINE configs[2]; configs[3] at 8 GPUs)" if (n, B) == (4000, 128) else
+                                            " (BASELINE configs[1])" if (n, B) == (1000, 1) else ""))
                                    + ("" if args.trs == "tCG" else ", TRS_solver=Exact_RepMat + second-order test"),
                        "trs_solver": args.trs,
                        "n": n, "batch_per_gpu": B, "global_batch": B * world,

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define RIPTRM_ABI_VERSION 4
+#define RIPTRM_ABI_VERSION 5
 
 /* status codes */
 #define RIPTRM_OK 0
@@ -108,12 +108,19 @@ enum riptrm_log_field {
 };
 #define RIPTRM_LOG_NFIELDS 32
 
+/* Log slots.  Record k of an instance (k counted from the last riptrm_log_rebase, k = LOG_COUNT -
+ * LOG_BASE at the time it is written) goes to slot k while k < capacity; past that the first
+ * capacity/2 slots keep the earliest records and the remaining T = capacity - capacity/2 slots
+ * form a ring holding the latest T (slot capacity/2 + (k - capacity/2) mod T), LOG_OVERFLOW
+ * counts the records dropped from the middle.  riptrm_log_rebase between solve_advance calls
+ * (after the host has copied the slots out) keeps a log of any length complete. */
+
 /* Per-instance result record: RIPTRM_STAT_NFIELDS doubles. */
 enum riptrm_stat_field {
     RIPTRM_STAT_OUTER_ITERS = 0, RIPTRM_STAT_INNER_ITERS, RIPTRM_STAT_TCG_ITERS, RIPTRM_STAT_PASSES,
     RIPTRM_STAT_STOP_CODE, RIPTRM_STAT_STOP_RUNTIME, RIPTRM_STAT_FINAL_RESIDUAL, RIPTRM_STAT_LOG_COUNT,
     RIPTRM_STAT_LOG_OVERFLOW, RIPTRM_STAT_PHASE, RIPTRM_STAT_MU, RIPTRM_STAT_TR_RADIUS,
-    RIPTRM_STAT_TCG_LAST_J, RIPTRM_STAT_TCG_LAST_STOP, RIPTRM_STAT_ERROR,
+    RIPTRM_STAT_TCG_LAST_J, RIPTRM_STAT_TCG_LAST_STOP, RIPTRM_STAT_ERROR, RIPTRM_STAT_LOG_BASE,
     RIPTRM_STAT_NFIELDS_USED
 };
 #define RIPTRM_STAT_NFIELDS 16
@@ -218,6 +225,10 @@ int riptrm_solve_begin(riptrm_ctx* ctx, const riptrm_options* opt, const double*
  * `outer_target` + 1 (pass INT32_MAX to run to completion).  Synchronises and returns the
  * number of instances still running in *n_active. */
 int riptrm_solve_advance(riptrm_ctx* ctx, int32_t steps, int32_t outer_target, int32_t* n_active);
+/* Mark every log record written so far as drained (LOG_BASE <- LOG_COUNT for every instance of the
+ * NonnegPCA batch): the next record of each instance goes to slot 0 again.  Call between
+ * riptrm_solve_advance calls, after copying the records out.  Asynchronous. */
+int riptrm_log_rebase(riptrm_ctx* ctx);
 /* Device timestamps for timing windows: wall-clock ticks per second of the device clock. */
 double riptrm_device_clock_hz(riptrm_ctx* ctx);
 
@@ -231,16 +242,20 @@ int riptrm_set_stream_groups(riptrm_ctx* ctx, int32_t groups);
  * unless profiling is on.  on = 0 disables it (default 1).  Results do not depend on it. */
 int riptrm_set_graphs(riptrm_ctx* ctx, int32_t on);
 
-/* S-pass kernel of the symmetric-tile layout: 1 = automatic (default: once every compute unit
- * gets a unit of 2 x 2 tiles, the persistent super-tile kernel — whose partial-sum writes leave
- * the HBM read stream in bursts — or the per-tile kernel, whichever streamed faster when
- * riptrm_nonnegpca_bind timed both on one instance group; the per-tile kernel below that),
- * 0 = per-tile kernel only, 2 = super-tile kernel always.  Set before riptrm_nonnegpca_bind.
- * Results agree to rounding (the partial sums are added in a different, still fixed, order). */
+/* S-pass kernel of the symmetric-tile layout: 1 = automatic (default: the persistent super-tile
+ * kernel — whose partial-sum writes leave the HBM read stream in bursts — for n >= 2561, where an
+ * instance has >= 64 units of 2 x 2 tiles, the per-tile kernel below; the rule depends on n only,
+ * so an instance gives bitwise identical results alone or inside any batch, run after run),
+ * 0 = per-tile kernel only, 2 = super-tile kernel always, 3 = the super-tile kernel for launches
+ * that give every compute unit a unit of work if a bind-time timing of both kernels on one
+ * instance group preferred it (fastest on a given box; the choice — and so the last bits of the
+ * results — can then depend on the box and on how many instances are active).  Set before
+ * riptrm_nonnegpca_bind.  Results agree to rounding (the partial sums are added in a different,
+ * still fixed, order). */
 int riptrm_set_spass_kind(riptrm_ctx* ctx, int32_t kind);
-/* Bind-time calibration of the automatic choice: ms per S-pass launch over one instance group of
- * the per-tile and the super-tile kernel (0 when not calibrated) and the kind in use for large
- * launches (0 per-tile, 1 super-tile). */
+/* ms per S-pass launch over one instance group of the per-tile and the super-tile kernel (0 unless
+ * kind 3 timed them at bind) and the kernel a launch over the whole batch uses (0 per-tile,
+ * 1 super-tile). */
 int riptrm_get_spass_calibration(riptrm_ctx* ctx, double* ms_tile, double* ms_super, int32_t* chosen);
 
 /* ---- measurement ---- */

@@ -135,9 +135,18 @@ class NonnegPCAStructured:
     ineq      src/NonnegPCA/coordinator.py:66-75   g_i(x) = -x_i  (egrad -e_i, ehess 0)
     wrappers  src/solver/utils.py:93-173           rgrad_i = P_x(egrad_i); rhess_i = e2rh(...)
     helpers   src/solver/RIPTRM.py:475-571         gradLagrangefun/hessLagrangefun/Gxfun/Gxajfun
+
+    ``lincomb`` / ``embedded`` select the reference's ``do_euclidean_lincomb=True`` /
+    ``is_euclidean_embedded=True`` branches (RIPTRM.py:480-482, :514-517, :543-545, :567-568):
+    Euclidean linear combinations converted once, and <egrad g_i, dx> in place of <rgrad g_i, dx>.
+    On the Sphere both give the same operators as the default branches on tangent vectors (the
+    conversions are linear; <-e_i, dx> = <P_x(-e_i), dx> when x^T dx = 0), so they differ from the
+    default only by rounding (tests/test_oracle.py::test_euclidean_branch_options_agree).
     """
 
-    def __init__(self, Z: np.ndarray):
+    def __init__(self, Z: np.ndarray, lincomb: bool = False, embedded: bool = False):
+        self.lincomb = bool(lincomb)
+        self.embedded = bool(embedded)
         self.Z = np.asarray(Z, dtype=np.float64)
         self.n = self.Z.shape[0]
         self.manifold = Sphere(self.n)
@@ -175,6 +184,7 @@ class NonnegPCAStructured:
         cons = [mk(i) for i in range(n)]
         self.ineq = [c[0] for c in cons]
         self.ineq_egrad = [c[1] for c in cons]
+        self.ineq_ehess = [c[2] for c in cons]
         self.ineq_rgrad = [c[3] for c in cons]
         self.ineq_rhess = [c[4] for c in cons]
 
@@ -185,32 +195,57 @@ class NonnegPCAStructured:
     def slack(self, x):
         return np.array([-g(x) for g in self.ineq])
 
-    # RIPTRM.py:475-489 (do_euclidean_lincomb=False)
+    # RIPTRM.py:457-473 egradLagrangefun
+    def egradlag(self, x, y):
+        vec = self.euclidean_gradient(x)
+        ev = [-eg(x) for eg in self.ineq_egrad]
+        for i in range(len(y)):
+            vec = vec - y[i] * ev[i]
+        return vec
+
+    # RIPTRM.py:475-489
     def gradlag(self, x, y):
+        if self.lincomb:
+            return self.manifold.euclidean_to_riemannian_gradient(x, self.egradlag(x, y))
         vec = self.riemannian_gradient(x)
         gv = [-grad(x) for grad in self.ineq_rgrad]
         for i in range(len(y)):
             vec = vec - y[i] * gv[i]
         return vec
 
-    # RIPTRM.py:491-523 (False branch)
+    # RIPTRM.py:491-523
     def hesslag(self, x, y, dx):
+        if self.lincomb:   # :514-517
+            vec = self.euclidean_hessian(x, dx)
+            ehv = [-eh(x, dx) for eh in self.ineq_ehess]
+            for i in range(len(y)):
+                vec = vec - y[i] * ehv[i]
+            return self.manifold.euclidean_to_riemannian_hessian(x, self.egradlag(x, y), vec, dx)
         vec = self.riemannian_hessian(x, dx)
         hv = [-h(x, dx) for h in self.ineq_rhess]
         for i in range(len(y)):
             vec = vec - y[i] * hv[i]
         return vec
 
-    # RIPTRM.py:525-551 (False branch)
+    # RIPTRM.py:525-551
     def Gx(self, x, v):
+        if self.lincomb:   # :543-545
+            ev = [-eg(x) for eg in self.ineq_egrad]
+            vec = self.manifold.zero_vector(x)
+            for idx in range(len(ev)):
+                vec = vec + v[idx] * ev[idx]
+            return self.manifold.euclidean_to_riemannian_gradient(x, vec)
         gv = [-grad(x) for grad in self.ineq_rgrad]
         vec = self.manifold.zero_vector(x)
         for idx in range(len(gv)):
             vec = vec + v[idx] * gv[idx]
         return vec
 
-    # RIPTRM.py:553-571 (False branch)
+    # RIPTRM.py:553-571
     def Gxaj(self, x, dx):
+        if self.embedded:   # :567-568
+            ev = [-eg(x) for eg in self.ineq_egrad]
+            return np.array([self.manifold.inner_product(x, g, dx) for g in ev])
         gv = [-grad(x) for grad in self.ineq_rgrad]
         return np.array([self.manifold.inner_product(x, g, dx) for g in gv])
 
@@ -786,7 +821,10 @@ def ripm_operator_aw_vectorized(Z, x, z, s, v):
 
 
 def solve(Z, x0, y0, option=None, structured=False, clock=time.time) -> OracleResult:
-    P = NonnegPCAStructured(Z) if structured else NonnegPCAVectorized(Z)
+    o = option or {}
+    P = (NonnegPCAStructured(Z, lincomb=o.get('do_euclidean_lincomb', False),
+                             embedded=o.get('is_euclidean_embedded', False))
+         if structured else NonnegPCAVectorized(Z))
     return RIPTRMOracle(option, clock=clock).run(P, x0, y0)
 
 

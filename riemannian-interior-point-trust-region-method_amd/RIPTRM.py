@@ -14,7 +14,12 @@ eqLagmult)`` whose ``log`` has the reference's columns, one row per inner iterat
   closures cannot execute on the GPU;
 * ``manviofun`` must be 0 or the problem's simulator function (NonnegPCA ``||x|| - 1``,
   StableIdentification's symmetry / definiteness violation); ``callbackfun`` and wandb are not
-  supported.
+  supported;
+* ``do_euclidean_lincomb`` (RIPTRM.py:480-482, :514-517, :543-545) is accepted for both problems:
+  the device evaluates the Lagrangian's derivatives in closed form, which is what both branches
+  compute (the conversions are linear), up to rounding.  ``is_euclidean_embedded``
+  (:567-568) is accepted for NonnegPCA (on the Sphere <egrad g_i, dx> = <rgrad g_i, dx> for
+  tangent dx) and raises for StableIdentification (a different operator on the SPD factors).
 
 ``run_batch(problems)`` solves many instances of the same size at once (the reference runs its
 Hydra multi-run axis one after another, ``config_simulation.yaml:35-42``).
@@ -60,11 +65,16 @@ class RIPTRM(Solver):
         return self.run_batch([problem])[0]
 
     def run_batch(self, problems: Sequence[Any], log_capacity: int = 8192) -> List[Output]:
+        """NonnegPCA: the device log is drained to the host whenever it is half full, so logs of
+        any length are complete.  StableIdentification runs each solve in one launch: its log
+        keeps the first log_capacity/2 and the latest records (default capacity 65536 rows per
+        instance, bounded to ~8 GB per batch)."""
         problems = list(problems)
         if not problems:
             return []
         if all(isinstance(p, SIProblem) for p in problems):
-            return self._run_batch_si(problems, log_capacity)
+            cap = max(log_capacity, min(65536, int(8e9 // (256 * len(problems)))))
+            return self._run_batch_si(problems, cap)
         for p in problems:
             if not isinstance(p, NonnegPCAProblem):
                 raise NotImplementedError(
@@ -102,10 +112,19 @@ class RIPTRM(Solver):
             if p.has_eqconstraints:
                 warnings.warn("Equality constraints detecred. Currently, RIPTRM does not support equality "
                               "constraints and will completely ignore them.", Warning)
+        if self.option.get('is_euclidean_embedded'):
+            # RIPTRM.py:567-568: <egrad g_i, dx> in the manifold metric; on the SPD factors that is
+            # tr(X^-1 G X^-1 dX), not <rgrad g_i, dx> = tr(sym(G) dX): a different operator
+            raise NotImplementedError("is_euclidean_embedded=True changes Gxajfun on the SPD factors and is not "
+                                      "implemented for StableIdentification on the device")
         B = len(problems)
         eng = SIBatch(d, N_, m, B, log_capacity=log_capacity)
-        same = all(p.X is p0.X or (np.array_equal(p.X, p0.X) and np.array_equal(p.XP, p0.XP)
-                                   and np.array_equal(p.cons, p0.cons) and p.h == p0.h) for p in problems)
+
+        def _same(a, b):   # `is` only as a per-field fast path
+            return a is b or np.array_equal(a, b)
+
+        same = all(_same(p.X, p0.X) and _same(p.XP, p0.XP) and _same(p.cons, p0.cons) and p.h == p0.h
+                   for p in problems)
         if same:   # the problem_initialpoint axis: one data set, many starts
             eng.load(p0.X, p0.XP, p0.h, p0.cons)
         else:
@@ -131,8 +150,11 @@ class RIPTRM(Solver):
             reason = res.stopping_criterion(b)
             if reason is not None:
                 opt["stoppingcriterion"] = reason
-            if int(res.stat(b, "LOG_OVERFLOW")) > 0:
-                warnings.warn(f"instance {b}: log capacity {log_capacity} exceeded; later rows dropped")
+            dropped = int(res.dropped[b]) if res.dropped is not None else 0
+            if dropped > 0:
+                warnings.warn(f"instance {b}: log capacity {log_capacity} exceeded within one device launch; "
+                              f"{dropped} records from the middle of the log were dropped (the first and the "
+                              f"latest records are kept)")
             log = res.log(b)
             if self.option.get("verbosity", 0) == 1:
                 for it, c, r, m, st in zip(log["iteration"], log["cost"], log["residual"], log["mu"],

@@ -34,8 +34,9 @@ struct riptrm_ctx {
   hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_pass[2] = {nullptr, nullptr};
   double clock_hz = 1e8;
   int ncu = 256;              // compute units (persistent S-pass grid)
-  int sup_req = 1;            // riptrm_set_spass_kind: 0 = tile S-pass only, 1 = automatic, 2 = super-tile always
-  int sup_auto = 1;           // automatic: the super-tile kernel won the bind-time calibration
+  int sup_req = 1;            // riptrm_set_spass_kind: 0 = tile S-pass only, 1 = automatic (fixed rule),
+                              // 2 = super-tile always, 3 = automatic with bind-time timing
+  int sup_auto = 1;           // kind 3: the super-tile kernel won the bind-time calibration
   float spass_cal_ms[2] = {0.0f, 0.0f};   // calibration: ms per launch of the per-tile / super-tile kernel
   // optional HIP-event timing of every k_gemv / k_state launch (riptrm_profile_*)
   bool prof = false;

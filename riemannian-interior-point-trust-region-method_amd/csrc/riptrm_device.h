@@ -55,10 +55,10 @@ enum St : int {
   // last inner_info (for save_inner_iteration == False rows)
   ST_I_HAS, ST_I_NUM, ST_I_STATUS, ST_I_TR, ST_I_DXTYPE, ST_I_NORMDX, ST_I_MINX, ST_I_MINY,
   ST_I_COMPL, ST_I_HASRATIO, ST_I_RATIO, ST_I_RU, ST_I_DC, ST_I_HASMIN, ST_I_MINEIG,
-  ST_ERROR,
+  ST_ERROR, ST_LOG_BASE,
   ST_N_USED
 };
-constexpr int ST_N = 64;
+constexpr int ST_N = 72;
 constexpr int ST_HOT = ST_HOT_END;
 static_assert(ST_HOT_END <= 40, "hot scalar slots overflow into cold ones");
 static_assert(ST_N_USED <= ST_N, "state slots overflow");
@@ -78,6 +78,15 @@ struct Layout {
 };
 
 inline int64_t round_up(int64_t a, int64_t m) { return (a + m - 1) / m * m; }
+
+// log slot of record k (counted from the last rebase) in a log of `cap` slots: linear while
+// k < cap, then the first cap/2 slots keep the head and the rest is a ring of the latest records
+// (include/riptrm.h "Log slots").  cap >= 1.
+__host__ __device__ inline int64_t log_slot(int64_t k, int64_t cap) {
+  if (k < cap) return k;
+  const int64_t h = cap / 2, t = cap - h;
+  return h + (k - h) % t;
+}
 inline int64_t ld_of(int32_t n) { return round_up(n > 0 ? n : 1, TS); }
 inline int64_t rows_of(int32_t n) { return round_up(n > 0 ? n : 1, 32); }  // k_pack writes 32-row sub-tiles
 inline int32_t nt_of(int32_t n) { return (int32_t)(ld_of(n) / TS); }

@@ -988,6 +988,7 @@ struct MachineT {
       o[RIPTRM_STAT_TCG_LAST_J] = s[ST_J];
       o[RIPTRM_STAT_TCG_LAST_STOP] = s[ST_TCG_STOP];
       o[RIPTRM_STAT_ERROR] = g[ST_ERROR];
+      o[RIPTRM_STAT_LOG_BASE] = g[ST_LOG_BASE];
     }
   }
 
@@ -1086,8 +1087,11 @@ struct MachineT {
     if (tid == 0) {
       const double* c = cold;
       const int cnt = (int)c[ST_LOG_COUNT];
-      if (cnt < P.opt.log_capacity && cnt < P.cap) {
-        double* L = P.log + ((int64_t)b * P.cap + cnt) * RIPTRM_LOG_NFIELDS;
+      const int64_t k = (int64_t)(c[ST_LOG_COUNT] - c[ST_LOG_BASE]);
+      const int64_t capl = P.opt.log_capacity < P.cap ? P.opt.log_capacity : P.cap;
+      if (capl > 0) {
+        if (k >= capl) cold[ST_LOG_OVERFLOW] += 1.0;   // a record leaves the middle of the log
+        double* L = P.log + ((int64_t)b * P.cap + log_slot(k, capl)) * RIPTRM_LOG_NFIELDS;
         L[RIPTRM_LOG_ITERATION] = s[ST_OUTER_IT];
         L[RIPTRM_LOG_TIME] = (cnt == 0) ? 0.0 : (t_now - s[ST_T_START]) / P.clock_hz;
         L[RIPTRM_LOG_COST] = ev[0];
@@ -1948,6 +1952,15 @@ __global__ void __launch_bounds__(ST_THREADS) k_state(DevParams P, int full, int
   M.finish_write();
 }
 
+// riptrm_log_rebase: every record logged so far counts as drained
+__global__ void __launch_bounds__(256) k_log_rebase(DevParams P) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= P.batch) return;
+  double* c = P.st + (int64_t)b * ST_N;
+  c[ST_LOG_BASE] = c[ST_LOG_COUNT];
+  P.stats[(int64_t)b * RIPTRM_STAT_NFIELDS + RIPTRM_STAT_LOG_BASE] = c[ST_LOG_COUNT];
+}
+
 // initialise a solve: x0/y0 -> X/Y, scalars
 __global__ void __launch_bounds__(256) k_init(DevParams P, const double* x0, const double* y0, int64_t ldv,
                                               const double* mu, const double* delta, int mode) {
@@ -2198,17 +2211,20 @@ __global__ void k_list_range(DevParams P, int base, int count) {
   if (k == 0) P.cnt[0] = count;
 }
 
-// Which S-pass kernel streams faster on this device for this batch: the two kinds' HBM rates
-// differ by box (the per-tile kernel ran at 5.9-6.7 TB/s in the bench on different boxes of the
-// pool, the super-tile kernel at 6.4-6.5 on all of them), so `automatic` times both once at bind
-// on a full instance group (3 timed launches each after a warm-up) and keeps the faster.
+// Optional (riptrm_set_spass_kind(3) only): which S-pass kernel streams faster on this device for
+// this batch.  The two kinds' HBM rates differ by box (the per-tile kernel ran at 5.9-6.7 TB/s in
+// the bench on different boxes of the pool, the super-tile kernel at 6.2-6.5 on all of them), so
+// kind 3 times both once at bind on a full instance group (3 timed launches each after a warm-up)
+// and keeps the faster.  The two kernels add the same products in different fixed orders, so a
+// timing-based choice could make two runs of the same solve differ in the last bits; the default
+// (kind 1) therefore uses the fixed rule of spass_mode and never times anything.
 static int launch_gemv(riptrm_ctx* c, hipStream_t st, int list_in, int zero_cnt, int bound, int smode);
 
 static int calibrate_spass(riptrm_ctx* c) {
   c->sup_auto = 1;
   c->spass_cal_ms[0] = c->spass_cal_ms[1] = 0.0f;
   const int count = c->gsize[0];
-  if (c->P.layout != RIPTRM_LAYOUT_SYMTILE || c->sup_req != 1 || (int64_t)count * c->P.nsup < (int64_t)4 * c->ncu)
+  if (c->P.layout != RIPTRM_LAYOUT_SYMTILE || c->sup_req != 3 || (int64_t)count * c->P.nsup < (int64_t)4 * c->ncu)
     return RIPTRM_OK;   // calibrated on groups of >= 4 units per CU (the bench's and the headline's case)
   hipLaunchKernelGGL(k_list_range, dim3((unsigned)((count + 255) / 256)), dim3(256), 0, c->stream, c->P, c->gbase[0], count);
   HIPCHK(c, hipGetLastError());
@@ -2297,14 +2313,22 @@ int riptrm_nonnegpca_bind(riptrm_ctx* ctx, const double* S, int32_t n, int32_t b
   return calibrate_spass(ctx);
 }
 
-// S-pass kind for a launch over at most `bound` instances: the persistent super-tile kernel once
-// every CU gets a unit of work (and the bind-time calibration preferred it); below that the
-// per-tile kernel spreads the few instances' tiles over more workgroups (latency).  The state
-// kernel that gathers the pass gets the same mode.
+// S-pass kind of the symmetric-tile layout.  Kind 1 (default): the persistent super-tile kernel
+// for problems of at least SUP_MIN_UNITS 2 x 2-tile units per instance (n >= 2561), the per-tile
+// kernel below that.  The rule depends on n alone, never on how many instances are active: the
+// two kernels add the same products in different fixed orders, so a rule that followed the
+// active count would make an instance's last bits depend on the other instances of its batch
+// (and on when they finish).  With it, an instance gives bitwise the same results alone or inside
+// any batch, run after run.  Kind 3 keeps the older rule (super-tile once every CU gets a unit,
+// if the bind-time timing preferred it; fastest, not batch-independent).  The state kernel that
+// gathers the pass gets the same mode.
+constexpr int SUP_MIN_UNITS = 64;
 static int spass_mode(const riptrm_ctx* c, int bound) {
   if (c->P.layout != RIPTRM_LAYOUT_SYMTILE || c->sup_req == 0) return 0;
   if (c->sup_req == 2) return 1;
-  return ((int64_t)bound * c->P.nsup >= (int64_t)c->ncu && c->sup_auto) ? 1 : 0;
+  if (c->sup_req == 1) return c->P.nsup >= SUP_MIN_UNITS ? 1 : 0;
+  const bool wide = (int64_t)bound * c->P.nsup >= (int64_t)c->ncu;
+  return (wide && c->sup_auto) ? 1 : 0;
 }
 
 static DevParams params_for(const riptrm_ctx* c, int smode) {
@@ -2636,12 +2660,12 @@ int riptrm_get_spass_calibration(riptrm_ctx* ctx, double* ms_tile, double* ms_su
   if (!ctx || !ms_tile || !ms_super || !chosen) return RIPTRM_E_ARG;
   *ms_tile = ctx->spass_cal_ms[0];
   *ms_super = ctx->spass_cal_ms[1];
-  *chosen = ctx->P.layout != RIPTRM_LAYOUT_SYMTILE || ctx->sup_req == 0 ? 0 : (ctx->sup_req == 2 ? 1 : ctx->sup_auto);
+  *chosen = spass_mode(ctx, ctx->P.batch);
   return RIPTRM_OK;
 }
 
 int riptrm_set_spass_kind(riptrm_ctx* ctx, int32_t kind) {
-  if (!ctx || kind < 0 || kind > 2) return RIPTRM_E_ARG;
+  if (!ctx || kind < 0 || kind > 3) return RIPTRM_E_ARG;
   ctx->sup_req = kind;
   ctx->pver++;   // a captured graph holds the old kernel
   return RIPTRM_OK;
@@ -2674,6 +2698,15 @@ int riptrm_profile_read(riptrm_ctx* ctx, double* gemv_ms, int64_t* gemv_launches
   if (gemv_launches) *gemv_launches = ctx->gemv_n;
   if (state_ms) *state_ms = ctx->state_ms;
   if (state_launches) *state_launches = ctx->state_n;
+  return RIPTRM_OK;
+}
+
+int riptrm_log_rebase(riptrm_ctx* ctx) {
+  if (!ctx) return RIPTRM_E_ARG;
+  if (!ctx->bound) return fail(ctx, RIPTRM_E_STATE, "log_rebase: bind first");
+  HIPCHK(ctx, hipSetDevice(ctx->device));
+  hipLaunchKernelGGL(k_log_rebase, dim3((unsigned)((ctx->P.batch + 255) / 256)), dim3(256), 0, ctx->stream, ctx->P);
+  HIPCHK(ctx, hipGetLastError());
   return RIPTRM_OK;
 }
 

@@ -837,8 +837,10 @@ struct Eng {
                           double t_now, double t_start, double& count, double& overflow) {
     if (l == 0) {
       const int cnt = (int)count;
-      if (cnt < P.opt.log_capacity && cnt < P.cap) {
-        double* L = P.log + ((int64_t)b * P.cap + cnt) * RIPTRM_LOG_NFIELDS;
+      const int64_t capl = P.opt.log_capacity < P.cap ? P.opt.log_capacity : P.cap;
+      if (capl > 0) {
+        if (cnt >= capl) overflow += 1.0;   // a record leaves the middle of the log (head + latest kept)
+        double* L = P.log + ((int64_t)b * P.cap + riptrm::log_slot(cnt, capl)) * RIPTRM_LOG_NFIELDS;
         for (int k = 0; k < RIPTRM_LOG_NFIELDS; ++k) L[k] = 0.0;
         L[RIPTRM_LOG_ITERATION] = outer_it;
         L[RIPTRM_LOG_TIME] = (cnt == 0) ? 0.0 : (t_now - t_start) / P.clock_hz;

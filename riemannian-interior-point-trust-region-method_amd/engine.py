@@ -43,6 +43,20 @@ STATUS_NAMES = {0: None, 1: "initial", 2: "converged", 3: "primal_infeasible", 4
                 5: "unsuccessful", 6: "max-time-exceeded", 7: "max-iter-exceeded"}
 RU_NAMES = {0: None, 1: "reduced", 2: "expanded", 3: "unchanged"}
 
+def assemble_log(slots: np.ndarray, k: int, cap: int):
+    """Records of one instance in chronological order from its device log slots, given k records
+    written since the last rebase into a log of `cap` slots (include/riptrm.h "Log slots": slot k
+    while k < cap, then the first cap/2 slots keep the head and the rest is a ring of the latest
+    records).  Returns (rows, dropped): dropped = records lost from the middle (0 unless k > cap)."""
+    if k <= cap:
+        return slots[:k], 0
+    h = cap // 2
+    t = cap - h
+    k0 = k - t                                   # oldest record still in the ring
+    order = [h + ((k0 - h + i) % t) for i in range(t)]
+    return np.concatenate([slots[:h], slots[order]]), k - cap
+
+
 def dxtype_name(code: int) -> str:
     """inner_info['dxtype'] (RIPTRM.py:734): TRSgep's type or f"tCG_{stop_tCG}"."""
     return TRS_NAMES[code] if code in TRS_NAMES else f"tCG_{TCG_NAMES[code]}"
@@ -200,7 +214,7 @@ class NonnegPCABatch:
     problem_initialpoint axis), S-pass on the fp64 matrix cores."""
 
     def __init__(self, n: int, batch: int, device: Optional[int] = None, log_capacity: int = 4096,
-                 layout: str = "sym", stream_groups: int = 0, spass_kind: int = 1):
+                 layout: str = "sym", stream_groups: int = 0, spass_kind: int = 1, drain_logs: bool = True):
         if not torch.cuda.is_available():
             raise RuntimeError("NonnegPCABatch needs a ROCm GPU (gfx950); there is no CPU fallback")
         if n < 2 or batch < 1:
@@ -229,6 +243,10 @@ class NonnegPCABatch:
         self.ws_bytes = nbytes
         self.bound = False
         self._keep: List[torch.Tensor] = []
+        # log records copied to the host by drain_logs() (riptrm_log_rebase), per instance
+        self.drain = bool(drain_logs)
+        self._drained: List[List[np.ndarray]] = [[] for _ in range(self.batch)]
+        self._dropped = np.zeros(self.batch, dtype=np.int64)
 
     # ---- views into the workspace -------------------------------------------------------
     def _view(self, kind: int, shape, dtype=torch.float64):
@@ -247,6 +265,30 @@ class NonnegPCABatch:
     def log_rows(self, count: int) -> np.ndarray:
         lg = self._view(5, (self.batch, self.cap, NLOG))
         return lg[:, :max(0, min(count, self.cap))].cpu().numpy()
+
+    def _pending_logs(self, st: np.ndarray):
+        """Per instance: the records written since the last rebase, in order, and how many of them
+        the slots dropped."""
+        k = (st[:, C["RIPTRM_STAT_LOG_COUNT"]] - st[:, C["RIPTRM_STAT_LOG_BASE"]]).astype(np.int64)
+        cap = min(self.cap, int(self.ro.c_opt.log_capacity)) if getattr(self, "ro", None) else self.cap
+        kmax = int(k.max()) if self.batch else 0
+        slots = self.log_rows(kmax)
+        out = []
+        for b in range(self.batch):
+            out.append(assemble_log(slots[b], int(k[b]), cap) if k[b] > 0 else (slots[b, :0], 0))
+        return out
+
+    def drain_logs(self):
+        """Copy every instance's new log records to the host and rebase the device log
+        (riptrm_log_rebase), so a solve of any length keeps its whole log."""
+        torch.cuda.synchronize(self.device)
+        st = self.stats()
+        for b, (rows, dropped) in enumerate(self._pending_logs(st)):
+            if len(rows):
+                self._drained[b].append(rows.copy())
+            self._dropped[b] += dropped
+        self._sync_stream()
+        self.ctx.check(self.lib.riptrm_log_rebase(self.ctx.h), "riptrm_log_rebase")
 
     # ---- data ---------------------------------------------------------------------------
     def _sync_stream(self):
@@ -377,7 +419,8 @@ class NonnegPCABatch:
         return out
 
     def spass_calibration(self) -> Dict[str, Any]:
-        """riptrm_get_spass_calibration: the bind-time timing behind the automatic S-pass choice."""
+        """riptrm_get_spass_calibration: the S-pass kernel of wide launches (and, for spass_kind 3
+        only, the bind-time timing that chose it; zeros otherwise)."""
         t, u, k = ctypes.c_double(), ctypes.c_double(), ctypes.c_int32()
         self.ctx.check(self.lib.riptrm_get_spass_calibration(self.ctx.h, ctypes.byref(t), ctypes.byref(u),
                                                              ctypes.byref(k)), "riptrm_get_spass_calibration")
@@ -447,6 +490,8 @@ class NonnegPCABatch:
                        "riptrm_solve_begin")
         self.ro = ro
         self._target = 2 ** 31 - 1
+        self._drained = [[] for _ in range(self.batch)]
+        self._dropped = np.zeros(self.batch, dtype=np.int64)
         return ro
 
     def advance(self, steps: int, outer_target: Optional[int] = None) -> int:
@@ -458,12 +503,22 @@ class NonnegPCABatch:
         return int(act.value)
 
     def run_until(self, outer_target: Optional[int] = None, max_chunk: int = 512, timeout_s: float = 1e9) -> int:
-        """Advance until every instance is finished or paused at ``outer_target``."""
+        """Advance until every instance is finished or paused at ``outer_target``.  With log draining
+        on, a chunk is at most a quarter of the log capacity in lock-step iterations (each writes at
+        most one record per instance on the tCG path) and the device log is drained once half full."""
         chunk, t0 = 4, time.time()
+        cap = min(self.cap, int(self.ro.c_opt.log_capacity))
+        if self.drain:
+            max_chunk = max(1, min(max_chunk, cap // 4))
         act = self.advance(0, outer_target)
         while act > 0:
-            act = self.advance(chunk, outer_target)
+            act = self.advance(min(chunk, max_chunk), outer_target)
             chunk = min(chunk * 2, max_chunk)
+            if self.drain and cap > 0:
+                st = self.stats()
+                pend = st[:, C["RIPTRM_STAT_LOG_COUNT"]] - st[:, C["RIPTRM_STAT_LOG_BASE"]]
+                if pend.max() > cap // 2:
+                    self.drain_logs()
             if time.time() - t0 > timeout_s:
                 raise TimeoutError("RIPTRM device solve exceeded the host timeout")
         return act
@@ -478,9 +533,11 @@ class NonnegPCABatch:
         st = self.stats()
         x = self.vec(0).clone()
         y = self.vec(1).clone()
-        count = int(st[:, C["RIPTRM_STAT_LOG_COUNT"]].max()) if self.batch else 0
-        logs = self.log_rows(count)
-        return BatchResult(x=x, y=y, stats=st, raw_log=logs, ro=self.ro)
+        logs, dropped = [], []
+        for b, (rows, drop) in enumerate(self._pending_logs(st)):
+            logs.append(np.concatenate(self._drained[b] + [rows]) if self._drained[b] else rows.copy())
+            dropped.append(int(self._dropped[b]) + drop)
+        return BatchResult(x=x, y=y, stats=st, raw_log=logs, ro=self.ro, dropped=np.array(dropped))
 
 
 @dataclass
@@ -488,8 +545,9 @@ class BatchResult:
     x: torch.Tensor
     y: torch.Tensor
     stats: np.ndarray
-    raw_log: np.ndarray
+    raw_log: List[np.ndarray]        # per instance: its log records in order (NLOG doubles each)
     ro: ResolvedOptions
+    dropped: Optional[np.ndarray] = None   # per instance: records lost from the middle of the log
 
     def stat(self, b: int, name: str) -> float:
         return float(self.stats[b, C[f"RIPTRM_STAT_{name}"]])
@@ -511,7 +569,7 @@ class BatchResult:
     def log(self, b: int) -> Dict[str, list]:
         """Instance b's log in the reference's column schema (base_solver.py:58-76,
         utils.py:356-364, RIPTRM.py:986-1023)."""
-        cnt = min(int(self.stat(b, "LOG_COUNT")), self.raw_log.shape[1])
+        rows = self.raw_log[b]
         save_inner = bool(self.ro.option['save_inner_iteration'])
         cols: Dict[str, list] = {k: [] for k in (
             "iteration", "time", "cost", "distance", "residual", "gradnorm", "complviolation",
@@ -524,7 +582,7 @@ class BatchResult:
                 cols[k] = []
         cols["maxabsLagmult"] = []
         F = lambda name: C[f"RIPTRM_LOG_{name}"]
-        for r in self.raw_log[b, :cnt]:
+        for r in rows:
             it = int(r[F("ITERATION")])
             cols["iteration"].append(it)
             cols["time"].append(0 if len(cols["time"]) == 0 else float(r[F("TIME")]))
@@ -554,8 +612,7 @@ class BatchResult:
         return cols
 
     def tcg_iters_per_row(self, b: int) -> List[int]:
-        cnt = min(int(self.stat(b, "LOG_COUNT")), self.raw_log.shape[1])
-        return [int(v) for v in self.raw_log[b, :cnt, C["RIPTRM_LOG_TCG_ITERS"]]]
+        return [int(v) for v in self.raw_log[b][:, C["RIPTRM_LOG_TCG_ITERS"]]]
 
 
 def profile_enable(batch: NonnegPCABatch, on: bool = True):

@@ -71,6 +71,7 @@ SIGNATURES: Dict[str, tuple] = {
                                      c_void_p, c_void_p, c_void_p, c_int32]),
     "riptrm_solve_advance": (c_int32, [c_void_p, c_int32, c_int32, P_int32]),
     "riptrm_device_clock_hz": (c_double, [c_void_p]),
+    "riptrm_log_rebase": (c_int32, [c_void_p]),
     "riptrm_set_stream_groups": (c_int32, [c_void_p, c_int32]),
     "riptrm_set_graphs": (c_int32, [c_void_p, c_int32]),
     "riptrm_set_spass_kind": (c_int32, [c_void_p, c_int32]),

@@ -18,7 +18,7 @@ import numpy as np
 import torch
 
 import riptrm_native as N
-from engine import BatchResult, C, NSTAT, NLOG, ResolvedOptions, TCG_NAMES, _stream_handle, resolve_options
+from engine import BatchResult, C, NSTAT, NLOG, ResolvedOptions, TCG_NAMES, _stream_handle, assemble_log, resolve_options
 
 
 def expand_constset(constset) -> np.ndarray:
@@ -295,5 +295,13 @@ class SIBatch:
     def result(self) -> BatchResult:
         torch.cuda.synchronize(self.device)
         st = self.stats()
-        count = int(st[:, C["RIPTRM_STAT_LOG_COUNT"]].max()) if self.batch else 0
-        return BatchResult(x=self.x().clone(), y=self.y().clone(), stats=st, raw_log=self.log_rows(count), ro=self.ro)
+        count = st[:, C["RIPTRM_STAT_LOG_COUNT"]].astype(np.int64)
+        cap = min(self.cap, int(self.ro.c_opt.log_capacity))
+        slots = self.log_rows(int(count.max()) if self.batch else 0)
+        logs, dropped = [], []
+        for b in range(self.batch):   # one launch per solve: no draining, head + latest records kept
+            rows, drop = assemble_log(slots[b], int(count[b]), cap)
+            logs.append(rows.copy())
+            dropped.append(drop)
+        return BatchResult(x=self.x().clone(), y=self.y().clone(), stats=st, raw_log=logs, ro=self.ro,
+                           dropped=np.array(dropped))

@@ -1,0 +1,135 @@
+"""GPU parity at the headline size (BASELINE configs[2]: NonnegPCA n = 4000, 128 instances).
+
+* teacher-forced tCG (RIPTRM.py:41-216 via compute_direction :445-452) at n = 4000 from states
+  taken out of the oracle's own trajectory: mu from 0.1 down to ~1e-7, Delta = pi/8 (the
+  reference's initial radius, :855-860) and 1e-3, the longest tCG run of that trajectory
+  included;
+* a whole solve (K = 12 outer iterations, mu 0.1 -> 2.5e-5) of two instances against the oracle
+  (tests/parity.py bar), on the default pipeline for n = 4000 (symmetric tiles, super-tile S-pass);
+* the headline pipeline itself: 128 instances drawn on the device (two stream groups, persistent
+  super-tile S-pass), three of them solved again alone -> bitwise identical iterates and logs
+  (the S-pass kernel is chosen by n alone, riptrm_set_spass_kind), and two of those against an
+  oracle trajectory built from the device's own S (RIPTRM.py:707-783).
+"""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+from oracle import nonnegpca_gen as G
+from oracle import riptrm_oracle as O
+
+N = 4000
+OPT = dict(tolresid=0.0, maxtime=1e9)
+
+
+def _gpu_opt(**kw):
+    from problems import manviofun
+    o = {"TRS_solver": "tCG", "second_order_stationarity": False, "manviofun": manviofun}
+    o.update(OPT)
+    o.update(kw)
+    return o
+
+
+def _oracle_opt(**kw):
+    o = dict(OPT, manviofun=O.sphere_manvio)
+    o.update(kw)
+    return o
+
+
+class _Recorder(O.RIPTRMOracle):
+    """The oracle with every inner step's starting state recorded (x, y, mu, Delta, tCG length)."""
+
+    def __init__(self, option):
+        super().__init__(option)
+        self.states = []
+
+    def inner_step(self, P, x, y, mu, Delta, inner_iteration, inner_option):
+        out = super().inner_step(P, x, y, mu, Delta, inner_iteration, inner_option)
+        self.states.append((x.copy(), y.copy(), mu, Delta, self.trace[-1]["tcg_iters"]))
+        return out
+
+
+@pytest.fixture(scope="module")
+def trajectory():
+    Z, x0, y0 = G.generate_instance(N, 4000)
+    rec = _Recorder(_oracle_opt(maxiter=18))
+    rec.run(O.NonnegPCAVectorized(Z), x0, y0)
+    return Z, rec.states
+
+
+def test_n4000_tcg_teacher_forced(trajectory):
+    """Same (x, y, mu, Delta) in -> same tCG exit (stop reason and j) and eta to 1e-9."""
+    import engine
+    Z, states = trajectory
+    longest = max(range(len(states)), key=lambda i: states[i][4])
+    small_mu = next(i for i, s in enumerate(states) if s[2] <= 1e-6)
+    picks = [(0, None), (len(states) // 3, None), (longest, None), (small_mu, None),
+             (small_mu, 1e-3), (longest, np.pi / 8)]
+    B = len(picks)
+    xs = np.stack([states[i][0] for i, _ in picks])
+    ys = np.stack([states[i][1] for i, _ in picks])
+    mus = np.array([states[i][2] for i, _ in picks])
+    deltas = np.array([states[i][3] if d is None else d for i, d in picks])
+    eng = engine.NonnegPCABatch(N, B)
+    eng.load_Z(np.broadcast_to(Z, (B, N, N)))
+    eta, heta, js, stops = eng.tcg(xs, ys, mus, deltas)
+    eta = eta.cpu().numpy()
+    heta = heta.cpu().numpy()
+    P = O.NonnegPCAVectorized(Z)
+    assert states[longest][4] >= 50          # a long CG run is really in the set
+    assert mus.min() <= 1e-6
+    for b in range(B):
+        _, _, Hw, c = P.begin_inner(xs[b], ys[b], mus[b])
+        e, he, j, stop = O.truncated_conjugate_gradient(P.manifold, Hw, xs[b], c, deltas[b], 1, 0.1, 1, N - 1)
+        assert stops[b] == stop and js[b] == j, (b, mus[b], deltas[b], stops[b], stop, js[b], j)
+        assert np.linalg.norm(eta[b] - e) <= 1e-9 * np.linalg.norm(e), (b, np.linalg.norm(eta[b] - e) / np.linalg.norm(e))
+        assert np.linalg.norm(heta[b] - he) <= 1e-8 * np.linalg.norm(he), b
+
+
+def test_n4000_solve_matches_oracle():
+    """Two instances, 12 outer iterations, the default n = 4000 pipeline against the oracle."""
+    import engine
+    from parity import compare_logs
+    K = 12
+    insts = [G.generate_instance(N, 4000 + b) for b in range(2)]
+    eng = engine.NonnegPCABatch(N, 2)
+    eng.load_Z(np.stack([z for z, _, _ in insts]))
+    assert eng.spass_calibration()["kernel"] == "k_spass_sup"
+    res = eng.solve(np.stack([x for _, x, _ in insts]), np.stack([y for _, _, y in insts]), _gpu_opt(maxiter=K))
+    xs = res.x.cpu().numpy()
+    for b, (Z, x0, y0) in enumerate(insts):
+        ref = O.solve(Z, x0, y0, _oracle_opt(maxiter=K))
+        compare_logs(res.log(b), ref.log)
+        np.testing.assert_allclose(xs[b], ref.x, atol=1e-7)
+        assert int(res.stat(b, "OUTER_ITERS")) == K
+
+
+def test_n4000_b128_headline_pipeline_batch_independent():
+    """128 instances on the headline pipeline vs the same instances alone: bitwise equal."""
+    import engine
+    K = 2
+    ids = [0, 77, 127]
+    big = engine.NonnegPCABatch(N, 128)
+    x0, y0 = big.generate_synthetic(ids=list(range(128)))
+    res = big.solve(x0, y0, _gpu_opt(maxiter=K))
+    cal = big.spass_calibration()
+    assert cal["kernel"] == "k_spass_sup"
+    for k in ids:
+        one = engine.NonnegPCABatch(N, 1)
+        xa, ya = one.generate_synthetic(ids=[k])
+        assert torch.equal(xa[0], x0[k])
+        ra = one.solve(xa, ya, _gpu_opt(maxiter=K))
+        assert torch.equal(ra.x[0], res.x[k]) and torch.equal(ra.y[0], res.y[k]), k
+        la, lb = ra.log(0), res.log(k)
+        for key in la:
+            if key != "time":
+                assert la[key] == lb[key] or np.array_equal(np.array(la[key], float), np.array(lb[key], float)), (k, key)
+        if k != 77:   # two of them against the oracle, built from the device's own S and x0
+            from parity import compare_logs
+            S = one.unpack(0)
+            P = O.NonnegPCAVectorized(S, S=S)
+            ref = O.RIPTRMOracle(_oracle_opt(maxiter=K)).run(P, xa[0].cpu().numpy(), ya[0].cpu().numpy())
+            compare_logs(la, ref.log)
+        del one

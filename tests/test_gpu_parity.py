@@ -474,12 +474,21 @@ def test_spass_kinds_agree(n, B):
             auto = eng.hvp(np.stack(xs), np.stack(ys), 0.0123, np.stack(vs)).cpu().numpy()
             if layout == "sym2":
                 np.testing.assert_array_equal(auto, outs["sym2"])
-    if n == 4000:   # default engine: the bind-time calibration picked one of the two kernels
+    if n == 4000:
+        # default engine (kind 1): a rule on n alone, the super-tile kernel at n = 4000
         eng = _engine(np.stack(Zs))
         cal = eng.spass_calibration()
-        assert cal["ms_per_launch_tile"] > 0 and cal["ms_per_launch_super"] > 0, cal
+        assert cal["kernel"] == "k_spass_sup" and cal["ms_per_launch_tile"] == 0.0, cal
         got = eng.hvp(np.stack(xs), np.stack(ys), 0.0123, np.stack(vs)).cpu().numpy()
-        np.testing.assert_array_equal(got, outs["sym2" if cal["kernel"] == "k_spass_sup" else "sym"])
+        np.testing.assert_array_equal(got, outs["sym2"])
+        # kind 3: timed at bind, either kernel may win
+        import engine
+        eng3 = engine.NonnegPCABatch(n, B, layout="sym", spass_kind=3)
+        eng3.load_Z(np.stack(Zs))
+        cal3 = eng3.spass_calibration()
+        assert cal3["ms_per_launch_tile"] > 0 and cal3["ms_per_launch_super"] > 0, cal3
+        got3 = eng3.hvp(np.stack(xs), np.stack(ys), 0.0123, np.stack(vs)).cpu().numpy()
+        np.testing.assert_array_equal(got3, outs["sym2" if cal3["kernel"] == "k_spass_sup" else "sym"])
     a, b2 = outs["sym"], outs["sym2"]
     scale = np.abs(a).max(axis=1, keepdims=True)
     assert np.max(np.abs(a - b2) / scale) < 1e-13
@@ -496,3 +505,37 @@ def test_super_spass_solve_is_deterministic():
         res = eng.solve(np.stack([x for _, x, _ in insts]), np.stack([y for _, _, y in insts]), _gpu_opt(maxiter=6))
         xs.append(res.x.cpu().numpy())
     np.testing.assert_array_equal(xs[0], xs[1])
+
+
+def test_log_longer_than_capacity_is_complete(fixture_n50):
+    """A solve whose log outgrows the device capacity (16 records here) is drained to the host
+    between lock-step chunks (riptrm_log_rebase): every record arrives, in order, and matches the
+    oracle's log row for row."""
+    Z, x0, y0 = fixture_n50
+    K = 14
+    eng = _engine(Z, cap=16)
+    res = eng.solve(x0[None], y0[None], _gpu_opt(maxiter=K))
+    ref = O.solve(Z, x0, y0, _oracle_opt(maxiter=K))
+    gl = res.log(0)
+    assert len(gl["iteration"]) == len(ref.log["iteration"]) > 16
+    assert int(res.dropped[0]) == 0
+    _compare_logs(gl, ref.log)
+    full = _engine(Z).solve(x0[None], y0[None], _gpu_opt(maxiter=K))
+    notime = lambda a: np.delete(a, 1, axis=1)   # every field but RIPTRM_LOG_TIME
+    np.testing.assert_array_equal(notime(res.raw_log[0]), notime(full.raw_log[0]))
+
+
+def test_log_without_draining_keeps_head_and_latest(fixture_n50):
+    """Draining off: the device keeps the first capacity/2 records and a ring of the latest."""
+    import engine
+    Z, x0, y0 = fixture_n50
+    K = 14
+    eng = engine.NonnegPCABatch(Z.shape[0], 1, log_capacity=16, drain_logs=False)
+    eng.load_Z(Z[None])
+    res = eng.solve(x0[None], y0[None], _gpu_opt(maxiter=K))
+    full = _engine(Z).solve(x0[None], y0[None], _gpu_opt(maxiter=K))
+    a, b = res.raw_log[0], full.raw_log[0]
+    assert len(a) == 16 and int(res.dropped[0]) == len(b) - 16
+    notime = lambda a: np.delete(a, 1, axis=1)   # every field but RIPTRM_LOG_TIME
+    np.testing.assert_array_equal(notime(a[:8]), notime(b[:8]))
+    np.testing.assert_array_equal(notime(a[8:]), notime(b[-8:]))

@@ -137,7 +137,7 @@ def test_log_decoding_schema_matches_oracle(fixture_n50):
     stats = np.zeros((1, C["RIPTRM_STAT_NFIELDS"]))
     stats[0, C["RIPTRM_STAT_LOG_COUNT"]] = 3
     stats[0, C["RIPTRM_STAT_STOP_CODE"]] = C["RIPTRM_STOP_MAXITER"]
-    res = engine.BatchResult(x=None, y=None, stats=stats, raw_log=raw, ro=ro)
+    res = engine.BatchResult(x=None, y=None, stats=stats, raw_log=[raw[0]], ro=ro)
     log = res.log(0)
     assert list(log.keys()) == list(ref.log.keys())
     assert log["inner_status"] == [None, "successful", "converged"]
@@ -188,3 +188,22 @@ def test_save_output_reference_layout(tmp_path):
     assert open(tmp_path / "RIPTRM_tCG_eqLagmult.csv").read() == ""
     # csv.writerows on the name string: one character per row, as the reference writes it
     assert open(tmp_path / "RIPTRM_tCG_name.csv").read().split() == list("RIPTRM_tCG")
+
+
+def test_log_slot_assembly_keeps_head_and_latest():
+    """include/riptrm.h "Log slots": linear up to the capacity, then the first cap/2 records and a
+    ring of the latest; assemble_log restores chronological order and counts the dropped middle."""
+    import engine
+    for cap in (1, 2, 7, 8):
+        for k in range(0, 40):
+            slots = np.full((cap, 1), -1.0)
+            for r in range(k):       # the device's slot rule (riptrm_device.h log_slot)
+                i = r if r < cap else cap // 2 + (r - cap // 2) % (cap - cap // 2)
+                slots[i, 0] = r
+            rows, dropped = engine.assemble_log(slots, k, cap)
+            if k <= cap:
+                assert dropped == 0 and list(rows[:, 0]) == list(range(k))
+            else:
+                h = cap // 2
+                want = list(range(h)) + list(range(k - (cap - h), k))
+                assert dropped == k - cap and list(rows[:, 0]) == want, (cap, k)

@@ -200,3 +200,31 @@ def test_ripm_operator_aw_closed_form():
     l = P.manifold.inner_product(x, O.ripm_operator_aw(P, x, z, s, u), w)
     r = P.manifold.inner_product(x, u, O.ripm_operator_aw(P, x, z, s, w))
     assert abs(l - r) <= 1e-11 * max(1.0, abs(l))
+
+
+@pytest.mark.parametrize("lincomb,embedded", [(True, False), (False, True), (True, True)])
+def test_euclidean_branch_options_agree(lincomb, embedded):
+    """do_euclidean_lincomb / is_euclidean_embedded (RIPTRM.py:480-482, :514-517, :543-545,
+    :567-568) restated per constraint: on the Sphere they compute the default branches' operators
+    (linear conversions; x^T dx = 0 for tangent dx), so the whole trajectory matches the default
+    one at the summation-order bar, and the device's closed form (which serves all four option
+    combinations) stands for each of them."""
+    from parity import compare_logs
+    Z, x0, y0 = G.generate_instance(37, 100)
+    opt = dict(OPT, maxiter=8, do_euclidean_lincomb=lincomb, is_euclidean_embedded=embedded)
+    a = O.solve(Z, x0, y0, opt, structured=True)
+    b = O.solve(Z, x0, y0, dict(OPT, maxiter=8), structured=True)
+    c = O.solve(Z, x0, y0, dict(OPT, maxiter=8))
+    compare_logs(a.log, b.log)
+    compare_logs(a.log, c.log)
+    P = O.NonnegPCAStructured(Z, lincomb=lincomb, embedded=embedded)
+    Q = O.NonnegPCAStructured(Z)
+    rs = np.random.RandomState(3)
+    x = x0 / np.linalg.norm(x0)
+    y = rs.rand(37) + 0.1
+    u = Q.manifold.projection(x, rs.randn(37))
+    _, _, Hp, cp = P.begin_inner(x, y, 0.01)
+    _, _, Hq, cq = Q.begin_inner(x, y, 0.01)
+    assert np.linalg.norm(Hp(u) - Hq(u)) <= 1e-12 * np.linalg.norm(Hq(u))
+    assert np.linalg.norm(cp - cq) <= 1e-12 * np.linalg.norm(cq)
+    assert np.linalg.norm(P.gradlag(x, y) - Q.gradlag(x, y)) <= 1e-12 * np.linalg.norm(Q.gradlag(x, y))
