@@ -342,7 +342,26 @@ def main():
                     traffic = tj["hbm_bytes_per_instance_pass"] * passes_r0 / nl
             except Exception as e:  # pragma: no cover
                 log(f"traffic json unreadable: {e}")
-        if args.layout == "shared":
+        persist = eng.persistent_state()["active"] if args.layout == "sym" else False
+        if persist:
+            # k_persist: the whole lock-step loop in one launch per chunk, S held in LDS.  Its time
+            # is per-pass latency (barrier + reductions), not bandwidth: price the passes it served
+            # at the bytes the lock-step S-pass would stream, and give the per-pass latency.
+            kern_s = prof["state_ms"] / 1e3
+            eff = (passes_r0 * bytes_per_pass / kern_s / 1e9) if kern_s > 0 else None
+            nl = max(1, int(prof["state_launches"]))
+            roofline = {"bound": "hbm", "achieved": eff, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": (eff / HBM_PEAK_GBS) if eff else None, "traffic": None,
+                        "bytes_definition": ("stored S per instance-pass (symmetric tiles, "
+                                             f"{s_bytes / 1e6:.2f} MB at n={n}) + 16 n, as the lock-step S-pass would "
+                                             "stream it; k_persist reads S from HBM once per launch and serves every "
+                                             "pass from LDS, so this is an effective rate of a latency-bound loop"),
+                        "kernel": ("k_persist (one launch per chunk: every 128x128 tile of S in LDS, one workgroup "
+                                   "per tile, replicated state machine, one in-launch barrier per pass)"),
+                        "bytes_per_launch": passes_r0 * bytes_per_pass / nl,
+                        "avg_launch_us": prof["state_ms"] * 1e3 / nl,
+                        "us_per_pass": (kern_s * 1e6 / passes_r0) if passes_r0 > 0 else None}
+        elif args.layout == "shared":
             # dense product on the fp64 matrix cores: 2 n^2 algorithmic flops per right-hand side
             flops = passes_r0 * 2.0 * n * n
             tf = flops / gemv_s / 1e12 if gemv_s > 0 else None

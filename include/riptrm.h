@@ -242,6 +242,23 @@ int riptrm_set_stream_groups(riptrm_ctx* ctx, int32_t groups);
  * unless profiling is on.  on = 0 disables it (default 1).  Results do not depend on it. */
 int riptrm_set_graphs(riptrm_ctx* ctx, int32_t on);
 
+/* Persistent lock-step mode (symmetric-tile layout, TRS_solver tCG): when batch x tiles per
+ * instance <= min(256, compute units) — e.g. n <= 1024 for up to 7 instances, n <= 2048 for one
+ * (BASELINE configs[1]: n = 1000, one instance) — each riptrm_solve_advance / riptrm_tcg chunk is
+ * ONE launch in which every stored tile keeps its 128 x 128 block of S in LDS and every workgroup
+ * runs a replica of its instance's state machine (bitwise the lock-step results; replaces
+ * RIPTRM.py:41-216 + :707-896 for such batches).  mode 1 = automatic (default), 0 = never.  Set
+ * before riptrm_nonnegpca_bind.  riptrm_get_persistent: whether the bound shape allows it on this
+ * device and whether the current solve uses it. */
+int riptrm_set_persistent(riptrm_ctx* ctx, int32_t mode);
+int riptrm_get_persistent(riptrm_ctx* ctx, int32_t* possible, int32_t* active);
+/* Diagnostics: per in-launch step of workgroups 0 and reps - 1 of every k_persist launch, record
+ * device-clock stamps (0 step start, 1 tile pass done, 2 barrier passed, 3 state step done; tCG
+ * steps also 4 partial sums gathered, 5 iteration arithmetic done) into the caller's device
+ * buffer buf[2][cap][24] (uint64, overwritten by each launch; 8..14: stamps inside the tCG
+ * arithmetic, 16..17 inside the tile product); cap = 0 turns it off. */
+int riptrm_persist_trace(riptrm_ctx* ctx, uint64_t* buf, int32_t cap);
+
 /* S-pass kernel of the symmetric-tile layout: 1 = automatic (default: the persistent super-tile
  * kernel — whose partial-sum writes leave the HBM read stream in bursts — for n >= 2561, where an
  * instance has >= 64 units of 2 x 2 tiles, the per-tile kernel below; the rule depends on n only,

@@ -52,6 +52,12 @@ struct riptrm_ctx {
   uint64_t g_pver = ~0ull;
   uint64_t pver = 0;          // bumped whenever P (kernel parameters) changes
   int graphs = 1;             // riptrm_set_graphs
+  // persistent lock-step mode (k_persist): requested (riptrm_set_persistent), possible for the
+  // bound shape on this device, and active for the current solve (tCG only)
+  int persist_req = 1;
+  bool persist_ok = false, persist_on = false;
+  unsigned long long* persist_trace = nullptr;   // riptrm_persist_trace (diagnostics)
+  int persist_trace_cap = 0;
   // StableIdentification binding (riptrm_si.hip)
   riptrm_si::Bound* si = nullptr;
 };

@@ -73,8 +73,14 @@ enum Mode : int { MODE_SOLVE = 0, MODE_TCG_ONLY = 1 };
 
 struct Layout {
   int32_t n, batch, cap, layout, nt;
+  int32_t reps;        // persistent-mode replicas per instance (0: the layout has no persistent region)
   int64_t ld;
-  int64_t off_vec, off_state, off_stats, off_log, off_pbuf, off_lists, off_req, off_cnt, total;
+  int64_t off_vec, off_state, off_stats, off_log, off_pbuf, off_lists, off_req, off_cnt;
+  // persistent mode (k_persist): the replicas' private state (vectors, scalars, stats, requests)
+  // for batch x (reps - 1) replicas, the second parity of the partial grid, and the sync block
+  // (per-instance arrival counters + published clocks + the timeout flag; zeroed before every launch)
+  int64_t off_rvec, off_rstate, off_rstats, off_rreq, off_pbuf2, off_sync, sync_bytes;
+  int64_t total;
 };
 
 inline int64_t round_up(int64_t a, int64_t m) { return (a + m - 1) / m * m; }
@@ -128,6 +134,19 @@ inline int64_t s_elems_of(int32_t n, int32_t layout) {
   return rows_of(n) * ld_of(n);
 }
 
+// Persistent lock-step mode (k_persist; symmetric-tile layout, tCG): one 512-thread workgroup per
+// stored tile of every instance, all co-resident (one per CU: the tile sits in 128 KiB of LDS), so
+// at most PERSIST_MAX_WG workgroups; every workgroup of an instance runs a private replica of the
+// instance's state machine.  The workspace carries the replica region whenever the shape allows it;
+// riptrm_nonnegpca_bind enables the mode only if the device has that many CUs.
+constexpr int PERSIST_MAX_WG = 256;
+constexpr int PERSIST_MAX_N = 2048;   // nt <= 16: 136 tiles
+inline int32_t persist_reps_of(int32_t n, int32_t batch, int32_t layout) {
+  if (layout != RIPTRM_LAYOUT_SYMTILE || n > PERSIST_MAX_N) return 0;
+  const int64_t t = ntiles_of(n);
+  return (int64_t)batch * t <= PERSIST_MAX_WG ? (int32_t)t : 0;
+}
+
 inline Layout make_layout(int32_t n, int32_t batch, int32_t cap, int32_t layout) {
   Layout L;
   L.n = n; L.batch = batch; L.cap = cap; L.ld = ld_of(n); L.layout = layout; L.nt = nt_of(n);
@@ -143,6 +162,16 @@ inline Layout make_layout(int32_t n, int32_t batch, int32_t cap, int32_t layout)
   L.off_lists = o; o += (int64_t)4 * batch * 4;                          o = round_up(o, 256);
   L.off_req = o;   o += (int64_t)batch * 4;                              o = round_up(o, 256);
   L.off_cnt = o;   o += 16;                                              o = round_up(o, 256);
+  L.reps = persist_reps_of(n, batch, layout);
+  const int64_t bs = L.reps > 0 ? (int64_t)batch * (L.reps - 1) : 0;   // replicas beyond the instance itself
+  L.off_rvec = o;   o += (int64_t)NVEC * bs * L.ld * 8;                  o = round_up(o, 256);
+  L.off_rstate = o; o += bs * ST_N * 8;                                  o = round_up(o, 256);
+  L.off_rstats = o; o += bs * RIPTRM_STAT_NFIELDS * 8;                   o = round_up(o, 256);
+  L.off_rreq = o;   o += bs * 4;                                         o = round_up(o, 256);
+  L.off_pbuf2 = o;  if (L.reps > 0) o += (int64_t)2 * batch * pgrid_of(n) * 8;  o = round_up(o, 256);
+  L.off_sync = o;
+  L.sync_bytes = L.reps > 0 ? round_up((int64_t)batch * 4, 16) + (int64_t)2 * batch * 8 + 16 : 0;
+  o += L.sync_bytes;                                                     o = round_up(o, 256);
   L.total = o;
   return L;
 }
@@ -160,8 +189,10 @@ struct DevParams {
   int32_t wl;           // stored columns of the last tile column (symmetric-tile layout)
   int32_t nst, nsup;    // super-blocks per dimension, super-tile units per instance
   int32_t smode;        // per launch: 0 = tile S-pass (grid [nt][nt][TS]), 1 = super-tile ([nst][nst][SW])
-  double* pbuf;         // S-pass partial sums: 2 x batch x pgrid_of(n) (symmetric-tile layout),
+  double* pbuf;         // S-pass partial sums: 2 x pbatch x pgrid_of(n) (symmetric-tile layout),
                         // MM_KZ x 2 x batch x ld (shared layout)
+  int32_t pbatch;       // instances of the partial grid (= batch; the persistent replicas' parameter
+                        // block has batch = replica count but shares the instances' grid)
   double* vec;          // workspace vectors
   double* st;           // workspace scalars
   double* stats;

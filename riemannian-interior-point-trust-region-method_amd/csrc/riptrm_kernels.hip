@@ -15,6 +15,7 @@
 #include <vector>
 #include <cstring>
 #include <cstdio>
+#include <type_traits>
 #include "riptrm_device.h"
 #include "riptrm_ctx.h"
 #include "riptrm_wave.h"
@@ -282,7 +283,7 @@ __device__ __forceinline__ void spass_tile(const DevParams& P, int b, int t) {
   if (NR == 2) vj1 = *(const dbl2*)(v1 + J * TS + 2 * lane);
   const int64_t nn = (int64_t)P.nt * P.nt * TS;
   double* __restrict__ pb0 = P.pbuf + (int64_t)b * nn;
-  double* __restrict__ pb1 = P.pbuf + ((int64_t)P.batch + b) * nn;
+  double* __restrict__ pb1 = P.pbuf + ((int64_t)P.pbatch + b) * nn;
   double c0x = 0.0, c0y = 0.0, c1x = 0.0, c1y = 0.0;
   const int rrow = 4 * ((lane >> 5) & 1) + 2 * ((lane >> 4) & 1) + ((lane >> 3) & 1);
   constexpr int ROWS = TS / SP_WAVES;  // rows per wave
@@ -511,7 +512,7 @@ __device__ __forceinline__ void sup_flush(const DevParams& P, const double* outb
     tile_ij(u - slot * P.nsup, P.nst, Pq, Qq);
     const int t = threadIdx.x, side = t / SW, c = t - side * SW;   // 512 threads: row side, column side
     for (int k = 0; k < nr; ++k) {
-      double* pb = P.pbuf + ((int64_t)k * P.batch + b) * nn;
+      double* pb = P.pbuf + ((int64_t)k * P.pbatch + b) * nn;
       if (side == 0) pb[((int64_t)Pq * P.nst + Qq) * SW + c] = outb[off + (2 * k) * SW + c];
       else if (Pq != Qq) pb[((int64_t)Qq * P.nst + Pq) * SW + c] = outb[off + (2 * k + 1) * SW + c];
     }
@@ -736,9 +737,8 @@ enum Act : int { ACT_YIELD = 0, ACT_DONE = 1, ACT_PAUSE = 2, ACT_CONTINUE = 3 };
 // ---- register-path operand loads (free functions: k_state prefetches them before the machine's
 // scalars arrive) --------------------------------------------------------------------------------
 template <int K>
-__device__ __forceinline__ void rl_load(const DevParams& P, int b, int kind, double (&r)[K]) {
-  const int tid = threadIdx.x, n = P.n;
-  const double* a = vp(P, kind, b);
+__device__ __forceinline__ void rl_load(const double* a, int n, double (&r)[K]) {
+  const int tid = threadIdx.x;
 #pragma unroll
   for (int k = 0; k < K; ++k) {
     const int i = tid + k * ST_THREADS;
@@ -746,21 +746,41 @@ __device__ __forceinline__ void rl_load(const DevParams& P, int b, int kind, dou
   }
 }
 template <int K>
-__device__ __forceinline__ void rl_store(const DevParams& P, int b, int kind, const double (&r)[K]) {
-  const int tid = threadIdx.x, n = P.n;
-  double* a = vp(P, kind, b);
+__device__ __forceinline__ void rl_store(double* a, int n, const double (&r)[K]) {
+  const int tid = threadIdx.x;
 #pragma unroll
   for (int k = 0; k < K; ++k) {
     const int i = tid + k * ST_THREADS;
     if (i < n) a[i] = r[k];
   }
 }
+// Partial-grid words handed between workgroups INSIDE a launch (k_persist): written by `sc1`
+// (write-through) stores and read by `sc1` loads, which bypass the reading CU's L1, after the
+// arrival counter says every producer has drained its stores (MI355X_MICROARCH.md, visibility:
+// the counter form with sc1 payload stores and loads).  Agent-scope relaxed atomics on global
+// pointers lower to exactly those instructions.
+typedef __attribute__((address_space(1))) unsigned long long gu64_t;
+typedef __attribute__((address_space(1))) unsigned int gu32_t;
+__device__ __forceinline__ void st_sc1(double* p, double v) {
+  __hip_atomic_store((gu64_t*)p, (unsigned long long)__double_as_longlong(v), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double ld_sc1(const double* p) {
+  return __longlong_as_double((long long)__hip_atomic_load((gu64_t*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+template <bool SC1>
+__device__ __forceinline__ double ldp(const double* p) {
+  if constexpr (SC1) return ld_sc1(p);
+  else return *p;
+}
+
 // S delta of the last S-pass into registers (the layouts' partial sums, in gather_out's order).
 // K <= 2 (n <= 1024, nt <= 8): every partial of the element issued at once — one memory round
 // trip instead of one per tile column (the partials come from S-pass workgroups on every XCD,
-// so they are L2 misses).
-template <int K>
-__device__ __forceinline__ void rl_gather(const DevParams& P, int b, double (&u)[K]) {
+// so they are L2 misses).  pbuf / bp: the partial grid and the instance's slot in it (the
+// persistent replicas read their instance's grid; SC1 = the in-launch hand-off loads).
+template <int K, bool SC1 = false>
+__device__ __forceinline__ void rl_gather(const DevParams& P, const double* pbuf, int bp, double (&u)[K]) {
   const int tid = threadIdx.x, n = P.n;
   if (P.layout == RIPTRM_LAYOUT_SYMTILE) {
     // tile grid [nt][nt][TS] or super-tile grid [nst][nst][SW] (P.smode), summed in block order
@@ -768,7 +788,7 @@ __device__ __forceinline__ void rl_gather(const DevParams& P, int b, double (&u)
     const int sh = P.smode ? 8 : 7, wd = 1 << sh;
     static_assert(SW == 256 && TS == 128, "partial-grid shifts");
     const int64_t nn = (int64_t)nt * nt * wd;
-    const double* pb = P.pbuf + (int64_t)b * nn;
+    const double* pb = pbuf + (int64_t)bp * nn;
     const double* q[K];
 #pragma unroll
     for (int e = 0; e < K; ++e) {
@@ -783,7 +803,7 @@ __device__ __forceinline__ void rl_gather(const DevParams& P, int b, double (&u)
 #pragma unroll
       for (int e = 0; e < K; ++e)
 #pragma unroll
-        for (int J = 0; J < NTS; ++J) t[e][J] = (J < nt) ? q[e][(int64_t)J * wd] : 0.0;
+        for (int J = 0; J < NTS; ++J) t[e][J] = (J < nt) ? ldp<SC1>(q[e] + (int64_t)J * wd) : 0.0;
 #pragma unroll
       for (int e = 0; e < K; ++e) {
         u[e] = t[e][0];
@@ -793,14 +813,14 @@ __device__ __forceinline__ void rl_gather(const DevParams& P, int b, double (&u)
       }
     } else {
 #pragma unroll
-      for (int e = 0; e < K; ++e) u[e] = q[e][0];
+      for (int e = 0; e < K; ++e) u[e] = ldp<SC1>(q[e]);
       constexpr int GJ = 2;
       for (int J = 1; J < nt; J += GJ) {
         double t[K][GJ];
 #pragma unroll
         for (int e = 0; e < K; ++e)
 #pragma unroll
-          for (int v = 0; v < GJ; ++v) t[e][v] = (J + v < nt) ? q[e][(int64_t)(J + v) * wd] : 0.0;
+          for (int v = 0; v < GJ; ++v) t[e][v] = (J + v < nt) ? ldp<SC1>(q[e] + (int64_t)(J + v) * wd) : 0.0;
 #pragma unroll
         for (int e = 0; e < K; ++e)
 #pragma unroll
@@ -813,7 +833,7 @@ __device__ __forceinline__ void rl_gather(const DevParams& P, int b, double (&u)
       if (tid + e * ST_THREADS >= n) u[e] = 0.0;
   } else if (P.layout == RIPTRM_LAYOUT_SHARED) {
     const int64_t ld = P.ld, slab = (int64_t)P.batch * ld;
-    const double* pb = P.pbuf + (int64_t)b * ld;
+    const double* pb = pbuf + (int64_t)bp * ld;
 #pragma unroll
     for (int e = 0; e < K; ++e) {
       const int i = tid + e * ST_THREADS;
@@ -826,32 +846,163 @@ __device__ __forceinline__ void rl_gather(const DevParams& P, int b, double (&u)
       u[e] = acc;
     }
   } else {
-    rl_load<K>(P, b, V_OUT0, u);
+    rl_load<K>(vp(P, V_OUT0, bp), P.n, u);
   }
 }
 
 
-// every operand of one register-path tCG iteration (independent loads, one round trip)
-template <int K>
-struct TcgOps {
-  double u[K], d[K], x[K], y[K], c[K], e[K], he[K], rv[K];
+// The persistent replicas' slots (k_persist): vectors (NVEC x batch x ld), scalars, stats and
+// request words of batch x (reps - 1) replicas, laid out like the instances' own.
+struct RepBlock {
+  double* vec;
+  double* st;
+  double* stats;
+  int32_t* req;
+  int32_t batch;
 };
-template <int K>
-__device__ __forceinline__ void load_tcg_ops(const DevParams& P, int b, TcgOps<K>& o) {
-  rl_gather<K>(P, b, o.u);
-  rl_load<K>(P, b, V_IN0, o.d);
-  rl_load<K>(P, b, V_X, o.x);
-  rl_load<K>(P, b, V_Y, o.y);
-  rl_load<K>(P, b, V_C, o.c);
-  rl_load<K>(P, b, V_ETA, o.e);
-  rl_load<K>(P, b, V_HETA, o.he);
-  rl_load<K>(P, b, V_R, o.rv);
+
+// ---- one tCG iteration (RIPTRM.py:100-214) on register-resident vectors ------------------------
+// u = S delta on entry (the S-pass); d, x, y, c, e, he, rv = delta, x, y, cxCur, eta, Heta, r for
+// this thread's elements i = tid + k ST_THREADS.  Updates the vectors and the scalars and returns
+// TCG_CONTINUE (d is the next direction, j advanced) or the stop code (eta / Heta final, j as the
+// reference leaves it).  The hooks load late operands / store results for the workspace-backed
+// caller (k_state); the persistent fast path passes no-ops and keeps everything in registers.  One
+// body for both, so the two paths are bitwise identical.
+struct TcgScalars {
+  double coef, z_r, e_Pd, d_Pd, e_Pe, Delta, model, nr0, j;
+  double nr0t;   // pow(nr0, tCG_theta): constant over a tCG run (RIPTRM.py:180-182), computed once
+};
+constexpr int TCG_CONTINUE = -1;
+
+template <int K, class Hooks>
+__device__ __forceinline__ int tcg_math(TcgScalars& t, const riptrm_options& opt, int n, Red& R, double (&u)[K],
+                                        double (&d)[K], const double (&x)[K], const double (&y)[K],
+                                        const double (&c)[K], double (&e)[K], double (&he)[K], double (&rv)[K],
+                                        Hooks& h) {
+  const int tid = threadIdx.x;
+  // hw_apply(U, D, U)
+  double r1[2] = {0.0, 0.0};
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    r1[0] += x[k] * u[k];
+    r1[1] += x[k] * d[k];
+  }
+  bsum<2>(R, r1);
+  h.stamp(0);
+  const double xu = r1[0], xv = r1[1];
+  double r2[1] = {0.0};
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const bool ok = tid + k * ST_THREADS < n;
+    const double q = ok ? (y[k] * (d[k] - x[k] * xv)) / x[k] : 0.0;
+    r2[0] += ok ? x[k] * q : 0.0;
+  }
+  bsum<1>(R, r2);
+  h.stamp(1);
+  const double xq = r2[0];
+  const double coef = t.coef;
+#pragma unroll
+  for (int k = 0; k < K; ++k) {   // q recomputed, as hw_apply does
+    const bool ok = tid + k * ST_THREADS < n;
+    const double q = ok ? (y[k] * (d[k] - x[k] * xv)) / x[k] : 0.0;
+    const double hf = -u[k] + xu * x[k];
+    u[k] = (hf + coef * d[k]) + (q - xq * x[k]);
+  }
+  h.late_ceh();
+  double d1[1] = {0.0};
+#pragma unroll
+  for (int k = 0; k < K; ++k) d1[0] += d[k] * u[k];
+  bsum<1>(R, d1);
+  h.stamp(2);
+  const double d_Hd = d1[0];
+  const double z_r = t.z_r, e_Pd = t.e_Pd, d_Pd = t.d_Pd, e_Pe = t.e_Pe;
+  const double Delta = t.Delta;
+  double alpha = 0.0, e_Pe_new;
+  if (d_Hd != 0.0) {
+    alpha = z_r / d_Hd;
+    e_Pe_new = (e_Pe + 2.0 * alpha * e_Pd) + (alpha * alpha) * d_Pd;
+  } else {
+    e_Pe_new = e_Pe;
+  }
+  const double D2 = Delta * Delta;
+  if (d_Hd <= 0.0 || e_Pe_new >= D2) {
+    const double tau = (-e_Pd + sqrt(e_Pd * e_Pd + d_Pd * (D2 - e_Pe))) / d_Pd;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      e[k] = e[k] + tau * d[k];
+      he[k] = he[k] + tau * u[k];
+    }
+    h.store_eh();
+    return d_Hd <= 0.0 ? RIPTRM_TCG_NEGATIVE_CURVATURE : RIPTRM_TCG_EXCEEDED_TR;
+  }
+  t.e_Pe = e_Pe_new;
+  double m2[2] = {0.0, 0.0};
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const double ne = e[k] + alpha * d[k];
+    const double nh = he[k] + alpha * u[k];
+    m2[0] += ne * c[k];
+    m2[1] += ne * nh;
+  }
+  bsum<2>(R, m2);
+  h.stamp(3);
+  const double new_model = m2[0] + 0.5 * m2[1];
+  if (new_model >= t.model) return RIPTRM_TCG_MODEL_INCREASED;
+  t.model = new_model;
+  h.late_r();
+  double r2b[1] = {0.0};
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    e[k] = e[k] + alpha * d[k];
+    he[k] = he[k] + alpha * u[k];
+    const double r = rv[k] + alpha * u[k];
+    rv[k] = r;
+    r2b[0] += r * r;
+  }
+  h.store_ehr();
+  bsum<1>(R, r2b);
+  h.stamp(4);
+  const double r_r = r2b[0];
+  const double norm_r = sqrt(r_r);
+  const double nr0 = t.nr0;
+  const double ka = opt.tcg_kappa;
+  const double nr0t = t.nr0t;
+  const double j = t.j;
+  if (j >= (double)opt.tcg_mininner && norm_r <= nr0 * fmin(nr0t, ka))
+    return ka < nr0t ? RIPTRM_TCG_REACHED_TARGET_LINEAR : RIPTRM_TCG_REACHED_TARGET_SUPERLINEAR;
+  h.stamp(5);
+  const double znew = r_r;
+  const double beta = znew / z_r;
+  double p1[1] = {0.0};
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const double dn = -rv[k] + beta * d[k];
+    d[k] = dn;
+    p1[0] += x[k] * dn;
+  }
+  bsum<1>(R, p1);
+  h.stamp(6);
+  const double xd = p1[0];
+#pragma unroll
+  for (int k = 0; k < K; ++k) d[k] = d[k] - xd * x[k];  // to_tangent_space
+  h.store_d();
+  t.z_r = znew;
+  t.e_Pd = beta * (e_Pd + alpha * d_Pd);
+  t.d_Pd = znew + (beta * beta) * d_Pd;
+  t.j = j + 1.0;
+  if (j + 1.0 >= (double)(n - 1)) {  // range(maxinner) exhausted; Python j stays maxinner-1
+    t.j = j;
+    return RIPTRM_TCG_MAX_INNER_ITER;
+  }
+  return TCG_CONTINUE;
 }
 
 // EXACT = false: the tCG machine (every shipped config); EXACT = true adds the Exact_RepMat
 // branches (a separate k_state instantiation, so the tCG kernel carries none of its code or
-// register / scratch pressure).
-template <bool EXACT>
+// register / scratch pressure).  PERSIST = true: a replica inside k_persist (partial grid read
+// with sc1 loads from the instance's slot `bp` of the grid `pb`, no active-list appends, the
+// clock published at the last in-launch barrier so every replica takes the same decisions).
+template <bool EXACT, bool PERSIST = false>
 struct MachineT {
   const DevParams P;
   const int b;
@@ -862,15 +1013,39 @@ struct MachineT {
   double s[ST_HOT];   // hot scalars: identical in every thread, drive uniform control flow
   double* cold;       // cold scalars (ST_HOT..ST_N): read and written by thread 0 only
   double* tl;         // LDS of the Exact_RepMat subproblem (dynamic; Exact_RepMat solves only)
+  const double* pb;   // S-pass partial grid of this step and this instance's slot in it
+  int bp;
+  // this instance's (or persistent replica's) slots: V(k) = vbase + k vkstride, scalars, stats,
+  // request word, log (replicas keep no log)
+  double* vbase;
+  int64_t vkstride;
+  double* ostats;
+  int32_t* oreq;
+  double* olog;
+  int ocap;
+  double uclk = 0.0;  // PERSIST: the workgroup-uniform clock of the last in-launch barrier
+  int last_nr = 1;    // right-hand sides of the last request()
+  bool tcg_cont = false;   // tcg_reg_core ended by requesting the next pass of the SAME tCG run
 
-  __device__ __forceinline__ MachineT(const DevParams& P_, int b_, int out_list_, double* redbuf, double* tl_ = nullptr)
-      : P(P_), b(b_), tid(threadIdx.x), n(P_.n), out_list(out_list_), tl(tl_) {
+  // hot: where the hot scalars come from (nullptr = the workspace; k_persist keeps them in LDS
+  // between its steps, so they are not live in registers across the tile pass).  use_rep: b is a
+  // slot of the persistent replica block rb instead of an instance of P.
+  __device__ __forceinline__ MachineT(const DevParams& P_, int b_, int out_list_, double* redbuf, double* tl_ = nullptr,
+                                      const double* hot = nullptr, bool use_rep = false, RepBlock rb = RepBlock{})
+      : P(P_), b(b_), tid(threadIdx.x), n(P_.n), out_list(out_list_), tl(tl_), pb(P_.pbuf), bp(b_) {
     R.buf = redbuf;
     R.parity = 0;
-    const double* g = P.st + (int64_t)b * ST_N;
+    vbase = (use_rep ? rb.vec : P.vec) + (int64_t)b * P.ld;
+    vkstride = (int64_t)(use_rep ? rb.batch : P.batch) * P.ld;
+    double* stb = (use_rep ? rb.st : P.st) + (int64_t)b * ST_N;
+    ostats = (use_rep ? rb.stats : P.stats) + (int64_t)b * RIPTRM_STAT_NFIELDS;
+    oreq = (use_rep ? rb.req : P.req) + b;
+    olog = use_rep ? nullptr : P.log + (int64_t)b * P.cap * RIPTRM_LOG_NFIELDS;
+    ocap = use_rep ? 0 : P.cap;
+    const double* g = hot ? hot : stb;
 #pragma unroll
     for (int k = 0; k < ST_HOT; ++k) s[k] = g[k];
-    cold = P.st + (int64_t)b * ST_N;
+    cold = stb;
   }
 
   // thread-0-owned counters / info fields
@@ -879,13 +1054,14 @@ struct MachineT {
 
   // workgroup-uniform device clock (thread 0 reads it, max-reduction broadcasts it)
   __device__ __forceinline__ double unow() {
+    if constexpr (PERSIST) return uclk;
     double t[1] = {tid == 0 ? (double)wall_clock64() : -INFINITY};
     const int op[1] = {2};
     bred<1>(R, t, op);
     return t[0];
   }
 
-  __device__ __forceinline__ double* V(int k) const { return vp(P, k, b); }
+  __device__ __forceinline__ double* V(int k) const { return vbase + k * vkstride; }
   __device__ __forceinline__ double elapsed_u(double t0) { return (unow() - t0) / P.clock_hz; }
   __device__ __forceinline__ double mu_at(int idx) const {
     const int i = idx < P.tab_len ? idx : P.tab_len - 1;
@@ -923,7 +1099,7 @@ struct MachineT {
     const int sh = P.smode ? 8 : 7, wd = 1 << sh;
     const int64_t nn = (int64_t)nt * nt * wd;
     for (int k = 0; k < nr; ++k) {
-      const double* pb = P.pbuf + ((int64_t)k * P.batch + b) * nn;
+      const double* pbk = pb + ((int64_t)k * P.pbatch + bp) * nn;
       double* O = V(k == 0 ? V_OUT0 : V_OUT1);
       for (int base = tid; base < n; base += ST_THREADS * GE) {
         const double* q[GE];
@@ -933,15 +1109,15 @@ struct MachineT {
           int i = base + e * ST_THREADS;
           i = i < n ? i : n - 1;  // clamp: duplicate work, stored only if in range
           const int I = i >> sh, c = i - (I << sh);
-          q[e] = pb + (int64_t)I * nt * wd + c;
-          acc[e] = q[e][0];
+          q[e] = pbk + (int64_t)I * nt * wd + c;
+          acc[e] = ldp<PERSIST>(q[e]);
         }
         for (int J = 1; J < nt; J += GJ) {
           double t[GE][GJ];
 #pragma unroll
           for (int e = 0; e < GE; ++e)
 #pragma unroll
-            for (int u = 0; u < GJ; ++u) t[e][u] = (J + u < nt) ? q[e][(int64_t)(J + u) * wd] : 0.0;
+            for (int u = 0; u < GJ; ++u) t[e][u] = (J + u < nt) ? ldp<PERSIST>(q[e] + (int64_t)(J + u) * wd) : 0.0;
 #pragma unroll
           for (int e = 0; e < GE; ++e)
 #pragma unroll
@@ -958,10 +1134,13 @@ struct MachineT {
   }
 
   __device__ __forceinline__ int request(int nrhs) {
+    last_nr = nrhs;
     if (tid == 0) {
-      P.req[b] = nrhs;
-      const int slot = atomicAdd(&P.cnt[out_list], 1);
-      P.lists[out_list * P.batch + slot] = le_make(b, nrhs);
+      *oreq = nrhs;
+      if constexpr (!PERSIST) {
+        const int slot = atomicAdd(&P.cnt[out_list], 1);
+        P.lists[out_list * P.batch + slot] = le_make(b, nrhs);
+      }
     }
     cadd(ST_PASSES, 1.0);
     return ACT_YIELD;
@@ -972,7 +1151,7 @@ struct MachineT {
       double* g = cold;
 #pragma unroll
       for (int k = 0; k < ST_HOT; ++k) g[k] = s[k];
-      double* o = P.stats + (int64_t)b * RIPTRM_STAT_NFIELDS;
+      double* o = ostats;
       o[RIPTRM_STAT_OUTER_ITERS] = s[ST_OUTER_IT];
       o[RIPTRM_STAT_INNER_ITERS] = g[ST_INNER_TOTAL];
       o[RIPTRM_STAT_TCG_ITERS] = g[ST_TCG_TOTAL];
@@ -1088,10 +1267,10 @@ struct MachineT {
       const double* c = cold;
       const int cnt = (int)c[ST_LOG_COUNT];
       const int64_t k = (int64_t)(c[ST_LOG_COUNT] - c[ST_LOG_BASE]);
-      const int64_t capl = P.opt.log_capacity < P.cap ? P.opt.log_capacity : P.cap;
+      const int64_t capl = P.opt.log_capacity < ocap ? P.opt.log_capacity : ocap;
       if (capl > 0) {
         if (k >= capl) cold[ST_LOG_OVERFLOW] += 1.0;   // a record leaves the middle of the log
-        double* L = P.log + ((int64_t)b * P.cap + log_slot(k, capl)) * RIPTRM_LOG_NFIELDS;
+        double* L = olog + log_slot(k, capl) * RIPTRM_LOG_NFIELDS;
         L[RIPTRM_LOG_ITERATION] = s[ST_OUTER_IT];
         L[RIPTRM_LOG_TIME] = (cnt == 0) ? 0.0 : (t_now - s[ST_T_START]) / P.clock_hz;
         L[RIPTRM_LOG_COST] = ev[0];
@@ -1364,148 +1543,130 @@ struct MachineT {
   static constexpr int RT_EPT = 8;
 
   template <int K>
-  __device__ __forceinline__ void load_reg(int kind, double (&r)[K]) const { rl_load<K>(P, b, kind, r); }
+  __device__ __forceinline__ void load_reg(int kind, double (&r)[K]) const { rl_load<K>(V(kind), n, r); }
   template <int K>
-  __device__ __forceinline__ void store_reg(int kind, const double (&r)[K]) const { rl_store<K>(P, b, kind, r); }
+  __device__ __forceinline__ void store_reg(int kind, const double (&r)[K]) const { rl_store<K>(V(kind), n, r); }
   template <int K>
-  __device__ __forceinline__ void gather_reg(double (&u)[K]) { rl_gather<K>(P, b, u); }
+  __device__ __forceinline__ void gather_reg(double (&u)[K]) { rl_gather<K, PERSIST>(P, pb, bp, u); }
+
+  template <int K>
+  struct TcgVecs {
+    double d[K], x[K], y[K], c[K], e[K], he[K], rv[K];
+  };
 
   template <int K>
   __device__ __forceinline__ int tcg_step_reg() {
     // K <= 2 (n <= 1024): every operand loaded up front, one memory round trip (few registers);
     // K = 8: c / e / he / rv loaded where first needed, so fewer vectors are live at once
-    double u[K], d[K], x[K], y[K], c[K], e[K], he[K], rv[K];
+    TcgVecs<K> v;
+    double u[K];
     gather_reg<K>(u);
-    load_reg<K>(V_IN0, d);
-    load_reg<K>(V_X, x);
-    load_reg<K>(V_Y, y);
+    load_reg<K>(V_IN0, v.d);
+    load_reg<K>(V_X, v.x);
+    load_reg<K>(V_Y, v.y);
     if constexpr (K <= 2) {
-      load_reg<K>(V_C, c);
-      load_reg<K>(V_ETA, e);
-      load_reg<K>(V_HETA, he);
-      load_reg<K>(V_R, rv);
+      load_reg<K>(V_C, v.c);
+      load_reg<K>(V_ETA, v.e);
+      load_reg<K>(V_HETA, v.he);
+      load_reg<K>(V_R, v.rv);
     }
-    // hw_apply(U, D, U)
-    double r1[2] = {0.0, 0.0};
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-      r1[0] += x[k] * u[k];
-      r1[1] += x[k] * d[k];
-    }
-    bsum<2>(R, r1);
-    const double xu = r1[0], xv = r1[1];
-    double r2[1] = {0.0};
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-      const bool ok = tid + k * ST_THREADS < n;
-      const double q = ok ? (y[k] * (d[k] - x[k] * xv)) / x[k] : 0.0;
-      r2[0] += ok ? x[k] * q : 0.0;
-    }
-    bsum<1>(R, r2);
-    const double xq = r2[0];
-    const double coef = s[ST_COEF];
-#pragma unroll
-    for (int k = 0; k < K; ++k) {   // q recomputed, as hw_apply does
-      const bool ok = tid + k * ST_THREADS < n;
-      const double q = ok ? (y[k] * (d[k] - x[k] * xv)) / x[k] : 0.0;
-      const double hf = -u[k] + xu * x[k];
-      u[k] = (hf + coef * d[k]) + (q - xq * x[k]);
-    }
-    if constexpr (K > 2) {
-      load_reg<K>(V_C, c);
-      load_reg<K>(V_ETA, e);
-      load_reg<K>(V_HETA, he);
-    }
-    double d1[1] = {0.0};
-#pragma unroll
-    for (int k = 0; k < K; ++k) d1[0] += d[k] * u[k];
-    bsum<1>(R, d1);
-    const double d_Hd = d1[0];
-    const double z_r = s[ST_ZR], e_Pd = s[ST_EPD], d_Pd = s[ST_DPD], e_Pe = s[ST_EPE];
-    const double Delta = s[ST_DELTA];
-    double alpha = 0.0, e_Pe_new;
-    if (d_Hd != 0.0) {
-      alpha = z_r / d_Hd;
-      e_Pe_new = (e_Pe + 2.0 * alpha * e_Pd) + (alpha * alpha) * d_Pd;
-    } else {
-      e_Pe_new = e_Pe;
-    }
-    const double D2 = Delta * Delta;
-    if (d_Hd <= 0.0 || e_Pe_new >= D2) {
-      const double tau = (-e_Pd + sqrt(e_Pd * e_Pd + d_Pd * (D2 - e_Pe))) / d_Pd;
-#pragma unroll
-      for (int k = 0; k < K; ++k) {
-        e[k] = e[k] + tau * d[k];
-        he[k] = he[k] + tau * u[k];
+    return tcg_reg_core<K, true>(v, u);
+  }
+
+  // k_persist: every operand already in registers (v carried over from the previous iteration)
+  template <int K>
+  __device__ __forceinline__ void tcg_fast_load(TcgVecs<K>& v) const {
+    load_reg<K>(V_IN0, v.d);
+    load_reg<K>(V_X, v.x);
+    load_reg<K>(V_Y, v.y);
+    load_reg<K>(V_C, v.c);
+    load_reg<K>(V_ETA, v.e);
+    load_reg<K>(V_HETA, v.he);
+    load_reg<K>(V_R, v.rv);
+  }
+  template <int K>
+  __device__ __forceinline__ void tcg_fast_flush(const TcgVecs<K>& v) const {
+    store_reg(V_IN0, v.d);
+    store_reg(V_ETA, v.e);
+    store_reg(V_HETA, v.he);
+    store_reg(V_R, v.rv);
+  }
+
+  // One tCG iteration on register-resident vectors, u = S delta (tcg_math below).  MEM = true
+  // (k_state): the vectors round-trip through the workspace every iteration (stores as each is
+  // final, c / e / he / rv loaded late for K > 2).  MEM = false (k_persist's fast path): v holds
+  // every operand and stays in registers across iterations; nothing is stored until the tCG stops
+  // (then every modified vector is flushed before tcg_end reads it).
+  template <int K, bool MEM>
+  struct TcgHooks {
+    MachineT& M;
+    TcgVecs<K>& v;
+    __device__ __forceinline__ void late_ceh() {
+      if constexpr (MEM && K > 2) {
+        M.load_reg(V_C, v.c);
+        M.load_reg(V_ETA, v.e);
+        M.load_reg(V_HETA, v.he);
       }
-      store_reg(V_ETA, e);
-      store_reg(V_HETA, he);
-      s[ST_TCG_STOP] = d_Hd <= 0.0 ? RIPTRM_TCG_NEGATIVE_CURVATURE : RIPTRM_TCG_EXCEEDED_TR;
+    }
+    __device__ __forceinline__ void late_r() {
+      if constexpr (MEM && K > 2) M.load_reg(V_R, v.rv);
+    }
+    __device__ __forceinline__ void store_eh() {
+      if constexpr (MEM) {
+        M.store_reg(V_ETA, v.e);
+        M.store_reg(V_HETA, v.he);
+      }
+    }
+    __device__ __forceinline__ void store_ehr() {
+      if constexpr (MEM) {
+        M.store_reg(V_ETA, v.e);
+        M.store_reg(V_HETA, v.he);
+        M.store_reg(V_R, v.rv);
+      }
+    }
+    __device__ __forceinline__ void store_d() {
+      if constexpr (MEM) M.store_reg(V_IN0, v.d);
+    }
+    __device__ __forceinline__ void stamp(int) {}
+  };
+
+  __device__ __forceinline__ TcgScalars tcg_scalars() const {
+    TcgScalars t;
+    t.coef = s[ST_COEF];
+    t.z_r = s[ST_ZR];
+    t.e_Pd = s[ST_EPD];
+    t.d_Pd = s[ST_DPD];
+    t.e_Pe = s[ST_EPE];
+    t.Delta = s[ST_DELTA];
+    t.model = s[ST_MODEL];
+    t.nr0 = s[ST_NORMR0];
+    t.j = s[ST_J];
+    t.nr0t = pow(t.nr0, P.opt.tcg_theta);
+    return t;
+  }
+  __device__ __forceinline__ void tcg_scalars_back(const TcgScalars& t) {
+    s[ST_ZR] = t.z_r;
+    s[ST_EPD] = t.e_Pd;
+    s[ST_DPD] = t.d_Pd;
+    s[ST_EPE] = t.e_Pe;
+    s[ST_MODEL] = t.model;
+    s[ST_J] = t.j;
+  }
+
+  template <int K, bool MEM>
+  __device__ __forceinline__ int tcg_reg_core(TcgVecs<K>& v, double (&u)[K]) {
+    tcg_cont = false;   // a stop may start a new tCG (infeasible trial -> tcg_begin) whose
+                        // request must not be mistaken for this run's next pass
+    TcgScalars t = tcg_scalars();
+    TcgHooks<K, MEM> h{*this, v};
+    const int stop = tcg_math<K>(t, P.opt, n, R, u, v.d, v.x, v.y, v.c, v.e, v.he, v.rv, h);
+    tcg_scalars_back(t);
+    if (stop != TCG_CONTINUE) {
+      if constexpr (!MEM) tcg_fast_flush(v);
+      s[ST_TCG_STOP] = stop;
       return tcg_end();
     }
-    s[ST_EPE] = e_Pe_new;
-    double m2[2] = {0.0, 0.0};
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-      const double ne = e[k] + alpha * d[k];
-      const double nh = he[k] + alpha * u[k];
-      m2[0] += ne * c[k];
-      m2[1] += ne * nh;
-    }
-    bsum<2>(R, m2);
-    const double new_model = m2[0] + 0.5 * m2[1];
-    if (new_model >= s[ST_MODEL]) {
-      s[ST_TCG_STOP] = RIPTRM_TCG_MODEL_INCREASED;
-      return tcg_end();
-    }
-    s[ST_MODEL] = new_model;
-    if constexpr (K > 2) load_reg<K>(V_R, rv);
-    double r2b[1] = {0.0};
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-      e[k] = e[k] + alpha * d[k];
-      he[k] = he[k] + alpha * u[k];
-      const double r = rv[k] + alpha * u[k];
-      rv[k] = r;
-      r2b[0] += r * r;
-    }
-    store_reg(V_ETA, e);
-    store_reg(V_HETA, he);
-    store_reg(V_R, rv);
-    bsum<1>(R, r2b);
-    const double r_r = r2b[0];
-    const double norm_r = sqrt(r_r);
-    const double nr0 = s[ST_NORMR0];
-    const double th = P.opt.tcg_theta, ka = P.opt.tcg_kappa;
-    const double nr0t = pow(nr0, th);
-    const double j = s[ST_J];
-    if (j >= (double)P.opt.tcg_mininner && norm_r <= nr0 * fmin(nr0t, ka)) {
-      s[ST_TCG_STOP] = ka < nr0t ? RIPTRM_TCG_REACHED_TARGET_LINEAR : RIPTRM_TCG_REACHED_TARGET_SUPERLINEAR;
-      return tcg_end();
-    }
-    const double znew = r_r;
-    const double beta = znew / z_r;
-    double p1[1] = {0.0};
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-      const double dn = -rv[k] + beta * d[k];
-      d[k] = dn;
-      p1[0] += x[k] * dn;
-    }
-    bsum<1>(R, p1);
-    const double xd = p1[0];
-#pragma unroll
-    for (int k = 0; k < K; ++k) d[k] = d[k] - xd * x[k];  // to_tangent_space
-    store_reg(V_IN0, d);
-    s[ST_ZR] = znew;
-    s[ST_EPD] = beta * (e_Pd + alpha * d_Pd);
-    s[ST_DPD] = znew + (beta * beta) * d_Pd;
-    s[ST_J] = j + 1.0;
-    if (j + 1.0 >= (double)(n - 1)) {  // range(maxinner) exhausted; Python j stays maxinner-1
-      s[ST_J] = j;
-      s[ST_TCG_STOP] = RIPTRM_TCG_MAX_INNER_ITER;
-      return tcg_end();
-    }
+    tcg_cont = true;
     return request(1);
   }
 
@@ -1952,6 +2113,465 @@ __global__ void __launch_bounds__(ST_THREADS) k_state(DevParams P, int full, int
   M.finish_write();
 }
 
+// ------------------------------------------------------------------------------------------
+// k_persist: the lock-step loop of a small symmetric-tile batch (tCG) in ONE launch.
+// Why: at n = 1000 with one instance (BASELINE configs[1]) a lock-step iteration is a 5 us
+// S-pass plus a 12.5 us state kernel, latency and launch bound (profiles/r1_cfg1_*).  Here every
+// stored tile of every instance gets one 512-thread workgroup that keeps the tile in LDS for the
+// whole launch (S is read from HBM once per launch, not once per pass), and every workgroup of an
+// instance runs a private REPLICA of the instance's state machine on identical data: the
+// replicas take bitwise identical decisions (same code, same operands, same reduction orders; the
+// clock comes from the barrier, below), so no state is ever exchanged.  Per pass each workgroup
+// multiplies its tile by its own replica's S-pass vectors (spass_tile's arithmetic, operands from
+// LDS) into the instance's partial grid, with write-through (sc1) stores; one arrival counter per
+// instance (agent-scope atomic add after every wave drained its stores, sc1 polling) is the only
+// synchronisation, and every replica then gathers the grid (sc1 loads) exactly as k_state does.
+// Results are bitwise those of the lock-step path (k_spass_sym + k_state), which stays the
+// general path.  The partial grid and the published clock alternate between two buffers by pass
+// parity, so a fast replica never overwrites what a slow one still reads.  Every spin is bounded.
+// Replica 0 of instance b is the instance itself (P); replica t > 0 is slot b (reps - 1) + t - 1
+// of the replica block Q.
+// ------------------------------------------------------------------------------------------
+struct PersistSync {
+  unsigned int* ctr;    // [batch] arrivals, zeroed before every launch
+  double* clk;          // [2][batch] clock published by replica 0 at each barrier (parity)
+  unsigned int* flag;   // [0]: some barrier wait timed out
+  double* pbuf2;        // the partial grid's second parity
+  unsigned long long* trace;   // diagnostics (riptrm_persist_trace): per step of workgroups 0 and
+  int trace_cap;               // reps - 1, the device clock at the step's start / tile pass done /
+                               // barrier passed / state step done; nullptr = off
+};
+constexpr unsigned long long PERSIST_TIMEOUT_TICKS = 200000000ull;   // 2 s of the 100 MHz clock
+
+// spass_tile with the tile in LDS (row stride colsT) and the input vectors' two blocks it needs
+// staged in LDS (vl[rhs][0] = block I, vl[rhs][1] = block J); the partial sums go to the
+// instance's slot bp of the grid pbase with sc1 stores
+template <int NR>
+__device__ __forceinline__ void spass_tile_lds(const DevParams& P, const double* Tl, const double (*vl)[2][TS],
+                                               double* pbase, int bp, int t, double (*csl)[SP_WAVES][TS],
+                                               unsigned long long* tr = nullptr) {
+  int I, J;
+  tile_ij(t, P.nt, I, J);
+  const int lane = (int)__lane_id();
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int nt = P.nt, wl = P.wl;
+  const int rowsT = (I == nt - 1) ? wl : TS;
+  const int colsT = (J == nt - 1) ? wl : TS;
+  const bool cl = 2 * lane < colsT;
+  const dbl2 vj0 = *(const dbl2*)(&vl[0][1][2 * lane]);
+  dbl2 vj1 = dbl2{0.0, 0.0};
+  if (NR == 2) vj1 = *(const dbl2*)(&vl[1][1][2 * lane]);
+  const int64_t nn = (int64_t)P.nt * P.nt * TS;
+  double* pb0 = pbase + (int64_t)bp * nn;
+  double* pb1 = pbase + ((int64_t)P.pbatch + bp) * nn;
+  double c0x = 0.0, c0y = 0.0, c1x = 0.0, c1y = 0.0;
+  const int rrow = 4 * ((lane >> 5) & 1) + 2 * ((lane >> 4) & 1) + ((lane >> 3) & 1);
+  constexpr int ROWS = TS / SP_WAVES;
+  static_assert(ST_THREADS == SP_THREADS, "k_persist: one state workgroup = one tile workgroup");
+  // the row sums of both 8-row batches are stored after the loop: on gfx950 loads and stores share
+  // one counter, so any load wait after a write-through store would wait for its round trip
+  double rs[2][2] = {{0.0, 0.0}, {0.0, 0.0}};
+  bool rv[2] = {false, false};
+#pragma unroll
+  for (int rb = 0; rb < ROWS / 8; ++rb) {
+    const int r0 = w * ROWS + rb * 8;
+    if (r0 >= rowsT) break;
+    dbl2 sv[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) sv[k] = cl ? *(const dbl2*)(Tl + (r0 + k) * colsT + 2 * lane) : dbl2{0.0, 0.0};
+    double a[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const double vi0 = vl[0][0][r0 + k];
+      a[k] = __builtin_fma(sv[k].y, vj0.y, sv[k].x * vj0.x);
+      c0x = __builtin_fma(sv[k].x, vi0, c0x);
+      c0y = __builtin_fma(sv[k].y, vi0, c0y);
+    }
+    rs[rb][0] = reduce_scatter8(a);
+    rv[rb] = true;
+    if (NR == 2) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const double vi1 = vl[1][0][r0 + k];
+        a[k] = __builtin_fma(sv[k].y, vj1.y, sv[k].x * vj1.x);
+        c1x = __builtin_fma(sv[k].x, vi1, c1x);
+        c1y = __builtin_fma(sv[k].y, vi1, c1y);
+      }
+      rs[rb][1] = reduce_scatter8(a);
+    }
+  }
+  if ((lane & 7) == 0) {
+#pragma unroll
+    for (int rb = 0; rb < ROWS / 8; ++rb) {
+      if (!rv[rb]) continue;
+      const int r0 = w * ROWS + rb * 8;
+      st_sc1(pb0 + ((int64_t)I * P.nt + J) * TS + r0 + rrow, rs[rb][0]);
+      if (NR == 2) st_sc1(pb1 + ((int64_t)I * P.nt + J) * TS + r0 + rrow, rs[rb][1]);
+    }
+  }
+  if (tr) tr[16] = wall_clock64();   // wave 0's rows done
+  if (I != J) {   // csl: LDS [2][SP_WAVES][TS], the column sums across waves
+    csl[0][w][2 * lane] = c0x;
+    csl[0][w][2 * lane + 1] = c0y;
+    if (NR == 2) {
+      csl[1][w][2 * lane] = c1x;
+      csl[1][w][2 * lane + 1] = c1y;
+    }
+    __syncthreads();
+    if (tr) tr[17] = wall_clock64();   // every wave's rows done
+    if (threadIdx.x < TS) {
+      const int c = threadIdx.x;
+      double s0 = csl[0][0][c];
+#pragma unroll
+      for (int q = 1; q < SP_WAVES; ++q) s0 += csl[0][q][c];
+      st_sc1(pb0 + ((int64_t)J * P.nt + I) * TS + c, s0);
+      if (NR == 2) {
+        double s1 = csl[1][0][c];
+#pragma unroll
+        for (int q = 1; q < SP_WAVES; ++q) s1 += csl[1][q][c];
+        st_sc1(pb1 + ((int64_t)J * P.nt + I) * TS + c, s1);
+      }
+    }
+    __syncthreads();   // csl is rewritten by the next pass
+  }
+}
+
+// Arrival of workgroup (b, replica) at in-launch barrier `epoch` (1, 2, ...) of instance b: every
+// wave drains its sc1 stores, one lane publishes (replica 0: the clock) and adds to the counter,
+// then polls it (relaxed sc1 loads, bounded) until all `reps` workgroups of the instance arrived.
+// Returns false on a timeout (then the caller stops; the flag tells the host).
+__device__ __forceinline__ bool persist_barrier(const PersistSync& sy, int batch, int b, int reps, bool rep0,
+                                                unsigned epoch, double& clk, double* bclk, int* bfail) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double* cslot = sy.clk + (int64_t)(epoch & 1u) * batch + b;
+    gu32_t* ctr = (gu32_t*)(sy.ctr + b);
+    if (rep0) {
+      st_sc1(cslot, (double)wall_clock64());
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned target = epoch * (unsigned)reps;
+    const unsigned long long t0 = wall_clock64();
+    int fail = 0;
+    while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+      __builtin_amdgcn_s_sleep(1);
+      if (wall_clock64() - t0 > PERSIST_TIMEOUT_TICKS) {
+        fail = 1;
+        break;
+      }
+    }
+    if (fail) __hip_atomic_store((gu32_t*)sy.flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *bclk = fail ? 0.0 : ld_sc1(cslot);
+    *bfail = fail;
+  }
+  __syncthreads();
+  clk = *bclk;
+  return *bfail == 0;
+}
+
+using riptrm_trs::lds_f64;
+
+// What a lean tCG run reads (by value: one copy at the call, then registers).
+struct LeanArgs {
+  double* vk;          // the replica's vector kind 0 (kind k at vk + k vks)
+  int64_t vks;
+  double* gcold;       // the replica's scalar slots (ST_PASSES)
+  double* pb[2];       // the instance's partial grid, both parities
+  PersistSync sy;
+  int n, b, t, R, I, J, steps, batch;
+  int rep0, tsel;
+  double kappa, theta;
+  int mininner, pbatch, nt, wl;
+};
+// In / out of a lean run: the next pass index, barrier epoch, published clock, barrier ok, stop code.
+struct LeanIO {
+  int k;
+  unsigned epoch;
+  double clk;
+  int ok;
+  int stop;
+};
+
+// A lean tCG run of a k_persist replica: passes of S delta (the instance's tiles multiply the
+// direction staged in LDS, the barrier, the partial sums gathered with sc1 loads) and tcg_math on
+// register-resident vectors and scalars, until the run stops or the step budget ends; then the
+// vectors go back to the workspace, the scalars to the LDS copy `hot`, the passes to ST_PASSES.
+// Not inlined: its operands stay in registers (inside the kernel body, next to the inlined state
+// machine, the register allocator kept them in scratch and every reload waited on memory).  LDS
+// operands come in as address-space-3 pointers, so every access stays a ds_* instruction.
+template <int K>
+__device__ __noinline__ void lean_tcg_run(LeanArgs a, LeanIO* io, const lds_f64* tile, lds_f64* vl_, lds_f64* csl_,
+                                          lds_f64* red_, lds_f64* hot, lds_f64* bclk, int* bfail) {
+  const int n = a.n, tid = threadIdx.x;
+  double (*vl)[2][TS] = (double (*)[2][TS])(double*)vl_;
+  double (*csl)[SP_WAVES][TS] = (double (*)[SP_WAVES][TS])(double*)csl_;
+  DevParams Pt;   // the fields spass_tile_lds reads
+  Pt.nt = a.nt;
+  Pt.wl = a.wl;
+  Pt.pbatch = a.pbatch;
+  Pt.n = n;
+  Pt.smode = 0;
+  Pt.layout = RIPTRM_LAYOUT_SYMTILE;
+  Pt.nst = 0;
+  typename MachineT<false, true>::template TcgVecs<K> tv;
+  rl_load<K>(a.vk + V_IN0 * a.vks, n, tv.d);
+  rl_load<K>(a.vk + V_X * a.vks, n, tv.x);
+  rl_load<K>(a.vk + V_Y * a.vks, n, tv.y);
+  rl_load<K>(a.vk + V_C * a.vks, n, tv.c);
+  rl_load<K>(a.vk + V_ETA * a.vks, n, tv.e);
+  rl_load<K>(a.vk + V_HETA * a.vks, n, tv.he);
+  rl_load<K>(a.vk + V_R * a.vks, n, tv.rv);
+  TcgScalars ts;
+  ts.coef = hot[ST_COEF];
+  ts.z_r = hot[ST_ZR];
+  ts.e_Pd = hot[ST_EPD];
+  ts.d_Pd = hot[ST_DPD];
+  ts.e_Pe = hot[ST_EPE];
+  ts.Delta = hot[ST_DELTA];
+  ts.model = hot[ST_MODEL];
+  ts.nr0 = hot[ST_NORMR0];
+  ts.j = hot[ST_J];
+  ts.nr0t = pow(ts.nr0, a.theta);
+  riptrm_options opt;
+  opt.tcg_kappa = a.kappa;
+  opt.tcg_mininner = a.mininner;
+  int k = io->k;
+  unsigned epoch = io->epoch;
+  double clk = io->clk;
+  int ok = 1;
+  double passes = 0.0;
+  int stop = TCG_CONTINUE;
+  while (true) {
+#pragma unroll
+    for (int q = 0; q < K; ++q) {   // the direction's blocks I and J
+      const int i = tid + q * ST_THREADS;
+      const double dv = i < n ? tv.d[q] : 0.0;
+      if (i / TS == a.I) vl[0][0][i - a.I * TS] = dv;
+      if (i / TS == a.J) vl[0][1][i - a.J * TS] = dv;
+    }
+    __syncthreads();
+    unsigned long long* tr = (a.sy.trace && a.tsel >= 0 && k < a.sy.trace_cap && tid == 0)
+                                 ? a.sy.trace + ((int64_t)a.tsel * a.sy.trace_cap + k) * 24 : nullptr;
+    if (tr) tr[0] = wall_clock64();
+    spass_tile_lds<1>(Pt, (const double*)tile, vl, a.pb[k & 1], a.b, a.t, csl, tr);
+    if (tr) tr[1] = wall_clock64();
+    ok = persist_barrier(a.sy, a.batch, a.b, a.R, a.rep0 != 0, epoch++, clk, (double*)bclk, bfail);
+    if (!ok) break;
+    if (tr) tr[2] = wall_clock64();
+    double u[K];
+    rl_gather<K, true>(Pt, a.pb[k & 1], a.b, u);
+    if (tr) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      tr[4] = wall_clock64();
+    }
+    ++k;
+    Red Rd;
+    Rd.buf = (double*)red_;
+    Rd.parity = 0;
+    struct NoHooks {   // nothing to load or store; optional trace stamps (diagnostics)
+      unsigned long long* tr;
+      __device__ __forceinline__ void late_ceh() {}
+      __device__ __forceinline__ void late_r() {}
+      __device__ __forceinline__ void store_eh() {}
+      __device__ __forceinline__ void store_ehr() {}
+      __device__ __forceinline__ void store_d() {}
+      __device__ __forceinline__ void stamp(int i) {
+        if (tr) tr[8 + i] = wall_clock64();
+      }
+    } nohooks{tr};
+    stop = tcg_math<K>(ts, opt, n, Rd, u, tv.d, tv.x, tv.y, tv.c, tv.e, tv.he, tv.rv, nohooks);
+    if (tr) {
+      tr[5] = wall_clock64();
+      tr[3] = wall_clock64();
+    }
+    if (stop != TCG_CONTINUE) break;
+    passes += 1.0;   // request(1) of the same run
+    if (k >= a.steps) break;
+  }
+  // flush: vectors to the workspace, scalars to LDS, the requested passes to ST_PASSES
+  rl_store<K>(a.vk + V_IN0 * a.vks, n, tv.d);
+  rl_store<K>(a.vk + V_ETA * a.vks, n, tv.e);
+  rl_store<K>(a.vk + V_HETA * a.vks, n, tv.he);
+  rl_store<K>(a.vk + V_R * a.vks, n, tv.rv);
+  __syncthreads();
+  if (tid == 0) {
+    hot[ST_ZR] = ts.z_r;
+    hot[ST_EPD] = ts.e_Pd;
+    hot[ST_DPD] = ts.d_Pd;
+    hot[ST_EPE] = ts.e_Pe;
+    hot[ST_MODEL] = ts.model;
+    hot[ST_J] = ts.j;
+    if (stop != TCG_CONTINUE) hot[ST_TCG_STOP] = stop;
+    a.gcold[ST_PASSES] += passes;
+    io->k = k;
+    io->epoch = epoch;
+    io->clk = clk;
+    io->ok = ok;
+    io->stop = stop;
+  }
+  __syncthreads();
+}
+
+// K: elements per thread of the register-resident tCG iterations (n <= K ST_THREADS; 2 or 4)
+// P: the instances' parameters; rq: the replicas' slots (replica t > 0 of instance b is slot
+// b (reps - 1) + t - 1)
+template <int K>
+__global__ void __launch_bounds__(ST_THREADS) k_persist(DevParams P, RepBlock rq, PersistSync sy, int steps) {
+  extern __shared__ double tile_lds[];   // TS x TS doubles (the stored tile)
+  __shared__ double redbuf[2 * ST_WAVES * RED_MAX];
+  __shared__ double csl[2][SP_WAVES][TS];
+  __shared__ double vl[2][2][TS];        // the pass inputs' blocks I and J (per right-hand side)
+  __shared__ double hot[ST_HOT];         // the replica's hot scalars between steps
+  __shared__ double bclk;
+  __shared__ int bfail, bnr, bact;
+  __shared__ LeanIO lio;
+  const int R = P.ntiles;
+  const int b = blockIdx.x / R, t = blockIdx.x - b * R;
+  if (b >= P.batch || steps <= 0) return;
+  const bool rep0 = t == 0;
+  const int bm = rep0 ? b : b * (R - 1) + (t - 1);   // the replica's slot in its parameter block
+  double* const gst = (rep0 ? P.st : rq.st) + (int64_t)bm * ST_N;
+  // every replica of an instance sees the same phase, so these exits are uniform per instance
+  const int ph0 = (int)gst[ST_PHASE];
+  const bool waiting = ph0 == PH_TCG || ph0 == PH_TRIAL || ph0 == PH_AFTER_SX0 || ph0 == PH_TCGO_SX;
+  const bool startable = ph0 == PH_START || ph0 == PH_TCGO_START ||
+                         (ph0 == PH_PAUSED && (double)P.outer_target > gst[ST_OUTER_IT]);
+  if (!waiting && !startable) return;
+  if (threadIdx.x < ST_HOT) hot[threadIdx.x] = gst[threadIdx.x];
+  if (threadIdx.x == 0) {
+    bnr = (rep0 ? P.req : rq.req)[bm];   // the pass the previous launch left pending (if waiting)
+    bact = ACT_YIELD;
+  }
+  int I, J;
+  tile_ij(t, P.nt, I, J);
+  {  // the tile, once per launch
+    const int rowsT = (I == P.nt - 1) ? P.wl : TS;
+    const int colsT = (J == P.nt - 1) ? P.wl : TS;
+    const double* T = P.S + (int64_t)b * P.inst_stride + sym_off(I, J, P.nt, P.wl);
+    for (int i = 2 * (int)threadIdx.x; i < rowsT * colsT; i += 2 * ST_THREADS)
+      *(dbl2*)(tile_lds + i) = __builtin_nontemporal_load((const dbl2*)(T + i));
+  }
+  double* const vbm = (rep0 ? P.vec : rq.vec) + (int64_t)bm * P.ld;
+  const int64_t vks = (int64_t)(rep0 ? P.batch : rq.batch) * P.ld;
+  double* const pb0 = P.pbuf;
+  double* const pb1 = sy.pbuf2;
+  const int tsel = blockIdx.x == 0 ? 0 : ((int)blockIdx.x == R - 1 ? 1 : -1);
+  unsigned epoch = 1;
+  double clk = 0.0;
+  bool ok = persist_barrier(sy, P.batch, b, R, rep0, epoch++, clk, &bclk, &bfail);   // uniform start clock
+  // Step k >= 0 = S-pass k, then the state machine until its next request; tCG iterations run as
+  // lean runs (lean_tcg_run, not inlined: vectors and scalars in registers across iterations,
+  // tcg_math = the function k_state's tcg_step_reg runs, bitwise identical); every other step
+  // builds the machine from the LDS copy of its hot scalars, runs it inline, and writes them back.
+  int k = startable ? -1 : 0;
+  while (ok && bact == ACT_YIELD && k < steps) {
+    int stop = TCG_CONTINUE;
+    if (k >= 0 && (int)hot[ST_PHASE] == PH_TCG && P.n <= K * ST_THREADS) {
+      LeanArgs la;
+      la.vk = vbm;
+      la.vks = vks;
+      la.gcold = gst;
+      la.pb[0] = pb0;
+      la.pb[1] = pb1;
+      la.sy = sy;
+      la.n = P.n;
+      la.b = b;
+      la.t = t;
+      la.R = R;
+      la.I = I;
+      la.J = J;
+      la.steps = steps;
+      la.batch = P.batch;
+      la.rep0 = rep0 ? 1 : 0;
+      la.tsel = tsel;
+      la.kappa = P.opt.tcg_kappa;
+      la.theta = P.opt.tcg_theta;
+      la.mininner = P.opt.tcg_mininner;
+      la.pbatch = P.pbatch;
+      la.nt = P.nt;
+      la.wl = P.wl;
+      if (threadIdx.x == 0) {
+        lio.k = k;
+        lio.epoch = epoch;
+        lio.clk = clk;
+      }
+      __syncthreads();
+      lean_tcg_run<K>(la, &lio, (const lds_f64*)tile_lds, (lds_f64*)&vl[0][0][0], (lds_f64*)&csl[0][0][0],
+                      (lds_f64*)redbuf, (lds_f64*)hot, (lds_f64*)&bclk, &bfail);
+      k = lio.k;
+      epoch = lio.epoch;
+      clk = lio.clk;
+      ok = lio.ok != 0;
+      stop = lio.stop;
+      if (!ok || stop == TCG_CONTINUE) continue;   // barrier failure, or the budget ended mid-run
+    } else if (k >= 0) {
+      // one pass of the machine's request: blocks I and J of its inputs, one load round trip
+      const int q = threadIdx.x >> 7, e = threadIdx.x & (TS - 1);   // q: rhs * 2 + block
+      if (q < 2 * bnr) vl[q >> 1][q & 1][e] = vbm[(q >> 1 ? V_IN1 : V_IN0) * vks + ((q & 1) ? J : I) * TS + e];
+      __syncthreads();
+      unsigned long long* tr = (sy.trace && tsel >= 0 && k < sy.trace_cap && threadIdx.x == 0)
+                                   ? sy.trace + ((int64_t)tsel * sy.trace_cap + k) * 24 : nullptr;
+      if (tr) tr[0] = wall_clock64();
+      if (bnr == 2) spass_tile_lds<2>(P, tile_lds, vl, (k & 1) ? pb1 : pb0, b, t, csl);
+      else spass_tile_lds<1>(P, tile_lds, vl, (k & 1) ? pb1 : pb0, b, t, csl);
+      if (tr) tr[1] = wall_clock64();
+      ok = persist_barrier(sy, P.batch, b, R, rep0, epoch++, clk, &bclk, &bfail);
+      if (!ok) break;
+      if (tr) tr[2] = wall_clock64();
+    }
+    // the machine: (re)start (k = -1), after a pass, or after a lean run stopped (then tcg_end)
+    MachineT<false, true> M(P, bm, 0, redbuf, nullptr, hot, !rep0, rq);
+    M.bp = b;
+    M.uclk = clk;
+    const int kp = k >= 0 ? k : 0;
+    M.pb = ((stop != TCG_CONTINUE ? kp - 1 : kp) & 1) ? pb1 : pb0;
+    int act;
+    if (stop != TCG_CONTINUE) {   // a lean run stopped: the rest of compute_direction + the trial point
+      act = M.tcg_end();
+    } else {   // one dispatch call site (as in k_state): the machine is inlined once
+      if (k >= 0) M.gather_out(bnr);
+      act = M.dispatch();
+      ++k;
+    }
+    __syncthreads();   // every thread has read hot / bnr
+    if (threadIdx.x == 0) {   // static indices: s[] stays in registers
+#pragma unroll
+      for (int q = 0; q < ST_HOT; ++q) hot[q] = M.s[q];
+      bnr = M.last_nr;
+      bact = act;
+    }
+    if (act != ACT_YIELD) M.finish_write();
+    __syncthreads();
+  }
+  if (ok && bact != ACT_YIELD) return;   // finished or paused: finish_write done in the step
+  // still waiting for an S-pass (step budget used up) or a peer never arrived: write the scalars back
+  MachineT<false, true> M(P, bm, 0, redbuf, nullptr, hot, !rep0, rq);
+  if (!ok) {   // the instance stops with an error (the host reports it)
+    M.s[ST_PHASE] = PH_ERROR;
+    M.cset(ST_ERROR, 2.0);
+  }
+  M.finish_write();
+}
+
+// instances of the batch still running after a persistent launch (waiting for an S-pass, or
+// startable): the count the lock-step path keeps in its active list
+__global__ void __launch_bounds__(256) k_persist_count(DevParams P, int list) {
+  __shared__ int c;
+  if (threadIdx.x == 0) c = 0;
+  __syncthreads();
+  for (int b = threadIdx.x; b < P.batch; b += blockDim.x) {
+    const double* g = P.st + (int64_t)b * ST_N;
+    const int ph = (int)g[ST_PHASE];
+    const bool run = ph == PH_TCG || ph == PH_TRIAL || ph == PH_AFTER_SX0 || ph == PH_TCGO_SX || ph == PH_START ||
+                     ph == PH_TCGO_START || (ph == PH_PAUSED && (double)P.outer_target > g[ST_OUTER_IT]);
+    if (run) atomicAdd(&c, 1);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) P.cnt[list] = c;
+}
+
 // riptrm_log_rebase: every record logged so far counts as drained
 __global__ void __launch_bounds__(256) k_log_rebase(DevParams P) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1962,14 +2582,17 @@ __global__ void __launch_bounds__(256) k_log_rebase(DevParams P) {
 }
 
 // initialise a solve: x0/y0 -> X/Y, scalars
+// rep_div > 1: P is the persistent replicas' block (batch x (reps - 1) slots), slot b replicates
+// instance b / rep_div of the caller's arrays
 __global__ void __launch_bounds__(256) k_init(DevParams P, const double* x0, const double* y0, int64_t ldv,
-                                              const double* mu, const double* delta, int mode) {
+                                              const double* mu, const double* delta, int mode, int rep_div) {
   const int b = blockIdx.x;
+  const int src = b / rep_div;
   double* X = vp(P, V_X, b);
   double* Y = vp(P, V_Y, b);
   for (int i = threadIdx.x; i < P.n; i += blockDim.x) {
-    X[i] = x0[(int64_t)b * ldv + i];
-    Y[i] = y0[(int64_t)b * ldv + i];
+    X[i] = x0[(int64_t)src * ldv + i];
+    Y[i] = y0[(int64_t)src * ldv + i];
   }
   if (threadIdx.x == 0) {
     double* s = P.st + (int64_t)b * ST_N;
@@ -1981,8 +2604,8 @@ __global__ void __launch_bounds__(256) k_init(DevParams P, const double* x0, con
       s[ST_DELTA] = P.opt.initial_tr_radius;
     } else {
       s[ST_PHASE] = PH_TCGO_START;
-      s[ST_MU] = mu[b];
-      s[ST_DELTA] = delta[b];
+      s[ST_MU] = mu[src];
+      s[ST_DELTA] = delta[src];
     }
     s[ST_I_DC] = -1.0;
     s[ST_T_START] = (double)wall_clock64();
@@ -2219,6 +2842,88 @@ __global__ void k_list_range(DevParams P, int base, int count) {
 // timing-based choice could make two runs of the same solve differ in the last bits; the default
 // (kind 1) therefore uses the fixed rule of spass_mode and never times anything.
 static int launch_gemv(riptrm_ctx* c, hipStream_t st, int list_in, int zero_cnt, int bound, int smode);
+static DevParams params_for(const riptrm_ctx* c, int smode);
+
+// the persistent replicas' parameter block: the instances' parameters with the replica region's
+// vectors, scalars, stats and requests (batch x (reps - 1) slots), no log, the instances' grid
+static DevParams persist_params(const riptrm_ctx* c) {
+  DevParams Q = c->P;
+  const Layout& L = c->L;
+  Q.batch = c->P.batch * (L.reps > 1 ? L.reps - 1 : 0);
+  Q.vec = (double*)(c->ws + L.off_rvec);
+  Q.st = (double*)(c->ws + L.off_rstate);
+  Q.stats = (double*)(c->ws + L.off_rstats);
+  Q.req = (int32_t*)(c->ws + L.off_rreq);
+  Q.log = nullptr;
+  Q.cap = 0;
+  Q.pbatch = c->P.batch;
+  Q.smode = 0;
+  return Q;
+}
+
+static PersistSync persist_sync(const riptrm_ctx* c) {
+  const Layout& L = c->L;
+  PersistSync sy;
+  char* base = c->ws + L.off_sync;
+  sy.ctr = (unsigned int*)base;
+  sy.clk = (double*)(base + round_up((int64_t)c->P.batch * 4, 16));
+  sy.flag = (unsigned int*)(base + round_up((int64_t)c->P.batch * 4, 16) + (int64_t)2 * c->P.batch * 8);
+  sy.pbuf2 = (double*)(c->ws + L.off_pbuf2);
+  sy.trace = c->persist_trace;
+  sy.trace_cap = c->persist_trace_cap;
+  return sy;
+}
+
+// solve / tCG start: replicas get the instances' starting state too
+static int persist_init(riptrm_ctx* c, const double* x, const double* y, int64_t ldv, const double* mu,
+                        const double* delta, int mode) {
+  c->persist_on = c->persist_ok && c->P.opt.trs_solver == RIPTRM_TRS_SOLVER_TCG;
+  if (!c->persist_on || c->L.reps <= 1) return RIPTRM_OK;
+  const DevParams Q = persist_params(c);
+  hipLaunchKernelGGL(k_init, dim3((unsigned)Q.batch), dim3(256), 0, c->stream, Q, x, y, ldv, mu, delta, mode,
+                     c->L.reps - 1);
+  HIPCHK(c, hipGetLastError());
+  return RIPTRM_OK;
+}
+
+// `steps` lock-step iterations of the whole batch in one k_persist launch
+static int persist_run(riptrm_ctx* c, int steps, int* n_active) {
+  const PersistSync sy = persist_sync(c);
+  HIPCHK(c, hipMemsetAsync(c->ws + c->L.off_sync, 0, (size_t)c->L.sync_bytes, c->stream));
+  if (steps > 0) {
+    int i0 = -1, i1 = -1;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (c->prof && (e0 = prof_event(c, &i0)) && (e1 = prof_event(c, &i1))) HIPCHK(c, hipEventRecord(e0, c->stream));
+    const unsigned grid = (unsigned)(c->P.batch * c->L.reps);
+    const DevParams Q = persist_params(c);
+    const RepBlock rq{Q.vec, Q.st, Q.stats, Q.req, Q.batch};
+    static_assert(PERSIST_MAX_N <= 4 * ST_THREADS, "k_persist<4> covers every persistent shape");
+    if (c->P.n <= 2 * ST_THREADS)
+      hipLaunchKernelGGL(k_persist<2>, dim3(grid), dim3(ST_THREADS), (size_t)TS * TS * sizeof(double), c->stream,
+                         params_for(c, 0), rq, sy, steps);
+    else
+      hipLaunchKernelGGL(k_persist<4>, dim3(grid), dim3(ST_THREADS), (size_t)TS * TS * sizeof(double), c->stream,
+                         params_for(c, 0), rq, sy, steps);
+    HIPCHK(c, hipGetLastError());
+    if (c->prof && e1) {
+      HIPCHK(c, hipEventRecord(e1, c->stream));
+      c->ev_state.push_back({i0, i1});
+    }
+  }
+  hipLaunchKernelGGL(k_persist_count, dim3(1), dim3(256), 0, c->stream, c->P, c->parity[0]);
+  HIPCHK(c, hipGetLastError());
+  int32_t h = 0;
+  uint32_t flag = 0;
+  HIPCHK(c, hipMemcpyAsync(&h, c->P.cnt + c->parity[0], sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipMemcpyAsync(&flag, sy.flag, sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (c->prof) prof_collect(c);
+  c->active_bound[0] = h;
+  if (n_active) *n_active = h;
+  if (flag) return fail(c, RIPTRM_E_HIP, "persistent lock-step: a workgroup waited > 2 s at an in-launch barrier "
+                                        "(instance stopped with STAT_ERROR = 2)");
+  return RIPTRM_OK;
+}
 
 static int calibrate_spass(riptrm_ctx* c) {
   c->sup_auto = 1;
@@ -2296,8 +3001,18 @@ int riptrm_nonnegpca_bind(riptrm_ctx* ctx, const double* S, int32_t n, int32_t b
   P.lists = (int32_t*)(ctx->ws + L.off_lists);
   P.req = (int32_t*)(ctx->ws + L.off_req);
   P.cnt = (int32_t*)(ctx->ws + L.off_cnt);
+  P.pbatch = batch;
   P.clock_hz = ctx->clock_hz;
   P.outer_target = INT32_MAX;
+  // persistent mode: the workspace has the replica region and every workgroup fits on its own CU
+  ctx->persist_ok = ctx->persist_req != 0 && L.reps > 0 && (int64_t)batch * L.reps <= ctx->ncu;
+  ctx->persist_on = false;
+  if (ctx->persist_ok) {
+    HIPCHK(ctx, hipFuncSetAttribute((const void*)k_persist<2>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)(TS * TS * sizeof(double))));
+    HIPCHK(ctx, hipFuncSetAttribute((const void*)k_persist<4>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)(TS * TS * sizeof(double))));
+  }
   // two groups only when one group's S-pass is long enough (>= ~0.6 GB, ~100 us) to hide the
   // other group's state kernel; small batches are launch/latency bound and lose from the split
   ctx->ngroups = (layout != RIPTRM_LAYOUT_SHARED && batch >= 8 &&
@@ -2494,6 +3209,7 @@ static int capture_graph(riptrm_ctx* c, int bound) {
 }
 
 static int run_steps(riptrm_ctx* c, int steps, int* n_active) {
+  if (c->persist_on) return persist_run(c, steps, n_active);
   // short kernels (small n x batch): replay a captured graph of GRAPH_STEPS iterations instead of
   // launching 2 kernels per step from the host
   const bool small = (double)c->P.batch * (double)s_elems_of(c->P.n, c->P.layout) * 8.0 < 2.0e8 ||
@@ -2553,6 +3269,10 @@ static int run_steps(riptrm_ctx* c, int steps, int* n_active) {
 // launch per group that APPENDS their requests to the group's list `parity`, the one its next
 // S-pass reads, so the requests of instances already in flight stay queued.
 static int kick(riptrm_ctx* c) {
+  if (c->persist_on) {   // k_persist starts startable instances itself (with the uniform clock)
+    c->active_bound[0] = c->P.batch;
+    return RIPTRM_OK;
+  }
   int rc = fork_streams(c);
   if (rc) return rc;
   for (int g = 0; g < c->ngroups; ++g) {
@@ -2582,8 +3302,9 @@ int riptrm_tcg(riptrm_ctx* ctx, const double* x, const double* y, int64_t ldv, c
     P.opt.tcg_mininner = 1;
     ctx->pver++;
   }
-  hipLaunchKernelGGL(k_init, dim3(P.batch), dim3(256), 0, ctx->stream, P, x, y, ldv, mu, delta, (int)MODE_TCG_ONLY);
+  hipLaunchKernelGGL(k_init, dim3(P.batch), dim3(256), 0, ctx->stream, P, x, y, ldv, mu, delta, (int)MODE_TCG_ONLY, 1);
   HIPCHK(ctx, hipGetLastError());
+  if (int rc0 = persist_init(ctx, x, y, ldv, mu, delta, (int)MODE_TCG_ONLY)) return rc0;
   reset_groups(ctx);
   HIPCHK(ctx, hipMemsetAsync(P.cnt, 0, 4 * sizeof(int32_t), ctx->stream));
   int rc = kick(ctx);
@@ -2641,8 +3362,9 @@ int riptrm_solve_begin(riptrm_ctx* ctx, const riptrm_options* opt, const double*
   P.outer_target = INT32_MAX;
   ctx->pver++;
   hipLaunchKernelGGL(k_init, dim3(P.batch), dim3(256), 0, ctx->stream, P, x0, y0, ldv, (const double*)nullptr,
-                     (const double*)nullptr, (int)MODE_SOLVE);
+                     (const double*)nullptr, (int)MODE_SOLVE, 1);
   HIPCHK(ctx, hipGetLastError());
+  if (int rc0 = persist_init(ctx, x0, y0, ldv, nullptr, nullptr, (int)MODE_SOLVE)) return rc0;
   reset_groups(ctx);
   HIPCHK(ctx, hipMemsetAsync(P.cnt, 0, 4 * sizeof(int32_t), ctx->stream));
   ctx->solving = true;
@@ -2668,6 +3390,27 @@ int riptrm_set_spass_kind(riptrm_ctx* ctx, int32_t kind) {
   if (!ctx || kind < 0 || kind > 3) return RIPTRM_E_ARG;
   ctx->sup_req = kind;
   ctx->pver++;   // a captured graph holds the old kernel
+  return RIPTRM_OK;
+}
+
+int riptrm_set_persistent(riptrm_ctx* ctx, int32_t mode) {
+  if (!ctx || mode < 0 || mode > 1) return RIPTRM_E_ARG;
+  if (ctx->solving) return fail(ctx, RIPTRM_E_STATE, "set_persistent: call before riptrm_nonnegpca_bind");
+  ctx->persist_req = mode;
+  return RIPTRM_OK;
+}
+
+int riptrm_persist_trace(riptrm_ctx* ctx, uint64_t* buf, int32_t cap) {
+  if (!ctx || cap < 0 || (cap > 0 && !buf)) return RIPTRM_E_ARG;
+  ctx->persist_trace = cap > 0 ? (unsigned long long*)buf : nullptr;
+  ctx->persist_trace_cap = cap;
+  return RIPTRM_OK;
+}
+
+int riptrm_get_persistent(riptrm_ctx* ctx, int32_t* possible, int32_t* active) {
+  if (!ctx || !possible || !active) return RIPTRM_E_ARG;
+  *possible = ctx->persist_ok ? 1 : 0;
+  *active = ctx->persist_on ? 1 : 0;
   return RIPTRM_OK;
 }
 

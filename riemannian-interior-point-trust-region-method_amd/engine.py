@@ -214,7 +214,8 @@ class NonnegPCABatch:
     problem_initialpoint axis), S-pass on the fp64 matrix cores."""
 
     def __init__(self, n: int, batch: int, device: Optional[int] = None, log_capacity: int = 4096,
-                 layout: str = "sym", stream_groups: int = 0, spass_kind: int = 1, drain_logs: bool = True):
+                 layout: str = "sym", stream_groups: int = 0, spass_kind: int = 1, drain_logs: bool = True,
+                 persistent: int = 1):
         if not torch.cuda.is_available():
             raise RuntimeError("NonnegPCABatch needs a ROCm GPU (gfx950); there is no CPU fallback")
         if n < 2 or batch < 1:
@@ -233,6 +234,8 @@ class NonnegPCABatch:
         self.ctx = N.Context(self.device.index, _stream_handle(self.device))
         self.ctx.check(self.lib.riptrm_set_stream_groups(self.ctx.h, int(stream_groups)), "riptrm_set_stream_groups")
         self.ctx.check(self.lib.riptrm_set_spass_kind(self.ctx.h, int(spass_kind)), "riptrm_set_spass_kind")
+        # small symmetric-tile batches: the whole lock-step loop in one launch per chunk (k_persist)
+        self.ctx.check(self.lib.riptrm_set_persistent(self.ctx.h, int(persistent)), "riptrm_set_persistent")
         self.S = torch.zeros((1 if self.shared else self.batch, self.inst_stride), dtype=torch.float64,
                              device=self.device)
         nbytes = int(self.lib.riptrm_workspace_bytes(self.n, self.batch, self.cap, self.layout))
@@ -426,6 +429,14 @@ class NonnegPCABatch:
                                                              ctypes.byref(k)), "riptrm_get_spass_calibration")
         return {"ms_per_launch_tile": t.value, "ms_per_launch_super": u.value,
                 "kernel": "k_spass_sup" if k.value == 1 else "k_spass_sym"}
+
+    def persistent_state(self) -> Dict[str, bool]:
+        """riptrm_get_persistent: whether the bound shape runs k_persist on this device, and whether
+        the current solve / tCG run uses it."""
+        pos, act = ctypes.c_int32(), ctypes.c_int32()
+        self.ctx.check(self.lib.riptrm_get_persistent(self.ctx.h, ctypes.byref(pos), ctypes.byref(act)),
+                       "riptrm_get_persistent")
+        return {"possible": bool(pos.value), "active": bool(act.value)}
 
     def hvp(self, x, y, mu: float, v) -> torch.Tensor:
         """HwCur(v) at (x, y, mu) for every instance (RIPTRM.py:729)."""

@@ -74,6 +74,9 @@ SIGNATURES: Dict[str, tuple] = {
     "riptrm_log_rebase": (c_int32, [c_void_p]),
     "riptrm_set_stream_groups": (c_int32, [c_void_p, c_int32]),
     "riptrm_set_graphs": (c_int32, [c_void_p, c_int32]),
+    "riptrm_set_persistent": (c_int32, [c_void_p, c_int32]),
+    "riptrm_get_persistent": (c_int32, [c_void_p, P_int32, P_int32]),
+    "riptrm_persist_trace": (c_int32, [c_void_p, c_void_p, c_int32]),
     "riptrm_set_spass_kind": (c_int32, [c_void_p, c_int32]),
     "riptrm_get_spass_calibration": (c_int32, [c_void_p, ctypes.POINTER(c_double), ctypes.POINTER(c_double), P_int32]),
     "riptrm_profile_enable": (c_int32, [c_void_p, c_int32]),

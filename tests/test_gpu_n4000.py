@@ -60,7 +60,18 @@ def trajectory():
 
 
 def test_n4000_tcg_teacher_forced(trajectory):
-    """Same (x, y, mu, Delta) in -> same tCG exit (stop reason and j) and eta to 1e-9."""
+    """Same (x, y, mu, Delta) in -> same tCG exit reason, and j and eta within the spread of CPU
+    oracles that differ only in summation order.
+
+    Calibration: at n = 4000 the longest tCG of the trajectory (mu ~ 2e-7, j ~ 2000 of at most
+    3999 iterations) is a CG run far past the point where rounding stops mattering: the iteration
+    index of its REACHED_TARGET exit and eta's last digits are rounding quantities (the dsymv
+    oracle exits at j = 2011 on the GPU box and 2015 here; dsymv vs dgemv differ by 8 iterations
+    and 2e-8..5e-7 in eta depending on the machine's BLAS).  So short runs (j < 50) must match j
+    exactly and eta to 1e-9; long ones are compared with an envelope of three CPU variants that are
+    the same arithmetic in another order (dgemv, and dsymv on two symmetric permutations of the
+    problem, P S P^T with x, y permuted): |dj| <= max(2 x their largest |dj|, 0.5% of j), eta
+    within 3 x their largest distance."""
     import engine
     Z, states = trajectory
     longest = max(range(len(states)), key=lambda i: states[i][4])
@@ -78,14 +89,41 @@ def test_n4000_tcg_teacher_forced(trajectory):
     eta = eta.cpu().numpy()
     heta = heta.cpu().numpy()
     P = O.NonnegPCAVectorized(Z)
+    perms = [np.random.RandomState(s).permutation(N) for s in (1, 2)]
+    variants = [(O.NonnegPCAVectorized(Z, symv=False), None)] + \
+               [(O.NonnegPCAVectorized(np.ascontiguousarray(Z[p][:, p])), p) for p in perms]
     assert states[longest][4] >= 50          # a long CG run is really in the set
     assert mus.min() <= 1e-6
+    done = {}
     for b in range(B):
         _, _, Hw, c = P.begin_inner(xs[b], ys[b], mus[b])
         e, he, j, stop = O.truncated_conjugate_gradient(P.manifold, Hw, xs[b], c, deltas[b], 1, 0.1, 1, N - 1)
-        assert stops[b] == stop and js[b] == j, (b, mus[b], deltas[b], stops[b], stop, js[b], j)
-        assert np.linalg.norm(eta[b] - e) <= 1e-9 * np.linalg.norm(e), (b, np.linalg.norm(eta[b] - e) / np.linalg.norm(e))
-        assert np.linalg.norm(heta[b] - he) <= 1e-8 * np.linalg.norm(he), b
+        assert stops[b] == stop, (b, mus[b], deltas[b], stops[b], stop, js[b], j)
+        if j < 50:
+            assert js[b] == j, (b, js[b], j)
+            assert np.linalg.norm(eta[b] - e) <= 1e-9 * np.linalg.norm(e), (b, np.linalg.norm(eta[b] - e) / np.linalg.norm(e))
+            assert np.linalg.norm(heta[b] - he) <= 1e-8 * np.linalg.norm(he), b
+            continue
+        key = (picks[b][0], deltas[b])
+        if key not in done:
+            dj, de, dh = 0, 0.0, 0.0
+            for Pv, p in variants:
+                x, y = (xs[b], ys[b]) if p is None else (xs[b][p], ys[b][p])
+                _, _, Hv, cv = Pv.begin_inner(x, y, mus[b])
+                e2, he2, j2, stop2 = O.truncated_conjugate_gradient(Pv.manifold, Hv, x, cv, deltas[b], 1, 0.1, 1, N - 1)
+                if p is not None:
+                    inv = np.argsort(p)
+                    e2, he2 = e2[inv], he2[inv]
+                assert stop2 == stop, (b, stop2, stop)
+                dj = max(dj, abs(j2 - j))
+                de = max(de, np.linalg.norm(e2 - e))
+                dh = max(dh, np.linalg.norm(he2 - he))
+            done[key] = (dj, de, dh)
+        dj, de, dh = done[key]
+        assert abs(int(js[b]) - j) <= max(2 * dj, 0.005 * j), (b, js[b], j, dj)
+        ne, nh = np.linalg.norm(e), np.linalg.norm(he)
+        assert np.linalg.norm(eta[b] - e) <= max(1e-9 * ne, 3 * de), (b, np.linalg.norm(eta[b] - e) / ne, de / ne)
+        assert np.linalg.norm(heta[b] - he) <= max(1e-8 * nh, 3 * dh), (b, np.linalg.norm(heta[b] - he) / nh, dh / nh)
 
 
 def test_n4000_solve_matches_oracle():

@@ -1,0 +1,111 @@
+"""Persistent lock-step mode (k_persist, csrc/riptrm_kernels.hip) against the lock-step kernels
+(k_spass_sym + k_state) on the same inputs: bitwise identical iterates, logs (except the time
+column) and counters.  k_persist runs the reference's tCG loop (RIPTRM.py:41-216) and the inner /
+outer loops (:707-896) of small symmetric-tile batches in one launch per chunk: every stored tile
+of S stays in LDS, every workgroup of an instance runs a replica of the instance's state machine,
+and the S-pass partial sums are exchanged through write-through stores + one arrival counter per
+instance.  The arithmetic (tile products, partial-sum order, reductions) is the lock-step path's,
+so the bar is equality, not a tolerance.  Shapes: n <= 1024 (2 elements per thread) and
+1024 < n <= 2048 (4 per thread), one tile (no exchange) up to 136 tiles, up to 7 instances.
+"""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+from oracle import nonnegpca_gen as G
+
+
+def _opt(**kw):
+    from problems import manviofun
+    o = {"TRS_solver": "tCG", "second_order_stationarity": False, "manviofun": manviofun,
+         "tolresid": 0.0, "maxtime": 1e9}
+    o.update(kw)
+    return o
+
+
+def _solve(insts, persistent, **kw):
+    import engine
+    n, B = insts[0][0].shape[0], len(insts)
+    eng = engine.NonnegPCABatch(n, B, log_capacity=4096, persistent=persistent)
+    eng.load_Z(np.stack([z for z, _, _ in insts]))
+    res = eng.solve(np.stack([x for _, x, _ in insts]), np.stack([y for _, _, y in insts]), _opt(**kw))
+    return eng, res
+
+
+def _assert_same(ra, rb, B):
+    import engine
+    assert torch.equal(ra.x, rb.x) and torch.equal(ra.y, rb.y)
+    for b in range(B):
+        la, lb = ra.log(b), rb.log(b)
+        assert list(la.keys()) == list(lb.keys())
+        for k in la:
+            if k != "time":
+                assert la[k] == lb[k] or np.array_equal(np.array(la[k], float), np.array(lb[k], float)), (b, k)
+        for f in ("OUTER_ITERS", "INNER_ITERS", "TCG_ITERS", "PASSES", "STOP_CODE"):
+            assert ra.stat(b, f) == rb.stat(b, f), (b, f)
+
+
+@pytest.mark.parametrize("n,B,K", [(37, 5, 10), (200, 4, 10), (1000, 1, 10), (1000, 7, 6), (1500, 1, 6),
+                                   (2048, 1, 5)])
+def test_persistent_matches_lockstep_bitwise(n, B, K):
+    insts = [G.generate_instance(n, 900 + b) for b in range(B)]
+    e1, r1 = _solve(insts, 1, maxiter=K)
+    assert e1.persistent_state() == {"possible": True, "active": True}
+    e0, r0 = _solve(insts, 0, maxiter=K)
+    assert e0.persistent_state()["active"] is False
+    _assert_same(r1, r0, B)
+
+
+def test_persistent_teacher_forced_tcg_bitwise():
+    """riptrm_tcg (MODE_TCG_ONLY) through k_persist == through the lock-step kernels."""
+    import engine
+    n, B = 1000, 3
+    Z, x0, _ = G.generate_instance(n, 77)
+    rs = np.random.RandomState(4)
+    xs = np.stack([np.abs(rs.rand(n)) for _ in range(B)])
+    xs /= np.linalg.norm(xs, axis=1, keepdims=True)
+    ys = rs.rand(B, n) + 0.1
+    mus, deltas = np.array([0.1, 1e-3, 1e-6]), np.array([np.pi / 8, 1e-3, 5.0])
+    out = []
+    for mode in (1, 0):
+        eng = engine.NonnegPCABatch(n, B, persistent=mode)
+        eng.load_Z(np.broadcast_to(Z, (B, n, n)))
+        out.append(eng.tcg(xs, ys, mus, deltas))
+    (e1, h1, j1, s1), (e0, h0, j0, s0) = out
+    assert torch.equal(e1, e0) and torch.equal(h1, h0)
+    assert list(j1) == list(j0) and s1 == s0
+
+
+def test_persistent_pause_resume_and_drain():
+    """outer_target pauses, resumes and host log drains between persistent launches change nothing."""
+    import engine
+    n, B = 1000, 2
+    insts = [G.generate_instance(n, 950 + b) for b in range(B)]
+    Z = np.stack([z for z, _, _ in insts])
+    X0 = np.stack([x for _, x, _ in insts])
+    Y0 = np.stack([y for _, _, y in insts])
+    ref = engine.NonnegPCABatch(n, B, log_capacity=4096, persistent=0)
+    ref.load_Z(Z)
+    r0 = ref.solve(X0, Y0, _opt(maxiter=9))
+    eng = engine.NonnegPCABatch(n, B, log_capacity=16, persistent=1)   # 16 slots: drained every few chunks
+    eng.load_Z(Z)
+    eng.begin(X0, Y0, _opt(maxiter=9))
+    for tgt in (2, 5, None):
+        eng.run_until(tgt)
+    r1 = eng.result()
+    assert eng.persistent_state()["active"]
+    _assert_same(r1, r0, B)
+
+
+def test_persistent_not_used_when_too_large():
+    """Shapes beyond one workgroup per tile per CU keep the lock-step kernels."""
+    import engine
+    eng = engine.NonnegPCABatch(2176, 1)   # n > 2048
+    Z, x0, y0 = G.generate_instance(2176, 3)
+    eng.load_Z(Z[None])
+    assert eng.persistent_state()["possible"] is False
+    eng2 = engine.NonnegPCABatch(1000, 8)  # 8 x 36 tiles > 256 workgroups
+    eng2.load_Z(np.broadcast_to(Z[:1000, :1000], (8, 1000, 1000)))
+    assert eng2.persistent_state()["possible"] is False

@@ -133,20 +133,64 @@ def test_si_batch_of_fixture_starts_matches_oracle(data):
         compare_until_flip(res.log(b), ref.log)
 
 
-def test_si_reaches_published_residual(data):
-    """analyzer.ipynb (StableIdentification): RIPTRM (tCG) median log10 residual -12.37 in 240 s.
-    The inner loop cannot meet max(mu, 1e-14) once mu bottoms out, so bound it with inner_maxiter."""
-    xs, ys = _starts(PTS)
-    res = _batch(data, len(PTS), cap=8192).solve(xs, ys, _gpu_opt(maxiter=36, inner_maxiter=300))
-    best = []
-    for b in range(len(PTS)):
+def _pins():
+    import json
+    with open(os.path.join(GOLDEN, "si_1_pins", "oracle_minres.json")) as f:
+        return json.load(f)
+
+
+def _min_log_res(res, B):
+    """analyzer.ipynb box-plot cell: per start, log10 of the minimum KKT residual over every log row."""
+    out = []
+    for b in range(B):
         lg = res.log(b)
         r = np.array(lg["residual"], float)
-        conv = [i for i, s in enumerate(lg["inner_status"]) if s in (None, "converged")]
-        best.append(np.log10(r[conv].min()))
-    best = np.array(best)
-    assert (best < -11.0).all(), best
-    assert -13.5 <= np.median(best) <= -11.5, np.median(best)
+        out.append((float(np.log10(r.min())), int(lg["iteration"][int(r.argmin())])))
+    return out
+
+
+def test_si_tcg_pinned_to_published_result(data):
+    """The reference's own RIPTRM (tCG) result on this fixture (analyzer.ipynb, box-plot cell):
+    per-start min log10 KKT residual, start t = -12.475348, quartiles over the 20 starts
+    Q1 / median / Q3 = -12.444660 / -12.368153 / -12.225336.  Those minima sit on the rounding
+    plateau near mu ~ 1e-13 (outer iteration 33-35), where two fp64 implementations of the same
+    algorithm differ by ~0.05 per start: the CPU oracle under the same protocol gives quartiles
+    -12.458 / -12.414 / -12.238 (tests/golden/si_1_pins, generated by tests/golden/make_si_pins.py).
+    Protocol: maxiter 35, inner_maxiter 300 (the reference ran into its 240 s limit in the stalled
+    outer iteration instead).  Bar: quartiles within 0.1 of the published ones, start t within 0.1,
+    every start below 1e-11 and its minimum in outer iteration >= 32."""
+    pins = _pins()
+    pub = pins["published"]
+    xs, ys = _starts(PTS)
+    opt = pins["protocol"]["tcg"]
+    res = _batch(data, len(PTS), cap=16384).solve(xs, ys, _gpu_opt(maxiter=opt["maxiter"], inner_maxiter=opt["inner_maxiter"]))
+    got = _min_log_res(res, len(PTS))
+    v = np.array([g for g, _ in got])
+    q = [np.quantile(v, 0.25), np.median(v), np.quantile(v, 0.75)]
+    assert all(abs(a - p) <= 0.1 for a, p in zip(q, pub["tcg_quartiles"])), (q, pub["tcg_quartiles"], pins["tcg_quartiles"])
+    assert abs(got[PTS.index("t")][0] - pub["tcg_start_t"]) <= 0.1, got[PTS.index("t")]
+    assert (v < -11.0).all() and all(it >= 32 for _, it in got), got
+
+
+def test_si_exact_pinned_to_published_plateau(data):
+    """The reference's RIPTRM (exact) result (analyzer.ipynb, box-plot cell): min log10 KKT residual
+    -8.787497 for EVERY one of the 20 starts (Q1 = median = Q3).  The exact runs stall inside outer
+    iteration 25 (mu_25 = 4.078e-10: the inner loop keeps taking successful steps at residual
+    4 mu_25 = 1.6312e-9 and never meets its tolerance), so the published minimum is a property of the
+    algorithm: the mu schedule (RIPTRM.py:866-896), Exact_RepMat's steps (:218-299, :433-444) and the
+    second-order test (:599-617) reaching that point from every start.  The CPU oracle reproduces it
+    to 1e-9 in log10 (tests/golden/si_1_pins).  Bar: every start's minimum within 1e-6 of -8.787497
+    (the published value's last digit), attained in outer iteration 25."""
+    pins = _pins()
+    opt = pins["protocol"]["exact"]
+    xs, ys = _starts(PTS)
+    res = _batch(data, len(PTS), cap=8192).solve(xs, ys, _gpu_opt(
+        TRS_solver="Exact_RepMat", second_order_stationarity=True, maxiter=opt["maxiter"],
+        inner_maxiter=opt["inner_maxiter"]))
+    got = _min_log_res(res, len(PTS))
+    for p, (g, it) in zip(PTS, got):
+        assert abs(g - pins["published"]["exact_every_start"]) <= 1e-6, (p, g, it)
+        assert it == 25, (p, it)
 
 
 def test_si_per_instance_data_stride(data):

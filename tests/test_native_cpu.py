@@ -207,3 +207,33 @@ def test_log_slot_assembly_keeps_head_and_latest():
                 h = cap // 2
                 want = list(range(h)) + list(range(k - (cap - h), k))
                 assert dropped == k - cap and list(rows[:, 0]) == want, (cap, k)
+
+
+@pytest.mark.parametrize("problem", ["NonnegPCA", "StableIdentification"])
+def test_dropin_coordinator_module_resolves_by_name(problem, tmp_path):
+    """base_simulator.py:44-49: importlib.import_module(cfg.problem_coordinator_name).Coordinator(cfg)
+    with 'coordinator' resolved through sys.path alone yields the structured problem (subprocess,
+    so the module name 'coordinator' does not leak into this session)."""
+    import shutil
+    import subprocess
+    import textwrap
+    from conftest import GOLDEN
+    ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    src = os.path.join(GOLDEN, "nonnegpca_1" if problem == "NonnegPCA" else "si_1")
+    shutil.copytree(src, tmp_path / "dataset" / problem / "1")
+    dropin = os.path.join(ROOT, "riemannian-interior-point-trust-region-method_amd", "dropin", problem)
+    code = textwrap.dedent(f"""
+        import importlib, sys, types
+        sys.path.insert(0, {dropin!r})
+        cfg = types.SimpleNamespace(problem_name={problem!r}, problem_instance=1, problem_initialpoint='a',
+                                    problem_coordinator_name='coordinator', is_X_noisy=True,
+                                    Xset=[1, 2, 3, 4, 5], h=0.02)
+        mod = importlib.import_module(cfg.problem_coordinator_name)
+        prob = mod.Coordinator(cfg).run()
+        print(type(prob).__name__, mod.__file__)
+    """)
+    out = subprocess.run([sys.executable, "-c", code], cwd=tmp_path, capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stderr
+    name, path = out.stdout.split()
+    assert name == ("NonnegPCAProblem" if problem == "NonnegPCA" else "SIProblem")
+    assert path.startswith(dropin)

@@ -150,3 +150,26 @@ def test_host_si_helpers(tmp_path):
     assert np.array_equal(prob.point_array(), x0) and np.array_equal(prob.initialineqLagmult, y0)
     with pytest.raises(RuntimeError):
         si.SIBatch(5, 95, 16, 2)   # no GPU here: no CPU fallback
+
+
+def test_oracle_exact_pinned_to_published_plateau():
+    """The oracle's RIPTRM (exact) on fixture start a stalls in outer iteration 25 at the reference's
+    published min log10 KKT residual -8.787497 (src/StableIdentification/analyzer.ipynb box-plot
+    cell; every start).  Also the committed pins (tests/golden/si_1_pins) match the published
+    numbers: the tCG quartiles within 0.05, the exact plateau to 1e-6."""
+    import json
+    from conftest import GOLDEN
+    with open(os.path.join(GOLDEN, "si_1_pins", "oracle_minres.json")) as f:
+        pins = json.load(f)
+    pub = pins["published"]
+    assert all(abs(a - p) <= 0.05 for a, p in zip(pins["tcg_quartiles"], pub["tcg_quartiles"]))
+    for p, (v, it) in pins["exact"].items():
+        assert abs(v - pub["exact_every_start"]) <= 1e-6 and it == 25, (p, v, it)
+    ds = os.path.join(GOLDEN, "si_1")
+    data = SI.SIData.load(ds)
+    x0, y0 = SI.load_start(ds, "a")
+    opt = dict(pins["protocol"]["exact"], manviofun=SI.si_manvio)
+    ref = SI.solve(data, x0, y0, opt)
+    r = np.array(ref.log["residual"], float)
+    assert abs(np.log10(r.min()) - pub["exact_every_start"]) <= 1e-6
+    assert ref.log["iteration"][int(r.argmin())] == 25
