@@ -79,7 +79,7 @@ struct Layout {
   // persistent mode (k_persist): the replicas' private state (vectors, scalars, stats, requests)
   // for batch x (reps - 1) replicas, the second parity of the partial grid, and the sync block
   // (per-instance arrival counters + published clocks + the timeout flag; zeroed before every launch)
-  int64_t off_rvec, off_rstate, off_rstats, off_rreq, off_pbuf2, off_sync, sync_bytes;
+  int64_t off_rvec, off_rstate, off_rstats, off_rreq, off_pbuf2, off_sync, sync_bytes, off_tgrid, tgrid_bytes;
   int64_t total;
 };
 
@@ -172,6 +172,10 @@ inline Layout make_layout(int32_t n, int32_t batch, int32_t cap, int32_t layout)
   L.off_sync = o;
   L.sync_bytes = L.reps > 0 ? round_up((int64_t)batch * 4, 16) + (int64_t)2 * batch * 8 + 16 : 0;
   o += L.sync_bytes;                                                     o = round_up(o, 256);
+  // the tagged grid of lean tCG passes right after the sync block (one memset zeroes both)
+  L.off_tgrid = o;
+  L.tgrid_bytes = L.reps > 0 ? (int64_t)2 * batch * nt_of(n) * nt_of(n) * TS * 16 : 0;
+  o += L.tgrid_bytes;                                                    o = round_up(o, 256);
   L.total = o;
   return L;
 }

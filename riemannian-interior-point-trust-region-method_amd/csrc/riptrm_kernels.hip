@@ -78,11 +78,14 @@ __device__ __forceinline__ void bred(Red& R, double (&v)[K], const int (&op)[K])
     for (int k = 0; k < K; ++k) b[w * RED_MAX + k] = v[k];
   }
   __syncthreads();
+  static_assert(ST_WAVES == 8, "bred: pairwise tree over 8 wave partials");
 #pragma unroll
-  for (int k = 0; k < K; ++k) {
-    double s = b[k];
-    for (int i = 1; i < ST_WAVES; ++i) s = comb(op[k], s, b[i * RED_MAX + k]);
-    v[k] = s;
+  for (int k = 0; k < K; ++k) {   // fixed pairwise tree: 3 dependent combines instead of 7
+    const double s01 = comb(op[k], b[k], b[RED_MAX + k]);
+    const double s23 = comb(op[k], b[2 * RED_MAX + k], b[3 * RED_MAX + k]);
+    const double s45 = comb(op[k], b[4 * RED_MAX + k], b[5 * RED_MAX + k]);
+    const double s67 = comb(op[k], b[6 * RED_MAX + k], b[7 * RED_MAX + k]);
+    v[k] = comb(op[k], comb(op[k], s01, s23), comb(op[k], s45, s67));
   }
   R.parity ^= 1;
 }
@@ -874,39 +877,54 @@ struct TcgScalars {
 };
 constexpr int TCG_CONTINUE = -1;
 
-template <int K, class Hooks>
-__device__ __forceinline__ int tcg_math(TcgScalars& t, const riptrm_options& opt, int n, Red& R, double (&u)[K],
-                                        double (&d)[K], const double (&x)[K], const double (&y)[K],
-                                        const double (&c)[K], double (&e)[K], double (&he)[K], double (&rv)[K],
-                                        Hooks& h) {
+// The part of the barrier-Hessian action that does not need u = S delta: xv = <x, delta>,
+// q = y (delta - x xv) / x and xq = <x, q> (the lean path computes it while the S-pass's partial
+// sums are in flight).  Each reduction is its own slot of the same tree as before, so the values
+// are those of the fused form.
+template <int K>
+struct HwPre {
+  double xv, xq;
+  double q[K];
+};
+template <int K>
+__device__ __forceinline__ void tcg_math_pre(HwPre<K>& p, int n, Red& R, const double (&d)[K], const double (&x)[K],
+                                             const double (&y)[K]) {
   const int tid = threadIdx.x;
-  // hw_apply(U, D, U)
-  double r1[2] = {0.0, 0.0};
+  double r1[1] = {0.0};
 #pragma unroll
-  for (int k = 0; k < K; ++k) {
-    r1[0] += x[k] * u[k];
-    r1[1] += x[k] * d[k];
-  }
-  bsum<2>(R, r1);
-  h.stamp(0);
-  const double xu = r1[0], xv = r1[1];
+  for (int k = 0; k < K; ++k) r1[0] += x[k] * d[k];
+  bsum<1>(R, r1);
+  p.xv = r1[0];
   double r2[1] = {0.0};
 #pragma unroll
   for (int k = 0; k < K; ++k) {
     const bool ok = tid + k * ST_THREADS < n;
-    const double q = ok ? (y[k] * (d[k] - x[k] * xv)) / x[k] : 0.0;
-    r2[0] += ok ? x[k] * q : 0.0;
+    p.q[k] = ok ? (y[k] * (d[k] - x[k] * p.xv)) / x[k] : 0.0;
+    r2[0] += ok ? x[k] * p.q[k] : 0.0;
   }
   bsum<1>(R, r2);
+  p.xq = r2[0];
+}
+
+template <int K, class Hooks>
+__device__ __forceinline__ int tcg_math(TcgScalars& t, const riptrm_options& opt, int n, Red& R, double (&u)[K],
+                                        double (&d)[K], const double (&x)[K], const double (&y)[K],
+                                        const double (&c)[K], double (&e)[K], double (&he)[K], double (&rv)[K],
+                                        Hooks& h, const HwPre<K>& pre) {
+  // hw_apply(U, D, U): xu = <x, S delta>; the u-free part came in `pre`
+  double r1[1] = {0.0};
+#pragma unroll
+  for (int k = 0; k < K; ++k) r1[0] += x[k] * u[k];
+  bsum<1>(R, r1);
+  h.stamp(0);
   h.stamp(1);
-  const double xq = r2[0];
+  const double xu = r1[0];
+  const double xq = pre.xq;
   const double coef = t.coef;
 #pragma unroll
-  for (int k = 0; k < K; ++k) {   // q recomputed, as hw_apply does
-    const bool ok = tid + k * ST_THREADS < n;
-    const double q = ok ? (y[k] * (d[k] - x[k] * xv)) / x[k] : 0.0;
+  for (int k = 0; k < K; ++k) {
     const double hf = -u[k] + xu * x[k];
-    u[k] = (hf + coef * d[k]) + (q - xq * x[k]);
+    u[k] = (hf + coef * d[k]) + (pre.q[k] - xq * x[k]);
   }
   h.late_ceh();
   double d1[1] = {0.0};
@@ -1659,7 +1677,9 @@ struct MachineT {
                         // request must not be mistaken for this run's next pass
     TcgScalars t = tcg_scalars();
     TcgHooks<K, MEM> h{*this, v};
-    const int stop = tcg_math<K>(t, P.opt, n, R, u, v.d, v.x, v.y, v.c, v.e, v.he, v.rv, h);
+    HwPre<K> pre;
+    tcg_math_pre<K>(pre, n, R, v.d, v.x, v.y);
+    const int stop = tcg_math<K>(t, P.opt, n, R, u, v.d, v.x, v.y, v.c, v.e, v.he, v.rv, h, pre);
     tcg_scalars_back(t);
     if (stop != TCG_CONTINUE) {
       if constexpr (!MEM) tcg_fast_flush(v);
@@ -2137,19 +2157,44 @@ struct PersistSync {
   double* clk;          // [2][batch] clock published by replica 0 at each barrier (parity)
   unsigned int* flag;   // [0]: some barrier wait timed out
   double* pbuf2;        // the partial grid's second parity
+  double* tgrid;        // the tagged grid of lean passes (zeroed before every launch)
+  int tgrid_bytes;
   unsigned long long* trace;   // diagnostics (riptrm_persist_trace): per step of workgroups 0 and
   int trace_cap;               // reps - 1, the device clock at the step's start / tile pass done /
                                // barrier passed / state step done; nullptr = off
 };
 constexpr unsigned long long PERSIST_TIMEOUT_TICKS = 200000000ull;   // 2 s of the 100 MHz clock
 
+// ---- tagged partial sums (lean tCG passes of k_persist) ---------------------------------------
+// A lean pass exchanges its partial sums as 16-byte granules {value, tag} written by ONE 16-B
+// write-through store each: the data are their own flag, so the pass needs neither an arrival
+// counter nor a separate gather round trip (every consumer polls exactly the granules it sums).
+// tag = (pass << 32) | (lo ^ hi ^ pass * 0x9E3779B9): the pass index (unique within a launch; the
+// grid is zeroed before every launch) and a check of the value bits, so a granule read half old /
+// half new is never accepted.  The grid alternates between two parities by pass, as the plain one.
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ unsigned tag_check(unsigned lo, unsigned hi, unsigned pass) {
+  return lo ^ hi ^ (pass * 0x9E3779B9u);
+}
+struct TagOut {
+  __amdgpu_buffer_rsrc_t rsrc;   // the tagged grid (both parities)
+  int base;                      // granule index of this pass's parity and instance, rhs 0
+  unsigned pass;                 // tag of this pass (>= 1)
+};
+__device__ __forceinline__ void st_tag(const TagOut& to, int g, double v) {
+  const unsigned lo = (unsigned)__double2loint(v), hi = (unsigned)__double2hiint(v);
+  const u32x4 q = {lo, hi, tag_check(lo, hi, to.pass), to.pass};
+  __builtin_amdgcn_raw_buffer_store_b128(q, to.rsrc, (to.base + g) * 16, 0, 16);   // aux 16 = sc1
+}
+
 // spass_tile with the tile in LDS (row stride colsT) and the input vectors' two blocks it needs
 // staged in LDS (vl[rhs][0] = block I, vl[rhs][1] = block J); the partial sums go to the
 // instance's slot bp of the grid pbase with sc1 stores
+// (to != nullptr: tagged granules instead, one right-hand side)
 template <int NR>
 __device__ __forceinline__ void spass_tile_lds(const DevParams& P, const double* Tl, const double (*vl)[2][TS],
                                                double* pbase, int bp, int t, double (*csl)[SP_WAVES][TS],
-                                               unsigned long long* tr = nullptr) {
+                                               unsigned long long* tr = nullptr, const TagOut* to = nullptr) {
   int I, J;
   tile_ij(t, P.nt, I, J);
   const int lane = (int)__lane_id();
@@ -2205,7 +2250,8 @@ __device__ __forceinline__ void spass_tile_lds(const DevParams& P, const double*
     for (int rb = 0; rb < ROWS / 8; ++rb) {
       if (!rv[rb]) continue;
       const int r0 = w * ROWS + rb * 8;
-      st_sc1(pb0 + ((int64_t)I * P.nt + J) * TS + r0 + rrow, rs[rb][0]);
+      if (to) st_tag(*to, (I * P.nt + J) * TS + r0 + rrow, rs[rb][0]);
+      else st_sc1(pb0 + ((int64_t)I * P.nt + J) * TS + r0 + rrow, rs[rb][0]);
       if (NR == 2) st_sc1(pb1 + ((int64_t)I * P.nt + J) * TS + r0 + rrow, rs[rb][1]);
     }
   }
@@ -2224,7 +2270,8 @@ __device__ __forceinline__ void spass_tile_lds(const DevParams& P, const double*
       double s0 = csl[0][0][c];
 #pragma unroll
       for (int q = 1; q < SP_WAVES; ++q) s0 += csl[0][q][c];
-      st_sc1(pb0 + ((int64_t)J * P.nt + I) * TS + c, s0);
+      if (to) st_tag(*to, (J * P.nt + I) * TS + c, s0);
+      else st_sc1(pb0 + ((int64_t)J * P.nt + I) * TS + c, s0);
       if (NR == 2) {
         double s1 = csl[1][0][c];
 #pragma unroll
@@ -2279,6 +2326,8 @@ struct LeanArgs {
   int64_t vks;
   double* gcold;       // the replica's scalar slots (ST_PASSES)
   double* pb[2];       // the instance's partial grid, both parities
+  double* tg;          // the tagged grid [2 parities][batch][nt][nt][TS] of 16-B granules
+  int tg_bytes;
   PersistSync sy;
   int n, b, t, R, I, J, steps, batch;
   int rep0, tsel;
@@ -2315,6 +2364,7 @@ __device__ __noinline__ void lean_tcg_run(LeanArgs a, LeanIO* io, const lds_f64*
   Pt.smode = 0;
   Pt.layout = RIPTRM_LAYOUT_SYMTILE;
   Pt.nst = 0;
+  const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(a.tg, 0, a.tg_bytes, 0x00020000);
   typename MachineT<false, true>::template TcgVecs<K> tv;
   rl_load<K>(a.vk + V_IN0 * a.vks, n, tv.d);
   rl_load<K>(a.vk + V_X * a.vks, n, tv.x);
@@ -2355,21 +2405,79 @@ __device__ __noinline__ void lean_tcg_run(LeanArgs a, LeanIO* io, const lds_f64*
     unsigned long long* tr = (a.sy.trace && a.tsel >= 0 && k < a.sy.trace_cap && tid == 0)
                                  ? a.sy.trace + ((int64_t)a.tsel * a.sy.trace_cap + k) * 24 : nullptr;
     if (tr) tr[0] = wall_clock64();
-    spass_tile_lds<1>(Pt, (const double*)tile, vl, a.pb[k & 1], a.b, a.t, csl, tr);
+    const int nn = a.nt * a.nt * TS;
+    TagOut to;
+    to.rsrc = rsrc;
+    to.base = ((k & 1) * a.batch + a.b) * nn;
+    to.pass = (unsigned)k + 1u;
+    spass_tile_lds<1>(Pt, (const double*)tile, vl, nullptr, a.b, a.t, csl, tr, &to);
     if (tr) tr[1] = wall_clock64();
-    ok = persist_barrier(a.sy, a.batch, a.b, a.R, a.rep0 != 0, epoch++, clk, (double*)bclk, bfail);
-    if (!ok) break;
-    if (tr) tr[2] = wall_clock64();
-    double u[K];
-    rl_gather<K, true>(Pt, a.pb[k & 1], a.b, u);
-    if (tr) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      tr[4] = wall_clock64();
-    }
-    ++k;
     Red Rd;
     Rd.buf = (double*)red_;
     Rd.parity = 0;
+    HwPre<K> pre;   // while the granules travel
+    tcg_math_pre<K>(pre, n, Rd, tv.d, tv.x, tv.y);
+    // gather = poll: each thread's granules of its K elements (the same summation order as
+    // rl_gather), re-read until every tag says this pass; bounded
+    double u[K];
+    {
+      constexpr int NTS = K <= 2 ? 8 : 16;
+      double tv_[K][NTS];
+      int gi[K];
+#pragma unroll
+      for (int e = 0; e < K; ++e) {
+        int i = tid + e * ST_THREADS;
+        i = i < n ? i : n - 1;
+        const int Ib = i >> 7, c = i & (TS - 1);
+        gi[e] = to.base + Ib * a.nt * TS + c;
+      }
+      unsigned long long pend = 0;
+#pragma unroll
+      for (int e = 0; e < K; ++e)
+#pragma unroll
+        for (int J = 0; J < NTS; ++J)
+          if (J < a.nt) pend |= 1ull << (e * NTS + J);
+      const unsigned long long t0 = wall_clock64();
+      while (true) {
+        u32x4 q[K][NTS];
+#pragma unroll
+        for (int e = 0; e < K; ++e)
+#pragma unroll
+          for (int J = 0; J < NTS; ++J)
+            if (pend & (1ull << (e * NTS + J)))
+              q[e][J] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, (gi[e] + J * TS) * 16, 0, 16);
+#pragma unroll
+        for (int e = 0; e < K; ++e)
+#pragma unroll
+          for (int J = 0; J < NTS; ++J)
+            if (pend & (1ull << (e * NTS + J))) {
+              const u32x4 g = q[e][J];
+              if (g.w == to.pass && g.z == tag_check(g.x, g.y, to.pass)) {
+                tv_[e][J] = __hiloint2double((int)g.y, (int)g.x);
+                pend &= ~(1ull << (e * NTS + J));
+              }
+            }
+        if (!__any(pend != 0)) break;
+        if (wall_clock64() - t0 > PERSIST_TIMEOUT_TICKS) {
+          if (pend) __hip_atomic_store((gu32_t*)a.sy.flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          ok = 0;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      ok = __syncthreads_and(ok);
+      if (!ok) break;
+#pragma unroll
+      for (int e = 0; e < K; ++e) {
+        u[e] = tv_[e][0];
+#pragma unroll
+        for (int J = 1; J < NTS; ++J)
+          if (J < a.nt) u[e] += tv_[e][J];
+        if (tid + e * ST_THREADS >= n) u[e] = 0.0;
+      }
+    }
+    if (tr) tr[4] = tr[2] = wall_clock64();
+    ++k;
     struct NoHooks {   // nothing to load or store; optional trace stamps (diagnostics)
       unsigned long long* tr;
       __device__ __forceinline__ void late_ceh() {}
@@ -2381,7 +2489,7 @@ __device__ __noinline__ void lean_tcg_run(LeanArgs a, LeanIO* io, const lds_f64*
         if (tr) tr[8 + i] = wall_clock64();
       }
     } nohooks{tr};
-    stop = tcg_math<K>(ts, opt, n, Rd, u, tv.d, tv.x, tv.y, tv.c, tv.e, tv.he, tv.rv, nohooks);
+    stop = tcg_math<K>(ts, opt, n, Rd, u, tv.d, tv.x, tv.y, tv.c, tv.e, tv.he, tv.rv, nohooks, pre);
     if (tr) {
       tr[5] = wall_clock64();
       tr[3] = wall_clock64();
@@ -2475,6 +2583,8 @@ __global__ void __launch_bounds__(ST_THREADS) k_persist(DevParams P, RepBlock rq
       la.gcold = gst;
       la.pb[0] = pb0;
       la.pb[1] = pb1;
+      la.tg = sy.tgrid;
+      la.tg_bytes = sy.tgrid_bytes;
       la.sy = sy;
       la.n = P.n;
       la.b = b;
@@ -2869,6 +2979,8 @@ static PersistSync persist_sync(const riptrm_ctx* c) {
   sy.clk = (double*)(base + round_up((int64_t)c->P.batch * 4, 16));
   sy.flag = (unsigned int*)(base + round_up((int64_t)c->P.batch * 4, 16) + (int64_t)2 * c->P.batch * 8);
   sy.pbuf2 = (double*)(c->ws + L.off_pbuf2);
+  sy.tgrid = (double*)(c->ws + L.off_tgrid);
+  sy.tgrid_bytes = (int)L.tgrid_bytes;
   sy.trace = c->persist_trace;
   sy.trace_cap = c->persist_trace_cap;
   return sy;
@@ -2889,7 +3001,9 @@ static int persist_init(riptrm_ctx* c, const double* x, const double* y, int64_t
 // `steps` lock-step iterations of the whole batch in one k_persist launch
 static int persist_run(riptrm_ctx* c, int steps, int* n_active) {
   const PersistSync sy = persist_sync(c);
-  HIPCHK(c, hipMemsetAsync(c->ws + c->L.off_sync, 0, (size_t)c->L.sync_bytes, c->stream));
+  // the sync block and the tagged grid (adjacent): counters, clocks and tags start at zero
+  HIPCHK(c, hipMemsetAsync(c->ws + c->L.off_sync, 0, (size_t)(c->L.off_tgrid - c->L.off_sync + c->L.tgrid_bytes),
+                           c->stream));
   if (steps > 0) {
     int i0 = -1, i1 = -1;
     hipEvent_t e0 = nullptr, e1 = nullptr;

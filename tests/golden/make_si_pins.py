@@ -7,7 +7,7 @@ min over the log of the 240 s run, log10; printed rows and quartiles).
   RIPTRM (tCG):   maxiter 35, inner_maxiter 300 (the outer loop stalls at mu ~ 3e-14 once the
                   inner tolerance max(mu, 1e-14) is out of reach; the reference ran into its
                   240 s limit there instead)
-  RIPTRM (exact): Exact_RepMat + second-order test, maxiter 25, inner_maxiter 20 (the reference's
+  RIPTRM (exact): Exact_RepMat + second-order test, maxiter 25, inner_maxiter 300 (the reference's
                   exact runs stall inside outer iteration 25, mu_25 = 4.08e-10, at residual
                   4 mu_25 for every start)
 
@@ -31,7 +31,7 @@ PUBLISHED = {
     "exact_every_start": -8.787497,
 }
 TCG = dict(tolresid=0.0, maxtime=1e9, maxiter=35, inner_maxiter=300)
-EXACT = dict(tolresid=0.0, maxtime=1e9, maxiter=25, inner_maxiter=20, TRS_solver="Exact_RepMat",
+EXACT = dict(tolresid=0.0, maxtime=1e9, maxiter=25, inner_maxiter=300, TRS_solver="Exact_RepMat",
              second_order_stationarity=True)
 
 
