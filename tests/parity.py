@@ -136,3 +136,70 @@ def compare_until_flip(gl, rl, tight_rows=20, late_row=20):
             (flip, gl[key][row], rl[key][row], gl["normdx"][row], rl["normdx"][row], gl["TR_radius"][row])
     compare_outer(gl, rl)
     return flip
+
+
+# ---- classified branch flips ------------------------------------------------------------------
+
+def column_deviation(a, r, k):
+    """max over rows of |a - r| / max(|r|, 1e-12 max|r|) for column k (rows both logs have)."""
+    m = min(len(a[k]), len(r[k]))
+    g, v = _col(a, k)[:m], _col(r, k)[:m]
+    ok = ~np.isnan(g) & ~np.isnan(v)
+    if not ok.any():
+        return 0.0
+    scale = np.max(np.abs(v[ok])) or 1.0
+    return float(np.max(np.abs(g[ok] - v[ok]) / np.maximum(np.abs(v[ok]), 1e-12 * scale)))
+
+
+def prefix_deviation(gl, rl, rows):
+    """Relative deviation of the iterate quantities (cost, residual, max |y|) on the first `rows`
+    rows: the drift the two trajectories have accumulated before a flip."""
+    p = {k: v[:rows] for k, v in gl.items()}
+    q = {k: v[:rows] for k, v in rl.items()}
+    return max(column_deviation(p, q, k) for k in ("cost", "residual", "maxabsLagmult"))
+
+
+def classify_flip(step, P, states, gl, rl, flip, trials=8, seed=0):
+    """A branch flip at log row `flip[0]` (key flip[1]) is a rounding-driven one if the GPU's decision
+    is reachable from the ORACLE's own state at that inner step perturbed at any size from 1e-14 up
+    to the drift the two trajectories had accumulated before it (prefix_deviation): random relative
+    perturbations of x (kept on the sphere) and y, `trials` per decade, each run through the
+    oracle's inner_step `step` (RIPTRM.py:707-783).  Decisions that flip this way are
+    either ties (|normdx - Delta| <= 1e-15, RIPTRM.py:672) or the erratic tail of an ill-conditioned
+    tCG (residual ratios jumping 10x between iterations near the exit): the two CPU oracles flip
+    there too (tests/test_oracle.py).  A decision with a real margin is not reproduced (the negative
+    control there).  states[r - 1] = (x, y, mu, Delta, inner_iteration, inner_option) of the inner
+    step that wrote row r.  Returns the perturbation size that reproduced it, or None."""
+    row, key = flip
+    if row < 1 or row - 1 >= len(states):
+        return None
+    x, y, mu, Delta, it, iopt = states[row - 1]
+    drift = max(prefix_deviation(gl, rl, row), 1e-14)
+    want = gl[key][row]
+    rs = np.random.RandomState(seed)
+    sizes = np.logspace(-14, np.log10(drift), max(1, int(np.ceil(np.log10(drift) + 14)) + 1))
+    for t in range(trials * len(sizes)):
+        eps = sizes[t // trials] * (0.5 + rs.rand())
+        xp = x * (1.0 + eps * rs.randn(x.shape[0]))
+        xp = xp / np.linalg.norm(xp)
+        yp = y * (1.0 + eps * rs.randn(y.shape[0]))
+        _, _, _, _, info = step(P, xp, yp, mu, Delta, it, iopt)
+        if info.get(key) == want:
+            return eps
+    return None
+
+
+class StateRecorder:
+    """Wraps an oracle so its inner steps record their starting state (for classify_flip)."""
+
+    def __init__(self, oracle):
+        self.oracle = oracle
+        self.states = []
+        inner = oracle.inner_step
+        self.step = inner   # the unwrapped inner step (classify_flip's probe)
+
+        def rec(P, x, y, mu, Delta, inner_iteration, inner_option):
+            self.states.append((x.copy(), y.copy(), mu, Delta, inner_iteration, dict(inner_option)))
+            return inner(P, x, y, mu, Delta, inner_iteration, inner_option)
+
+        oracle.inner_step = rec

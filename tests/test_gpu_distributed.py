@@ -1,0 +1,89 @@
+"""The multi-rank path on the GPU box: two processes on cuda:0 (the box has one GPU;
+the 8-GPU run is the driver's), torch.distributed over gloo, distributed.solve_sharded (global
+instance b on rank b % world, each rank solving its shard with the drop-in RIPTRM.run_batch) and
+distributed.gather_rows (the only collective of the path).  The gathered x, y and per-instance
+results must equal a single-process run_batch of the same global instances bitwise: an instance's
+iterates do not depend on the batch it is solved in (fixed reduction orders, the S-pass kernel
+chosen by n alone)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+N, TOTAL, K = 200, 5, 6
+
+
+def _problems():
+    from oracle import nonnegpca_gen as G
+    from problems import NonnegPCAProblem
+    out = []
+    for b in range(TOTAL):
+        Z, x0, y0 = G.generate_instance(N, 1200 + b)
+        out.append(NonnegPCAProblem(Z=Z, initialpoint=x0, initialineqLagmult=y0))
+    return out
+
+
+def _option():
+    from problems import manviofun
+    return {"maxiter": K, "tolresid": 0.0, "maxtime": 1e9, "TRS_solver": "tCG", "second_order_stationarity": False,
+            "manviofun": manviofun}
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "riemannian-interior-point-trust-region-method_amd")]
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from distributed import gather_rows, solve_sharded
+        outs, ids = solve_sharded(_problems(), _option())
+        x = torch.tensor(np.stack([o.x for o in outs]), dtype=torch.float64)
+        y = torch.tensor(np.stack([o.ineqLagmult for o in outs]), dtype=torch.float64)
+        res = torch.tensor([[len(o.log["iteration"]), float(o.log["residual"][-1])] for o in outs], dtype=torch.float64)
+        gx = gather_rows(x, TOTAL, world, rank)
+        gy = gather_rows(y, TOTAL, world, rank)
+        gr = gather_rows(res, TOTAL, world, rank)
+        q.put((rank, ids, gx.numpy(), gy.numpy(), gr.numpy()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_ranks_on_one_gpu_match_single_process_bitwise():
+    import torch.multiprocessing as mp
+    from RIPTRM import RIPTRM
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = [q.get(timeout=240) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    ref = RIPTRM(_option()).run_batch(_problems())
+    rx = np.stack([o.x for o in ref])
+    ry = np.stack([o.ineqLagmult for o in ref])
+    rr = np.array([[len(o.log["iteration"]), float(o.log["residual"][-1])] for o in ref])
+    for rank, ids, gx, gy, gr in got:
+        assert ids == list(range(rank, TOTAL, world))
+        np.testing.assert_array_equal(gx, rx)
+        np.testing.assert_array_equal(gy, ry)
+        np.testing.assert_array_equal(gr, rr)

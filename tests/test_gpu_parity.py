@@ -142,31 +142,49 @@ def test_fixture_reaches_published_residual_on_gpu(fixture_n50):
     assert res[conv][-1] < 2e-14
 
 
+def _check_instance(gl, Z, x0, y0, K, gpu_x=None, S=None):
+    """One instance's GPU trajectory against the oracle (dsymv) with tests/parity.py's bar
+    (compare_logs: identical branches, values within the bounds the two CPU oracles need).  A branch flip must be a classified rounding tie
+    (parity.classify_flip: the GPU's decision is reachable from the oracle's own state at that
+    step perturbed by the drift accumulated before it); the trajectories must then still agree at
+    the outer level (parity.compare_outer).  Returns the flip (row, key, eps) or None."""
+    from parity import BranchFlip, StateRecorder, classify_flip, compare_logs, compare_outer, first_branch_flip
+    Pa = O.NonnegPCAVectorized(Z, S=S)
+    oa = O.RIPTRMOracle(_oracle_opt(maxiter=K))
+    rec = StateRecorder(oa)
+    ra = oa.run(Pa, x0, y0)
+    try:
+        compare_logs(gl, ra.log)
+    except BranchFlip:
+        flip = first_branch_flip(gl, ra.log)
+        eps = classify_flip(rec.step, Pa, rec.states, gl, ra.log, flip)
+        assert eps is not None, ("branch flip not reachable within the accumulated drift", flip,
+                                 gl[flip[1]][flip[0]], ra.log[flip[1]][flip[0]])
+        compare_outer(gl, ra.log)
+        return flip + (eps,)
+    if gpu_x is not None:
+        np.testing.assert_allclose(gpu_x, ra.x, atol=1e-6)
+    return None
+
+
 @pytest.mark.parametrize("n,B,K,layout", [(37, 5, 10, "sym"), (200, 4, 12, "sym"), (1000, 2, 10, "sym"),
                                           (300, 3, 10, "sym2"), (1000, 2, 10, "sym2")])
 def test_batched_solve_matches_oracle(n, B, K, layout):
-    """Per instance: identical branches + tests/parity.py values; an instance whose inner
-    branches flip at a rounding tie (the CPU oracles show such flips against each other too)
-    must still agree at the outer level (parity.compare_outer)."""
-    from parity import BranchFlip, compare_outer
+    """Per instance (_check_instance): identical branches and values within tests/parity.py's bar; a
+    flip only where classify_flip shows it is rounding-driven.  (Replaces round 1's "at most B/2
+    instances may flip" allowance.)"""
     insts = [G.generate_instance(n, 100 + b) for b in range(B)]
     eng = _engine(np.stack([z for z, _, _ in insts]), layout=layout)
     res = eng.solve(np.stack([x for _, x, _ in insts]), np.stack([y for _, _, y in insts]), _gpu_opt(maxiter=K))
     xs = res.x.cpu().numpy()
-    flips = 0
+    flips = {}
     for b, (Z, x0, y0) in enumerate(insts):
-        ref = O.solve(Z, x0, y0, _oracle_opt(maxiter=K))
-        try:
-            _compare_logs(res.log(b), ref.log)
-        except BranchFlip:
-            flips += 1
-            compare_outer(res.log(b), ref.log)
-            continue
-        np.testing.assert_allclose(xs[b], ref.x, atol=1e-6)
-        # same branches; a REACHED_TARGET exit may move by an iteration or two (rounding)
-        assert abs(int(res.stat(b, "TCG_ITERS")) - ref.tcg_iterations) <= max(2, 0.03 * ref.tcg_iterations)
-        assert abs(int(res.stat(b, "PASSES")) - ref.passes) <= max(2, 0.03 * ref.passes)
-    assert flips <= B // 2, flips
+        f = _check_instance(res.log(b), Z, x0, y0, K, gpu_x=xs[b])
+        if f is not None:
+            flips[b] = f
+        else:
+            assert int(res.stat(b, "OUTER_ITERS")) == K
+    print("classified flips:", flips)
 
 
 def test_edge_options_match_oracle():
@@ -345,8 +363,7 @@ def test_shared_tcg_matches_oracle_teacher_forced(n, B):
 
 @pytest.mark.parametrize("n,B,K", [(60, 40, 10), (1000, 5, 8)])
 def test_shared_multistart_solve_matches_oracle(n, B, K):
-    """One Z, B feasible starts: every start's trajectory against the oracle's."""
-    from parity import BranchFlip, compare_outer
+    """One Z, B feasible starts: every start's trajectory against the oracle's (_check_instance)."""
     Z, _, y0 = G.generate_instance(n, 500)
     starts = []
     for b in range(B):
@@ -355,17 +372,12 @@ def test_shared_multistart_solve_matches_oracle(n, B, K):
     eng = _shared_engine(Z, B)
     res = eng.solve(np.stack(starts), np.stack([y0] * B), _gpu_opt(maxiter=K))
     xs = res.x.cpu().numpy()
-    flips = 0
+    flips = {}
     for b in range(B):
-        ref = O.solve(Z, starts[b], y0, _oracle_opt(maxiter=K))
-        try:
-            _compare_logs(res.log(b), ref.log)
-        except BranchFlip:
-            flips += 1
-            compare_outer(res.log(b), ref.log)
-            continue
-        np.testing.assert_allclose(xs[b], ref.x, atol=1e-6)
-    assert flips <= B // 2, flips
+        f = _check_instance(res.log(b), Z, starts[b], y0, K, gpu_x=xs[b])
+        if f is not None:
+            flips[b] = f
+    print("classified flips:", flips)
 
 
 def test_run_batch_detects_shared_Z(fixture_n50):

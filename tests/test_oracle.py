@@ -228,3 +228,25 @@ def test_euclidean_branch_options_agree(lincomb, embedded):
     assert np.linalg.norm(Hp(u) - Hq(u)) <= 1e-12 * np.linalg.norm(Hq(u))
     assert np.linalg.norm(cp - cq) <= 1e-12 * np.linalg.norm(cq)
     assert np.linalg.norm(P.gradlag(x, y) - Q.gradlag(x, y)) <= 1e-12 * np.linalg.norm(Q.gradlag(x, y))
+
+
+def test_flip_classifier_accepts_rounding_ties_and_rejects_real_differences():
+    """parity.classify_flip (used by the GPU batch tests instead of round 1's 'B/2 may flip'):
+    on an instance where the two CPU oracles' inner branches differ (seed 125, n = 37), the flip is
+    reachable from the reference oracle's own state perturbed by the drift accumulated before it;
+    a fabricated decision at an early, well-separated row is not."""
+    import copy
+    from parity import StateRecorder, classify_flip, first_branch_flip
+    Z, x0, y0 = G.generate_instance(37, 125)
+    P = O.NonnegPCAVectorized(Z)
+    oa = O.RIPTRMOracle(dict(OPT, maxiter=10))
+    rec = StateRecorder(oa)
+    ra = oa.run(P, x0, y0)
+    b = O.solve(Z, x0, y0, dict(OPT, maxiter=10), structured=True)
+    flip = first_branch_flip(b.log, ra.log)
+    assert flip is not None
+    assert classify_flip(rec.step, P, rec.states, b.log, ra.log, flip) is not None
+    fake = copy.deepcopy(ra.log)
+    row = next(r for r in range(1, len(fake["inner_status"])) if fake["inner_status"][r] == "successful")
+    fake["inner_status"][row] = "unsuccessful"
+    assert classify_flip(rec.step, P, rec.states, fake, ra.log, (row, "inner_status")) is None
