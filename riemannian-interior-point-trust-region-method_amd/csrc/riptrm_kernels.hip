@@ -565,119 +565,179 @@ __global__ void __launch_bounds__(SP_THREADS, 1) k_spass_sup(DevParams P, int li
 // SAME S, so one pass is the dense product Y^T = V^T S over the active right-hand sides
 // (column c = active slot for in0, bound + slot for in1 when the instance asked for two).
 // v_mfma_f64_16x16x4_f64: A = 16 right-hand sides x 4 k, B = 4 k x 16 rows of S (S is
-// symmetric, so row i of S is column i of S^T), D = 16 x 16 fp64 accumulators.  A wave holds
-// WM x WN such tiles and walks K in 32-wide chunks: lane l loads 8 consecutive k (64 B) of
-// right-hand side / S row (l & 15) at offset 8 (l >> 4) and MFMA m of the chunk consumes
-// element m — the same k permutation on both operands, so the sum is over every k exactly once.
-// KS waves of a workgroup take interleaved chunks of one K slice and are summed through LDS in
-// wave order; MM_KZ workgroup slices (grid.z) write partial slabs that the state kernel adds in
-// slice order (deterministic; tools/mfma_bench.hip: 8x2 tiles, 4 waves, 4 slices = 34 TFLOP/s
-// at n = 4000 and 128 right-hand sides, against a 70 TFLOP/s issue-rate probe).
+// symmetric, so row i of S is column i of S^T), D = 16 x 16 fp64 accumulators.
+//
+// A workgroup (8 waves, two per SIMD) owns CT = 16 WM right-hand sides x RT rows of S over one
+// of MM_KZ K slices.  Each 32-deep K step stages V[CT][32] and S[RT][32] into LDS with
+// global_load_lds_dwordx4 (256-B rows; 16-B chunk c of row r kept at chunk c ^ (r & 15), written
+// through the SOURCE address since the LDS side of the copy is lane-linear, so the fragment reads
+// below are bank-conflict free), double-buffered: step t+1's copy is in flight while the waves
+// run step t's MFMAs out of LDS, one barrier per step.  The waves form a rows x columns grid over
+// the tile (8 x 1 for 128-row tiles: 16 rows x all CT columns each) and read, for MFMA pair jj,
+// lane (r, q)'s 16 B at k = 8q + 2jj: MFMA m = 2 jj + {0,1} sums k in {m, 8+m, 16+m, 24+m} — the
+// same order for every kernel shape, so an instance's product does not depend on CT / RT or on
+// the other right-hand sides.  The next pair's fragments are read while the current pair's
+// MFMAs issue, and the SIMD's second wave covers one wave's LDS reads and barrier wait.  Partial
+// slabs of the MM_KZ slices are added in slice order by the state kernel (deterministic, no
+// atomics).  Linear block id -> slice = id % MM_KZ, so a slice (and the V columns it reads)
+// stays on one XCD.  tools/mfma_bench.hip at n = 4000, 128 right-hand sides: 72.5 us = 56.5
+// TFLOP/s (4 waves: 81.5 us; the register-fed tile this replaced: 115 us; issue-rate probe 70.8).
 // ------------------------------------------------------------------------------------------
 typedef double dbl4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) unsigned char lds_u8;
+constexpr int MM_WAVES = 8;  // tools/mfma_bench.hip: 8 waves (2 per SIMD) 72.5 us vs 4 waves 81.5 us at n = 4000
+typedef __attribute__((address_space(3))) dbl2 lds_dbl2;
 
-template <int WM, int WN, int KS>
-__global__ void __launch_bounds__(64 * KS) k_spass_mm(DevParams P, int list_in, int zero_cnt, int bound) {
-  if (zero_cnt >= 0 && blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0 && threadIdx.x == 0) P.cnt[zero_cnt] = 0;
-  const int nact = P.cnt[list_in];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+template <int WM, int RT>
+struct MmShape {
+  static constexpr int NW = MM_WAVES;                  // waves per workgroup (two per SIMD)
+  static constexpr int CT = 16 * WM;                   // right-hand sides per workgroup
+  static constexpr int NWR = NW < RT / 16 ? NW : RT / 16, NWC = NW / NWR;  // wave grid: rows x columns
+  static constexpr int WMW = WM / NWC;                 // 16-column accumulator rows per wave
+  static constexpr int RW = RT / NWR, WN = RW / 16;    // rows per wave, 16-row accumulator columns
+  static constexpr int VT = CT * 256;                  // V tile bytes per stage
+  static constexpr int STAGE = VT + RT * 256;          // + S tile
+  static constexpr int VP = CT / 4 / NW, SP = RT / 4 / NW;  // glds wave-instructions per wave per stage
+  static_assert(WMW >= 1 && WN >= 1 && VP >= 1 && SP >= 1 && NWR * NWC == NW, "tile shape");
+};
+
+// One tile: right-hand-side columns v = 0..CT-1 of the tile are instance slots slot_of(v) (valid
+// while v < nv), reading V kind vk and writing slab (z, which).  slot_of(v) = s0 + v for in0
+// tiles, the v-th entry of an LDS map for compacted in1 tiles.
+template <int WM, int RT, typename SlotOf>
+__device__ __forceinline__ void mm_tile(const DevParams& P, lds_u8* smem, const int32_t* lst, int vk, int which, int nv,
+                                        SlotOf slot_of, int z, int i0, int rows) {
+  using Sh = MmShape<WM, RT>;
+  constexpr int CT = Sh::CT, WN = Sh::WN, WMW = Sh::WMW, RW = Sh::RW, NWR = Sh::NWR;
+  constexpr int VT = Sh::VT, STAGE = Sh::STAGE, VP = Sh::VP, SP = Sh::SP;
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+  const int wr = w % NWR, wc = w / NWR;  // this wave's rows RW wr .. and columns 16 WMW wc ..
   const int r = lane & 15, q = lane >> 4;
-  constexpr int CT = 16 * WM;                     // right-hand sides per workgroup
-  const int t0 = (bound + CT - 1) / CT;           // column tiles of in0
-  const int which = (int)blockIdx.y >= t0 ? 1 : 0;
-  const int s0 = ((int)blockIdx.y - which * t0) * CT;
-  if (s0 >= nact) return;
-  if (which) {  // in1 tiles: skip unless some instance of the tile asked for two right-hand sides
-    __shared__ int any2;
-    if (threadIdx.x == 0) any2 = 0;
-    __syncthreads();
-    if (threadIdx.x < CT) {
-      const int sl = s0 + threadIdx.x;
-      if (sl < nact && le_nrhs(P.lists[list_in * P.batch + sl]) == 2) any2 = 1;
-    }
-    __syncthreads();
-    if (!any2) return;
-  }
   const int64_t ld = P.ld;
-  const int rows = (P.n + 31) / 32 * 32;  // rows_of(n)
-  const int i0 = blockIdx.x * 16 * WN;
-  const int vk = which ? V_IN1 : V_IN0;
-  const double* ap[WM];
-  const double* bp[WN];
+  const double* vsrc[VP];
+  const double* ssrc[SP];
 #pragma unroll
-  for (int a = 0; a < WM; ++a) {
-    int sl = s0 + 16 * a + r;
-    sl = sl < nact ? sl : nact - 1;
-    ap[a] = vp(P, vk, le_b(P.lists[list_in * P.batch + sl])) + 8 * q;
+  for (int p = 0; p < VP; ++p) {
+    const int row = 4 * (VP * w + p) + q;
+    vsrc[p] = vp(P, vk, le_b(lst[slot_of(min(row, nv - 1))])) + 2 * (r ^ (row & 15));
   }
 #pragma unroll
-  for (int c = 0; c < WN; ++c) {
-    int i = i0 + 16 * c + r;
-    i = i < rows ? i : rows - 1;
-    bp[c] = P.S + (int64_t)i * ld + 8 * q;
+  for (int p = 0; p < SP; ++p) {
+    const int row = 4 * (SP * w + p) + q;
+    const int i = min(i0 + row, rows - 1);
+    ssrc[p] = P.S + (int64_t)i * ld + 2 * (r ^ (row & 15));
   }
-  dbl4 acc[WM][WN];
+  const int nch = (int)(ld / 32), per = (nch + MM_KZ - 1) / MM_KZ;
+  const int lo = z * per, hi = min(nch, lo + per);
+  auto issue = [&](int ch, int buf) {
+    const int64_t k0 = (int64_t)ch * 32;
+    lds_u8* vb = smem + buf * STAGE;
 #pragma unroll
-  for (int a = 0; a < WM; ++a)
+    for (int p = 0; p < VP; ++p)
+      __builtin_amdgcn_global_load_lds((const void*)(vsrc[p] + k0), vb + 4 * (VP * w + p) * 256, 16, 0, 0);
+#pragma unroll
+    for (int p = 0; p < SP; ++p)
+      __builtin_amdgcn_global_load_lds((const void*)(ssrc[p] + k0), vb + VT + 4 * (SP * w + p) * 256, 16, 0, 0);
+  };
+  dbl4 acc[WMW][WN];
+#pragma unroll
+  for (int a = 0; a < WMW; ++a)
 #pragma unroll
     for (int c = 0; c < WN; ++c) acc[a][c] = dbl4{0.0, 0.0, 0.0, 0.0};
-  const int nch_all = (int)(ld / 32), per = (nch_all + MM_KZ - 1) / MM_KZ;
-  const int ch_lo = blockIdx.z * per, ch_hi = min(nch_all, ch_lo + per);
-  for (int ch = ch_lo + w; ch < ch_hi; ch += KS) {
-    const int64_t k0 = (int64_t)ch * 32;
-    dbl2 fa[WM][4], fb[WN][4];
+  // wave-uniform: rows of the tile past n, and column groups past the tile's last column, idle
+  const bool live = i0 + RW * wr < P.n && 16 * WMW * wc < nv;
+  if (lo < hi) issue(lo, 0);
+  for (int ch = lo; ch < hi; ++ch) {
+    const int s = (ch - lo) & 1;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's copies of step ch landed
+    __syncthreads();                                    // everyone's landed; step ch-1's reads done
+    if (ch + 1 < hi) issue(ch + 1, s ^ 1);
+    if (!live) continue;
+    const lds_u8* vb = smem + s * STAGE + 16 * WMW * wc * 256;
+    const lds_u8* sb = smem + s * STAGE + VT + RW * wr * 256;
+    dbl2 fa[2][WMW], fb[2][WN];
+    auto frag = [&](int jj, int u) {
+      const int off = ((4 * q + jj) ^ r) * 16;
 #pragma unroll
-    for (int a = 0; a < WM; ++a)
+      for (int a = 0; a < WMW; ++a) fa[u][a] = *(const lds_dbl2*)(vb + (16 * a + r) * 256 + off);
 #pragma unroll
-      for (int h = 0; h < 4; ++h) fa[a][h] = *(const dbl2*)(ap[a] + k0 + 2 * h);
+      for (int c = 0; c < WN; ++c) fb[u][c] = *(const lds_dbl2*)(sb + (16 * c + r) * 256 + off);
+    };
+    frag(0, 0);
 #pragma unroll
-    for (int c = 0; c < WN; ++c)
+    for (int jj = 0; jj < 4; ++jj) {
+      const int u = jj & 1;
+      if (jj < 3) frag(jj + 1, u ^ 1);
 #pragma unroll
-      for (int h = 0; h < 4; ++h) fb[c][h] = __builtin_nontemporal_load((const dbl2*)(bp[c] + k0 + 2 * h));
+      for (int mm = 0; mm < 2; ++mm)
 #pragma unroll
-    for (int m = 0; m < 8; ++m)
+        for (int a = 0; a < WMW; ++a)
 #pragma unroll
-      for (int a = 0; a < WM; ++a)
-#pragma unroll
-        for (int c = 0; c < WN; ++c) {
-          const double av = (m & 1) ? fa[a][m >> 1].y : fa[a][m >> 1].x;
-          const double bv = (m & 1) ? fb[c][m >> 1].y : fb[c][m >> 1].x;
-          acc[a][c] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc[a][c], 0, 0, 0);
-        }
-  }
-  if (KS > 1) {  // waves 1..KS-1 accumulate in turn into one LDS slab, wave 0 adds it last
-    __shared__ dbl4 red[WM][WN][64];
-    for (int s = 1; s < KS; ++s) {
-      if (w == s)
-#pragma unroll
-        for (int a = 0; a < WM; ++a)
-#pragma unroll
-          for (int c = 0; c < WN; ++c) red[a][c][lane] = s == 1 ? acc[a][c] : red[a][c][lane] + acc[a][c];
-      __syncthreads();
+          for (int c = 0; c < WN; ++c)
+            acc[a][c] = __builtin_amdgcn_mfma_f64_16x16x4f64(mm ? fa[u][a].y : fa[u][a].x, mm ? fb[u][c].y : fb[u][c].x,
+                                                             acc[a][c], 0, 0, 0);
     }
-    if (w != 0) return;
-#pragma unroll
-    for (int a = 0; a < WM; ++a)
-#pragma unroll
-      for (int c = 0; c < WN; ++c) acc[a][c] += red[a][c][lane];
   }
+  (void)CT;
+  if (!live) return;
   // D (f64): column = lane & 15 -> row i of S, row = (lane >> 4) + 4 g -> right-hand side
-  double* slab = P.pbuf + ((int64_t)blockIdx.z * 2 + which) * P.batch * ld;
+  double* slab = P.pbuf + ((int64_t)z * 2 + which) * P.batch * ld;
 #pragma unroll
-  for (int a = 0; a < WM; ++a)
+  for (int a = 0; a < WMW; ++a)
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
-      const int sl = s0 + 16 * a + q + 4 * g;
-      if (sl >= nact) continue;
-      const int32_t eb = P.lists[list_in * P.batch + sl];
-      const int bb = le_b(eb);
-      if (which && le_nrhs(eb) != 2) continue;
+      const int v = 16 * (WMW * wc + a) + q + 4 * g;
+      if (v >= nv) continue;
+      double* o = slab + (int64_t)le_b(lst[slot_of(v)]) * ld;
 #pragma unroll
       for (int c = 0; c < WN; ++c) {
-        const int i = i0 + 16 * c + r;
-        if (i < P.n) slab[(int64_t)bb * ld + i] = acc[a][c][g];
+        const int i = i0 + RW * wr + 16 * c + r;
+        if (i < P.n) o[i] = acc[a][c][g];
       }
     }
+}
+
+// dynamic LDS: two stages of the in0 tile shape + the in1 column map
+template <int WM0, int RT>
+constexpr int mm_shm() { return 2 * MmShape<WM0, RT>::STAGE + 32 * 4; }
+
+// Grid (1-D): MM_KZ slices x row blocks x (t0 in0 tiles of 16 WM0 columns + t1 in1 tiles of 32).
+// The second right-hand side exists only for the instances that asked for two (le_nrhs): their
+// in1 columns are compacted in list order into 32-wide tiles, so a pass where a few instances
+// need two products costs a narrow tile, not a second full-width one.
+template <int WM0, int RT>
+__global__ void __launch_bounds__(64 * MM_WAVES) k_spass_mm(DevParams P, int list_in, int zero_cnt, int bound) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char mm_smem_raw[];
+  lds_u8* smem = (lds_u8*)mm_smem_raw;
+  if (zero_cnt >= 0 && blockIdx.x == 0 && threadIdx.x == 0) P.cnt[zero_cnt] = 0;
+  const int nact = P.cnt[list_in];
+  const int rows = (P.n + 31) / 32 * 32;  // rows_of(n)
+  const int nrb = (rows + RT - 1) / RT, t0 = (bound + 16 * WM0 - 1) / (16 * WM0);
+  const int L = blockIdx.x, z = L % MM_KZ, rest = L / MM_KZ;
+  const int i0 = (rest % nrb) * RT, y = rest / nrb;
+  const int32_t* lst = P.lists + (int64_t)list_in * P.batch;
+  if (y < t0) {
+    const int s0 = y * 16 * WM0;
+    if (s0 >= nact) return;
+    mm_tile<WM0, RT>(P, smem, lst, V_IN0, 0, min(16 * WM0, nact - s0), [&](int v) { return s0 + v; }, z, i0, rows);
+    return;
+  }
+  // in1 tile: map its 32 columns to the instances asking for a second product, in list order
+  const int s0 = (y - t0) * 32;
+  int32_t* map = (int32_t*)(mm_smem_raw + 2 * MmShape<WM0, RT>::STAGE);
+  const int lane = threadIdx.x & 63;
+  int n2 = 0;
+  for (int c = 0; c < nact; c += 64) {
+    const int sl = c + lane;
+    const bool two = sl < nact && le_nrhs(lst[sl]) == 2;
+    const uint64_t m = __ballot(two);
+    const int k = n2 + __popcll(m & ((1ull << lane) - 1));
+    if (two && threadIdx.x < 64 && k >= s0 && k < s0 + 32) map[k - s0] = sl;
+    n2 += __popcll(m);
+  }
+  if (s0 >= n2) return;  // n2 is the same in every wave: the workgroup leaves together
+  __syncthreads();
+  mm_tile<2, RT>(P, smem, lst, V_IN1, 1, min(32, n2 - s0), [&](int v) { return (int)map[v]; }, z, i0, rows);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -3127,6 +3187,16 @@ int riptrm_nonnegpca_bind(riptrm_ctx* ctx, const double* S, int32_t n, int32_t b
     HIPCHK(ctx, hipFuncSetAttribute((const void*)k_persist<4>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                     (int)(TS * TS * sizeof(double))));
   }
+  if (layout == RIPTRM_LAYOUT_SHARED) {  // the MFMA S-pass stages two K steps of V and S tiles in LDS
+    HIPCHK(ctx, hipFuncSetAttribute((const void*)k_spass_mm<8, 128>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    mm_shm<8, 128>()));
+    HIPCHK(ctx, hipFuncSetAttribute((const void*)k_spass_mm<8, 64>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    mm_shm<8, 64>()));
+    HIPCHK(ctx, hipFuncSetAttribute((const void*)k_spass_mm<2, 128>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    mm_shm<2, 128>()));
+    HIPCHK(ctx, hipFuncSetAttribute((const void*)k_spass_mm<2, 64>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    mm_shm<2, 64>()));
+  }
   // two groups only when one group's S-pass is long enough (>= ~0.6 GB, ~100 us) to hide the
   // other group's state kernel; small batches are launch/latency bound and lose from the split
   ctx->ngroups = (layout != RIPTRM_LAYOUT_SHARED && batch >= 8 &&
@@ -3174,16 +3244,23 @@ static int launch_gemv(riptrm_ctx* c, hipStream_t st, int list_in, int zero_cnt,
   hipEvent_t e0 = nullptr, e1 = nullptr;
   if (c->prof && (e0 = prof_event(c, &i0)) && (e1 = prof_event(c, &i1))) HIPCHK(c, hipEventRecord(e0, st));
   if (c->P.layout == RIPTRM_LAYOUT_SHARED) {
-    // 8 x 2 tiles (128 right-hand sides x 32 rows) for wide batches, 2 x 1 for narrow ones
-    const unsigned rows = (unsigned)rows_of(c->P.n);
+    // 128 right-hand sides per workgroup for wide batches, 32 for narrow ones; 128-row tiles when
+    // they alone give every CU a workgroup, else 64 (the k order, hence every product, is the same)
+    const int rows = rows_of(c->P.n);
+    const bool rt128 = (int64_t)((rows + 127) / 128) * MM_KZ >= c->ncu;
+    const int nrb = rt128 ? (rows + 127) / 128 : (rows + 63) / 64;
+    const int t0 = bound > 32 ? (bound + 127) / 128 : (bound + 31) / 32, t1 = (bound + 31) / 32;
+    const dim3 grid((unsigned)(nrb * (t0 + t1) * MM_KZ));
     if (bound > 32) {
-      const unsigned ct = (unsigned)((bound + 127) / 128);
-      hipLaunchKernelGGL((k_spass_mm<8, 2, 4>), dim3(rows / 32, 2 * ct, MM_KZ), dim3(256), 0, st, c->P, list_in,
-                         zero_cnt, bound);
+      if (rt128)
+        hipLaunchKernelGGL((k_spass_mm<8, 128>), grid, dim3(64 * MM_WAVES), (mm_shm<8, 128>()), st, c->P, list_in, zero_cnt, bound);
+      else
+        hipLaunchKernelGGL((k_spass_mm<8, 64>), grid, dim3(64 * MM_WAVES), (mm_shm<8, 64>()), st, c->P, list_in, zero_cnt, bound);
     } else {
-      const unsigned ct = (unsigned)((bound + 31) / 32);
-      hipLaunchKernelGGL((k_spass_mm<2, 1, 4>), dim3(rows / 16, 2 * ct, MM_KZ), dim3(256), 0, st, c->P, list_in,
-                         zero_cnt, bound);
+      if (rt128)
+        hipLaunchKernelGGL((k_spass_mm<2, 128>), grid, dim3(64 * MM_WAVES), (mm_shm<2, 128>()), st, c->P, list_in, zero_cnt, bound);
+      else
+        hipLaunchKernelGGL((k_spass_mm<2, 64>), grid, dim3(64 * MM_WAVES), (mm_shm<2, 64>()), st, c->P, list_in, zero_cnt, bound);
     }
   } else if (sym && smode) {
     const int64_t units = (int64_t)bound * c->P.nsup;

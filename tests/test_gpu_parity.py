@@ -337,6 +337,48 @@ def test_shared_barrier_hessian_matches_oracle(n, B):
         assert err < 1e-12, (b, err)
 
 
+@pytest.mark.parametrize("n", [129, 1000, 4000])
+def test_shared_product_independent_of_batch_bitwise(n):
+    """k_spass_mm sums k in one order for every tile shape (128 or 32 right-hand sides per
+    workgroup, 128- or 64-row tiles) and the K slices in slice order: an instance's Hessian
+    action in a 40-wide batch equals, bit for bit, the same instance's in a 3-wide batch."""
+    Z, _, _ = G.generate_instance(n, 13)
+    B = 40
+    xs, ys, vs = [], [], []
+    for b in range(B):
+        x, y = _state(n, 700 + b)
+        xs.append(x); ys.append(y)
+        vs.append(np.random.RandomState(800 + b).randn(n))
+    xs, ys, vs = np.stack(xs), np.stack(ys), np.stack(vs)
+    wide = _shared_engine(Z, B).hvp(xs, ys, 0.0123, vs)
+    pick = [0, 17, 39]
+    narrow = _shared_engine(Z, 3).hvp(xs[pick], ys[pick], 0.0123, vs[pick])
+    assert torch.equal(wide[pick], narrow)
+
+
+@pytest.mark.parametrize("n,B,K", [(200, 40, 8), (1000, 70, 5)])
+def test_shared_solve_independent_of_batch_bitwise(n, B, K):
+    """Whole multi-start solves: the passes where some starts ask for a second product (their
+    in1 columns compacted into 32-wide tiles in list order) change no start's arithmetic, so
+    three starts of a wide batch follow the same trajectory bit for bit when solved alone."""
+    Z, _, y0 = G.generate_instance(n, 510)
+    starts = []
+    for b in range(B):
+        x0 = np.abs(np.random.RandomState(900 + b).rand(n))
+        starts.append(x0 / np.linalg.norm(x0))
+    starts = np.stack(starts)
+    ys = np.stack([y0] * B)
+    wide = _shared_engine(Z, B).solve(starts, ys, _gpu_opt(maxiter=K))
+    pick = [0, B // 2, B - 1]
+    alone = _shared_engine(Z, 3).solve(starts[pick], ys[pick], _gpu_opt(maxiter=K))
+    assert torch.equal(wide.x[pick], alone.x) and torch.equal(wide.y[pick], alone.y)
+    for j, b in enumerate(pick):
+        la, lb = wide.log(b), alone.log(j)
+        for key in la:
+            if key != "time":
+                assert la[key] == lb[key] or np.array_equal(np.array(la[key], float), np.array(lb[key], float)), (b, key)
+
+
 @pytest.mark.parametrize("n,B", [(200, 6), (1000, 36)])
 def test_shared_tcg_matches_oracle_teacher_forced(n, B):
     Z, _, _ = G.generate_instance(n, 41)

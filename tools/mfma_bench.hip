@@ -97,6 +97,222 @@ __global__ void __launch_bounds__(64 * KS) k_mm(const double* __restrict__ S, co
     }
 }
 
+// Software-pipelined variant: K chunks of 16 (lane l loads 4 consecutive k = 32 B of row l & 15
+// at offset 4 (l >> 4); MFMA m of the chunk consumes element m), the next chunk's operands
+// loaded into a second register set while the current one feeds the MFMAs (one wave per SIMD
+// cannot hide a load phase behind another wave).  Loop manually unrolled by two so the buffers
+// swap without register moves.
+template <int WM, int WN>
+struct MmFrag {
+  dbl2 a[WM][2], b[WN][2];
+};
+
+template <int WM, int WN>
+__device__ __forceinline__ void mm_load(MmFrag<WM, WN>& f, const double* const* ap, const double* const* bp, int64_t k0) {
+#pragma unroll
+  for (int a = 0; a < WM; ++a)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) f.a[a][h] = *(const dbl2*)(ap[a] + k0 + 2 * h);
+#pragma unroll
+  for (int b = 0; b < WN; ++b)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) f.b[b][h] = __builtin_nontemporal_load((const dbl2*)(bp[b] + k0 + 2 * h));
+}
+
+template <int WM, int WN>
+__device__ __forceinline__ void mm_fma(dbl4 (&acc)[WM][WN], const MmFrag<WM, WN>& f) {
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int a = 0; a < WM; ++a)
+#pragma unroll
+      for (int b = 0; b < WN; ++b) {
+        const double av = (m & 1) ? f.a[a][m >> 1].y : f.a[a][m >> 1].x;
+        const double bv = (m & 1) ? f.b[b][m >> 1].y : f.b[b][m >> 1].x;
+        acc[a][b] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc[a][b], 0, 0, 0);
+      }
+}
+
+template <int WM, int WN, int KS>
+__global__ void __launch_bounds__(64 * KS) k_mm2(const double* __restrict__ S, const double* __restrict__ V,
+                                                 double* __restrict__ Y, int n, int rows, int64_t ld, int C) {
+  Y += (int64_t)blockIdx.z * C * ld;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int i0 = blockIdx.x * 16 * WN, c0 = blockIdx.y * 16 * WM;
+  const int r = lane & 15, q = lane >> 4;
+  const double* ap[WM];
+  const double* bp[WN];
+#pragma unroll
+  for (int a = 0; a < WM; ++a) {
+    int c = c0 + 16 * a + r;
+    c = c < C ? c : C - 1;
+    ap[a] = V + (int64_t)c * ld + 4 * q;
+  }
+#pragma unroll
+  for (int b = 0; b < WN; ++b) {
+    int i = i0 + 16 * b + r;
+    i = i < rows ? i : rows - 1;
+    bp[b] = S + (int64_t)i * ld + 4 * q;
+  }
+  dbl4 acc[WM][WN];
+#pragma unroll
+  for (int a = 0; a < WM; ++a)
+#pragma unroll
+    for (int b = 0; b < WN; ++b) acc[a][b] = dbl4{0.0, 0.0, 0.0, 0.0};
+  const int nch_all = (int)(ld / 16), per = (nch_all + gridDim.z - 1) / gridDim.z;
+  const int ch_lo = blockIdx.z * per, ch_hi = min(nch_all, ch_lo + per);
+  int ch = ch_lo + w;
+  MmFrag<WM, WN> f0, f1;
+  if (ch < ch_hi) mm_load(f0, ap, bp, (int64_t)ch * 16);
+  while (ch < ch_hi) {
+    const int c1 = ch + KS;
+    if (c1 < ch_hi) mm_load(f1, ap, bp, (int64_t)c1 * 16);
+    mm_fma(acc, f0);
+    if (c1 >= ch_hi) break;
+    const int c2 = c1 + KS;
+    if (c2 < ch_hi) mm_load(f0, ap, bp, (int64_t)c2 * 16);
+    mm_fma(acc, f1);
+    ch = c2;
+  }
+  if (KS > 1) {
+    __shared__ dbl4 red[WM][WN][64];
+    for (int s = 1; s < KS; ++s) {
+      if (w == s)
+#pragma unroll
+        for (int a = 0; a < WM; ++a)
+#pragma unroll
+          for (int b = 0; b < WN; ++b) red[a][b][lane] = s == 1 ? acc[a][b] : red[a][b][lane] + acc[a][b];
+      __syncthreads();
+    }
+    if (w != 0) return;
+#pragma unroll
+    for (int a = 0; a < WM; ++a)
+#pragma unroll
+      for (int b = 0; b < WN; ++b) acc[a][b] += red[a][b][lane];
+  }
+#pragma unroll
+  for (int a = 0; a < WM; ++a)
+#pragma unroll
+    for (int b = 0; b < WN; ++b) {
+      const int i = i0 + 16 * b + r;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int c = c0 + 16 * a + q + 4 * g;
+        if (i < n && c < C) Y[(int64_t)c * ld + i] = acc[a][b][g];
+      }
+    }
+}
+
+// LDS-staged variant: a workgroup owns 128 right-hand sides x 128 rows of S over one K slice;
+// each 32-deep K step stages V[128][32] and S[128][32] (256-B rows, 16-B chunk c of row r kept at
+// chunk c ^ (r & 15)) with global_load_lds_dwordx4, double-buffered: the next step's copy is in
+// flight while the 4 waves (32 rows each, 8 x 2 accumulators) run this step's 128 MFMAs from
+// LDS.  One barrier per step.  Linear block id -> (slice = id % kz, so a K slice stays on one
+// XCD and its V slice in that XCD's L2; row block; column block).
+constexpr int M3_VT = 128 * 256;  // bytes of the V tile per stage
+typedef __attribute__((address_space(3))) unsigned char lds_u8;
+typedef __attribute__((address_space(3))) dbl2 lds_dbl2;
+
+template <int RT>
+struct M3 {
+  static constexpr int STAGE = M3_VT + RT * 256;  // V tile + S tile
+};
+
+// NW waves per workgroup, each owning RT / NW rows of the tile (WN = RT / (16 NW) accumulator
+// columns): NW = 8 puts two waves on every SIMD, so one wave's LDS reads / barrier wait hide
+// under the other's MFMAs.
+template <int RT, bool PF, int NW = 4>
+__global__ void __launch_bounds__(64 * NW) k_mm3(const double* __restrict__ S, const double* __restrict__ V,
+                                                 double* __restrict__ Y, int n, int rows, int64_t ld, int C, int kz) {
+  constexpr int RW = RT / NW, WN = RW / 16, STAGE = M3<RT>::STAGE;
+  constexpr int VPW = 32 / NW, SPW = RT / 4 / NW;  // glds per wave per stage
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+  lds_u8* smem = (lds_u8*)smem_raw;
+  const int L = blockIdx.x, z = L % kz, rest = L / kz;
+  const int nrb = (rows + RT - 1) / RT;
+  const int i0 = (rest % nrb) * RT, c0 = (rest / nrb) * 128;
+  Y += (int64_t)z * C * ld;
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int r = lane & 15, q = lane >> 4;
+  const double* vsrc[VPW];
+  const double* ssrc[SPW];
+#pragma unroll
+  for (int p = 0; p < VPW; ++p) {
+    const int row = 4 * (VPW * w + p) + q;
+    const int c = min(c0 + row, C - 1);
+    vsrc[p] = V + (int64_t)c * ld + 2 * (r ^ (row & 15));
+  }
+#pragma unroll
+  for (int p = 0; p < SPW; ++p) {
+    const int row = 4 * (SPW * w + p) + q;
+    const int i = min(i0 + row, rows - 1);
+    ssrc[p] = S + (int64_t)i * ld + 2 * (r ^ (row & 15));
+  }
+  const int nch = (int)(ld / 32), per = (nch + kz - 1) / kz;
+  const int lo = z * per, hi = min(nch, lo + per);
+  auto issue = [&](int ch, int buf) {
+    const int64_t k0 = (int64_t)ch * 32;
+    lds_u8* vb = smem + buf * STAGE;
+#pragma unroll
+    for (int p = 0; p < VPW; ++p)
+      __builtin_amdgcn_global_load_lds((const void*)(vsrc[p] + k0), (lds_u8*)(vb + 4 * (VPW * w + p) * 256), 16, 0, 0);
+#pragma unroll
+    for (int p = 0; p < SPW; ++p)
+      __builtin_amdgcn_global_load_lds((const void*)(ssrc[p] + k0), (lds_u8*)(vb + M3_VT + 4 * (SPW * w + p) * 256), 16, 0, 0);
+  };
+  dbl4 acc[8][WN];
+#pragma unroll
+  for (int a = 0; a < 8; ++a)
+#pragma unroll
+    for (int b = 0; b < WN; ++b) acc[a][b] = dbl4{0.0, 0.0, 0.0, 0.0};
+  const bool live = i0 + RW * w < n;
+  if (lo < hi) issue(lo, 0);
+  for (int ch = lo; ch < hi; ++ch) {
+    const int s = (ch - lo) & 1;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (ch + 1 < hi) issue(ch + 1, s ^ 1);
+    if (!live) continue;
+    const lds_u8* vb = smem + s * STAGE;
+    const lds_u8* sb = vb + M3_VT;
+    dbl2 fa[2][8], fb[2][WN];
+    auto frag = [&](int jj, int u) {
+      const int off = ((4 * q + jj) ^ r) * 16;
+#pragma unroll
+      for (int a = 0; a < 8; ++a) fa[u][a] = *(const lds_dbl2*)(vb + (16 * a + r) * 256 + off);
+#pragma unroll
+      for (int b = 0; b < WN; ++b) fb[u][b] = *(const lds_dbl2*)(sb + (RW * w + 16 * b + r) * 256 + off);
+    };
+    frag(0, 0);
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) {
+      const int u = PF ? (jj & 1) : 0;
+      if (PF && jj < 3) frag(jj + 1, u ^ 1);
+#pragma unroll
+      for (int mm = 0; mm < 2; ++mm)
+#pragma unroll
+        for (int a = 0; a < 8; ++a)
+#pragma unroll
+          for (int b = 0; b < WN; ++b)
+            acc[a][b] = __builtin_amdgcn_mfma_f64_16x16x4f64(mm ? fa[u][a].y : fa[u][a].x, mm ? fb[u][b].y : fb[u][b].x,
+                                                             acc[a][b], 0, 0, 0);
+      if (!PF && jj < 3) frag(jj + 1, 0);
+    }
+  }
+  if (!live) return;
+#pragma unroll
+  for (int a = 0; a < 8; ++a)
+#pragma unroll
+    for (int b = 0; b < WN; ++b) {
+      const int i = i0 + RW * w + 16 * b + r;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int c = c0 + 16 * a + q + 4 * g;
+        if (i < n && c < C) Y[(int64_t)c * ld + i] = acc[a][b][g];
+      }
+    }
+}
+
 // sum of KZ partial slabs in fixed order into slab 0
 __global__ void k_red(double* Y, int64_t slab, int kz) {
   const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
@@ -120,6 +336,8 @@ __global__ void k_peak(double* out, int iters) {
   if (s == 12345.678) out[0] = s;
 }
 
+static bool g_red = true;  // timing loops skip the slab sum (the solver's state kernel does it)
+
 struct Variant {
   std::string name;
   void (*launch)(const double*, const double*, double*, int, int, int64_t, int, hipStream_t);
@@ -129,13 +347,40 @@ template <int WM, int WN, int KS, int KZ = 1>
 void launch_mm(const double* S, const double* V, double* Y, int n, int rows, int64_t ld, int C, hipStream_t st) {
   dim3 grid((rows + 16 * WN - 1) / (16 * WN), (C + 16 * WM - 1) / (16 * WM), KZ);
   hipLaunchKernelGGL((k_mm<WM, WN, KS>), grid, dim3(64 * KS), 0, st, S, V, Y, n, rows, ld, C);
-  if (KZ > 1) {
+  if (KZ > 1 && g_red) {
+    const int64_t slab = (int64_t)C * ld;
+    hipLaunchKernelGGL(k_red, dim3((unsigned)((slab + 255) / 256)), dim3(256), 0, st, Y, slab, KZ);
+  }
+}
+
+template <int WM, int WN, int KS, int KZ = 1>
+void launch_mm2(const double* S, const double* V, double* Y, int n, int rows, int64_t ld, int C, hipStream_t st) {
+  dim3 grid((rows + 16 * WN - 1) / (16 * WN), (C + 16 * WM - 1) / (16 * WM), KZ);
+  hipLaunchKernelGGL((k_mm2<WM, WN, KS>), grid, dim3(64 * KS), 0, st, S, V, Y, n, rows, ld, C);
+  if (KZ > 1 && g_red) {
+    const int64_t slab = (int64_t)C * ld;
+    hipLaunchKernelGGL(k_red, dim3((unsigned)((slab + 255) / 256)), dim3(256), 0, st, Y, slab, KZ);
+  }
+}
+
+template <int RT, bool PF, int KZ, int NW = 4>
+void launch_mm3(const double* S, const double* V, double* Y, int n, int rows, int64_t ld, int C, hipStream_t st) {
+  const int nrb = (rows + RT - 1) / RT, ncb = (C + 127) / 128;
+  hipLaunchKernelGGL((k_mm3<RT, PF, NW>), dim3(nrb * ncb * KZ), dim3(64 * NW), M3<RT>::STAGE * 2, st, S, V, Y, n, rows, ld,
+                     C, KZ);
+  if (KZ > 1 && g_red) {
     const int64_t slab = (int64_t)C * ld;
     hipLaunchKernelGGL(k_red, dim3((unsigned)((slab + 255) / 256)), dim3(256), 0, st, Y, slab, KZ);
   }
 }
 
 int main(int argc, char** argv) {
+  CHK(hipFuncSetAttribute((const void*)k_mm3<128, false>, hipFuncAttributeMaxDynamicSharedMemorySize, M3<128>::STAGE * 2));
+  CHK(hipFuncSetAttribute((const void*)k_mm3<128, true>, hipFuncAttributeMaxDynamicSharedMemorySize, M3<128>::STAGE * 2));
+  CHK(hipFuncSetAttribute((const void*)k_mm3<64, false>, hipFuncAttributeMaxDynamicSharedMemorySize, M3<64>::STAGE * 2));
+  CHK(hipFuncSetAttribute((const void*)k_mm3<64, true>, hipFuncAttributeMaxDynamicSharedMemorySize, M3<64>::STAGE * 2));
+  CHK(hipFuncSetAttribute((const void*)k_mm3<128, true, 8>, hipFuncAttributeMaxDynamicSharedMemorySize, M3<128>::STAGE * 2));
+  CHK(hipFuncSetAttribute((const void*)k_mm3<64, true, 8>, hipFuncAttributeMaxDynamicSharedMemorySize, M3<64>::STAGE * 2));
   const int n = argc > 1 ? atoi(argv[1]) : 4000;
   const int C = argc > 2 ? atoi(argv[2]) : 128;
   const int64_t ld = (n + 127) / 128 * 128;
@@ -160,8 +405,9 @@ int main(int argc, char** argv) {
   double *S, *V, *Y;
   CHK(hipMalloc(&S, hS.size() * 8));
   CHK(hipMalloc(&V, hV.size() * 8));
-  CHK(hipMalloc(&Y, (size_t)4 * C * ld * 8));
-  {
+  CHK(hipMalloc(&Y, (size_t)16 * C * ld * 8));
+  const char* only = argc > 3 ? argv[3] : nullptr;  // run only variants whose name contains this
+  if (!only) {
     hipEvent_t a, b;
     CHK(hipEventCreate(&a));
     CHK(hipEventCreate(&b));
@@ -189,12 +435,22 @@ int main(int argc, char** argv) {
       {"wm4 wn4 ks4 kz4", launch_mm<4, 4, 4, 4>}, {"wm4 wn2 ks4 kz4", launch_mm<4, 2, 4, 4>},
       {"wm2 wn1 ks4 kz4", launch_mm<2, 1, 4, 4>}, {"wm2 wn1 ks8", launch_mm<2, 1, 8>},
       {"wm2 wn2 ks8 kz2", launch_mm<2, 2, 8, 2>}, {"wm1 wn2 ks8", launch_mm<1, 2, 8>},
+      {"pipe wm8 wn2 ks4 kz4", launch_mm2<8, 2, 4, 4>}, {"pipe wm8 wn2 ks4 kz2", launch_mm2<8, 2, 4, 2>},
+      {"pipe wm8 wn2 ks4 kz1", launch_mm2<8, 2, 4, 1>}, {"pipe wm4 wn4 ks4 kz4", launch_mm2<4, 4, 4, 4>},
+      {"pipe wm8 wn4 ks4 kz4", launch_mm2<8, 4, 4, 4>}, {"pipe wm4 wn2 ks4 kz4", launch_mm2<4, 2, 4, 4>},
+      {"pipe wm4 wn2 ks8 kz4", launch_mm2<4, 2, 8, 4>}, {"pipe wm8 wn1 ks4 kz4", launch_mm2<8, 1, 4, 4>},
+      {"pipe wm2 wn1 ks4 kz4", launch_mm2<2, 1, 4, 4>},
+      {"glds r128 kz8", launch_mm3<128, false, 8>}, {"glds r128 pf kz8", launch_mm3<128, true, 8>},
+      {"glds r64 kz4", launch_mm3<64, false, 4>},   {"glds r64 pf kz4", launch_mm3<64, true, 4>},
+      {"glds r64 pf kz8", launch_mm3<64, true, 8>}, {"glds r128 pf kz16", launch_mm3<128, true, 16>},
+      {"glds r128 pf kz8 nw8", launch_mm3<128, true, 8, 8>}, {"glds r64 pf kz8 nw8", launch_mm3<64, true, 8, 8>},
   };
   hipEvent_t e0, e1;
   CHK(hipEventCreate(&e0));
   CHK(hipEventCreate(&e1));
   std::vector<double> hY((size_t)C * ld);
   for (auto& v : vs) {
+    if (only && v.name.find(only) == std::string::npos) continue;
     CHK(hipMemset(Y, 0, (size_t)C * ld * 8));
     v.launch(S, V, Y, n, rows, ld, C, 0);
     CHK(hipDeviceSynchronize());
@@ -206,10 +462,12 @@ int main(int argc, char** argv) {
         maxrel = fmax(maxrel, d / (fabs(ref[(size_t)c * n + i]) + 1e-3));
       }
     const int reps = 50;
+    g_red = false;
     CHK(hipEventRecord(e0, 0));
     for (int r = 0; r < reps; ++r) v.launch(S, V, Y, n, rows, ld, C, 0);
     CHK(hipEventRecord(e1, 0));
     CHK(hipEventSynchronize(e1));
+    g_red = true;
     float ms = 0;
     CHK(hipEventElapsedTime(&ms, e0, e1));
     const double t = ms / reps;
