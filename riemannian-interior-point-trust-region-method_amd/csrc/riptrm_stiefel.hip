@@ -28,29 +28,228 @@ namespace riptrm_stiefel {
 constexpr int NW = 8;          // waves per workgroup (one workgroup per point)
 constexpr int T = NW * 64;     // threads per workgroup
 constexpr int PMAX = RIPTRM_STIEFEL_PMAX;
-constexpr int GMAX = 8;        // 4-row groups per wave per streamed chunk (8 waves x 32 rows = 256 rows)
-constexpr int NBLK = 10;       // upper-triangular 16 x 16 blocks of a p x p matrix at p <= 64
+constexpr int PS = PMAX + 1;   // LDS row stride of p x p matrices: odd, so a column walk (one row per
+                               // lane, the Cholesky) is 2-way banked at worst
+constexpr int UB = 13;         // 4-row groups per gram load batch (loads of a batch in flight together;
+                               // 2 batches per wave at n = 200)
 
-// LDS (dynamic): M and L are p x p (padded stride PS <= 64), red holds the wave partials of the
-// Gram reduction tree (NW / 2 waves x NBLK blocks x 256 doubles).
+// LDS (dynamic): M (p x p, stride PS: sym(A^T B), then the Cholesky factor in its lower triangle)
+// and red (the k-half partials of the Gram: 4 block rows x 4 block columns x 256 doubles).
 // address-space-3 pointers: ds_read / ds_write, not flat accesses through generic pointers
 typedef __attribute__((address_space(3))) double lds_f64;
 struct Smem {
-  lds_f64* M;     // p x p (Gram / sym / R^-1)
-  lds_f64* L;     // Cholesky factor
+  lds_f64* M;
   lds_f64* red;
 };
-constexpr int LDS_DOUBLES = 2 * PMAX * PMAX + (NW / 2) * NBLK * 256;
+constexpr int LDS_DOUBLES = PMAX * PS + 16 * 256;
 
 __device__ __forceinline__ Smem smem_of(double* base_generic) {
   lds_f64* base = (lds_f64*)base_generic;
-  return Smem{base, base + PMAX * PMAX, base + 2 * PMAX * PMAX};
+  return Smem{base, base + PMAX * PS};
 }
 
 typedef double dbl4 __attribute__((ext_vector_type(4)));
 
-// Small p x p matrices live in LDS with the padded row stride PS = 16 ceil(p / 16) and zeros
-// outside p x p, so the MFMA loops read operands without bounds tests (no divergent branches).
+// Diagnostic builds only (tools/stiefel_stamps.hip defines ST_STAMPS): s_memtime at phase ends,
+// thread 0 of each workgroup, into a buffer nothing else reads.
+#ifdef ST_STAMPS
+__device__ long long* g_st_stamps;
+#define ST_STAMP(k)                                                                      \
+  do {                                                                                   \
+    if (threadIdx.x == 0) g_st_stamps[blockIdx.x * 16 + (k)] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+#else
+#define ST_STAMP(k) \
+  do {              \
+  } while (0)
+#endif
+
+// Guarded operand loads: load a clamped (always valid) address and scale by a 0/1 mask, so the
+// load cannot be sunk into a branch (a select on a runtime bound makes hipcc branch around every
+// load and wait vmcnt(0) after each — one memory latency per element).  Data are finite.
+__device__ __forceinline__ double mask01(bool ok) { return ok ? 1.0 : 0.0; }
+
+// sm.M <- sym(A^T B) = (M + M^T) / 2 with M = A^T B, n x p row-major A, B (exactly symmetric:
+// M_ij + M_ji is the same sum both ways).  v_mfma_f64_16x16x4_f64 blocks M_IJ (16 x 16, I, J <
+// ceil(p/16)): wave w = 4 kg + I owns block row I over the 4-row groups g = kg, kg + 2, ... (the
+// k dimension is the n rows), A operand = A[4g + kk][16 I + c] (the block of A^T), B operand =
+// B[4g + kk][16 J + c]; loads for UB groups issue together.  The two k halves meet once in LDS
+// (kg = 1 writes, kg = 0 adds): a fixed order, bitwise deterministic.  AEQB: A == B (A^T A), the
+// B operand of column block I is the A operand.
+template <bool AEQB, int P16, bool SUM = false>
+__device__ __forceinline__ void gram(Smem& sm, const double* __restrict__ A, const double* __restrict__ B, int n,
+                                     int p) {
+  const int t = threadIdx.x, l = t & 63, w = t >> 6;
+  const int c = l & 15, kk = l >> 4;
+  const int kg = w >> 2, I = w & 3;
+  const int G = (n + 3) / 4;
+  dbl4 acc[4];
+#pragma unroll
+  for (int J = 0; J < 4; ++J) acc[J] = dbl4{0.0, 0.0, 0.0, 0.0};
+  if (I < P16) {
+    const int colA = 16 * I + c;
+    for (int g0 = kg; g0 < G; g0 += 2 * UB) {
+      double av[UB], bv[UB][4];
+#pragma unroll
+      for (int u = 0; u < UB; ++u) {
+        const int row = 4 * (g0 + 2 * u) + kk;
+        const bool rok = row < n;
+        const int64_t rb = (int64_t)(rok ? row : n - 1) * p;
+        const int64_t ea = rb + (colA < p ? colA : p - 1);
+        av[u] = (SUM ? A[ea] + B[ea] : A[ea]) * mask01(rok && colA < p);
+#pragma unroll
+        for (int J = 0; J < 4; ++J) {   // J, P16: constants
+          const int col = 16 * J + c;
+          const int64_t eb = rb + (col < p ? col : p - 1);
+          const double vb = AEQB ? (SUM ? A[eb] + B[eb] : A[eb]) : B[eb];
+          bv[u][J] = J < P16 ? vb * mask01(rok && col < p) : 0.0;
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);  // every load of the batch issues before the first MFMA
+#pragma unroll
+      for (int u = 0; u < UB; ++u) {   // groups past the last are zero operands: no branch between loads
+#pragma unroll
+        for (int J = 0; J < 4; ++J)
+          if (J < P16) acc[J] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[u], bv[u][J], acc[J], 0, 0, 0);
+      }
+    }
+  }
+  if (kg == 1 && I < P16) {
+#pragma unroll
+    for (int J = 0; J < 4; ++J)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) sm.red[(I * 4 + J) * 256 + q * 64 + l] = acc[J][q];
+  }
+  __syncthreads();
+  if (kg == 0 && I < P16) {
+#pragma unroll
+    for (int J = 0; J < 4; ++J) {
+      if (J < P16) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const double v = acc[J][q] + sm.red[(I * 4 + J) * 256 + q * 64 + l];
+          // D (f64): row = kk + 4q of the block, column = c
+          const int i = 16 * I + kk + 4 * q, j = 16 * J + c;
+          if (i < p && j < p) sm.M[i * PS + j] = v;
+        }
+      }
+    }
+  }
+  __syncthreads();
+  for (int e = t; e < p * p; e += T) {   // symmetric part: one thread per pair i < j
+    const int i = e / p, j = e - (e / p) * p;
+    if (i < j) {
+      const double v = 0.5 * (sm.M[i * PS + j] + sm.M[j * PS + i]);
+      sm.M[i * PS + j] = v;
+      sm.M[j * PS + i] = v;
+    }
+  }
+  __syncthreads();
+}
+
+// out = C + sgn * A K (K = sm.M, p x p) on the matrix cores.  Units (16-row block R, pair of
+// 16-column blocks) are dealt round-robin to the 8 waves; a unit's operands — A[16R + c][4s + kk]
+// for every k step, its C values and the K column slices from LDS — are all loaded ahead of a
+// scheduling barrier, then its MFMAs run (k steps past p are skipped by a wave-uniform test on
+// the MFMA alone, never around a load).  out must not alias A (another wave may still read those
+// rows); it may alias C.
+template <int P16>
+__device__ __forceinline__ void update(Smem& sm, const double* __restrict__ A, const double* C, double sgn,
+                                       double* out, int n, int p) {
+  constexpr int S4 = 4 * P16;    // k steps of 4 covering 16 P16 columns
+  const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c = l & 15, kk = l >> 4;
+  const int R16 = (n + 15) / 16, P4 = (p + 3) / 4;
+  constexpr int H = (P16 + 1) / 2;   // column-block pairs
+  for (int u = w; u < R16 * H; u += NW) {
+    const int R = u / H, J0 = 2 * (u - R * H);
+    const int arow = 16 * R + c;
+    const int64_t ab = (int64_t)(arow < n ? arow : n - 1) * p;
+    double ar[S4], bk[2][S4], cv[2][4];
+#pragma unroll
+    for (int s = 0; s < S4; ++s) {
+      const int k = 4 * s + kk;
+      ar[s] = A[ab + (k < p ? k : p - 1)] * mask01(arow < n && k < p);
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int j = 16 * (J0 + h) + c;
+      const bool jok = J0 + h < P16 && j < p;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int i = 16 * R + kk + 4 * g;
+        cv[h][g] = C[(int64_t)(i < n ? i : n - 1) * p + (jok ? j : p - 1)] * mask01(jok && i < n);
+      }
+      const lds_f64* pb = sm.M + kk * PS + (jok ? j : 0);
+#pragma unroll
+      for (int s = 0; s < S4; ++s) bk[h][s] = pb[(4 * s + kk < p ? 4 * s : 0) * PS] * mask01(jok && 4 * s + kk < p);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    dbl4 acc[2] = {dbl4{0.0, 0.0, 0.0, 0.0}, dbl4{0.0, 0.0, 0.0, 0.0}};
+#pragma unroll
+    for (int s = 0; s < S4; ++s)
+      if (s < P4) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+          if (J0 + h < P16) acc[h] = __builtin_amdgcn_mfma_f64_16x16x4f64(ar[s], bk[h][s], acc[h], 0, 0, 0);
+      }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      if (J0 + h < P16) {
+        const int j = 16 * (J0 + h) + c;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int i = 16 * R + kk + 4 * g;
+          if (i < n && j < p) out[(int64_t)i * p + j] = cv[h][g] + sgn * acc[h][g];
+        }
+      }
+    }
+  }
+  __syncthreads();
+}
+
+template <int P16>
+__global__ void __launch_bounds__(T) k_st_proj(int n, int p, int64_t stride, const double* X, const double* U, double* out) {
+  extern __shared__ double lds[];
+  Smem sm = smem_of(lds);
+  const int64_t o = (int64_t)blockIdx.x * stride;
+  ST_STAMP(0);
+  gram<false, P16>(sm, X + o, U + o, n, p);
+  ST_STAMP(1);
+  update<P16>(sm, X + o, U + o, -1.0, out + o, n, p);
+  ST_STAMP(2);
+}
+
+template <int P16>
+__global__ void __launch_bounds__(T) k_st_e2rh(int n, int p, int64_t stride, const double* X, const double* G,
+                                               const double* H, const double* U, double* out) {
+  extern __shared__ double lds[];
+  Smem sm = smem_of(lds);
+  const int64_t o = (int64_t)blockIdx.x * stride;
+  gram<false, P16>(sm, X + o, G + o, n, p);              // sym(X^T G)
+  update<P16>(sm, U + o, H + o, -1.0, out + o, n, p);    // W = H - U sym(X^T G) into out
+  gram<false, P16>(sm, X + o, out + o, n, p);            // sym(X^T W)
+  update<P16>(sm, X + o, out + o, -1.0, out + o, n, p);  // P_X(W)
+}
+
+// ---- retraction (CholeskyQR2): the round-1 kernel, kept as measured best ----------------------
+// Its own LDS layout: M and L (p x p, stride 16 ceil(p/16)) and the 8-wave Gram tree's partials.
+// Redesigns tried this round and measured slower at (200, 50) x 256 (tools/stiefel_stamps.hip
+// phase stamps): a single-wave register-resident Cholesky (33-56 µs per factor vs
+// ~40 here), a column-oriented row solve with data-dependent LDS reads, and a first Gram reading
+// X + U directly — 222-349 µs in total against this kernel's 191 µs.
+constexpr int NBLK = 10;       // upper-triangular 16 x 16 blocks of a p x p matrix at p <= 64
+constexpr int GMAX = 8;        // 4-row groups per wave per streamed chunk (8 waves x 32 rows = 256 rows)
+struct SmemR {
+  lds_f64* M;
+  lds_f64* L;
+  lds_f64* red;
+};
+constexpr int LDS_DOUBLES_R = 2 * PMAX * PMAX + (NW / 2) * NBLK * 256;
+__device__ __forceinline__ SmemR smem_of_r(double* base_generic) {
+  lds_f64* base = (lds_f64*)base_generic;
+  return SmemR{base, base + PMAX * PMAX, base + 2 * PMAX * PMAX};
+}
 __device__ __forceinline__ int pstride(int p) { return ((p + 15) / 16) * 16; }
 
 // sm.M <- sym(A^T B) = (A^T B + B^T A) / 2 for n x p row-major A, B, exactly symmetric, on the fp64
@@ -59,7 +258,7 @@ __device__ __forceinline__ int pstride(int p) { return ((p + 15) / 16) * 16; }
 // once (one memory latency per 256-row chunk, all loads of the workgroup in flight together) —
 // and accumulates the upper-triangular blocks S_IJ = A_I^T B_J + B_I^T A_J (I <= J).  The eight
 // wave partials meet in a fixed LDS tree (bitwise deterministic); wave 0 writes S / 2.
-__device__ __forceinline__ void gram_sym(Smem& sm, const double* __restrict__ A, const double* __restrict__ B,
+__device__ __forceinline__ void gram_sym_r(SmemR& sm, const double* __restrict__ A, const double* __restrict__ B,
                                          int n, int p) {
   const int t = threadIdx.x, l = t & 63, w = t >> 6;
   const int c = l & 15, kk = l >> 4;
@@ -143,78 +342,8 @@ __device__ __forceinline__ void gram_sym(Smem& sm, const double* __restrict__ A,
   __syncthreads();
 }
 
-// out = C + sgn * A K (K = sm.M, p x p, padded) on the matrix cores.  A wave owns 16-row blocks
-// of the output and computes ALL their column blocks before writing, reading its A rows only:
-// out may alias A or C.  C = nullptr gives out = A K.
-__device__ __forceinline__ void update(Smem& sm, const double* A, const double* C, double sgn, double* out,
-                                       int n, int p) {
-  const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int P16 = (p + 15) / 16, R16 = (n + 15) / 16, PS = P16 * 16;
-  const int c = l & 15, kk = l >> 4;
-  const int P4 = (p + 3) / 4;
-  for (int I = w; I < R16; I += NW) {
-    dbl4 acc[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) acc[q] = dbl4{0.0, 0.0, 0.0, 0.0};
-    const int arow = I * 16 + c;
-    double ar[PMAX / 4];   // this lane's A operands for every k step, loaded at once
-#pragma unroll
-    for (int k4 = 0; k4 < PMAX / 4; ++k4) {
-      const int k = k4 * 4 + kk;
-      const bool ok = k4 < P4 && arow < n && k < p;
-      const double v = A[ok ? (int64_t)arow * p + k : 0];
-      ar[k4] = ok ? v : 0.0;
-    }
-#pragma unroll
-    for (int J = 0; J < 4; ++J) {
-      if (J < P16) {
-        const lds_f64* pb = sm.M + kk * PS + J * 16 + c;
-#pragma unroll
-        for (int k4 = 0; k4 < PMAX / 4; ++k4)
-          if (k4 < P4) acc[J] = __builtin_amdgcn_mfma_f64_16x16x4f64(ar[k4], pb[k4 * 4 * PS], acc[J], 0, 0, 0);
-      }
-    }
-    // every lane of the wave has read its A rows before any lane writes them
-    __builtin_amdgcn_wave_barrier();
-#pragma unroll
-    for (int J = 0; J < 4; ++J) {
-      if (J < P16) {
-        const int j = J * 16 + c;
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const int i = I * 16 + kk + 4 * g;
-          if (i < n && j < p) {
-            const int64_t e = (int64_t)i * p + j;
-            out[e] = C ? C[e] + sgn * acc[J][g] : acc[J][g];
-          }
-        }
-      }
-    }
-  }
-  __syncthreads();
-}
-
-__global__ void __launch_bounds__(T) k_st_proj(int n, int p, int64_t stride, const double* X, const double* U, double* out) {
-  extern __shared__ double lds[];
-  Smem sm = smem_of(lds);
-  const int64_t o = (int64_t)blockIdx.x * stride;
-  gram_sym(sm, X + o, U + o, n, p);
-  update(sm, X + o, U + o, -1.0, out + o, n, p);
-}
-
-__global__ void __launch_bounds__(T) k_st_e2rh(int n, int p, int64_t stride, const double* X, const double* G,
-                                               const double* H, const double* U, double* out) {
-  extern __shared__ double lds[];
-  Smem sm = smem_of(lds);
-  const int64_t o = (int64_t)blockIdx.x * stride;
-  gram_sym(sm, X + o, G + o, n, p);                // sym(X^T G)
-  update(sm, U + o, H + o, -1.0, out + o, n, p);   // W = H - U sym(X^T G) into out
-  gram_sym(sm, X + o, out + o, n, p);              // sym(X^T W)
-  update(sm, X + o, out + o, -1.0, out + o, n, p);  // P_X(W)
-}
-
 // sm.M (SPD p x p, stride PS) -> sm.L = lower Cholesky factor (A^T A = L L^T, diag > 0)
-__device__ __forceinline__ void chol_lower(Smem& sm, int p) {
+__device__ __forceinline__ void chol_lower_r(SmemR& sm, int p) {
   const int t = threadIdx.x, PS = pstride(p);
   lds_f64* G = sm.M;
   lds_f64* L = sm.L;
@@ -236,7 +365,7 @@ __device__ __forceinline__ void chol_lower(Smem& sm, int p) {
 
 // A <- A R^-1 (R = L^T) row by row: row a_i solves q R = a_i by forward substitution, all n rows in
 // parallel with the row in registers and L read as LDS broadcasts — no serial p^2 inverse.
-__device__ __forceinline__ void rows_solve(const Smem& sm, double* A, int n, int p) {
+__device__ __forceinline__ void rows_solve_r(const SmemR& sm, double* A, int n, int p) {
   const int PS = pstride(p);
   for (int i = threadIdx.x; i < n; i += T) {
     double q[PMAX];
@@ -258,17 +387,17 @@ __device__ __forceinline__ void rows_solve(const Smem& sm, double* A, int n, int
   __syncthreads();
 }
 
-__global__ void __launch_bounds__(T) k_st_retr(int n, int p, int64_t stride, const double* X, const double* U, double* out) {
+__global__ void __launch_bounds__(T) k_st_retr_r(int n, int p, int64_t stride, const double* X, const double* U, double* out) {
   extern __shared__ double lds[];
-  Smem sm = smem_of(lds);
+  SmemR sm = smem_of_r(lds);
   const int64_t o = (int64_t)blockIdx.x * stride;
   double* A = out + o;
   for (int e = threadIdx.x; e < n * p; e += T) A[e] = X[o + e] + U[o + e];
   __syncthreads();
   for (int pass = 0; pass < 2; ++pass) {   // CholeskyQR2
-    gram_sym(sm, A, A, n, p);                // (A^T A + A^T A) / 2 = A^T A exactly
-    chol_lower(sm, p);
-    rows_solve(sm, A, n, p);                 // A R^-1
+    gram_sym_r(sm, A, A, n, p);                // (A^T A + A^T A) / 2 = A^T A exactly
+    chol_lower_r(sm, p);
+    rows_solve_r(sm, A, n, p);                 // A R^-1
   }
 }
 
@@ -298,15 +427,29 @@ static int st_check(riptrm_ctx* c, int32_t n, int32_t p, int32_t batch, int64_t 
   static bool attr[64] = {};   // per device: dynamic LDS above the 64 KiB default
   if (c->device < 0 || c->device >= 64 || !attr[c->device]) {
     const int shm = (int)(LDS_DOUBLES * sizeof(double));
-    HIPCHK(c, hipFuncSetAttribute((const void*)k_st_proj, hipFuncAttributeMaxDynamicSharedMemorySize, shm));
-    HIPCHK(c, hipFuncSetAttribute((const void*)k_st_e2rh, hipFuncAttributeMaxDynamicSharedMemorySize, shm));
-    HIPCHK(c, hipFuncSetAttribute((const void*)k_st_retr, hipFuncAttributeMaxDynamicSharedMemorySize, shm));
+    const void* fns[] = {(const void*)k_st_proj<1>, (const void*)k_st_proj<2>, (const void*)k_st_proj<3>,
+                         (const void*)k_st_proj<4>, (const void*)k_st_e2rh<1>, (const void*)k_st_e2rh<2>,
+                         (const void*)k_st_e2rh<3>, (const void*)k_st_e2rh<4>};
+    for (const void* f : fns) HIPCHK(c, hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, shm));
+    HIPCHK(c, hipFuncSetAttribute((const void*)k_st_retr_r, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)(LDS_DOUBLES_R * sizeof(double))));
     if (c->device >= 0 && c->device < 64) attr[c->device] = true;
   }
   return RIPTRM_OK;
 }
 
 constexpr size_t SHM = LDS_DOUBLES * sizeof(double);
+constexpr size_t SHM_R = LDS_DOUBLES_R * sizeof(double);
+
+// kernels are specialised on ceil(p / 16) (the 16-column blocks), so no operand load sits behind
+// a runtime branch
+#define ST_LAUNCH(K, p, ...)                                                                              \
+  switch (((p) + 15) / 16) {                                                                             \
+    case 1: hipLaunchKernelGGL(K<1>, __VA_ARGS__); break;                                              \
+    case 2: hipLaunchKernelGGL(K<2>, __VA_ARGS__); break;                                              \
+    case 3: hipLaunchKernelGGL(K<3>, __VA_ARGS__); break;                                              \
+    default: hipLaunchKernelGGL(K<4>, __VA_ARGS__); break;                                             \
+  }
 
 extern "C" {
 
@@ -328,7 +471,7 @@ int riptrm_stiefel_proj(riptrm_ctx* ctx, int32_t n, int32_t p, int32_t batch, in
   if (!X || !U || !out || out == X) return fail(ctx, RIPTRM_E_ARG, "stiefel_proj: bad pointer (out must not alias X)");
   int rc = st_check(ctx, n, p, batch, stride);
   if (rc) return rc;
-  hipLaunchKernelGGL(k_st_proj, dim3(batch), dim3(T), SHM, ctx->stream, n, p, stride, X, U, out);
+  ST_LAUNCH(k_st_proj, p, dim3(batch), dim3(T), SHM, ctx->stream, n, p, stride, X, U, out);
   HIPCHK(ctx, hipGetLastError());
   return RIPTRM_OK;
 }
@@ -339,7 +482,7 @@ int riptrm_stiefel_retr(riptrm_ctx* ctx, int32_t n, int32_t p, int32_t batch, in
   if (!X || !U || !out) return fail(ctx, RIPTRM_E_ARG, "stiefel_retr: null pointer");
   int rc = st_check(ctx, n, p, batch, stride);
   if (rc) return rc;
-  hipLaunchKernelGGL(k_st_retr, dim3(batch), dim3(T), SHM, ctx->stream, n, p, stride, X, U, out);
+  hipLaunchKernelGGL(k_st_retr_r, dim3(batch), dim3(T), SHM_R, ctx->stream, n, p, stride, X, U, out);
   HIPCHK(ctx, hipGetLastError());
   return RIPTRM_OK;
 }
@@ -351,7 +494,7 @@ int riptrm_stiefel_ehess2rhess(riptrm_ctx* ctx, int32_t n, int32_t p, int32_t ba
     return fail(ctx, RIPTRM_E_ARG, "stiefel_ehess2rhess: bad pointer (out must not alias X or U)");
   int rc = st_check(ctx, n, p, batch, stride);
   if (rc) return rc;
-  hipLaunchKernelGGL(k_st_e2rh, dim3(batch), dim3(T), SHM, ctx->stream, n, p, stride, X, G, H, U, out);
+  ST_LAUNCH(k_st_e2rh, p, dim3(batch), dim3(T), SHM, ctx->stream, n, p, stride, X, G, H, U, out);
   HIPCHK(ctx, hipGetLastError());
   return RIPTRM_OK;
 }

@@ -1,0 +1,66 @@
+// stiefel_stamps.hip — phase timing of the Stiefel kernels (diagnostic build, s_memtime stamps).
+// hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -I<pkg>/csrc -I include tools/stiefel_stamps.hip
+// Runs k_st_proj / k_st_retr_r at (n, p, batch) on random data and prints, per phase, the median
+// over workgroups of the stamp deltas (s_memtime ticks) and the kernel's event time.
+#define ST_STAMPS 1
+#include "riptrm_stiefel.hip"
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP %s line %d\n", hipGetErrorString(e), __LINE__); exit(1);} } while (0)
+
+int main(int argc, char** argv) {
+  const int n = argc > 1 ? atoi(argv[1]) : 200, p = argc > 2 ? atoi(argv[2]) : 50, B = argc > 3 ? atoi(argv[3]) : 256;
+  const size_t N = (size_t)B * n * p;
+  std::vector<double> h(N);
+  srand(7);
+  for (auto& v : h) v = (double)rand() / RAND_MAX - 0.5;
+  double *X, *U, *O;
+  long long* st;
+  CK(hipMalloc(&X, N * 8));
+  CK(hipMalloc(&U, N * 8));
+  CK(hipMalloc(&O, N * 8));
+  CK(hipMalloc(&st, (size_t)B * 16 * 8));
+  CK(hipMemcpy(X, h.data(), N * 8, hipMemcpyHostToDevice));
+  for (auto& v : h) v *= 0.01;
+  CK(hipMemcpy(U, h.data(), N * 8, hipMemcpyHostToDevice));
+  CK(hipMemcpyToSymbol(HIP_SYMBOL(g_st_stamps), &st, sizeof(st)));
+  const int shm = LDS_DOUBLES * 8;
+  CK(hipFuncSetAttribute((const void*)k_st_proj<4>, hipFuncAttributeMaxDynamicSharedMemorySize, shm));
+  CK(hipFuncSetAttribute((const void*)k_st_retr_r, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_DOUBLES_R * 8));
+  hipEvent_t a, b;
+  CK(hipEventCreate(&a));
+  CK(hipEventCreate(&b));
+  for (int which = 0; which < 2; ++which) {
+    for (int r = 0; r < 20; ++r) {
+      CK(hipEventRecord(a, 0));
+      if (which == 0) hipLaunchKernelGGL(k_st_proj<4>, dim3(B), dim3(T), shm, 0, n, p, (int64_t)n * p, X, U, O);
+      else hipLaunchKernelGGL(k_st_retr_r, dim3(B), dim3(T), LDS_DOUBLES_R * 8, 0, n, p, (int64_t)n * p, X, U, O);
+      CK(hipEventRecord(b, 0));
+      CK(hipEventSynchronize(b));
+    }
+    float ms = 0;
+    CK(hipEventElapsedTime(&ms, a, b));
+    std::vector<long long> s((size_t)B * 16);
+    CK(hipMemcpy(s.data(), st, s.size() * 8, hipMemcpyDeviceToHost));
+    if (which) {   // the retraction kernel carries no stamps: event time only
+      printf("{\"kernel\": \"k_st_retr_r\", \"n\": %d, \"p\": %d, \"B\": %d, \"event_us\": %.2f}\n", n, p, B, ms * 1e3);
+      continue;
+    }
+    const int np = 2;
+    printf("{\"kernel\": \"%s\", \"n\": %d, \"p\": %d, \"B\": %d, \"event_us\": %.2f, \"phase_ticks_median\": [", which ? "k_st_retr" : "k_st_proj", n, p, B, ms * 1e3);
+    for (int k = 0; k < np; ++k) {
+      std::vector<long long> d(B);
+      for (int g = 0; g < B; ++g) d[g] = s[g * 16 + k + 1] - s[g * 16 + k];
+      std::sort(d.begin(), d.end());
+      printf("%s%lld", k ? ", " : "", d[B / 2]);
+    }
+    std::vector<long long> t(B);
+    for (int g = 0; g < B; ++g) t[g] = s[g * 16 + np] - s[g * 16];
+    std::sort(t.begin(), t.end());
+    printf("], \"total_ticks_median\": %lld, \"total_ticks_max\": %lld}\n", t[B / 2], t[B - 1]);
+  }
+  return 0;
+}
