@@ -38,7 +38,7 @@ for p in (ROOT, PKG):
 
 METRIC = "outer RIPTRM iterations/sec, batched NonnegPCA n=4000, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0
-MM_KZ = 8  # K slices of the shared-layout MFMA S-pass (csrc/riptrm_device.h)
+MM_KZ = 4  # K slices of the shared-layout MFMA S-pass (csrc/riptrm_device.h)
 MFMA_F64_PEAK_TFS = 78.6  # MI355X dense FP64 matrix peak (spec); tools/mfma_bench.hip issue probe: 70 TFLOP/s
 
 
@@ -369,7 +369,8 @@ def main():
             roofline = {"bound": "mfma", "achieved": tf, "peak": MFMA_F64_PEAK_TFS, "unit": "TFLOP/s",
                         "frac": (tf / MFMA_F64_PEAK_TFS) if tf else None, "traffic": None,
                         "kernel": ("k_spass_mm (shared-S multi-start S-pass, v_mfma_f64_16x16x4_f64; 128 right-hand sides x "
-                                   "128 rows per workgroup, V and S K-steps staged in LDS by global_load_lds, "
+                                   f"{64 if ((n + 31) // 32 * 32 + 127) // 128 * MM_KZ < 256 else 128} rows per "
+                                   "workgroup, 8 waves, V and S K-steps staged in LDS by global_load_lds, "
                                    f"{MM_KZ} K slices)"),
                         "flops_per_launch": flops / nl, "avg_launch_us": prof["gemv_ms"] * 1e3 / nl}
         else:

@@ -111,7 +111,7 @@ inline int64_t pgrid_of(int32_t n) {
 }
 // shared-S MFMA S-pass: K is split over MM_KZ workgroup slices whose partial products land in
 // MM_KZ x 2 x batch x ld slabs, summed in slice order by the state kernel
-constexpr int MM_KZ = 8;
+constexpr int MM_KZ = 4;  // csrc/riptrm_kernels.hip k_spass_mm: 4 vs 8 slices measured
 
 // Symmetric-tile layout: tiles (I, J), I <= J, row by row; full TS x TS tiles except the last
 // tile column (J = nt - 1), which keeps only the wl = round_up(n - (nt - 1) TS, 32) columns that

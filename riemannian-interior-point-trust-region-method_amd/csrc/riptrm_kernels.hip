@@ -573,15 +573,19 @@ __global__ void __launch_bounds__(SP_THREADS, 1) k_spass_sup(DevParams P, int li
 // through the SOURCE address since the LDS side of the copy is lane-linear, so the fragment reads
 // below are bank-conflict free), double-buffered: step t+1's copy is in flight while the waves
 // run step t's MFMAs out of LDS, one barrier per step.  The waves form a rows x columns grid over
-// the tile (8 x 1 for 128-row tiles: 16 rows x all CT columns each) and read, for MFMA pair jj,
+// the tile (8 x 1 for 128-row tiles: 16 rows x all CT columns each; 4 x 2 for 64-row tiles, the
+// shape at n = 4000 where 4 K slices x 63 row blocks fill the chip) and read, for MFMA pair jj,
 // lane (r, q)'s 16 B at k = 8q + 2jj: MFMA m = 2 jj + {0,1} sums k in {m, 8+m, 16+m, 24+m} — the
 // same order for every kernel shape, so an instance's product does not depend on CT / RT or on
 // the other right-hand sides.  The next pair's fragments are read while the current pair's
 // MFMAs issue, and the SIMD's second wave covers one wave's LDS reads and barrier wait.  Partial
 // slabs of the MM_KZ slices are added in slice order by the state kernel (deterministic, no
 // atomics).  Linear block id -> slice = id % MM_KZ, so a slice (and the V columns it reads)
-// stays on one XCD.  tools/mfma_bench.hip at n = 4000, 128 right-hand sides: 72.5 us = 56.5
-// TFLOP/s (4 waves: 81.5 us; the register-fed tile this replaced: 115 us; issue-rate probe 70.8).
+// stays on one XCD.  4 slices rather than 8: the state kernel adds half the slabs (k_state 37.9 ->
+// 29.8 us per launch in the n = 4000 multi-start solve) at an equal S-pass time (82 us).
+// tools/mfma_bench.hip at n = 4000, 128 right-hand sides: 72.5 us = 56.5 TFLOP/s with 128-row
+// tiles and 8 slices (4 waves: 81.5 us; the register-fed tile this replaced: 115 us; issue-rate
+// probe 70.8).
 // ------------------------------------------------------------------------------------------
 typedef double dbl4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) unsigned char lds_u8;
