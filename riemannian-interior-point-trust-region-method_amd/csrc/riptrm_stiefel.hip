@@ -235,9 +235,10 @@ __global__ void __launch_bounds__(T) k_st_e2rh(int n, int p, int64_t stride, con
 // ---- retraction (CholeskyQR2): the round-1 kernel, kept as measured best ----------------------
 // Its own LDS layout: M and L (p x p, stride 16 ceil(p/16)) and the 8-wave Gram tree's partials.
 // Redesigns tried this round and measured slower at (200, 50) x 256 (tools/stiefel_stamps.hip
-// phase stamps): a single-wave register-resident Cholesky (33-56 µs per factor vs
-// ~40 here), a column-oriented row solve with data-dependent LDS reads, and a first Gram reading
-// X + U directly — 222-349 µs in total against this kernel's 191 µs.
+// phase stamps, profiles/r2_stiefel_phase_stamps.jsonl): single-wave Cholesky
+// variants, a column-oriented row solve with data-dependent LDS reads, a first Gram reading X + U
+// directly, and a 16-column-blocked factor + solve (MFMA off-diagonal blocks, 16-step row
+// chains; agrees with this kernel to 2.8e-16) — 222-349 µs in total against this kernel's 191 µs.
 constexpr int NBLK = 10;       // upper-triangular 16 x 16 blocks of a p x p matrix at p <= 64
 constexpr int GMAX = 8;        // 4-row groups per wave per streamed chunk (8 waves x 32 rows = 256 rows)
 struct SmemR {

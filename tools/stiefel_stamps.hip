@@ -8,6 +8,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <vector>
+#include <cmath>
 
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP %s line %d\n", hipGetErrorString(e), __LINE__); exit(1);} } while (0)
 
@@ -45,12 +46,12 @@ int main(int argc, char** argv) {
     CK(hipEventElapsedTime(&ms, a, b));
     std::vector<long long> s((size_t)B * 16);
     CK(hipMemcpy(s.data(), st, s.size() * 8, hipMemcpyDeviceToHost));
-    if (which) {   // the retraction kernel carries no stamps: event time only
+    if (which == 1) {   // the round-1 retraction kernel carries no stamps: event time only
       printf("{\"kernel\": \"k_st_retr_r\", \"n\": %d, \"p\": %d, \"B\": %d, \"event_us\": %.2f}\n", n, p, B, ms * 1e3);
       continue;
     }
     const int np = 2;
-    printf("{\"kernel\": \"%s\", \"n\": %d, \"p\": %d, \"B\": %d, \"event_us\": %.2f, \"phase_ticks_median\": [", which ? "k_st_retr" : "k_st_proj", n, p, B, ms * 1e3);
+    printf("{\"kernel\": \"%s\", \"n\": %d, \"p\": %d, \"B\": %d, \"event_us\": %.2f, \"phase_ticks_median\": [", "k_st_proj", n, p, B, ms * 1e3);
     for (int k = 0; k < np; ++k) {
       std::vector<long long> d(B);
       for (int g = 0; g < B; ++g) d[g] = s[g * 16 + k + 1] - s[g * 16 + k];
