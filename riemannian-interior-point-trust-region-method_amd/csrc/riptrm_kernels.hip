@@ -1638,20 +1638,19 @@ struct MachineT {
 
   template <int K>
   __device__ __forceinline__ int tcg_step_reg() {
-    // K <= 2 (n <= 1024): every operand loaded up front, one memory round trip (few registers);
-    // K = 8: c / e / he / rv loaded where first needed, so fewer vectors are live at once
+    // every operand loaded up front: one memory round trip per iteration instead of three (the
+    // ~150 VGPRs of K = 8 fit the 256 a wave has at two waves per SIMD; one workgroup per
+    // instance never fills the chip, so occupancy is not the limit)
     TcgVecs<K> v;
     double u[K];
     gather_reg<K>(u);
     load_reg<K>(V_IN0, v.d);
     load_reg<K>(V_X, v.x);
     load_reg<K>(V_Y, v.y);
-    if constexpr (K <= 2) {
-      load_reg<K>(V_C, v.c);
-      load_reg<K>(V_ETA, v.e);
-      load_reg<K>(V_HETA, v.he);
-      load_reg<K>(V_R, v.rv);
-    }
+    load_reg<K>(V_C, v.c);
+    load_reg<K>(V_ETA, v.e);
+    load_reg<K>(V_HETA, v.he);
+    load_reg<K>(V_R, v.rv);
     return tcg_reg_core<K, true>(v, u);
   }
 
@@ -1684,14 +1683,10 @@ struct MachineT {
     MachineT& M;
     TcgVecs<K>& v;
     __device__ __forceinline__ void late_ceh() {
-      if constexpr (MEM && K > 2) {
-        M.load_reg(V_C, v.c);
-        M.load_reg(V_ETA, v.e);
-        M.load_reg(V_HETA, v.he);
-      }
+      // (operands are loaded up front by tcg_step_reg)
     }
     __device__ __forceinline__ void late_r() {
-      if constexpr (MEM && K > 2) M.load_reg(V_R, v.rv);
+      // (operands are loaded up front by tcg_step_reg)
     }
     __device__ __forceinline__ void store_eh() {
       if constexpr (MEM) {
