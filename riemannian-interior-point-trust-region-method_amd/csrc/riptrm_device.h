@@ -161,7 +161,7 @@ inline Layout make_layout(int32_t n, int32_t batch, int32_t cap, int32_t layout)
   o = round_up(o, 256);
   L.off_lists = o; o += (int64_t)4 * batch * 4;                          o = round_up(o, 256);
   L.off_req = o;   o += (int64_t)batch * 4;                              o = round_up(o, 256);
-  L.off_cnt = o;   o += 16;                                              o = round_up(o, 256);
+  L.off_cnt = o;   o += 64;   // [0..3] list counts, [8..11] S-pass unit tickets, [12..15] done counts                                              o = round_up(o, 256);
   L.reps = persist_reps_of(n, batch, layout);
   const int64_t bs = L.reps > 0 ? (int64_t)batch * (L.reps - 1) : 0;   // replicas beyond the instance itself
   L.off_rvec = o;   o += (int64_t)NVEC * bs * L.ld * 8;                  o = round_up(o, 256);
@@ -193,6 +193,7 @@ struct DevParams {
   int32_t wl;           // stored columns of the last tile column (symmetric-tile layout)
   int32_t nst, nsup;    // super-blocks per dimension, super-tile units per instance
   int32_t smode;        // per launch: 0 = tile S-pass (grid [nt][nt][TS]), 1 = super-tile ([nst][nst][SW])
+  int32_t sup_dyn;      // k_spass_sup: 1 = units handed out by a ticket counter (cnt[8 + list]), 0 = static
   double* pbuf;         // S-pass partial sums: 2 x pbatch x pgrid_of(n) (symmetric-tile layout),
                         // MM_KZ x 2 x batch x ld (shared layout)
   int32_t pbatch;       // instances of the partial grid (= batch; the persistent replicas' parameter

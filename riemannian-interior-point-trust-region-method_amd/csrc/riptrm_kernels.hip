@@ -524,16 +524,34 @@ __device__ __forceinline__ void sup_flush(const DevParams& P, const double* outb
   __syncthreads();
 }
 
+// Unit order: static (u = g, g + G, ...) or, with P.sup_dyn, tickets from a per-list counter
+// (cnt[8 + list_in]): a workgroup takes its next unit when it finishes one, so CUs that also run
+// the other group's state kernel, and units of 3 vs 4 tiles or two right-hand sides, no longer
+// decide the launch's end.  The next ticket is fetched at the start of the current unit (its
+// latency overlaps the unit's first loads); the last workgroup to finish resets the counter for
+// the next launch.  Every unit writes its fixed slots, so results do not depend on the order.
 __global__ void __launch_bounds__(SP_THREADS, 1) k_spass_sup(DevParams P, int list_in, int zero_cnt) {
   static_assert(SP_THREADS == 2 * SW, "sup_flush: one thread per element of the two sides");
   __shared__ double red[2][SP_WAVES][SW];
   __shared__ double outb[SUP_OCAP];
   __shared__ int meta[SUP_MAXU][2];
+  __shared__ int tick_next;
   if (zero_cnt >= 0 && blockIdx.x == 0 && threadIdx.x == 0) P.cnt[zero_cnt] = 0;
   const int nact = P.cnt[list_in];
   const int total = nact * P.nsup;
   int used = 0, nslot = 0, rsel = 0;
-  for (int u = blockIdx.x; u < total; u += gridDim.x) {
+  const bool dyn = P.sup_dyn != 0;
+  unsigned int* tick = (unsigned int*)P.cnt + 8 + list_in;
+  unsigned int* done = (unsigned int*)P.cnt + 12 + list_in;
+  int u = blockIdx.x;
+  if (dyn) {
+    if (threadIdx.x == 0) tick_next = (int)atomicAdd(tick, 1u);
+    __syncthreads();
+    u = tick_next;
+  }
+  while (u < total) {
+    unsigned int pre = 0;
+    if (dyn && threadIdx.x == 0) pre = atomicAdd(tick, 1u);   // next unit, in flight during this one
     const int slot = u / P.nsup;
     const int32_t e = P.lists[list_in * P.batch + slot];
     const int b = le_b(e), nr = le_nrhs(e);
@@ -556,8 +574,23 @@ __global__ void __launch_bounds__(SP_THREADS, 1) k_spass_sup(DevParams P, int li
     }
     used += nr * 2 * SW;
     ++nslot;
+    if (dyn) {
+      __syncthreads();                 // every thread has read tick_next (and meta is ordered)
+      if (threadIdx.x == 0) tick_next = (int)pre;
+      __syncthreads();
+      u = tick_next;
+    } else {
+      u += gridDim.x;
+    }
   }
   if (nslot > 0) sup_flush(P, outb, meta, nslot, list_in);
+  if (dyn && threadIdx.x == 0) {
+    // every workgroup has drawn its last ticket before it counts itself done: the last one resets
+    if (atomicAdd(done, 1u) == gridDim.x - 1) {
+      atomicExch(tick, 0u);
+      atomicExch(done, 0u);
+    }
+  }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -3175,6 +3208,10 @@ int riptrm_nonnegpca_bind(riptrm_ctx* ctx, const double* S, int32_t n, int32_t b
   P.req = (int32_t*)(ctx->ws + L.off_req);
   P.cnt = (int32_t*)(ctx->ws + L.off_cnt);
   P.pbatch = batch;
+  {   // S-pass unit order (k_spass_sup): RIPTRM_SUP_DYNAMIC=0 / 1 overrides the default
+    const char* ev = getenv("RIPTRM_SUP_DYNAMIC");
+    P.sup_dyn = ev ? (atoi(ev) != 0) : 0;
+  }
   P.clock_hz = ctx->clock_hz;
   P.outer_target = INT32_MAX;
   // persistent mode: the workspace has the replica region and every workgroup fits on its own CU
