@@ -402,6 +402,240 @@ __global__ void __launch_bounds__(T) k_st_retr_r(int n, int p, int64_t stride, c
   }
 }
 
+// ---- retraction, round 2: the point resident in LDS ---------------------------------------------
+// The round-1 kernel above re-reads A from global memory in every phase and spends most of its time
+// in LDS-latency chains (a row solve that waits on one L read per FMA; a factor with an integer
+// division per element and two barriers per step).  This one keeps A = X + U (then Q1) in LDS for
+// the whole CholeskyQR2 and turns every O(n p^2) step into fp64 MFMA work:
+//   1. A -> LDS, row-major with stride S = 16 ceil(p/16), zero padded to NR = 16 ceil(n/16) rows,
+//      element (r, c) at r S + (c ^ (r & 15)) (XOR swizzle inside 16-column groups: the Gram reads a
+//      row's 16 consecutive columns per lane group, the product reads 16 rows of one column; both
+//      are bank-conflict free);
+//   2. G = A^T A: the upper 16 x 16 blocks (I <= J), each split over two k halves, the
+//      (block, half) tasks dealt to the 8 waves; halves meet once in a fixed order;
+//   3. E = L^-1 (G = L L^T) by symmetric Gauss-Jordan elimination on registers: thread (j = lane,
+//      rows 8 w .. 8 w + 7) holds G[i][j] and E[i][j]; per step k the lane-k threads publish G's
+//      column k and wave k / 8 publishes E's row k (double-buffered in LDS, ONE barrier per step),
+//      then every thread applies E_i -= (G_ik / G_kk) E_k, G_ij -= (G_ik / G_kk) G_jk (i > k) and
+//      scales E_k by G_kk^-1/2 — no division by a runtime size, no second barrier;
+//   4. Q = A R^-1 = A E^T on MFMA (E^T upper triangular: only the K <= J blocks), the wave's 16-row
+//      blocks in registers; Q1 overwrites A in LDS, the second pass writes Q to global memory.
+// diag(R) = diag(L^T) > 0 by construction: pymanopt's qf up to rounding, as the round-1 kernel.
+template <int P16>
+__host__ __device__ constexpr int r2_lds_doubles_nr(int NR) {
+  return NR * 16 * P16 + (16 * P16) * (16 * P16) + (P16 * (P16 + 1) / 2) * 256;
+}
+
+template <int P16>
+__device__ __forceinline__ void r2_block_ij(int b, int& I, int& J) {
+  int i = 0;
+#pragma unroll
+  for (int q = 0; q < P16; ++q)
+    if (b >= P16 - i) {
+      b -= P16 - i;
+      ++i;
+    }
+  I = i;
+  J = i + b;
+}
+
+template <int P16>
+__device__ __forceinline__ void r2_gram(lds_f64* As, lds_f64* Gm, lds_f64* red, int NR) {
+  constexpr int S = 16 * P16, NB = P16 * (P16 + 1) / 2, UB2 = 8;
+  const int t = threadIdx.x, l = t & 63, w = t >> 6, c = l & 15, kk = l >> 4;
+  const int NG = NR / 4, H0 = NG / 2;   // k groups of 4 rows; half 0 = [0, H0), half 1 = [H0, NG)
+  for (int task = w; task < 2 * NB; task += NW) {   // wave-uniform
+    const int b = task % NB, h = task / NB;
+    int I, J;
+    r2_block_ij<P16>(b, I, J);
+    const int g0 = h ? H0 : 0, g1 = h ? NG : H0;
+    dbl4 acc = dbl4{0.0, 0.0, 0.0, 0.0};
+    for (int g = g0; g < g1; g += UB2) {
+      double av[UB2], bv[UB2];
+#pragma unroll
+      for (int u = 0; u < UB2; ++u) {
+        const bool ok = g + u < g1;
+        const int r = 4 * (ok ? g + u : g1 - 1) + kk;
+        const lds_f64* row = As + r * S;
+        av[u] = row[(16 * I + c) ^ (r & 15)] * mask01(ok);
+        bv[u] = row[(16 * J + c) ^ (r & 15)];
+      }
+#pragma unroll
+      for (int u = 0; u < UB2; ++u) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av[u], bv[u], acc, 0, 0, 0);
+    }
+    lds_f64* dst = (h ? red : Gm) + b * 256;   // half 0 partials in Gm's space, half 1 in red
+#pragma unroll
+    for (int q = 0; q < 4; ++q) dst[q * 64 + l] = acc[q];
+  }
+  __syncthreads();
+  constexpr int PER = (NB * 256 + T - 1) / T;
+  double v[PER];
+#pragma unroll
+  for (int m = 0; m < PER; ++m) {
+    const int e = t + m * T;
+    v[m] = e < NB * 256 ? Gm[e] + red[e] : 0.0;   // fixed order: half 0 + half 1
+  }
+  __syncthreads();
+#pragma unroll
+  for (int m = 0; m < PER; ++m) {
+    const int e = t + m * T;
+    if (e < NB * 256) {
+      const int b = e >> 8, q = (e >> 6) & 3, ll = e & 63;
+      int I, J;
+      r2_block_ij<P16>(b, I, J);
+      const int i = 16 * I + (ll >> 4) + 4 * q, j = 16 * J + (ll & 15);   // f64 D: row (l >> 4) + 4 q, col l & 15
+      if (I < J || i <= j) {   // one writer per symmetric pair: G exactly symmetric
+        Gm[i * S + j] = v[m];
+        Gm[j * S + i] = v[m];
+      }
+    }
+  }
+  __syncthreads();
+}
+
+// Gm (G, stride S) -> Gm (W = R^-1 = E^T, stride S); xch: 4 S doubles of exchange space
+template <int P16>
+__device__ __forceinline__ void r2_factor_inverse(lds_f64* Gm, lds_f64* xch, int p) {
+  constexpr int S = 16 * P16;
+  const int t = threadIdx.x, l = t & 63, w = t >> 6;
+  double g[8], e[8];
+#pragma unroll
+  for (int r = 0; r < 8; ++r) {
+    const int i = 8 * w + r;
+    const bool ok = i < S && l < S;
+    g[r] = ok ? Gm[i * S + l] : 0.0;
+    e[r] = (i == l) ? 1.0 : 0.0;
+  }
+  for (int kb = 0; 8 * kb < p; ++kb) {
+#pragma unroll
+    for (int r0 = 0; r0 < 8; ++r0) {
+      const int k = 8 * kb + r0;
+      if (k >= p) break;   // uniform
+      lds_f64* cg = xch + (r0 & 1) * 2 * S;   // [G column k | E row k], alternating by step parity
+      lds_f64* re = cg + S;
+      if (l == k) {
+#pragma unroll
+        for (int r = 0; r < 8; ++r)
+          if (8 * w + r < S) cg[8 * w + r] = g[r];
+      }
+      if (w == kb && l < S) re[l] = e[r0];
+      __syncthreads();
+      const double d = cg[k];
+      const double inv = 1.0 / d;
+      const bool lok = l < S;
+      const double lj = cg[lok ? l : 0];   // G[j][k] (= G[k][j])
+      const double ek = re[lok ? l : 0];   // E[k][j]
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        const int i = 8 * w + r;
+        if (i > k && i < S) {   // wave-uniform
+          const double m = cg[i] * inv;
+          g[r] = g[r] - m * lj;
+          e[r] = e[r] - m * ek;
+        }
+      }
+      if (w == kb) e[r0] = ek * (1.0 / sqrt(d));
+    }
+  }
+  __syncthreads();   // every read of Gm (initial load) and of the exchange is done
+#pragma unroll
+  for (int r = 0; r < 8; ++r) {
+    const int i = 8 * w + r;
+    if (i < S && l < S) Gm[l * S + i] = e[r];   // W[j][i] = E[i][j]
+  }
+  __syncthreads();
+}
+
+// Q = A W (W upper triangular): wave w owns the 16-row blocks R = w, w + 8, ...; FINAL writes Q to
+// global memory, otherwise Q overwrites A in LDS (a wave writes only the rows it read)
+template <int P16, bool FINAL>
+__device__ __forceinline__ void r2_apply(lds_f64* As, const lds_f64* Wt, int NR, int n, int p, double* out) {
+  constexpr int S = 16 * P16;
+  const int l = threadIdx.x & 63, w = threadIdx.x >> 6, c = l & 15, kk = l >> 4;
+  double wf[P16][P16][4];
+#pragma unroll
+  for (int K = 0; K < P16; ++K)
+#pragma unroll
+    for (int J = K; J < P16; ++J)
+#pragma unroll
+      for (int s = 0; s < 4; ++s) wf[K][J][s] = Wt[(16 * K + 4 * s + kk) * S + 16 * J + c];
+  for (int R = w; R < NR / 16; R += NW) {
+    double af[P16][4];
+    const int row = 16 * R + c;
+#pragma unroll
+    for (int K = 0; K < P16; ++K)
+#pragma unroll
+      for (int s = 0; s < 4; ++s) af[K][s] = As[row * S + ((16 * K + 4 * s + kk) ^ c)];
+    dbl4 acc[P16];
+#pragma unroll
+    for (int J = 0; J < P16; ++J) {
+      acc[J] = dbl4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int K = 0; K <= J; ++K)
+#pragma unroll
+        for (int s = 0; s < 4; ++s) acc[J] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[K][s], wf[K][J][s], acc[J], 0, 0, 0);
+    }
+#pragma unroll
+    for (int J = 0; J < P16; ++J)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int r = 16 * R + kk + 4 * q, col = 16 * J + c;
+        if (FINAL) {
+          if (r < n && col < p) out[(int64_t)r * p + col] = acc[J][q];
+        } else {
+          As[r * S + (col ^ (r & 15))] = acc[J][q];
+        }
+      }
+  }
+  __syncthreads();
+}
+
+template <int P16>
+__global__ void __launch_bounds__(T) k_st_retr2(int n, int p, int64_t stride, const double* __restrict__ X,
+                                                const double* __restrict__ U, double* __restrict__ out) {
+  constexpr int S = 16 * P16, UL = 8;
+  extern __shared__ double lds[];
+  const int NR = (n + 15) & ~15;
+  lds_f64* As = (lds_f64*)lds;
+  lds_f64* Gm = As + NR * S;
+  lds_f64* red = Gm + S * S;
+  const int t = threadIdx.x;
+  const int64_t o = (int64_t)blockIdx.x * stride;
+  ST_STAMP(0);
+  const int tot = NR * S;
+  for (int e0 = 0; e0 < tot; e0 += T * UL) {
+    double v[UL];
+#pragma unroll
+    for (int u = 0; u < UL; ++u) {
+      const int e = e0 + u * T + t;
+      const int r = e / S, col = e - (e / S) * S;
+      const bool ok = r < n && col < p;
+      const int64_t gi = o + (ok ? (int64_t)r * p + col : 0);
+      v[u] = (X[gi] + U[gi]) * mask01(ok);
+    }
+#pragma unroll
+    for (int u = 0; u < UL; ++u) {
+      const int e = e0 + u * T + t;
+      const int r = e / S, col = e - (e / S) * S;
+      if (e < tot) As[r * S + (col ^ (r & 15))] = v[u];
+    }
+  }
+  __syncthreads();
+  ST_STAMP(1);
+  r2_gram<P16>(As, Gm, red, NR);
+  ST_STAMP(2);
+  r2_factor_inverse<P16>(Gm, red, p);
+  ST_STAMP(3);
+  r2_apply<P16, false>(As, Gm, NR, n, p, out + o);
+  ST_STAMP(4);
+  r2_gram<P16>(As, Gm, red, NR);
+  ST_STAMP(5);
+  r2_factor_inverse<P16>(Gm, red, p);
+  ST_STAMP(6);
+  r2_apply<P16, true>(As, Gm, NR, n, p, out + o);
+  ST_STAMP(7);
+}
+
 __global__ void __launch_bounds__(T) k_st_inner(int n, int p, int64_t stride, const double* U, const double* V, double* out) {
   __shared__ double red[T / 64];
   const int64_t o = (int64_t)blockIdx.x * stride;
@@ -421,6 +655,8 @@ __global__ void __launch_bounds__(T) k_st_inner(int n, int p, int64_t stride, co
 
 using namespace riptrm_stiefel;
 
+constexpr int R2_LDS_MAX = 160 * 1024;   // LDS per workgroup on gfx950
+
 static int st_check(riptrm_ctx* c, int32_t n, int32_t p, int32_t batch, int64_t stride) {
   if (n < 1 || p < 1 || p > PMAX || p > n || batch < 1 || stride < (int64_t)n * p)
     return fail(c, RIPTRM_E_ARG, "stiefel: need 1 <= p <= min(n, 64), batch >= 1, stride >= n*p");
@@ -434,12 +670,35 @@ static int st_check(riptrm_ctx* c, int32_t n, int32_t p, int32_t batch, int64_t 
     for (const void* f : fns) HIPCHK(c, hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, shm));
     HIPCHK(c, hipFuncSetAttribute((const void*)k_st_retr_r, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   (int)(LDS_DOUBLES_R * sizeof(double))));
+    const void* fr[] = {(const void*)k_st_retr2<1>, (const void*)k_st_retr2<2>, (const void*)k_st_retr2<3>,
+                        (const void*)k_st_retr2<4>};
+    for (const void* f : fr) HIPCHK(c, hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, R2_LDS_MAX));
     if (c->device >= 0 && c->device < 64) attr[c->device] = true;
   }
   return RIPTRM_OK;
 }
 
 constexpr size_t SHM = LDS_DOUBLES * sizeof(double);
+
+// LDS bytes of k_st_retr2 at (n, p), 0 if the point does not fit (the round-1 kernel runs then)
+static size_t retr2_lds_bytes(int n, int p) {
+  const int NR = ((n + 15) / 16) * 16;
+  int d = 0;
+  switch ((p + 15) / 16) {
+    case 1: d = r2_lds_doubles_nr<1>(NR); break;
+    case 2: d = r2_lds_doubles_nr<2>(NR); break;
+    case 3: d = r2_lds_doubles_nr<3>(NR); break;
+    default: d = r2_lds_doubles_nr<4>(NR); break;
+  }
+  const size_t b = (size_t)d * sizeof(double);
+  return b <= (size_t)R2_LDS_MAX ? b : 0;
+}
+
+// RIPTRM_STIEFEL_RETR=r1 forces the round-1 retraction kernel (A/B measurements)
+static bool retr_force_r1() {
+  const char* e = getenv("RIPTRM_STIEFEL_RETR");
+  return e && e[0] == 'r' && e[1] == '1';
+}
 constexpr size_t SHM_R = LDS_DOUBLES_R * sizeof(double);
 
 // kernels are specialised on ceil(p / 16) (the 16-column blocks), so no operand load sits behind
@@ -483,7 +742,12 @@ int riptrm_stiefel_retr(riptrm_ctx* ctx, int32_t n, int32_t p, int32_t batch, in
   if (!X || !U || !out) return fail(ctx, RIPTRM_E_ARG, "stiefel_retr: null pointer");
   int rc = st_check(ctx, n, p, batch, stride);
   if (rc) return rc;
-  hipLaunchKernelGGL(k_st_retr_r, dim3(batch), dim3(T), SHM_R, ctx->stream, n, p, stride, X, U, out);
+  const size_t shm2 = retr_force_r1() ? 0 : retr2_lds_bytes(n, p);
+  if (shm2) {
+    ST_LAUNCH(k_st_retr2, p, dim3(batch), dim3(T), shm2, ctx->stream, n, p, stride, X, U, out);
+  } else {
+    hipLaunchKernelGGL(k_st_retr_r, dim3(batch), dim3(T), SHM_R, ctx->stream, n, p, stride, X, U, out);
+  }
   HIPCHK(ctx, hipGetLastError());
   return RIPTRM_OK;
 }

@@ -24,7 +24,8 @@ def _t(a):
     return torch.as_tensor(np.ascontiguousarray(a), device="cuda")
 
 
-@pytest.mark.parametrize("n,p,B", [(5, 1, 3), (37, 7, 5), (200, 50, 16), (257, 64, 3), (64, 64, 2)])
+@pytest.mark.parametrize("n,p,B", [(5, 1, 3), (37, 7, 5), (200, 50, 16), (257, 64, 3), (64, 64, 2),
+                                     (3, 3, 2), (208, 64, 4), (300, 40, 4), (700, 20, 2)])
 def test_stiefel_ops_match_oracle(n, p, B):
     from stiefel import StiefelBatch
     M, X, U, W = _data(n, p, B, seed=n)
@@ -44,6 +45,22 @@ def test_stiefel_ops_match_oracle(n, p, B):
         ref = M.euclidean_to_riemannian_hessian(X[b], G[b], H[b], U[b])
         assert np.linalg.norm(E[b] - ref) <= 1e-12 * np.linalg.norm(ref)
         assert abs(ip[b] - M.inner_product(X[b], U[b], W[b])) <= 1e-12 * max(1.0, abs(ip[b]))
+
+
+@pytest.mark.parametrize("n,p", [(200, 50), (37, 7), (208, 64)])
+def test_stiefel_retraction_kernels_agree(n, p, monkeypatch):
+    """k_st_retr2 (point resident in LDS, Gauss-Jordan inverse factor) against the round-1
+    CholeskyQR2 kernel (RIPTRM_STIEFEL_RETR=r1): the same qf to rounding."""
+    from stiefel import StiefelBatch
+    M, X, U, _ = _data(n, p, 8, seed=3)
+    st = StiefelBatch(n, p)
+    Xt, Ut = _t(X), _t(0.5 * U)
+    R2 = st.retraction(Xt, Ut).cpu().numpy()
+    monkeypatch.setenv("RIPTRM_STIEFEL_RETR", "r1")
+    R1 = st.retraction(Xt, Ut).cpu().numpy()
+    assert np.abs(R2 - R1).max() <= 1e-13
+    for b in range(8):
+        assert np.abs(R2[b].T @ R2[b] - np.eye(p)).max() <= 1e-13
 
 
 def test_stiefel_rejects_bad_shapes():

@@ -1,6 +1,6 @@
 // stiefel_stamps.hip — phase timing of the Stiefel kernels (diagnostic build, s_memtime stamps).
 // hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -I<pkg>/csrc -I include tools/stiefel_stamps.hip
-// Runs k_st_proj / k_st_retr_r at (n, p, batch) on random data and prints, per phase, the median
+// Runs k_st_proj / k_st_retr_r / k_st_retr2 at (n, p, batch) on random data and prints, per phase, the median
 // over workgroups of the stamp deltas (s_memtime ticks) and the kernel's event time.
 #define ST_STAMPS 1
 #include "riptrm_stiefel.hip"
@@ -31,14 +31,17 @@ int main(int argc, char** argv) {
   const int shm = LDS_DOUBLES * 8;
   CK(hipFuncSetAttribute((const void*)k_st_proj<4>, hipFuncAttributeMaxDynamicSharedMemorySize, shm));
   CK(hipFuncSetAttribute((const void*)k_st_retr_r, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_DOUBLES_R * 8));
+  const int shm2 = r2_lds_doubles_nr<4>((n + 15) / 16 * 16) * 8;
+  CK(hipFuncSetAttribute((const void*)k_st_retr2<4>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
   hipEvent_t a, b;
   CK(hipEventCreate(&a));
   CK(hipEventCreate(&b));
-  for (int which = 0; which < 2; ++which) {
+  for (int which = 0; which < 3; ++which) {
     for (int r = 0; r < 20; ++r) {
       CK(hipEventRecord(a, 0));
       if (which == 0) hipLaunchKernelGGL(k_st_proj<4>, dim3(B), dim3(T), shm, 0, n, p, (int64_t)n * p, X, U, O);
-      else hipLaunchKernelGGL(k_st_retr_r, dim3(B), dim3(T), LDS_DOUBLES_R * 8, 0, n, p, (int64_t)n * p, X, U, O);
+      else if (which == 1) hipLaunchKernelGGL(k_st_retr_r, dim3(B), dim3(T), LDS_DOUBLES_R * 8, 0, n, p, (int64_t)n * p, X, U, O);
+      else hipLaunchKernelGGL(k_st_retr2<4>, dim3(B), dim3(T), shm2, 0, n, p, (int64_t)n * p, X, U, O);
       CK(hipEventRecord(b, 0));
       CK(hipEventSynchronize(b));
     }
@@ -50,8 +53,9 @@ int main(int argc, char** argv) {
       printf("{\"kernel\": \"k_st_retr_r\", \"n\": %d, \"p\": %d, \"B\": %d, \"event_us\": %.2f}\n", n, p, B, ms * 1e3);
       continue;
     }
-    const int np = 2;
-    printf("{\"kernel\": \"%s\", \"n\": %d, \"p\": %d, \"B\": %d, \"event_us\": %.2f, \"phase_ticks_median\": [", "k_st_proj", n, p, B, ms * 1e3);
+    const int np = which == 0 ? 2 : 7;
+    printf("{\"kernel\": \"%s\", \"n\": %d, \"p\": %d, \"B\": %d, \"event_us\": %.2f, \"phase_ticks_median\": [",
+           which == 0 ? "k_st_proj" : "k_st_retr2 (load, gram1, factor1, apply1, gram2, factor2, apply2)", n, p, B, ms * 1e3);
     for (int k = 0; k < np; ++k) {
       std::vector<long long> d(B);
       for (int g = 0; g < B; ++g) d[g] = s[g * 16 + k + 1] - s[g * 16 + k];
