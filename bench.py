@@ -490,6 +490,27 @@ def bench_stiefel(args, world, rank, dev, dist):
     tfs = 4.0 * n * p * p * B / tp / 1e12
     hbm_floor = 3.0 * n * p * 8 * B / (HBM_PEAK_GBS * 1e9)
     mfma_floor = 4.0 * n * p * p * B / (MFMA_F64_PEAK_TFS * 1e12)
+    # k_st_retr2 (point resident in LDS) when (n, p) fits 160 KiB, else the round-1 kernel
+    nr, s16 = -(-n // 16) * 16, 16 * (-(-p // 16))
+    fits = (nr * s16 + s16 * s16 + (s16 // 16) * (s16 // 16 + 1) // 2 * 256) * 8 <= 160 * 1024
+    retr_kernel = ("k_st_retr2" if fits and os.environ.get("RIPTRM_STIEFEL_RETR", "") != "r1" else "k_st_retr_r")
+    # CPU baseline: the pymanopt restatement (oracle/stiefel_oracle.py, NumPy) on the host, over the
+    # same points until ~2 s have passed (a bounded sample; BLAS threads as configured)
+    from oracle.stiefel_oracle import Stiefel as _CpuStiefel
+    M = _CpuStiefel(n, p)
+    Xh, Wh, Uh = X.cpu().numpy(), W.cpu().numpy(), U.cpu().numpy()
+    rates = {}
+    for name, fn in (("projection", lambda b: M.projection(Xh[b], Wh[b])),
+                     ("retraction", lambda b: M.retraction(Xh[b], Uh[b]))):
+        cnt, t0 = 0, time.perf_counter()
+        while time.perf_counter() - t0 < 2.0:
+            fn(cnt % B)
+            cnt += 1
+        rates[name] = cnt / (time.perf_counter() - t0)
+    cpu = {"value": rates["projection"], "unit": "projections/s", "cores": int(os.environ.get("OMP_NUM_THREADS", "1")),
+           "kind": "port", "sample": f"oracle/stiefel_oracle.py (NumPy) projection of the first points of the batch, "
+                                     f"{n}x{p}, repeated for 2 s on the host"}
+    cpu_retr = rates["retraction"]
     print(json.dumps({
         "metric": f"Stiefel({n},{p}) projections/sec, batch {B}/GPU",
         "value": B * world / tp, "unit": "projections/s", "n_gpus": world, "steps": args.steps,
@@ -507,10 +528,14 @@ def bench_stiefel(args, world, rank, dev, dist):
                      "hbm_floor_us": hbm_floor * 1e6, "mfma_floor_us": mfma_floor * 1e6,
                      "mfma_achieved_tflops": tfs,
                      "traffic": None, "kernel": "k_st_proj (U - X sym(X^T U), one workgroup per point)"},
-        "cpu_baseline": None,
+        "cpu_baseline": cpu,
         "detail": {"retractions_per_s": B * world / tr, "retraction_ms": tr * 1e3,
-                   "retraction_note": "CholeskyQR2 (k_st_retr_r), latency-bound: p Cholesky steps and a p^2/2-long "
-                                      "forward substitution per row, one point per CU"},
+                   "retraction_roofline": {"bound": "hbm", "achieved": 3.0 * n * p * 8 * B / tr / 1e9,
+                                           "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": hbm_floor / tr,
+                                           "kernel": retr_kernel},
+                   "retraction_cpu_per_s": cpu_retr,
+                   "retraction_note": "CholeskyQR2, latency-bound: two p-step factorisations per point, one point "
+                                      "per CU"},
     }), flush=True)
 
 

@@ -416,8 +416,8 @@ __global__ void __launch_bounds__(T) k_st_retr_r(int n, int p, int64_t stride, c
 //   3. E = L^-1 (G = L L^T) by symmetric Gauss-Jordan elimination on registers: thread (j = lane,
 //      rows 8 w .. 8 w + 7) holds G[i][j] and E[i][j]; per step k the lane-k threads publish G's
 //      column k and wave k / 8 publishes E's row k (double-buffered in LDS, ONE barrier per step),
-//      then every thread applies E_i -= (G_ik / G_kk) E_k, G_ij -= (G_ik / G_kk) G_jk (i > k) and
-//      scales E_k by G_kk^-1/2 — no division by a runtime size, no second barrier;
+//      then every thread applies E_i -= (G_ik / G_kk) E_k, G_ij -= (G_ik / G_kk) G_jk (i > k); row k
+//      is scaled by G_kk^-1/2 after the loop — no division by a runtime size, no second barrier;
 //   4. Q = A R^-1 = A E^T on MFMA (E^T upper triangular: only the K <= J blocks), the wave's 16-row
 //      blocks in registers; Q1 overwrites A in LDS, the second pass writes Q to global memory.
 // diag(R) = diag(L^T) > 0 by construction: pymanopt's qf up to rounding, as the round-1 kernel.
@@ -441,7 +441,7 @@ __device__ __forceinline__ void r2_block_ij(int b, int& I, int& J) {
 
 template <int P16>
 __device__ __forceinline__ void r2_gram(lds_f64* As, lds_f64* Gm, lds_f64* red, int NR) {
-  constexpr int S = 16 * P16, NB = P16 * (P16 + 1) / 2, UB2 = 8;
+  constexpr int S = 16 * P16, NB = P16 * (P16 + 1) / 2, UB2 = 14;
   const int t = threadIdx.x, l = t & 63, w = t >> 6, c = l & 15, kk = l >> 4;
   const int NG = NR / 4, H0 = NG / 2;   // k groups of 4 rows; half 0 = [0, H0), half 1 = [H0, NG)
   for (int task = w; task < 2 * NB; task += NW) {   // wave-uniform
@@ -449,7 +449,7 @@ __device__ __forceinline__ void r2_gram(lds_f64* As, lds_f64* Gm, lds_f64* red, 
     int I, J;
     r2_block_ij<P16>(b, I, J);
     const int g0 = h ? H0 : 0, g1 = h ? NG : H0;
-    dbl4 acc = dbl4{0.0, 0.0, 0.0, 0.0};
+    dbl4 acc2[2] = {dbl4{0.0, 0.0, 0.0, 0.0}, dbl4{0.0, 0.0, 0.0, 0.0}};   // two chains: MFMAs of a batch overlap
     for (int g = g0; g < g1; g += UB2) {
       double av[UB2], bv[UB2];
 #pragma unroll
@@ -460,9 +460,12 @@ __device__ __forceinline__ void r2_gram(lds_f64* As, lds_f64* Gm, lds_f64* red, 
         av[u] = row[(16 * I + c) ^ (r & 15)] * mask01(ok);
         bv[u] = row[(16 * J + c) ^ (r & 15)];
       }
+      __builtin_amdgcn_sched_barrier(0);   // the batch's reads issue together
 #pragma unroll
-      for (int u = 0; u < UB2; ++u) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av[u], bv[u], acc, 0, 0, 0);
+      for (int u = 0; u < UB2; ++u)
+        acc2[u & 1] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[u], bv[u], acc2[u & 1], 0, 0, 0);
     }
+    const dbl4 acc = acc2[0] + acc2[1];
     lds_f64* dst = (h ? red : Gm) + b * 256;   // half 0 partials in Gm's space, half 1 in red
 #pragma unroll
     for (int q = 0; q < 4; ++q) dst[q * 64 + l] = acc[q];
@@ -498,45 +501,81 @@ template <int P16>
 __device__ __forceinline__ void r2_factor_inverse(lds_f64* Gm, lds_f64* xch, int p) {
   constexpr int S = 16 * P16;
   const int t = threadIdx.x, l = t & 63, w = t >> 6;
-  double g[8], e[8];
+  double g[8], e[8], piv[8];
 #pragma unroll
   for (int r = 0; r < 8; ++r) {
     const int i = 8 * w + r;
     const bool ok = i < S && l < S;
     g[r] = ok ? Gm[i * S + l] : 0.0;
     e[r] = (i == l) ? 1.0 : 0.0;
+    piv[r] = 1.0;   // rows past p keep E's identity rows
   }
+  // two columns per step (k, k + 1): half the barriers.  The first elimination changes column k + 1
+  // to G'_ik1 = G_ik1 - G_ik b / d0 (b = G_k1k, d0 = G_kk), pivot d1' = d1 - b^2 / d0 = det / d0;
+  // m0_i = G_ik / d0, m1_i = G'_ik1 / d1' = (d0 G_ik1 - b G_ik) / det, two independent divisions.
   for (int kb = 0; 8 * kb < p; ++kb) {
 #pragma unroll
-    for (int r0 = 0; r0 < 8; ++r0) {
-      const int k = 8 * kb + r0;
+    for (int r0 = 0; r0 < 8; r0 += 2) {
+      const int k = 8 * kb + r0, k1 = k + 1;
       if (k >= p) break;   // uniform
-      lds_f64* cg = xch + (r0 & 1) * 2 * S;   // [G column k | E row k], alternating by step parity
-      lds_f64* re = cg + S;
-      if (l == k) {
+      const bool two = k1 < p;
+      lds_f64* cg0 = xch + ((r0 >> 1) & 1) * 4 * S;   // [G col k | G col k+1 | E row k | E row k+1], 2 buffers
+      lds_f64* cg1 = cg0 + S;
+      lds_f64* re0 = cg0 + 2 * S;
+      lds_f64* re1 = cg0 + 3 * S;
+      if (l == k || (two && l == k1)) {
+        lds_f64* dst = l == k ? cg0 : cg1;
 #pragma unroll
         for (int r = 0; r < 8; ++r)
-          if (8 * w + r < S) cg[8 * w + r] = g[r];
+          if (8 * w + r < S) dst[8 * w + r] = g[r];
       }
-      if (w == kb && l < S) re[l] = e[r0];
+      if (w == kb && l < S) {
+        re0[l] = e[r0];
+        re1[l] = e[r0 + 1];
+      }
       __syncthreads();
-      const double d = cg[k];
-      const double inv = 1.0 / d;
+      // every operand of the step read at once (a load under the row guard would get its own wait:
+      // one LDS round trip per row); rows past S read neighbouring exchange slots, masked out
       const bool lok = l < S;
-      const double lj = cg[lok ? l : 0];   // G[j][k] (= G[k][j])
-      const double ek = re[lok ? l : 0];   // E[k][j]
+      const int jl = lok ? l : 0;
+      const double d0 = cg0[k];
+      const double bb = two ? cg0[k1] : 0.0;
+      const double d1 = two ? cg1[k1] : 1.0;
+      const double lj0 = cg0[jl], lj1 = cg1[jl];   // G[j][k], G[j][k+1]
+      const double ek0 = re0[jl], ek1 = re1[jl];   // E[k][j], E[k+1][j]
+      double ci0[8], ci1[8];
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        ci0[r] = cg0[8 * w + r];
+        ci1[r] = cg1[8 * w + r];
+      }
+      const double inv0 = 1.0 / d0;
+      const double det = d0 * d1 - bb * bb;
+      const double invdet = 1.0 / det;
+      const double t0 = bb * inv0;
+      const double lj1p = lj1 - lj0 * t0;   // G'[j][k+1]
+      const double ek1p = ek1 - t0 * ek0;   // E'[k+1][j] (row k+1 after the first elimination)
+      const double two01 = mask01(two);
 #pragma unroll
       for (int r = 0; r < 8; ++r) {
         const int i = 8 * w + r;
-        if (i > k && i < S) {   // wave-uniform
-          const double m = cg[i] * inv;
-          g[r] = g[r] - m * lj;
-          e[r] = e[r] - m * ek;
+        const double ok = mask01(i > k1 && i < S);   // 0 leaves the row bitwise unchanged
+        const double m0 = ci0[r] * inv0 * ok;
+        const double m1 = (d0 * ci1[r] - bb * ci0[r]) * invdet * ok * two01;
+        g[r] = g[r] - m0 * lj0 - m1 * lj1p;
+        e[r] = e[r] - m0 * ek0 - m1 * ek1p;
+      }
+      if (w == kb) {   // rows k, k + 1 are final up to their scales (applied after the loop)
+        piv[r0] = d0;
+        if (two) {
+          e[r0 + 1] = ek1p;
+          piv[r0 + 1] = det * inv0;
         }
       }
-      if (w == kb) e[r0] = ek * (1.0 / sqrt(d));
     }
   }
+#pragma unroll
+  for (int r = 0; r < 8; ++r) e[r] = e[r] * (1.0 / sqrt(piv[r]));
   __syncthreads();   // every read of Gm (initial load) and of the exchange is done
 #pragma unroll
   for (int r = 0; r < 8; ++r) {
@@ -592,7 +631,7 @@ __device__ __forceinline__ void r2_apply(lds_f64* As, const lds_f64* Wt, int NR,
 
 template <int P16>
 __global__ void __launch_bounds__(T) k_st_retr2(int n, int p, int64_t stride, const double* __restrict__ X,
-                                                const double* __restrict__ U, double* __restrict__ out) {
+                                                const double* __restrict__ U, double* out) {   // out may alias X or U (all reads precede the first write)
   constexpr int S = 16 * P16, UL = 8;
   extern __shared__ double lds[];
   const int NR = (n + 15) & ~15;

@@ -33,6 +33,7 @@ int main(int argc, char** argv) {
   CK(hipFuncSetAttribute((const void*)k_st_retr_r, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_DOUBLES_R * 8));
   const int shm2 = r2_lds_doubles_nr<4>((n + 15) / 16 * 16) * 8;
   CK(hipFuncSetAttribute((const void*)k_st_retr2<4>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+
   hipEvent_t a, b;
   CK(hipEventCreate(&a));
   CK(hipEventCreate(&b));
@@ -53,7 +54,7 @@ int main(int argc, char** argv) {
       printf("{\"kernel\": \"k_st_retr_r\", \"n\": %d, \"p\": %d, \"B\": %d, \"event_us\": %.2f}\n", n, p, B, ms * 1e3);
       continue;
     }
-    const int np = which == 0 ? 2 : 7;
+    const int np = which == 2 ? 7 : 2;
     printf("{\"kernel\": \"%s\", \"n\": %d, \"p\": %d, \"B\": %d, \"event_us\": %.2f, \"phase_ticks_median\": [",
            which == 0 ? "k_st_proj" : "k_st_retr2 (load, gram1, factor1, apply1, gram2, factor2, apply2)", n, p, B, ms * 1e3);
     for (int k = 0; k < np; ++k) {
