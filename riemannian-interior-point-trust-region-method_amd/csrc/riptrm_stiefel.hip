@@ -496,7 +496,16 @@ __device__ __forceinline__ void r2_gram(lds_f64* As, lds_f64* Gm, lds_f64* red, 
   __syncthreads();
 }
 
-// Gm (G, stride S) -> Gm (W = R^-1 = E^T, stride S); xch: 4 S doubles of exchange space
+// Gm (G, stride S) -> Gm (W = R^-1 = E^T, stride S); xch: 4 FB S doubles of exchange space (the Gram's
+// partial-sum area, NB * 256 >= 16 S doubles)
+// columns eliminated per barrier step of r2_factor_inverse (tools/stiefel_stamps.hip builds 1 / 2 / 4 for A/B)
+#ifndef RIPTRM_ST_FB
+#define RIPTRM_ST_FB 2   // measured: 1 -> 75.7k, 2 -> 69.3k, 4 -> 77.6k ticks per factor at p = 50
+#endif
+constexpr int FB = RIPTRM_ST_FB;
+
+static_assert(FB <= 4 && 8 % FB == 0, "the exchange alternates 2 buffers within a group of 8 rows");
+
 template <int P16>
 __device__ __forceinline__ void r2_factor_inverse(lds_f64* Gm, lds_f64* xch, int p) {
   constexpr int S = 16 * P16;
@@ -510,67 +519,90 @@ __device__ __forceinline__ void r2_factor_inverse(lds_f64* Gm, lds_f64* xch, int
     e[r] = (i == l) ? 1.0 : 0.0;
     piv[r] = 1.0;   // rows past p keep E's identity rows
   }
-  // two columns per step (k, k + 1): half the barriers.  The first elimination changes column k + 1
-  // to G'_ik1 = G_ik1 - G_ik b / d0 (b = G_k1k, d0 = G_kk), pivot d1' = d1 - b^2 / d0 = det / d0;
-  // m0_i = G_ik / d0, m1_i = G'_ik1 / d1' = (d0 G_ik1 - b G_ik) / det, two independent divisions.
+  // FB columns per step (block elimination): the FB x FB pivot block P = G[K][K] is factored
+  // P = L D L^T by every thread (unit lower L, redundant, in registers); with C' = C L^-T (the pivot
+  // columns) and E'_K = L^-1 E_K (the pivot rows) the step is G_ij -= sum_c C'_ic C'_jc / D_c,
+  // E_i -= sum_c (C'_ic / D_c) E'_Kc for the rows after the block; E'_K and D are the block's final
+  // (unscaled) E rows and pivots.  FB = 1 is the plain Gauss-Jordan step; FB columns cost one barrier.
   for (int kb = 0; 8 * kb < p; ++kb) {
 #pragma unroll
-    for (int r0 = 0; r0 < 8; r0 += 2) {
-      const int k = 8 * kb + r0, k1 = k + 1;
+    for (int r0 = 0; r0 < 8; r0 += FB) {
+      const int k = 8 * kb + r0;
       if (k >= p) break;   // uniform
-      const bool two = k1 < p;
-      lds_f64* cg0 = xch + ((r0 >> 1) & 1) * 4 * S;   // [G col k | G col k+1 | E row k | E row k+1], 2 buffers
-      lds_f64* cg1 = cg0 + S;
-      lds_f64* re0 = cg0 + 2 * S;
-      lds_f64* re1 = cg0 + 3 * S;
-      if (l == k || (two && l == k1)) {
-        lds_f64* dst = l == k ? cg0 : cg1;
+      const int nb = p - k < FB ? p - k : FB;   // valid columns of this block
+      lds_f64* cgs = xch + ((r0 / FB) & 1) * 2 * FB * S;   // [G cols k..k+FB-1 | E rows k..k+FB-1], 2 buffers
+      lds_f64* res = cgs + FB * S;
+      if (l >= k && l < k + nb) {
+        lds_f64* dst = cgs + (l - k) * S;
 #pragma unroll
         for (int r = 0; r < 8; ++r)
           if (8 * w + r < S) dst[8 * w + r] = g[r];
       }
       if (w == kb && l < S) {
-        re0[l] = e[r0];
-        re1[l] = e[r0 + 1];
+#pragma unroll
+        for (int a = 0; a < FB; ++a) res[a * S + l] = e[r0 + a];
       }
       __syncthreads();
       // every operand of the step read at once (a load under the row guard would get its own wait:
-      // one LDS round trip per row); rows past S read neighbouring exchange slots, masked out
-      const bool lok = l < S;
-      const int jl = lok ? l : 0;
-      const double d0 = cg0[k];
-      const double bb = two ? cg0[k1] : 0.0;
-      const double d1 = two ? cg1[k1] : 1.0;
-      const double lj0 = cg0[jl], lj1 = cg1[jl];   // G[j][k], G[j][k+1]
-      const double ek0 = re0[jl], ek1 = re1[jl];   // E[k][j], E[k+1][j]
-      double ci0[8], ci1[8];
+      // one LDS round trip per row); slots past S or past nb hold finite stale values, masked out
+      const int jl = l < S ? l : 0;
+      double P[FB][FB], colj[FB], ekr[FB], ci[FB][8];
 #pragma unroll
-      for (int r = 0; r < 8; ++r) {
-        ci0[r] = cg0[8 * w + r];
-        ci1[r] = cg1[8 * w + r];
+      for (int c = 0; c < FB; ++c) {
+#pragma unroll
+        for (int a = 0; a < FB; ++a) P[a][c] = cgs[c * S + k + a];
+        colj[c] = cgs[c * S + jl];
+        ekr[c] = res[c * S + jl];
+#pragma unroll
+        for (int r = 0; r < 8; ++r) ci[c][r] = cgs[c * S + 8 * w + r];
       }
-      const double inv0 = 1.0 / d0;
-      const double det = d0 * d1 - bb * bb;
-      const double invdet = 1.0 / det;
-      const double t0 = bb * inv0;
-      const double lj1p = lj1 - lj0 * t0;   // G'[j][k+1]
-      const double ek1p = ek1 - t0 * ek0;   // E'[k+1][j] (row k+1 after the first elimination)
-      const double two01 = mask01(two);
+      double Lf[FB][FB], D[FB], invD[FB];
+#pragma unroll
+      for (int c = 0; c < FB; ++c) {
+        const bool cv = c < nb;
+        double dc = P[c][c];
+#pragma unroll
+        for (int t = 0; t < c; ++t) dc = dc - Lf[c][t] * Lf[c][t] * D[t];
+        D[c] = cv ? dc : 1.0;
+        invD[c] = 1.0 / D[c];
+#pragma unroll
+        for (int a = c + 1; a < FB; ++a) {
+          double v = P[a][c];
+#pragma unroll
+          for (int t = 0; t < c; ++t) v = v - Lf[a][t] * Lf[c][t] * D[t];
+          Lf[a][c] = (cv && a < nb) ? v * invD[c] : 0.0;
+        }
+      }
+#pragma unroll
+      for (int c = 0; c < FB; ++c)
+#pragma unroll
+        for (int t = 0; t < c; ++t) {
+          colj[c] = colj[c] - Lf[c][t] * colj[t];
+          ekr[c] = ekr[c] - Lf[c][t] * ekr[t];
+#pragma unroll
+          for (int r = 0; r < 8; ++r) ci[c][r] = ci[c][r] - Lf[c][t] * ci[t][r];
+        }
 #pragma unroll
       for (int r = 0; r < 8; ++r) {
         const int i = 8 * w + r;
-        const double ok = mask01(i > k1 && i < S);   // 0 leaves the row bitwise unchanged
-        const double m0 = ci0[r] * inv0 * ok;
-        const double m1 = (d0 * ci1[r] - bb * ci0[r]) * invdet * ok * two01;
-        g[r] = g[r] - m0 * lj0 - m1 * lj1p;
-        e[r] = e[r] - m0 * ek0 - m1 * ek1p;
-      }
-      if (w == kb) {   // rows k, k + 1 are final up to their scales (applied after the loop)
-        piv[r0] = d0;
-        if (two) {
-          e[r0 + 1] = ek1p;
-          piv[r0 + 1] = det * inv0;
+        const double ok = mask01(i >= k + nb && i < S);   // 0 leaves the row bitwise unchanged
+        double gr = g[r], er = e[r];
+#pragma unroll
+        for (int c = 0; c < FB; ++c) {
+          const double m = ci[c][r] * invD[c] * ok * mask01(c < nb);
+          gr = gr - m * colj[c];
+          er = er - m * ekr[c];
         }
+        g[r] = gr;
+        e[r] = er;
+      }
+      if (w == kb) {   // the block's rows are final up to their scales (applied after the loop)
+#pragma unroll
+        for (int a = 0; a < FB; ++a)
+          if (a < nb) {
+            e[r0 + a] = ekr[a];
+            piv[r0 + a] = D[a];
+          }
       }
     }
   }
