@@ -9,8 +9,8 @@ echo "pytest stiefel rc=$rc"; tail -20 $O/gpu_stiefel.log
 [ $rc -eq 0 ] || exit $rc
 C=riemannian-interior-point-trust-region-method_amd/csrc
 for fb in ${FBS:-1 2 4}; do
-  hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -DRIPTRM_ST_FB=$fb -I$C -Iinclude tools/stiefel_stamps.hip -o /tmp/stamps$fb > $O/stamps_build.log 2>&1 || { cat $O/stamps_build.log; exit 3; }
-  echo "# FB=$fb" >> $O/stamps.jsonl
+  hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -DRIPTRM_ST_FB=$fb -DRIPTRM_ST_COMBINED=${COMB:-0} -I$C -Iinclude tools/stiefel_stamps.hip -o /tmp/stamps$fb > $O/stamps_build.log 2>&1 || { cat $O/stamps_build.log; exit 3; }
+  echo "# FB=$fb COMBINED=${COMB:-0}" >> $O/stamps.jsonl
   timeout -k 10 120 /tmp/stamps$fb 200 50 256 >> $O/stamps.jsonl 2>&1; rc=$?
   [ $rc -eq 0 ] || { cat $O/stamps.jsonl; exit $rc; }
 done
