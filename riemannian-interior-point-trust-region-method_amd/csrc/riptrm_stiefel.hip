@@ -617,77 +617,6 @@ __device__ __forceinline__ void r2_factor_inverse(lds_f64* Gm, lds_f64* xch, int
   __syncthreads();
 }
 
-// The same factor with G and E in ONE register array (in-place Gauss-Jordan): before step k a
-// row i > k holds E[i][j] for j < k and G[i][j] for j >= k (E's columns past k are zero apart from
-// its implicit unit diagonal), so a step updates each element once: columns j > k with G's pivot
-// column, j < k with E's pivot row, and column k becomes E[i][k] = -m_i.  Waves whose 8 rows are
-// all finished skip the update (wave-uniform): half the VALU work of the two-array form, again
-// halved on average by the skip.
-template <int P16>
-__device__ __forceinline__ void r2_factor_inverse_c(lds_f64* Gm, lds_f64* xch, int p) {
-  constexpr int S = 16 * P16;
-  const int t = threadIdx.x, l = t & 63, w = t >> 6;
-  double h[8], piv[8];
-#pragma unroll
-  for (int r = 0; r < 8; ++r) {
-    const int i = 8 * w + r;
-    h[r] = (i < S && l < S) ? Gm[i * S + l] : 0.0;
-    piv[r] = 1.0;
-  }
-  for (int kb = 0; 8 * kb < p; ++kb) {
-#pragma unroll
-    for (int r0 = 0; r0 < 8; ++r0) {
-      const int k = 8 * kb + r0;
-      if (k >= p) break;   // uniform
-      lds_f64* cg = xch + (r0 & 1) * 2 * S;   // [column k of h | row k of h], alternating by step parity
-      lds_f64* re = cg + S;
-      if (l == k) {
-#pragma unroll
-        for (int r = 0; r < 8; ++r)
-          if (8 * w + r < S) cg[8 * w + r] = h[r];
-      }
-      if (w == kb && l < S) re[l] = h[r0];
-      __syncthreads();
-      const int jl = l < S ? l : 0;
-      const double d = cg[k];
-      const double lj = cg[jl], ek = re[jl];
-      double ci[8];
-#pragma unroll
-      for (int r = 0; r < 8; ++r) ci[r] = cg[8 * w + r];
-      const double inv = 1.0 / d;
-      const double x = l > k ? lj : (l == k ? 1.0 : ek);
-      if (8 * w + 7 > k) {   // wave-uniform: some row of this wave comes after k
-#pragma unroll
-        for (int r = 0; r < 8; ++r) {
-          const int i = 8 * w + r;
-          const bool after = i > k && i < S;
-          const double m = ci[r] * inv * mask01(after);   // 0 leaves the row bitwise unchanged
-          const double hk = (after && l == k) ? 0.0 : h[r];
-          h[r] = hk - m * x;
-        }
-      }
-      if (w == kb) {   // the pivot row: E's row k (unscaled), zero past the diagonal
-        h[r0] = l < k ? h[r0] : (l == k ? 1.0 : 0.0);
-        piv[r0] = d;
-      }
-    }
-  }
-#pragma unroll
-  for (int r = 0; r < 8; ++r) h[r] = h[r] * (1.0 / sqrt(piv[r]));
-  __syncthreads();
-#pragma unroll
-  for (int r = 0; r < 8; ++r) {
-    const int i = 8 * w + r;
-    if (i < S && l < S) Gm[l * S + i] = h[r];   // W[j][i] = E[i][j]
-  }
-  __syncthreads();
-}
-
-// default factor form (RIPTRM_STIEFEL_FACTOR=inplace / =split override it per call)
-#ifndef RIPTRM_ST_COMBINED
-#define RIPTRM_ST_COMBINED 0
-#endif
-
 // Q = A W (W upper triangular): wave w owns the 16-row blocks R = w, w + 8, ...; FINAL writes Q to
 // global memory, otherwise Q overwrites A in LDS (a wave writes only the rows it read)
 template <int P16, bool FINAL>
@@ -732,8 +661,8 @@ __device__ __forceinline__ void r2_apply(lds_f64* As, const lds_f64* Wt, int NR,
   __syncthreads();
 }
 
-template <int P16, bool COMB>
-__device__ __forceinline__ void st_retr2_body(int n, int p, int64_t stride, const double* __restrict__ X,
+template <int P16>
+__global__ void __launch_bounds__(T) k_st_retr2(int n, int p, int64_t stride, const double* __restrict__ X,
                                                 const double* __restrict__ U, double* out) {   // out may alias X or U (all reads precede the first write)
   constexpr int S = 16 * P16, UL = 8;
   extern __shared__ double lds[];
@@ -766,30 +695,16 @@ __device__ __forceinline__ void st_retr2_body(int n, int p, int64_t stride, cons
   ST_STAMP(1);
   r2_gram<P16>(As, Gm, red, NR);
   ST_STAMP(2);
-  if (COMB) r2_factor_inverse_c<P16>(Gm, red, p);
-  else r2_factor_inverse<P16>(Gm, red, p);
+  r2_factor_inverse<P16>(Gm, red, p);
   ST_STAMP(3);
   r2_apply<P16, false>(As, Gm, NR, n, p, out + o);
   ST_STAMP(4);
   r2_gram<P16>(As, Gm, red, NR);
   ST_STAMP(5);
-  if (COMB) r2_factor_inverse_c<P16>(Gm, red, p);
-  else r2_factor_inverse<P16>(Gm, red, p);
+  r2_factor_inverse<P16>(Gm, red, p);
   ST_STAMP(6);
   r2_apply<P16, true>(As, Gm, NR, n, p, out + o);
   ST_STAMP(7);
-}
-
-// split factor (G and E in two register arrays, FB columns per step) / in-place factor
-template <int P16>
-__global__ void __launch_bounds__(T) k_st_retr2_s(int n, int p, int64_t stride, const double* __restrict__ X,
-                                                  const double* __restrict__ U, double* out) {
-  st_retr2_body<P16, false>(n, p, stride, X, U, out);
-}
-template <int P16>
-__global__ void __launch_bounds__(T) k_st_retr2_c(int n, int p, int64_t stride, const double* __restrict__ X,
-                                                  const double* __restrict__ U, double* out) {
-  st_retr2_body<P16, true>(n, p, stride, X, U, out);
 }
 
 __global__ void __launch_bounds__(T) k_st_inner(int n, int p, int64_t stride, const double* U, const double* V, double* out) {
@@ -826,9 +741,8 @@ static int st_check(riptrm_ctx* c, int32_t n, int32_t p, int32_t batch, int64_t 
     for (const void* f : fns) HIPCHK(c, hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, shm));
     HIPCHK(c, hipFuncSetAttribute((const void*)k_st_retr_r, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   (int)(LDS_DOUBLES_R * sizeof(double))));
-    const void* fr[] = {(const void*)k_st_retr2_s<1>, (const void*)k_st_retr2_s<2>, (const void*)k_st_retr2_s<3>,
-                        (const void*)k_st_retr2_s<4>, (const void*)k_st_retr2_c<1>, (const void*)k_st_retr2_c<2>,
-                        (const void*)k_st_retr2_c<3>, (const void*)k_st_retr2_c<4>};
+    const void* fr[] = {(const void*)k_st_retr2<1>, (const void*)k_st_retr2<2>, (const void*)k_st_retr2<3>,
+                        (const void*)k_st_retr2<4>};
     for (const void* f : fr) HIPCHK(c, hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, R2_LDS_MAX));
     if (c->device >= 0 && c->device < 64) attr[c->device] = true;
   }
@@ -836,7 +750,6 @@ static int st_check(riptrm_ctx* c, int32_t n, int32_t p, int32_t batch, int64_t 
 }
 
 constexpr size_t SHM = LDS_DOUBLES * sizeof(double);
-
 
 // LDS bytes of k_st_retr2 at (n, p), 0 if the point does not fit (the round-1 kernel runs then)
 static size_t retr2_lds_bytes(int n, int p) {
@@ -902,13 +815,7 @@ int riptrm_stiefel_retr(riptrm_ctx* ctx, int32_t n, int32_t p, int32_t batch, in
   if (rc) return rc;
   const size_t shm2 = retr_force_r1() ? 0 : retr2_lds_bytes(n, p);
   if (shm2) {
-    const char* fe = getenv("RIPTRM_STIEFEL_FACTOR");
-    const bool comb = fe ? (fe[0] == 'i') : (RIPTRM_ST_COMBINED != 0);   // "inplace" / "split"
-    if (comb) {
-      ST_LAUNCH(k_st_retr2_c, p, dim3(batch), dim3(T), shm2, ctx->stream, n, p, stride, X, U, out);
-    } else {
-      ST_LAUNCH(k_st_retr2_s, p, dim3(batch), dim3(T), shm2, ctx->stream, n, p, stride, X, U, out);
-    }
+    ST_LAUNCH(k_st_retr2, p, dim3(batch), dim3(T), shm2, ctx->stream, n, p, stride, X, U, out);
   } else {
     hipLaunchKernelGGL(k_st_retr_r, dim3(batch), dim3(T), SHM_R, ctx->stream, n, p, stride, X, U, out);
   }

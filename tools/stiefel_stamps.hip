@@ -32,7 +32,7 @@ int main(int argc, char** argv) {
   CK(hipFuncSetAttribute((const void*)k_st_proj<4>, hipFuncAttributeMaxDynamicSharedMemorySize, shm));
   CK(hipFuncSetAttribute((const void*)k_st_retr_r, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_DOUBLES_R * 8));
   const int shm2 = r2_lds_doubles_nr<4>((n + 15) / 16 * 16) * 8;
-  CK(hipFuncSetAttribute((const void*)(RIPTRM_ST_COMBINED ? k_st_retr2_c<4> : k_st_retr2_s<4>), hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+  CK(hipFuncSetAttribute((const void*)k_st_retr2<4>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
 
   hipEvent_t a, b;
   CK(hipEventCreate(&a));
@@ -42,7 +42,7 @@ int main(int argc, char** argv) {
       CK(hipEventRecord(a, 0));
       if (which == 0) hipLaunchKernelGGL(k_st_proj<4>, dim3(B), dim3(T), shm, 0, n, p, (int64_t)n * p, X, U, O);
       else if (which == 1) hipLaunchKernelGGL(k_st_retr_r, dim3(B), dim3(T), LDS_DOUBLES_R * 8, 0, n, p, (int64_t)n * p, X, U, O);
-      else hipLaunchKernelGGL((RIPTRM_ST_COMBINED ? k_st_retr2_c<4> : k_st_retr2_s<4>), dim3(B), dim3(T), shm2, 0, n, p, (int64_t)n * p, X, U, O);
+      else hipLaunchKernelGGL(k_st_retr2<4>, dim3(B), dim3(T), shm2, 0, n, p, (int64_t)n * p, X, U, O);
       CK(hipEventRecord(b, 0));
       CK(hipEventSynchronize(b));
     }
