@@ -300,6 +300,8 @@ class NonnegPCABatch:
     def load_Z(self, Z) -> "NonnegPCABatch":
         """Z: (batch, n, n) fp64 (numpy or torch).  S_b = Z_b + Z_b^T packed on the device.
         Shared layout: one (n, n) (or (1, n, n)) Z for the whole batch."""
+        if isinstance(Z, np.ndarray) and not Z.flags.writeable:   # torch wants writable host memory
+            Z = Z.copy()
         Zt = torch.as_tensor(Z, dtype=torch.float64)
         if self.shared:
             if Zt.dim() == 3 and Zt.shape[0] == 1:
