@@ -184,9 +184,52 @@ def cpu_reference_structured(n: int, budget_s: float):
                        f"budget")}
 
 
+def _free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n: int, script: str | None = None, argv=None) -> int:
+    """torch.distributed.run-style launcher for ``bench.py --gpus N`` run directly: N child
+    processes of this same command line, rank i on LOCAL_RANK i, rendezvous on 127.0.0.1.  The
+    children inherit stdout, and only rank 0 prints the JSON line, so the parent relays it as is.
+    If any rank fails, the rest are terminated and the first non-zero exit code is returned."""
+    import subprocess
+    port = os.environ.get("MASTER_PORT") or str(_free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, script or os.path.abspath(__file__)]
+                                      + list(sys.argv[1:] if argv is None else argv), env=env))
+    log(f"launched {n} ranks (pids {[p.pid for p in procs]}, master 127.0.0.1:{port})")
+    rc = 0
+    pending = list(procs)
+    while pending:
+        for p in list(pending):
+            code = p.poll()
+            if code is None:
+                continue
+            pending.remove(p)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 128 - code
+                log(f"rank pid {p.pid} exited with {code}; stopping the other ranks")
+                for q in pending:
+                    q.terminate()
+        time.sleep(0.2)
+    return rc
+
+
 def main():
     if len(sys.argv) > 1 and sys.argv[1] == "--cpu-worker":
         _cpu_worker(sys.argv[2:])
+        return
+    if len(sys.argv) > 1 and sys.argv[1] == "--si-cpu-worker":
+        _si_cpu_worker(sys.argv[2:])
         return
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -218,11 +261,19 @@ def main():
                     help="sym layout S-pass: 1 = automatic (rule on n alone: persistent super-tile kernel for n >= 2561, "
                          "per-tile kernel below; batch-independent bits), 0 = per-tile kernel only, 2 = super-tile kernel "
                          "always, 3 = super-tile for launches with >= 1 unit per CU if a bind-time timing preferred it")
+    ap.add_argument("--persistent", type=int, default=1, choices=[0, 1, 2],
+                    help="k_persist for small batches: 1 = cooperative launch (default), 2 = plain launch (A/B), 0 = off")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_gemv.json"))
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend (nccl = RCCL)")
     ap.add_argument("--same-device", action="store_true",
                     help="rehearsal only: every rank on cuda:0 (use with --backend gloo on a 1-GPU box)")
     args = ap.parse_args()
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # `python bench.py --gpus N` outside torchrun: launch the N ranks here, before anything
+        # touches the GPU (children are started as subprocesses, never exec'd)
+        sys.exit(launch_ranks(args.gpus))
 
     import numpy as np
     import torch
@@ -231,6 +282,8 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; launch one rank per GPU")
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dev_idx = 0 if args.same_device else local
@@ -239,6 +292,7 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", dev_idx))
         else:
             dist.init_process_group(args.backend)
+        assert dist.get_world_size() == args.gpus, (dist.get_world_size(), args.gpus)
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
@@ -259,7 +313,7 @@ def main():
 
     n, B, W, K = args.dim, args.batch, args.warmup, args.steps
     eng = engine.NonnegPCABatch(n, B, log_capacity=2048, layout=args.layout, stream_groups=args.stream_groups,
-                                spass_kind=args.spass_kind, drain_logs=False)
+                                spass_kind=args.spass_kind, drain_logs=False, persistent=args.persistent)
     nS = 1 if args.layout == "shared" else B
     log(f"rank {rank}/{world}: generating {B} instances n={n} ({nS * eng.inst_stride * 8 / 1e9:.1f} GB S)")
     # global instance ids owned by this rank: rank, rank+world, ... (seed seed0 + id)
@@ -435,7 +489,7 @@ def main():
                        "trs_solver": args.trs,
                        "n": n, "batch_per_gpu": B, "global_batch": B * world,
                        "outer_window": [W + 1, W + K], "restart_every": args.cycle, "layout": args.layout,
-                       "parallelism": f"instance-sharded x{world}"},
+                       "parallelism": f"instance-sharded x{world}", "world_size": world},
             "roofline": roofline,
             "cpu_baseline": cpu,
             "detail": {"inner_iterations_per_s": inner_all / T, "tcg_iterations_per_s": tcg_all / T,
@@ -517,7 +571,7 @@ def bench_stiefel(args, world, rank, dev, dist):
         "warmup": args.warmup, "ms_per_step": tp * 1e3, "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "f64", "data": "synthetic (random orthonormal X, Gaussian U)",
         "config": {"workload": f"Stiefel(n={n}, p={p}) x {B} per GPU (BASELINE configs[4] size)",
-                   "global_batch": B * world, "parallelism": f"instance-sharded x{world}"},
+                   "global_batch": B * world, "parallelism": f"instance-sharded x{world}", "world_size": world},
         # binding roof = the larger of the two floors: 24 n p bytes (read X, U; write the result)
         # at HBM peak vs 4 n p^2 flops (X^T U and X sym(.)) at the FP64-matrix peak
         "roofline": {"bound": "hbm" if hbm_floor >= mfma_floor else "mfma",
@@ -561,6 +615,58 @@ def si_starts(B: int, ids):
         xs.append(x)
         ys.append(y0)
     return np.stack(xs), np.stack(ys), SI.SIData.load(ds)
+
+
+def _si_oracle_window(gid: int, K: int, budget_s: float, trs: str):
+    """The SI oracle on bench start `gid` (si_starts), outer iterations 1..K or as many as the
+    budget allows; returns (completed outer iterations, solver seconds) or None."""
+    from oracle import riptrm_oracle as RO
+    from oracle import si_oracle as SI
+    xs, ys, data = si_starts(1, [gid])
+    orc = RO.RIPTRMOracle(dict(maxiter=K, tolresid=0.0, maxtime=1e12, manviofun=SI.si_manvio,
+                               **trs_options(trs)), deadline=time.time() + budget_s)
+    try:
+        orc.run(SI.SIVectorized(data), xs[0], ys[0])
+    except RO.BudgetExceeded:
+        pass
+    heads = orc.outer_heads
+    last = max(heads)
+    return (last, heads[last]) if last > 0 and heads[last] > 0 else None
+
+
+def _si_cpu_worker(argv):
+    """One single-threaded SI oracle process (run by si_cpu_pool)."""
+    gid, K, budget, trs = int(argv[0]), int(argv[1]), float(argv[2]), argv[3]
+    r = _si_oracle_window(gid, K, budget, trs)
+    print(json.dumps(None if r is None else {"outer": r[0], "secs": r[1]}), flush=True)
+
+
+def si_cpu_pool(K: int, budget_s: float, procs: int, trs: str):
+    """The StableIdentification analogue of cpu_baseline_pool: `procs` single-threaded oracle
+    processes run concurrently, process i solving the GPU batch's start i (si_starts) over the
+    same outer window 1..K; aggregate = mean complete per-process rate x procs."""
+    import subprocess
+    env = dict(os.environ, OMP_NUM_THREADS="1", OPENBLAS_NUM_THREADS="1", MKL_NUM_THREADS="1")
+    ps = [subprocess.Popen([sys.executable, os.path.abspath(__file__), "--si-cpu-worker", str(i), str(K),
+                            str(budget_s), trs], stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, env=env, text=True)
+          for i in range(procs)]
+    rates = []
+    for p in ps:
+        out, _ = p.communicate(timeout=budget_s + 600)
+        try:
+            r = json.loads(out.strip().splitlines()[-1])
+        except Exception:
+            continue
+        if r is not None and r["outer"] == K:
+            rates.append(r["outer"] / r["secs"])
+    if not rates:
+        return None
+    return {"value": sum(rates) / len(rates) * procs, "unit": "outer iterations/s", "cores": int(procs),
+            "kind": "port",
+            "sample": (f"oracle/si_oracle.py SIVectorized, {procs} single-threaded processes, process i solving the GPU "
+                       f"batch's start i (fixture starts a.. in order) over outer iterations 1..{K} within a "
+                       f"{budget_s:.0f} s budget; {len(rates)}/{procs} completed, aggregate = mean complete per-process "
+                       f"rate x {procs}, evaluation time excluded as RIPTRM.py:932-941")}
 
 
 def bench_si(args, world, rank, dev, dist):
@@ -613,20 +719,24 @@ def bench_si(args, world, rank, dev, dist):
         return
     cpu = None
     if args.cpu_budget > 0 and world == 1:
-        from oracle import riptrm_oracle as RO
-        from oracle import si_oracle as SI
-        orc = RO.RIPTRMOracle(dict(maxiter=K, tolresid=0.0, maxtime=1e12, manviofun=SI.si_manvio,
-                                   **trs_options(args.trs)), deadline=time.time() + args.cpu_budget)
-        try:
-            orc.run(SI.SIVectorized(data), xs[0], ys[0])
-        except RO.BudgetExceeded:
-            pass
-        heads = orc.outer_heads
-        last = max(heads)
-        if last > 0:
-            cpu = {"value": last / heads[last], "unit": "outer iterations/s", "cores": 1, "kind": "port",
+        one = _si_oracle_window(0, K, args.cpu_budget, args.trs)
+        if one is not None:
+            last, secs = one
+            cpu = {"value": last / secs, "unit": "outer iterations/s", "cores": 1, "kind": "port",
                    "sample": f"oracle/si_oracle.py SIVectorized (NumPy, closed-form Lagrangian), start 'a', outer "
-                             f"iterations 1..{last} ({heads[last]:.1f} s, evaluation time excluded as RIPTRM.py:932-941)"}
+                             f"iterations 1..{last} ({secs:.1f} s, evaluation time excluded as RIPTRM.py:932-941)"}
+        procs = min(args.cpu_procs, B)
+        if procs > 0:
+            log(f"SI CPU baseline, {procs} single-threaded processes ...")
+            pool = si_cpu_pool(K, args.cpu_pool_budget, procs, args.trs)
+            if pool is not None:
+                alt = cpu
+                if cpu is None or pool["value"] > cpu["value"]:
+                    cpu, alt = pool, cpu
+                if alt is not None:
+                    cpu["other_variant"] = {"value": alt["value"], "cores": alt["cores"], "sample": alt["sample"]}
+        if cpu is not None:
+            cpu["gpu_over_cpu"] = (outer / T) / cpu["value"]
     print(json.dumps({
         "metric": f"outer RIPTRM iterations/sec, StableIdentification d=5 (Product(Skew,SPD,SPD)), batch {B}/GPU",
         "value": outer / T, "unit": "outer iterations/s", "n_gpus": world, "steps": K, "warmup": W,
@@ -636,7 +746,7 @@ def bench_si(args, world, rank, dev, dist):
         "config": {"workload": f"StableIdentification d=5 N=95 m=16, {B} starts per GPU, outer iterations 1..{K}"
                                + ("" if args.trs == "tCG" else ", TRS_solver=Exact_RepMat + second-order test"),
                    "trs_solver": args.trs,
-                   "global_batch": B * world, "parallelism": f"instance-sharded x{world}"},
+                   "global_batch": B * world, "parallelism": f"instance-sharded x{world}", "world_size": world},
         "roofline": {"bound": "latency", "achieved": hvps / kern_s / 1e6, "peak": None, "unit": "M HVP/s",
                      "frac": None, "traffic": None,
                      "kernel": "k_si (one 64-lane workgroup per instance, whole solve per launch)",

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define RIPTRM_ABI_VERSION 5
+#define RIPTRM_ABI_VERSION 6
 
 /* status codes */
 #define RIPTRM_OK 0
@@ -48,6 +48,20 @@ extern "C" {
 #define RIPTRM_TRS_BOUNDARY 6
 #define RIPTRM_TRS_INTERIOR 7
 #define RIPTRM_TRS_HARDCASE_1 8
+/* not a reference code: tCG met a non-finite <delta, H delta> (the instance then stops with
+ * RIPTRM_ERR_NONFINITE) */
+#define RIPTRM_TCG_NONFINITE 9
+
+/* per-instance error codes (RIPTRM_STAT_ERROR).  An instance with an error stops (phase error);
+ * the others of the batch go on.  RIPTRM_ERR_NONFINITE is the device's counterpart of the
+ * reference's do_exit_on_error break (RIPTRM.py:961-966: an exception inside outer_step ends the
+ * run with the iterate that outer step started from): a NaN / Inf in the KKT residual at the
+ * outer loop head, in ||cxCur|| or Delta at a tCG start, or in <delta, H delta> inside tCG stops
+ * the instance and restores x, y to the start of the outer step it appeared in. */
+#define RIPTRM_ERR_NONE 0
+#define RIPTRM_ERR_NO_TCG_ITER 1       /* manifold.dim = 0: tCG cannot iterate */
+#define RIPTRM_ERR_BARRIER_TIMEOUT 2   /* persistent mode: a peer workgroup never arrived (2 s) */
+#define RIPTRM_ERR_NONFINITE 3
 
 /* TRS_solver option (RIPTRM.py:325) */
 #define RIPTRM_TRS_SOLVER_TCG 0
@@ -247,11 +261,18 @@ int riptrm_set_graphs(riptrm_ctx* ctx, int32_t on);
  * (BASELINE configs[1]: n = 1000, one instance) — each riptrm_solve_advance / riptrm_tcg chunk is
  * ONE launch in which every stored tile keeps its 128 x 128 block of S in LDS and every workgroup
  * runs a replica of its instance's state machine (bitwise the lock-step results; replaces
- * RIPTRM.py:41-216 + :707-896 for such batches).  mode 1 = automatic (default), 0 = never.  Set
- * before riptrm_nonnegpca_bind.  riptrm_get_persistent: whether the bound shape allows it on this
- * device and whether the current solve uses it. */
+ * RIPTRM.py:41-216 + :707-896 for such batches).  mode 1 = automatic (default): a cooperative
+ * launch, allowed at bind only if the occupancy calculator fits every workgroup with its 128 KiB
+ * of LDS at once; 0 = never; 2 = automatic with a plain launch (A/B only: no co-residency
+ * guarantee); 3 = as 1, with the first launch of every solve treated as refused (tests the
+ * fallback).  A launch refused before any persistent step of the solve ran hands the solve to
+ * the lock-step pipeline (same results bitwise); refused later, the call fails.  Set before
+ * riptrm_nonnegpca_bind.  riptrm_get_persistent: whether the bound shape allows it on this device
+ * and whether the current solve uses it; riptrm_persist_fallbacks: solves since bind that fell
+ * back to lock-step. */
 int riptrm_set_persistent(riptrm_ctx* ctx, int32_t mode);
 int riptrm_get_persistent(riptrm_ctx* ctx, int32_t* possible, int32_t* active);
+int riptrm_persist_fallbacks(riptrm_ctx* ctx, int32_t* count);
 /* Diagnostics: per in-launch step of workgroups 0 and reps - 1 of every k_persist launch, record
  * device-clock stamps (0 step start, 1 tile pass done, 2 barrier passed, 3 state step done; tCG
  * steps also 4 partial sums gathered, 5 iteration arithmetic done) into the caller's device

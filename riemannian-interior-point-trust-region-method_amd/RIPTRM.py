@@ -64,17 +64,23 @@ class RIPTRM(Solver):
     def run(self, problem) -> Output:
         return self.run_batch([problem])[0]
 
-    def run_batch(self, problems: Sequence[Any], log_capacity: int = 8192) -> List[Output]:
+    SI_LOG_BYTES = 8e9   # upper bound of the StableIdentification device log per batch
+
+    def run_batch(self, problems: Sequence[Any], log_capacity: int | None = None) -> List[Output]:
         """NonnegPCA: the device log is drained to the host whenever it is half full, so logs of
-        any length are complete.  StableIdentification runs each solve in one launch: its log
-        keeps the first log_capacity/2 and the latest records (default capacity 65536 rows per
-        instance, bounded to ~8 GB per batch)."""
+        any length are complete (log_capacity = rows of the device ring, default 8192).
+        StableIdentification runs each solve in one launch: its log keeps the first
+        log_capacity/2 and the latest records.  Its capacity is the requested one (default 65536
+        rows per instance), capped so the batch's log stays within SI_LOG_BYTES (256 B per row)."""
         problems = list(problems)
         if not problems:
             return []
         if all(isinstance(p, SIProblem) for p in problems):
-            cap = max(log_capacity, min(65536, int(8e9 // (256 * len(problems)))))
+            req = 65536 if log_capacity is None else int(log_capacity)
+            cap = max(16, min(req, int(self.SI_LOG_BYTES // (256 * len(problems)))))
             return self._run_batch_si(problems, cap)
+        if log_capacity is None:
+            log_capacity = 8192
         for p in problems:
             if not isinstance(p, NonnegPCAProblem):
                 raise NotImplementedError(
@@ -147,6 +153,9 @@ class RIPTRM(Solver):
         B = len(xs)
         for b in range(B):
             opt = copy.copy(self.option)
+            err = res.error(b)
+            if err is not None:   # RIPTRM.py:961-966: print the error, no stoppingcriterion
+                print(f"Error: {err}")
             reason = res.stopping_criterion(b)
             if reason is not None:
                 opt["stoppingcriterion"] = reason

@@ -54,8 +54,13 @@ struct riptrm_ctx {
   int graphs = 1;             // riptrm_set_graphs
   // persistent lock-step mode (k_persist): requested (riptrm_set_persistent), possible for the
   // bound shape on this device, and active for the current solve (tCG only)
+  // persist_req: 0 never, 1 automatic (cooperative launch: co-residency checked by the runtime),
+  // 2 automatic with a plain launch (A/B), 3 = 1 with the first launch of each solve treated as
+  // refused (tests the lock-step fallback).  persist_launched: a k_persist launch of the current
+  // solve has run (after that a refused launch is an error, before it the solve falls back).
   int persist_req = 1;
-  bool persist_ok = false, persist_on = false;
+  bool persist_ok = false, persist_on = false, persist_launched = false;
+  int persist_fallbacks = 0;   // solves that fell back to lock-step since bind
   unsigned long long* persist_trace = nullptr;   // riptrm_persist_trace (diagnostics)
   int persist_trace_cap = 0;
   // StableIdentification binding (riptrm_si.hip)

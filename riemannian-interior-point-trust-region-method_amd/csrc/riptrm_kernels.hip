@@ -1030,6 +1030,7 @@ __device__ __forceinline__ int tcg_math(TcgScalars& t, const riptrm_options& opt
   bsum<1>(R, d1);
   h.stamp(2);
   const double d_Hd = d1[0];
+  if (!isfinite(d_Hd)) return RIPTRM_TCG_NONFINITE;   // non-finite guard (include/riptrm.h)
   const double z_r = t.z_r, e_Pd = t.e_Pd, d_Pd = t.d_Pd, e_Pe = t.e_Pe;
   const double Delta = t.Delta;
   double alpha = 0.0, e_Pe_new;
@@ -1422,6 +1423,21 @@ struct MachineT {
     }
   }
 
+  // Non-finite guard (include/riptrm.h RIPTRM_ERR_NONFINITE; RIPTRM.py:961-966): stop the
+  // instance and hand back the iterate its current (or, at the loop head, its last) outer step
+  // started from.  Outer iteration 0 / a tCG-only run keep x, y as they are.
+  __device__ __forceinline__ int nonfinite_stop() {
+    if (s[ST_OUTER_IT] > 0.0 && (int)s[ST_MODE] == MODE_SOLVE) {
+      copy(V_X, V_X0);
+      copy(V_Y, V_Y0);
+      copy(V_SX, V_SX0);
+    }
+    cset(ST_ERROR, (double)RIPTRM_ERR_NONFINITE);
+    cset(ST_STOP_RUNTIME, (unow() - s[ST_T_START]) / P.clock_hz);
+    s[ST_PHASE] = PH_ERROR;
+    return ACT_DONE;
+  }
+
   // ---- outer loop head: RIPTRM.py:931-959 + base_solver.check_stoppingcriterion ------------
   __device__ __forceinline__ int outer_top() {
     double ev[10];
@@ -1430,6 +1446,7 @@ struct MachineT {
     const double tn = unow();
     if (s[ST_OUTER_IT] == 0.0 || !save_inner) log_row(ev, s[ST_OUTER_IT] != 0.0, tn);
     cset(ST_RESIDUAL, ev[2]);
+    if (!isfinite(ev[2])) return nonfinite_stop();
     const double rt = (tn - s[ST_T_START]) / P.clock_hz;
     int stop = RIPTRM_STOP_NONE;
     if (rt >= P.opt.maxtime) stop = RIPTRM_STOP_MAXTIME;
@@ -1529,6 +1546,7 @@ struct MachineT {
     }
     bsum<1>(R, rr);
     s[ST_NORMR0] = sqrt(rr[0]);
+    if (!isfinite(s[ST_NORMR0]) || !isfinite(s[ST_DELTA])) return nonfinite_stop();
     s[ST_ZR] = rr[0];
     s[ST_DPD] = rr[0];
     s[ST_EPE] = 0.0;
@@ -1545,7 +1563,7 @@ struct MachineT {
       }
     }
     if (n - 1 <= 0) {  // maxinner = manifold.dim = 0: no tCG iteration is possible
-      cset(ST_ERROR, 1.0);
+      cset(ST_ERROR, (double)RIPTRM_ERR_NO_TCG_ITER);
       s[ST_PHASE] = PH_ERROR;
       return ACT_DONE;
     }
@@ -1569,6 +1587,10 @@ struct MachineT {
     for (int i = tid; i < n; i += ST_THREADS) d1[0] += D[i] * U[i];
     bsum<1>(R, d1);
     const double d_Hd = d1[0];
+    if (!isfinite(d_Hd)) {   // non-finite guard (include/riptrm.h)
+      s[ST_TCG_STOP] = RIPTRM_TCG_NONFINITE;
+      return tcg_end();
+    }
     const double z_r = s[ST_ZR], e_Pd = s[ST_EPD], d_Pd = s[ST_DPD], e_Pe = s[ST_EPE];
     const double Delta = s[ST_DELTA];
     double alpha = 0.0, e_Pe_new;
@@ -1900,6 +1922,7 @@ struct MachineT {
 
   // after tCG: RIPTRM.py:733-746 (direction, ||dx||, dy, retraction) + feasibility part of :591
   __device__ __forceinline__ int tcg_end() {
+    if (s[ST_TCG_STOP] == RIPTRM_TCG_NONFINITE) return nonfinite_stop();
     cadd(ST_TCG_TOTAL, s[ST_J] + 1.0);
     const double* X = V(V_X);
     const double* Y = V(V_Y);
@@ -2752,7 +2775,7 @@ __global__ void __launch_bounds__(ST_THREADS) k_persist(DevParams P, RepBlock rq
   MachineT<false, true> M(P, bm, 0, redbuf, nullptr, hot, !rep0, rq);
   if (!ok) {   // the instance stops with an error (the host reports it)
     M.s[ST_PHASE] = PH_ERROR;
-    M.cset(ST_ERROR, 2.0);
+    M.cset(ST_ERROR, (double)RIPTRM_ERR_BARRIER_TIMEOUT);
   }
   M.finish_write();
 }
@@ -3082,6 +3105,7 @@ static PersistSync persist_sync(const riptrm_ctx* c) {
 static int persist_init(riptrm_ctx* c, const double* x, const double* y, int64_t ldv, const double* mu,
                         const double* delta, int mode) {
   c->persist_on = c->persist_ok && c->P.opt.trs_solver == RIPTRM_TRS_SOLVER_TCG;
+  c->persist_launched = false;
   if (!c->persist_on || c->L.reps <= 1) return RIPTRM_OK;
   const DevParams Q = persist_params(c);
   hipLaunchKernelGGL(k_init, dim3((unsigned)Q.batch), dim3(256), 0, c->stream, Q, x, y, ldv, mu, delta, mode,
@@ -3090,7 +3114,30 @@ static int persist_init(riptrm_ctx* c, const double* x, const double* y, int64_t
   return RIPTRM_OK;
 }
 
+static void reset_groups(riptrm_ctx* c) {
+  c->parity[0] = c->parity[1] = 0;
+  c->active_bound[0] = c->active_bound[1] = 0;
+}
+
 // `steps` lock-step iterations of the whole batch in one k_persist launch
+static int kick(riptrm_ctx* c);
+static int run_steps(riptrm_ctx* c, int steps, int* n_active);
+
+// launch k_persist<K>: cooperative (the runtime refuses a grid that cannot be co-resident instead
+// of letting its workgroups spin against each other) unless persist_req == 2
+extern "C++" template <int K>
+static hipError_t persist_launch(riptrm_ctx* c, unsigned grid, DevParams p, RepBlock rq, PersistSync sy, int steps) {
+  const size_t shm = (size_t)TS * TS * sizeof(double);
+  if (c->persist_req == 2) {
+    hipLaunchKernelGGL(k_persist<K>, dim3(grid), dim3(ST_THREADS), shm, c->stream, p, rq, sy, steps);
+    return hipGetLastError();
+  }
+  if (c->persist_req == 3 && !c->persist_launched) return hipErrorCooperativeLaunchTooLarge;   // test hook
+  void* args[] = {&p, &rq, &sy, &steps};
+  return hipLaunchCooperativeKernel((const void*)k_persist<K>, dim3(grid), dim3(ST_THREADS), args, (unsigned)shm,
+                                    c->stream);
+}
+
 static int persist_run(riptrm_ctx* c, int steps, int* n_active) {
   const PersistSync sy = persist_sync(c);
   // the sync block and the tagged grid (adjacent): counters, clocks and tags start at zero
@@ -3104,13 +3151,23 @@ static int persist_run(riptrm_ctx* c, int steps, int* n_active) {
     const DevParams Q = persist_params(c);
     const RepBlock rq{Q.vec, Q.st, Q.stats, Q.req, Q.batch};
     static_assert(PERSIST_MAX_N <= 4 * ST_THREADS, "k_persist<4> covers every persistent shape");
-    if (c->P.n <= 2 * ST_THREADS)
-      hipLaunchKernelGGL(k_persist<2>, dim3(grid), dim3(ST_THREADS), (size_t)TS * TS * sizeof(double), c->stream,
-                         params_for(c, 0), rq, sy, steps);
-    else
-      hipLaunchKernelGGL(k_persist<4>, dim3(grid), dim3(ST_THREADS), (size_t)TS * TS * sizeof(double), c->stream,
-                         params_for(c, 0), rq, sy, steps);
-    HIPCHK(c, hipGetLastError());
+    const hipError_t le = c->P.n <= 2 * ST_THREADS ? persist_launch<2>(c, grid, params_for(c, 0), rq, sy, steps)
+                                                    : persist_launch<4>(c, grid, params_for(c, 0), rq, sy, steps);
+    if (le != hipSuccess) {
+      (void)hipGetLastError();
+      if (c->persist_launched)
+        return fail(c, RIPTRM_E_HIP, std::string("persistent lock-step launch refused mid-solve: ") + hipGetErrorString(le));
+      // nothing of this solve has run persistently yet: the instances are still at their start
+      // (replicas only initialised), so the lock-step pipeline takes over from here
+      c->persist_on = false;
+      c->persist_fallbacks++;
+      c->ev_used -= (e0 ? 1 : 0) + (e1 ? 1 : 0);   // the unused events go back to the pool
+      reset_groups(c);
+      HIPCHK(c, hipMemsetAsync(c->P.cnt, 0, 4 * sizeof(int32_t), c->stream));
+      if (int rc = kick(c)) return rc;
+      return run_steps(c, steps, n_active);
+    }
+    c->persist_launched = true;
     if (c->prof && e1) {
       HIPCHK(c, hipEventRecord(e1, c->stream));
       c->ev_state.push_back({i0, i1});
@@ -3217,11 +3274,20 @@ int riptrm_nonnegpca_bind(riptrm_ctx* ctx, const double* S, int32_t n, int32_t b
   // persistent mode: the workspace has the replica region and every workgroup fits on its own CU
   ctx->persist_ok = ctx->persist_req != 0 && L.reps > 0 && (int64_t)batch * L.reps <= ctx->ncu;
   ctx->persist_on = false;
+  ctx->persist_fallbacks = 0;
   if (ctx->persist_ok) {
     HIPCHK(ctx, hipFuncSetAttribute((const void*)k_persist<2>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                     (int)(TS * TS * sizeof(double))));
     HIPCHK(ctx, hipFuncSetAttribute((const void*)k_persist<4>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                     (int)(TS * TS * sizeof(double))));
+    // every workgroup must be resident at once: ask the occupancy calculator with the launch's
+    // dynamic LDS (one 128 KiB tile per workgroup -> at most one per CU), and the device for
+    // cooperative launch support
+    int nb = 0, coop = 0;
+    const void* kp = n <= 2 * ST_THREADS ? (const void*)k_persist<2> : (const void*)k_persist<4>;
+    HIPCHK(ctx, hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kp, ST_THREADS, (size_t)TS * TS * sizeof(double)));
+    HIPCHK(ctx, hipDeviceGetAttribute(&coop, hipDeviceAttributeCooperativeLaunch, ctx->device));
+    ctx->persist_ok = nb >= 1 && (int64_t)batch * L.reps <= (int64_t)nb * ctx->ncu && (coop || ctx->persist_req == 2);
   }
   if (layout == RIPTRM_LAYOUT_SHARED) {  // the MFMA S-pass stages two K steps of V and S tiles in LDS
     HIPCHK(ctx, hipFuncSetAttribute((const void*)k_spass_mm<8, 128>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -3511,10 +3577,6 @@ static int kick(riptrm_ctx* c) {
   return join_streams(c);
 }
 
-static void reset_groups(riptrm_ctx* c) {
-  c->parity[0] = c->parity[1] = 0;
-  c->active_bound[0] = c->active_bound[1] = 0;
-}
 
 int riptrm_tcg(riptrm_ctx* ctx, const double* x, const double* y, int64_t ldv, const double* mu, const double* delta,
                int32_t* iters, int32_t* stop, int32_t max_steps) {
@@ -3621,7 +3683,7 @@ int riptrm_set_spass_kind(riptrm_ctx* ctx, int32_t kind) {
 }
 
 int riptrm_set_persistent(riptrm_ctx* ctx, int32_t mode) {
-  if (!ctx || mode < 0 || mode > 1) return RIPTRM_E_ARG;
+  if (!ctx || mode < 0 || mode > 3) return RIPTRM_E_ARG;
   if (ctx->solving) return fail(ctx, RIPTRM_E_STATE, "set_persistent: call before riptrm_nonnegpca_bind");
   ctx->persist_req = mode;
   return RIPTRM_OK;
@@ -3638,6 +3700,12 @@ int riptrm_get_persistent(riptrm_ctx* ctx, int32_t* possible, int32_t* active) {
   if (!ctx || !possible || !active) return RIPTRM_E_ARG;
   *possible = ctx->persist_ok ? 1 : 0;
   *active = ctx->persist_on ? 1 : 0;
+  return RIPTRM_OK;
+}
+
+int riptrm_persist_fallbacks(riptrm_ctx* ctx, int32_t* count) {
+  if (!ctx || !count) return RIPTRM_E_ARG;
+  *count = ctx->persist_fallbacks;
   return RIPTRM_OK;
 }
 

@@ -38,7 +38,13 @@ TCG_NAMES = {C["RIPTRM_TCG_MAX_INNER_ITER"]: "MAX_INNER_ITER",
              C["RIPTRM_TCG_EXCEEDED_TR"]: "EXCEEDED_TR",
              C["RIPTRM_TCG_MODEL_INCREASED"]: "MODEL_INCREASED",
              C["RIPTRM_TCG_REACHED_TARGET_LINEAR"]: "REACHED_TARGET_LINEAR",
-             C["RIPTRM_TCG_REACHED_TARGET_SUPERLINEAR"]: "REACHED_TARGET_SUPERLINEAR"}
+             C["RIPTRM_TCG_REACHED_TARGET_SUPERLINEAR"]: "REACHED_TARGET_SUPERLINEAR",
+             C["RIPTRM_TCG_NONFINITE"]: "NONFINITE"}
+ERROR_TEXT = {C["RIPTRM_ERR_NO_TCG_ITER"]: "manifold dimension 0: truncated CG cannot iterate",
+              C["RIPTRM_ERR_BARRIER_TIMEOUT"]: "persistent lock-step: a peer workgroup did not arrive within 2 s",
+              C["RIPTRM_ERR_NONFINITE"]: ("non-finite value (NaN/Inf) in the KKT residual, the tCG residual, the "
+                                          "trust-region radius or <delta, H delta>; returning the iterate the outer "
+                                          "step started from")}
 STATUS_NAMES = {0: None, 1: "initial", 2: "converged", 3: "primal_infeasible", 4: "successful",
                 5: "unsuccessful", 6: "max-time-exceeded", 7: "max-iter-exceeded"}
 RU_NAMES = {0: None, 1: "reduced", 2: "expanded", 3: "unchanged"}
@@ -435,10 +441,11 @@ class NonnegPCABatch:
     def persistent_state(self) -> Dict[str, bool]:
         """riptrm_get_persistent: whether the bound shape runs k_persist on this device, and whether
         the current solve / tCG run uses it."""
-        pos, act = ctypes.c_int32(), ctypes.c_int32()
+        pos, act, fb = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
         self.ctx.check(self.lib.riptrm_get_persistent(self.ctx.h, ctypes.byref(pos), ctypes.byref(act)),
                        "riptrm_get_persistent")
-        return {"possible": bool(pos.value), "active": bool(act.value)}
+        self.ctx.check(self.lib.riptrm_persist_fallbacks(self.ctx.h, ctypes.byref(fb)), "riptrm_persist_fallbacks")
+        return {"possible": bool(pos.value), "active": bool(act.value), "fallbacks": int(fb.value)}
 
     def hvp(self, x, y, mu: float, v) -> torch.Tensor:
         """HwCur(v) at (x, y, mu) for every instance (RIPTRM.py:729)."""
@@ -564,6 +571,12 @@ class BatchResult:
 
     def stat(self, b: int, name: str) -> float:
         return float(self.stats[b, C[f"RIPTRM_STAT_{name}"]])
+
+    def error(self, b: int) -> Optional[str]:
+        """The instance's error (RIPTRM_STAT_ERROR) as the text the reference prints after
+        "Error: " when outer_step raises (RIPTRM.py:961-966), or None."""
+        code = int(self.stat(b, "ERROR"))
+        return None if code == C["RIPTRM_ERR_NONE"] else ERROR_TEXT.get(code, f"device error code {code}")
 
     def stopping_criterion(self, b: int) -> Optional[str]:
         code = int(self.stat(b, "STOP_CODE"))

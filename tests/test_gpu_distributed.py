@@ -87,3 +87,24 @@ def test_two_ranks_on_one_gpu_match_single_process_bitwise():
         np.testing.assert_array_equal(gx, rx)
         np.testing.assert_array_equal(gy, ry)
         np.testing.assert_array_equal(gr, rr)
+
+
+def test_bench_launches_its_own_ranks():
+    """`python bench.py --gpus 2` (the driver's command form, no torchrun) starts two ranks itself
+    (bench.launch_ranks) and reports the whole-job line: n_gpus 2, twice the per-GPU batch."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--same-device",
+                        "--backend", "gloo", "--dim", "200", "--batch", "4", "--warmup", "1", "--steps", "3",
+                        "--cpu-budget", "0"], env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2
+    assert out["config"]["world_size"] == 2
+    assert out["config"]["global_batch"] == 8
+    assert out["value"] > 0

@@ -52,7 +52,8 @@ def _assert_same(ra, rb, B):
 def test_persistent_matches_lockstep_bitwise(n, B, K):
     insts = [G.generate_instance(n, 900 + b) for b in range(B)]
     e1, r1 = _solve(insts, 1, maxiter=K)
-    assert e1.persistent_state() == {"possible": True, "active": True}
+    st = e1.persistent_state()
+    assert st["possible"] and st["active"] and st["fallbacks"] == 0
     e0, r0 = _solve(insts, 0, maxiter=K)
     assert e0.persistent_state()["active"] is False
     _assert_same(r1, r0, B)
@@ -109,3 +110,63 @@ def test_persistent_not_used_when_too_large():
     eng2 = engine.NonnegPCABatch(1000, 8)  # 8 x 36 tiles > 256 workgroups
     eng2.load_Z(np.broadcast_to(Z[:1000, :1000], (8, 1000, 1000)))
     assert eng2.persistent_state()["possible"] is False
+
+
+def test_refused_persistent_launch_falls_back_to_lockstep():
+    """A persistent launch the runtime refuses before the solve's first persistent step (mode 3
+    simulates it) hands the solve to the lock-step kernels: same results bitwise, one fallback."""
+    n, B = 1000, 3
+    insts = [G.generate_instance(n, 960 + b) for b in range(B)]
+    e3, r3 = _solve(insts, 3, maxiter=6)
+    st = e3.persistent_state()
+    assert st["possible"] and not st["active"] and st["fallbacks"] == 1
+    e0, r0 = _solve(insts, 0, maxiter=6)
+    _assert_same(r3, r0, B)
+
+
+def test_plain_launch_mode_matches():
+    """Mode 2 (plain launch, the round-2 path; A/B only) gives the same bits as the cooperative one."""
+    n, B = 200, 4
+    insts = [G.generate_instance(n, 970 + b) for b in range(B)]
+    e2, r2 = _solve(insts, 2, maxiter=8)
+    assert e2.persistent_state()["active"]
+    e1, r1 = _solve(insts, 1, maxiter=8)
+    _assert_same(r2, r1, B)
+
+
+def test_two_persistent_solves_on_concurrent_streams():
+    """Two batches whose persistent grids together exceed the CUs (2 x 7 x 36 = 504 workgroups of one
+    CU each), solved at the same time from two threads on two streams: the cooperative launches may
+    not interleave their workgroups (the in-launch barriers would spin against each other), so both
+    must finish without a barrier timeout and match the lock-step results."""
+    import threading
+    import engine
+    n, B = 1000, 7
+    sets = [[G.generate_instance(n, 980 + 10 * k + b) for b in range(B)] for k in range(2)]
+    refs = [_solve(s_, 0, maxiter=4)[1] for s_ in sets]
+    out, errs = [None, None], []
+
+    def run(k):
+        try:
+            with torch.cuda.stream(torch.cuda.Stream()):
+                eng = engine.NonnegPCABatch(n, B, log_capacity=4096, persistent=1)
+                eng.load_Z(np.stack([z for z, _, _ in sets[k]]))
+                res = eng.solve(np.stack([x for _, x, _ in sets[k]]), np.stack([y for _, _, y in sets[k]]),
+                                _opt(maxiter=4))
+                torch.cuda.current_stream().synchronize()
+                out[k] = (eng.persistent_state(), res)
+        except Exception as e:   # reported below
+            errs.append(repr(e))
+
+    th = [threading.Thread(target=run, args=(k,)) for k in range(2)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=120)
+    assert not errs, errs
+    for k in range(2):
+        st, res = out[k]
+        assert st["possible"]
+        for b in range(B):
+            assert res.stat(b, "ERROR") == 0
+        _assert_same(res, refs[k], B)
