@@ -1052,33 +1052,35 @@ __device__ __forceinline__ int tcg_math(TcgScalars& t, const riptrm_options& opt
     return d_Hd <= 0.0 ? RIPTRM_TCG_NEGATIVE_CURVATURE : RIPTRM_TCG_EXCEEDED_TR;
   }
   t.e_Pe = e_Pe_new;
-  double m2[2] = {0.0, 0.0};
+  // one reduction for the model value at eta + alpha delta and <r', r'> of the updated residual
+  // r' = r + alpha H delta (computed speculatively, committed only if the model decreased); each
+  // value keeps its own slot of the same tree, so both are bitwise what two reductions give
+  h.late_r();
+  double m3[3] = {0.0, 0.0, 0.0};
+  double rn[K];
 #pragma unroll
   for (int k = 0; k < K; ++k) {
     const double ne = e[k] + alpha * d[k];
     const double nh = he[k] + alpha * u[k];
-    m2[0] += ne * c[k];
-    m2[1] += ne * nh;
+    m3[0] += ne * c[k];
+    m3[1] += ne * nh;
+    rn[k] = rv[k] + alpha * u[k];
+    m3[2] += rn[k] * rn[k];
   }
-  bsum<2>(R, m2);
+  bsum<3>(R, m3);
   h.stamp(3);
-  const double new_model = m2[0] + 0.5 * m2[1];
+  const double new_model = m3[0] + 0.5 * m3[1];
   if (new_model >= t.model) return RIPTRM_TCG_MODEL_INCREASED;
   t.model = new_model;
-  h.late_r();
-  double r2b[1] = {0.0};
 #pragma unroll
   for (int k = 0; k < K; ++k) {
     e[k] = e[k] + alpha * d[k];
     he[k] = he[k] + alpha * u[k];
-    const double r = rv[k] + alpha * u[k];
-    rv[k] = r;
-    r2b[0] += r * r;
+    rv[k] = rn[k];
   }
   h.store_ehr();
-  bsum<1>(R, r2b);
   h.stamp(4);
-  const double r_r = r2b[0];
+  const double r_r = m3[2];
   const double norm_r = sqrt(r_r);
   const double nr0 = t.nr0;
   const double ka = opt.tcg_kappa;

@@ -17,6 +17,15 @@ The bar therefore is:
   |g-r| <= |r| or |g-r| <= 1e-2 max|r| (observed between the CPU oracles: step norms 54% apart
   after a MAX_INNER_ITER tCG with identical branches, n=200 seed 101, row 45);
 * plus an absolute 1e-14 everywhere (e.g. ||x|| - 1 is pure rounding, ~1e-16).
+
+That calibrated trial bound is loose by design.  The NonnegPCA GPU solve tests tighten it with
+an ENVELOPE: five CPU oracle runs that are the same arithmetic in another summation order
+(order_variants: dgemv, and dsymv on four symmetric permutations) measure how far this very
+trajectory moves under rounding, column by column; the GPU's trial values must stay within 10x
+that (compare_logs(envelope=...)), its tCG exit indices within the variants' spread
+(compare_tcg_iters), and only a budgeted few instances per test (excursion_budget) may show a
+rare amplification past it -- still inside the calibrated bound, as a further CPU variant does in
+~1 comparison of 40.
 """
 import numpy as np
 
@@ -37,7 +46,20 @@ def _col(log, k):
     return np.array([np.nan if v is None else float(v) for v in log[k]], dtype=float)
 
 
-def compare_logs(gl, rl, rtol=1e-4, ascale=1e-5, trial_rtol=1.0, trial_ascale=1e-2, atol=1e-14):
+def compare_logs(gl, rl, rtol=1e-4, ascale=1e-5, trial_rtol=1.0, trial_ascale=1e-2, atol=1e-14,
+                 envelope=None, env_mult=10.0, env_rel=1e-9, excursions=None):
+    """envelope (see `envelope`): per key and row, the distance between the reference log and
+    order-perturbed oracle runs that share its branches up to that row.  Where it is given, the
+    trial-bar rows of a column must satisfy |g - r| <= (env_mult * E + env_rel) |r| + atol with E
+    the variants' largest relative deviation over the column's trial-bar rows, instead of the
+    calibrated trial_rtol / trial_ascale bound (rows no variant covers, past every variant's own
+    first flip, keep that bound).  Column- rather than row-level, and 10x rather than 3x: a
+    further CPU order variant exceeds the row-level 3x envelope of three variants by up to 470x
+    and the column-level one by up to 8.2x.  Even so, with five variants about one comparison in
+    forty shows a rare amplification (a trial value 1000x past every variant, still inside the
+    calibrated bound; tests/test_oracle.py::test_envelope_calibration).  Pass a list as
+    `excursions` to collect such columns instead of failing; the caller then bounds how many
+    instances of a test may have one (excursion_budget)."""
     assert list(gl.keys()) == list(rl.keys()), (list(gl.keys()), list(rl.keys()))
     for k in BRANCH_KEYS:
         if k in gl and gl[k] != rl[k]:
@@ -57,6 +79,23 @@ def compare_logs(gl, rl, rtol=1e-4, ascale=1e-5, trial_rtol=1.0, trial_ascale=1e
         d = np.abs(g - r)
         ok_outer = d <= rtol * np.abs(r) + ascale * scale + atol
         ok_trial = (d <= trial_rtol * np.abs(r)) | (d <= trial_ascale * scale + atol)
+        if envelope is not None and k in envelope:
+            # column-level envelope: over the rows the variants cover, the largest relative
+            # deviation of this column stays within env_mult x the variants' largest one
+            e = envelope[k][:len(r)]
+            den = np.maximum(np.abs(r), 1e-12 * scale)
+            cov = m & ~np.isnan(e) & ~(outer if k not in STEP_KEYS else np.zeros_like(outer))
+            if cov.any():
+                lim = env_mult * np.max(e[cov] / den[cov]) + env_rel
+                ok_env = d <= lim * den + atol
+                rows_t = m & ~(outer if k not in STEP_KEYS else np.zeros_like(outer))
+                over = rows_t & ~np.isnan(e) & ~ok_env
+                if over.any() and excursions is not None and not (over & ~ok_trial).any():
+                    # within the calibrated bound but past the envelope: a rare amplification
+                    # (the caller budgets these across a test's instances)
+                    excursions.append((k, [int(i) for i in np.nonzero(over)[0][:5]]))
+                else:
+                    ok_trial = np.where(np.isnan(e), ok_trial, ok_env)
         rows_outer = outer if k not in STEP_KEYS else np.zeros_like(outer)
         bad = m & np.where(rows_outer, ~ok_outer, ~ok_trial)
         assert not bad.any(), (k, np.nonzero(bad)[0][:5], g[bad][:5], r[bad][:5])
@@ -138,6 +177,81 @@ def compare_until_flip(gl, rl, tight_rows=20, late_row=20):
     return flip
 
 
+# ---- envelopes of order-perturbed oracle runs -------------------------------------------------
+
+def order_variants(Z, x0, y0, option, S=None, seeds=(1, 2, 6, 7), structured_too=False):
+    """Oracle runs that are the same arithmetic in another summation order: dgemv instead of
+    dsymv, and dsymv on symmetric permutations P S P^T (x0, y0 permuted; every logged quantity is
+    permutation invariant).  The spread of these runs around the reference run is the rounding
+    sensitivity of the trajectory itself (the method of test_gpu_n4000's teacher-forced test)."""
+    from oracle import riptrm_oracle as O
+    S = np.asarray(Z, dtype=np.float64) + np.asarray(Z, dtype=np.float64).T if S is None else S
+    out = [O.RIPTRMOracle(option).run(O.NonnegPCAVectorized(S, S=S, symv=False), x0, y0)]
+    for sd in seeds:
+        # progress on stdout: long runs (n = 4000) must not look hung to the GPU job runner
+        print(f"[parity] order variant {len(out)}/{len(seeds) + 1} done (n = {S.shape[0]})", flush=True)
+        p = np.random.RandomState(sd).permutation(S.shape[0])
+        Sp = np.ascontiguousarray(S[p][:, p])
+        out.append(O.RIPTRMOracle(option).run(O.NonnegPCAVectorized(Sp, S=Sp), x0[p], y0[p]))
+    if structured_too:
+        out.append(O.RIPTRMOracle(option).run(O.NonnegPCAStructured(Z), x0, y0))
+    return out
+
+
+def envelope(ref, variants):
+    """Per VALUE_KEYS column: row-wise max |v - r| over the variants whose branch decisions agree
+    with the reference up to that row (NaN where none does).  Key "_tcg": per inner step, the
+    largest |j_v - j_r| of the tCG exit iteration over the same variants."""
+    rl = ref.log
+    nrows = len(rl["iteration"])
+    env = {}
+    flips = [first_branch_flip(v.log, rl) for v in variants]
+    for k in VALUE_KEYS:
+        if k not in rl:
+            continue
+        r = _col(rl, k)
+        e = np.full(nrows, np.nan)
+        for v, f in zip(variants, flips):
+            lim = nrows if f is None else f[0]
+            d = np.abs(_col(v.log, k)[:lim] - r[:lim])
+            d = np.where(np.isnan(d), 0.0, d)
+            e[:lim] = np.fmax(e[:lim], d)
+        env[k] = e
+    steps = len(ref.trace)
+    dj = np.full(steps, np.nan)
+    for v, f in zip(variants, flips):
+        lim = min(steps, len(v.trace), steps if f is None else max(0, f[0] - 1))
+        a = np.array([t["tcg_iters"] for t in v.trace[:lim]], float)
+        b = np.array([t["tcg_iters"] for t in ref.trace[:lim]], float)
+        dj[:lim] = np.fmax(dj[:lim], np.abs(a - b))
+    env["_tcg"] = dj
+    return env
+
+
+def excursion_budget(instances: int) -> int:
+    """Instances of one test allowed an envelope excursion: the CPU calibration rate is ~1/40
+    per comparison; allow 10% of the instances (at least one)."""
+    return max(1, instances // 10)
+
+
+def compare_tcg_iters(g_iters, ref, env, mult=3.0, rel=0.005, slack=2):
+    """tCG exit iterations per inner step (GPU log rows 1.. = oracle trace) and their total: each
+    within max(slack, mult x the variants' largest |dj| over the run, rel x j), the total within
+    max(mult x the variants' largest per-step |dj| x steps moved, rel x total).  CG's exit index
+    is itself a rounding quantity near a stopping threshold (a fourth CPU order variant moves
+    short runs by one or two iterations where the three variants agree)."""
+    r = np.array([t["tcg_iters"] for t in ref.trace], float)
+    g = np.asarray(g_iters, float)[:len(r)]
+    assert len(g) == len(r), (len(g), len(r))
+    dj = env["_tcg"][:len(r)]
+    djmax = float(np.nanmax(dj)) if np.any(~np.isnan(dj)) else 0.0
+    lim = np.maximum(np.maximum(slack, mult * djmax), rel * r)
+    bad = np.abs(g - r) > lim
+    assert not bad.any(), (np.nonzero(bad)[0][:5], g[bad][:5], r[bad][:5], djmax)
+    moved = int(np.sum(g != r))
+    assert abs(g.sum() - r.sum()) <= max(slack * moved, mult * djmax * moved, rel * r.sum()), (g.sum(), r.sum())
+
+
 # ---- classified branch flips ------------------------------------------------------------------
 
 def column_deviation(a, r, k):
@@ -151,18 +265,27 @@ def column_deviation(a, r, k):
     return float(np.max(np.abs(g[ok] - v[ok]) / np.maximum(np.abs(v[ok]), 1e-12 * scale)))
 
 
-def prefix_deviation(gl, rl, rows):
-    """Relative deviation of the iterate quantities (cost, residual, max |y|) on the first `rows`
-    rows: the drift the two trajectories have accumulated before a flip."""
-    p = {k: v[:rows] for k, v in gl.items()}
-    q = {k: v[:rows] for k, v in rl.items()}
-    return max(column_deviation(p, q, k) for k in ("cost", "residual", "maxabsLagmult"))
+DRIFT_CAP = 1e-8
+
+
+def prefix_deviation(gl, rl, rows, cap=DRIFT_CAP):
+    """Relative deviation of the iterate quantities (cost, residual, max |y|) on the OUTER-iterate
+    rows (row 0 and each outer iteration's last row) among the first `rows` rows: the drift the
+    two trajectories have accumulated before a flip.  Trial rows are left out (their values differ
+    by up to O(1) between any two fp64 implementations), and the result is capped at `cap`."""
+    keep = [i for i in outer_rows(rl) if i < rows and i < len(gl["iteration"])]
+    if not keep:
+        return 0.0
+    p = {k: [v[i] for i in keep] for k, v in gl.items()}
+    q = {k: [v[i] for i in keep] for k, v in rl.items()}
+    return min(cap, max(column_deviation(p, q, k) for k in ("cost", "residual", "maxabsLagmult")))
 
 
 def classify_flip(step, P, states, gl, rl, flip, trials=8, seed=0):
     """A branch flip at log row `flip[0]` (key flip[1]) is a rounding-driven one if the GPU's decision
     is reachable from the ORACLE's own state at that inner step perturbed at any size from 1e-14 up
-    to the drift the two trajectories had accumulated before it (prefix_deviation): random relative
+    to the drift the two trajectories had accumulated before it on their outer iterates
+    (prefix_deviation, capped at DRIFT_CAP = 1e-8 relative): random relative
     perturbations of x (kept on the sphere) and y, `trials` per decade, each run through the
     oracle's inner_step `step` (RIPTRM.py:707-783).  Decisions that flip this way are
     either ties (|normdx - Delta| <= 1e-15, RIPTRM.py:672) or the erratic tail of an ill-conditioned
@@ -203,3 +326,63 @@ class StateRecorder:
             return inner(P, x, y, mu, Delta, inner_iteration, inner_option)
 
         oracle.inner_step = rec
+
+
+# ---- one GPU instance against the oracle ----------------------------------------------------
+
+def check_instance(gl, Z, x0, y0, opt, gpu_x=None, S=None, gpu_tcg=None):
+    """One instance's GPU trajectory against the oracle (dsymv) with tests/parity.py's bar:
+    identical branches, outer-iterate values within 1e-4, trial values within 10x the envelope of
+    five order-perturbed oracle runs (parity.order_variants / envelope), and the tCG exit index
+    of every inner step within the variants' spread (parity.compare_tcg_iters; gpu_tcg = the
+    GPU's per-row tCG iterations).  A branch flip must be a classified rounding tie
+    (parity.classify_flip: the GPU's decision is reachable from the oracle's own state at that
+    step perturbed by at most the outer-iterate drift accumulated before it, capped at 1e-8); the
+    trajectories must then still agree at the outer level (parity.compare_outer).
+    Returns ("flip", (row, key, eps)), ("excursion", [(key, rows)]) or None."""
+    from oracle import riptrm_oracle as O
+    Pa = O.NonnegPCAVectorized(Z, S=S)
+    oa = O.RIPTRMOracle(opt)
+    rec = StateRecorder(oa)
+    ra = oa.run(Pa, x0, y0)
+    exc = []
+    try:
+        compare_logs(gl, ra.log)   # branches + the calibrated bound first (flip detection)
+        env = envelope(ra, order_variants(Z, x0, y0, opt, S=S))
+        compare_logs(gl, ra.log, envelope=env, excursions=exc)
+        if gpu_tcg is not None:
+            compare_tcg_iters(gpu_tcg, ra, env)
+    except BranchFlip:
+        flip = first_branch_flip(gl, ra.log)
+        eps = classify_flip(rec.step, Pa, rec.states, gl, ra.log, flip)
+        assert eps is not None, ("branch flip not reachable within the accumulated drift", flip,
+                                 gl[flip[1]][flip[0]], ra.log[flip[1]][flip[0]])
+        compare_outer(gl, ra.log)
+        # the rows before the flip still meet the envelope bar (and their tCG exit indices)
+        row = flip[0]
+        if row > 1:
+            env = envelope(ra, order_variants(Z, x0, y0, opt, S=S))
+            compare_logs(_prefix(gl, row), _prefix(ra.log, row), envelope=env, excursions=exc)
+            if gpu_tcg is not None:
+                pre = type("Pre", (), {"trace": ra.trace[:row - 1]})()
+                compare_tcg_iters(list(gpu_tcg)[:row - 1], pre, {"_tcg": env["_tcg"][:row - 1]})
+        return ("flip", flip + (eps, len(gl["iteration"]), exc))
+    if gpu_x is not None:
+        np.testing.assert_allclose(gpu_x, ra.x, atol=1e-6)
+    return ("excursion", exc) if exc else None
+
+
+def check_budget(results, B, late_ties_free=False):
+    """At most B/2 instances of a test may flip (each a classified rounding tie) and at most
+    excursion_budget(B) may show an envelope excursion (before a flip, for flipped ones).
+    late_ties_free: flips in the last quarter of an instance's rows reproduced by a perturbation
+    <= 1e-12 (the tie regime of small-mu iterations: |normdx - Delta| <= 1e-15 with a tiny Delta,
+    RIPTRM.py:672) do not count against the B/2."""
+    flips = {b: r[1] for b, r in results.items() if r and r[0] == "flip"}
+    exc = {b: r[1] for b, r in results.items() if r and r[0] == "excursion"}
+    exc.update({b: f[4] for b, f in flips.items() if f[4]})   # flip = (row, key, eps, rows, excursions)
+    print("classified flips:", flips, "envelope excursions:", exc)
+    counted = {b: f for b, f in flips.items()
+               if not (late_ties_free and f[0] >= 0.75 * f[3] and f[2] <= 1e-12)}
+    assert len(counted) <= B // 2, flips
+    assert len(exc) <= excursion_budget(B), exc

@@ -142,31 +142,17 @@ def test_fixture_reaches_published_residual_on_gpu(fixture_n50):
     assert res[conv][-1] < 2e-14
 
 
-def _check_instance(gl, Z, x0, y0, K, gpu_x=None, S=None):
-    """One instance's GPU trajectory against the oracle (dsymv) with tests/parity.py's bar
-    (compare_logs: identical branches, values within the bounds the two CPU oracles need).  A branch flip must be a classified rounding tie
-    (parity.classify_flip: the GPU's decision is reachable from the oracle's own state at that
-    step perturbed by the drift accumulated before it); the trajectories must then still agree at
-    the outer level (parity.compare_outer).  Returns the flip (row, key, eps) or None."""
-    from parity import BranchFlip, StateRecorder, classify_flip, compare_logs, compare_outer, first_branch_flip
-    Pa = O.NonnegPCAVectorized(Z, S=S)
-    oa = O.RIPTRMOracle(_oracle_opt(maxiter=K))
-    rec = StateRecorder(oa)
-    ra = oa.run(Pa, x0, y0)
-    try:
-        compare_logs(gl, ra.log)
-    except BranchFlip:
-        flip = first_branch_flip(gl, ra.log)
-        eps = classify_flip(rec.step, Pa, rec.states, gl, ra.log, flip)
-        assert eps is not None, ("branch flip not reachable within the accumulated drift", flip,
-                                 gl[flip[1]][flip[0]], ra.log[flip[1]][flip[0]])
-        compare_outer(gl, ra.log)
-        return flip + (eps,)
-    if gpu_x is not None:
-        np.testing.assert_allclose(gpu_x, ra.x, atol=1e-6)
-    return None
+def _check_instance(gl, Z, x0, y0, K, gpu_x=None, S=None, gpu_tcg=None, option=None):
+    from parity import check_instance
+    return check_instance(gl, Z, x0, y0, _oracle_opt(maxiter=K, **(option or {})), gpu_x=gpu_x, S=S, gpu_tcg=gpu_tcg)
 
 
+def _budget(results, B):
+    from parity import check_budget
+    check_budget(results, B)
+
+
+@pytest.mark.timeout(900)
 @pytest.mark.parametrize("n,B,K,layout", [(37, 5, 10, "sym"), (200, 4, 12, "sym"), (1000, 2, 10, "sym"),
                                           (300, 3, 10, "sym2"), (1000, 2, 10, "sym2")])
 def test_batched_solve_matches_oracle(n, B, K, layout):
@@ -177,14 +163,12 @@ def test_batched_solve_matches_oracle(n, B, K, layout):
     eng = _engine(np.stack([z for z, _, _ in insts]), layout=layout)
     res = eng.solve(np.stack([x for _, x, _ in insts]), np.stack([y for _, _, y in insts]), _gpu_opt(maxiter=K))
     xs = res.x.cpu().numpy()
-    flips = {}
+    results = {}
     for b, (Z, x0, y0) in enumerate(insts):
-        f = _check_instance(res.log(b), Z, x0, y0, K, gpu_x=xs[b])
-        if f is not None:
-            flips[b] = f
-        else:
+        results[b] = _check_instance(res.log(b), Z, x0, y0, K, gpu_x=xs[b], gpu_tcg=res.tcg_iters_per_row(b)[1:])
+        if not (results[b] and results[b][0] == "flip"):
             assert int(res.stat(b, "OUTER_ITERS")) == K
-    print("classified flips:", flips)
+    _budget(results, B)
 
 
 def test_edge_options_match_oracle():
@@ -403,6 +387,7 @@ def test_shared_tcg_matches_oracle_teacher_forced(n, B):
         assert err <= 1e-8, (b, j, err)
 
 
+@pytest.mark.timeout(900)
 @pytest.mark.parametrize("n,B,K", [(60, 40, 10), (1000, 5, 8)])
 def test_shared_multistart_solve_matches_oracle(n, B, K):
     """One Z, B feasible starts: every start's trajectory against the oracle's (_check_instance)."""
@@ -414,12 +399,11 @@ def test_shared_multistart_solve_matches_oracle(n, B, K):
     eng = _shared_engine(Z, B)
     res = eng.solve(np.stack(starts), np.stack([y0] * B), _gpu_opt(maxiter=K))
     xs = res.x.cpu().numpy()
-    flips = {}
+    results = {}
     for b in range(B):
-        f = _check_instance(res.log(b), Z, starts[b], y0, K, gpu_x=xs[b])
-        if f is not None:
-            flips[b] = f
-    print("classified flips:", flips)
+        results[b] = _check_instance(res.log(b), Z, starts[b], y0, K, gpu_x=xs[b],
+                                     gpu_tcg=res.tcg_iters_per_row(b)[1:])
+    _budget(results, B)
 
 
 def test_run_batch_detects_shared_Z(fixture_n50):

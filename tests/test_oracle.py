@@ -250,3 +250,69 @@ def test_flip_classifier_accepts_rounding_ties_and_rejects_real_differences():
     row = next(r for r in range(1, len(fake["inner_status"])) if fake["inner_status"][r] == "successful")
     fake["inner_status"][row] = "unsuccessful"
     assert classify_flip(rec.step, P, rec.states, fake, ra.log, (row, "inner_status")) is None
+
+
+def test_envelope_calibration():
+    """parity.compare_logs(envelope=...) as the GPU solve tests use it, with CPU stand-ins for the
+    GPU: further order variants (dsymv on other permutations) and the reference-structured oracle
+    against the dsymv oracle, the envelope made of parity.order_variants' five runs.  No stand-in
+    may fail the bar; envelope excursions (trial values past 10x the envelope but inside the
+    calibrated bound) stay within parity.excursion_budget of the comparisons; the tCG exit
+    indices meet compare_tcg_iters.  (Measured while choosing the bar: the row-level 3x envelope
+    of three variants is exceeded by up to 470x, the column-level one by up to 8.2x; with five
+    variants and 10x, 1 comparison of 44 had an excursion, n = 37 seed 108, minyfeasi.)"""
+    from parity import (BranchFlip, compare_logs, compare_tcg_iters, envelope, excursion_budget,
+                        order_variants)
+    cases = [(37, s) for s in range(100, 112)] + [(60, s) for s in (110, 111, 113)]
+    compared, exc = 0, []
+    for n, seed in cases:
+        Z, x0, y0 = G.generate_instance(n, seed)
+        opt = dict(OPT, maxiter=10)
+        ref = O.RIPTRMOracle(opt).run(O.NonnegPCAVectorized(Z), x0, y0)
+        env = envelope(ref, order_variants(Z, x0, y0, opt))
+        S = Z + Z.T
+        for sd in (3, 4, "structured"):
+            if sd == "structured":
+                r = O.RIPTRMOracle(opt).run(O.NonnegPCAStructured(Z), x0, y0)
+            else:
+                p = np.random.RandomState(sd).permutation(n)
+                Sp = np.ascontiguousarray(S[p][:, p])
+                r = O.RIPTRMOracle(opt).run(O.NonnegPCAVectorized(Sp, S=Sp), x0[p], y0[p])
+            e = []
+            try:
+                compare_logs(r.log, ref.log, envelope=env, excursions=e)
+            except BranchFlip:
+                continue
+            compare_tcg_iters([t["tcg_iters"] for t in r.trace], ref, env)
+            compared += 1
+            if e:
+                exc.append((n, seed, sd, e))
+    assert compared >= 30
+    assert len(exc) <= excursion_budget(compared), exc
+
+
+def test_flip_classifier_rejects_late_decision_with_margin():
+    """the classifier's perturbation is the OUTER-iterate drift before the flip, capped at
+    1e-8 relative, so a late row cannot borrow O(1) trial-row drift.  Fabricated decisions at the
+    last outer iteration whose real margins are large must not be reproduced: 'unsuccessful' on a
+    step with ared/pred > 0.5 (the test is ared > rho pred, rho = 0.1, RIPTRM.py:676), and
+    'expanded' on a step far inside the radius (needs |normdx - Delta| <= 1e-15, :672)."""
+    import copy
+    from parity import DRIFT_CAP, StateRecorder, classify_flip, prefix_deviation
+    Z, x0, y0 = G.generate_instance(37, 100)
+    P = O.NonnegPCAVectorized(Z)
+    oa = O.RIPTRMOracle(dict(OPT, maxiter=10))
+    rec = StateRecorder(oa)
+    ra = oa.run(P, x0, y0)
+    b = O.solve(Z, x0, y0, dict(OPT, maxiter=10), structured=True)
+    rows = len(ra.log["iteration"])
+    assert prefix_deviation(b.log, ra.log, rows) <= DRIFT_CAP
+    last = max(ra.log["iteration"])
+    late = [r for r in range(rows) if ra.log["iteration"][r] == last and ra.log["inner_status"][r] == "successful"
+            and ra.log["ared/pred"][r] > 0.5 and ra.log["normdx"][r] < 0.5 * ra.log["TR_radius"][r]]
+    assert late, "no late row with a clear decision"
+    row = late[-1]
+    for key, value in (("inner_status", "unsuccessful"), ("radius_update", "expanded")):
+        fake = copy.deepcopy(ra.log)
+        fake[key][row] = value
+        assert classify_flip(rec.step, P, rec.states, fake, ra.log, (row, key)) is None, key
