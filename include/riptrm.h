@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define RIPTRM_ABI_VERSION 6
+#define RIPTRM_ABI_VERSION 7
 
 /* status codes */
 #define RIPTRM_OK 0
@@ -66,8 +66,9 @@ extern "C" {
 /* TRS_solver option (RIPTRM.py:325) */
 #define RIPTRM_TRS_SOLVER_TCG 0
 #define RIPTRM_TRS_SOLVER_EXACT_REPMAT 1
-/* Exact_RepMat works on the dim x dim matrix of HwCur in LDS: manifold.dim <= this
- * (NonnegPCA n <= 97, StableIdentification d <= 7) */
+/* Exact_RepMat works on the dim x dim matrix of HwCur in LDS up to manifold.dim = this
+ * (NonnegPCA n <= 97, StableIdentification d <= 7); larger NonnegPCA problems keep the matrix in
+ * HBM scratch bound with riptrm_trs_bind_workspace (below) */
 #define RIPTRM_TRS_DIM_MAX 96
 
 /* inner_status codes (RIPTRM.py:763,770,678,698,829,837); 0 = None */
@@ -368,10 +369,24 @@ int riptrm_si_solve(riptrm_ctx* ctx, const riptrm_options* opt, const double* x0
  * symmetric dim x dim matrices: instance b's A at A + b*a_stride (row-major, leading dimension
  * lda), a / x at a + b*ldv, x + b*ldv; Delta, lam1, mineig: batch doubles; kind: batch int32
  * (RIPTRM_TRS_*).  mineig (may be NULL) = the smallest eigenvalue of A (RIPTRM.py:611).
- * 1 <= dim <= RIPTRM_TRS_DIM_MAX.  One workgroup per instance.  Asynchronous. */
+ * dim <= RIPTRM_TRS_DIM_MAX: one workgroup per instance, A staged in LDS, asynchronous.
+ * dim > RIPTRM_TRS_DIM_MAX: needs riptrm_trs_bind_workspace(order >= dim); the instances are solved
+ * one after another on the HBM-resident matrix (SciPy CG restated, rocSOLVER dsyevd, secular
+ * Newton on one workgroup); synchronises. */
 int riptrm_trs_gep(riptrm_ctx* ctx, int32_t dim, int32_t batch, const double* A, int64_t lda, int64_t a_stride,
                    const double* a, int64_t ldv, const double* Delta, double tolhardcase, double* x,
                    double* lam1, int32_t* kind, double* mineig);
+
+/* Scratch of the HBM path of Exact_RepMat (manifold.dim > RIPTRM_TRS_DIM_MAX; RIPTRM.py:433-444,
+ * :599-617 and TRSgep :218-299 at any size): `slots` subproblems of matrix order `order` (NonnegPCA:
+ * order = n, the n x n frame matrix; riptrm_trs_gep: order = dim).  Bytes for riptrm_trs_bind_workspace,
+ * caller-owned device memory (256-byte aligned).  The eigendecomposition is rocSOLVER's dsyevd,
+ * loaded at first use (dlopen of librocsolver.so.0); rocSOLVER manages its own internal workspace.
+ * In a NonnegPCA solve an instance that reaches the subproblem (or, with the second-order test, a
+ * trial point) parks; riptrm_solve_advance serves parked instances after its lock-step chunk and
+ * synchronises then.  Binding NULL unbinds. */
+int64_t riptrm_trs_workspace_bytes(int32_t order, int32_t slots);
+int riptrm_trs_bind_workspace(riptrm_ctx* ctx, void* ws, int64_t bytes, int32_t order, int32_t slots);
 
 /* ==== Stiefel(n, p) manifold operations =========================================
  * Not in the reference (north_star / BASELINE configs[4] ask for them): pymanopt 2.x formulas,

@@ -6,9 +6,10 @@ module named ``RIPTRM`` from its solver path and calls ``RIPTRM(option).run(prob
 eqLagmult)`` whose ``log`` has the reference's columns, one row per inner iteration
 (``RIPTRM.py:812-818``).  Differences, all explicit errors rather than silent fallbacks:
 
-* ``TRS_solver='tCG'`` (what every shipped config selects) at any size; ``'Exact_RepMat'`` (the
-  class default, with ``second_order_stationarity``) while ``manifold.dim <= 96`` — the matrix of
-  HwCur lives in LDS (csrc/riptrm_trs.h); larger problems raise;
+* ``TRS_solver='tCG'`` (what every shipped config selects) and ``'Exact_RepMat'`` (the class
+  default, with ``second_order_stationarity``) at any size: up to ``manifold.dim = 96`` the matrix
+  of HwCur lives in LDS (csrc/riptrm_trs.h), beyond that in HBM with rocSOLVER's dsyevd
+  (csrc/riptrm_trs_big.hip);
 * the problem is a structured descriptor (``problems.NonnegPCAProblem`` or
   ``si.SIProblem`` for StableIdentification) instead of a list of autograd closures, because
   closures cannot execute on the GPU;

@@ -65,7 +65,19 @@ struct riptrm_ctx {
   int persist_trace_cap = 0;
   // StableIdentification binding (riptrm_si.hip)
   riptrm_si::Bound* si = nullptr;
+  // Exact_RepMat above RIPTRM_TRS_DIM_MAX (riptrm_trs_big.hip): caller-owned scratch bound by
+  // riptrm_trs_bind_workspace (slots of order big_order) and the rocBLAS handle of rocSOLVER
+  char* big_ws = nullptr;
+  int big_order = 0, big_slots = 0;
+  void* big_handle = nullptr;
 };
+
+// riptrm_trs_big.hip
+int riptrm_big_service(riptrm_ctx* c, int* served);
+int riptrm_big_trs_gep(riptrm_ctx* c, int dim, int batch, const double* A, int64_t lda, int64_t a_stride, const double* a,
+                       int64_t ldv, const double* Delta, double tolhc, double* x, double* lam1, int32_t* kind,
+                       double* mineig);
+void riptrm_big_release(riptrm_ctx* c);
 
 
 inline int fail(riptrm_ctx* c, int code, const std::string& msg) {

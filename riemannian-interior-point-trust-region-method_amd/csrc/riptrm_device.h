@@ -66,7 +66,10 @@ static_assert(ST_N_USED <= ST_N, "state slots overflow");
 enum Phase : int {
   PH_IDLE = 0, PH_START, PH_AFTER_SX0, PH_TCG, PH_TRIAL, PH_PAUSED, PH_DONE,
   PH_TCGO_START, PH_TCGO_SX, PH_ERROR,
-  PH_TRS, PH_TRS_END   // Exact_RepMat: subproblem solve / rest of the inner step (no S-pass between)
+  PH_TRS, PH_TRS_END,  // Exact_RepMat: subproblem solve / rest of the inner step (no S-pass between)
+  // Exact_RepMat above RIPTRM_TRS_DIM_MAX (riptrm_trs_big.hip): parked until the host has served the
+  // subproblem (-> PH_TRS_END) or the trial point's smallest eigenvalue (-> PH_MINEIG_END)
+  PH_TRS_HOST, PH_MINEIG_HOST, PH_MINEIG_END
 };
 
 enum Mode : int { MODE_SOLVE = 0, MODE_TCG_ONLY = 1 };

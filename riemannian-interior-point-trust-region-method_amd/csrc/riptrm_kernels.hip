@@ -1425,6 +1425,10 @@ struct MachineT {
     }
   }
 
+  // Exact_RepMat beyond the LDS solver's size: the host serves the subproblem and the trial-point
+  // eigenvalue from HBM (riptrm_trs_big.hip)
+  __device__ __forceinline__ bool trs_big() const { return n - 1 > riptrm_trs::DIM_MAX; }
+
   // Non-finite guard (include/riptrm.h RIPTRM_ERR_NONFINITE; RIPTRM.py:961-966): stop the
   // instance and hand back the iterate its current (or, at the loop head, its last) outer step
   // started from.  Outer iteration 0 / a tCG-only run keep x, y as they are.
@@ -1560,6 +1564,10 @@ struct MachineT {
     s[ST_MINEIG_OK] = 1.0;
     if constexpr (EXACT) {
       if (P.opt.trs_solver == RIPTRM_TRS_SOLVER_EXACT_REPMAT && (int)s[ST_MODE] == MODE_SOLVE) {
+        if (trs_big()) {   // the host serves the subproblem (riptrm_trs_big.hip), then PH_TRS_END
+          s[ST_PHASE] = PH_TRS_HOST;
+          return ACT_PAUSE;
+        }
         s[ST_PHASE] = PH_TRS;
         return ACT_CONTINUE;
       }
@@ -1983,21 +1991,35 @@ struct MachineT {
     s[ST_YFEAS] = (c3[3] == 0.0) ? 1.0 : 0.0;
     if (EXACT && P.opt.trs_solver == RIPTRM_TRS_SOLVER_EXACT_REPMAT && P.opt.second_order_stationarity) {
       // compute_inner_stoppingcriteria's eigen-check at (x_new, y_new), RIPTRM.py:599-613
+      if (trs_big()) {   // the host takes the smallest eigenvalue, then PH_MINEIG_END
+        s[ST_PHASE] = PH_MINEIG_HOST;
+        return ACT_PAUSE;
+      }
       double me = 0.0;
       if constexpr (EXACT) me = trial_mineig();
-      const int mi = (int)s[ST_MU_IDX];
-      const double tol2 = P.opt.tol2_table ? P.opt.tol2_table[mi < P.tab_len ? mi : P.tab_len - 1] : mu;
-      s[ST_HASMIN] = 1.0;
       s[ST_MINEIG] = me;
-      s[ST_MINEIG_OK] = (me >= -tol2) ? 1.0 : 0.0;
+      mineig_test();
     }
+    return tcg_end_tail();
+  }
+
+  // s[ST_MINEIG] against -forcing_function_second_order(mu) (RIPTRM.py:613)
+  __device__ __forceinline__ void mineig_test() {
+    const int mi = (int)s[ST_MU_IDX];
+    const double tol2 = P.opt.tol2_table ? P.opt.tol2_table[mi < P.tab_len ? mi : P.tab_len - 1] : s[ST_MU];
+    s[ST_HASMIN] = 1.0;
+    s[ST_MINEIG_OK] = (s[ST_MINEIG] >= -tol2) ? 1.0 : 0.0;
+  }
+
+  // the rest of the step after the trial point's criteria: RIPTRM.py:746-775
+  __device__ __forceinline__ int tcg_end_tail() {
     if (s[ST_XFEAS] != 0.0) {
       s[ST_PHASE] = PH_TRIAL;
       return request(2);
     }
     // primal infeasible: RIPTRM.py:769-775
     set_info(RIPTRM_IS_PRIMAL_INFEASIBLE, false, 0.0, RIPTRM_RU_NONE, -1.0);
-    s[ST_DELTA] = P.opt.gamma * normdx;
+    s[ST_DELTA] = P.opt.gamma * s[ST_NORMDX];
     return inner_loop_tail(false);
   }
 
@@ -2191,6 +2213,9 @@ struct MachineT {
         return ACT_DONE;
       case PH_TRS_END:
         return tcg_end();
+      case PH_MINEIG_END:   // the host wrote s[ST_MINEIG] (riptrm_trs_big.hip)
+        mineig_test();
+        return tcg_end_tail();
       default:
         return ACT_DONE;
     }
@@ -2216,7 +2241,7 @@ __global__ void __launch_bounds__(ST_THREADS) k_state(DevParams P, int full, int
     // a full launch (solve start / resume) only (re)starts instances that wait for no S-pass
     const double* g = P.st + (int64_t)b * ST_N;
     const int ph = (int)g[ST_PHASE];
-    const bool startable = ph == PH_START || ph == PH_TCGO_START ||
+    const bool startable = ph == PH_START || ph == PH_TCGO_START || ph == PH_TRS_END || ph == PH_MINEIG_END ||
                            (ph == PH_PAUSED && (double)P.outer_target > g[ST_OUTER_IT]);
     if (!startable) return;
   } else if (full == 2) {
@@ -2993,6 +3018,7 @@ int riptrm_ctx_destroy(riptrm_ctx* ctx) {
   if (ctx) {
     if (ctx->gexec) (void)hipGraphExecDestroy(ctx->gexec);
     if (ctx->si) riptrm_si_release(ctx->si);
+    riptrm_big_release(ctx);
     for (auto e : ctx->ev_pool) (void)hipEventDestroy(e);
     for (auto e : {ctx->ev_fork, ctx->ev_join, ctx->ev_pass[0], ctx->ev_pass[1]})
       if (e) (void)hipEventDestroy(e);
@@ -3384,7 +3410,7 @@ static int launch_gemv(riptrm_ctx* c, hipStream_t st, int list_in, int zero_cnt,
 
 // dynamic LDS of k_state: the Exact_RepMat work area (Machine::trs_wvec / trs_uvec / trs_red)
 static size_t state_lds_bytes(const DevParams& P) {
-  if (P.opt.trs_solver != RIPTRM_TRS_SOLVER_EXACT_REPMAT) return 0;
+  if (P.opt.trs_solver != RIPTRM_TRS_SOLVER_EXACT_REPMAT || P.n - 1 > riptrm_trs::DIM_MAX) return 0;
   return ((size_t)riptrm_trs::work_doubles(P.n - 1) + 2 * (riptrm_trs::DIM_MAX + 1) + 2 * ST_WAVES) * sizeof(double);
 }
 
@@ -3636,8 +3662,12 @@ int riptrm_solve_begin(riptrm_ctx* ctx, const riptrm_options* opt, const double*
     return fail(ctx, RIPTRM_E_ARG, "solve_begin: riptrm_options.struct_size mismatch");
   if (opt->trs_solver != RIPTRM_TRS_SOLVER_TCG && opt->trs_solver != RIPTRM_TRS_SOLVER_EXACT_REPMAT)
     return fail(ctx, RIPTRM_E_ARG, "solve_begin: unknown trs_solver");
-  if (opt->trs_solver == RIPTRM_TRS_SOLVER_EXACT_REPMAT && (ctx->P.n < 2 || ctx->P.n - 1 > RIPTRM_TRS_DIM_MAX))
-    return fail(ctx, RIPTRM_E_ARG, "solve_begin: Exact_RepMat needs 2 <= n <= RIPTRM_TRS_DIM_MAX + 1");
+  if (opt->trs_solver == RIPTRM_TRS_SOLVER_EXACT_REPMAT && ctx->P.n < 2)
+    return fail(ctx, RIPTRM_E_ARG, "solve_begin: Exact_RepMat needs n >= 2");
+  if (opt->trs_solver == RIPTRM_TRS_SOLVER_EXACT_REPMAT && ctx->P.n - 1 > RIPTRM_TRS_DIM_MAX &&
+      (!ctx->big_ws || ctx->big_order < ctx->P.n || ctx->big_slots < 1))
+    return fail(ctx, RIPTRM_E_STATE, "solve_begin: Exact_RepMat above RIPTRM_TRS_DIM_MAX + 1 needs "
+                                     "riptrm_trs_bind_workspace(order >= n) first");
   if (!x0 || !y0 || ldv < ctx->P.n || !mu_table || !tolL_table || !tolC_table || table_len <= 0)
     return fail(ctx, RIPTRM_E_ARG, "solve_begin: bad argument");
   if (opt->log_capacity > ctx->L.cap) return fail(ctx, RIPTRM_E_ARG, "solve_begin: log_capacity exceeds bound capacity");
@@ -3764,7 +3794,20 @@ int riptrm_solve_advance(riptrm_ctx* ctx, int32_t steps, int32_t outer_target, i
       if (rc) return rc;
     }
   }
-  return run_steps(ctx, steps, n_active);
+  int act = 0;
+  if (int rc = run_steps(ctx, steps, &act)) return rc;
+  if (ctx->P.opt.trs_solver == RIPTRM_TRS_SOLVER_EXACT_REPMAT && ctx->P.n - 1 > RIPTRM_TRS_DIM_MAX) {
+    // instances parked for a host-served subproblem / trial eigenvalue (riptrm_trs_big.hip): serve
+    // them and let them run on from PH_TRS_END / PH_MINEIG_END with the next chunk
+    int served = 0;
+    if (int rc = riptrm_big_service(ctx, &served)) return rc;
+    if (served > 0) {
+      if (int rc = kick(ctx)) return rc;
+      act += served;
+    }
+  }
+  if (n_active) *n_active = act;
+  return RIPTRM_OK;
 }
 
 }  // extern "C"

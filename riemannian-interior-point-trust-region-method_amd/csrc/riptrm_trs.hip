@@ -45,11 +45,14 @@ extern "C" int riptrm_trs_gep(riptrm_ctx* ctx, int32_t dim, int32_t batch, const
                               double* x, double* lam1, int32_t* kind, double* mineig) {
   using namespace riptrm_trs;
   if (!ctx) return RIPTRM_E_ARG;
-  if (dim < 1 || dim > DIM_MAX) return fail(ctx, RIPTRM_E_ARG, "trs_gep: dim must be in [1, RIPTRM_TRS_DIM_MAX]");
+  if (dim < 1) return fail(ctx, RIPTRM_E_ARG, "trs_gep: dim must be >= 1");
   if (batch < 0 || lda < dim || ldv < dim || (batch > 1 && a_stride < (int64_t)dim * lda))
     return fail(ctx, RIPTRM_E_ARG, "trs_gep: bad batch / lda / a_stride / ldv");
   if (batch == 0) return RIPTRM_OK;
   if (!A || !a || !Delta || !x || !lam1 || !kind) return fail(ctx, RIPTRM_E_ARG, "trs_gep: null pointer");
+  HIPCHK(ctx, hipSetDevice(ctx->device));
+  if (dim > DIM_MAX)   // HBM-resident matrix, rocSOLVER eigendecomposition (riptrm_trs_big.hip)
+    return riptrm_big_trs_gep(ctx, dim, batch, A, lda, a_stride, a, ldv, Delta, tolhardcase, x, lam1, kind, mineig);
   const size_t shm = (size_t)work_doubles(dim) * sizeof(double);
   HIPCHK(ctx, hipFuncSetAttribute((const void*)k_trs_gep, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm));
   hipLaunchKernelGGL(k_trs_gep, dim3(batch), dim3(TRS_THREADS), shm, ctx->stream, (int)dim, A, lda, a_stride, a, ldv,

@@ -252,6 +252,7 @@ class NonnegPCABatch:
         self.ws_bytes = nbytes
         self.bound = False
         self._keep: List[torch.Tensor] = []
+        self._trs_ws: Optional[torch.Tensor] = None   # Exact_RepMat above RIPTRM_TRS_DIM_MAX
         # log records copied to the host by drain_logs() (riptrm_log_rebase), per instance
         self.drain = bool(drain_logs)
         self._drained: List[List[np.ndarray]] = [[] for _ in range(self.batch)]
@@ -497,8 +498,16 @@ class NonnegPCABatch:
         assert self.bound
         ro = resolve_options(option, math.pi, self.cap, restart_every)
         if ro.exact and self.n - 1 > C["RIPTRM_TRS_DIM_MAX"]:
-            raise NotImplementedError(f"TRS_solver='Exact_RepMat' on the GPU needs manifold.dim = n - 1 <= "
-                                      f"{C['RIPTRM_TRS_DIM_MAX']} (got n = {self.n}); use TRS_solver='tCG'")
+            # Exact_RepMat beyond the LDS solver: the frame matrix (n x n) lives in HBM scratch
+            # (riptrm_trs_bind_workspace; csrc/riptrm_trs_big.hip)
+            if self._trs_ws is None:
+                nbytes = int(self.lib.riptrm_trs_workspace_bytes(self.n, 1))
+                self._trs_ws = torch.empty(nbytes + 256, dtype=torch.uint8, device=self.device)
+            base = self._trs_ws.data_ptr()
+            ptr = base + (-base) % 256
+            self.ctx.check(self.lib.riptrm_trs_bind_workspace(self.ctx.h, ctypes.c_void_p(ptr),
+                                                              self._trs_ws.numel() - (ptr - base), self.n, 1),
+                           "riptrm_trs_bind_workspace")
         X, Y = self._padded(x0), self._padded(y0)
         tabs = ro.device_tables(self.device)
         self._keep = [X, Y] + tabs

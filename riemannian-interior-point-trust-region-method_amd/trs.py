@@ -2,8 +2,10 @@
 
 ``TRSgep(A, a, B, Del, tolhardcase)`` keeps the reference's signature and return value
 (src/solver/RIPTRM.py:218-299: ``(x, lam1, type)``); ``trs_gep_batched`` solves a batch of
-subproblems held as torch tensors on the GPU in one launch.  Only B = I is supported — the one
-call site passes ``np.eye(xdim)`` (RIPTRM.py:441).  No CPU fallback.
+subproblems held as torch tensors on the GPU (dim <= RIPTRM_TRS_DIM_MAX: one launch, the matrix in
+LDS; larger: the HBM path — SciPy CG restated, rocSOLVER dsyevd, secular Newton — one subproblem
+after another).  Only B = I is supported — the one call site passes ``np.eye(xdim)``
+(RIPTRM.py:441).  No CPU fallback.
 """
 from __future__ import annotations
 
@@ -32,6 +34,27 @@ def _context(device: torch.device) -> N.Context:
     return c
 
 
+_ws = {}
+
+
+def bind_trs_workspace(ctx: N.Context, device: torch.device, order: int, slots: int = 1) -> torch.Tensor:
+    """Allocate (or reuse) and bind the HBM scratch of Exact_RepMat above RIPTRM_TRS_DIM_MAX for
+    matrices of order `order` (riptrm_trs_workspace_bytes / riptrm_trs_bind_workspace).  The
+    tensor is kept alive with the context."""
+    key = (id(ctx), device.index)
+    have = _ws.get(key)
+    if have is None or have[1] < order or have[2] < slots:
+        nbytes = int(ctx.lib.riptrm_trs_workspace_bytes(int(order), int(slots)))
+        buf = torch.empty(nbytes + 256, dtype=torch.uint8, device=device)
+        have = _ws[key] = (buf, int(order), int(slots))
+    buf, o, sl = have
+    base = buf.data_ptr()
+    ptr = base + (-base) % 256
+    ctx.check(ctx.lib.riptrm_trs_bind_workspace(ctx.h, ctypes.c_void_p(ptr), buf.numel() - (ptr - base), o, sl),
+              "riptrm_trs_bind_workspace")
+    return buf
+
+
 def trs_gep_batched(A: torch.Tensor, a: torch.Tensor, Delta: torch.Tensor, tolhardcase: float = 1e-8
                     ) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor, torch.Tensor]:
     """A: (batch, dim, dim) symmetric, a: (batch, dim), Delta: (batch,), fp64 contiguous on one GPU.
@@ -45,9 +68,11 @@ def trs_gep_batched(A: torch.Tensor, a: torch.Tensor, Delta: torch.Tensor, tolha
         if t.dtype != torch.float64 or t.device != dev or not t.is_contiguous():
             raise ValueError("expected contiguous float64 tensors on one GPU")
     B, dim = A.shape[0], A.shape[1]
-    if not 1 <= dim <= DIM_MAX:
-        raise ValueError(f"Exact_RepMat on the GPU supports 1 <= dim <= {DIM_MAX} (got {dim})")
+    if dim < 1:
+        raise ValueError("dim must be >= 1")
     ctx = _context(dev)
+    if dim > DIM_MAX:   # HBM path: scratch for one subproblem of order dim (riptrm_trs_workspace_bytes)
+        bind_trs_workspace(ctx, dev, dim)
     x = torch.empty((B, dim), dtype=torch.float64, device=dev)
     lam1 = torch.empty(B, dtype=torch.float64, device=dev)
     kind = torch.empty(B, dtype=torch.int32, device=dev)

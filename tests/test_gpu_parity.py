@@ -477,7 +477,8 @@ def test_exact_repmat_batch_matches_oracle():
 
 
 def test_exact_repmat_reference_defaults_drop_in(fixture_n50):
-    """RIPTRM(option) without TRS_solver runs the class default Exact_RepMat (RIPTRM.py:325)."""
+    """RIPTRM(option) without TRS_solver runs the class default Exact_RepMat (RIPTRM.py:325), in
+    LDS at n = 50 and on the HBM path at n = 120 (manifold.dim 119 > RIPTRM_TRS_DIM_MAX)."""
     from problems import NonnegPCAProblem, manviofun
     from RIPTRM import RIPTRM
     Z, x0, y0 = fixture_n50
@@ -485,9 +486,51 @@ def test_exact_repmat_reference_defaults_drop_in(fixture_n50):
         NonnegPCAProblem(Z=Z, initialpoint=x0, initialineqLagmult=y0))
     assert out.name == "RIPTRM_Exact_RepMat"
     assert any(v is not None for v in out.log["mineigvalHw"])
-    with pytest.raises(NotImplementedError):
-        Zb, xb, yb = G.generate_instance(120, 1)
-        RIPTRM({"maxiter": 1}).run(NonnegPCAProblem(Z=Zb, initialpoint=xb, initialineqLagmult=yb))
+    Zb, xb, yb = G.generate_instance(120, 1)
+    ob = RIPTRM({"maxiter": 2, "tolresid": 0.0, "maxtime": 1e9, "manviofun": manviofun}).run(
+        NonnegPCAProblem(Z=Zb, initialpoint=xb, initialineqLagmult=yb))
+    assert ob.name == "RIPTRM_Exact_RepMat" and max(ob.log["iteration"]) == 2
+    assert any(v is not None for v in ob.log["mineigvalHw"])
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("sos", [True, False])
+def test_exact_repmat_above_lds_size_matches_oracle(sos):
+    """NonnegPCA n = 200 (manifold.dim 199) with Exact_RepMat: the HBM path (frame matrix densified
+    from S, SciPy CG, rocSOLVER dsyevd, the trial-point eigenvalue with the second-order test) against
+    the oracle (the reference's 2n x 2n pencil per inner step, trs_oracle.trs_gep; its per-constraint
+    HVPs build the matrix), with the Exact_RepMat trajectory bar (parity.compare_until_flip)."""
+    from parity import compare_until_flip
+    Z, x0, y0 = G.generate_instance(200, 77)
+    opt = dict(TRS_solver="Exact_RepMat", second_order_stationarity=sos, maxiter=4)
+    eng = _engine(Z)
+    res = eng.solve(x0[None], y0[None], _gpu_opt(**opt))
+    ref = O.solve(Z, x0, y0, _oracle_opt(**opt))
+    gl = res.log(0)
+    kinds = [k for k in gl["dxtype"] if k is not None]
+    assert kinds and all(k in ("boundary", "interior", "hardcase_1") for k in kinds), kinds
+    assert any(v is not None for v in gl["mineigvalHw"]) == sos
+    compare_until_flip(gl, ref.log)
+
+
+@pytest.mark.timeout(900)
+def test_exact_repmat_configs1_size_drop_in(monkeypatch):
+    """BASELINE configs[1] size (n = 1000) with the reference's class defaults (Exact_RepMat +
+    second-order test) through the drop-in: runs (no size cap, RIPTRM.py:324-326), and its first
+    outer iteration matches the oracle driven by the eigh formulation of TRSgep (trs_oracle.trs_eigh;
+    the pencil's QZ on 1998 x 1998 takes ~90 s per inner step on the CPU, and trs_eigh agrees with it
+    to 5e-14 at this size, see tests/test_gpu_trs.py)."""
+    from oracle import trs_oracle as TO
+    from parity import compare_until_flip
+    from problems import NonnegPCAProblem, manviofun
+    from RIPTRM import RIPTRM
+    Z, x0, y0 = G.generate_instance(1000, 5)
+    out = RIPTRM({"maxiter": 1, "tolresid": 0.0, "maxtime": 1e9, "manviofun": manviofun}).run(
+        NonnegPCAProblem(Z=Z, initialpoint=x0, initialineqLagmult=y0))
+    assert out.name == "RIPTRM_Exact_RepMat" and max(out.log["iteration"]) == 1
+    monkeypatch.setattr(TO, "trs_gep", lambda A, a, Del, tol=1e-4: TO.trs_eigh(A, a, Del, tol))
+    ref = O.solve(Z, x0, y0, _oracle_opt(maxiter=1, TRS_solver="Exact_RepMat", second_order_stationarity=True))
+    compare_until_flip(out.log, ref.log)
 
 
 @pytest.mark.parametrize("n,B", [(2, 3), (129, 4), (300, 5), (1000, 3), (4000, 9)])
