@@ -49,6 +49,7 @@ __device__ __forceinline__ Smem smem_of(double* base_generic) {
 }
 
 typedef double dbl4 __attribute__((ext_vector_type(4)));
+typedef double dbl2 __attribute__((ext_vector_type(2)));
 
 // Diagnostic builds only (tools/stiefel_stamps.hip defines ST_STAMPS): s_memtime at phase ends,
 // thread 0 of each workgroup, into a buffer nothing else reads.
@@ -218,6 +219,197 @@ __global__ void __launch_bounds__(T) k_st_proj(int n, int p, int64_t stride, con
   ST_STAMP(1);
   update<P16>(sm, X + o, U + o, -1.0, out + o, n, p);
   ST_STAMP(2);
+}
+
+// ---- projection, round 3: the point resident in LDS, every operand read from HBM once -----------
+// k_st_proj above streams X and U from global memory twice (Gram, then update) in register batches,
+// so each phase waits on memory latency several times.  Here the whole point is copied into LDS up
+// front (X then U, row-major with their own stride p: 2 n p doubles, 160 KB at (200, 50)) by one
+// burst of 16-B loads from every thread, and both products run out of LDS:
+//   Gram  M = X^T U: the 16 x 16 blocks M_IJ, two per wave, each wave either a transposed pair
+//         (M_IJ, M_JI) or two diagonal blocks, all n rows (k) in order: one accumulator chain per
+//         block, no cross-wave sum; the blocks land in LDS where U's rows were, after every wave has
+//         taken its own output blocks' U values (the update's C operand) into registers;
+//   update out = U - X sym(M): unit (16-row block R, 16-column block J); wave w keeps J = w % 4, so
+//         its B operand sym(M)[k][J] = (M[k][j] + M[j][k]) / 2 (exactly symmetric) is read once.
+// HBM traffic: 24 n p bytes per point, the minimum.  Needs n p even and 2 n p (+ the 64 x 64 M when
+// U's area is smaller) doubles of LDS; other shapes run k_st_proj.
+constexpr int P3_LDS_DOUBLES = 160 * 1024 / 8;
+
+__host__ __device__ inline int p3_lds_doubles(int n, int p, int P16) {
+  const int S = 16 * P16;
+  return 2 * n * p + (n * p >= S * S ? 0 : S * S);
+}
+
+template <int P16>
+__device__ __forceinline__ void p3_unit(int w, int& I0, int& J0, int& I1, int& J1) {
+  constexpr int NP = P16 * (P16 - 1) / 2;   // off-diagonal pairs (I < J)
+  I0 = J0 = I1 = J1 = -1;
+  if (w < NP) {   // pair index w -> (I, J), row by row
+    int i = 0, r = w;
+#pragma unroll
+    for (int q = 0; q < P16; ++q)
+      if (r >= P16 - 1 - i && i < P16 - 1) {
+        r -= P16 - 1 - i;
+        ++i;
+      }
+    I0 = i; J0 = i + 1 + r;
+    I1 = J0; J1 = I0;
+  } else {
+    const int d = 2 * (w - NP);
+    if (d < P16) { I0 = d; J0 = d; }
+    if (d + 1 < P16) { I1 = d + 1; J1 = d + 1; }
+  }
+}
+
+template <int P16>
+__global__ void __launch_bounds__(T) k_st_proj3(int n, int p, int64_t stride, const double* X, const double* U,
+                                                double* out) {
+  constexpr int S = 16 * P16;
+  constexpr int UL = 10;   // 16-B copies per thread per matrix in flight
+  extern __shared__ double lds[];
+  lds_f64* Xs = (lds_f64*)lds;
+  lds_f64* Us = Xs + n * p;
+  lds_f64* Ms = (n * p >= S * S) ? Us : Us + n * p;   // M over U's rows once they are consumed
+  const int t = threadIdx.x, l = t & 63, w = t >> 6, c = l & 15, kk = l >> 4;
+  const int64_t o = (int64_t)blockIdx.x * stride;
+  ST_STAMP(0);
+  {   // X, U -> LDS: np / 2 16-byte chunks each, every load of a batch in flight together
+    const int nc = n * p / 2;
+    const dbl2* Xg = (const dbl2*)(X + o);
+    const dbl2* Ug = (const dbl2*)(U + o);
+    for (int e0 = 0; e0 < nc; e0 += T * UL) {
+      dbl2 vx[UL], vu[UL];
+#pragma unroll
+      for (int u = 0; u < UL; ++u) {
+        const int e = e0 + u * T + t;
+        const int ec = e < nc ? e : nc - 1;
+        vx[u] = Xg[ec];
+        vu[u] = Ug[ec];
+      }
+#pragma unroll
+      for (int u = 0; u < UL; ++u) {
+        const int e = e0 + u * T + t;
+        if (e < nc) {
+          *(__attribute__((address_space(3))) dbl2*)(Xs + 2 * e) = vx[u];
+          *(__attribute__((address_space(3))) dbl2*)(Us + 2 * e) = vu[u];
+        }
+      }
+    }
+  }
+  __syncthreads();
+  ST_STAMP(1);
+  // Gram: this wave's two blocks over all n rows
+  int I0, J0, I1, J1;
+  p3_unit<P16>(w, I0, J0, I1, J1);
+  dbl4 acc0 = dbl4{0.0, 0.0, 0.0, 0.0}, acc1 = dbl4{0.0, 0.0, 0.0, 0.0};
+  if (I0 >= 0) {
+    const int ca0 = 16 * I0 + c, cb0 = 16 * J0 + c;
+    const int ca1 = 16 * (I1 >= 0 ? I1 : I0) + c, cb1 = 16 * (J1 >= 0 ? J1 : J0) + c;
+    // A (lane c = row of M) and B (lane c = column of M) are masked separately
+    const double ma0 = mask01(ca0 < p), mb0 = mask01(cb0 < p);
+    const double ma1 = mask01(I1 >= 0 && ca1 < p), mb1 = mask01(cb1 < p);
+    const int a0 = ca0 < p ? ca0 : p - 1, b0 = cb0 < p ? cb0 : p - 1;
+    const int a1 = ca1 < p ? ca1 : p - 1, b1 = cb1 < p ? cb1 : p - 1;
+    constexpr int GB = 5;   // 4-row groups per batch of LDS reads
+    const int G = (n + 3) / 4;
+    for (int g0 = 0; g0 < G; g0 += GB) {
+      double xa0[GB], ub0[GB], xa1[GB], ub1[GB];
+#pragma unroll
+      for (int u = 0; u < GB; ++u) {
+        const int r = 4 * (g0 + u) + kk;
+        const double rm = mask01(r < n);
+        const lds_f64* xr = Xs + (r < n ? r : n - 1) * p;
+        const lds_f64* ur = Us + (r < n ? r : n - 1) * p;
+        xa0[u] = xr[a0] * (rm * ma0);
+        ub0[u] = ur[b0] * mb0;
+        xa1[u] = xr[a1] * (rm * ma1);
+        ub1[u] = ur[b1] * mb1;
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int u = 0; u < GB; ++u) {
+        acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(xa0[u], ub0[u], acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(xa1[u], ub1[u], acc1, 0, 0, 0);
+      }
+    }
+  }
+  ST_STAMP(2);
+  // the update's C operand (U at this wave's output blocks) while U is still in LDS
+  constexpr int UMAX = 7;   // units per wave: ceil(R16 P16 / 8) <= 7 for n <= 208 at P16 = 4
+  const int R16 = (n + 15) / 16;
+  const int J = w % P16;
+  const int nunits = R16 * P16;
+  double cv[UMAX][4];
+#pragma unroll
+  for (int q = 0; q < UMAX; ++q) {
+    const int u = w + NW * q;
+    const int R = u / P16;
+    const int j = 16 * J + c;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int i = 16 * R + kk + 4 * g;
+      const bool ok = u < nunits && i < n && j < p;
+      cv[q][g] = Us[(ok ? i : 0) * p + (ok ? j : 0)] * mask01(ok);
+    }
+  }
+  __syncthreads();   // every read of U in LDS is done: M may overwrite it
+  if (I0 >= 0) {
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      Ms[(16 * I0 + kk + 4 * g) * S + 16 * J0 + c] = acc0[g];
+      if (I1 >= 0) Ms[(16 * I1 + kk + 4 * g) * S + 16 * J1 + c] = acc1[g];
+    }
+  }
+  __syncthreads();
+  ST_STAMP(3);
+  // update: B = sym(M)[4s + kk][16 J + c] for this wave's column block J, read once
+  constexpr int S4 = 4 * P16;
+  const int P4 = (p + 3) / 4;
+  double bk[S4];
+#pragma unroll
+  for (int s = 0; s < S4; ++s) {
+    const int k = 4 * s + kk, j = 16 * J + c;
+    bk[s] = 0.5 * (Ms[k * S + j] + Ms[j * S + k]);   // zero past p (M is zero there)
+  }
+  // units two at a time: two independent accumulator chains per wave (four per SIMD), each
+  // unit's k steps in order
+#pragma unroll
+  for (int q = 0; q < UMAX; q += 2) {
+    const int u0 = w + NW * q, u1 = w + NW * (q + 1);
+    if (u0 >= nunits) break;   // wave-uniform
+    const bool two = q + 1 < UMAX && u1 < nunits;
+    const int R0 = u0 / P16, R1 = two ? u1 / P16 : R0;
+    const int ar0 = 16 * R0 + c, ar1 = 16 * R1 + c;
+    const lds_f64* xr0 = Xs + (ar0 < n ? ar0 : n - 1) * p;
+    const lds_f64* xr1 = Xs + (ar1 < n ? ar1 : n - 1) * p;
+    const double rm0 = mask01(ar0 < n), rm1 = mask01(ar1 < n);
+    double a0[S4], a1[S4];
+#pragma unroll
+    for (int s = 0; s < S4; ++s) {
+      const int k = 4 * s + kk;
+      const int kc = k < p ? k : p - 1;
+      const double km = mask01(k < p);
+      a0[s] = xr0[kc] * (rm0 * km);
+      a1[s] = xr1[kc] * (rm1 * km);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    dbl4 acc0u = dbl4{0.0, 0.0, 0.0, 0.0}, acc1u = dbl4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int s = 0; s < S4; ++s)
+      if (s < P4) {
+        acc0u = __builtin_amdgcn_mfma_f64_16x16x4f64(a0[s], bk[s], acc0u, 0, 0, 0);
+        acc1u = __builtin_amdgcn_mfma_f64_16x16x4f64(a1[s], bk[s], acc1u, 0, 0, 0);
+      }
+    const int j = 16 * J + c;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int i0 = 16 * R0 + kk + 4 * g, i1 = 16 * R1 + kk + 4 * g;
+      if (i0 < n && j < p) out[o + (int64_t)i0 * p + j] = cv[q][g] - acc0u[g];
+      if (two && i1 < n && j < p) out[o + (int64_t)i1 * p + j] = cv[q + 1 < UMAX ? q + 1 : q][g] - acc1u[g];
+    }
+  }
+  ST_STAMP(4);
 }
 
 template <int P16>
@@ -617,6 +809,42 @@ __device__ __forceinline__ void r2_factor_inverse(lds_f64* Gm, lds_f64* xch, int
   __syncthreads();
 }
 
+// The second CholeskyQR pass factors G2 = Q1^T Q1 = I + D with D at the rounding level of the first
+// pass (~kappa(A)^2 eps).  Then L2 = I + N with N = tril(D, -1) + diag(D) / 2 up to O(D^2), and
+// W2 = R2^-1 = (L2^-1)^T = I - N^T up to O(D^2): elementwise, no dependent chain.  Used when
+// max |D_ij| <= FO_MAX, where the dropped O(D^2) terms (<= 1e-20) sit far below the rounding of
+// the full factor; otherwise (a badly conditioned A) the exact factor runs.  Gm: G2 in, W2 out
+// (stride S, W2[i][j] at i S + j, upper triangular, identity past p).  Returns the uniform verdict.
+constexpr double FO_MAX = 1e-10;
+
+template <int P16>
+__device__ __forceinline__ bool r2_inverse_first_order(lds_f64* Gm, lds_f64* red, int p) {
+  constexpr int S = 16 * P16;
+  const int t = threadIdx.x;
+  double dev = 0.0;
+  for (int e = t; e < S * S; e += T) {
+    const int i = e / S, j = e - (e / S) * S;
+    if (i < p && j < p) dev = fmax(dev, fabs(Gm[e] - (i == j ? 1.0 : 0.0)));
+  }
+  for (int off = 32; off > 0; off >>= 1) dev = fmax(dev, __shfl_xor(dev, off));
+  if ((t & 63) == 0) red[t >> 6] = dev;
+  __syncthreads();
+  double mx = red[0];
+#pragma unroll
+  for (int w = 1; w < NW; ++w) mx = fmax(mx, red[w]);
+  if (!(mx <= FO_MAX)) return false;   // NaN-safe: the exact factor decides then
+  for (int e = t; e < S * S; e += T) {
+    const int i = e / S, j = e - (e / S) * S;
+    double v;
+    if (i >= p || j >= p) v = (i == j) ? 1.0 : 0.0;
+    else if (i == j) v = 1.0 - 0.5 * (Gm[e] - 1.0);
+    else v = (i < j) ? -Gm[e] : 0.0;
+    Gm[e] = v;   // every thread reads only the element it writes
+  }
+  __syncthreads();
+  return true;
+}
+
 // Q = A W (W upper triangular): wave w owns the 16-row blocks R = w, w + 8, ...; FINAL writes Q to
 // global memory, otherwise Q overwrites A in LDS (a wave writes only the rows it read)
 template <int P16, bool FINAL>
@@ -701,7 +929,7 @@ __global__ void __launch_bounds__(T) k_st_retr2(int n, int p, int64_t stride, co
   ST_STAMP(4);
   r2_gram<P16>(As, Gm, red, NR);
   ST_STAMP(5);
-  r2_factor_inverse<P16>(Gm, red, p);
+  if (!r2_inverse_first_order<P16>(Gm, red, p)) r2_factor_inverse<P16>(Gm, red, p);
   ST_STAMP(6);
   r2_apply<P16, true>(As, Gm, NR, n, p, out + o);
   ST_STAMP(7);
@@ -742,7 +970,7 @@ static int st_check(riptrm_ctx* c, int32_t n, int32_t p, int32_t batch, int64_t 
     HIPCHK(c, hipFuncSetAttribute((const void*)k_st_retr_r, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   (int)(LDS_DOUBLES_R * sizeof(double))));
     const void* fr[] = {(const void*)k_st_retr2<1>, (const void*)k_st_retr2<2>, (const void*)k_st_retr2<3>,
-                        (const void*)k_st_retr2<4>};
+                        (const void*)k_st_retr2<4>, (const void*)k_st_proj3<4>};
     for (const void* f : fr) HIPCHK(c, hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, R2_LDS_MAX));
     if (c->device >= 0 && c->device < 64) attr[c->device] = true;
   }
@@ -771,6 +999,15 @@ static bool retr_force_r1() {
   return e && e[0] == 'r' && e[1] == '1';
 }
 constexpr size_t SHM_R = LDS_DOUBLES_R * sizeof(double);
+
+// k_st_proj3 (point resident in LDS) for 49 <= p <= 64 when the point fits 160 KB, n p is even (16-B
+// copies) and the stride keeps points 16-B aligned; RIPTRM_STIEFEL_PROJ=r2 forces k_st_proj (A/B)
+static bool proj3_ok(int n, int p, int64_t stride) {
+  const char* e = getenv("RIPTRM_STIEFEL_PROJ");
+  if (e && e[0] == 'r' && e[1] == '2') return false;
+  return (p + 15) / 16 == 4 && (n * p) % 2 == 0 && stride % 2 == 0 && (n + 15) / 16 <= 14 &&
+         p3_lds_doubles(n, p, 4) <= P3_LDS_DOUBLES;
+}
 
 // kernels are specialised on ceil(p / 16) (the 16-column blocks), so no operand load sits behind
 // a runtime branch
@@ -802,6 +1039,12 @@ int riptrm_stiefel_proj(riptrm_ctx* ctx, int32_t n, int32_t p, int32_t batch, in
   if (!X || !U || !out || out == X) return fail(ctx, RIPTRM_E_ARG, "stiefel_proj: bad pointer (out must not alias X)");
   int rc = st_check(ctx, n, p, batch, stride);
   if (rc) return rc;
+  if (proj3_ok(n, p, stride)) {
+    hipLaunchKernelGGL(k_st_proj3<4>, dim3(batch), dim3(T), (size_t)p3_lds_doubles(n, p, 4) * sizeof(double),
+                       ctx->stream, n, p, stride, X, U, out);
+    HIPCHK(ctx, hipGetLastError());
+    return RIPTRM_OK;
+  }
   ST_LAUNCH(k_st_proj, p, dim3(batch), dim3(T), SHM, ctx->stream, n, p, stride, X, U, out);
   HIPCHK(ctx, hipGetLastError());
   return RIPTRM_OK;

@@ -33,16 +33,19 @@ int main(int argc, char** argv) {
   CK(hipFuncSetAttribute((const void*)k_st_retr_r, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_DOUBLES_R * 8));
   const int shm2 = r2_lds_doubles_nr<4>((n + 15) / 16 * 16) * 8;
   CK(hipFuncSetAttribute((const void*)k_st_retr2<4>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+  CK(hipFuncSetAttribute((const void*)k_st_proj3<4>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+  const int shm3 = p3_lds_doubles(n, p, 4) * 8;
 
   hipEvent_t a, b;
   CK(hipEventCreate(&a));
   CK(hipEventCreate(&b));
-  for (int which = 0; which < 3; ++which) {
+  for (int which = 0; which < 4; ++which) {
     for (int r = 0; r < 20; ++r) {
       CK(hipEventRecord(a, 0));
       if (which == 0) hipLaunchKernelGGL(k_st_proj<4>, dim3(B), dim3(T), shm, 0, n, p, (int64_t)n * p, X, U, O);
       else if (which == 1) hipLaunchKernelGGL(k_st_retr_r, dim3(B), dim3(T), LDS_DOUBLES_R * 8, 0, n, p, (int64_t)n * p, X, U, O);
-      else hipLaunchKernelGGL(k_st_retr2<4>, dim3(B), dim3(T), shm2, 0, n, p, (int64_t)n * p, X, U, O);
+      else if (which == 2) hipLaunchKernelGGL(k_st_retr2<4>, dim3(B), dim3(T), shm2, 0, n, p, (int64_t)n * p, X, U, O);
+      else hipLaunchKernelGGL(k_st_proj3<4>, dim3(B), dim3(T), shm3, 0, n, p, (int64_t)n * p, X, U, O);
       CK(hipEventRecord(b, 0));
       CK(hipEventSynchronize(b));
     }
@@ -54,9 +57,10 @@ int main(int argc, char** argv) {
       printf("{\"kernel\": \"k_st_retr_r\", \"n\": %d, \"p\": %d, \"B\": %d, \"event_us\": %.2f}\n", n, p, B, ms * 1e3);
       continue;
     }
-    const int np = which == 2 ? 7 : 2;
+    const int np = which == 2 ? 7 : (which == 3 ? 4 : 2);
     printf("{\"kernel\": \"%s\", \"n\": %d, \"p\": %d, \"B\": %d, \"event_us\": %.2f, \"phase_ticks_median\": [",
-           which == 0 ? "k_st_proj" : "k_st_retr2 (load, gram1, factor1, apply1, gram2, factor2, apply2)", n, p, B, ms * 1e3);
+           which == 0 ? "k_st_proj" : which == 3 ? "k_st_proj3 (load, gram, M to LDS, update)"
+                                  : "k_st_retr2 (load, gram1, factor1, apply1, gram2, factor2, apply2)", n, p, B, ms * 1e3);
     for (int k = 0; k < np; ++k) {
       std::vector<long long> d(B);
       for (int g = 0; g < B; ++g) d[g] = s[g * 16 + k + 1] - s[g * 16 + k];
