@@ -348,6 +348,7 @@ def main():
         prof = engine.profile_read(eng)
         st_p = eng.stats()
         passes_prof = float((st_p[:, engine.C["RIPTRM_STAT_PASSES"]] - st1[:, engine.C["RIPTRM_STAT_PASSES"]]).sum())
+        rhs_prof = float((st_p[:, engine.C["RIPTRM_STAT_RHS"]] - st1[:, engine.C["RIPTRM_STAT_RHS"]]).sum())
     else:
         prof = engine.profile_read(eng)
     engine.profile_enable(eng, False)
@@ -379,8 +380,9 @@ def main():
         # rank-0 kernel timing (every rank runs the same kernel on its own batch)
         gemv_s = prof["gemv_ms"] / 1e3
         passes_r0 = float((st1[:, C["RIPTRM_STAT_PASSES"]] - st0[:, C["RIPTRM_STAT_PASSES"]]).sum())
+        rhs_r0 = float((st1[:, C["RIPTRM_STAT_RHS"]] - st0[:, C["RIPTRM_STAT_RHS"]]).sum())
         if graph_mode:   # kernel timing came from the profiled second window
-            passes_r0 = passes_prof
+            passes_r0, rhs_r0 = passes_prof, rhs_prof
         achieved = (passes_r0 * bytes_per_pass / gemv_s / 1e9) if gemv_s > 0 else None
         nl = max(1, int(prof["gemv_launches"]))
         traffic = None
@@ -418,7 +420,8 @@ def main():
                         "us_per_pass": (kern_s * 1e6 / passes_r0) if passes_r0 > 0 else None}
         elif args.layout == "shared":
             # dense product on the fp64 matrix cores: 2 n^2 algorithmic flops per right-hand side
-            flops = passes_r0 * 2.0 * n * n
+            # (RIPTRM_STAT_RHS: a trial pass multiplies two, a tCG pass one)
+            flops = rhs_r0 * 2.0 * n * n
             tf = flops / gemv_s / 1e12 if gemv_s > 0 else None
             roofline = {"bound": "mfma", "achieved": tf, "peak": MFMA_F64_PEAK_TFS, "unit": "TFLOP/s",
                         "frac": (tf / MFMA_F64_PEAK_TFS) if tf else None, "traffic": None,

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define RIPTRM_ABI_VERSION 7
+#define RIPTRM_ABI_VERSION 8
 
 /* status codes */
 #define RIPTRM_OK 0
@@ -136,9 +136,10 @@ enum riptrm_stat_field {
     RIPTRM_STAT_STOP_CODE, RIPTRM_STAT_STOP_RUNTIME, RIPTRM_STAT_FINAL_RESIDUAL, RIPTRM_STAT_LOG_COUNT,
     RIPTRM_STAT_LOG_OVERFLOW, RIPTRM_STAT_PHASE, RIPTRM_STAT_MU, RIPTRM_STAT_TR_RADIUS,
     RIPTRM_STAT_TCG_LAST_J, RIPTRM_STAT_TCG_LAST_STOP, RIPTRM_STAT_ERROR, RIPTRM_STAT_LOG_BASE,
+    RIPTRM_STAT_RHS,   /* S-pass right-hand sides (PASSES counts requests; a trial pass carries 2) */
     RIPTRM_STAT_NFIELDS_USED
 };
-#define RIPTRM_STAT_NFIELDS 16
+#define RIPTRM_STAT_NFIELDS 24
 
 /* Solver options: the tCG-path keys of the RIPTRM default_option (RIPTRM.py:305-358).
  * Option callables (forcing functions, barrier schedule) are evaluated by the host into the

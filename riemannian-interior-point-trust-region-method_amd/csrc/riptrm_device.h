@@ -55,7 +55,7 @@ enum St : int {
   // last inner_info (for save_inner_iteration == False rows)
   ST_I_HAS, ST_I_NUM, ST_I_STATUS, ST_I_TR, ST_I_DXTYPE, ST_I_NORMDX, ST_I_MINX, ST_I_MINY,
   ST_I_COMPL, ST_I_HASRATIO, ST_I_RATIO, ST_I_RU, ST_I_DC, ST_I_HASMIN, ST_I_MINEIG,
-  ST_ERROR, ST_LOG_BASE,
+  ST_ERROR, ST_LOG_BASE, ST_RHS,
   ST_N_USED
 };
 constexpr int ST_N = 72;
@@ -114,7 +114,10 @@ inline int64_t pgrid_of(int32_t n) {
 }
 // shared-S MFMA S-pass: K is split over MM_KZ workgroup slices whose partial products land in
 // MM_KZ x 2 x batch x ld slabs, summed in slice order by the state kernel
-constexpr int MM_KZ = 4;  // csrc/riptrm_kernels.hip k_spass_mm: 4 vs 8 slices measured
+#ifndef RIPTRM_MM_KZ
+#define RIPTRM_MM_KZ 4   // A/B builds: -DRIPTRM_MM_KZ=8 (scripts/gpu_r3mm.sh)
+#endif
+constexpr int MM_KZ = RIPTRM_MM_KZ;  // csrc/riptrm_kernels.hip k_spass_mm: 4 vs 8 slices measured
 
 // Symmetric-tile layout: tiles (I, J), I <= J, row by row; full TS x TS tiles except the last
 // tile column (J = nt - 1), which keeps only the wl = round_up(n - (nt - 1) TS, 32) columns that

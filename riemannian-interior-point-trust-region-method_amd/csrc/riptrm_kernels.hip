@@ -622,20 +622,48 @@ __global__ void __launch_bounds__(SP_THREADS, 1) k_spass_sup(DevParams P, int li
 // ------------------------------------------------------------------------------------------
 typedef double dbl4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) unsigned char lds_u8;
-constexpr int MM_WAVES = 8;  // tools/mfma_bench.hip: 8 waves (2 per SIMD) 72.5 us vs 4 waves 81.5 us at n = 4000
+#ifndef RIPTRM_MM_WAVES
+#define RIPTRM_MM_WAVES 16   // A/B builds: -DRIPTRM_MM_WAVES=8 (the round-2 workgroup)
+#endif
+// tools/mfma_bench.hip at n = 4000, 128 right-hand sides (profiles/r3_mfma_tile_sweep.jsonl):
+// 64-row tiles 4 waves 81.5 us, 8 waves (4 x 2 grid) 75.4 us, 16 waves (4 x 4) 70.8 us
+constexpr int MM_WAVES = RIPTRM_MM_WAVES;
 typedef __attribute__((address_space(3))) dbl2 lds_dbl2;
+#ifndef RIPTRM_MM_NST
+#define RIPTRM_MM_NST 3   // A/B builds: -DRIPTRM_MM_NST=2 (the round-2 double buffer)
+#endif
+
+// Wait until at most N of this wave's LDS copies are in flight, then a bare workgroup barrier.
+// __syncthreads() would add a release fence, which waits for every copy (vmcnt(0)) and so would
+// serialise the copy of the step after next with this one.  The "memory" clobber keeps the
+// compiler from moving LDS reads across.
+template <int N>
+__device__ __forceinline__ void mm_wait_barrier() {
+#define MM_WB_CASE(K) else if constexpr (N == K) asm volatile("s_waitcnt vmcnt(" #K ")\n\ts_barrier" ::: "memory");
+  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+  MM_WB_CASE(1) MM_WB_CASE(2) MM_WB_CASE(3) MM_WB_CASE(4) MM_WB_CASE(5) MM_WB_CASE(6) MM_WB_CASE(7)
+  MM_WB_CASE(8) MM_WB_CASE(9) MM_WB_CASE(10) MM_WB_CASE(11) MM_WB_CASE(12)
+#undef MM_WB_CASE
+  else static_assert(N < 0, "mm_wait_barrier: add the count");
+}
 
 template <int WM, int RT>
 struct MmShape {
-  static constexpr int NW = MM_WAVES;                  // waves per workgroup (two per SIMD)
+  static constexpr int NW = MM_WAVES;                  // waves per workgroup (NW / 4 per SIMD)
   static constexpr int CT = 16 * WM;                   // right-hand sides per workgroup
-  static constexpr int NWR = NW < RT / 16 ? NW : RT / 16, NWC = NW / NWR;  // wave grid: rows x columns
+  // wave grid: rows x columns; waves past NWR x NWC (narrow in1 tiles) only copy
+  static constexpr int NWR = NW < RT / 16 ? NW : RT / 16;
+  static constexpr int NWC = NW / NWR < WM ? NW / NWR : WM, NACT = NWR * NWC;
   static constexpr int WMW = WM / NWC;                 // 16-column accumulator rows per wave
   static constexpr int RW = RT / NWR, WN = RW / 16;    // rows per wave, 16-row accumulator columns
   static constexpr int VT = CT * 256;                  // V tile bytes per stage
   static constexpr int STAGE = VT + RT * 256;          // + S tile
-  static constexpr int VP = CT / 4 / NW, SP = RT / 4 / NW;  // glds wave-instructions per wave per stage
-  static_assert(WMW >= 1 && WN >= 1 && VP >= 1 && SP >= 1 && NWR * NWC == NW, "tile shape");
+  // glds wave-instructions (4 rows of 256 B each) per stage: waves < VW copy VP of V's, < SW SP of S's
+  static constexpr int VW = NW < CT / 4 ? NW : CT / 4, VP = CT / 4 / VW;
+  static constexpr int SW = NW < RT / 4 ? NW : RT / 4, SP = RT / 4 / SW;
+  // LDS stages: three where they fit next to the in1 map (64-row tiles: 3 x 48 KiB), else two
+  static constexpr int NST = RIPTRM_MM_NST >= 3 && 3 * STAGE + 32 * 4 <= 160 * 1024 ? 3 : 2;
+  static_assert(WMW >= 1 && WN >= 1 && WM % NWC == 0 && VP * VW * 4 == CT && SP * SW * 4 == RT, "tile shape");
 };
 
 // One tile: right-hand-side columns v = 0..CT-1 of the tile are instance slots slot_of(v) (valid
@@ -646,7 +674,8 @@ __device__ __forceinline__ void mm_tile(const DevParams& P, lds_u8* smem, const 
                                         SlotOf slot_of, int z, int i0, int rows) {
   using Sh = MmShape<WM, RT>;
   constexpr int CT = Sh::CT, WN = Sh::WN, WMW = Sh::WMW, RW = Sh::RW, NWR = Sh::NWR;
-  constexpr int VT = Sh::VT, STAGE = Sh::STAGE, VP = Sh::VP, SP = Sh::SP;
+  constexpr int VT = Sh::VT, STAGE = Sh::STAGE, VP = Sh::VP, SP = Sh::SP, NST = Sh::NST;
+  constexpr int VW = Sh::VW, SW = Sh::SW, NACT = Sh::NACT;
   const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
   const int wr = w % NWR, wc = w / NWR;  // this wave's rows RW wr .. and columns 16 WMW wc ..
   const int r = lane & 15, q = lane >> 4;
@@ -656,7 +685,7 @@ __device__ __forceinline__ void mm_tile(const DevParams& P, lds_u8* smem, const 
 #pragma unroll
   for (int p = 0; p < VP; ++p) {
     const int row = 4 * (VP * w + p) + q;
-    vsrc[p] = vp(P, vk, le_b(lst[slot_of(min(row, nv - 1))])) + 2 * (r ^ (row & 15));
+    vsrc[p] = vp(P, vk, le_b(lst[slot_of(min(row, nv - 1))])) + 2 * (r ^ (row & 15));   // row < CT when w < VW
   }
 #pragma unroll
   for (int p = 0; p < SP; ++p) {
@@ -671,10 +700,12 @@ __device__ __forceinline__ void mm_tile(const DevParams& P, lds_u8* smem, const 
     lds_u8* vb = smem + buf * STAGE;
 #pragma unroll
     for (int p = 0; p < VP; ++p)
-      __builtin_amdgcn_global_load_lds((const void*)(vsrc[p] + k0), vb + 4 * (VP * w + p) * 256, 16, 0, 0);
+      if (VW == Sh::NW || w < VW)   // wave-uniform
+        __builtin_amdgcn_global_load_lds((const void*)(vsrc[p] + k0), vb + 4 * (VP * w + p) * 256, 16, 0, 0);
 #pragma unroll
     for (int p = 0; p < SP; ++p)
-      __builtin_amdgcn_global_load_lds((const void*)(ssrc[p] + k0), vb + VT + 4 * (SP * w + p) * 256, 16, 0, 0);
+      if (SW == Sh::NW || w < SW)
+        __builtin_amdgcn_global_load_lds((const void*)(ssrc[p] + k0), vb + VT + 4 * (SP * w + p) * 256, 16, 0, 0);
   };
   dbl4 acc[WMW][WN];
 #pragma unroll
@@ -682,16 +713,30 @@ __device__ __forceinline__ void mm_tile(const DevParams& P, lds_u8* smem, const 
 #pragma unroll
     for (int c = 0; c < WN; ++c) acc[a][c] = dbl4{0.0, 0.0, 0.0, 0.0};
   // wave-uniform: rows of the tile past n, and column groups past the tile's last column, idle
-  const bool live = i0 + RW * wr < P.n && 16 * WMW * wc < nv;
+  const bool live = w < NACT && i0 + RW * wr < P.n && 16 * WMW * wc < nv;
+  // NST-stage ring: step ch + NST - 1's copy is issued right after the barrier of step ch (the
+  // buffer step ch - 1 read), so a copy has NST - 1 steps of MFMA work to land
   if (lo < hi) issue(lo, 0);
+  if (NST == 3 && lo + 1 < hi) issue(lo + 1, 1);
+  int s = 0;
   for (int ch = lo; ch < hi; ++ch) {
-    const int s = (ch - lo) & 1;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's copies of step ch landed
-    __syncthreads();                                    // everyone's landed; step ch-1's reads done
-    if (ch + 1 < hi) issue(ch + 1, s ^ 1);
+    // this wave's copies of step ch landed (the NST - 2 later steps' may still fly); after the
+    // barrier everyone's have, and step ch - 1's LDS reads are done
+    if (NST == 3 && ch + 1 < hi) {
+      // copies this wave issues per stage (wave-uniform branches, one barrier each)
+      if (w < VW && w < SW) mm_wait_barrier<VP + SP>();
+      else if (w < VW) mm_wait_barrier<VP>();
+      else if (w < SW) mm_wait_barrier<SP>();
+      else mm_wait_barrier<0>();
+    } else {
+      mm_wait_barrier<0>();
+    }
+    if (ch + NST - 1 < hi) issue(ch + NST - 1, s == 0 ? NST - 1 : s - 1);
+    const int sc = s;
+    s = s + 1 == NST ? 0 : s + 1;
     if (!live) continue;
-    const lds_u8* vb = smem + s * STAGE + 16 * WMW * wc * 256;
-    const lds_u8* sb = smem + s * STAGE + VT + RW * wr * 256;
+    const lds_u8* vb = smem + sc * STAGE + 16 * WMW * wc * 256;
+    const lds_u8* sb = smem + sc * STAGE + VT + RW * wr * 256;
     dbl2 fa[2][WMW], fb[2][WN];
     auto frag = [&](int jj, int u) {
       const int off = ((4 * q + jj) ^ r) * 16;
@@ -734,9 +779,9 @@ __device__ __forceinline__ void mm_tile(const DevParams& P, lds_u8* smem, const 
     }
 }
 
-// dynamic LDS: two stages of the in0 tile shape + the in1 column map
+// dynamic LDS: the stages of the in0 tile shape + the in1 column map (in1 tiles' stages are smaller)
 template <int WM0, int RT>
-constexpr int mm_shm() { return 2 * MmShape<WM0, RT>::STAGE + 32 * 4; }
+constexpr int mm_shm() { return MmShape<WM0, RT>::NST * MmShape<WM0, RT>::STAGE + 32 * 4; }
 
 // Grid (1-D): MM_KZ slices x row blocks x (t0 in0 tiles of 16 WM0 columns + t1 in1 tiles of 32).
 // The second right-hand side exists only for the instances that asked for two (le_nrhs): their
@@ -761,7 +806,7 @@ __global__ void __launch_bounds__(64 * MM_WAVES) k_spass_mm(DevParams P, int lis
   }
   // in1 tile: map its 32 columns to the instances asking for a second product, in list order
   const int s0 = (y - t0) * 32;
-  int32_t* map = (int32_t*)(mm_smem_raw + 2 * MmShape<WM0, RT>::STAGE);
+  int32_t* map = (int32_t*)(mm_smem_raw + MmShape<WM0, RT>::NST * MmShape<WM0, RT>::STAGE);
   const int lane = threadIdx.x & 63;
   int n2 = 0;
   for (int c = 0; c < nact; c += 64) {
@@ -1261,6 +1306,7 @@ struct MachineT {
       }
     }
     cadd(ST_PASSES, 1.0);
+    cadd(ST_RHS, (double)nrhs);
     return ACT_YIELD;
   }
 
@@ -1274,6 +1320,7 @@ struct MachineT {
       o[RIPTRM_STAT_INNER_ITERS] = g[ST_INNER_TOTAL];
       o[RIPTRM_STAT_TCG_ITERS] = g[ST_TCG_TOTAL];
       o[RIPTRM_STAT_PASSES] = g[ST_PASSES];
+      o[RIPTRM_STAT_RHS] = g[ST_RHS];
       o[RIPTRM_STAT_STOP_CODE] = g[ST_STOP_CODE];
       o[RIPTRM_STAT_STOP_RUNTIME] = g[ST_STOP_RUNTIME];
       o[RIPTRM_STAT_FINAL_RESIDUAL] = g[ST_RESIDUAL];
@@ -2655,6 +2702,7 @@ __device__ __noinline__ void lean_tcg_run(LeanArgs a, LeanIO* io, const lds_f64*
     hot[ST_J] = ts.j;
     if (stop != TCG_CONTINUE) hot[ST_TCG_STOP] = stop;
     a.gcold[ST_PASSES] += passes;
+    a.gcold[ST_RHS] += passes;   // lean passes carry one right-hand side
     io->k = k;
     io->epoch = epoch;
     io->clk = clk;

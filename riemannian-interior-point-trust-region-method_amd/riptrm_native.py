@@ -140,11 +140,13 @@ CONST = header_constants() if os.path.exists(HEADER_PATH) else {}
 _lib: Optional[ctypes.CDLL] = None
 
 
-def load(path: str = LIB_PATH) -> ctypes.CDLL:
-    """Load the HIP library (cached).  Raises RuntimeError if it is missing."""
+def load(path: Optional[str] = None) -> ctypes.CDLL:
+    """Load the HIP library (cached).  Raises RuntimeError if it is missing.  RIPTRM_LIB names an
+    alternative in-tree build (A/B measurements of compile-time variants)."""
     global _lib
     if _lib is not None:
         return _lib
+    path = path or os.environ.get("RIPTRM_LIB") or LIB_PATH
     if not os.path.exists(path):
         raise RuntimeError(f"libriptrm_hip.so not built at {path}; run __graft_entry__.build() "
                            "(hipcc --offload-arch=gfx950). There is no CPU fallback.")

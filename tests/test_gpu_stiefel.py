@@ -72,3 +72,26 @@ def test_stiefel_rejects_bad_shapes():
     with pytest.raises(ValueError):
         st.projection(torch.zeros(2, 8, 3, dtype=torch.float64, device="cuda"),
                       torch.zeros(2, 8, 3, dtype=torch.float64, device="cuda"))
+
+
+@pytest.mark.parametrize("cond", [1e2, 1e5])
+def test_stiefel_retraction_conditioning(cond):
+    """qf(A) for A of condition number `cond` (passed as X = A, U = 0): at 1e2 the second
+    CholeskyQR pass takes its first-order factor (|Q1^T Q1 - I| ~ 1e-14), at 1e5 (~1e-6) the exact
+    factor runs.  Both against the Householder restatement; CholeskyQR2 loses ~cond * eps."""
+    from stiefel import StiefelBatch
+    n, p, B = 200, 50, 4
+    M = Stiefel(n, p)
+    rs = np.random.RandomState(11)
+    A = []
+    for _ in range(B):
+        Q0, _ = np.linalg.qr(rs.randn(n, p))
+        V, _ = np.linalg.qr(rs.randn(p, p))
+        A.append(Q0 @ np.diag(np.logspace(0, -np.log10(cond), p)) @ V.T)
+    A = np.stack(A)
+    st = StiefelBatch(n, p)
+    R = st.retraction(_t(A), _t(np.zeros_like(A))).cpu().numpy()
+    for b in range(B):
+        ref = M.retraction(A[b], np.zeros((n, p)))
+        assert np.abs(R[b] - ref).max() <= 1e-15 * cond * 100, (b, np.abs(R[b] - ref).max())
+        assert np.abs(R[b].T @ R[b] - np.eye(p)).max() <= 1e-13

@@ -313,6 +313,121 @@ __global__ void __launch_bounds__(64 * NW) k_mm3(const double* __restrict__ S, c
     }
 }
 
+// The solver's tile (csrc/riptrm_kernels.hip mm_tile) with the wave grid as parameters: NWR x NWC
+// waves over RT rows x 128 columns (WMW = 8 / NWC 16-column and WN = RT / NWR / 16 16-row
+// accumulators per wave), NST-stage LDS ring, bare barrier after an explicit vmcnt wait.
+// SCHED interleaves each fragment read group with the previous group's MFMAs
+// (__builtin_amdgcn_sched_group_barrier: 1 DS read, then MFMAs).
+template <int RT, int NWR, int NWC, int NST, bool SCHED>
+__global__ void __launch_bounds__(64 * NWR * NWC) k_mm4(const double* __restrict__ S, const double* __restrict__ V,
+                                                        double* __restrict__ Y, int n, int rows, int64_t ld, int C, int kz) {
+  constexpr int NW = NWR * NWC, WMW = 8 / NWC, RW = RT / NWR, WN = RW / 16, STAGE = M3<RT>::STAGE;
+  constexpr int VP = 32 / NW, SP = RT / 4 / NW;
+  static_assert(VP >= 1 && SP >= 1 && WMW >= 1 && WN >= 1, "shape");
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+  lds_u8* smem = (lds_u8*)smem_raw;
+  const int L = blockIdx.x, z = L % kz, rest = L / kz;
+  const int nrb = (rows + RT - 1) / RT;
+  const int i0 = (rest % nrb) * RT, c0 = (rest / nrb) * 128;
+  Y += (int64_t)z * C * ld;
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = w % NWR, wc = w / NWR;
+  const int r = lane & 15, q = lane >> 4;
+  const double* vsrc[VP];
+  const double* ssrc[SP];
+#pragma unroll
+  for (int p = 0; p < VP; ++p) {
+    const int row = 4 * (VP * w + p) + q;
+    vsrc[p] = V + (int64_t)min(c0 + row, C - 1) * ld + 2 * (r ^ (row & 15));
+  }
+#pragma unroll
+  for (int p = 0; p < SP; ++p) {
+    const int row = 4 * (SP * w + p) + q;
+    ssrc[p] = S + (int64_t)min(i0 + row, rows - 1) * ld + 2 * (r ^ (row & 15));
+  }
+  const int nch = (int)(ld / 32), per = (nch + kz - 1) / kz;
+  const int lo = z * per, hi = min(nch, lo + per);
+  auto issue = [&](int ch, int buf) {
+    const int64_t k0 = (int64_t)ch * 32;
+    lds_u8* vb = smem + buf * STAGE;
+#pragma unroll
+    for (int p = 0; p < VP; ++p)
+      __builtin_amdgcn_global_load_lds((const void*)(vsrc[p] + k0), (lds_u8*)(vb + 4 * (VP * w + p) * 256), 16, 0, 0);
+#pragma unroll
+    for (int p = 0; p < SP; ++p)
+      __builtin_amdgcn_global_load_lds((const void*)(ssrc[p] + k0), (lds_u8*)(vb + M3_VT + 4 * (SP * w + p) * 256), 16, 0, 0);
+  };
+  dbl4 acc[WMW][WN];
+#pragma unroll
+  for (int a = 0; a < WMW; ++a)
+#pragma unroll
+    for (int b = 0; b < WN; ++b) acc[a][b] = dbl4{0.0, 0.0, 0.0, 0.0};
+  const bool live = i0 + RW * wr < n;
+  if (lo < hi) issue(lo, 0);
+  if (NST == 3 && lo + 1 < hi) issue(lo + 1, 1);
+  int s = 0;
+  for (int ch = lo; ch < hi; ++ch) {
+    if (NST == 3 && ch + 1 < hi) {
+#define WB(K) if constexpr (VP + SP == K) asm volatile("s_waitcnt vmcnt(" #K ")\n\ts_barrier" ::: "memory");
+      WB(1) WB(2) WB(3) WB(4) WB(5) WB(6) WB(7) WB(8) WB(9) WB(10) WB(12)
+#undef WB
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+    }
+    if (ch + NST - 1 < hi) issue(ch + NST - 1, s == 0 ? NST - 1 : s - 1);
+    const int sc = s;
+    s = s + 1 == NST ? 0 : s + 1;
+    if (!live) continue;
+    const lds_u8* vb = smem + sc * STAGE + 16 * WMW * wc * 256;
+    const lds_u8* sb = smem + sc * STAGE + M3_VT + RW * wr * 256;
+    dbl2 fa[2][WMW], fb[2][WN];
+    auto frag = [&](int jj, int u) {
+      const int off = ((4 * q + jj) ^ r) * 16;
+#pragma unroll
+      for (int a = 0; a < WMW; ++a) fa[u][a] = *(const lds_dbl2*)(vb + (16 * a + r) * 256 + off);
+#pragma unroll
+      for (int b = 0; b < WN; ++b) fb[u][b] = *(const lds_dbl2*)(sb + (16 * b + r) * 256 + off);
+    };
+    frag(0, 0);
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) {
+      const int u = jj & 1;
+      if (jj < 3) frag(jj + 1, u ^ 1);
+#pragma unroll
+      for (int mm = 0; mm < 2; ++mm)
+#pragma unroll
+        for (int a = 0; a < WMW; ++a)
+#pragma unroll
+          for (int b = 0; b < WN; ++b)
+            acc[a][b] = __builtin_amdgcn_mfma_f64_16x16x4f64(mm ? fa[u][a].y : fa[u][a].x, mm ? fb[u][b].y : fb[u][b].x,
+                                                             acc[a][b], 0, 0, 0);
+      if constexpr (SCHED) {
+        if (jj < 3) {
+          // next group's reads spread over this group's MFMAs
+#pragma unroll
+          for (int t = 0; t < WMW + WN; ++t) {
+            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);   // DS read
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // MFMA
+          }
+          __builtin_amdgcn_sched_group_barrier(0x008, 2 * WMW * WN - (WMW + WN) > 0 ? 2 * WMW * WN - (WMW + WN) : 0, 0);
+        }
+      }
+    }
+  }
+  if (!live) return;
+#pragma unroll
+  for (int a = 0; a < WMW; ++a)
+#pragma unroll
+    for (int b = 0; b < WN; ++b) {
+      const int i = i0 + RW * wr + 16 * b + r;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int c = c0 + 16 * (WMW * wc + a) + q + 4 * g;
+        if (i < n && c < C) Y[(int64_t)c * ld + i] = acc[a][b][g];
+      }
+    }
+}
+
 // sum of KZ partial slabs in fixed order into slab 0
 __global__ void k_red(double* Y, int64_t slab, int kz) {
   const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
@@ -374,6 +489,23 @@ void launch_mm3(const double* S, const double* V, double* Y, int n, int rows, in
   }
 }
 
+template <int RT, int NWR, int NWC, int NST, int KZ, bool SCHED = false>
+void launch_mm4(const double* S, const double* V, double* Y, int n, int rows, int64_t ld, int C, hipStream_t st) {
+  static bool attr = false;
+  if (!attr) {
+    CHK(hipFuncSetAttribute((const void*)k_mm4<RT, NWR, NWC, NST, SCHED>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            M3<RT>::STAGE * NST));
+    attr = true;
+  }
+  const int nrb = (rows + RT - 1) / RT, ncb = (C + 127) / 128;
+  hipLaunchKernelGGL((k_mm4<RT, NWR, NWC, NST, SCHED>), dim3(nrb * ncb * KZ), dim3(64 * NWR * NWC), M3<RT>::STAGE * NST, st,
+                     S, V, Y, n, rows, ld, C, KZ);
+  if (KZ > 1 && g_red) {
+    const int64_t slab = (int64_t)C * ld;
+    hipLaunchKernelGGL(k_red, dim3((unsigned)((slab + 255) / 256)), dim3(256), 0, st, Y, slab, KZ);
+  }
+}
+
 int main(int argc, char** argv) {
   CHK(hipFuncSetAttribute((const void*)k_mm3<128, false>, hipFuncAttributeMaxDynamicSharedMemorySize, M3<128>::STAGE * 2));
   CHK(hipFuncSetAttribute((const void*)k_mm3<128, true>, hipFuncAttributeMaxDynamicSharedMemorySize, M3<128>::STAGE * 2));
@@ -411,18 +543,24 @@ int main(int argc, char** argv) {
     hipEvent_t a, b;
     CHK(hipEventCreate(&a));
     CHK(hipEventCreate(&b));
-    for (int waves : {1024, 2048, 4096}) {
+    auto probe = [&](auto kern, int nacc, int waves) {
       const int iters = 4000;
-      hipLaunchKernelGGL(k_peak<4>, dim3(waves / 4), dim3(256), 0, 0, Y, 10);
+      hipLaunchKernelGGL(kern, dim3(waves / 4), dim3(256), 0, 0, Y, 10);
       CHK(hipEventRecord(a, 0));
-      hipLaunchKernelGGL(k_peak<4>, dim3(waves / 4), dim3(256), 0, 0, Y, iters);
+      hipLaunchKernelGGL(kern, dim3(waves / 4), dim3(256), 0, 0, Y, iters);
       CHK(hipEventRecord(b, 0));
       CHK(hipEventSynchronize(b));
       float ms = 0;
       CHK(hipEventElapsedTime(&ms, a, b));
-      const double fl = (double)waves * iters * 4 * 2048.0;
-      printf("{\"variant\": \"mfma_f64_16x16x4 peak probe\", \"waves\": %d, \"TFLOPs\": %.2f}\n", waves, fl / (ms * 1e-3) / 1e12);
-    }
+      const double fl = (double)waves * iters * nacc * 2048.0;
+      printf("{\"variant\": \"mfma_f64_16x16x4 peak probe\", \"chains\": %d, \"waves\": %d, \"TFLOPs\": %.2f}\n", nacc, waves,
+             fl / (ms * 1e-3) / 1e12);
+    };
+    for (int waves : {1024, 2048, 4096}) probe(k_peak<4>, 4, waves);
+    for (int waves : {1024, 2048}) probe(k_peak<8>, 8, waves);
+    probe(k_peak<16>, 16, 1024);
+    probe(k_peak<2>, 2, 2048);
+    probe(k_peak<1>, 1, 4096);
   }
   CHK(hipMemcpy(S, hS.data(), hS.size() * 8, hipMemcpyHostToDevice));
   CHK(hipMemcpy(V, hV.data(), hV.size() * 8, hipMemcpyHostToDevice));
@@ -444,6 +582,16 @@ int main(int argc, char** argv) {
       {"glds r64 kz4", launch_mm3<64, false, 4>},   {"glds r64 pf kz4", launch_mm3<64, true, 4>},
       {"glds r64 pf kz8", launch_mm3<64, true, 8>}, {"glds r128 pf kz16", launch_mm3<128, true, 16>},
       {"glds r128 pf kz8 nw8", launch_mm3<128, true, 8, 8>}, {"glds r64 pf kz8 nw8", launch_mm3<64, true, 8, 8>},
+      // t4: the solver's tile shape family (rows x cols wave grid, stages, K slices)
+      {"t4 r64 4x2 st2 kz4", launch_mm4<64, 4, 2, 2, 4>},  {"t4 r64 4x2 st3 kz4", launch_mm4<64, 4, 2, 3, 4>},
+      {"t4 r64 4x2 st2 kz4 sched", launch_mm4<64, 4, 2, 2, 4, true>},
+      {"t4 r64 2x4 st2 kz4", launch_mm4<64, 2, 4, 2, 4>},  {"t4 r64 4x4 st2 kz4", launch_mm4<64, 4, 4, 2, 4>},
+      {"t4 r64 2x8 st2 kz4", launch_mm4<64, 2, 8, 2, 4>},  {"t4 r64 4x1 st2 kz4", launch_mm4<64, 4, 1, 2, 4>},
+      {"t4 r64 2x2 st2 kz4", launch_mm4<64, 2, 2, 2, 4>},  {"t4 r64 2x4 st3 kz4", launch_mm4<64, 2, 4, 3, 4>},
+      {"t4 r128 8x1 st2 kz8", launch_mm4<128, 8, 1, 2, 8>}, {"t4 r128 4x2 st2 kz8", launch_mm4<128, 4, 2, 2, 8>},
+      {"t4 r128 8x2 st2 kz8", launch_mm4<128, 8, 2, 2, 8>}, {"t4 r128 4x4 st2 kz8", launch_mm4<128, 4, 4, 2, 8>},
+      {"t4 r128 4x2 st2 kz4", launch_mm4<128, 4, 2, 2, 4>}, {"t4 r32 2x4 st3 kz4", launch_mm4<32, 2, 4, 3, 4>},
+      {"t4 r32 2x4 st3 kz2", launch_mm4<32, 2, 4, 3, 2>},
   };
   hipEvent_t e0, e1;
   CHK(hipEventCreate(&e0));
