@@ -783,10 +783,10 @@ __device__ __forceinline__ void mm_tile(const DevParams& P, lds_u8* smem, const 
 template <int WM0, int RT>
 constexpr int mm_shm() { return MmShape<WM0, RT>::NST * MmShape<WM0, RT>::STAGE + 32 * 4; }
 
-// Grid (1-D): MM_KZ slices x row blocks x (t0 in0 tiles of 16 WM0 columns + t1 in1 tiles of 32).
-// The second right-hand side exists only for the instances that asked for two (le_nrhs): their
-// in1 columns are compacted in list order into 32-wide tiles, so a pass where a few instances
-// need two products costs a narrow tile, not a second full-width one.
+// Grid (1-D): MM_KZ slices x row blocks x t0 in0 tiles of 16 WM0 columns.  The second right-hand
+// side exists only for the instances that asked for two (le_nrhs): their in1 columns are
+// compacted in list order into 32-wide tiles, run by the same workgroups after their in0 tile, so
+// a pass where a few instances need two products costs a narrow tile, not a second full-width one.
 template <int WM0, int RT>
 __global__ void __launch_bounds__(64 * MM_WAVES) k_spass_mm(DevParams P, int list_in, int zero_cnt, int bound) {
   extern __shared__ __attribute__((aligned(16))) unsigned char mm_smem_raw[];
@@ -798,28 +798,38 @@ __global__ void __launch_bounds__(64 * MM_WAVES) k_spass_mm(DevParams P, int lis
   const int L = blockIdx.x, z = L % MM_KZ, rest = L / MM_KZ;
   const int i0 = (rest % nrb) * RT, y = rest / nrb;
   const int32_t* lst = P.lists + (int64_t)list_in * P.batch;
-  if (y < t0) {
-    const int s0 = y * 16 * WM0;
-    if (s0 >= nact) return;
+  const int s0 = y * 16 * WM0;
+  if (s0 < nact)
     mm_tile<WM0, RT>(P, smem, lst, V_IN0, 0, min(16 * WM0, nact - s0), [&](int v) { return s0 + v; }, z, i0, rows);
-    return;
-  }
-  // in1 tile: map its 32 columns to the instances asking for a second product, in list order
-  const int s0 = (y - t0) * 32;
+  // in1 tiles j = y, y + t0, ... of this row block and slice, after the in0 one: their 32 columns
+  // are the instances asking for a second product, in list order.  Run by the in0 workgroups
+  // rather than as workgroups of their own: in most passes no instance asks, and a grid of idle
+  // in1 workgroups, each holding the in0 tile's LDS, dispatched behind the in0 tiles costs
+  // ~8 us per launch at n = 4000 (profiles/r3_shared_16w_ab.jsonl vs r3_shared_in1_inline_ab.jsonl).
+  const int t1 = (bound + 31) / 32;
+  if (y >= t1) return;
   int32_t* map = (int32_t*)(mm_smem_raw + MmShape<WM0, RT>::NST * MmShape<WM0, RT>::STAGE);
   const int lane = threadIdx.x & 63;
-  int n2 = 0;
+  int n2 = 0;   // instances asking for two products (the same in every wave)
   for (int c = 0; c < nact; c += 64) {
-    const int sl = c + lane;
-    const bool two = sl < nact && le_nrhs(lst[sl]) == 2;
-    const uint64_t m = __ballot(two);
-    const int k = n2 + __popcll(m & ((1ull << lane) - 1));
-    if (two && threadIdx.x < 64 && k >= s0 && k < s0 + 32) map[k - s0] = sl;
-    n2 += __popcll(m);
+    const bool two = c + lane < nact && le_nrhs(lst[c + lane]) == 2;
+    n2 += __popcll(__ballot(two));
   }
-  if (s0 >= n2) return;  // n2 is the same in every wave: the workgroup leaves together
-  __syncthreads();
-  mm_tile<2, RT>(P, smem, lst, V_IN1, 1, min(32, n2 - s0), [&](int v) { return (int)map[v]; }, z, i0, rows);
+  for (int j = y; j < t1 && 32 * j < n2; j += t0) {
+    const int u0 = 32 * j;
+    __syncthreads();   // the previous tile's LDS reads (and map reads) are done
+    int k0 = 0;
+    for (int c = 0; c < nact; c += 64) {
+      const int sl = c + lane;
+      const bool two = sl < nact && le_nrhs(lst[sl]) == 2;
+      const uint64_t m = __ballot(two);
+      const int k = k0 + __popcll(m & ((1ull << lane) - 1));
+      if (two && threadIdx.x < 64 && k >= u0 && k < u0 + 32) map[k - u0] = sl;
+      k0 += __popcll(m);
+    }
+    __syncthreads();
+    mm_tile<2, RT>(P, smem, lst, V_IN1, 1, min(32, n2 - u0), [&](int v) { return (int)map[v]; }, z, i0, rows);
+  }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -3427,8 +3437,8 @@ static int launch_gemv(riptrm_ctx* c, hipStream_t st, int list_in, int zero_cnt,
     const int rows = rows_of(c->P.n);
     const bool rt128 = (int64_t)((rows + 127) / 128) * MM_KZ >= c->ncu;
     const int nrb = rt128 ? (rows + 127) / 128 : (rows + 63) / 64;
-    const int t0 = bound > 32 ? (bound + 127) / 128 : (bound + 31) / 32, t1 = (bound + 31) / 32;
-    const dim3 grid((unsigned)(nrb * (t0 + t1) * MM_KZ));
+    const int t0 = bound > 32 ? (bound + 127) / 128 : (bound + 31) / 32;
+    const dim3 grid((unsigned)(nrb * t0 * MM_KZ));   // in1 tiles run inside these workgroups
     if (bound > 32) {
       if (rt128)
         hipLaunchKernelGGL((k_spass_mm<8, 128>), grid, dim3(64 * MM_WAVES), (mm_shm<8, 128>()), st, c->P, list_in, zero_cnt, bound);
