@@ -600,18 +600,18 @@ __global__ void __launch_bounds__(SP_THREADS, 1) k_spass_sup(DevParams P, int li
 // v_mfma_f64_16x16x4_f64: A = 16 right-hand sides x 4 k, B = 4 k x 16 rows of S (S is
 // symmetric, so row i of S is column i of S^T), D = 16 x 16 fp64 accumulators.
 //
-// A workgroup (8 waves, two per SIMD) owns CT = 16 WM right-hand sides x RT rows of S over one
+// A workgroup (MM_WAVES = 16 waves, four per SIMD) owns CT = 16 WM right-hand sides x RT rows of S over one
 // of MM_KZ K slices.  Each 32-deep K step stages V[CT][32] and S[RT][32] into LDS with
 // global_load_lds_dwordx4 (256-B rows; 16-B chunk c of row r kept at chunk c ^ (r & 15), written
 // through the SOURCE address since the LDS side of the copy is lane-linear, so the fragment reads
-// below are bank-conflict free), double-buffered: step t+1's copy is in flight while the waves
-// run step t's MFMAs out of LDS, one barrier per step.  The waves form a rows x columns grid over
-// the tile (8 x 1 for 128-row tiles: 16 rows x all CT columns each; 4 x 2 for 64-row tiles, the
-// shape at n = 4000 where 4 K slices x 63 row blocks fill the chip) and read, for MFMA pair jj,
+// below are bank-conflict free), in a ring of NST = 3 stages where it fits LDS (else 2): step
+// t + NST - 1's copy is in flight while the waves run step t's MFMAs out of LDS, one barrier per
+// step.  The waves form a rows x columns grid over the tile (8 x 2 for 128-row tiles; 4 x 4 for
+// 64-row tiles, the shape at n = 4000 where 4 K slices x 63 row blocks fill the chip) and read, for MFMA pair jj,
 // lane (r, q)'s 16 B at k = 8q + 2jj: MFMA m = 2 jj + {0,1} sums k in {m, 8+m, 16+m, 24+m} — the
 // same order for every kernel shape, so an instance's product does not depend on CT / RT or on
 // the other right-hand sides.  The next pair's fragments are read while the current pair's
-// MFMAs issue, and the SIMD's second wave covers one wave's LDS reads and barrier wait.  Partial
+// MFMAs issue, and the SIMD's other waves cover one wave's LDS reads and barrier wait.  Partial
 // slabs of the MM_KZ slices are added in slice order by the state kernel (deterministic, no
 // atomics).  Linear block id -> slice = id % MM_KZ, so a slice (and the V columns it reads)
 // stays on one XCD.  4 slices rather than 8: the state kernel adds half the slabs (k_state 37.9 ->
