@@ -551,6 +551,20 @@ def bench_stiefel(args, world, rank, dev, dist):
     nr, s16 = -(-n // 16) * 16, 16 * (-(-p // 16))
     fits = (nr * s16 + s16 * s16 + (s16 // 16) * (s16 // 16 + 1) // 2 * 256) * 8 <= 160 * 1024
     retr_kernel = ("k_st_retr2" if fits and os.environ.get("RIPTRM_STIEFEL_RETR", "") != "r1" else "k_st_retr_r")
+    # k_st_proj3 (X and U resident in LDS) for 49 <= p <= 64, n <= 224 (csrc/riptrm_stiefel.hip proj3_ok)
+    proj_kernel = ("k_st_proj3" if -(-p // 16) == 4 and n * p % 2 == 0 and -(-n // 16) <= 14 and
+                   2 * n * p + (0 if n * p >= 64 * 64 else 64 * 64) <= 160 * 1024 // 8 and
+                   os.environ.get("RIPTRM_STIEFEL_PROJ", "") != "r2" else "k_st_proj")
+    # HBM bytes per launch from the committed PMC passes of this exact shape (FETCH_SIZE doubled
+    # per MI355X_MICROARCH.md, + WRITE_SIZE); None for any other shape
+    traffic = {}
+    pmc_path = os.path.join(ROOT, "profiles", "r3_stiefel_pmc.json")
+    if os.path.exists(pmc_path):
+        pm = json.load(open(pmc_path))
+        if (pm.get("n"), pm.get("p"), pm.get("B")) == (n, p, B * 1):
+            for kname, m in pm["kernels"].items():
+                if "read_bytes_corrected" in m and "write_bytes" in m:
+                    traffic[kname.split("::")[-1].split("<")[0]] = m["read_bytes_corrected"] + m["write_bytes"]
     # CPU baseline: the pymanopt restatement (oracle/stiefel_oracle.py, NumPy) on the host, over the
     # same points until ~2 s have passed (a bounded sample; BLAS threads as configured)
     from oracle.stiefel_oracle import Stiefel as _CpuStiefel
@@ -584,12 +598,13 @@ def bench_stiefel(args, world, rank, dev, dist):
                      "frac": max(hbm_floor, mfma_floor) / tp,
                      "hbm_floor_us": hbm_floor * 1e6, "mfma_floor_us": mfma_floor * 1e6,
                      "mfma_achieved_tflops": tfs,
-                     "traffic": None, "kernel": "k_st_proj (U - X sym(X^T U), one workgroup per point)"},
+                     "traffic": traffic.get(proj_kernel),
+                     "kernel": f"{proj_kernel} (U - X sym(X^T U), one workgroup per point)"},
         "cpu_baseline": cpu,
         "detail": {"retractions_per_s": B * world / tr, "retraction_ms": tr * 1e3,
                    "retraction_roofline": {"bound": "hbm", "achieved": 3.0 * n * p * 8 * B / tr / 1e9,
                                            "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": hbm_floor / tr,
-                                           "kernel": retr_kernel},
+                                           "traffic": traffic.get(retr_kernel), "kernel": retr_kernel},
                    "retraction_cpu_per_s": cpu_retr,
                    "retraction_note": "CholeskyQR2, latency-bound: two p-step factorisations per point, one point "
                                       "per CU"},
