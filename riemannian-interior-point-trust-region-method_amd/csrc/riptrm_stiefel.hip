@@ -50,6 +50,7 @@ __device__ __forceinline__ Smem smem_of(double* base_generic) {
 
 typedef double dbl4 __attribute__((ext_vector_type(4)));
 typedef double dbl2 __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(3))) dbl2 lds_dbl2;
 
 // Diagnostic builds only (tools/stiefel_stamps.hip defines ST_STAMPS): s_memtime at phase ends,
 // thread 0 of each workgroup, into a buffer nothing else reads.
@@ -695,6 +696,12 @@ __device__ __forceinline__ void r2_gram(lds_f64* As, lds_f64* Gm, lds_f64* red, 
 #define RIPTRM_ST_FB 2   // measured: 1 -> 75.7k, 2 -> 69.3k, 4 -> 77.6k ticks per factor at p = 50
 #endif
 constexpr int FB = RIPTRM_ST_FB;
+// the factor of k_st_retr2: 0 = the 8-wave exchange (r2_factor_inverse, default); 1 = one wave, no
+// barrier per step (r2_factor_inverse_1w), measured 159k vs 69k ticks per factor at (200, 50)
+// (profiles/r3_stiefel_factor_1wave_stamps.jsonl).  A/B: tools/stiefel_stamps.hip -DRIPTRM_ST_FACTOR=1
+#ifndef RIPTRM_ST_FACTOR
+#define RIPTRM_ST_FACTOR 0
+#endif
 
 static_assert(FB <= 4 && 8 % FB == 0, "the exchange alternates 2 buffers within a group of 8 rows");
 
@@ -806,6 +813,72 @@ __device__ __forceinline__ void r2_factor_inverse(lds_f64* Gm, lds_f64* xch, int
     const int i = 8 * w + r;
     if (i < S && l < S) Gm[l * S + i] = e[r];   // W[j][i] = E[i][j]
   }
+  __syncthreads();
+}
+
+// The same factor on ONE wave, no barrier per step (r2_factor_inverse exchanges every pivot column
+// across the 8 waves: publish -> barrier -> read, ~1.4k ticks per column).  Lane i holds row i in
+// place: R[j] = -E[i][j] for the columns already eliminated (j < k) and G[i][j] - delta_ij for the
+// rest.  With that storage the Gauss-Jordan step is ONE uniform formula over the whole row,
+// R_i[j] -= m_i R_k[j] with m_i = G_ik / G_kk: at j < k it is E_i -= m_i E_k (both negated), at
+// j > k G_i -= m_i G_k (the diagonal offset rides along), and at j = k it turns G_ik into -E_ik =
+// m_i because R_k[k] = G_kk - 1.  Per step lane k writes its row to LDS and every lane reads it
+// back (one wave's LDS traffic is in order, so no wait or barrier sits between the two).
+// Not inlined, and called by wave 0 only: inlined next to the kernel's other phases the 64-double
+// row did not fit beside their live values (spills in the step loop); as a callee only the
+// callee-saved registers go to scratch, once, in the one wave that calls it.
+template <int P16>
+__device__ __noinline__ void r2_factor_1w_body(lds_f64* Gm, lds_f64* xch, int p) {
+  constexpr int S = 16 * P16;
+  const int l = threadIdx.x & 63;
+  {
+    double R[S];
+    const int lr = l < S ? l : 0;
+#pragma unroll
+    for (int j = 0; j < S; ++j) R[j] = Gm[lr * S + j] - (l == j ? 1.0 : 0.0);
+    double piv = 1.0;
+    for (int k = 0; k < p; ++k) {
+      if (l == k) {
+#pragma unroll
+        for (int q = 0; q < S / 2; ++q)
+          if (2 * q < p) *(lds_dbl2*)(xch + 2 * q) = dbl2{R[2 * q], R[2 * q + 1]};
+      }
+      const double dk = xch[k] + 1.0;   // G_kk
+      const double bi = xch[lr];        // G_ki = G_ik
+      if (l == k) piv = dk;
+      if (l > k && l < p) {
+        const double m = bi / dk;
+        // 16 columns at a time: their reads, then their FMAs (the scheduler would otherwise hoist
+        // every read of the row and spill)
+#pragma unroll
+        for (int q0 = 0; q0 < S / 2; q0 += 8) {
+          if (2 * q0 >= p) break;   // uniform
+          dbl2 b[8];
+#pragma unroll
+          for (int q = 0; q < 8; ++q) b[q] = *(const lds_dbl2*)(xch + 2 * (q0 + q));
+#pragma unroll
+          for (int q = 0; q < 8; ++q) {
+            R[2 * (q0 + q)] = __builtin_fma(-m, b[q].x, R[2 * (q0 + q)]);
+            R[2 * (q0 + q) + 1] = __builtin_fma(-m, b[q].y, R[2 * (q0 + q) + 1]);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+    }
+    // row l of E: -R[j] left of the diagonal, 1 on it, scaled by G_ll^-1/2 (rows past p: identity);
+    // W[j][l] = E[l][j]
+    const double sc = l < p ? 1.0 / sqrt(piv) : 1.0;
+#pragma unroll
+    for (int j = 0; j < S; ++j) {
+      const double v = (j < l && l < p) ? -R[j] : (j == l ? 1.0 : 0.0);
+      if (l < S) Gm[j * S + l] = v * sc;
+    }
+  }
+}
+
+template <int P16>
+__device__ __forceinline__ void r2_factor_inverse_1w(lds_f64* Gm, lds_f64* xch, int p) {
+  if ((threadIdx.x >> 6) == 0) r2_factor_1w_body<P16>(Gm, xch, p);
   __syncthreads();
 }
 
@@ -923,13 +996,21 @@ __global__ void __launch_bounds__(T) k_st_retr2(int n, int p, int64_t stride, co
   ST_STAMP(1);
   r2_gram<P16>(As, Gm, red, NR);
   ST_STAMP(2);
+#if RIPTRM_ST_FACTOR == 1
+  r2_factor_inverse_1w<P16>(Gm, red, p);
+#else
   r2_factor_inverse<P16>(Gm, red, p);
+#endif
   ST_STAMP(3);
   r2_apply<P16, false>(As, Gm, NR, n, p, out + o);
   ST_STAMP(4);
   r2_gram<P16>(As, Gm, red, NR);
   ST_STAMP(5);
+#if RIPTRM_ST_FACTOR == 1
+  if (!r2_inverse_first_order<P16>(Gm, red, p)) r2_factor_inverse_1w<P16>(Gm, red, p);
+#else
   if (!r2_inverse_first_order<P16>(Gm, red, p)) r2_factor_inverse<P16>(Gm, red, p);
+#endif
   ST_STAMP(6);
   r2_apply<P16, true>(As, Gm, NR, n, p, out + o);
   ST_STAMP(7);
