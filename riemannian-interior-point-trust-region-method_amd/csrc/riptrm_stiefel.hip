@@ -263,6 +263,36 @@ __device__ __forceinline__ void p3_unit(int w, int& I0, int& J0, int& I1, int& J
   }
 }
 
+// the Gram of k_st_proj3 over the 4-row groups [g0, g1), GB groups per batch of LDS reads; RMASK: a
+// batch runs past row rend = min(n, 4 g1), those rows are masked
+constexpr int P3_GB = 5;
+template <bool RMASK>
+__device__ __forceinline__ void p3_gram(const lds_f64* Xs, const lds_f64* Us, int n, int p, int kk, int a0, int b0,
+                                        int a1, int b1, int gs, int ge, dbl4& acc0, dbl4& acc1) {
+  constexpr int GB = P3_GB;
+  const int rend = 4 * ge < n ? 4 * ge : n;
+  for (int g0 = gs; g0 < ge; g0 += GB) {
+    double xa0[GB], ub0[GB], xa1[GB], ub1[GB];
+#pragma unroll
+    for (int u = 0; u < GB; ++u) {
+      const int r = 4 * (g0 + u) + kk;
+      const lds_f64* xr = Xs + (!RMASK || r < rend ? r : rend - 1) * p;
+      const lds_f64* ur = Us + (!RMASK || r < rend ? r : rend - 1) * p;
+      const double rm = RMASK ? mask01(r < rend) : 1.0;
+      xa0[u] = RMASK ? xr[a0] * rm : xr[a0];
+      ub0[u] = ur[b0];
+      xa1[u] = RMASK ? xr[a1] * rm : xr[a1];
+      ub1[u] = ur[b1];
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int u = 0; u < GB; ++u) {
+      acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(xa0[u], ub0[u], acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(xa1[u], ub1[u], acc1, 0, 0, 0);
+    }
+  }
+}
+
 template <int P16>
 __global__ void __launch_bounds__(T) k_st_proj3(int n, int p, int64_t stride, const double* X, const double* U,
                                                 double* out) {
@@ -275,7 +305,8 @@ __global__ void __launch_bounds__(T) k_st_proj3(int n, int p, int64_t stride, co
   const int t = threadIdx.x, l = t & 63, w = t >> 6, c = l & 15, kk = l >> 4;
   const int64_t o = (int64_t)blockIdx.x * stride;
   ST_STAMP(0);
-  {   // X, U -> LDS: np / 2 16-byte chunks each, every load of a batch in flight together
+  {   // X, U -> LDS: np / 2 16-byte chunks each, every load of a batch in flight together (loading the
+      // second row half while the Gram runs over the first measured slower: 33.8 vs 31.3 us)
     const int nc = n * p / 2;
     const dbl2* Xg = (const dbl2*)(X + o);
     const dbl2* Ug = (const dbl2*)(U + o);
@@ -305,35 +336,16 @@ __global__ void __launch_bounds__(T) k_st_proj3(int n, int p, int64_t stride, co
   p3_unit<P16>(w, I0, J0, I1, J1);
   dbl4 acc0 = dbl4{0.0, 0.0, 0.0, 0.0}, acc1 = dbl4{0.0, 0.0, 0.0, 0.0};
   if (I0 >= 0) {
+    // columns past p are clamped, not masked: they only feed M's rows / columns past p, which are
+    // stored as zero below (a 0/1 factor on each operand would make every read's multiply wait on
+    // that read inside the batch)
     const int ca0 = 16 * I0 + c, cb0 = 16 * J0 + c;
     const int ca1 = 16 * (I1 >= 0 ? I1 : I0) + c, cb1 = 16 * (J1 >= 0 ? J1 : J0) + c;
-    // A (lane c = row of M) and B (lane c = column of M) are masked separately
-    const double ma0 = mask01(ca0 < p), mb0 = mask01(cb0 < p);
-    const double ma1 = mask01(I1 >= 0 && ca1 < p), mb1 = mask01(cb1 < p);
     const int a0 = ca0 < p ? ca0 : p - 1, b0 = cb0 < p ? cb0 : p - 1;
     const int a1 = ca1 < p ? ca1 : p - 1, b1 = cb1 < p ? cb1 : p - 1;
-    constexpr int GB = 5;   // 4-row groups per batch of LDS reads
     const int G = (n + 3) / 4;
-    for (int g0 = 0; g0 < G; g0 += GB) {
-      double xa0[GB], ub0[GB], xa1[GB], ub1[GB];
-#pragma unroll
-      for (int u = 0; u < GB; ++u) {
-        const int r = 4 * (g0 + u) + kk;
-        const double rm = mask01(r < n);
-        const lds_f64* xr = Xs + (r < n ? r : n - 1) * p;
-        const lds_f64* ur = Us + (r < n ? r : n - 1) * p;
-        xa0[u] = xr[a0] * (rm * ma0);
-        ub0[u] = ur[b0] * mb0;
-        xa1[u] = xr[a1] * (rm * ma1);
-        ub1[u] = ur[b1] * mb1;
-      }
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int u = 0; u < GB; ++u) {
-        acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(xa0[u], ub0[u], acc0, 0, 0, 0);
-        acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(xa1[u], ub1[u], acc1, 0, 0, 0);
-      }
-    }
+    if (n % (4 * P3_GB) == 0) p3_gram<false>(Xs, Us, n, p, kk, a0, b0, a1, b1, 0, G, acc0, acc1);
+    else p3_gram<true>(Xs, Us, n, p, kk, a0, b0, a1, b1, 0, G, acc0, acc1);
   }
   ST_STAMP(2);
   // the update's C operand (U at this wave's output blocks) while U is still in LDS
@@ -351,15 +363,16 @@ __global__ void __launch_bounds__(T) k_st_proj3(int n, int p, int64_t stride, co
     for (int g = 0; g < 4; ++g) {
       const int i = 16 * R + kk + 4 * g;
       const bool ok = u < nunits && i < n && j < p;
-      cv[q][g] = Us[(ok ? i : 0) * p + (ok ? j : 0)] * mask01(ok);
+      cv[q][g] = Us[(ok ? i : 0) * p + (ok ? j : 0)];   // unmasked: outputs past n or p are not stored
     }
   }
   __syncthreads();   // every read of U in LDS is done: M may overwrite it
   if (I0 >= 0) {
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      Ms[(16 * I0 + kk + 4 * g) * S + 16 * J0 + c] = acc0[g];
-      if (I1 >= 0) Ms[(16 * I1 + kk + 4 * g) * S + 16 * J1 + c] = acc1[g];
+    for (int g = 0; g < 4; ++g) {   // M is zero outside [0, p)^2 (the update's k steps past p rely on it)
+      const int i0 = 16 * I0 + kk + 4 * g, j0 = 16 * J0 + c, i1 = 16 * I1 + kk + 4 * g, j1 = 16 * J1 + c;
+      Ms[i0 * S + j0] = acc0[g] * mask01(i0 < p && j0 < p);
+      if (I1 >= 0) Ms[i1 * S + j1] = acc1[g] * mask01(i1 < p && j1 < p);
     }
   }
   __syncthreads();
@@ -384,15 +397,13 @@ __global__ void __launch_bounds__(T) k_st_proj3(int n, int p, int64_t stride, co
     const int ar0 = 16 * R0 + c, ar1 = 16 * R1 + c;
     const lds_f64* xr0 = Xs + (ar0 < n ? ar0 : n - 1) * p;
     const lds_f64* xr1 = Xs + (ar1 < n ? ar1 : n - 1) * p;
-    const double rm0 = mask01(ar0 < n), rm1 = mask01(ar1 < n);
     double a0[S4], a1[S4];
 #pragma unroll
-    for (int s = 0; s < S4; ++s) {
+    for (int s = 0; s < S4; ++s) {   // unmasked: sym(M) is zero at k >= p, rows past n are not stored
       const int k = 4 * s + kk;
       const int kc = k < p ? k : p - 1;
-      const double km = mask01(k < p);
-      a0[s] = xr0[kc] * (rm0 * km);
-      a1[s] = xr1[kc] * (rm1 * km);
+      a0[s] = xr0[kc];
+      a1[s] = xr1[kc];
     }
     __builtin_amdgcn_sched_barrier(0);
     dbl4 acc0u = dbl4{0.0, 0.0, 0.0, 0.0}, acc1u = dbl4{0.0, 0.0, 0.0, 0.0};
@@ -632,13 +643,18 @@ __device__ __forceinline__ void r2_block_ij(int b, int& I, int& J) {
   J = i + b;
 }
 
-template <int P16>
-__device__ __forceinline__ void r2_gram(lds_f64* As, lds_f64* Gm, lds_f64* red, int NR) {
-  constexpr int S = 16 * P16, NB = P16 * (P16 + 1) / 2, UB2 = 14;
+// MASK = false when every batch is full (both halves a multiple of the batch size, e.g. n = 200): the
+// 0/1 factor on each A operand is then dropped — with it in, each read's multiply waits on that read
+// inside the batch (s_waitcnt lgkmcnt after every 4 reads), which serialises the batch's LDS latency.
+// hsel: run only the tasks of k half hsel (0 or 1; -1: both)
+template <int P16, bool MASK, int UB2>
+__device__ __forceinline__ void r2_gram_tasks(lds_f64* As, lds_f64* Gm, lds_f64* red, int NR, int hsel) {
+  constexpr int S = 16 * P16, NB = P16 * (P16 + 1) / 2;
   const int t = threadIdx.x, l = t & 63, w = t >> 6, c = l & 15, kk = l >> 4;
   const int NG = NR / 4, H0 = NG / 2;   // k groups of 4 rows; half 0 = [0, H0), half 1 = [H0, NG)
   for (int task = w; task < 2 * NB; task += NW) {   // wave-uniform
     const int b = task % NB, h = task / NB;
+    if (hsel >= 0 && h != hsel) continue;
     int I, J;
     r2_block_ij<P16>(b, I, J);
     const int g0 = h ? H0 : 0, g1 = h ? NG : H0;
@@ -647,10 +663,10 @@ __device__ __forceinline__ void r2_gram(lds_f64* As, lds_f64* Gm, lds_f64* red, 
       double av[UB2], bv[UB2];
 #pragma unroll
       for (int u = 0; u < UB2; ++u) {
-        const bool ok = g + u < g1;
+        const bool ok = !MASK || g + u < g1;
         const int r = 4 * (ok ? g + u : g1 - 1) + kk;
         const lds_f64* row = As + r * S;
-        av[u] = row[(16 * I + c) ^ (r & 15)] * mask01(ok);
+        av[u] = MASK ? row[(16 * I + c) ^ (r & 15)] * mask01(ok) : row[(16 * I + c) ^ (r & 15)];
         bv[u] = row[(16 * J + c) ^ (r & 15)];
       }
       __builtin_amdgcn_sched_barrier(0);   // the batch's reads issue together
@@ -663,6 +679,20 @@ __device__ __forceinline__ void r2_gram(lds_f64* As, lds_f64* Gm, lds_f64* red, 
 #pragma unroll
     for (int q = 0; q < 4; ++q) dst[q * 64 + l] = acc[q];
   }
+}
+
+template <int P16>
+__device__ __forceinline__ void r2_gram_half(lds_f64* As, lds_f64* Gm, lds_f64* red, int NR, int hsel) {
+  const int NG = NR / 4, H0 = NG / 2;
+  if (H0 % 13 == 0 && (NG - H0) % 13 == 0) r2_gram_tasks<P16, false, 13>(As, Gm, red, NR, hsel);   // n = 200: 2 x 13 per half
+  else r2_gram_tasks<P16, true, 14>(As, Gm, red, NR, hsel);
+}
+
+// the halves' partials (half 0 in Gm's area, half 1 in red) -> the symmetric G in Gm
+template <int P16>
+__device__ __forceinline__ void r2_gram_finish(lds_f64* Gm, lds_f64* red) {
+  constexpr int S = 16 * P16, NB = P16 * (P16 + 1) / 2;
+  const int t = threadIdx.x;
   __syncthreads();
   constexpr int PER = (NB * 256 + T - 1) / T;
   double v[PER];
@@ -689,6 +719,12 @@ __device__ __forceinline__ void r2_gram(lds_f64* As, lds_f64* Gm, lds_f64* red, 
   __syncthreads();
 }
 
+template <int P16>
+__device__ __forceinline__ void r2_gram(lds_f64* As, lds_f64* Gm, lds_f64* red, int NR) {
+  r2_gram_half<P16>(As, Gm, red, NR, -1);
+  r2_gram_finish<P16>(Gm, red);
+}
+
 // Gm (G, stride S) -> Gm (W = R^-1 = E^T, stride S); xch: 4 FB S doubles of exchange space (the Gram's
 // partial-sum area, NB * 256 >= 16 S doubles)
 // columns eliminated per barrier step of r2_factor_inverse (tools/stiefel_stamps.hip builds 1 / 2 / 4 for A/B)
@@ -700,7 +736,11 @@ constexpr int FB = RIPTRM_ST_FB;
 // barrier per step (r2_factor_inverse_1w), measured 159k vs 69k ticks per factor at (200, 50)
 // (profiles/r3_stiefel_factor_1wave_stamps.jsonl).  A/B: tools/stiefel_stamps.hip -DRIPTRM_ST_FACTOR=1
 #ifndef RIPTRM_ST_FACTOR
-#define RIPTRM_ST_FACTOR 0
+#define RIPTRM_ST_FACTOR 2
+#endif
+// pivot reciprocal of the blocked factor's diagonal blocks: IEEE division (0) or v_rcp_f64 + Newton (1)
+#ifndef RIPTRM_ST_RCP
+#define RIPTRM_ST_RCP 1   // measured 37.9k vs 39.3k ticks per factor at (200, 50)
 #endif
 
 static_assert(FB <= 4 && 8 % FB == 0, "the exchange alternates 2 buffers within a group of 8 rows");
@@ -882,6 +922,250 @@ __device__ __forceinline__ void r2_factor_inverse_1w(lds_f64* Gm, lds_f64* xch, 
   __syncthreads();
 }
 
+// ---- blocked factor (round 3): 16-column diagonal blocks on one wave, the rest on MFMA -----------
+// r2_factor_inverse pays one workgroup barrier and one cross-wave LDS round trip per pivot pair
+// (~1.4k ticks per column at p = 50).  Here the chain of p pivots runs inside ONE wave on 16 x 16
+// diagonal blocks with lane shuffles only, and everything else is block algebra on the matrix cores
+// with three barriers per 16-column block:
+//   for K = 0 .. ceil(p/16) - 1 (E starts as the identity):
+//     (a) F = L_KK^-1 from the current G_KK: Gauss-Jordan on [G_KK | I] in registers of one wave
+//         (lane = (row group q, column j), 4 rows each; pivot row and column by ds_bpermute, pivot by
+//         readlane), row i scaled by D_i^-1/2 — no LDS, no barrier inside;
+//     (b) C_IK = L_IK = G_IK F^T (I > K) and E_KJ <- F E_KJ (J < K; E_KK = F);
+//     (c) G_IJ -= C_IK C_JK^T (K < J <= I, the trailing Schur complement) and E_IJ -= C_IK E_KJ
+//         (I > K, J <= K); the wave that updates G_{K+1,K+1} goes straight on to (a) of K + 1.
+//   E = L^-1, and W = R^-1 = E^T as r2_factor_inverse leaves it.
+// Storage: G's trailing blocks are kept in Gm's UPPER triangle (G_IK read as G_KI^T, so every
+// operand read walks 16 consecutive doubles), C_IK in Gm's lower block (I, K) and E's lower blocks
+// (block-major, 256 doubles each) in the exchange area; both with the column XOR-swizzled by the
+// row (element (a, b) at column b ^ a), so the MFMA operand reads of a column are bank-conflict
+// free.  Columns past p are the identity (W = diag(W_p, I)), as in r2_factor_inverse.
+__device__ __forceinline__ double r3_shfl(double v, int src) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_ds_bpermute(src << 2, (int)b);
+  const int hi = __builtin_amdgcn_ds_bpermute(src << 2, (int)(b >> 32));
+  return __longlong_as_double((long long)(unsigned)lo | ((long long)hi << 32));
+}
+__device__ __forceinline__ double r3_readlane(double v, int lane) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)b, lane);
+  const int hi = __builtin_amdgcn_readlane((int)(b >> 32), lane);
+  return __longlong_as_double((long long)(unsigned)lo | ((long long)hi << 32));
+}
+__device__ __forceinline__ double r3_recip(double d) {
+#if RIPTRM_ST_RCP
+  double r = __builtin_amdgcn_rcp(d);   // v_rcp_f64 + two Newton steps
+  r = __builtin_fma(r, __builtin_fma(-d, r, 1.0), r);
+  return __builtin_fma(r, __builtin_fma(-d, r, 1.0), r);
+#else
+  return 1.0 / d;
+#endif
+}
+__device__ __forceinline__ int r3_eb(int I, int J) { return (I * (I + 1) / 2 + J) * 256; }   // E block (I, J), J <= I
+
+// (a): one wave; Fb = the E block (K, K) (swizzled)
+template <int P16>
+__device__ __forceinline__ void r3_diag_factor(const lds_f64* Gm, lds_f64* Fb, int K, int p) {
+  constexpr int S = 16 * P16;
+  const int l = threadIdx.x & 63, q = l >> 4, j = l & 15;
+  const int kmax = p - 16 * K < 16 ? p - 16 * K : 16;   // pivots past p: identity rows
+  const int jj = 16 * K + j;
+  double g[4], e[4], piv[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    const int a = 4 * q + s, i = 16 * K + a;
+    const double v = Gm[i * S + jj];   // always in range (i, jj < S)
+    g[s] = (i < p && jj < p) ? v : (a == j ? 1.0 : 0.0);
+    e[s] = a == j ? 1.0 : 0.0;
+    piv[s] = 1.0;
+  }
+  // one pivot per step (two per step — a 2 x 2 pivot block with independent reciprocals — measured
+  // 9.2k vs 8.8k ticks per 16-column block: the shuffles, not the reciprocal chain, set the step time)
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    if (k >= kmax) continue;   // uniform (a break here keeps the loop from unrolling: runtime slot indices)
+    const int kq = k >> 2, ks = k & 3;
+    const double gk = r3_shfl(g[ks], 16 * kq + j);   // G[k][j]
+    const double ek = r3_shfl(e[ks], 16 * kq + j);   // E[k][j]
+    double ck[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) ck[s] = r3_shfl(g[s], 16 * q + k);   // G[4q + s][k]
+    const double d = r3_readlane(g[ks], 16 * kq + k);                // G[k][k]
+    const double inv = r3_recip(d);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int a = 4 * q + s;
+      const double m = ck[s] * inv * mask01(a > k);   // 0 leaves rows <= k bitwise unchanged
+      g[s] = g[s] - m * gk;
+      e[s] = e[s] - m * ek;
+      if (a == k) piv[s] = d;
+    }
+  }
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    const int a = 4 * q + s;
+    Fb[a * 16 + (j ^ a)] = e[s] * (1.0 / sqrt(piv[s]));
+  }
+}
+
+// (b) C_IK = G_IK F^T into Gm's lower block (I, K)
+template <int P16>
+__device__ __forceinline__ void r3_task_C(lds_f64* Gm, const lds_f64* Fb, int I, int K) {
+  constexpr int S = 16 * P16;
+  const int l = threadIdx.x & 63, c = l & 15, kk = l >> 4;
+  double a[4], b[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    const int x = 4 * s + kk;
+    a[s] = Gm[(16 * K + x) * S + 16 * I + c];   // G_IK[c][x] = G_KI[x][c]
+    b[s] = Fb[c * 16 + (x ^ c)];               // F^T[x][c] = F[c][x]
+  }
+  dbl4 acc = dbl4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int s = 0; s < 4; ++s) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[s], b[s], acc, 0, 0, 0);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int row = kk + 4 * r;
+    Gm[(16 * I + row) * S + 16 * K + (c ^ row)] = acc[r];
+  }
+}
+
+// (b) E_KJ <- F E_KJ (in place)
+__device__ __forceinline__ void r3_task_EF(lds_f64* Ea, int K, int J) {
+  const int l = threadIdx.x & 63, c = l & 15, kk = l >> 4;
+  const lds_f64* Fb = Ea + r3_eb(K, K);
+  lds_f64* R = Ea + r3_eb(K, J);
+  double a[4], b[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    const int x = 4 * s + kk;
+    a[s] = Fb[c * 16 + (x ^ c)];
+    b[s] = R[x * 16 + (c ^ x)];
+  }
+  dbl4 acc = dbl4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int s = 0; s < 4; ++s) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[s], b[s], acc, 0, 0, 0);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int row = kk + 4 * r;
+    R[row * 16 + (c ^ row)] = acc[r];
+  }
+}
+
+// (c) G_JI -= C_JK C_IK^T (K < J <= I; upper storage, the diagonal block whole)
+template <int P16>
+__device__ __forceinline__ void r3_task_G(lds_f64* Gm, int J, int I, int K) {
+  constexpr int S = 16 * P16;
+  const int l = threadIdx.x & 63, c = l & 15, kk = l >> 4;
+  double a[4], b[4];
+  dbl4 acc;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) acc[r] = Gm[(16 * J + kk + 4 * r) * S + 16 * I + c];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    const int x = 4 * s + kk;
+    a[s] = -Gm[(16 * J + c) * S + 16 * K + (x ^ c)];   // -C_JK[c][x]
+    b[s] = Gm[(16 * I + c) * S + 16 * K + (x ^ c)];    //  C_IK[c][x]
+  }
+#pragma unroll
+  for (int s = 0; s < 4; ++s) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[s], b[s], acc, 0, 0, 0);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) Gm[(16 * J + kk + 4 * r) * S + 16 * I + c] = acc[r];
+}
+
+// (c) E_IJ -= C_IK E_KJ (I > K, J <= K)
+template <int P16>
+__device__ __forceinline__ void r3_task_R(const lds_f64* Gm, lds_f64* Ea, int I, int J, int K) {
+  constexpr int S = 16 * P16;
+  const int l = threadIdx.x & 63, c = l & 15, kk = l >> 4;
+  lds_f64* R = Ea + r3_eb(I, J);
+  const lds_f64* Ek = Ea + r3_eb(K, J);
+  double a[4], b[4];
+  dbl4 acc;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int row = kk + 4 * r;
+    acc[r] = R[row * 16 + (c ^ row)];
+  }
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    const int x = 4 * s + kk;
+    a[s] = -Gm[(16 * I + c) * S + 16 * K + (x ^ c)];   // -C_IK[c][x]
+    b[s] = Ek[x * 16 + (c ^ x)];                       //  E_KJ[x][c]
+  }
+#pragma unroll
+  for (int s = 0; s < 4; ++s) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[s], b[s], acc, 0, 0, 0);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int row = kk + 4 * r;
+    R[row * 16 + (c ^ row)] = acc[r];
+  }
+}
+
+// Gm (G, stride S, both triangles) -> Gm (W = E^T in the upper blocks, stride S); Ea: P16 (P16 + 1) / 2
+// blocks of 256 doubles (the Gram's partial-sum area)
+// STAMPS: the first call's sub-phases go to stamp slots 8..15 (tools/stiefel_stamps.hip only)
+template <int P16, bool STAMPS = false>
+__device__ __forceinline__ void r3_factor_blocked(lds_f64* Gm, lds_f64* Ea, int p) {
+  constexpr int S = 16 * P16, NB = P16 * (P16 + 1) / 2;
+  const int t = threadIdx.x, w = t >> 6;
+  if (STAMPS) ST_STAMP(8);
+  for (int e = t; e < NB * 256; e += T) {   // E's off-diagonal blocks start at zero (the diagonal ones are written by (a))
+    const int blk = e >> 8;
+    bool diag = false;
+#pragma unroll
+    for (int I = 0; I < P16; ++I) diag = diag || blk == I * (I + 3) / 2;
+    if (!diag) Ea[e] = 0.0;
+  }
+  if (w == 0) r3_diag_factor<P16>(Gm, Ea + r3_eb(0, 0), 0, p);
+  if (STAMPS) ST_STAMP(9);
+  __syncthreads();
+  for (int K = 0; K < P16; ++K) {
+    const int nC = P16 - 1 - K;
+    for (int task = w; task < nC + K; task += NW) {   // (b)
+      if (task < nC) r3_task_C<P16>(Gm, Ea + r3_eb(K, K), K + 1 + task, K);
+      else r3_task_EF(Ea, K, task - nC);
+    }
+    __syncthreads();
+    if (STAMPS && K < 2) ST_STAMP(10 + 3 * K);
+    if (K == P16 - 1) break;
+    if (w == 0) {   // (c) G_{K+1,K+1}, then (a) of K + 1
+      r3_task_G<P16>(Gm, K + 1, K + 1, K);
+      r3_diag_factor<P16>(Gm, Ea + r3_eb(K + 1, K + 1), K + 1, p);
+      if (STAMPS && K < 2) ST_STAMP(11 + 3 * K);
+    } else {
+      const int m = P16 - 1 - K;             // trailing block rows
+      const int nG = m * (m + 1) / 2 - 1;    // pairs (J, I), K < J <= I, without (K + 1, K + 1)
+      const int nR = m * (K + 1);
+      for (int task = w - 1; task < nG + nR; task += NW - 1) {
+        if (task < nG) {
+          int u = task + 1, J = K + 1;
+          while (u >= P16 - J) {   // row J of the pair triangle holds P16 - J pairs
+            u -= P16 - J;
+            ++J;
+          }
+          r3_task_G<P16>(Gm, J, J + u, K);
+        } else {
+          const int u = task - nG;
+          r3_task_R<P16>(Gm, Ea, K + 1 + u / (K + 1), u % (K + 1), K);
+        }
+      }
+    }
+    __syncthreads();
+    if (STAMPS && K == 0) ST_STAMP(12);
+  }
+  for (int e = t; e < NB * 256; e += T) {   // W[16 J + b][16 I + a] = E_IJ[a][b]; consecutive lanes: consecutive a
+    const int blk = e >> 8, b = (e >> 4) & 15, a = e & 15;
+    int I = 0;
+#pragma unroll
+    for (int q = 1; q < P16; ++q) I += blk >= q * (q + 1) / 2;
+    const int J = blk - I * (I + 1) / 2;
+    Gm[(16 * J + b) * S + 16 * I + a] = Ea[blk * 256 + a * 16 + (b ^ a)];
+  }
+  __syncthreads();
+  if (STAMPS) ST_STAMP(15);
+}
+
 // The second CholeskyQR pass factors G2 = Q1^T Q1 = I + D with D at the rounding level of the first
 // pass (~kappa(A)^2 eps).  Then L2 = I + N with N = tril(D, -1) + diag(D) / 2 up to O(D^2), and
 // W2 = R2^-1 = (L2^-1)^T = I - N^T up to O(D^2): elementwise, no dependent chain.  Used when
@@ -940,13 +1224,17 @@ __device__ __forceinline__ void r2_apply(lds_f64* As, const lds_f64* Wt, int NR,
       for (int s = 0; s < 4; ++s) af[K][s] = As[row * S + ((16 * K + 4 * s + kk) ^ c)];
     dbl4 acc[P16];
 #pragma unroll
-    for (int J = 0; J < P16; ++J) {
-      acc[J] = dbl4{0.0, 0.0, 0.0, 0.0};
+    for (int J = 0; J < P16; ++J) acc[J] = dbl4{0.0, 0.0, 0.0, 0.0};
+    // (K, s) outer, J inner: consecutive MFMAs feed different accumulators; A's columns past p are
+    // zero, so k steps past p are skipped
 #pragma unroll
-      for (int K = 0; K <= J; ++K)
+    for (int K = 0; K < P16; ++K)
 #pragma unroll
-        for (int s = 0; s < 4; ++s) acc[J] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[K][s], wf[K][J][s], acc[J], 0, 0, 0);
-    }
+      for (int s = 0; s < 4; ++s)
+        if (16 * K + 4 * s < p) {
+#pragma unroll
+          for (int J = K; J < P16; ++J) acc[J] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[K][s], wf[K][J][s], acc[J], 0, 0, 0);
+        }
 #pragma unroll
     for (int J = 0; J < P16; ++J)
 #pragma unroll
@@ -962,6 +1250,21 @@ __device__ __forceinline__ void r2_apply(lds_f64* As, const lds_f64* Wt, int NR,
   __syncthreads();
 }
 
+// the second pass's exact factor (rare: only when Q1 is not orthonormal to 1e-10) as a call, so its
+// code does not sit inline in the kernel (the kernel is ~54 KB with it inlined)
+#ifndef RIPTRM_ST_FB_INLINE
+#define RIPTRM_ST_FB_INLINE 0
+#endif
+template <int P16>
+#if RIPTRM_ST_FB_INLINE
+__device__ __forceinline__
+#else
+__device__ __noinline__
+#endif
+void r3_factor_blocked_call(lds_f64* Gm, lds_f64* Ea, int p) {
+  r3_factor_blocked<P16>(Gm, Ea, p);
+}
+
 template <int P16>
 __global__ void __launch_bounds__(T) k_st_retr2(int n, int p, int64_t stride, const double* __restrict__ X,
                                                 const double* __restrict__ U, double* out) {   // out may alias X or U (all reads precede the first write)
@@ -974,6 +1277,8 @@ __global__ void __launch_bounds__(T) k_st_retr2(int n, int p, int64_t stride, co
   const int t = threadIdx.x;
   const int64_t o = (int64_t)blockIdx.x * stride;
   ST_STAMP(0);
+  // (loading the second row half while the first half's Gram tasks run measured slower: 35.1k vs
+  // 32.6k ticks for load + Gram)
   const int tot = NR * S;
   for (int e0 = 0; e0 < tot; e0 += T * UL) {
     double v[UL];
@@ -998,6 +1303,12 @@ __global__ void __launch_bounds__(T) k_st_retr2(int n, int p, int64_t stride, co
   ST_STAMP(2);
 #if RIPTRM_ST_FACTOR == 1
   r2_factor_inverse_1w<P16>(Gm, red, p);
+#elif RIPTRM_ST_FACTOR == 2
+#ifdef ST_STAMPS
+  r3_factor_blocked<P16, true>(Gm, red, p);
+#else
+  r3_factor_blocked<P16>(Gm, red, p);
+#endif
 #else
   r2_factor_inverse<P16>(Gm, red, p);
 #endif
@@ -1008,6 +1319,8 @@ __global__ void __launch_bounds__(T) k_st_retr2(int n, int p, int64_t stride, co
   ST_STAMP(5);
 #if RIPTRM_ST_FACTOR == 1
   if (!r2_inverse_first_order<P16>(Gm, red, p)) r2_factor_inverse_1w<P16>(Gm, red, p);
+#elif RIPTRM_ST_FACTOR == 2
+  if (!r2_inverse_first_order<P16>(Gm, red, p)) r3_factor_blocked_call<P16>(Gm, red, p);
 #else
   if (!r2_inverse_first_order<P16>(Gm, red, p)) r2_factor_inverse<P16>(Gm, red, p);
 #endif

@@ -70,7 +70,20 @@ int main(int argc, char** argv) {
     std::vector<long long> t(B);
     for (int g = 0; g < B; ++g) t[g] = s[g * 16 + np] - s[g * 16];
     std::sort(t.begin(), t.end());
-    printf("], \"total_ticks_median\": %lld, \"total_ticks_max\": %lld}\n", t[B / 2], t[B - 1]);
+    printf("], \"total_ticks_median\": %lld, \"total_ticks_max\": %lld", t[B / 2], t[B - 1]);
+#if RIPTRM_ST_FACTOR == 2
+    if (which == 2) {   // blocked factor sub-phases (first factor): diag0, b0, G11+diag1 (wave 0), wait, b1, G22+diag2, rest
+      printf(", \"factor1_sub_ticks_median\": [");
+      for (int k = 8; k < 15; ++k) {
+        std::vector<long long> d(B);
+        for (int g = 0; g < B; ++g) d[g] = s[g * 16 + k + 1] - s[g * 16 + k];
+        std::sort(d.begin(), d.end());
+        printf("%s%lld", k > 8 ? ", " : "", d[B / 2]);
+      }
+      printf("]");
+    }
+#endif
+    printf("}\n");
   }
   return 0;
 }
