@@ -979,8 +979,10 @@ __device__ __forceinline__ void r3_diag_factor(const lds_f64* Gm, lds_f64* Fb, i
     e[s] = a == j ? 1.0 : 0.0;
     piv[s] = 1.0;
   }
-  // one pivot per step (two per step — a 2 x 2 pivot block with independent reciprocals — measured
-  // 9.2k vs 8.8k ticks per 16-column block: the shuffles, not the reciprocal chain, set the step time)
+  // one pivot per step.  Measured alternatives at (200, 50): two pivots per step (a 2 x 2 pivot block,
+  // independent reciprocals) 9.2k vs 8.8k ticks per 16-column block; the pivot row through LDS (one
+  // lane group writes, all read back, wave-scope fences) 8.9k: each step is a dependent chain
+  // (exchange -> reciprocal -> update of the next pivot row) of ~500 ticks however the row travels
 #pragma unroll
   for (int k = 0; k < 16; ++k) {
     if (k >= kmax) continue;   // uniform (a break here keeps the loop from unrolling: runtime slot indices)
