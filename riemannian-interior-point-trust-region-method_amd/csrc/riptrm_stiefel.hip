@@ -293,6 +293,47 @@ __device__ __forceinline__ void p3_gram(const lds_f64* Xs, const lds_f64* Us, in
   }
 }
 
+// the update of k_st_proj3: out = U - X sym(M) for this wave's units (16-row block R, column block J),
+// two at a time (two independent accumulator chains per wave, four per SIMD), each unit's P4T k steps
+// in order (P4T = ceil(p / 4) as a template parameter: with a runtime bound every MFMA pair sat
+// behind its own branch; measured 21.9k ticks for the update at (200, 50))
+template <int P16, int P4T, int UMAX>
+__device__ __forceinline__ void p3_update(const lds_f64* Xs, const double (&bk)[4 * P16], const double (&cv)[UMAX][4],
+                                          double* out, int n, int p, int w, int c, int kk, int J, int nunits) {
+#pragma unroll
+  for (int q = 0; q < UMAX; q += 2) {
+    const int u0 = w + NW * q, u1 = w + NW * (q + 1);
+    if (u0 >= nunits) continue;   // wave-uniform (no break: the loop stays unrolled)
+    const bool two = q + 1 < UMAX && u1 < nunits;
+    const int R0 = u0 / P16, R1 = two ? u1 / P16 : R0;
+    const int ar0 = 16 * R0 + c, ar1 = 16 * R1 + c;
+    const lds_f64* xr0 = Xs + (ar0 < n ? ar0 : n - 1) * p;
+    const lds_f64* xr1 = Xs + (ar1 < n ? ar1 : n - 1) * p;
+    double a0[P4T], a1[P4T];
+#pragma unroll
+    for (int s = 0; s < P4T; ++s) {   // unmasked: sym(M) is zero at k >= p, rows past n are not stored
+      const int k = 4 * s + kk;
+      const int kc = k < p ? k : p - 1;
+      a0[s] = xr0[kc];
+      a1[s] = xr1[kc];
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    dbl4 acc0u = dbl4{0.0, 0.0, 0.0, 0.0}, acc1u = dbl4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int s = 0; s < P4T; ++s) {
+      acc0u = __builtin_amdgcn_mfma_f64_16x16x4f64(a0[s], bk[s], acc0u, 0, 0, 0);
+      acc1u = __builtin_amdgcn_mfma_f64_16x16x4f64(a1[s], bk[s], acc1u, 0, 0, 0);
+    }
+    const int j = 16 * J + c;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int i0 = 16 * R0 + kk + 4 * g, i1 = 16 * R1 + kk + 4 * g;
+      if (i0 < n && j < p) out[(int64_t)i0 * p + j] = cv[q][g] - acc0u[g];
+      if (two && i1 < n && j < p) out[(int64_t)i1 * p + j] = cv[q + 1 < UMAX ? q + 1 : q][g] - acc1u[g];
+    }
+  }
+}
+
 template <int P16>
 __global__ void __launch_bounds__(T) k_st_proj3(int n, int p, int64_t stride, const double* X, const double* U,
                                                 double* out) {
@@ -386,40 +427,11 @@ __global__ void __launch_bounds__(T) k_st_proj3(int n, int p, int64_t stride, co
     const int k = 4 * s + kk, j = 16 * J + c;
     bk[s] = 0.5 * (Ms[k * S + j] + Ms[j * S + k]);   // zero past p (M is zero there)
   }
-  // units two at a time: two independent accumulator chains per wave (four per SIMD), each
-  // unit's k steps in order
-#pragma unroll
-  for (int q = 0; q < UMAX; q += 2) {
-    const int u0 = w + NW * q, u1 = w + NW * (q + 1);
-    if (u0 >= nunits) break;   // wave-uniform
-    const bool two = q + 1 < UMAX && u1 < nunits;
-    const int R0 = u0 / P16, R1 = two ? u1 / P16 : R0;
-    const int ar0 = 16 * R0 + c, ar1 = 16 * R1 + c;
-    const lds_f64* xr0 = Xs + (ar0 < n ? ar0 : n - 1) * p;
-    const lds_f64* xr1 = Xs + (ar1 < n ? ar1 : n - 1) * p;
-    double a0[S4], a1[S4];
-#pragma unroll
-    for (int s = 0; s < S4; ++s) {   // unmasked: sym(M) is zero at k >= p, rows past n are not stored
-      const int k = 4 * s + kk;
-      const int kc = k < p ? k : p - 1;
-      a0[s] = xr0[kc];
-      a1[s] = xr1[kc];
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    dbl4 acc0u = dbl4{0.0, 0.0, 0.0, 0.0}, acc1u = dbl4{0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-    for (int s = 0; s < S4; ++s)
-      if (s < P4) {
-        acc0u = __builtin_amdgcn_mfma_f64_16x16x4f64(a0[s], bk[s], acc0u, 0, 0, 0);
-        acc1u = __builtin_amdgcn_mfma_f64_16x16x4f64(a1[s], bk[s], acc1u, 0, 0, 0);
-      }
-    const int j = 16 * J + c;
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const int i0 = 16 * R0 + kk + 4 * g, i1 = 16 * R1 + kk + 4 * g;
-      if (i0 < n && j < p) out[o + (int64_t)i0 * p + j] = cv[q][g] - acc0u[g];
-      if (two && i1 < n && j < p) out[o + (int64_t)i1 * p + j] = cv[q + 1 < UMAX ? q + 1 : q][g] - acc1u[g];
-    }
+  switch (P4) {   // the update specialised on the k steps, so no MFMA sits behind a per-step branch
+    case 13: p3_update<P16, 13, UMAX>(Xs, bk, cv, out + o, n, p, w, c, kk, J, nunits); break;
+    case 14: p3_update<P16, 14, UMAX>(Xs, bk, cv, out + o, n, p, w, c, kk, J, nunits); break;
+    case 15: p3_update<P16, 15, UMAX>(Xs, bk, cv, out + o, n, p, w, c, kk, J, nunits); break;
+    default: p3_update<P16, 16, UMAX>(Xs, bk, cv, out + o, n, p, w, c, kk, J, nunits); break;
   }
   ST_STAMP(4);
 }
@@ -1206,8 +1218,10 @@ __device__ __forceinline__ bool r2_inverse_first_order(lds_f64* Gm, lds_f64* red
 
 // Q = A W (W upper triangular): wave w owns the 16-row blocks R = w, w + 8, ...; FINAL writes Q to
 // global memory, otherwise Q overwrites A in LDS (a wave writes only the rows it read)
-template <int P16, bool FINAL>
-__device__ __forceinline__ void r2_apply(lds_f64* As, const lds_f64* Wt, int NR, int n, int p, double* out) {
+// KSL: k steps of the last 16-column block that hold columns of A (ceil((p - 16 (P16 - 1)) / 4)): a
+// template parameter, so no MFMA sits behind a per-step branch
+template <int P16, bool FINAL, int KSL>
+__device__ __forceinline__ void r2_apply_k(lds_f64* As, const lds_f64* Wt, int NR, int n, int p, double* out) {
   constexpr int S = 16 * P16;
   const int l = threadIdx.x & 63, w = threadIdx.x >> 6, c = l & 15, kk = l >> 4;
   double wf[P16][P16][4];
@@ -1232,11 +1246,10 @@ __device__ __forceinline__ void r2_apply(lds_f64* As, const lds_f64* Wt, int NR,
 #pragma unroll
     for (int K = 0; K < P16; ++K)
 #pragma unroll
-      for (int s = 0; s < 4; ++s)
-        if (16 * K + 4 * s < p) {
+      for (int s = 0; s < (K == P16 - 1 ? KSL : 4); ++s) {
 #pragma unroll
-          for (int J = K; J < P16; ++J) acc[J] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[K][s], wf[K][J][s], acc[J], 0, 0, 0);
-        }
+        for (int J = K; J < P16; ++J) acc[J] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[K][s], wf[K][J][s], acc[J], 0, 0, 0);
+      }
 #pragma unroll
     for (int J = 0; J < P16; ++J)
 #pragma unroll
@@ -1250,6 +1263,16 @@ __device__ __forceinline__ void r2_apply(lds_f64* As, const lds_f64* Wt, int NR,
       }
   }
   __syncthreads();
+}
+
+template <int P16, bool FINAL>
+__device__ __forceinline__ void r2_apply(lds_f64* As, const lds_f64* Wt, int NR, int n, int p, double* out) {
+  switch ((p - 16 * (P16 - 1) + 3) / 4) {
+    case 1: r2_apply_k<P16, FINAL, 1>(As, Wt, NR, n, p, out); break;
+    case 2: r2_apply_k<P16, FINAL, 2>(As, Wt, NR, n, p, out); break;
+    case 3: r2_apply_k<P16, FINAL, 3>(As, Wt, NR, n, p, out); break;
+    default: r2_apply_k<P16, FINAL, 4>(As, Wt, NR, n, p, out); break;
+  }
 }
 
 // the second pass's exact factor (rare: only when Q1 is not orthonormal to 1e-10) as a call, so its

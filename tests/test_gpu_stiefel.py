@@ -26,6 +26,9 @@ def _t(a):
 
 @pytest.mark.parametrize("n,p,B", [(5, 1, 3), (37, 7, 5), (200, 50, 16), (257, 64, 3), (64, 64, 2),
                                      (3, 3, 2), (208, 64, 4), (300, 40, 4), (700, 20, 2),
+                                     # every specialisation of the projection update (ceil(p/4) = 13..16)
+                                     # and of the retraction's last-block k steps (1..4)
+                                     (200, 55, 3), (200, 59, 3), (100, 27, 3), (96, 61, 2),
                                      (200, 50, 256)])   # BASELINE configs[4]: (200, 50) x 256
 def test_stiefel_ops_match_oracle(n, p, B):
     from stiefel import StiefelBatch
