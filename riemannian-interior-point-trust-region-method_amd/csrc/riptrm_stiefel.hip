@@ -297,40 +297,53 @@ __device__ __forceinline__ void p3_gram(const lds_f64* Xs, const lds_f64* Us, in
 // two at a time (two independent accumulator chains per wave, four per SIMD), each unit's P4T k steps
 // in order (P4T = ceil(p / 4) as a template parameter: with a runtime bound every MFMA pair sat
 // behind its own branch; measured 21.9k ticks for the update at (200, 50))
+// units (independent accumulator chains) per wave per step of the update; measured at (200, 50):
+// 2 / 3 / 4 -> 22.9k / 22.9k / 23.5k ticks (4 spills): the update is not bound by its chains
+#ifndef RIPTRM_P3_UB
+#define RIPTRM_P3_UB 2
+#endif
 template <int P16, int P4T, int UMAX>
 __device__ __forceinline__ void p3_update(const lds_f64* Xs, const double (&bk)[4 * P16], const double (&cv)[UMAX][4],
                                           double* out, int n, int p, int w, int c, int kk, int J, int nunits) {
+  constexpr int UB = RIPTRM_P3_UB;
 #pragma unroll
-  for (int q = 0; q < UMAX; q += 2) {
-    const int u0 = w + NW * q, u1 = w + NW * (q + 1);
-    if (u0 >= nunits) continue;   // wave-uniform (no break: the loop stays unrolled)
-    const bool two = q + 1 < UMAX && u1 < nunits;
-    const int R0 = u0 / P16, R1 = two ? u1 / P16 : R0;
-    const int ar0 = 16 * R0 + c, ar1 = 16 * R1 + c;
-    const lds_f64* xr0 = Xs + (ar0 < n ? ar0 : n - 1) * p;
-    const lds_f64* xr1 = Xs + (ar1 < n ? ar1 : n - 1) * p;
-    double a0[P4T], a1[P4T];
+  for (int q = 0; q < UMAX; q += UB) {
+    if (w + NW * q >= nunits) continue;   // wave-uniform (no break: the loop stays unrolled)
+    int R[UB];
+    bool on[UB];
 #pragma unroll
-    for (int s = 0; s < P4T; ++s) {   // unmasked: sym(M) is zero at k >= p, rows past n are not stored
-      const int k = 4 * s + kk;
-      const int kc = k < p ? k : p - 1;
-      a0[s] = xr0[kc];
-      a1[s] = xr1[kc];
+    for (int b = 0; b < UB; ++b) {
+      const int u = w + NW * (q + b);
+      on[b] = q + b < UMAX && u < nunits;
+      R[b] = (on[b] ? u : w + NW * q) / P16;
+    }
+    double a[UB][P4T];
+#pragma unroll
+    for (int b = 0; b < UB; ++b) {
+      const int ar = 16 * R[b] + c;
+      const lds_f64* xr = Xs + (ar < n ? ar : n - 1) * p;
+#pragma unroll
+      for (int s = 0; s < P4T; ++s) {   // unmasked: sym(M) is zero at k >= p, rows past n are not stored
+        const int k = 4 * s + kk;
+        a[b][s] = xr[k < p ? k : p - 1];
+      }
     }
     __builtin_amdgcn_sched_barrier(0);
-    dbl4 acc0u = dbl4{0.0, 0.0, 0.0, 0.0}, acc1u = dbl4{0.0, 0.0, 0.0, 0.0};
+    dbl4 acc[UB];
 #pragma unroll
-    for (int s = 0; s < P4T; ++s) {
-      acc0u = __builtin_amdgcn_mfma_f64_16x16x4f64(a0[s], bk[s], acc0u, 0, 0, 0);
-      acc1u = __builtin_amdgcn_mfma_f64_16x16x4f64(a1[s], bk[s], acc1u, 0, 0, 0);
-    }
+    for (int b = 0; b < UB; ++b) acc[b] = dbl4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int s = 0; s < P4T; ++s)
+#pragma unroll
+      for (int b = 0; b < UB; ++b) acc[b] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[b][s], bk[s], acc[b], 0, 0, 0);
     const int j = 16 * J + c;
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const int i0 = 16 * R0 + kk + 4 * g, i1 = 16 * R1 + kk + 4 * g;
-      if (i0 < n && j < p) out[(int64_t)i0 * p + j] = cv[q][g] - acc0u[g];
-      if (two && i1 < n && j < p) out[(int64_t)i1 * p + j] = cv[q + 1 < UMAX ? q + 1 : q][g] - acc1u[g];
-    }
+    for (int b = 0; b < UB; ++b)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int i = 16 * R[b] + kk + 4 * g;
+        if (on[b] && i < n && j < p) out[(int64_t)i * p + j] = cv[q + b < UMAX ? q + b : UMAX - 1][g] - acc[b][g];
+      }
   }
 }
 
