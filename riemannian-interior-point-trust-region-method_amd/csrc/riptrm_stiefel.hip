@@ -16,7 +16,9 @@
 // (SQ_VALU_MFMA_BUSY_CYCLES / SQ_INSTS_VALU_MFMA_F64 measured), so one point per CU is
 // latency-bound on its chain of loads, MFMAs and barriers.  The retraction is CholeskyQR2 (Q = A R^-1
 // with R = chol(A^T A), twice): diag(R) > 0 by construction, so it is pymanopt's qf up to
-// rounding for full-rank A.
+// rounding for full-rank A.  k_st_retr2 keeps the point in LDS; its first factor is blocked
+// (r3_factor_blocked: 16-column diagonal blocks on one wave, the rest on MFMA), its second is taken
+// in closed form when Q1 is orthonormal to 1e-10 (r2_inverse_first_order).
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include "riptrm_ctx.h"
@@ -1233,6 +1235,9 @@ __device__ __forceinline__ bool r2_inverse_first_order(lds_f64* Gm, lds_f64* red
 // global memory, otherwise Q overwrites A in LDS (a wave writes only the rows it read)
 // KSL: k steps of the last 16-column block that hold columns of A (ceil((p - 16 (P16 - 1)) / 4)): a
 // template parameter, so no MFMA sits behind a per-step branch
+// (Dealing the last NRB % 8 row blocks as (row block, column block) units in a snake over the waves,
+// so the SIMDs get 123 instead of 148 MFMAs at (200, 50), measured 12.5k vs 12.2k ticks per apply:
+// not kept; profiles/r3_stiefel_apply_snake_balance_stamps.jsonl)
 template <int P16, bool FINAL, int KSL>
 __device__ __forceinline__ void r2_apply_k(lds_f64* As, const lds_f64* Wt, int NR, int n, int p, double* out) {
   constexpr int S = 16 * P16;
