@@ -77,11 +77,12 @@ def test_stiefel_rejects_bad_shapes():
                       torch.zeros(2, 8, 3, dtype=torch.float64, device="cuda"))
 
 
-@pytest.mark.parametrize("cond", [1e2, 1e5])
+@pytest.mark.parametrize("cond", [1e2, 1e5, 1e7])
 def test_stiefel_retraction_conditioning(cond):
     """qf(A) for A of condition number `cond` (passed as X = A, U = 0): at 1e2 the second
-    CholeskyQR pass takes its first-order factor (|Q1^T Q1 - I| ~ 1e-14), at 1e5 (~1e-6) the exact
-    factor runs.  Both against the Householder restatement; CholeskyQR2 loses ~cond * eps."""
+    CholeskyQR pass takes its first-order factor (|Q1^T Q1 - I| ~ 1e-14), at 1e5 (~1e-6) and 1e7
+    (A^T A at 1e14) the exact (blocked) factor runs in both passes.  Against the Householder
+    restatement; CholeskyQR2 loses ~cond * eps."""
     from stiefel import StiefelBatch
     n, p, B = 200, 50, 4
     M = Stiefel(n, p)
