@@ -427,8 +427,8 @@ __global__ void __launch_bounds__(T) k_st_proj3(int n, int p, int64_t stride, co
 #pragma unroll
     for (int g = 0; g < 4; ++g) {   // M is zero outside [0, p)^2 (the update's k steps past p rely on it)
       const int i0 = 16 * I0 + kk + 4 * g, j0 = 16 * J0 + c, i1 = 16 * I1 + kk + 4 * g, j1 = 16 * J1 + c;
-      Ms[i0 * S + j0] = acc0[g] * mask01(i0 < p && j0 < p);
-      if (I1 >= 0) Ms[i1 * S + j1] = acc1[g] * mask01(i1 < p && j1 < p);
+      Ms[i0 * S + (j0 ^ (i0 & 15))] = acc0[g] * mask01(i0 < p && j0 < p);   // column XOR row: see bk below
+      if (I1 >= 0) Ms[i1 * S + (j1 ^ (i1 & 15))] = acc1[g] * mask01(i1 < p && j1 < p);
     }
   }
   __syncthreads();
@@ -440,7 +440,9 @@ __global__ void __launch_bounds__(T) k_st_proj3(int n, int p, int64_t stride, co
 #pragma unroll
   for (int s = 0; s < S4; ++s) {
     const int k = 4 * s + kk, j = 16 * J + c;
-    bk[s] = 0.5 * (Ms[k * S + j] + Ms[j * S + k]);   // zero past p (M is zero there)
+    // zero past p (M is zero there).  M's columns are XOR-swizzled by the row, so the transposed read
+    // (16 lanes on 16 rows of one column) is bank-conflict free (unswizzled: 16-way)
+    bk[s] = 0.5 * (Ms[k * S + (j ^ (k & 15))] + Ms[j * S + (k ^ (j & 15))]);
   }
   switch (P4) {   // the update specialised on the k steps, so no MFMA sits behind a per-step branch
     case 13: p3_update<P16, 13, UMAX>(Xs, bk, cv, out + o, n, p, w, c, kk, J, nunits); break;
