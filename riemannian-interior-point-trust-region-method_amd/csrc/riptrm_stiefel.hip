@@ -642,8 +642,10 @@ __global__ void __launch_bounds__(T) k_st_retr_r(int n, int p, int64_t stride, c
 // the whole CholeskyQR2 and turns every O(n p^2) step into fp64 MFMA work:
 //   1. A -> LDS, row-major with stride S = 16 ceil(p/16), zero padded to NR = 16 ceil(n/16) rows,
 //      element (r, c) at r S + (c ^ (r & 15)) (XOR swizzle inside 16-column groups: the Gram reads a
-//      row's 16 consecutive columns per lane group, the product reads 16 rows of one column; both
-//      are bank-conflict free);
+//      row's 16 consecutive columns per lane group, the product reads 16 rows of one column; a
+//      32-lane ds_read_b64 group still spans only 32 of the 64 banks, 2-way — swapping odd rows'
+//      16-column blocks in pairs removes that but measured no faster: Gram 16.5k vs 16.9k ticks,
+//      load 17.4k vs 14.7k; profiles/r3_stiefel_retr_block_pair_swizzle_stamps.jsonl);
 //   2. G = A^T A: the upper 16 x 16 blocks (I <= J), each split over two k halves, the
 //      (block, half) tasks dealt to the 8 waves; halves meet once in a fixed order;
 //   3. E = L^-1 (G = L L^T) by symmetric Gauss-Jordan elimination on registers: thread (j = lane,
