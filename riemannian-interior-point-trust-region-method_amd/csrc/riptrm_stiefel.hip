@@ -674,6 +674,14 @@ __device__ __forceinline__ void r2_block_ij(int b, int& I, int& J) {
   J = i + b;
 }
 
+// the factor of k_st_retr2: 2 = blocked (r3_factor_blocked, default); 0 = the 8-wave exchange
+// (r2_factor_inverse); 1 = one wave, no barrier per step (r2_factor_inverse_1w), measured 159k vs 69k
+// ticks per factor at (200, 50) (profiles/r3_stiefel_factor_1wave_stamps.jsonl).  A/B:
+// tools/stiefel_stamps.hip -DRIPTRM_ST_FACTOR=0/1.  With 2 the Gram writes only G's upper triangle.
+#ifndef RIPTRM_ST_FACTOR
+#define RIPTRM_ST_FACTOR 2
+#endif
+
 // MASK = false when every batch is full (both halves a multiple of the batch size, e.g. n = 200): the
 // 0/1 factor on each A operand is then dropped — with it in, each read's multiply waits on that read
 // inside the batch (s_waitcnt lgkmcnt after every 4 reads), which serialises the batch's LDS latency.
@@ -743,7 +751,9 @@ __device__ __forceinline__ void r2_gram_finish(lds_f64* Gm, lds_f64* red) {
       const int i = 16 * I + (ll >> 4) + 4 * q, j = 16 * J + (ll & 15);   // f64 D: row (l >> 4) + 4 q, col l & 15
       if (I < J || i <= j) {   // one writer per symmetric pair: G exactly symmetric
         Gm[i * S + j] = v[m];
+#if RIPTRM_ST_FACTOR != 2
         Gm[j * S + i] = v[m];
+#endif
       }
     }
   }
@@ -763,12 +773,6 @@ __device__ __forceinline__ void r2_gram(lds_f64* As, lds_f64* Gm, lds_f64* red, 
 #define RIPTRM_ST_FB 2   // measured: 1 -> 75.7k, 2 -> 69.3k, 4 -> 77.6k ticks per factor at p = 50
 #endif
 constexpr int FB = RIPTRM_ST_FB;
-// the factor of k_st_retr2: 0 = the 8-wave exchange (r2_factor_inverse, default); 1 = one wave, no
-// barrier per step (r2_factor_inverse_1w), measured 159k vs 69k ticks per factor at (200, 50)
-// (profiles/r3_stiefel_factor_1wave_stamps.jsonl).  A/B: tools/stiefel_stamps.hip -DRIPTRM_ST_FACTOR=1
-#ifndef RIPTRM_ST_FACTOR
-#define RIPTRM_ST_FACTOR 2
-#endif
 // pivot reciprocal of the blocked factor's diagonal blocks: IEEE division (0) or v_rcp_f64 + Newton (1)
 #ifndef RIPTRM_ST_RCP
 #define RIPTRM_ST_RCP 1   // measured 37.9k vs 39.3k ticks per factor at (200, 50)
@@ -1005,7 +1009,10 @@ __device__ __forceinline__ void r3_diag_factor(const lds_f64* Gm, lds_f64* Fb, i
 #pragma unroll
   for (int s = 0; s < 4; ++s) {
     const int a = 4 * q + s, i = 16 * K + a;
-    const double v = Gm[i * S + jj];   // always in range (i, jj < S)
+    // the upper triangle of the block (the Gram writes only the upper half of G; the trailing
+    // updates keep the diagonal blocks' upper half exact), mirrored below the diagonal
+    const double vu = Gm[i * S + jj], vl = Gm[jj * S + i];   // always in range (i, jj < S)
+    const double v = a <= j ? vu : vl;
     g[s] = (i < p && jj < p) ? v : (a == j ? 1.0 : 0.0);
     e[s] = a == j ? 1.0 : 0.0;
     piv[s] = 1.0;
@@ -1212,9 +1219,9 @@ __device__ __forceinline__ bool r2_inverse_first_order(lds_f64* Gm, lds_f64* red
   constexpr int S = 16 * P16;
   const int t = threadIdx.x;
   double dev = 0.0;
-  for (int e = t; e < S * S; e += T) {
+  for (int e = t; e < S * S; e += T) {   // the upper triangle (the Gram writes only that half)
     const int i = e / S, j = e - (e / S) * S;
-    if (i < p && j < p) dev = fmax(dev, fabs(Gm[e] - (i == j ? 1.0 : 0.0)));
+    if (i <= j && j < p) dev = fmax(dev, fabs(Gm[e] - (i == j ? 1.0 : 0.0)));
   }
   for (int off = 32; off > 0; off >>= 1) dev = fmax(dev, __shfl_xor(dev, off));
   if ((t & 63) == 0) red[t >> 6] = dev;
