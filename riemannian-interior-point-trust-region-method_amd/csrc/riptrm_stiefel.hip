@@ -766,6 +766,123 @@ __device__ __forceinline__ void r2_gram(lds_f64* As, lds_f64* Gm, lds_f64* red, 
   r2_gram_finish<P16>(Gm, red);
 }
 
+// The Gram with a narrow last column block (P16 = 4, tw = p - 48 <= 4 valid columns in it, e.g.
+// p = 50): the 16 x 16 MFMA blocks that touch that block (4 of the 10) do the work of 2 columns in
+// 16, so they are dropped — the matrix cores take the 6 blocks of the first 48 columns and the VALU
+// takes the tw last columns: wave w sums rows [26 w, 26 w + 26) of A[r][i] A[r][48 + t] in lane i,
+// the 8 wave partials meet in wave order.  G's last column block is written whole (zeros past p),
+// upper triangle only (RIPTRM_ST_FACTOR 2 reads nothing else).  Unmasked batches only.
+#ifndef RIPTRM_ST_GTAIL
+#define RIPTRM_ST_GTAIL 1
+#endif
+template <int TW>
+__device__ __forceinline__ void r4t_gram(lds_f64* As, lds_f64* Gm, lds_f64* red, int NR, int n, int p) {
+  constexpr int S = 64, PM = 3, NBm = 6, c0 = 48, UB2 = 13;
+  const int t = threadIdx.x, l = t & 63, w = t >> 6, c = l & 15, kk = l >> 4;
+  const int NG = NR / 4, H0 = NG / 2;
+  // (1) MFMA: the 6 upper blocks of the first 48 columns, both k halves
+  for (int task = w; task < 2 * NBm; task += NW) {   // wave-uniform
+    const int b = task % NBm, h = task / NBm;
+    int I, J;
+    r2_block_ij<PM>(b, I, J);
+    const int g0 = h ? H0 : 0, g1 = h ? NG : H0;
+    dbl4 acc2[2] = {dbl4{0.0, 0.0, 0.0, 0.0}, dbl4{0.0, 0.0, 0.0, 0.0}};
+    for (int g = g0; g < g1; g += UB2) {
+      double av[UB2], bv[UB2];
+#pragma unroll
+      for (int u = 0; u < UB2; ++u) {
+        const int r = 4 * (g + u) + kk;
+        const lds_f64* row = As + r * S;
+        av[u] = row[(16 * I + c) ^ (r & 15)];
+        bv[u] = row[(16 * J + c) ^ (r & 15)];
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int u = 0; u < UB2; ++u)
+        acc2[u & 1] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[u], bv[u], acc2[u & 1], 0, 0, 0);
+    }
+    const dbl4 acc = acc2[0] + acc2[1];
+    lds_f64* dst = (h ? red : Gm) + b * 256;   // half 0 partials in Gm's space, half 1 in red
+#pragma unroll
+    for (int q = 0; q < 4; ++q) dst[q * 64 + l] = acc[q];
+  }
+  // (2) VALU: this wave's rows of the tw last columns, column i = lane
+  lds_f64* tb = Gm + 2048;   // [NW][4][64] wave partials (past the half-0 MFMA partials)
+  {
+    const int RB = (NR + NW - 1) / NW, r0 = w * RB, r1 = r0 + RB < n ? r0 + RB : n;
+    const int ic = l < p ? l : p - 1;
+    double sum[TW];
+#pragma unroll
+    for (int q = 0; q < TW; ++q) sum[q] = 0.0;
+    for (int r = r0; r < r1; ++r) {
+      const lds_f64* row = As + r * S;
+      const double ai = row[(ic & ~15) | ((ic & 15) ^ (r & 15))];
+#pragma unroll
+      for (int q = 0; q < TW; ++q) sum[q] = __builtin_fma(ai, row[c0 + (q ^ (r & 15))], sum[q]);
+    }
+#pragma unroll
+    for (int q = 0; q < TW; ++q) tb[(w * 4 + q) * 64 + l] = sum[q];
+  }
+  __syncthreads();
+  // (3) partial sums into registers (MFMA halves in a fixed order; the tail in wave order)
+  constexpr int PER = (NBm * 256 + T - 1) / T;
+  double v[PER];
+#pragma unroll
+  for (int m = 0; m < PER; ++m) {
+    const int e = t + m * T;
+    v[m] = e < NBm * 256 ? Gm[e] + red[e] : 0.0;
+  }
+  double tv = 0.0;
+  if (t < TW * 64) {
+    const int q = t >> 6, i = t & 63;
+    tv = tb[q * 64 + i];
+#pragma unroll
+    for (int ww = 1; ww < NW; ++ww) tv = tv + tb[(ww * 4 + q) * 64 + i];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int m = 0; m < PER; ++m) {
+    const int e = t + m * T;
+    if (e < NBm * 256) {
+      const int b = e >> 8, q = (e >> 6) & 3, ll = e & 63;
+      int I, J;
+      r2_block_ij<PM>(b, I, J);
+      const int i = 16 * I + (ll >> 4) + 4 * q, j = 16 * J + (ll & 15);
+      if (I < J || i <= j) Gm[i * S + j] = v[m];
+    }
+  }
+  // the last column block: the tail sums at rows i < p, zero elsewhere (upper part)
+  for (int e = t; e < S * 16; e += T) {
+    const int i = e >> 4, jj = e & 15, j = c0 + jj;
+    if (i <= j && !(jj < TW && i < p)) Gm[i * S + j] = 0.0;
+  }
+  if (t < TW * 64) {
+    const int q = t >> 6, i = t & 63;
+    if (i < p && i <= c0 + q) Gm[i * S + c0 + q] = tv;
+  }
+  __syncthreads();
+}
+
+// r4t_gram where it applies (P16 = 4, 1 <= p - 48 <= 4, whole batches, the blocked factor), else r2_gram
+template <int P16>
+__device__ __forceinline__ void r2_gram_any(lds_f64* As, lds_f64* Gm, lds_f64* red, int NR, int n, int p) {
+#if RIPTRM_ST_GTAIL && RIPTRM_ST_FACTOR == 2
+  if (P16 == 4) {
+    const int NG = NR / 4, H0 = NG / 2;
+    if (H0 % 13 == 0 && (NG - H0) % 13 == 0) {
+      switch (p - 48) {
+        case 1: r4t_gram<1>(As, Gm, red, NR, n, p); return;
+        case 2: r4t_gram<2>(As, Gm, red, NR, n, p); return;
+        case 3: r4t_gram<3>(As, Gm, red, NR, n, p); return;
+        case 4: r4t_gram<4>(As, Gm, red, NR, n, p); return;
+        default: break;
+      }
+    }
+  }
+#endif
+  r2_gram<P16>(As, Gm, red, NR);
+}
+
 // Gm (G, stride S) -> Gm (W = R^-1 = E^T, stride S); xch: 4 FB S doubles of exchange space (the Gram's
 // partial-sum area, NB * 256 >= 16 S doubles)
 // columns eliminated per barrier step of r2_factor_inverse (tools/stiefel_stamps.hip builds 1 / 2 / 4 for A/B)
@@ -1353,7 +1470,7 @@ __global__ void __launch_bounds__(T) k_st_retr2(int n, int p, int64_t stride, co
   }
   __syncthreads();
   ST_STAMP(1);
-  r2_gram<P16>(As, Gm, red, NR);
+  r2_gram_any<P16>(As, Gm, red, NR, n, p);
   ST_STAMP(2);
 #if RIPTRM_ST_FACTOR == 1
   r2_factor_inverse_1w<P16>(Gm, red, p);
@@ -1369,7 +1486,7 @@ __global__ void __launch_bounds__(T) k_st_retr2(int n, int p, int64_t stride, co
   ST_STAMP(3);
   r2_apply<P16, false>(As, Gm, NR, n, p, out + o);
   ST_STAMP(4);
-  r2_gram<P16>(As, Gm, red, NR);
+  r2_gram_any<P16>(As, Gm, red, NR, n, p);
   ST_STAMP(5);
 #if RIPTRM_ST_FACTOR == 1
   if (!r2_inverse_first_order<P16>(Gm, red, p)) r2_factor_inverse_1w<P16>(Gm, red, p);
