@@ -184,6 +184,44 @@ def cpu_reference_structured(n: int, budget_s: float):
                        f"budget")}
 
 
+def host_cpu_info() -> dict:
+    """lscpu model name and os.cpu_count() of the host the CPU legs ran on."""
+    model = None
+    try:
+        import subprocess
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        for line in out.splitlines():
+            if line.split(":")[0].strip() == "Model name":
+                model = line.split(":", 1)[1].strip()
+                break
+    except Exception:
+        pass
+    if model is None:
+        try:
+            for line in open("/proc/cpuinfo"):
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+        except Exception:
+            pass
+    return {"cpu_model": model, "os_cpu_count": os.cpu_count()}
+
+
+def pick_cpu_baseline(threaded, pool):
+    """report the better of the two CPU variants (one process with all BLAS threads,
+    a pool of single-threaded processes) and name the other under ``other_variant``.  Either may be
+    None (not run or incomplete).  Returns a new dict (or None)."""
+    legs = [c for c in (threaded, pool) if c is not None]
+    if not legs:
+        return None
+    best = max(legs, key=lambda c: c["value"])
+    out = dict(best)
+    other = pool if best is threaded else threaded
+    if other is not None:
+        out["other_variant"] = {"value": other["value"], "cores": other["cores"], "sample": other["sample"]}
+    return out
+
+
 def _free_port() -> int:
     import socket
     s = socket.socket()
@@ -191,6 +229,24 @@ def _free_port() -> int:
     port = s.getsockname()[1]
     s.close()
     return port
+
+
+def rank_census(dist, world: int, rank: int, dev):
+    """Every rank's (rank, world size it saw, device index, backend is RCCL) gathered to all ranks
+    with one all_gather, so the JSON line shows which collective backend really ran with how many
+    ranks on which devices.  World 1: just this process."""
+    import torch
+    backend = dist.get_backend() if world > 1 else None
+    me = torch.tensor([rank, dist.get_world_size() if world > 1 else 1, dev.index if dev.index is not None else 0,
+                       1 if backend == "nccl" else 0], dtype=torch.int64,
+                      device=dev if backend == "nccl" else "cpu")
+    if world == 1:
+        rows = [me]
+    else:
+        rows = [torch.empty_like(me) for _ in range(world)]
+        dist.all_gather(rows, me)
+    return [{"rank": int(r[0]), "world_size_seen": int(r[1]), "device": int(r[2]), "rccl": bool(r[3])}
+            for r in (t.cpu() for t in rows)]
 
 
 def launch_ranks(n: int, script: str | None = None, argv=None) -> int:
@@ -265,6 +321,8 @@ def main():
                     help="k_persist for small batches: 1 = cooperative launch (default), 2 = plain launch (A/B), 0 = off")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_gemv.json"))
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend (nccl = RCCL)")
+    ap.add_argument("--dump", default="",
+                    help="rank 0 writes the gathered x, y and stats of every global instance to this .npz")
     ap.add_argument("--same-device", action="store_true",
                     help="rehearsal only: every rank on cuda:0 (use with --backend gloo on a 1-GPU box)")
     args = ap.parse_args()
@@ -359,6 +417,7 @@ def main():
     counts = torch.tensor([outer, passes, inner, tcg, prof["gemv_ms"], prof["gemv_launches"]],
                           dtype=torch.float64, device=dev)
     tmax = torch.tensor([el], dtype=torch.float64, device=dev)
+    ranks_seen = rank_census(dist, world, rank, dev)
     if world > 1:
         from distributed import gather_rows
         dist.all_reduce(counts, op=dist.ReduceOp.SUM)
@@ -366,9 +425,16 @@ def main():
         # final gather of per-instance results (x, y, stats) over RCCL, in global instance order
         res = eng.result()
         total = B * world
-        gather_rows(res.x.contiguous(), total, world, rank)
-        gather_rows(res.y.contiguous(), total, world, rank)
-        gather_rows(torch.as_tensor(res.stats, device=dev), total, world, rank)
+        gx = gather_rows(res.x.contiguous(), total, world, rank)
+        gy = gather_rows(res.y.contiguous(), total, world, rank)
+        gs = gather_rows(torch.as_tensor(res.stats, device=dev), total, world, rank)
+    elif args.dump:
+        res = eng.result()
+        gx, gy, gs = res.x, res.y, torch.as_tensor(res.stats)
+    if args.dump and rank == 0:
+        # gathered per-instance results in global instance order (tests compare them bitwise)
+        np.savez(args.dump, x=gx.cpu().numpy()[:, :n], y=gy.cpu().numpy()[:, :n], stats=gs.cpu().numpy(),
+                 ids=np.arange(B * world), seed0=args.seed0, outer_target=W + K)
     T = float(tmax.item())
     outer_all, passes_all, inner_all, tcg_all, gemv_ms_all, gemv_n_all = [float(v) for v in counts.tolist()]
 
@@ -451,20 +517,17 @@ def main():
         if args.cpu_budget > 0 and world == 1:
             positions = window_positions(W, K, args.cycle)
             log(f"CPU baseline (oracle) over positions {_pos_text(positions)} ...")
-            cpu = cpu_baseline(n, positions, args.cpu_budget, args.trs)
+            threaded = cpu_baseline(n, positions, args.cpu_budget, args.trs)
             # the pool runs one instance per process: never more processes than the workload has
             # instances (configs[1] is ONE instance; 16 processes would time 16x its work)
             procs = min(args.cpu_procs, B)
+            pool = None
             if procs > 0:
                 log(f"CPU baseline, {procs} single-threaded processes ...")
                 pool = cpu_baseline_pool(n, positions, args.cpu_pool_budget, procs, args.trs)
-                if pool is not None:
-                    alt = cpu
-                    if cpu is None or pool["value"] > cpu["value"]:
-                        cpu, alt = pool, cpu
-                    if alt is not None:   # report the better variant, name the other
-                        cpu["other_variant"] = {"value": alt["value"], "cores": alt["cores"], "sample": alt["sample"]}
+            cpu = pick_cpu_baseline(threaded, pool)
             if cpu is not None:
+                cpu.update(host_cpu_info())
                 cpu["gpu_over_cpu"] = (outer_all / T) / cpu["value"]
                 if args.ref_structured_dim > 0:
                     log(f"CPU reference-structured variant (R), n={args.ref_structured_dim} ...")
@@ -492,7 +555,8 @@ def main():
                        "trs_solver": args.trs,
                        "n": n, "batch_per_gpu": B, "global_batch": B * world,
                        "outer_window": [W + 1, W + K], "restart_every": args.cycle, "layout": args.layout,
-                       "parallelism": f"instance-sharded x{world}", "world_size": world},
+                       "parallelism": f"instance-sharded x{world}", "world_size": world,
+                       "backend": dist.get_backend() if world > 1 else None, "ranks": ranks_seen},
             "roofline": roofline,
             "cpu_baseline": cpu,
             "detail": {"inner_iterations_per_s": inner_all / T, "tcg_iterations_per_s": tcg_all / T,
@@ -503,7 +567,7 @@ def main():
                        if graph_mode else "HIP events inside the timed window",
                        "state_kernel_ms": prof["state_ms"], "state_launches": prof["state_launches"],
                        "gemv_launches": prof["gemv_launches"],
-                       "spass_calibration": cal or None},
+                       **({"spass_calibration": cal} if cal.get("ms_per_launch_tile") else {})},
         }
         print(json.dumps(out), flush=True)
     if world > 1:
@@ -744,16 +808,13 @@ def bench_si(args, world, rank, dev, dist):
                    "sample": f"oracle/si_oracle.py SIVectorized (NumPy, closed-form Lagrangian), start 'a', outer "
                              f"iterations 1..{last} ({secs:.1f} s, evaluation time excluded as RIPTRM.py:932-941)"}
         procs = min(args.cpu_procs, B)
+        pool = None
         if procs > 0:
             log(f"SI CPU baseline, {procs} single-threaded processes ...")
             pool = si_cpu_pool(K, args.cpu_pool_budget, procs, args.trs)
-            if pool is not None:
-                alt = cpu
-                if cpu is None or pool["value"] > cpu["value"]:
-                    cpu, alt = pool, cpu
-                if alt is not None:
-                    cpu["other_variant"] = {"value": alt["value"], "cores": alt["cores"], "sample": alt["sample"]}
+        cpu = pick_cpu_baseline(cpu, pool)
         if cpu is not None:
+            cpu.update(host_cpu_info())
             cpu["gpu_over_cpu"] = (outer / T) / cpu["value"]
     print(json.dumps({
         "metric": f"outer RIPTRM iterations/sec, StableIdentification d=5 (Product(Skew,SPD,SPD)), batch {B}/GPU",

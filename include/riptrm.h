@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define RIPTRM_ABI_VERSION 8
+#define RIPTRM_ABI_VERSION 9
 
 /* status codes */
 #define RIPTRM_OK 0
@@ -51,17 +51,27 @@ extern "C" {
 /* not a reference code: tCG met a non-finite <delta, H delta> (the instance then stops with
  * RIPTRM_ERR_NONFINITE) */
 #define RIPTRM_TCG_NONFINITE 9
+/* not a reference code: the Exact_RepMat eigendecomposition did not converge (the instance then
+ * stops with RIPTRM_ERR_EIGEN) */
+#define RIPTRM_TCG_EIGFAIL 10
 
 /* per-instance error codes (RIPTRM_STAT_ERROR).  An instance with an error stops (phase error);
- * the others of the batch go on.  RIPTRM_ERR_NONFINITE is the device's counterpart of the
- * reference's do_exit_on_error break (RIPTRM.py:961-966: an exception inside outer_step ends the
- * run with the iterate that outer step started from): a NaN / Inf in the KKT residual at the
- * outer loop head, in ||cxCur|| or Delta at a tCG start, or in <delta, H delta> inside tCG stops
- * the instance and restores x, y to the start of the outer step it appeared in. */
+ * the others of the batch go on.
+ * RIPTRM_ERR_NONFINITE: a NaN / Inf in ||cxCur|| or Delta at a tCG start, or in <delta, H delta>
+ * inside tCG, stops the instance and restores x, y to the start of the outer step it appeared in
+ * -- the reference's do_exit_on_error break (RIPTRM.py:961-966: an exception inside outer_step ends
+ * the run with the iterate that outer step started from; numpy would raise there on the NaN).
+ * A NaN / Inf KKT residual at the outer loop head also stops the instance, keeping x, y as they
+ * are.  That site is a deliberate deviation: the reference raises nothing there (`residual <=
+ * tolresid` is just False) and would keep iterating on the NaN iterate.
+ * RIPTRM_ERR_EIGEN: the HBM Exact_RepMat path's eigendecomposition (rocSOLVER dsyevd) reported
+ * info != 0, or the trial-point eigenvalue was not finite, where scipy.linalg.eig / eigh raises
+ * LinAlgError inside outer_step: same break and restore as RIPTRM_ERR_NONFINITE. */
 #define RIPTRM_ERR_NONE 0
 #define RIPTRM_ERR_NO_TCG_ITER 1       /* manifold.dim = 0: tCG cannot iterate */
 #define RIPTRM_ERR_BARRIER_TIMEOUT 2   /* persistent mode: a peer workgroup never arrived (2 s) */
 #define RIPTRM_ERR_NONFINITE 3
+#define RIPTRM_ERR_EIGEN 4
 
 /* TRS_solver option (RIPTRM.py:325) */
 #define RIPTRM_TRS_SOLVER_TCG 0
@@ -387,6 +397,10 @@ int riptrm_trs_gep(riptrm_ctx* ctx, int32_t dim, int32_t batch, const double* A,
  * trial point) parks; riptrm_solve_advance serves parked instances after its lock-step chunk and
  * synchronises then.  Binding NULL unbinds. */
 int64_t riptrm_trs_workspace_bytes(int32_t order, int32_t slots);
+/* Whether the HBM path's eigensolver could be loaded (host only, no device work): RIPTRM_OK, or
+ * RIPTRM_E_HIP with the dlopen message in msg (len bytes, NUL-terminated).  The libraries are
+ * librocblas.so.5 / librocsolver.so.0 unless RIPTRM_ROCBLAS_LIB / RIPTRM_ROCSOLVER_LIB name others. */
+int riptrm_trs_backend_status(char* msg, int32_t len);
 int riptrm_trs_bind_workspace(riptrm_ctx* ctx, void* ws, int64_t bytes, int32_t order, int32_t slots);
 
 /* ==== Stiefel(n, p) manifold operations =========================================

@@ -1486,16 +1486,17 @@ struct MachineT {
   // eigenvalue from HBM (riptrm_trs_big.hip)
   __device__ __forceinline__ bool trs_big() const { return n - 1 > riptrm_trs::DIM_MAX; }
 
-  // Non-finite guard (include/riptrm.h RIPTRM_ERR_NONFINITE; RIPTRM.py:961-966): stop the
-  // instance and hand back the iterate its current (or, at the loop head, its last) outer step
-  // started from.  Outer iteration 0 / a tCG-only run keep x, y as they are.
-  __device__ __forceinline__ int nonfinite_stop() {
-    if (s[ST_OUTER_IT] > 0.0 && (int)s[ST_MODE] == MODE_SOLVE) {
+  // Error stop (include/riptrm.h RIPTRM_ERR_NONFINITE / RIPTRM_ERR_EIGEN; RIPTRM.py:961-966):
+  // stop the instance; inside an outer step (restore) hand back the iterate that step started
+  // from, as the reference's break after an exception in outer_step does.  At the outer loop
+  // head (restore = false) the completed iterate stays.  A tCG-only run keeps x, y as they are.
+  __device__ __forceinline__ int nonfinite_stop(bool restore = true, int code = RIPTRM_ERR_NONFINITE) {
+    if (restore && s[ST_OUTER_IT] > 0.0 && (int)s[ST_MODE] == MODE_SOLVE) {
       copy(V_X, V_X0);
       copy(V_Y, V_Y0);
       copy(V_SX, V_SX0);
     }
-    cset(ST_ERROR, (double)RIPTRM_ERR_NONFINITE);
+    cset(ST_ERROR, (double)code);
     cset(ST_STOP_RUNTIME, (unow() - s[ST_T_START]) / P.clock_hz);
     s[ST_PHASE] = PH_ERROR;
     return ACT_DONE;
@@ -1509,7 +1510,7 @@ struct MachineT {
     const double tn = unow();
     if (s[ST_OUTER_IT] == 0.0 || !save_inner) log_row(ev, s[ST_OUTER_IT] != 0.0, tn);
     cset(ST_RESIDUAL, ev[2]);
-    if (!isfinite(ev[2])) return nonfinite_stop();
+    if (!isfinite(ev[2])) return nonfinite_stop(false);   // deliberate deviation, include/riptrm.h
     const double rt = (tn - s[ST_T_START]) / P.clock_hz;
     int stop = RIPTRM_STOP_NONE;
     if (rt >= P.opt.maxtime) stop = RIPTRM_STOP_MAXTIME;
@@ -1990,6 +1991,7 @@ struct MachineT {
   // after tCG: RIPTRM.py:733-746 (direction, ||dx||, dy, retraction) + feasibility part of :591
   __device__ __forceinline__ int tcg_end() {
     if (s[ST_TCG_STOP] == RIPTRM_TCG_NONFINITE) return nonfinite_stop();
+    if (s[ST_TCG_STOP] == RIPTRM_TCG_EIGFAIL) return nonfinite_stop(true, RIPTRM_ERR_EIGEN);
     cadd(ST_TCG_TOTAL, s[ST_J] + 1.0);
     const double* X = V(V_X);
     const double* Y = V(V_Y);
@@ -2270,7 +2272,8 @@ struct MachineT {
         return ACT_DONE;
       case PH_TRS_END:
         return tcg_end();
-      case PH_MINEIG_END:   // the host wrote s[ST_MINEIG] (riptrm_trs_big.hip)
+      case PH_MINEIG_END:   // the host wrote s[ST_MINEIG] (riptrm_trs_big.hip); NaN: dsyevd failed
+        if (!isfinite(s[ST_MINEIG])) return nonfinite_stop(true, RIPTRM_ERR_EIGEN);
         mineig_test();
         return tcg_end_tail();
       default:

@@ -23,6 +23,7 @@
 #include <hip/hip_runtime.h>
 #include <dlfcn.h>
 #include <math.h>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -424,7 +425,8 @@ __global__ void __launch_bounds__(256) k_pick(int m, const double* cgx, double* 
 
 // eta = H [0; x] (RIPTRM.py:442-444 in the Householder frame), the direction type, j = -1, and the
 // instance resumes at PH_TRS_END
-__global__ void __launch_bounds__(WG) k_finish_dir(DevParams P, int b, const double* w, const double* x, const double* sc) {
+__global__ void __launch_bounds__(WG) k_finish_dir(DevParams P, int b, const double* w, const double* x, const double* sc,
+                                                   const int32_t* info) {
   __shared__ double red[WG / 64];
   const int n = P.n;
   double wz = 0.0;
@@ -435,15 +437,17 @@ __global__ void __launch_bounds__(WG) k_finish_dir(DevParams P, int b, const dou
   for (int i = threadIdx.x; i < n; i += WG) E[i] = (i == 0 ? 0.0 : x[i - 1]) - tau * w[i] * wz;
   if (threadIdx.x == 0) {
     double* s = P.st + (int64_t)b * ST_N;
-    s[ST_TCG_STOP] = RIPTRM_TRS_BOUNDARY + sc[SC_KIND];
+    // dsyevd did not converge (info > 0): scipy.linalg.eig would raise LinAlgError inside
+    // outer_step (RIPTRM.py:961-966); the machine stops the instance at PH_TRS_END
+    s[ST_TCG_STOP] = *info != 0 ? (double)RIPTRM_TCG_EIGFAIL : RIPTRM_TRS_BOUNDARY + sc[SC_KIND];
     s[ST_J] = -1.0;
     s[ST_PHASE] = PH_TRS_END;
   }
 }
 
-__global__ void k_finish_mineig(DevParams P, int b, const double* ev) {
+__global__ void k_finish_mineig(DevParams P, int b, const double* ev, const int32_t* info) {
   double* s = P.st + (int64_t)b * ST_N;
-  s[ST_MINEIG] = ev[0];
+  s[ST_MINEIG] = *info != 0 ? NAN : ev[0];   // non-converged dsyevd: the machine stops the instance
   s[ST_PHASE] = PH_MINEIG_END;
 }
 
@@ -470,6 +474,8 @@ __global__ void __launch_bounds__(256) k_load(int m, const double* A, int64_t ld
 }
 
 // ---- rocSOLVER, loaded on first use (no link-time dependency of the library) -----------------------
+// (RIPTRM_ROCBLAS_LIB / RIPTRM_ROCSOLVER_LIB in the environment name other libraries: a host whose
+// ROCm is elsewhere, or a test that checks the failure path)
 typedef int (*fn_create_t)(void**);
 typedef int (*fn_set_stream_t)(void*, hipStream_t);
 typedef int (*fn_destroy_t)(void*);
@@ -489,12 +495,22 @@ static Solver& solver() {
   static Solver s;
   if (s.tried) return s;
   s.tried = true;
-  void* blas = dlopen("librocblas.so.5", RTLD_NOW | RTLD_GLOBAL);
-  if (!blas) blas = dlopen("librocblas.so", RTLD_NOW | RTLD_GLOBAL);
-  void* sol = dlopen("librocsolver.so.0", RTLD_NOW | RTLD_GLOBAL);
-  if (!sol) sol = dlopen("librocsolver.so", RTLD_NOW | RTLD_GLOBAL);
+  // dlerror() returns the last message once and clears it: record it right after each failure
+  auto open_first = [](const char* a, const char* b) -> void* {
+    void* h = dlopen(a, RTLD_NOW | RTLD_GLOBAL);
+    if (!h) h = dlopen(b, RTLD_NOW | RTLD_GLOBAL);
+    if (!h) {
+      const char* de = dlerror();
+      s.why += std::string(s.why.empty() ? "" : "; ") + a + ": " + (de ? de : "not found");
+    }
+    return h;
+  };
+  const char* eb = getenv("RIPTRM_ROCBLAS_LIB");
+  const char* es = getenv("RIPTRM_ROCSOLVER_LIB");
+  void* blas = eb && *eb ? open_first(eb, eb) : open_first("librocblas.so.5", "librocblas.so");
+  void* sol = es && *es ? open_first(es, es) : open_first("librocsolver.so.0", "librocsolver.so");
   if (!blas || !sol) {
-    s.why = std::string("cannot load rocBLAS / rocSOLVER: ") + (dlerror() ? dlerror() : "not found");
+    s.why = "cannot load rocBLAS / rocSOLVER: " + s.why;
     return s;
   }
   s.create = (fn_create_t)dlsym(blas, "rocblas_create_handle");
@@ -614,11 +630,11 @@ int riptrm_big_service(riptrm_ctx* c, int* served) {
       if (int rc = big_handle(c)) return rc;
       if (solver().syevd(c->big_handle, EVECT_NONE, FILL_UPPER, n - 1, A, n, q.v[VS_EV], q.v[VS_EW], q.info) != 0)
         return fail(c, RIPTRM_E_HIP, "rocsolver_dsyevd failed");
-      hipLaunchKernelGGL(k_finish_mineig, dim3(1), dim3(1), 0, c->stream, P, b, q.v[VS_EV]);
+      hipLaunchKernelGGL(k_finish_mineig, dim3(1), dim3(1), 0, c->stream, P, b, q.v[VS_EV], q.info);
     } else {
       const double* Delta = P.st + (int64_t)b * ST_N + ST_DELTA;
       if (int rc = big_solve(c, q, A, n, n - 1, Delta, P.opt.trs_tolhardcase)) return rc;
-      hipLaunchKernelGGL(k_finish_dir, dim3(1), dim3(WG), 0, c->stream, P, b, q.v[VS_W], q.v[VS_X], q.sc);
+      hipLaunchKernelGGL(k_finish_dir, dim3(1), dim3(WG), 0, c->stream, P, b, q.v[VS_W], q.v[VS_X], q.sc, q.info);
     }
     HIPCHK(c, hipGetLastError());
     ++*served;
@@ -638,6 +654,12 @@ int riptrm_big_trs_gep(riptrm_ctx* c, int dim, int batch, const double* A, int64
                        A + (int64_t)b * a_stride, lda, a + (int64_t)b * ldv, q.M, q.v[VS_A]);
     HIPCHK(c, hipGetLastError());
     if (int rc = big_solve(c, q, q.M, dim, dim, Delta + b, tolhc)) return rc;
+    int32_t info = 0;
+    HIPCHK(c, hipMemcpyAsync(&info, q.info, sizeof(info), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (info != 0)   // scipy.linalg.eig raises LinAlgError here
+      return fail(c, RIPTRM_E_HIP, "trs_gep: rocsolver_dsyevd did not converge (info " + std::to_string(info) +
+                                       ") on subproblem " + std::to_string(b));
     hipLaunchKernelGGL(k_gep_out, dim3(blocks_of(dim, 256)), dim3(256), 0, c->stream, dim, q.v[VS_X], q.sc, q.v[VS_EV],
                        x + (int64_t)b * ldv, lam1 + b, kind + b, mineig ? mineig + b : nullptr);
     HIPCHK(c, hipGetLastError());
@@ -646,6 +668,16 @@ int riptrm_big_trs_gep(riptrm_ctx* c, int dim, int batch, const double* A, int64
 }
 
 extern "C" {
+
+int riptrm_trs_backend_status(char* msg, int32_t len) {
+  Solver& s = solver();
+  if (msg && len > 0) {
+    const std::string t = s.ok ? std::string("rocBLAS + rocSOLVER dsyevd loaded") : s.why;
+    std::strncpy(msg, t.c_str(), (size_t)len - 1);
+    msg[len - 1] = 0;
+  }
+  return s.ok ? RIPTRM_OK : RIPTRM_E_HIP;
+}
 
 int64_t riptrm_trs_workspace_bytes(int32_t order, int32_t slots) {
   if (order < 1 || slots < 1) return 0;

@@ -39,12 +39,16 @@ TCG_NAMES = {C["RIPTRM_TCG_MAX_INNER_ITER"]: "MAX_INNER_ITER",
              C["RIPTRM_TCG_MODEL_INCREASED"]: "MODEL_INCREASED",
              C["RIPTRM_TCG_REACHED_TARGET_LINEAR"]: "REACHED_TARGET_LINEAR",
              C["RIPTRM_TCG_REACHED_TARGET_SUPERLINEAR"]: "REACHED_TARGET_SUPERLINEAR",
-             C["RIPTRM_TCG_NONFINITE"]: "NONFINITE"}
+             C["RIPTRM_TCG_NONFINITE"]: "NONFINITE", C["RIPTRM_TCG_EIGFAIL"]: "EIGFAIL"}
 ERROR_TEXT = {C["RIPTRM_ERR_NO_TCG_ITER"]: "manifold dimension 0: truncated CG cannot iterate",
               C["RIPTRM_ERR_BARRIER_TIMEOUT"]: "persistent lock-step: a peer workgroup did not arrive within 2 s",
               C["RIPTRM_ERR_NONFINITE"]: ("non-finite value (NaN/Inf) in the KKT residual, the tCG residual, the "
                                           "trust-region radius or <delta, H delta>; returning the iterate the outer "
-                                          "step started from")}
+                                          "step started from (the completed iterate when the residual at the outer "
+                                          "loop head is the non-finite value)"),
+              C["RIPTRM_ERR_EIGEN"]: ("Exact_RepMat: the eigendecomposition did not converge (rocSOLVER dsyevd info != 0; "
+                                      "scipy.linalg.eig raises LinAlgError); returning the iterate the outer step "
+                                      "started from")}
 STATUS_NAMES = {0: None, 1: "initial", 2: "converged", 3: "primal_infeasible", 4: "successful",
                 5: "unsuccessful", 6: "max-time-exceeded", 7: "max-iter-exceeded"}
 RU_NAMES = {0: None, 1: "reduced", 2: "expanded", 3: "unchanged"}

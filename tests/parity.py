@@ -330,6 +330,38 @@ class StateRecorder:
 
 # ---- one GPU instance against the oracle ----------------------------------------------------
 
+def check_against(gl, ra, states, variants, P, step, gpu_x=None, gpu_tcg=None):
+    """check_instance's bar, given the oracle's reference run `ra` (its inner steps' starting
+    states recorded: StateRecorder), the order-perturbed runs `variants` (order_variants), the
+    oracle problem P and its unwrapped inner step (classify_flip's probe)."""
+    exc = []
+    env = None
+    try:
+        compare_logs(gl, ra.log)   # branches + the calibrated bound first (flip detection)
+        env = envelope(ra, variants)
+        compare_logs(gl, ra.log, envelope=env, excursions=exc)
+        if gpu_tcg is not None:
+            compare_tcg_iters(gpu_tcg, ra, env)
+    except BranchFlip:
+        flip = first_branch_flip(gl, ra.log)
+        eps = classify_flip(step, P, states, gl, ra.log, flip)
+        assert eps is not None, ("branch flip not reachable within the accumulated drift", flip,
+                                 gl[flip[1]][flip[0]], ra.log[flip[1]][flip[0]])
+        compare_outer(gl, ra.log)
+        # the rows before the flip still meet the envelope bar (and their tCG exit indices)
+        row = flip[0]
+        if row > 1:
+            env = env if env is not None else envelope(ra, variants)
+            compare_logs(_prefix(gl, row), _prefix(ra.log, row), envelope=env, excursions=exc)
+            if gpu_tcg is not None:
+                pre = type("Pre", (), {"trace": ra.trace[:row - 1]})()
+                compare_tcg_iters(list(gpu_tcg)[:row - 1], pre, {"_tcg": env["_tcg"][:row - 1]})
+        return ("flip", flip + (eps, len(gl["iteration"]), exc))
+    if gpu_x is not None:
+        np.testing.assert_allclose(gpu_x, ra.x, atol=1e-6)
+    return ("excursion", exc) if exc else None
+
+
 def check_instance(gl, Z, x0, y0, opt, gpu_x=None, S=None, gpu_tcg=None):
     """One instance's GPU trajectory against the oracle (dsymv) with tests/parity.py's bar:
     identical branches, outer-iterate values within 1e-4, trial values within 10x the envelope of
@@ -339,37 +371,102 @@ def check_instance(gl, Z, x0, y0, opt, gpu_x=None, S=None, gpu_tcg=None):
     (parity.classify_flip: the GPU's decision is reachable from the oracle's own state at that
     step perturbed by at most the outer-iterate drift accumulated before it, capped at 1e-8); the
     trajectories must then still agree at the outer level (parity.compare_outer).
-    Returns ("flip", (row, key, eps)), ("excursion", [(key, rows)]) or None."""
+    Returns ("flip", (row, key, eps, rows, excursions)), ("excursion", [(key, rows)]) or None."""
     from oracle import riptrm_oracle as O
     Pa = O.NonnegPCAVectorized(Z, S=S)
     oa = O.RIPTRMOracle(opt)
     rec = StateRecorder(oa)
     ra = oa.run(Pa, x0, y0)
-    exc = []
-    try:
-        compare_logs(gl, ra.log)   # branches + the calibrated bound first (flip detection)
-        env = envelope(ra, order_variants(Z, x0, y0, opt, S=S))
-        compare_logs(gl, ra.log, envelope=env, excursions=exc)
-        if gpu_tcg is not None:
-            compare_tcg_iters(gpu_tcg, ra, env)
-    except BranchFlip:
-        flip = first_branch_flip(gl, ra.log)
-        eps = classify_flip(rec.step, Pa, rec.states, gl, ra.log, flip)
-        assert eps is not None, ("branch flip not reachable within the accumulated drift", flip,
-                                 gl[flip[1]][flip[0]], ra.log[flip[1]][flip[0]])
-        compare_outer(gl, ra.log)
-        # the rows before the flip still meet the envelope bar (and their tCG exit indices)
-        row = flip[0]
-        if row > 1:
-            env = envelope(ra, order_variants(Z, x0, y0, opt, S=S))
-            compare_logs(_prefix(gl, row), _prefix(ra.log, row), envelope=env, excursions=exc)
-            if gpu_tcg is not None:
-                pre = type("Pre", (), {"trace": ra.trace[:row - 1]})()
-                compare_tcg_iters(list(gpu_tcg)[:row - 1], pre, {"_tcg": env["_tcg"][:row - 1]})
-        return ("flip", flip + (eps, len(gl["iteration"]), exc))
-    if gpu_x is not None:
-        np.testing.assert_allclose(gpu_x, ra.x, atol=1e-6)
-    return ("excursion", exc) if exc else None
+    return check_against(gl, ra, rec.states, order_variants(Z, x0, y0, opt, S=S), Pa, rec.step,
+                         gpu_x=gpu_x, gpu_tcg=gpu_tcg)
+
+
+VARIANT_SEEDS = (1, 2, 6, 7)
+
+
+def _oracle_job(job):
+    """One oracle run in a pool worker (single-threaded BLAS): the reference run with its inner
+    steps' starting states recorded, the dgemv variant, or dsymv on a symmetric permutation (the
+    runs of check_instance / order_variants)."""
+    kind, s_path, x0, y0, opt, seed = job
+    from oracle import riptrm_oracle as O
+    S = np.load(s_path)
+    if kind == "ref":
+        oa = O.RIPTRMOracle(opt)
+        rec = StateRecorder(oa)
+        return oa.run(O.NonnegPCAVectorized(S, S=S), x0, y0), rec.states
+    if kind == "gemv":
+        return O.RIPTRMOracle(opt).run(O.NonnegPCAVectorized(S, S=S, symv=False), x0, y0), None
+    p = np.random.RandomState(seed).permutation(S.shape[0])
+    Sp = np.ascontiguousarray(S[p][:, p])
+    return O.RIPTRMOracle(opt).run(O.NonnegPCAVectorized(Sp, S=Sp), x0[p], y0[p]), None
+
+
+def check_instances_parallel(items, opt, workers=16, progress=print, every_s=20.0):
+    """check_instance for many instances with the 6 oracle runs of each (reference + the 5
+    order variants) spread over a pool of `workers` single-threaded processes.  items: dicts with
+    gl (the GPU log), S (n x n, the device's own S), x0, y0 and optionally gpu_x, gpu_tcg, name.
+    Checks run in the parent as each instance's runs complete; `progress(msg)` is called at least
+    every `every_s` seconds (long GPU-box tests must show output).  Returns {name: result}."""
+    import concurrent.futures as cf
+    import multiprocessing as mp
+    import os
+    import tempfile
+    import time
+    from oracle import riptrm_oracle as O
+    results = {}
+    keep = {k: os.environ.get(k) for k in ("OMP_NUM_THREADS", "OPENBLAS_NUM_THREADS", "MKL_NUM_THREADS")}
+    with tempfile.TemporaryDirectory() as td:
+        paths = []
+        for k, it in enumerate(items):
+            paths.append(os.path.join(td, f"S{k}.npy"))
+            np.save(paths[-1], np.ascontiguousarray(it["S"], dtype=np.float64))
+        jobs = {}
+        for k, it in enumerate(items):
+            args = (paths[k], np.asarray(it["x0"], np.float64), np.asarray(it["y0"], np.float64), opt)
+            jobs[(k, "ref")] = ("ref",) + args + (None,)
+            jobs[(k, "gemv")] = ("gemv",) + args + (None,)
+            for sd in VARIANT_SEEDS:
+                jobs[(k, sd)] = ("perm",) + args + (sd,)
+        for v in keep:
+            os.environ[v] = "1"
+        try:
+            with cf.ProcessPoolExecutor(max_workers=workers, mp_context=mp.get_context("spawn")) as ex:
+                futs = {ex.submit(_oracle_job, j): key for key, j in jobs.items()}
+                out, pending, t0, last = {}, set(futs), time.time(), time.time()
+                done_items = set()
+                while pending:
+                    fin, pending = cf.wait(pending, timeout=every_s, return_when=cf.FIRST_COMPLETED)
+                    for f in fin:
+                        out[futs[f]] = f.result()
+                    for k, it in enumerate(items):
+                        need = [(k, "ref"), (k, "gemv")] + [(k, sd) for sd in VARIANT_SEEDS]
+                        if k in done_items or any(q not in out for q in need):
+                            continue
+                        done_items.add(k)
+                        ra, states = out[(k, "ref")]
+                        variants = [out[q][0] for q in need[1:]]
+                        S = np.load(paths[k])
+                        P = O.NonnegPCAVectorized(S, S=S)
+                        name = it.get("name", k)
+                        r = check_against(it["gl"], ra, states, variants, P, O.RIPTRMOracle(opt).inner_step,
+                                          gpu_x=it.get("gpu_x"), gpu_tcg=it.get("gpu_tcg"))
+                        results[name] = r
+                        progress(f"[parity] instance {name}: {r} ({time.time() - t0:.0f} s)")
+                        for q in need:
+                            out.pop(q)
+                        last = time.time()
+                    if time.time() - last >= every_s:
+                        progress(f"[parity] {len(done_items)}/{len(items)} instances checked, {len(pending)} oracle runs "
+                                 f"pending ({time.time() - t0:.0f} s)")
+                        last = time.time()
+        finally:
+            for v, val in keep.items():
+                if val is None:
+                    os.environ.pop(v, None)
+                else:
+                    os.environ[v] = val
+    return results
 
 
 def check_budget(results, B, late_ties_free=False):

@@ -46,3 +46,31 @@ def test_gpus_mismatch_with_world_size_is_refused(monkeypatch, capsys):
                        capture_output=True, text=True, timeout=300)
     assert r.returncode != 0
     assert "WORLD_SIZE=1" in r.stderr
+
+
+def _leg(v, cores, name):
+    return {"value": v, "unit": "outer iterations/s", "cores": cores, "kind": "port", "sample": name}
+
+
+def test_cpu_baseline_selection_names_the_other_leg():
+    """the better CPU variant is the baseline, the other is kept under
+    other_variant -- also when the BLAS-threaded leg wins (the pool's number was lost)."""
+    threaded, pool = _leg(5.9, 16, "threaded"), _leg(4.1, 16, "pool")
+    out = bench.pick_cpu_baseline(threaded, pool)
+    assert out["sample"] == "threaded" and out["other_variant"]["sample"] == "pool"
+    assert out["other_variant"]["value"] == 4.1
+    out = bench.pick_cpu_baseline(_leg(3.0, 16, "threaded"), _leg(7.5, 16, "pool"))
+    assert out["sample"] == "pool" and out["other_variant"]["sample"] == "threaded"
+    out = bench.pick_cpu_baseline(None, pool)
+    assert out["sample"] == "pool" and "other_variant" not in out
+    out = bench.pick_cpu_baseline(threaded, None)
+    assert out["sample"] == "threaded" and "other_variant" not in out
+    assert bench.pick_cpu_baseline(None, None) is None
+    # the inputs are not modified
+    assert "other_variant" not in threaded and "other_variant" not in pool
+
+
+def test_host_cpu_info():
+    info = bench.host_cpu_info()
+    assert info["os_cpu_count"] == os.cpu_count()
+    assert info["cpu_model"]

@@ -61,3 +61,36 @@ def test_shard_ids_partition():
             assert max(sizes) - min(sizes) <= 1
     with pytest.raises(ValueError):
         shard_ids(4, 2, 2)
+
+
+def _census_worker(rank, world, port, q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    import bench
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        q.put((rank, bench.rank_census(dist, world, rank, torch.device("cpu"))))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_bench_rank_census_world2():
+    """bench.rank_census: every rank's view of the world, gathered with one all_gather (what the
+    driver's multi-GPU line reports under config.ranks)."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_census_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    for rank, census in res:
+        assert [c["rank"] for c in census] == [0, 1]
+        assert all(c["world_size_seen"] == 2 and not c["rccl"] for c in census)

@@ -108,3 +108,51 @@ def test_bench_launches_its_own_ranks():
     assert out["config"]["world_size"] == 2
     assert out["config"]["global_batch"] == 8
     assert out["value"] > 0
+
+
+def test_bench_configs3_per_rank_shape_two_ranks():
+    """BASELINE configs[3] (n = 4000, 128 instances per rank; src/NonnegPCA/config_simulation.yaml:35-42
+    is the reference's multi-run axis) at its real per-rank shape through bench.py's own launcher:
+    two ranks on the one GPU (2 x 8.5 GB of S), gloo standing in for RCCL on a 1-GPU box.  The line
+    must report both ranks and the backend, and the gathered x / y of global instances spread over
+    both shards must equal a single-process solve of the same instances bitwise."""
+    import json
+    import subprocess
+    import sys
+    import tempfile
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    W, K, n, B, seed0 = 1, 2, 4000, 128, 20251212
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    with tempfile.TemporaryDirectory() as td:
+        dump = os.path.join(td, "gathered.npz")
+        r = subprocess.run([sys.executable, "-u", os.path.join(root, "bench.py"), "--gpus", "2", "--same-device",
+                            "--backend", "gloo", "--dim", str(n), "--batch", str(B), "--warmup", str(W), "--steps", str(K),
+                            "--cpu-budget", "0", "--dump", dump], env=env, capture_output=True, text=True, timeout=500)
+        assert r.returncode == 0, r.stderr[-3000:]
+        lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+        assert len(lines) == 1, r.stdout
+        out = json.loads(lines[0])
+        g = np.load(dump)
+        gx, gy, gs = g["x"], g["y"], g["stats"]
+    assert out["n_gpus"] == 2 and out["config"]["world_size"] == 2
+    assert out["config"]["global_batch"] == 2 * B
+    assert out["config"]["backend"] == "gloo"
+    assert [c["rank"] for c in out["config"]["ranks"]] == [0, 1]
+    assert all(c["world_size_seen"] == 2 for c in out["config"]["ranks"])
+    assert gx.shape == (2 * B, n)
+    import engine
+    from problems import manviofun
+    C = engine.C
+    assert (gs[:, C["RIPTRM_STAT_OUTER_ITERS"]] == W + K).all()
+    ids = [0, 1, 2 * B - 1, 137]          # rank 0: 0, 137 is odd -> rank 1 too; both shards covered
+    eng = engine.NonnegPCABatch(n, len(ids), log_capacity=64, layout="sym", drain_logs=False)
+    xg, yg = eng.generate_synthetic(seed0, ids=ids)
+    opt = {"maxiter": W + 2 * K, "tolresid": 0.0, "maxtime": float("inf"), "manviofun": manviofun,
+           "TRS_solver": "tCG", "second_order_stationarity": False}
+    eng.begin(xg, yg, opt, restart_every=20)
+    eng.run_until(W + K)
+    res = eng.result()
+    rx, ry = res.x.cpu().numpy(), res.y.cpu().numpy()
+    for k, i in enumerate(ids):
+        np.testing.assert_array_equal(gx[i], rx[k], err_msg=f"global instance {i}")
+        np.testing.assert_array_equal(gy[i], ry[k], err_msg=f"global instance {i}")

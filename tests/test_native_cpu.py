@@ -36,6 +36,40 @@ def test_abi_version_and_no_device(built_lib):
     assert h.value is None
 
 
+_BACKEND_PROBE = """
+import ctypes, sys
+sys.path.insert(0, {pkg!r})
+import riptrm_native as N
+lib = N.load()
+buf = ctypes.create_string_buffer(512)
+rc = lib.riptrm_trs_backend_status(buf, 512)
+print(rc, buf.value.decode())
+"""
+
+
+@pytest.mark.parametrize("bogus", [False, True])
+def test_trs_backend_load_failure_is_reported_not_fatal(built_lib, bogus):
+    """riptrm_trs_big.hip loads rocBLAS / rocSOLVER with dlopen at first use.  A library that cannot
+    be loaded must come back as RIPTRM_E_HIP with dlopen's message (dlerror() was called
+    twice, the second NULL crashed the process).  Run in a child so the probe's cached state and the
+    environment override stay there."""
+    from conftest import PKG
+    env = dict(os.environ)
+    if bogus:
+        env["RIPTRM_ROCSOLVER_LIB"] = "libriptrm_no_such_solver.so.0"
+    r = subprocess.run([sys.executable, "-c", _BACKEND_PROBE.format(pkg=PKG)], env=env, capture_output=True,
+                       text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    rc, msg = r.stdout.strip().split(" ", 1)
+    if bogus:
+        assert int(rc) == N.CONST["RIPTRM_E_HIP"]
+        assert "libriptrm_no_such_solver.so.0" in msg and "cannot load" in msg
+    elif int(rc) != 0:
+        pytest.skip(f"rocSOLVER not loadable on this host: {msg}")
+    else:
+        assert "dsyevd" in msg
+
+
 def test_layout_functions(built_lib):
     C = N.CONST
     for n in (2, 17, 50, 1000, 4000, 4001):

@@ -316,3 +316,28 @@ def test_flip_classifier_rejects_late_decision_with_margin():
         fake = copy.deepcopy(ra.log)
         fake[key][row] = value
         assert classify_flip(rec.step, P, rec.states, fake, ra.log, (row, key)) is None, key
+
+
+def test_parallel_checker_matches_sequential():
+    """parity.check_instances_parallel (the n = 4000 GPU tests' pool of single-threaded oracle
+    processes) reaches the same verdict as parity.check_instance: here the 'GPU' log is the
+    reference-structured oracle's, one instance that agrees and one whose branches flip (seed 125,
+    test_outer_comparator_on_branch_flips)."""
+    from parity import check_instance, check_instances_parallel
+    opt = dict(OPT, maxiter=10)
+    items = []
+    for n, seed in ((37, 100), (37, 125)):
+        Z, x0, y0 = G.generate_instance(n, seed)
+        a = O.solve(Z, x0, y0, opt, structured=True)
+        items.append(dict(gl=a.log, S=Z + Z.T, x0=x0, y0=y0, gpu_x=a.x, name=seed, Z=Z))
+    msgs = []
+    par = check_instances_parallel(items, opt, workers=2, progress=msgs.append)
+    assert len(msgs) >= 2
+    for it in items:
+        seq = check_instance(it["gl"], it["Z"], it["x0"], it["y0"], opt, gpu_x=it["gpu_x"])
+        assert (seq is None) == (par[it["name"]] is None)
+        if seq is not None:
+            assert seq[0] == par[it["name"]][0]
+            if seq[0] == "flip":
+                assert seq[1][:2] == par[it["name"]][1][:2]
+    assert par[125] is not None and par[125][0] == "flip"
