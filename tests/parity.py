@@ -330,6 +330,26 @@ class StateRecorder:
 
 # ---- one GPU instance against the oracle ----------------------------------------------------
 
+def variant_supports_flip(variants, gl, rl, flip):
+    """A branch flip of the GPU log at row r is rounding-driven also if the oracle's own order
+    variants (the same arithmetic in another summation order: order_variants) leave the reference
+    run's branches there: one of them takes the GPU's decision at row r, or one of them already
+    flips at a row <= r (past that row the reference trajectory is not stable under reordering, so
+    its branch decisions are no target; the outer iterates must still agree, compare_outer).
+    Late in a K = 20 window (mu ~ 1e-8) the acceptance test ared > 0.1 pred (RIPTRM.py:677) compares
+    merit differences of ~1e-15 |phi|, and the four dsymv permutations split there themselves."""
+    row, key = flip
+    for v in variants:
+        vf = first_branch_flip(v.log, rl)
+        if vf is None:
+            continue
+        if vf[0] < row:
+            return True
+        if vf[0] == row and row < len(v.log[key]) and v.log[key][row] == gl[key][row]:
+            return True
+    return False
+
+
 def check_against(gl, ra, states, variants, P, step, gpu_x=None, gpu_tcg=None):
     """check_instance's bar, given the oracle's reference run `ra` (its inner steps' starting
     states recorded: StateRecorder), the order-perturbed runs `variants` (order_variants), the
@@ -345,8 +365,10 @@ def check_against(gl, ra, states, variants, P, step, gpu_x=None, gpu_tcg=None):
     except BranchFlip:
         flip = first_branch_flip(gl, ra.log)
         eps = classify_flip(step, P, states, gl, ra.log, flip)
-        assert eps is not None, ("branch flip not reachable within the accumulated drift", flip,
-                                 gl[flip[1]][flip[0]], ra.log[flip[1]][flip[0]])
+        if eps is None and variant_supports_flip(variants, gl, ra.log, flip):
+            eps = 0.0   # the oracle's own summation-order variants leave its branches there (no perturbation)
+        assert eps is not None, ("branch flip neither reachable within the accumulated drift nor left by the "
+                                 "oracle's order variants", flip, gl[flip[1]][flip[0]], ra.log[flip[1]][flip[0]])
         compare_outer(gl, ra.log)
         # the rows before the flip still meet the envelope bar (and their tCG exit indices)
         row = flip[0]

@@ -341,3 +341,28 @@ def test_parallel_checker_matches_sequential():
             if seq[0] == "flip":
                 assert seq[1][:2] == par[it["name"]][1][:2]
     assert par[125] is not None and par[125][0] == "flip"
+
+
+def test_variant_support_for_flips():
+    """parity.variant_supports_flip: a GPU flip at row r counts as rounding-driven when an order
+    variant of the oracle takes the same decision at r, or already leaves the reference's branches
+    at a row <= r; a variant that agrees with the reference everywhere supports nothing."""
+    from parity import variant_supports_flip
+    keys = ("iteration", "num_inner", "inner_status", "dxtype", "radius_update", "dual_clipping")
+
+    def log(status):
+        return {k: (list(status) if k == "inner_status" else [0] * len(status)) for k in keys}
+
+    ref = log(["successful"] * 6)
+    gpu = log(["successful"] * 4 + ["unsuccessful", "successful"])
+    V = type("V", (), {})
+    same = V(); same.log = log(["successful"] * 6)
+    assert not variant_supports_flip([same], gpu, ref, (4, "inner_status"))
+    at = V(); at.log = log(["successful"] * 4 + ["unsuccessful", "successful"])
+    assert variant_supports_flip([same, at], gpu, ref, (4, "inner_status"))
+    other = V(); other.log = log(["successful"] * 4 + ["converged", "successful"])
+    assert not variant_supports_flip([other], gpu, ref, (4, "inner_status"))
+    earlier = V(); earlier.log = log(["successful"] * 2 + ["unsuccessful"] + ["successful"] * 3)
+    assert variant_supports_flip([earlier], gpu, ref, (4, "inner_status"))
+    later = V(); later.log = log(["successful"] * 5 + ["unsuccessful"])
+    assert not variant_supports_flip([later], gpu, ref, (4, "inner_status"))
