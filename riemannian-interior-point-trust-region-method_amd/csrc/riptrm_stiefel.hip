@@ -453,124 +453,6 @@ __global__ void __launch_bounds__(T) k_st_proj3(int n, int p, int64_t stride, co
   ST_STAMP(4);
 }
 
-// ---- projection, round 4: operands streamed from global memory, only M in LDS ------------------
-// k_st_proj3 holds the whole point in LDS (160 KB), so one point runs per CU at a time and its
-// serial chain (load burst -> Gram -> M exchange -> update) cannot hide behind another point's
-// work: 8 points per CU took exactly 8x one point.  Here a 4-wave workgroup keeps only
-// M = X^T U (64 x 64, 32 KB) in LDS and reads every MFMA operand straight from global memory in
-// its fragment layout, so several points share a CU and one point's loads run under another's
-// MFMAs:
-//   Gram    wave w owns column block J = w of M: M_IJ, I = 0..3, over every 4-row group of the n
-//           rows (A operand X[4g + kk][16 I + c], B operand U[4g + kk][16 w + c]; X is read by the
-//           four waves, from L1 / L2 after the first);
-//   M       the blocks land in LDS (zero outside [0, p)^2), one barrier;
-//   update  wave w owns output column block J = w: for each 16-row block R, out = U - X sym(M)
-//           with A operand X[16 R + c][4 s + kk] (the rows again, from L2), B operand
-//           sym(M)[4 s + kk][16 w + c] read once into registers, C operand U at the output block.
-// HBM traffic stays 24 n p bytes per point when X's re-reads hit the caches.  out may alias U (a
-// wave reads U's output block before writing it; no other wave reads it then), not X.
-constexpr int W4 = 4;                 // waves per workgroup
-constexpr int T4 = 64 * W4;
-#ifndef P4_GB
-#define P4_GB 3                       // 4-row groups per Gram load batch
-#endif
-#ifndef P4_UB
-#define P4_UB 1                       // row blocks per update batch (independent accumulator chains)
-#endif
-constexpr int P4_MS = 64 + 1;         // LDS row stride of M
-#ifndef P4_OCC
-#define P4_OCC 4                      // waves per SIMD the registers are sized for (4 workgroups per CU)
-#endif
-
-template <int P4T, bool RMASK>
-__global__ void __launch_bounds__(T4, P4_OCC) k_st_proj4(int n, int p, int64_t stride, const double* __restrict__ X,
-                                                 const double* U, double* out) {
-  __shared__ double Ms_[64 * P4_MS];
-  lds_f64* Ms = (lds_f64*)Ms_;
-  const int t = threadIdx.x, l = t & 63, w = t >> 6, c = l & 15, kk = l >> 4;
-  const int64_t o = (int64_t)blockIdx.x * stride;
-  const double* __restrict__ Xp = X + o;
-  const double* Up = U + o;
-  double* Op = out + o;
-  // columns past p are clamped (finite data; they only feed M's rows / columns past p, stored as 0)
-  const int j = 16 * w + c;
-  const int jc = j < p ? j : p - 1;
-  int ac[4];
-#pragma unroll
-  for (int I = 0; I < 4; ++I) ac[I] = 16 * I + c < p ? 16 * I + c : p - 1;
-  dbl4 acc[4];
-#pragma unroll
-  for (int I = 0; I < 4; ++I) acc[I] = dbl4{0.0, 0.0, 0.0, 0.0};
-  const int G = (n + 3) / 4;
-  for (int g0 = 0; g0 < G; g0 += P4_GB) {
-    double xa[P4_GB][4], ub[P4_GB];
-#pragma unroll
-    for (int u = 0; u < P4_GB; ++u) {
-      const int r = 4 * (g0 + u) + kk;
-      const int rr = !RMASK || r < n ? r : n - 1;
-      const double* xr = Xp + (int64_t)rr * p;
-#pragma unroll
-      for (int I = 0; I < 4; ++I) xa[u][I] = xr[ac[I]];
-      ub[u] = RMASK ? Up[(int64_t)rr * p + jc] * mask01(r < n) : Up[(int64_t)rr * p + jc];
-    }
-    __builtin_amdgcn_sched_barrier(0);   // the batch's loads issue before its MFMAs
-#pragma unroll
-    for (int u = 0; u < P4_GB; ++u)
-#pragma unroll
-      for (int I = 0; I < 4; ++I) acc[I] = __builtin_amdgcn_mfma_f64_16x16x4f64(xa[u][I], ub[u], acc[I], 0, 0, 0);
-  }
-  // M_IJ -> LDS, zero outside [0, p)^2 (the update's k steps past p rely on it)
-#pragma unroll
-  for (int I = 0; I < 4; ++I)
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int i = 16 * I + kk + 4 * q;
-      Ms[i * P4_MS + j] = (i < p && j < p) ? acc[I][q] : 0.0;
-    }
-  __syncthreads();
-  double bk[P4T];   // sym(M)[4 s + kk][j] = (M_kj + M_jk) / 2: exactly symmetric
-#pragma unroll
-  for (int s = 0; s < P4T; ++s) {
-    const int k = 4 * s + kk;
-    bk[s] = 0.5 * (Ms[k * P4_MS + j] + Ms[j * P4_MS + k]);
-  }
-  const int R16 = (n + 15) / 16;
-  for (int R0 = 0; R0 < R16; R0 += P4_UB) {
-    double a[P4_UB][P4T], cv[P4_UB][4];
-#pragma unroll
-    for (int b = 0; b < P4_UB; ++b) {
-      const int R = R0 + b < R16 ? R0 + b : R16 - 1;
-      const int ar = 16 * R + c;
-      const double* xr = Xp + (int64_t)(ar < n ? ar : n - 1) * p;
-#pragma unroll
-      for (int s = 0; s < P4T; ++s) {   // k past p: M is zero there, X's value is any finite one
-        const int k = 4 * s + kk;
-        a[b][s] = xr[k < p ? k : p - 1];
-      }
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int i = 16 * R + kk + 4 * q;
-        cv[b][q] = Up[(int64_t)(i < n ? i : n - 1) * p + jc];
-      }
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    dbl4 acu[P4_UB];
-#pragma unroll
-    for (int b = 0; b < P4_UB; ++b) acu[b] = dbl4{0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-    for (int s = 0; s < P4T; ++s)
-#pragma unroll
-      for (int b = 0; b < P4_UB; ++b) acu[b] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[b][s], bk[s], acu[b], 0, 0, 0);
-#pragma unroll
-    for (int b = 0; b < P4_UB; ++b)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int i = 16 * (R0 + b) + kk + 4 * q;
-        if (R0 + b < R16 && i < n && j < p) Op[(int64_t)i * p + j] = cv[b][q] - acu[b][q];
-      }
-  }
-}
-
 template <int P16>
 __global__ void __launch_bounds__(T) k_st_e2rh(int n, int p, int64_t stride, const double* X, const double* G,
                                                const double* H, const double* U, double* out) {
@@ -1692,14 +1574,6 @@ static bool proj3_ok(int n, int p, int64_t stride) {
          p3_lds_doubles(n, p, 4) <= P3_LDS_DOUBLES;
 }
 
-// k_st_proj4 (operands from global memory, M in LDS) for 49 <= p <= 64; RIPTRM_STIEFEL_PROJ=r3 forces
-// k_st_proj3 (A/B)
-static bool proj4_ok(int n, int p) {
-  const char* e = getenv("RIPTRM_STIEFEL_PROJ");
-  if (e && e[0] == 'r' && (e[1] == '2' || e[1] == '3')) return false;
-  return (p + 15) / 16 == 4 && n >= 1;
-}
-
 // kernels are specialised on ceil(p / 16) (the 16-column blocks), so no operand load sits behind
 // a runtime branch
 #define ST_LAUNCH(K, p, ...)                                                                              \
@@ -1730,20 +1604,6 @@ int riptrm_stiefel_proj(riptrm_ctx* ctx, int32_t n, int32_t p, int32_t batch, in
   if (!X || !U || !out || out == X) return fail(ctx, RIPTRM_E_ARG, "stiefel_proj: bad pointer (out must not alias X)");
   int rc = st_check(ctx, n, p, batch, stride);
   if (rc) return rc;
-  if (proj4_ok(n, p)) {
-    const bool rm = n % (4 * P4_GB) != 0;
-    switch ((p + 3) / 4) {
-#define P4_CASE(K)                                                                                       \
-  case K:                                                                                                \
-    if (rm) hipLaunchKernelGGL((k_st_proj4<K, true>), dim3(batch), dim3(T4), 0, ctx->stream, n, p, stride, X, U, out); \
-    else hipLaunchKernelGGL((k_st_proj4<K, false>), dim3(batch), dim3(T4), 0, ctx->stream, n, p, stride, X, U, out); \
-    break;
-      P4_CASE(13) P4_CASE(14) P4_CASE(15) P4_CASE(16)
-#undef P4_CASE
-    }
-    HIPCHK(ctx, hipGetLastError());
-    return RIPTRM_OK;
-  }
   if (proj3_ok(n, p, stride)) {
     hipLaunchKernelGGL(k_st_proj3<4>, dim3(batch), dim3(T), (size_t)p3_lds_doubles(n, p, 4) * sizeof(double),
                        ctx->stream, n, p, stride, X, U, out);

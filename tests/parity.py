@@ -234,7 +234,37 @@ def excursion_budget(instances: int) -> int:
     return max(1, instances // 10)
 
 
-def compare_tcg_iters(g_iters, ref, env, mult=3.0, rel=0.005, slack=2):
+def tcg_exit_reachable(P, state, target, drift, trials=6, seed=0, slack=2, rel=0.005):
+    """A tCG exit index that differs from the oracle's by more than its order variants' spread is
+    still a rounding quantity if the oracle's own tCG (RIPTRM.py:41-216), started from the oracle's
+    state at that inner step perturbed at sizes from 1e-14 up to the drift the trajectories had
+    accumulated (prefix_deviation, capped at 1e-8), exits at indices whose range covers the GPU's
+    (within max(slack, rel j)).  Long CG runs at mu ~ 1e-7 (hundreds of iterations, condition numbers
+    ~ 1/mu) cross the residual target on a plateau, where such perturbations move the exit a lot.
+    state = (x, y, mu, Delta, inner_iteration, inner_option) as StateRecorder keeps it.  Returns the
+    (min, max) exit indices seen when the target is covered, else None."""
+    from oracle import riptrm_oracle as O
+    x, y, mu, Delta = state[:4]
+    n = x.shape[0]
+    rs = np.random.RandomState(seed)
+    sizes = np.logspace(-14, np.log10(max(drift, 1e-14)), max(1, int(np.ceil(np.log10(max(drift, 1e-14)) + 14)) + 1))
+    lo, hi = None, None
+    tol = max(slack, rel * target)
+    for t in range(trials * len(sizes)):
+        eps = sizes[t // trials] * (0.5 + rs.rand())
+        xp = x * (1.0 + eps * rs.randn(n))
+        xp = xp / np.linalg.norm(xp)
+        yp = y * (1.0 + eps * rs.randn(n))
+        _, _, Hw, c = P.begin_inner(xp, yp, mu)
+        _, _, j, _ = O.truncated_conjugate_gradient(P.manifold, Hw, xp, c, Delta, 1, 0.1, 1, n - 1)
+        lo = j if lo is None else min(lo, j)
+        hi = j if hi is None else max(hi, j)
+        if lo - tol <= target <= hi + tol:
+            return (lo, hi)
+    return None
+
+
+def compare_tcg_iters(g_iters, ref, env, mult=3.0, rel=0.005, slack=2, reachable=None):
     """tCG exit iterations per inner step (GPU log rows 1.. = oracle trace) and their total: each
     within max(slack, mult x the variants' largest |dj| over the run, rel x j), the total within
     max(mult x the variants' largest per-step |dj| x steps moved, rel x total).  CG's exit index
@@ -247,6 +277,16 @@ def compare_tcg_iters(g_iters, ref, env, mult=3.0, rel=0.005, slack=2):
     djmax = float(np.nanmax(dj)) if np.any(~np.isnan(dj)) else 0.0
     lim = np.maximum(np.maximum(slack, mult * djmax), rel * r)
     bad = np.abs(g - r) > lim
+    if bad.any() and reachable is not None:
+        # reachable(i, j_gpu): the exit index of inner step i is a rounding quantity there
+        # (tcg_exit_reachable); at most 8 such steps per instance are examined
+        idx = np.nonzero(bad)[0]
+        assert len(idx) <= 8, (idx[:10], g[bad][:10], r[bad][:10], djmax)
+        for i in idx:
+            assert reachable(int(i), int(g[i])) is not None, (int(i), g[i], r[i], djmax)
+        keep = ~bad
+        g, r = g[keep], r[keep]
+        bad = np.zeros(len(g), bool)
     assert not bad.any(), (np.nonzero(bad)[0][:5], g[bad][:5], r[bad][:5], djmax)
     moved = int(np.sum(g != r))
     assert abs(g.sum() - r.sum()) <= max(slack * moved, mult * djmax * moved, rel * r.sum()), (g.sum(), r.sum())
@@ -356,12 +396,18 @@ def check_against(gl, ra, states, variants, P, step, gpu_x=None, gpu_tcg=None):
     oracle problem P and its unwrapped inner step (classify_flip's probe)."""
     exc = []
     env = None
+
+    def reachable(i, j):   # inner step i + 1 wrote log row i + 1
+        if i >= len(states):
+            return None
+        return tcg_exit_reachable(P, states[i], j, max(prefix_deviation(gl, ra.log, i + 2), 1e-14))
+
     try:
         compare_logs(gl, ra.log)   # branches + the calibrated bound first (flip detection)
         env = envelope(ra, variants)
         compare_logs(gl, ra.log, envelope=env, excursions=exc)
         if gpu_tcg is not None:
-            compare_tcg_iters(gpu_tcg, ra, env)
+            compare_tcg_iters(gpu_tcg, ra, env, reachable=reachable)
     except BranchFlip:
         flip = first_branch_flip(gl, ra.log)
         eps = classify_flip(step, P, states, gl, ra.log, flip)
@@ -377,7 +423,7 @@ def check_against(gl, ra, states, variants, P, step, gpu_x=None, gpu_tcg=None):
             compare_logs(_prefix(gl, row), _prefix(ra.log, row), envelope=env, excursions=exc)
             if gpu_tcg is not None:
                 pre = type("Pre", (), {"trace": ra.trace[:row - 1]})()
-                compare_tcg_iters(list(gpu_tcg)[:row - 1], pre, {"_tcg": env["_tcg"][:row - 1]})
+                compare_tcg_iters(list(gpu_tcg)[:row - 1], pre, {"_tcg": env["_tcg"][:row - 1]}, reachable=reachable)
         return ("flip", flip + (eps, len(gl["iteration"]), exc))
     if gpu_x is not None:
         np.testing.assert_allclose(gpu_x, ra.x, atol=1e-6)
