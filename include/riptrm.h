@@ -322,9 +322,11 @@ int riptrm_profile_read(riptrm_ctx* ctx, double* gemv_ms, int64_t* gemv_launches
  * m inequality constraints on entries of A = (J-R)Q (:102-152), one row of RIPTRM_SI_CONS_FIELDS
  * doubles each: kind (0: -A_rc + p0, 1: A_rc - p0, 2: -(A_rc - p0)^2 + p1), r, c, p0, p1 — the
  * reference's constset rows expanded in order (type 0/1 -> kinds 0 then 1; type 2 -> kind 2 with
- * p1 = k^2).  One 64-lane workgroup runs one instance's whole RIPTRM solve in one launch. */
-#define RIPTRM_SI_DMAX 8
-#define RIPTRM_SI_MMAX 64
+ * p1 = k^2).  One workgroup runs one instance's whole RIPTRM solve in one launch: a 64-lane wave up
+ * to d = 8, 64 ceil(d^2 / 64) threads (one per element of a d x d block) above.  m <= 64 for d <= 8,
+ * m <= 64 ceil(d^2 / 64) above. */
+#define RIPTRM_SI_DMAX 16
+#define RIPTRM_SI_MMAX 256
 #define RIPTRM_SI_CONS_FIELDS 5
 
 typedef struct riptrm_si_problem {

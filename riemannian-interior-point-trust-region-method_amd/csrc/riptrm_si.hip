@@ -2,11 +2,18 @@
 //
 // Problem (src/StableIdentification/coordinator.py:13-152): Product(SkewSymmetric(d), SPD(d),
 // SPD(d)) with f(J,R,Q) = tr(E E^T)/N, E = XP - (I + h A) X, A = (J-R)Q, and m box constraints on
-// entries of A.  Everything is d x d (d <= 8, the fixture has d = 5, m = 16, N = 95), so one
-// 64-lane workgroup runs one instance's WHOLE solve in one launch: lane l < d*d owns element
-// (l / d, l % d) of every d x d block; products go through LDS (one staging write + d reads per
-// operand), inner products / norms are wave butterflies, Cholesky / Jacobi eigenvalues for the
-// evaluation (dist, manifold violation) run serially on lane 0.  No S-pass, no host round trip.
+// entries of A.  Everything is d x d (the fixture has d = 5, m = 16, N = 95), so one workgroup runs
+// one instance's WHOLE solve in one launch: thread l < d*d owns element (l / d, l % d) of every
+// d x d block; products go through LDS (one staging write + d reads per operand).  No S-pass, no
+// host round trip.
+//   d <= 8:  one 64-lane wave; inner products / norms are wave butterflies, R^-1 / Q^-1 and the
+//            evaluation's Cholesky / Jacobi eigenvalues (dist, manifold violation) run serially in
+//            the registers of 2 / 4 lanes.
+//   8 < d <= RIPTRM_SI_DMAX:  NT = 64 ceil(d^2 / 64) threads (one element each); inner products are
+//            workgroup reductions (riptrm_trs::Blk), lane reads go through LDS, and the dense
+//            solvers run on the whole workgroup: Gauss-Jordan inverse with partial pivoting and a
+//            right-looking Cholesky, one pivot per step, and the SPD distance's eigenvalues by the
+//            parallel Jacobi of riptrm_trs.h.
 //
 // Math = oracle/si_oracle.py::SIVectorized (the Lagrangian aggregated through dL/dA), i.e.
 //   HessL[v]  = e2rh(x, chain(G_L), chain_hess(G_L, dG_L, v), v)        RIPTRM.py:491-523
@@ -317,9 +324,19 @@ __device__ __forceinline__ double spd_dist_reg(const double (&A)[D * D], const d
   return ok ? sqrt(s2) : NAN;
 }
 
-template <int D>
+// threads of the workgroup for block size D: one wave up to D = 8, one thread per element above
+__host__ __device__ constexpr int si_threads(int D) { return D <= 8 ? W : (D * D + 63) / 64 * 64; }
+
+// LDS doubles a big-D workgroup needs besides its static arrays: the broadcast buffer, the
+// reduction buffers, the dense solvers' row / column buffers and the Jacobi work area
+__host__ __device__ constexpr int si_big_lds_doubles(int D) {
+  return si_threads(D) + 2 * (si_threads(D) / 64) + 4 * D + riptrm_trs::work_doubles(D);
+}
+
+template <int D, int NT = si_threads(D)>
 struct Eng {
   static constexpr int d = D, dd = D * D;
+  static constexpr bool BIG = NT > W;
   const SIParams& P;
   const int b, l, m, N;
   const int li, lj;
@@ -328,7 +345,8 @@ struct Eng {
   double* ser;     // LDS scratch for the per-lane serial solvers: 8 x 64 doubles
   int* cr_s;       // LDS constraint rows / cols / kinds
   int* cc_s;
-  double* tl;      // LDS work area of the Exact_RepMat subproblem (riptrm_trs.h), null for tCG
+  double* tl;      // LDS work area of the Exact_RepMat subproblem (riptrm_trs.h), null for tCG;
+                   // big D: bc (NT), red (2 NT / 64), colv / rowa / rowo / rowx (D each), the Jacobi work
   // constraint of this lane (l < m)
   int ck, cr, cc;
   double cp0, cp1;
@@ -339,10 +357,24 @@ struct Eng {
   double pt[RIPTRM_SI_PROF_NFIELDS];   // section tick totals (riptrm_si_profile_*)
   __device__ __forceinline__ double tick() const { return P.prof ? (double)wall_clock64() : 0.0; }
 
+  double* bc;      // big D: LDS broadcast buffer (NT)
+  riptrm_trs::Blk<NT> blk;   // big D: workgroup reductions
+  double* colv;    // big D: the dense solvers' pivot column / rows (D each)
+  double* rowa;
+  double* rowo;
+  double* rowx;
+  double* jw;      // big D: riptrm_trs Work area of the SPD distance's eigenvalues
+
   __device__ __forceinline__ Eng(const SIParams& P_, int b_, double* sh_, double* ser_, int* crs, int* ccs, double* tl_)
       : P(P_), b(b_), l((int)threadIdx.x), m(P_.m), N(P_.N),
         li((int)threadIdx.x / D), lj((int)threadIdx.x % D), act((int)threadIdx.x < D * D),
-        cact((int)threadIdx.x < P_.m), sh(sh_), ser(ser_), cr_s(crs), cc_s(ccs), tl(tl_) {
+        cact((int)threadIdx.x < P_.m), sh(sh_), ser(ser_), cr_s(crs), cc_s(ccs), tl(tl_),
+        bc(tl_), blk(BIG ? tl_ + NT : nullptr) {
+    colv = tl_ + NT + 2 * (NT / 64);
+    rowa = colv + D;
+    rowo = rowa + D;
+    rowx = rowo + D;
+    jw = rowx + D;
     Xd = P.X + (int64_t)b * P.data_stride;
     XPd = P.XP + (int64_t)b * P.data_stride;
     E = P.escr + (int64_t)b * d * N;
@@ -367,6 +399,32 @@ struct Eng {
     __syncthreads();
   }
 
+  // ---- reductions / lane reads: wave ops for one wave, workgroup ops above -------------------
+  __device__ __forceinline__ double rsum(double v) {
+    if constexpr (BIG) return blk.sum(v);
+    else return wsum(v);
+  }
+  __device__ __forceinline__ double rmin(double v) {
+    if constexpr (BIG) return blk.min(v);
+    else return wmin(v);
+  }
+  __device__ __forceinline__ double rmax(double v) {
+    if constexpr (BIG) return blk.max(v);
+    else return wmax(v);
+  }
+  // value of v on thread src: call on every thread
+  __device__ __forceinline__ double lread(double v, int src) {
+    if constexpr (BIG) {
+      bc[l] = v;
+      __syncthreads();
+      const double r = bc[src < NT ? src : 0];
+      __syncthreads();
+      return r;
+    } else {
+      return lane_read(v, src);
+    }
+  }
+
   // ---- d x d block primitives (one element per lane) ---------------------------------------
   __device__ __forceinline__ double tr(double a) {
     sh[l] = a;
@@ -378,14 +436,14 @@ struct Eng {
   // op(a) op(b), ta / tb transpose the operand
   __device__ __forceinline__ double mm(double a, double b, bool ta = false, bool tb = false) {
     sh[l] = a;
-    sh[W + l] = b;
+    sh[NT + l] = b;
     __syncthreads();
     double acc = 0.0;
     if (act) {
 #pragma unroll
       for (int k = 0; k < D; ++k) {
         const double av = ta ? sh[k * d + li] : sh[li * d + k];
-        const double bv = tb ? sh[W + lj * d + k] : sh[W + k * d + lj];
+        const double bv = tb ? sh[NT + lj * d + k] : sh[NT + k * d + lj];
         acc = acc + av * bv;
       }
     }
@@ -394,7 +452,7 @@ struct Eng {
   }
   __device__ __forceinline__ double sym(double a) { return 0.5 * (a + tr(a)); }
   __device__ __forceinline__ double skew(double a) { return 0.5 * (a - tr(a)); }
-  __device__ __forceinline__ double elem(double a, int i, int j) { return lane_read(a, i * d + j); }
+  __device__ __forceinline__ double elem(double a, int i, int j) { return lread(a, i * d + j); }
 
   // stage blocks into LDS slots (slot k = ser + k*W), every lane
   __device__ __forceinline__ void stage(int slot, double a) {
@@ -404,8 +462,88 @@ struct Eng {
 #pragma unroll
     for (int i = 0; i < D * D; ++i) r[i] = ser[slot * W + i];
   }
+  // ---- big D: dense solvers on the whole workgroup, one element per thread --------------------
+  // A^-1 by Gauss-Jordan with partial pivoting: inv_reg's arithmetic (first row of largest |a_rk|,
+  // row swap, pivot row divided by the pivot, the other rows eliminated), one pivot per step
+  __device__ __forceinline__ double par_inv(double a) {
+    double o = (act && li == lj) ? 1.0 : 0.0;
+    for (int k = 0; k < D; ++k) {
+      if (act && lj == k) colv[li] = a;   // column k
+      __syncthreads();
+      int p = k;
+      double best = fabs(colv[k]);
+      for (int r = k + 1; r < D; ++r) {
+        const double v = fabs(colv[r]);
+        if (v > best) { best = v; p = r; }
+      }
+      const double piv = colv[p];
+      const double f = (li == p) ? colv[k] : (act ? colv[li] : 0.0);   // a_rk after the swap
+      if (act && li == p) { rowa[lj] = a; rowo[lj] = o; }             // the new row k
+      if (act && li == k && p != k) { rowx[lj] = a; sh[lj] = o; }     // the old row k -> row p
+      __syncthreads();
+      if (act) {
+        const double sa = rowa[lj] / piv, so = rowo[lj] / piv;
+        if (li == k) {
+          a = sa;
+          o = so;
+        } else {
+          const double ar = li == p ? rowx[lj] : a, orr = li == p ? sh[lj] : o;
+          a = ar - f * sa;
+          o = orr - f * so;
+        }
+      }
+      __syncthreads();
+    }
+    return o;
+  }
+  // lower Cholesky factor (this thread's element; 0 above the diagonal), right-looking in pivot
+  // order: the same operations and order as chol_inv_reg / spd_dist_reg.  ok = every pivot > 0.
+  __device__ __forceinline__ double par_chol(double a, bool& ok) {
+    double L = 0.0;
+    ok = true;
+    for (int k = 0; k < D; ++k) {
+      if (act && lj == k) colv[li] = a;
+      __syncthreads();
+      const double sk = colv[k];
+      ok = ok && (sk > 0.0);
+      const double ckk = sqrt(sk > 0.0 ? sk : 1.0);
+      if (act) {
+        if (lj == k && li >= k) L = li == k ? ckk : a / ckk;
+        else if (li > k && lj > k) a = a - (colv[li] / ckk) * (colv[lj] / ckk);
+      }
+      __syncthreads();
+    }
+    return L;
+  }
+  // pymanopt SPD dist ||logm(C^-1 B C^-T)||_F, C = cholesky(A) (spd_dist_reg on the workgroup;
+  // the eigenvalues by riptrm_trs.h's parallel Jacobi); NaN if A is not PD
+  __device__ __forceinline__ double par_dist(double A, double Bm) {
+    bool ok;
+    const double C = par_chol(A, ok);
+    const double Ci = par_inv(C);
+    const double T = mm(Bm, Ci, false, true);
+    const double M = sym(mm(Ci, T));
+    riptrm_trs::Work w = riptrm_trs::make_work(jw, D);
+    if (act) w.A[li * w.lda + lj] = M;
+    __syncthreads();
+    riptrm_trs::jacobi<NT>(blk, w, false);
+    __syncthreads();
+    double s2 = 0.0;
+    for (int i = 0; i < D; ++i) {
+      const double lg = log(w.ev[i]);
+      s2 += lg * lg;
+    }
+    __syncthreads();
+    return ok ? sqrt(s2) : NAN;
+  }
+
   // R^-1 and Q^-1 at once: lane 0 inverts slot 0, lane 1 slot 1 (Gauss-Jordan, partial pivoting)
   __device__ __forceinline__ void inv2(double r, double q, double& ri, double& qi) {
+    if constexpr (BIG) {
+      ri = par_inv(r);
+      qi = par_inv(q);
+      return;
+    }
     stage(0, r);
     stage(1, q);
     __syncthreads();
@@ -423,6 +561,13 @@ struct Eng {
   }
   // evaluation's dense solvers, four lanes in parallel: PD(R), PD(Q), dist(Rp,R), dist(Qp,Q)
   __device__ __forceinline__ void eval_solvers(double rp, double r, double qp, double q, bool& pdr, bool& pdq, double& dR, double& dQ) {
+    if constexpr (BIG) {   // PD by Cholesky (the serial path: all Jacobi eigenvalues > 0)
+      (void)par_chol(r, pdr);
+      (void)par_chol(q, pdq);
+      dR = par_dist(rp, r);
+      dQ = par_dist(qp, q);
+      return;
+    }
     stage(0, r);
     stage(1, q);
     stage(2, rp);
@@ -462,10 +607,10 @@ struct Eng {
   __device__ __forceinline__ double spd_inner(double Xi, double u, double v) {
     const double pu = mm(Xi, u);
     const double pv = mm(Xi, v);
-    return wsum(pu * tr(pv));
+    return rsum(pu * tr(pv));
   }
   __device__ __forceinline__ double inner(const Metric& g, PV u, PV v) {
-    const double a = wsum(u.j * v.j);
+    const double a = rsum(u.j * v.j);
     const double br = spd_inner(g.XiR, u.r, v.r);
     const double bq = spd_inner(g.XiQ, u.q, v.q);
     return ((0.0 + a) + br) + bq;
@@ -492,12 +637,12 @@ struct Eng {
   }
   // constraint value g_k(x) on constraint lanes from A (this lane's element)
   __device__ __forceinline__ double cons_val(double A) {
-    const double a = lane_read(A, cr * d + cc);
+    const double a = lread(A, cr * d + cc);
     if (!cact) return 0.0;
     return ck == 0 ? (-a + cp0) : (ck == 1 ? (a - cp0) : (-((a - cp0) * (a - cp0)) + cp1));
   }
   __device__ __forceinline__ double cons_w(double A) {
-    const double a = lane_read(A, cr * d + cc);
+    const double a = lread(A, cr * d + cc);
     if (!cact) return 0.0;
     return ck == 0 ? -1.0 : (ck == 1 ? 1.0 : -2.0 * (a - cp0));
   }
@@ -519,7 +664,7 @@ struct Eng {
     __syncthreads();
     double part = 0.0;
     const int tot = d * N;
-    for (int e = l; e < tot; e += W) {
+    for (int e = l; e < tot; e += NT) {
       const int i = e / N, t = e - i * N;
       double s = 0.0;
       for (int k = 0; k < d; ++k) s = s + sh[i * d + k] * Xd[k * N + t];
@@ -528,7 +673,7 @@ struct Eng {
       part = part + ev * ev;
     }
     __syncthreads();
-    f = wsum(part) / (double)N;
+    f = rsum(part) / (double)N;
     double g = 0.0;
     if (act)
       for (int t = 0; t < N; ++t) g = g + E[li * N + t] * Xd[lj * N + t];
@@ -568,7 +713,7 @@ struct Eng {
   }
   // Gxaj(v) on constraint lanes from dA(v)
   __device__ __forceinline__ double gxaj(const AtX& a, double dA) {
-    const double da = lane_read(dA, cr * d + cc);
+    const double da = lread(dA, cr * d + cc);
     return cact ? -(a.w * da) : 0.0;
   }
   // HwCur(v) = HessL[v] + Gx(y Gxaj(v) / s)
@@ -577,7 +722,7 @@ struct Eng {
     const double dA = dAof(a, v);
     double dG = (2.0 * P.h * P.h / (double)N) * mm(dA, M2);
     {  // two-box second derivatives, constraint order
-      const double da = lane_read(dA, cr * d + cc);
+      const double da = lread(dA, cr * d + cc);
       const double t = (cact && ck == 2) ? a.y * (-2.0 * da) : 0.0;
       sh[l] = t;
       __syncthreads();
@@ -756,13 +901,13 @@ struct Eng {
   __device__ __forceinline__ riptrm_trs::Work repmat(const AtX& a, const Frame& F, double& hvps) {
     riptrm_trs::Work w = riptrm_trs::make_work(tl, DIMM);
     for (int j = 0; j < DIMM; ++j) {
-      for (int k = l; k < DIMM; k += W) w.p[k] = (k == j) ? 1.0 : 0.0;
+      for (int k = l; k < DIMM; k += NT) w.p[k] = (k == j) ? 1.0 : 0.0;
       __syncthreads();
       const PV bj = from_coords(F, (const double*)w.p);
       const PV h = hw(a, bj);
       hvps += 1.0;
       to_coords(F, h, (double*)w.q);
-      for (int k = l; k <= j; k += W) {
+      for (int k = l; k <= j; k += NT) {
         w.A[k * w.lda + j] = w.q[k];
         w.A[j * w.lda + k] = w.q[k];
       }
@@ -773,6 +918,10 @@ struct Eng {
   }
   // compute_direction's Exact_RepMat branch: returns the RIPTRM_TRS_* type
   __device__ __forceinline__ int trs_direction(const AtX& a, double Delta, PV& eta, double& hvps) {
+    if constexpr (BIG) {   // riptrm_si_solve refuses Exact_RepMat above d = 7 (manifold.dim > 96)
+      eta = PV{0.0, 0.0, 0.0};
+      return RIPTRM_TRS_BOUNDARY;
+    }
     const Frame F = frame(a.x);
     riptrm_trs::Work w = repmat(a, F, hvps);
     riptrm_trs::Blk<W> B(nullptr);
@@ -782,6 +931,7 @@ struct Eng {
   }
   // smallest eigenvalue of HwNew's matrix at (xN, yN, mu) (RIPTRM.py:599-613)
   __device__ __forceinline__ double mineig_at(PV xN, double yN, double mu, double& hvps) {
+    if constexpr (BIG) return 0.0;
     AtX aN;
     prepare(aN, xN, yN, mu);
     const Frame F = frame(xN);
@@ -797,25 +947,25 @@ struct Eng {
     const double gradnorm = gradlag_norm(x, y, f, A);
     const double g = cons_val(A);
     const double cv = cact ? y * g : 0.0;
-    const double sq_compl = wsum(cv * cv);
+    const double sq_compl = rsum(cv * cv);
     const double nv = cact ? fmax(-y, 0.0) : 0.0;
-    const double sq_nonneg = wsum(nv * nv);
+    const double sq_nonneg = rsum(nv * nv);
     const double iv = cact ? fmax(g, 0.0) : 0.0;
-    const double sq_ineq = wsum(iv * iv);
-    const double maxvio = wmax(cact ? iv : 0.0);
-    const double meanvio = wsum(iv) / (double)m;
-    const double maxy = wmax(cact ? fabs(y) : -INFINITY);
+    const double sq_ineq = rsum(iv * iv);
+    const double maxvio = rmax(cact ? iv : 0.0);
+    const double meanvio = rsum(iv) / (double)m;
+    const double maxy = rmax(cact ? fabs(y) : -INFINITY);
     double manvio = 0.0;
     if (P.opt.manvio_kind == RIPTRM_MANVIO_SI) {
       const double aj = x.j + tr(x.j), ar = x.r - tr(x.r), aq = x.q - tr(x.q);
-      manvio = (sqrt(wsum(aj * aj)) + sqrt(wsum(ar * ar))) + sqrt(wsum(aq * aq));
+      manvio = (sqrt(rsum(aj * aj)) + sqrt(rsum(ar * ar))) + sqrt(rsum(aq * aq));
     }
     bool pr, pq;
     double dR, dQ;
     eval_solvers(xprev.r, x.r, xprev.q, x.q, pr, pq, dR, dQ);
     if (P.opt.manvio_kind == RIPTRM_MANVIO_SI && (!pr || !pq)) manvio = INFINITY;
     const double dj = x.j - xprev.j;
-    const double dJ = sqrt(wsum(dj * dj));
+    const double dJ = sqrt(rsum(dj * dj));
     ev[0] = f;
     ev[1] = sqrt((dJ * dJ + dR * dR) + dQ * dQ);
     ev[2] = sqrt(((((gradnorm * gradnorm + sq_compl) + sq_nonneg) + sq_ineq) + 0.0) + manvio * manvio);
@@ -830,7 +980,7 @@ struct Eng {
 
   __device__ __forceinline__ double now() {
     double t = (l == 0) ? (double)wall_clock64() : -INFINITY;
-    return wmax(t);
+    return rmax(t);
   }
 
   __device__ __forceinline__ void log_row(const double (&ev)[10], double outer_it, double mu, const Info* inf, double tcg_iters,
@@ -980,12 +1130,12 @@ struct Eng {
         const double AN = Aof(xN);
         const double gN = cons_val(AN);
         const double sN = cact ? -gN : 1.0;
-        const double minx = wmin(cact ? sN : INFINITY);
-        const double miny = wmin(cact ? yN : INFINITY);
-        const bool xfeas = minx > 0.0 && wmin(cact ? (sN > 0.0 ? 1.0 : 0.0) : 1.0) > 0.0;
-        const bool yfeas = wmin(cact ? (yN > 0.0 ? 1.0 : 0.0) : 1.0) > 0.0;
+        const double minx = rmin(cact ? sN : INFINITY);
+        const double miny = rmin(cact ? yN : INFINITY);
+        const bool xfeas = minx > 0.0 && rmin(cact ? (sN > 0.0 ? 1.0 : 0.0) : 1.0) > 0.0;
+        const bool yfeas = rmin(cact ? (yN > 0.0 ? 1.0 : 0.0) : 1.0) > 0.0;
         const double cvv = cact ? yN * sN - mu : 0.0;
-        const double compl_ = sqrt(wsum(cvv * cvv));
+        const double compl_ = sqrt(rsum(cvv * cvv));
         info = Info{1.0, inner_it, 0.0, DeltaStep, (double)tstop, normdx, minx, miny, compl_, 0.0, 0.0, 0.0, -1.0,
                     0.0, 0.0};
         have_info = true;
@@ -1011,8 +1161,8 @@ struct Eng {
           info.status = RIPTRM_IS_PRIMAL_INFEASIBLE;
           Delta = P.opt.gamma * normdx;
         } else {  // update_xy_TR_radius, RIPTRM.py:631-705
-          const double ls = wsum(cact ? log(a.s) : 0.0);
-          const double lsN = wsum(cact ? log(sN) : 0.0);
+          const double ls = rsum(cact ? log(a.s) : 0.0);
+          const double lsN = rsum(cact ? log(sN) : 0.0);
           const double lb_c = a.f - mu * ls;
           const double lb_n = fN - mu * lsN;
           double ared = lb_c - lb_n;
@@ -1047,7 +1197,7 @@ struct Eng {
               const double il = cl * np_min(np_min(y, mu / sN), 1.0);
               yc = np_min(np_max(yN, il), iright);
             }
-            const double nd = wsum((cact && yc != yN) ? 1.0 : 0.0);
+            const double nd = rsum((cact && yc != yN) ? 1.0 : 0.0);
             x = xN;
             y = yc;
             info.status = RIPTRM_IS_SUCCESSFUL;
@@ -1154,11 +1304,12 @@ struct Eng {
 };
 
 template <int D>
-__global__ void __launch_bounds__(W) k_si(SIParams P) {
-  __shared__ double sh[2 * W];
-  __shared__ double ser[8 * W];
-  __shared__ int crs[MMAX], ccs[MMAX];
-  extern __shared__ double trs_lds[];   // Exact_RepMat only (dynamic size 0 otherwise)
+__global__ void __launch_bounds__(si_threads(D)) k_si(SIParams P) {
+  constexpr int NT = si_threads(D);
+  __shared__ double sh[2 * NT];
+  __shared__ double ser[NT == W ? 8 * W : 1];   // the one-wave serial solvers' slots
+  __shared__ int crs[NT], ccs[NT];
+  extern __shared__ double trs_lds[];   // one wave: Exact_RepMat only (size 0 otherwise); big D: si_big_lds_doubles
   const int b = blockIdx.x;
   if (b >= P.batch) return;
   Eng<D> e(P, b, sh, ser, crs, ccs, trs_lds);
@@ -1186,7 +1337,7 @@ void riptrm_si_release(riptrm_si::Bound* s) {
 }
 
 static bool si_dims_ok(int32_t d, int32_t N, int32_t m, int32_t batch, int32_t cap) {
-  return d >= 1 && d <= DMAX && N >= 1 && m >= 1 && m <= MMAX && batch >= 1 && cap >= 0;
+  return d >= 1 && d <= DMAX && N >= 1 && m >= 1 && m <= MMAX && m <= si_threads(d) && batch >= 1 && cap >= 0;
 }
 
 static SIParams si_params(riptrm_ctx* c, int mode) {
@@ -1226,9 +1377,11 @@ static int si_manifold_dim(int d) { return d * (d - 1) / 2 + d * (d + 1); }
 template <int D>
 static int si_launch_d(riptrm_ctx* c, const SIParams& P) {
   const bool exact = P.mode == MODE_SOLVE && P.opt.trs_solver == RIPTRM_TRS_SOLVER_EXACT_REPMAT;
-  const size_t shm = exact ? (size_t)riptrm_trs::work_doubles(si_manifold_dim(D)) * sizeof(double) : 0;
-  if (shm) HIPCHK(c, hipFuncSetAttribute((const void*)k_si<D>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm));
-  hipLaunchKernelGGL(k_si<D>, dim3((unsigned)P.batch), dim3(W), shm, c->stream, P);
+  const size_t shm = D > 8 ? (size_t)si_big_lds_doubles(D) * sizeof(double)
+                           : exact ? (size_t)riptrm_trs::work_doubles(si_manifold_dim(D)) * sizeof(double) : 0;
+  if (shm > 64 * 1024)
+    HIPCHK(c, hipFuncSetAttribute((const void*)k_si<D>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm));
+  hipLaunchKernelGGL(k_si<D>, dim3((unsigned)P.batch), dim3(si_threads(D)), shm, c->stream, P);
   HIPCHK(c, hipGetLastError());
   return RIPTRM_OK;
 }
@@ -1242,7 +1395,15 @@ static int si_launch(riptrm_ctx* c, const SIParams& P) {
     case 5: return si_launch_d<5>(c, P);
     case 6: return si_launch_d<6>(c, P);
     case 7: return si_launch_d<7>(c, P);
-    default: return si_launch_d<8>(c, P);
+    case 8: return si_launch_d<8>(c, P);
+    case 9: return si_launch_d<9>(c, P);
+    case 10: return si_launch_d<10>(c, P);
+    case 11: return si_launch_d<11>(c, P);
+    case 12: return si_launch_d<12>(c, P);
+    case 13: return si_launch_d<13>(c, P);
+    case 14: return si_launch_d<14>(c, P);
+    case 15: return si_launch_d<15>(c, P);
+    default: return si_launch_d<16>(c, P);
   }
 }
 
@@ -1273,7 +1434,8 @@ int riptrm_si_bind(riptrm_ctx* ctx, const riptrm_si_problem* prob, int32_t batch
   if (!prob || prob->struct_size != (int32_t)sizeof(riptrm_si_problem))
     return fail(ctx, RIPTRM_E_ARG, "si_bind: riptrm_si_problem.struct_size mismatch");
   if (!si_dims_ok(prob->d, prob->N, prob->m, batch, cap))
-    return fail(ctx, RIPTRM_E_ARG, "si_bind: need 1 <= d <= 8, N >= 1, 1 <= m <= 64, batch >= 1");
+    return fail(ctx, RIPTRM_E_ARG, "si_bind: need 1 <= d <= RIPTRM_SI_DMAX, N >= 1, 1 <= m <= 64 (d <= 8) or "
+                                   "m <= 64 ceil(d^2 / 64) (d > 8), batch >= 1");
   if (!prob->X || !prob->XP || !prob->cons || !ws || prob->data_stride < 0 || prob->cons_stride < 0)
     return fail(ctx, RIPTRM_E_ARG, "si_bind: bad argument");
   if (prob->data_stride != 0 && prob->data_stride < (int64_t)prob->d * prob->N)

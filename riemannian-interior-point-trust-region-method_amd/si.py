@@ -4,7 +4,8 @@ The reference (``src/StableIdentification/coordinator.py:13-187``) builds a pyma
 (SkewSymmetric(d), SPD(d), SPD(d)) problem whose cost and m box constraints are autograd closures
 over the trajectory data X / XP.  The drop-in takes the data instead (``SIProblem``) and runs every
 RIPTRM solve of a batch (the ``problem_initialpoint`` / ``problem_instance`` axes) inside ONE HIP
-launch, one 64-lane workgroup per instance (``csrc/riptrm_si.hip``).  No CPU fallback.
+launch, one workgroup per instance (``csrc/riptrm_si.hip``: a 64-lane wave up to d = 8, one thread per
+element of a d x d block above, d <= RIPTRM_SI_DMAX).  No CPU fallback.
 """
 from __future__ import annotations
 
@@ -172,7 +173,8 @@ class SIBatch:
         self.dd = self.d * self.d
         nbytes = int(self.lib.riptrm_si_workspace_bytes(self.d, self.N, self.m, self.batch, self.cap))
         if nbytes < 0:
-            raise ValueError("need 1 <= d <= 8, 1 <= m <= 64, batch >= 1")
+            raise ValueError(f"need 1 <= d <= {N.CONST['RIPTRM_SI_DMAX']}, 1 <= m <= 64 (d <= 8) or "
+                             f"m <= 64 ceil(d^2 / 64) (d > 8), batch >= 1")
         self.ctx = N.Context(self.device.index, _stream_handle(self.device))
         self.ws = torch.zeros(nbytes + 256, dtype=torch.uint8, device=self.device)
         base = self.ws.data_ptr()

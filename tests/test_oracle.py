@@ -366,3 +366,28 @@ def test_variant_support_for_flips():
     assert variant_supports_flip([earlier], gpu, ref, (4, "inner_status"))
     later = V(); later.log = log(["successful"] * 5 + ["unsuccessful"])
     assert not variant_supports_flip([later], gpu, ref, (4, "inner_status"))
+
+
+def test_decision_margins_reproduce_the_logged_ratio():
+    """parity.decision_margins re-runs one inner step of the oracle from its recorded state and
+    returns ared / pred (their ratio is the logged 'ared/pred' bit for bit) with the forward error
+    of both; a decision with a margin far above that error is not a tie."""
+    from parity import StateRecorder, decision_margins, decision_tie
+    Z, x0, y0 = G.generate_instance(37, 100)
+    P = O.NonnegPCAVectorized(Z)
+    oa = O.RIPTRMOracle(dict(OPT, maxiter=6))
+    rec = StateRecorder(oa)
+    r = oa.run(P, x0, y0)
+    rows = [i for i, s in enumerate(r.log["inner_status"]) if s in ("successful", "unsuccessful")]
+    assert rows
+    for row in rows[:4]:
+        m = decision_margins(rec.step, P, rec.states[row - 1])
+        assert m["ared"] / m["pred"] == r.log["ared/pred"][row]
+        assert 0 < m["err_ared"] < 1e-10 and 0 <= m["err_pred"] < 1e-10
+    # a well-separated decision is not a tie (the flipped log claims the other outcome)
+    row = rows[0]
+    m = decision_margins(rec.step, P, rec.states[row - 1])
+    if abs(m["ared"] - 0.1 * m["pred"]) > 10 * (m["err_ared"] + 0.1 * m["err_pred"]):
+        fake = {k: list(v) for k, v in r.log.items()}
+        fake["inner_status"][row] = "unsuccessful" if r.log["inner_status"][row] == "successful" else "successful"
+        assert decision_tie(rec.step, P, rec.states, fake, r.log, (row, "inner_status")) is None
