@@ -319,7 +319,8 @@ def main():
                          "always, 3 = super-tile for launches with >= 1 unit per CU if a bind-time timing preferred it")
     ap.add_argument("--persistent", type=int, default=1, choices=[0, 1, 2],
                     help="k_persist for small batches: 1 = cooperative launch (default), 2 = plain launch (A/B), 0 = off")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_gemv.json"))
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r4_traffic_spass_sup.json"),
+                    help="per instance-pass HBM bytes of the S-pass from a committed rocprofv3 PMC summary (scripts/gate.sh pmc_spass)")
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend (nccl = RCCL)")
     ap.add_argument("--dump", default="",
                     help="rank 0 writes the gathered x, y and stats of every global instance to this .npz")
@@ -513,6 +514,24 @@ def main():
                         "kernel": spass_label if args.layout == "sym" else "k_gemv (S-pass, full matrix)",
                         "bytes_per_launch": passes_r0 * bytes_per_pass / nl,
                         "avg_launch_us": prof["gemv_ms"] * 1e3 / nl}
+        # the state kernel's vector work (the Sphere projection / retraction and the tCG updates,
+        # fused in k_state): per instance-step it reads x, y, cxCur, delta, eta, Heta, r and the
+        # S-pass's partial sums of every element (one per super-tile / tile column), and writes
+        # delta, eta, Heta, r back
+        state_roofline = None
+        if not graph_mode and not persist and prof["state_ms"] > 0 and args.layout == "sym":
+            nt_ = -(-n // 128)
+            parts = -(-nt_ // 2) if spass_kernel == "k_spass_sup" else nt_
+            sbytes = passes_r0 * (11 + parts) * 8.0 * n
+            sach = sbytes / (prof["state_ms"] / 1e3) / 1e9
+            state_roofline = {"bound": "hbm", "achieved": sach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                              "frac": sach / HBM_PEAK_GBS, "bytes_per_launch": sbytes / max(1, prof["state_launches"]),
+                              "avg_launch_us": prof["state_ms"] * 1e3 / max(1, prof["state_launches"]),
+                              "bytes_definition": (f"per instance-step (11 + {parts}) x 8 n bytes: x, y, cxCur, delta, eta, "
+                                                   f"Heta, r read and delta, eta, Heta, r written, plus the {parts} "
+                                                   "partial sums of every element the S-pass left"),
+                              "kernel": "k_state (tCG step, Sphere projection / retraction, trial point, acceptance; "
+                                        "runs beside the other stream group's S-pass)"}
         cpu = None
         if args.cpu_budget > 0 and world == 1:
             positions = window_positions(W, K, args.cycle)
@@ -567,6 +586,7 @@ def main():
                        if graph_mode else "HIP events inside the timed window",
                        "state_kernel_ms": prof["state_ms"], "state_launches": prof["state_launches"],
                        "gemv_launches": prof["gemv_launches"],
+                       "state_kernel_roofline": state_roofline,
                        **({"spass_calibration": cal} if cal.get("ms_per_launch_tile") else {})},
         }
         print(json.dumps(out), flush=True)
