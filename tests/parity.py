@@ -321,7 +321,25 @@ def prefix_deviation(gl, rl, rows, cap=DRIFT_CAP):
     return min(cap, max(column_deviation(p, q, k) for k in ("cost", "residual", "maxabsLagmult")))
 
 
-def classify_flip(step, P, states, gl, rl, flip, trials=8, seed=0):
+def sphere_perturb(x, y, eps, rs):
+    """relative perturbation of a Sphere point (renormalised) and of the multipliers"""
+    xp = x * (1.0 + eps * rs.randn(x.shape[0]))
+    return xp / np.linalg.norm(xp), y * (1.0 + eps * rs.randn(y.shape[0]))
+
+
+def si_perturb(x, y, eps, rs):
+    """relative perturbation of a Product(Skew, SPD, SPD) point that keeps its structure (J skew,
+    R and Q symmetric: an elementwise factor 1 + eps sym(noise)) and of the multipliers"""
+    xp = np.empty_like(x)
+    a = rs.randn(*x.shape[1:])
+    xp[0] = x[0] * (1.0 + eps * (a + a.T) / 2)
+    for k in (1, 2):
+        b = rs.randn(*x.shape[1:])
+        xp[k] = x[k] * (1.0 + eps * (b + b.T) / 2)
+    return xp, y * (1.0 + eps * rs.randn(y.shape[0]))
+
+
+def classify_flip(step, P, states, gl, rl, flip, trials=8, seed=0, perturb=sphere_perturb):
     """A branch flip at log row `flip[0]` (key flip[1]) is a rounding-driven one if the GPU's decision
     is reachable from the ORACLE's own state at that inner step perturbed at any size from 1e-14 up
     to the drift the two trajectories had accumulated before it on their outer iterates
@@ -343,9 +361,7 @@ def classify_flip(step, P, states, gl, rl, flip, trials=8, seed=0):
     sizes = np.logspace(-14, np.log10(drift), max(1, int(np.ceil(np.log10(drift) + 14)) + 1))
     for t in range(trials * len(sizes)):
         eps = sizes[t // trials] * (0.5 + rs.rand())
-        xp = x * (1.0 + eps * rs.randn(x.shape[0]))
-        xp = xp / np.linalg.norm(xp)
-        yp = y * (1.0 + eps * rs.randn(y.shape[0]))
+        xp, yp = perturb(x, y, eps, rs)
         _, _, _, _, info = step(P, xp, yp, mu, Delta, it, iopt)
         if info.get(key) == want:
             return eps
