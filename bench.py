@@ -309,6 +309,8 @@ def main():
     ap.add_argument("--problem", default="nonnegpca", choices=["nonnegpca", "si", "stiefel"],
                     help="si: StableIdentification (d=5 fixture, starts cycled + perturbed), one launch per solve")
     ap.add_argument("--stiefel-p", type=int, default=50, help="p of Stiefel(n, p) for --problem stiefel")
+    ap.add_argument("--si-dim", type=int, default=5,
+                    help="block size d of --problem si (5: the reference fixture; else si.synthetic_problem)")
     ap.add_argument("--trs", default="tCG", choices=["tCG", "Exact_RepMat"],
                     help="subproblem solver (Exact_RepMat: manifold.dim <= 96, with the second-order test)")
     ap.add_argument("--stream-groups", type=int, default=0, choices=[0, 1, 2],
@@ -695,40 +697,59 @@ def bench_stiefel(args, world, rank, dev, dist):
     }), flush=True)
 
 
-def si_starts(B: int, ids):
-    """StableIdentification batch: the fixture's 20 starts (dataset/StableIdentification/1, a..t)
-    cycled; copies beyond the first 20 perturbed (seeded by global id) so no two solves match:
-    J + 1e-3 skew noise, R and Q congruence-scaled by (I + 1e-3 sym noise), which keeps them SPD."""
+def si_instance(d: int, starts: int = 20):
+    """The StableIdentification data of the SI bench line: the reference's fixture
+    (dataset/StableIdentification/1, d = 5: coordinator.py:54-90 stacking, constset.csv, starts a..t)
+    or, for another d, the product's restatement of the dataset recipe (si.synthetic_problem,
+    generator.py:18-134), seed 1000 + d.  Returns (X, XP, h, constset rows, [(x0, y0), ...])."""
     import numpy as np
-    from oracle import si_oracle as SI
-    ds = os.path.join(ROOT, "tests", "golden", "si_1")
-    base = [SI.load_start(ds, p) for p in "abcdefghijklmnopqrst"]
+    if d == 5:
+        ds = os.path.join(ROOT, "tests", "golden", "si_1")
+        X = XP = None
+        for i in (1, 2, 3, 4, 5):
+            Xo = np.loadtxt(os.path.join(ds, f"noisyX_{i}.csv"))
+            X = Xo[:, :-1] if X is None else np.hstack((X, Xo[:, :-1]))
+            XP = Xo[:, 1:] if XP is None else np.hstack((XP, Xo[:, 1:]))
+        y0 = np.atleast_1d(np.loadtxt(os.path.join(ds, "initineqLagmult.csv")))
+        st = [(np.stack([np.loadtxt(os.path.join(ds, f"init{c}_{p}.csv")) for c in "JRQ"]), y0)
+              for p in "abcdefghijklmnopqrst"]
+        return X, XP, 0.02, np.loadtxt(os.path.join(ds, "constset.csv")), st
+    import si
+    return si.synthetic_problem(d, 1000 + d, starts=starts)
+
+
+def si_starts(B: int, ids, d: int = 5):
+    """StableIdentification batch: the instance's starts (si_instance: 20) cycled; copies beyond the
+    first 20 perturbed (seeded by global id) so no two solves match: J + 1e-3 skew noise, R and Q
+    congruence-scaled by (I + 1e-3 sym noise), which keeps them SPD."""
+    import numpy as np
+    X, XP, h, constset, base = si_instance(d)
     xs, ys = [], []
     for gid in ids:
-        x0, y0 = base[gid % 20]
+        x0, y0 = base[gid % len(base)]
         x = x0.copy()
-        if gid >= 20:
+        if gid >= len(base):
             rs = np.random.RandomState(1000 + gid)
-            a = rs.randn(5, 5) * 1e-3
+            a = rs.randn(d, d) * 1e-3
             x[0] = x[0] + (a - a.T) / 2
             for k in (1, 2):
-                e = np.eye(5) + 1e-3 * (lambda b: (b + b.T) / 2)(rs.randn(5, 5))
+                e = np.eye(d) + 1e-3 * (lambda b: (b + b.T) / 2)(rs.randn(d, d))
                 x[k] = e @ x[k] @ e.T
         xs.append(x)
         ys.append(y0)
-    return np.stack(xs), np.stack(ys), SI.SIData.load(ds)
+    return np.stack(xs), np.stack(ys), (X, XP, h, constset)
 
 
-def _si_oracle_window(gid: int, K: int, budget_s: float, trs: str):
+def _si_oracle_window(gid: int, K: int, budget_s: float, trs: str, d: int = 5):
     """The SI oracle on bench start `gid` (si_starts), outer iterations 1..K or as many as the
     budget allows; returns (completed outer iterations, solver seconds) or None."""
     from oracle import riptrm_oracle as RO
     from oracle import si_oracle as SI
-    xs, ys, data = si_starts(1, [gid])
+    xs, ys, (X, XP, h, constset) = si_starts(1, [gid], d)
     orc = RO.RIPTRMOracle(dict(maxiter=K, tolresid=0.0, maxtime=1e12, manviofun=SI.si_manvio,
                                **trs_options(trs)), deadline=time.time() + budget_s)
     try:
-        orc.run(SI.SIVectorized(data), xs[0], ys[0])
+        orc.run(SI.SIVectorized(SI.SIData(X, XP, h, constset)), xs[0], ys[0])
     except RO.BudgetExceeded:
         pass
     heads = orc.outer_heads
@@ -738,19 +759,20 @@ def _si_oracle_window(gid: int, K: int, budget_s: float, trs: str):
 
 def _si_cpu_worker(argv):
     """One single-threaded SI oracle process (run by si_cpu_pool)."""
-    gid, K, budget, trs = int(argv[0]), int(argv[1]), float(argv[2]), argv[3]
-    r = _si_oracle_window(gid, K, budget, trs)
+    gid, K, budget, trs, d = int(argv[0]), int(argv[1]), float(argv[2]), argv[3], int(argv[4])
+    r = _si_oracle_window(gid, K, budget, trs, d)
     print(json.dumps(None if r is None else {"outer": r[0], "secs": r[1]}), flush=True)
 
 
-def si_cpu_pool(K: int, budget_s: float, procs: int, trs: str):
+def si_cpu_pool(K: int, budget_s: float, procs: int, trs: str, d: int = 5):
     """The StableIdentification analogue of cpu_baseline_pool: `procs` single-threaded oracle
     processes run concurrently, process i solving the GPU batch's start i (si_starts) over the
     same outer window 1..K; aggregate = mean complete per-process rate x procs."""
     import subprocess
     env = dict(os.environ, OMP_NUM_THREADS="1", OPENBLAS_NUM_THREADS="1", MKL_NUM_THREADS="1")
     ps = [subprocess.Popen([sys.executable, os.path.abspath(__file__), "--si-cpu-worker", str(i), str(K),
-                            str(budget_s), trs], stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, env=env, text=True)
+                            str(budget_s), trs, str(d)], stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, env=env,
+                           text=True)
           for i in range(procs)]
     rates = []
     for p in ps:
@@ -779,10 +801,11 @@ def bench_si(args, world, rank, dev, dist):
     import si
     B, W, K = args.batch, args.warmup, args.steps
     ids = [rank + world * i for i in range(B)]
-    xs, ys, data = si_starts(B, ids)
-    cons = si.expand_constset(np.loadtxt(os.path.join(ROOT, "tests", "golden", "si_1", "constset.csv")))
-    eng = si.SIBatch(data.d, data.N, data.m, B, log_capacity=16)
-    eng.load(data.X, data.XP, data.h, cons)
+    d = args.si_dim
+    xs, ys, (X, XP, h, constset) = si_starts(B, ids, d)
+    cons = si.expand_constset(constset)
+    eng = si.SIBatch(d, X.shape[1], cons.shape[0], B, log_capacity=16)
+    eng.load(X, XP, h, cons)
     opt = {"manviofun": si.si_manviofun, "tolresid": 0.0, "maxtime": math.inf,
            "maxiter": max(1, W), "save_inner_iteration": True, **trs_options(args.trs)}
     eng.solve(xs, ys, opt)          # warmup launch (W outer iterations), untimed
@@ -821,28 +844,31 @@ def bench_si(args, world, rank, dev, dist):
         return
     cpu = None
     if args.cpu_budget > 0 and world == 1:
-        one = _si_oracle_window(0, K, args.cpu_budget, args.trs)
+        one = _si_oracle_window(0, K, args.cpu_budget, args.trs, d)
         if one is not None:
             last, secs = one
             cpu = {"value": last / secs, "unit": "outer iterations/s", "cores": 1, "kind": "port",
-                   "sample": f"oracle/si_oracle.py SIVectorized (NumPy, closed-form Lagrangian), start 'a', outer "
+                   "sample": f"oracle/si_oracle.py SIVectorized (NumPy, closed-form Lagrangian), d={d}, start 0, outer "
                              f"iterations 1..{last} ({secs:.1f} s, evaluation time excluded as RIPTRM.py:932-941)"}
         procs = min(args.cpu_procs, B)
         pool = None
         if procs > 0:
             log(f"SI CPU baseline, {procs} single-threaded processes ...")
-            pool = si_cpu_pool(K, args.cpu_pool_budget, procs, args.trs)
+            pool = si_cpu_pool(K, args.cpu_pool_budget, procs, args.trs, d)
         cpu = pick_cpu_baseline(cpu, pool)
         if cpu is not None:
             cpu.update(host_cpu_info())
             cpu["gpu_over_cpu"] = (outer / T) / cpu["value"]
     print(json.dumps({
-        "metric": f"outer RIPTRM iterations/sec, StableIdentification d=5 (Product(Skew,SPD,SPD)), batch {B}/GPU",
+        "metric": f"outer RIPTRM iterations/sec, StableIdentification d={d} (Product(Skew,SPD,SPD)), batch {B}/GPU",
         "value": outer / T, "unit": "outer iterations/s", "n_gpus": world, "steps": K, "warmup": W,
         "ms_per_step": T / K * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
         "dtype": "f64",
-        "data": "reference fixture dataset/StableIdentification/1 (noisy X, 16 constraints), starts a..t cycled + perturbed",
-        "config": {"workload": f"StableIdentification d=5 N=95 m=16, {B} starts per GPU, outer iterations 1..{K}"
+        "data": ("reference fixture dataset/StableIdentification/1 (noisy X, 16 constraints), starts a..t cycled + perturbed"
+                 if d == 5 else f"synthetic: si.synthetic_problem(d={d}, seed {1000 + d}) (the reference's dataset recipe), "
+                                "20 starts cycled + perturbed"),
+        "config": {"workload": f"StableIdentification d={d} N={X.shape[1]} m={cons.shape[0]}, {B} starts per GPU, "
+                               f"outer iterations 1..{K}"
                                + ("" if args.trs == "tCG" else ", TRS_solver=Exact_RepMat + second-order test"),
                    "trs_solver": args.trs,
                    "global_batch": B * world, "parallelism": f"instance-sharded x{world}", "world_size": world},

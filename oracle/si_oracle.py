@@ -192,93 +192,13 @@ def load_start(dataset_path: str, pt: str):
     return x0, y0
 
 
-def synthetic_instance(d: int, seed: int, starts: int = 1, N: int = 20, Xset: Sequence[int] = (1, 2, 3, 4, 5),
-                       oneboxratio: float = 0.2, twoboxratio: float = 0.1, snr: float = 10.0, h: float = 0.02):
-    """A StableIdentification instance of block size d by the reference's dataset recipe
-    (src/StableIdentification/generator.py:18-134, config_dataset.yaml: N 20, one-box ratio 0.2,
-    two-box ratio 0.1, snr 10 dB, h 0.02, 5 trajectories), seeded (numpy legacy RandomState):
-      * true (J, R, Q): skew / SPD random points, A = (J - R) Q (:55-64);
-      * constraints on floor(ratio d^2) random entries of A (:66-109): one-box [A - a|A|, A + b|A|],
-        two-box [-|A| - a|A|, |A| + b|A|] plus -(A - c)^2 + k^2 <= 0 with c = cc A;
-      * trajectories x_i = exp(i h A) x_0 ELEMENTWISE (np.exp, as :124) from x_0 ~ U(-1000, 1000)^d,
-        AWGN at snr dB (:111-120), normalised (:127-128); X / XP = the noisy ones without their
-        last / first column, stacked (coordinator.py:54-90).
-    One deviation: the reference draws the constraint values around the true A and then finds
-    strictly interior starts with RALM (:136-207, out of scope).  Here a start is the true point
-    congruence-perturbed (J + 0.05 skew noise, R, Q -> E R E^T with E = I + 0.05 sym noise), the
-    constraint values are drawn around start 0's A (so it is strictly feasible: the two-box radius
-    is k = kc |A - c| with kc in [0.2, 0.8)), and further starts (start 0 perturbed the same way at
-    2e-3) are kept only if strictly feasible.
-    y0 = ones(m).  Returns (SIData, [(x0, y0), ...])."""
-    rs = np.random.RandomState(seed)
-
-    def skew_pt():
-        a = rs.randn(d, d)
-        return (a - a.T) / 2
-
-    def spd_pt():
-        q, _ = np.linalg.qr(rs.randn(d, d))
-        return (q * rs.uniform(0.5, 2.0, d)) @ q.T
-
-    J, R, Q = skew_pt(), spd_pt(), spd_pt()
-    A = (J - R) @ Q
-
-    def perturb(x, eps=0.05):
-        e = np.eye(d) + eps * (lambda b: (b + b.T) / 2)(rs.randn(d, d))
-        return np.stack([x[0] + eps * skew_pt(), e @ x[1] @ e.T, e @ x[2] @ e.T])
-
-    x_first = perturb(np.stack([J, R, Q]))
-    A0 = (x_first[0] - x_first[1]) @ x_first[2]
-    nel = d * d
-    n1, n2 = int(nel * oneboxratio), int(nel * twoboxratio)
-    idx = rs.permutation(nel)[:n1 + n2]
-    rows = []
-    for t, cind in enumerate(idx):
-        r, c = cind % d, cind // d
-        av = A0[r, c]
-        aa = abs(av)
-        if t < n1:
-            rows.append([0, r, c, av - rs.uniform(0.2, 0.8) * aa, av + rs.uniform(0.2, 0.8) * aa])
-        else:
-            cc = rs.uniform(0.2, 0.8) * av
-            k = rs.uniform(0.2, 0.8) * abs(av - cc)
-            rows.append([1, r, c, -aa - rs.uniform(0.2, 0.8) * aa, aa + rs.uniform(0.2, 0.8) * aa])
-            rows.append([2, r, c, cc, k])
-    constset = np.asarray(rows, dtype=np.float64)
-    Xs = XPs = None
-    for _ in Xset:
-        x0 = -1000 + 2000 * rs.rand(d)
-        Xt = np.zeros((d, N))
-        Xn = np.zeros((d, N))
-        for i in range(N):
-            xi = x0 if i == 0 else np.exp(i * h * A) @ x0
-            Xt[:, i] = xi
-            p = np.mean(np.abs(xi) ** 2) / 10 ** (snr / 10)
-            Xn[:, i] = xi + np.sqrt(p) * rs.randn(d)
-        Xn = Xn / np.linalg.norm(Xn[:, 0])
-        Xs = Xn[:, :N - 1] if Xs is None else np.hstack((Xs, Xn[:, :N - 1]))
-        XPs = Xn[:, 1:] if XPs is None else np.hstack((XPs, Xn[:, 1:]))
-    data = SIData(Xs, XPs, h, constset)
-
-    def feasible(x):
-        Ax = (x[0] - x[1]) @ x[2]
-        for kind, r, c, p0, p1 in data.cons:
-            a = Ax[r, c]
-            g = (-a + p0) if kind == 0 else ((a - p0) if kind == 1 else (-(a - p0) ** 2 + p1))
-            if not g < 0:
-                return False
-        return bool(np.all(np.linalg.eigvalsh(x[1]) > 0) and np.all(np.linalg.eigvalsh(x[2]) > 0))
-
-    assert feasible(x_first), "start 0 must be strictly feasible by construction"
-    out = [(x_first, np.ones(data.m))]
-    tries = 0
-    while len(out) < starts and tries < 100 * starts:
-        tries += 1
-        x = perturb(x_first, 2e-3)
-        if feasible(x):
-            out.append((x, np.ones(data.m)))
-    assert len(out) == starts, "could not draw enough strictly feasible starts"
-    return data, out
+def synthetic_instance(d: int, seed: int, starts: int = 1, **kw):
+    """A StableIdentification instance of block size d by the reference's dataset recipe: the
+    product's restatement si.synthetic_problem (src/StableIdentification/generator.py:18-134, its one
+    deviation documented there), wrapped as SIData.  Returns (SIData, [(x0, y0), ...])."""
+    import si
+    X, XP, h, constset, st = si.synthetic_problem(d, seed, starts=starts, **kw)
+    return SIData(X, XP, h, constset), st
 
 
 def si_manvio(x):
