@@ -301,13 +301,10 @@ __device__ __forceinline__ void p3_gram(const lds_f64* Xs, const lds_f64* Us, in
 // behind its own branch; measured 21.9k ticks for the update at (200, 50))
 // units (independent accumulator chains) per wave per step of the update; measured at (200, 50):
 // 2 / 3 / 4 -> 22.9k / 22.9k / 23.5k ticks (4 spills): the update is not bound by its chains
-#ifndef RIPTRM_P3_UB
-#define RIPTRM_P3_UB 2
-#endif
 template <int P16, int P4T, int UMAX>
 __device__ __forceinline__ void p3_update(const lds_f64* Xs, const double (&bk)[4 * P16], const double (&cv)[UMAX][4],
                                           double* out, int n, int p, int w, int c, int kk, int J, int nunits) {
-  constexpr int UB = RIPTRM_P3_UB;
+  constexpr int UB = 2;
 #pragma unroll
   for (int q = 0; q < UMAX; q += UB) {
     if (w + NW * q >= nunits) continue;   // wave-uniform (no break: the loop stays unrolled)
@@ -674,13 +671,8 @@ __device__ __forceinline__ void r2_block_ij(int b, int& I, int& J) {
   J = i + b;
 }
 
-// the factor of k_st_retr2: 2 = blocked (r3_factor_blocked, default); 0 = the 8-wave exchange
-// (r2_factor_inverse); 1 = one wave, no barrier per step (r2_factor_inverse_1w), measured 159k vs 69k
-// ticks per factor at (200, 50) (profiles/r3_stiefel_factor_1wave_stamps.jsonl).  A/B:
-// tools/stiefel_stamps.hip -DRIPTRM_ST_FACTOR=0/1.  With 2 the Gram writes only G's upper triangle.
-#ifndef RIPTRM_ST_FACTOR
-#define RIPTRM_ST_FACTOR 2
-#endif
+// The Gram writes only G's upper triangle: the blocked factor (r3_factor_blocked) and the
+// first-order inverse read nothing else.
 
 // MASK = false when every batch is full (both halves a multiple of the batch size, e.g. n = 200): the
 // 0/1 factor on each A operand is then dropped — with it in, each read's multiply waits on that read
@@ -751,9 +743,6 @@ __device__ __forceinline__ void r2_gram_finish(lds_f64* Gm, lds_f64* red) {
       const int i = 16 * I + (ll >> 4) + 4 * q, j = 16 * J + (ll & 15);   // f64 D: row (l >> 4) + 4 q, col l & 15
       if (I < J || i <= j) {   // one writer per symmetric pair: G exactly symmetric
         Gm[i * S + j] = v[m];
-#if RIPTRM_ST_FACTOR != 2
-        Gm[j * S + i] = v[m];
-#endif
       }
     }
   }
@@ -771,10 +760,7 @@ __device__ __forceinline__ void r2_gram(lds_f64* As, lds_f64* Gm, lds_f64* red, 
 // 16, so they are dropped — the matrix cores take the 6 blocks of the first 48 columns and the VALU
 // takes the tw last columns: wave w sums rows [26 w, 26 w + 26) of A[r][i] A[r][48 + t] in lane i,
 // the 8 wave partials meet in wave order.  G's last column block is written whole (zeros past p),
-// upper triangle only (RIPTRM_ST_FACTOR 2 reads nothing else).  Unmasked batches only.
-#ifndef RIPTRM_ST_GTAIL
-#define RIPTRM_ST_GTAIL 1
-#endif
+// upper triangle only (the blocked factor reads nothing else).  Unmasked batches only.
 template <int TW>
 __device__ __forceinline__ void r4t_gram(lds_f64* As, lds_f64* Gm, lds_f64* red, int NR, int n, int p) {
   constexpr int S = 64, PM = 3, NBm = 6, c0 = 48, UB2 = 13;
@@ -866,7 +852,6 @@ __device__ __forceinline__ void r4t_gram(lds_f64* As, lds_f64* Gm, lds_f64* red,
 // r4t_gram where it applies (P16 = 4, 1 <= p - 48 <= 4, whole batches, the blocked factor), else r2_gram
 template <int P16>
 __device__ __forceinline__ void r2_gram_any(lds_f64* As, lds_f64* Gm, lds_f64* red, int NR, int n, int p) {
-#if RIPTRM_ST_GTAIL && RIPTRM_ST_FACTOR == 2
   if (P16 == 4) {
     const int NG = NR / 4, H0 = NG / 2;
     if (H0 % 13 == 0 && (NG - H0) % 13 == 0) {
@@ -879,204 +864,12 @@ __device__ __forceinline__ void r2_gram_any(lds_f64* As, lds_f64* Gm, lds_f64* r
       }
     }
   }
-#endif
   r2_gram<P16>(As, Gm, red, NR);
 }
 
-// Gm (G, stride S) -> Gm (W = R^-1 = E^T, stride S); xch: 4 FB S doubles of exchange space (the Gram's
-// partial-sum area, NB * 256 >= 16 S doubles)
-// columns eliminated per barrier step of r2_factor_inverse (tools/stiefel_stamps.hip builds 1 / 2 / 4 for A/B)
-#ifndef RIPTRM_ST_FB
-#define RIPTRM_ST_FB 2   // measured: 1 -> 75.7k, 2 -> 69.3k, 4 -> 77.6k ticks per factor at p = 50
-#endif
-constexpr int FB = RIPTRM_ST_FB;
-// pivot reciprocal of the blocked factor's diagonal blocks: IEEE division (0) or v_rcp_f64 + Newton (1)
-#ifndef RIPTRM_ST_RCP
-#define RIPTRM_ST_RCP 1   // measured 37.9k vs 39.3k ticks per factor at (200, 50)
-#endif
-
-static_assert(FB <= 4 && 8 % FB == 0, "the exchange alternates 2 buffers within a group of 8 rows");
-
-template <int P16>
-__device__ __forceinline__ void r2_factor_inverse(lds_f64* Gm, lds_f64* xch, int p) {
-  constexpr int S = 16 * P16;
-  const int t = threadIdx.x, l = t & 63, w = t >> 6;
-  double g[8], e[8], piv[8];
-#pragma unroll
-  for (int r = 0; r < 8; ++r) {
-    const int i = 8 * w + r;
-    const bool ok = i < S && l < S;
-    g[r] = ok ? Gm[i * S + l] : 0.0;
-    e[r] = (i == l) ? 1.0 : 0.0;
-    piv[r] = 1.0;   // rows past p keep E's identity rows
-  }
-  // FB columns per step (block elimination): the FB x FB pivot block P = G[K][K] is factored
-  // P = L D L^T by every thread (unit lower L, redundant, in registers); with C' = C L^-T (the pivot
-  // columns) and E'_K = L^-1 E_K (the pivot rows) the step is G_ij -= sum_c C'_ic C'_jc / D_c,
-  // E_i -= sum_c (C'_ic / D_c) E'_Kc for the rows after the block; E'_K and D are the block's final
-  // (unscaled) E rows and pivots.  FB = 1 is the plain Gauss-Jordan step; FB columns cost one barrier.
-  for (int kb = 0; 8 * kb < p; ++kb) {
-#pragma unroll
-    for (int r0 = 0; r0 < 8; r0 += FB) {
-      const int k = 8 * kb + r0;
-      if (k >= p) break;   // uniform
-      const int nb = p - k < FB ? p - k : FB;   // valid columns of this block
-      lds_f64* cgs = xch + ((r0 / FB) & 1) * 2 * FB * S;   // [G cols k..k+FB-1 | E rows k..k+FB-1], 2 buffers
-      lds_f64* res = cgs + FB * S;
-      if (l >= k && l < k + nb) {
-        lds_f64* dst = cgs + (l - k) * S;
-#pragma unroll
-        for (int r = 0; r < 8; ++r)
-          if (8 * w + r < S) dst[8 * w + r] = g[r];
-      }
-      if (w == kb && l < S) {
-#pragma unroll
-        for (int a = 0; a < FB; ++a) res[a * S + l] = e[r0 + a];
-      }
-      __syncthreads();
-      // every operand of the step read at once (a load under the row guard would get its own wait:
-      // one LDS round trip per row); slots past S or past nb hold finite stale values, masked out
-      const int jl = l < S ? l : 0;
-      double P[FB][FB], colj[FB], ekr[FB], ci[FB][8];
-#pragma unroll
-      for (int c = 0; c < FB; ++c) {
-#pragma unroll
-        for (int a = 0; a < FB; ++a) P[a][c] = cgs[c * S + k + a];
-        colj[c] = cgs[c * S + jl];
-        ekr[c] = res[c * S + jl];
-#pragma unroll
-        for (int r = 0; r < 8; ++r) ci[c][r] = cgs[c * S + 8 * w + r];
-      }
-      double Lf[FB][FB], D[FB], invD[FB];
-#pragma unroll
-      for (int c = 0; c < FB; ++c) {
-        const bool cv = c < nb;
-        double dc = P[c][c];
-#pragma unroll
-        for (int t = 0; t < c; ++t) dc = dc - Lf[c][t] * Lf[c][t] * D[t];
-        D[c] = cv ? dc : 1.0;
-        invD[c] = 1.0 / D[c];
-#pragma unroll
-        for (int a = c + 1; a < FB; ++a) {
-          double v = P[a][c];
-#pragma unroll
-          for (int t = 0; t < c; ++t) v = v - Lf[a][t] * Lf[c][t] * D[t];
-          Lf[a][c] = (cv && a < nb) ? v * invD[c] : 0.0;
-        }
-      }
-#pragma unroll
-      for (int c = 0; c < FB; ++c)
-#pragma unroll
-        for (int t = 0; t < c; ++t) {
-          colj[c] = colj[c] - Lf[c][t] * colj[t];
-          ekr[c] = ekr[c] - Lf[c][t] * ekr[t];
-#pragma unroll
-          for (int r = 0; r < 8; ++r) ci[c][r] = ci[c][r] - Lf[c][t] * ci[t][r];
-        }
-#pragma unroll
-      for (int r = 0; r < 8; ++r) {
-        const int i = 8 * w + r;
-        const double ok = mask01(i >= k + nb && i < S);   // 0 leaves the row bitwise unchanged
-        double gr = g[r], er = e[r];
-#pragma unroll
-        for (int c = 0; c < FB; ++c) {
-          const double m = ci[c][r] * invD[c] * ok * mask01(c < nb);
-          gr = gr - m * colj[c];
-          er = er - m * ekr[c];
-        }
-        g[r] = gr;
-        e[r] = er;
-      }
-      if (w == kb) {   // the block's rows are final up to their scales (applied after the loop)
-#pragma unroll
-        for (int a = 0; a < FB; ++a)
-          if (a < nb) {
-            e[r0 + a] = ekr[a];
-            piv[r0 + a] = D[a];
-          }
-      }
-    }
-  }
-#pragma unroll
-  for (int r = 0; r < 8; ++r) e[r] = e[r] * (1.0 / sqrt(piv[r]));
-  __syncthreads();   // every read of Gm (initial load) and of the exchange is done
-#pragma unroll
-  for (int r = 0; r < 8; ++r) {
-    const int i = 8 * w + r;
-    if (i < S && l < S) Gm[l * S + i] = e[r];   // W[j][i] = E[i][j]
-  }
-  __syncthreads();
-}
-
-// The same factor on ONE wave, no barrier per step (r2_factor_inverse exchanges every pivot column
-// across the 8 waves: publish -> barrier -> read, ~1.4k ticks per column).  Lane i holds row i in
-// place: R[j] = -E[i][j] for the columns already eliminated (j < k) and G[i][j] - delta_ij for the
-// rest.  With that storage the Gauss-Jordan step is ONE uniform formula over the whole row,
-// R_i[j] -= m_i R_k[j] with m_i = G_ik / G_kk: at j < k it is E_i -= m_i E_k (both negated), at
-// j > k G_i -= m_i G_k (the diagonal offset rides along), and at j = k it turns G_ik into -E_ik =
-// m_i because R_k[k] = G_kk - 1.  Per step lane k writes its row to LDS and every lane reads it
-// back (one wave's LDS traffic is in order, so no wait or barrier sits between the two).
-// Not inlined, and called by wave 0 only: inlined next to the kernel's other phases the 64-double
-// row did not fit beside their live values (spills in the step loop); as a callee only the
-// callee-saved registers go to scratch, once, in the one wave that calls it.
-template <int P16>
-__device__ __noinline__ void r2_factor_1w_body(lds_f64* Gm, lds_f64* xch, int p) {
-  constexpr int S = 16 * P16;
-  const int l = threadIdx.x & 63;
-  {
-    double R[S];
-    const int lr = l < S ? l : 0;
-#pragma unroll
-    for (int j = 0; j < S; ++j) R[j] = Gm[lr * S + j] - (l == j ? 1.0 : 0.0);
-    double piv = 1.0;
-    for (int k = 0; k < p; ++k) {
-      if (l == k) {
-#pragma unroll
-        for (int q = 0; q < S / 2; ++q)
-          if (2 * q < p) *(lds_dbl2*)(xch + 2 * q) = dbl2{R[2 * q], R[2 * q + 1]};
-      }
-      const double dk = xch[k] + 1.0;   // G_kk
-      const double bi = xch[lr];        // G_ki = G_ik
-      if (l == k) piv = dk;
-      if (l > k && l < p) {
-        const double m = bi / dk;
-        // 16 columns at a time: their reads, then their FMAs (the scheduler would otherwise hoist
-        // every read of the row and spill)
-#pragma unroll
-        for (int q0 = 0; q0 < S / 2; q0 += 8) {
-          if (2 * q0 >= p) break;   // uniform
-          dbl2 b[8];
-#pragma unroll
-          for (int q = 0; q < 8; ++q) b[q] = *(const lds_dbl2*)(xch + 2 * (q0 + q));
-#pragma unroll
-          for (int q = 0; q < 8; ++q) {
-            R[2 * (q0 + q)] = __builtin_fma(-m, b[q].x, R[2 * (q0 + q)]);
-            R[2 * (q0 + q) + 1] = __builtin_fma(-m, b[q].y, R[2 * (q0 + q) + 1]);
-          }
-          __builtin_amdgcn_sched_barrier(0);
-        }
-      }
-    }
-    // row l of E: -R[j] left of the diagonal, 1 on it, scaled by G_ll^-1/2 (rows past p: identity);
-    // W[j][l] = E[l][j]
-    const double sc = l < p ? 1.0 / sqrt(piv) : 1.0;
-#pragma unroll
-    for (int j = 0; j < S; ++j) {
-      const double v = (j < l && l < p) ? -R[j] : (j == l ? 1.0 : 0.0);
-      if (l < S) Gm[j * S + l] = v * sc;
-    }
-  }
-}
-
-template <int P16>
-__device__ __forceinline__ void r2_factor_inverse_1w(lds_f64* Gm, lds_f64* xch, int p) {
-  if ((threadIdx.x >> 6) == 0) r2_factor_1w_body<P16>(Gm, xch, p);
-  __syncthreads();
-}
-
 // ---- blocked factor (round 3): 16-column diagonal blocks on one wave, the rest on MFMA -----------
-// r2_factor_inverse pays one workgroup barrier and one cross-wave LDS round trip per pivot pair
-// (~1.4k ticks per column at p = 50).  Here the chain of p pivots runs inside ONE wave on 16 x 16
+// A Gauss-Jordan factor spread over the 8 waves (round 2) paid one workgroup barrier and one
+// cross-wave LDS round trip per pivot pair (~1.4k ticks per column at p = 50).  Here the chain of p pivots runs inside ONE wave on 16 x 16
 // diagonal blocks with lane shuffles only, and everything else is block algebra on the matrix cores
 // with three barriers per 16-column block:
 //   for K = 0 .. ceil(p/16) - 1 (E starts as the identity):
@@ -1086,12 +879,12 @@ __device__ __forceinline__ void r2_factor_inverse_1w(lds_f64* Gm, lds_f64* xch, 
 //     (b) C_IK = L_IK = G_IK F^T (I > K) and E_KJ <- F E_KJ (J < K; E_KK = F);
 //     (c) G_IJ -= C_IK C_JK^T (K < J <= I, the trailing Schur complement) and E_IJ -= C_IK E_KJ
 //         (I > K, J <= K); the wave that updates G_{K+1,K+1} goes straight on to (a) of K + 1.
-//   E = L^-1, and W = R^-1 = E^T as r2_factor_inverse leaves it.
+//   E = L^-1, and W = R^-1 = E^T.
 // Storage: G's trailing blocks are kept in Gm's UPPER triangle (G_IK read as G_KI^T, so every
 // operand read walks 16 consecutive doubles), C_IK in Gm's lower block (I, K) and E's lower blocks
 // (block-major, 256 doubles each) in the exchange area; both with the column XOR-swizzled by the
 // row (element (a, b) at column b ^ a), so the MFMA operand reads of a column are bank-conflict
-// free.  Columns past p are the identity (W = diag(W_p, I)), as in r2_factor_inverse.
+// free.  Columns past p are the identity (W = diag(W_p, I)).
 __device__ __forceinline__ double r3_shfl(double v, int src) {
   const long long b = __double_as_longlong(v);
   const int lo = __builtin_amdgcn_ds_bpermute(src << 2, (int)b);
@@ -1105,13 +898,11 @@ __device__ __forceinline__ double r3_readlane(double v, int lane) {
   return __longlong_as_double((long long)(unsigned)lo | ((long long)hi << 32));
 }
 __device__ __forceinline__ double r3_recip(double d) {
-#if RIPTRM_ST_RCP
-  double r = __builtin_amdgcn_rcp(d);   // v_rcp_f64 + two Newton steps
+  // v_rcp_f64 + two Newton steps (measured 37.9k vs 39.3k ticks per factor against IEEE division
+  // at (200, 50))
+  double r = __builtin_amdgcn_rcp(d);
   r = __builtin_fma(r, __builtin_fma(-d, r, 1.0), r);
   return __builtin_fma(r, __builtin_fma(-d, r, 1.0), r);
-#else
-  return 1.0 / d;
-#endif
 }
 __device__ __forceinline__ int r3_eb(int I, int J) { return (I * (I + 1) / 2 + J) * 256; }   // E block (I, J), J <= I
 
@@ -1423,16 +1214,8 @@ __device__ __forceinline__ void r2_apply(lds_f64* As, const lds_f64* Wt, int NR,
 
 // the second pass's exact factor (rare: only when Q1 is not orthonormal to 1e-10) as a call, so its
 // code does not sit inline in the kernel (the kernel is ~54 KB with it inlined)
-#ifndef RIPTRM_ST_FB_INLINE
-#define RIPTRM_ST_FB_INLINE 0
-#endif
 template <int P16>
-#if RIPTRM_ST_FB_INLINE
-__device__ __forceinline__
-#else
-__device__ __noinline__
-#endif
-void r3_factor_blocked_call(lds_f64* Gm, lds_f64* Ea, int p) {
+__device__ __noinline__ void r3_factor_blocked_call(lds_f64* Gm, lds_f64* Ea, int p) {
   r3_factor_blocked<P16>(Gm, Ea, p);
 }
 
@@ -1472,29 +1255,17 @@ __global__ void __launch_bounds__(T) k_st_retr2(int n, int p, int64_t stride, co
   ST_STAMP(1);
   r2_gram_any<P16>(As, Gm, red, NR, n, p);
   ST_STAMP(2);
-#if RIPTRM_ST_FACTOR == 1
-  r2_factor_inverse_1w<P16>(Gm, red, p);
-#elif RIPTRM_ST_FACTOR == 2
 #ifdef ST_STAMPS
   r3_factor_blocked<P16, true>(Gm, red, p);
 #else
   r3_factor_blocked<P16>(Gm, red, p);
-#endif
-#else
-  r2_factor_inverse<P16>(Gm, red, p);
 #endif
   ST_STAMP(3);
   r2_apply<P16, false>(As, Gm, NR, n, p, out + o);
   ST_STAMP(4);
   r2_gram_any<P16>(As, Gm, red, NR, n, p);
   ST_STAMP(5);
-#if RIPTRM_ST_FACTOR == 1
-  if (!r2_inverse_first_order<P16>(Gm, red, p)) r2_factor_inverse_1w<P16>(Gm, red, p);
-#elif RIPTRM_ST_FACTOR == 2
   if (!r2_inverse_first_order<P16>(Gm, red, p)) r3_factor_blocked_call<P16>(Gm, red, p);
-#else
-  if (!r2_inverse_first_order<P16>(Gm, red, p)) r2_factor_inverse<P16>(Gm, red, p);
-#endif
   ST_STAMP(6);
   r2_apply<P16, true>(As, Gm, NR, n, p, out + o);
   ST_STAMP(7);

@@ -71,7 +71,6 @@ int main(int argc, char** argv) {
     for (int g = 0; g < B; ++g) t[g] = s[g * 16 + np] - s[g * 16];
     std::sort(t.begin(), t.end());
     printf("], \"total_ticks_median\": %lld, \"total_ticks_max\": %lld", t[B / 2], t[B - 1]);
-#if RIPTRM_ST_FACTOR == 2
     if (which == 2) {   // blocked factor sub-phases (first factor): diag0, b0, G11+diag1 (wave 0), wait, b1, G22+diag2, rest
       printf(", \"factor1_sub_ticks_median\": [");
       for (int k = 8; k < 15; ++k) {
@@ -82,7 +81,6 @@ int main(int argc, char** argv) {
       }
       printf("]");
     }
-#endif
     printf("}\n");
   }
   return 0;
