@@ -6,23 +6,30 @@
 // the same matrix at every trial point is tested (RIPTRM.py:599-617).  No size cap there.
 //
 // Up to dim 96 the whole subproblem runs inside the state kernel on a matrix held in LDS
-// (riptrm_trs.h).  Beyond that the matrix lives in HBM, in caller-owned scratch bound with
-// riptrm_trs_bind_workspace, and the library serves the subproblem between lock-step chunks:
+// (riptrm_trs.h).  Beyond that the matrices live in HBM, in caller-owned scratch bound with
+// riptrm_trs_bind_workspace as `slots` slots of order `order`, and the library serves the
+// subproblems between lock-step chunks, every parked instance at once (up to `slots` per pass;
+// slot k is blockIdx.y of every launch and holds instance ids[k]):
 //   1. A: NonnegPCA's closed form in the Householder frame of x^perp (the one trs_direction uses:
 //      A = (H M H)[1:, 1:] + coef I, M = -S + diag(y / x), O(n^2) work): M densified from S,
 //      u = M w by a wave-per-row mat-vec, then the rank-two update in place;
 //   2. the interior candidate: SciPy's CG on A p = -a restated loop for loop (oracle
-//      trs_oracle.scipy_cg), one mat-vec launch + one single-workgroup update launch per
-//      iteration, the convergence flag polled every CG_POLL iterations;
-//   3. A = Q diag(lam) Q^T by rocSOLVER dsyevd (loaded with dlopen the first time it is needed);
+//      trs_oracle.scipy_cg).  Small orders: the whole CG in ONE launch, one workgroup per slot
+//      (k_cg_wg: p and q in LDS, x and r in registers, A streamed from L2 / MALL every iteration).
+//      Large orders: one grid-wide mat-vec launch + two single-workgroup launches per iteration for
+//      all slots together, the "every slot done" flag polled every CG_POLL iterations;
+//   3. A = Q diag(lam) Q^T by rocSOLVER dsyevd_strided_batched over the slots (loaded with dlopen
+//      the first time it is needed);
 //   4. g = Q^T a, then the hard case / safeguarded secular Newton / interior choice of
-//      riptrm_trs::trs_solve (the same formulas, one workgroup) and x = Q c;
+//      riptrm_trs::trs_solve (the same formulas, one workgroup per slot) and x = Q c;
 //   5. eta = H [0; x] back in the ambient space, the state machine resumes at PH_TRS_END.
 // The trial-point test (second_order_stationarity) builds the matrix at (x_new, y_new) the same
-// way and takes dsyevd's smallest eigenvalue (eigenvalues only).
+// way and takes dsyevd's smallest eigenvalue (eigenvalues only).  Every reduction has a fixed
+// order, and a slot's arithmetic does not depend on which other slots share its pass.
 #include <hip/hip_runtime.h>
 #include <dlfcn.h>
 #include <math.h>
+#include <algorithm>
 #include <cstdlib>
 #include <cstring>
 #include <string>
@@ -38,8 +45,10 @@ namespace riptrm_big {
 
 constexpr int WG = 512;        // single-workgroup kernels
 constexpr int GV = 256;        // mat-vec workgroups: 4 waves, one row per wave at a time
-constexpr int CG_POLL = 32;    // CG iterations enqueued between flag polls
+constexpr int CG_POLL = 32;    // CG iterations enqueued between flag polls (grid-wide CG)
 constexpr int NSC = 32;        // scalar slots per workspace slot
+constexpr int CG_WG_MAX = 2048;            // largest order of the one-workgroup CG (LDS p, q)
+constexpr int CG_RPT = CG_WG_MAX / WG;     // x / r elements per thread there
 
 // scalar slots
 enum Sc : int {
@@ -51,8 +60,21 @@ __host__ __device__ inline int64_t vpad(int64_t n) { return (n + 63) / 64 * 64; 
 constexpr int NVS = 12;        // vectors per slot
 enum Vs : int { VS_W = 0, VS_U, VS_A, VS_CGX, VS_R, VS_P, VS_Q, VS_EV, VS_EW, VS_G, VS_PE, VS_X };
 
-// one slot for matrices of order N: [N x N][NVS vectors of vpad(N)][NSC scalars][info]
-__host__ __device__ inline int64_t slot_doubles(int64_t N) { return N * N + NVS * vpad(N) + NSC + 8; }
+// one slot for matrices of order N: [N x N][NVS vectors of vpad(N)][NSC scalars]; after the slots:
+// int32 info[slots], ids[slots], flag[8], sweeps[slots] (+ pad), double residual[slots]
+__host__ __device__ inline int64_t slot_doubles(int64_t N) { return N * N + NVS * vpad(N) + NSC; }
+__host__ __device__ inline int64_t off_vec(int64_t N, int k) { return N * N + k * vpad(N); }
+__host__ __device__ inline int64_t off_sc(int64_t N) { return N * N + NVS * vpad(N); }
+inline int64_t tail_ints(int64_t slots) { return (3 * slots + 8 + 1) / 2 * 2; }   // even: the doubles stay aligned
+inline int64_t tail_bytes(int64_t slots) { return tail_ints(slots) * 4 + slots * 8; }
+
+// the slots of one pass: slot k (blockIdx.y) holds instance / subproblem ids[k]
+struct Bat {
+  double* base;
+  int64_t N, sd;        // order, doubles per slot
+  const int32_t* ids;
+  int32_t* infos;
+};
 
 struct Slot {
   double* M;
@@ -61,13 +83,13 @@ struct Slot {
   int32_t* info;
 };
 
-inline Slot slot_at(char* base, int64_t N, int s) {
+__host__ __device__ inline Slot slot_at(const Bat& B, int k) {
   Slot q;
-  double* b = (double*)base + (int64_t)s * slot_doubles(N);
+  double* b = B.base + (int64_t)k * B.sd;
   q.M = b;
-  for (int k = 0; k < NVS; ++k) q.v[k] = b + N * N + k * vpad(N);
-  q.sc = b + N * N + NVS * vpad(N);
-  q.info = (int32_t*)(q.sc + NSC);
+  for (int i = 0; i < NVS; ++i) q.v[i] = b + off_vec(B.N, i);
+  q.sc = b + off_sc(B.N);
+  q.info = B.infos + k;
   return q;
 }
 
@@ -80,16 +102,6 @@ __device__ __forceinline__ double blk_sum(double v, double* red) {
   double s = red[0];
 #pragma unroll
   for (int i = 1; i < WG / 64; ++i) s += red[i];
-  return s;
-}
-__device__ __forceinline__ double blk_min(double v, double* red) {
-  v = riptrm_wave::wave_min(v);
-  __syncthreads();
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
-  __syncthreads();
-  double s = red[0];
-#pragma unroll
-  for (int i = 1; i < WG / 64; ++i) s = fmin(s, red[i]);
   return s;
 }
 __device__ __forceinline__ double blk_max(double v, double* red) {
@@ -122,21 +134,25 @@ __device__ __forceinline__ const double* vec_of(const DevParams& P, int kind, in
   return P.vec + ((int64_t)kind * P.batch + b) * P.ld;
 }
 
-// M = -S + diag(y / x) at (X, Y) = vectors xk, yk of instance b (n x n, row-major, lda n)
-__global__ void __launch_bounds__(256) k_dense(DevParams P, int b, int xk, int yk, double* M) {
+// M = -S + diag(y / x) at (X, Y) = vectors xk, yk of instance ids[k] (n x n, row-major, lda n)
+__global__ void __launch_bounds__(256) k_dense(DevParams P, Bat B, int xk, int yk) {
+  const int k = blockIdx.y, b = B.ids[k];
   const int n = P.n;
   const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (e >= (int64_t)n * n) return;
   const int i = (int)(e / n), j = (int)(e - (int64_t)i * n);
   double m = -s_at(P, b, i, j);
   if (i == j) m += vec_of(P, yk, b)[i] / vec_of(P, xk, b)[i];
-  M[e] = m;
+  slot_at(B, k).M[e] = m;
 }
 
 // w = x + sign(x_0) ||x|| e_0, tau = 2 / w^T w (the Householder reflector of trs_direction);
-// xx = x^T x; trial mode (coef < 0 flag): also y^T x for the coefficient
-__global__ void __launch_bounds__(WG) k_house(DevParams P, int b, int xk, int yk, double* w, double* sc) {
+// xx = x^T x; y^T x for the trial coefficient
+__global__ void __launch_bounds__(WG) k_house(DevParams P, Bat B, int xk, int yk) {
   __shared__ double red[WG / 64];
+  const int k = blockIdx.y, b = B.ids[k];
+  const Slot q = slot_at(B, k);
+  double* w = q.v[VS_W];
   const int n = P.n;
   const double* X = vec_of(P, xk, b);
   const double* Y = vec_of(P, yk, b);
@@ -156,43 +172,69 @@ __global__ void __launch_bounds__(WG) k_house(DevParams P, int b, int xk, int yk
   }
   ww = blk_sum(ww, red);
   if (threadIdx.x == 0) {
-    sc[SC_TAU] = 2.0 / ww;
-    sc[SC_XX] = xx;
-    sc[SC_YX] = yx;
+    q.sc[SC_TAU] = 2.0 / ww;
+    q.sc[SC_XX] = xx;
+    q.sc[SC_YX] = yx;
   }
 }
 
-// out_i = sum_j A[i lda + j] v_j for i < rows (one wave per row, lanes over j; fixed order:
-// lane partial sums in j order, then the wave tree).  skip: if non-null and *skip != 0, nothing.
-__global__ void __launch_bounds__(GV) k_gemv(const double* A, int64_t lda, int rows, int cols, const double* v,
-                                             double* out, const double* skip) {
-  if (skip && *skip != 0.0) return;
+// out_i = sum_j A[i lda + j] v_j for i < rows, per slot: A, v, out, skip at slot offsets (doubles
+// from the slot start; skip < 0: none).  One wave per row, lanes over j; fixed order: lane partial
+// sums in j order, then the wave tree.  If *skip != 0 the slot is left alone.
+__global__ void __launch_bounds__(GV) k_gemv(Bat B, int64_t aoff, int64_t lda, int rows, int cols, int64_t voff,
+                                             int64_t ooff, int64_t skipoff) {
+  double* base = B.base + (int64_t)blockIdx.y * B.sd;
+  if (skipoff >= 0 && base[skipoff] != 0.0) return;
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * (GV / 64) + (threadIdx.x >> 6);
   if (row >= rows) return;
-  const double* a = A + (int64_t)row * lda;
+  const double* a = base + aoff + (int64_t)row * lda;
+  const double* v = base + voff;
   double s = 0.0;
   for (int j = lane; j < cols; j += 64) s += a[j] * v[j];
   s = riptrm_wave::wave_sum(s);
-  if (lane == 0) out[row] = s;
+  if (lane == 0) base[ooff + row] = s;
+}
+
+// out = M x_new of instance ids[k] (the trial coefficient's x^T S x), the k_gemv arithmetic
+__global__ void __launch_bounds__(GV) k_gemv_x(DevParams P, Bat B, int xk) {
+  const int k = blockIdx.y, b = B.ids[k];
+  const Slot q = slot_at(B, k);
+  const int n = P.n;
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * (GV / 64) + (threadIdx.x >> 6);
+  if (row >= n) return;
+  const double* a = q.M + (int64_t)row * n;
+  const double* v = vec_of(P, xk, b);
+  double s = 0.0;
+  for (int j = lane; j < n; j += 64) s += a[j] * v[j];
+  s = riptrm_wave::wave_sum(s);
+  if (lane == 0) q.v[VS_Q][row] = s;
 }
 
 // out_i = sum_k A[k lda + i] v_k (columns of the row-major view: eigenvectors are rows of it);
 // rows split over workgroups, each thread one i, k in order
-__global__ void __launch_bounds__(256) k_gemv_t(const double* A, int64_t lda, int rows, int cols, const double* v,
-                                                double* out) {
+__global__ void __launch_bounds__(256) k_gemv_t(Bat B, int64_t aoff, int64_t lda, int rows, int cols, int64_t voff,
+                                                int64_t ooff) {
+  double* base = B.base + (int64_t)blockIdx.y * B.sd;
   const int i = blockIdx.x * 256 + threadIdx.x;
   if (i >= cols) return;
+  const double* A = base + aoff;
+  const double* v = base + voff;
   double s = 0.0;
   for (int k = 0; k < rows; ++k) s += A[(int64_t)k * lda + i] * v[k];
-  out[i] = s;
+  base[ooff + i] = s;
 }
 
 // gam = w^T u, then (iterate) a_k = c_k - tau w_k (w^T c) for k >= 1 and coef from the state,
 // or (trial) coef = (x^T S x + y^T x) x^T x with x^T S x = -x^T (M x) + y^T x (M = -S + diag(y/x))
-__global__ void __launch_bounds__(WG) k_repmat_vec(DevParams P, int b, int xk, int ck, const double* w, const double* u,
-                                                   const double* mx, double* a, double* sc, int trial) {
+__global__ void __launch_bounds__(WG) k_repmat_vec(DevParams P, Bat B, int xk, int ck, int trial) {
   __shared__ double red[WG / 64];
+  const int k = blockIdx.y, b = B.ids[k];
+  const Slot q = slot_at(B, k);
+  const double *w = q.v[VS_W], *u = q.v[VS_U], *mx = q.v[VS_Q];
+  double* a = q.v[VS_A];
+  double* sc = q.sc;
   const int n = P.n;
   double gam = 0.0, wc = 0.0, xmx = 0.0;
   const double* Cv = ck >= 0 ? vec_of(P, ck, b) : nullptr;
@@ -207,7 +249,7 @@ __global__ void __launch_bounds__(WG) k_repmat_vec(DevParams P, int b, int xk, i
   xmx = blk_sum(xmx, red);
   const double tau = sc[SC_TAU];
   if (Cv)
-    for (int k = threadIdx.x + 1; k < n; k += WG) a[k - 1] = Cv[k] - tau * w[k] * wc;
+    for (int i = threadIdx.x + 1; i < n; i += WG) a[i - 1] = Cv[i] - tau * w[i] * wc;
   if (threadIdx.x == 0) {
     sc[SC_GAM] = gam;
     sc[SC_WC] = wc;
@@ -223,7 +265,10 @@ __global__ void __launch_bounds__(WG) k_repmat_vec(DevParams P, int b, int xk, i
 
 // in place, rows / columns 1.. of M: A = M - tau (w u^T + u w^T) + tau^2 gam w w^T + coef I
 // (repmat's arithmetic, element for element)
-__global__ void __launch_bounds__(256) k_transform(int n, double* M, const double* w, const double* u, const double* sc) {
+__global__ void __launch_bounds__(256) k_transform(int n, Bat B) {
+  const Slot q = slot_at(B, blockIdx.y);
+  const double *w = q.v[VS_W], *u = q.v[VS_U], *sc = q.sc;
+  double* M = q.M;
   const int m = n - 1;
   const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (e >= (int64_t)m * m) return;
@@ -236,17 +281,161 @@ __global__ void __launch_bounds__(256) k_transform(int n, double* M, const doubl
 }
 
 // ---- SciPy CG on A p = -a (trs_oracle.scipy_cg; riptrm_trs::trs_solve's loop) ------------------
-__global__ void __launch_bounds__(WG) k_cg_init(int m, const double* a, double* cgx, double* r, double* sc) {
+// The one-workgroup form and the grid-wide form below do the same arithmetic in the same order
+// (sums over i = t, t + WG, ... then the workgroup tree; mat-vec rows as k_gemv).
+
+// ||A p1 + a|| / ||a|| < 1e-5 and p1^T p1 < Delta^2 (RIPTRM.py:246-251); p1's model value.
+// Thread t's terms are elements t, t + WG, ...
+__device__ __forceinline__ void cg_final_terms(double* red, double* sc, double an, double D, double v0, double v1,
+                                               double v2, double v3) {
+  v0 = blk_sum(v0, red);
+  v1 = blk_sum(v1, red);
+  v2 = blk_sum(v2, red);
+  v3 = blk_sum(v3, red);
+  if (threadIdx.x == 0) {
+    sc[SC_CG_OK] = (an != 0.0 && sqrt(v0) / an < 1e-5 && v1 < D * D) ? 1.0 : 0.0;
+    sc[SC_P1OBJ] = 0.5 * v2 + v3;
+    sc[SC_DELTA] = D;
+  }
+}
+
+// q[row] = A[row] . v over rows m, 8 waves, FOUR rows at a time per wave (independent chains;
+// each row's own sum in k_gemv's order)
+__device__ __forceinline__ void wg_matvec(const double* __restrict__ A, int64_t lda, int m, const double* v,
+                                          double* out) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  for (int r0 = 4 * w; r0 < m; r0 += 4 * (WG / 64)) {
+    double s[4] = {0.0, 0.0, 0.0, 0.0};
+    const double* a0 = A + (int64_t)r0 * lda;
+    for (int j = lane; j < m; j += 64) {
+      const double vj = v[j];
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (r0 + u < m) s[u] += a0[(int64_t)u * lda + j] * vj;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const double t = riptrm_wave::wave_sum(s[u]);
+      if (lane == 0 && r0 + u < m) out[r0 + u] = t;
+    }
+  }
+}
+
+// The whole CG (init, iterations, final test) for slot blockIdx.y, order m <= CG_WG_MAX; A at slot
+// offset aoff with leading dimension lda; Delta of the slot at D[ids[k] * dstride]
+__global__ void __launch_bounds__(WG) k_cg_wg(Bat B, int m, int64_t aoff, int64_t lda, const double* D,
+                                              int64_t dstride) {
   __shared__ double red[WG / 64];
+  __shared__ double ps[CG_WG_MAX], qs[CG_WG_MAX];
+  const int k = blockIdx.y;
+  const Slot q = slot_at(B, k);
+  const double* A = q.M + aoff;
+  const double* a = q.v[VS_A];
+  const int t = threadIdx.x;
+  double x[CG_RPT], r[CG_RPT];
+  double an = 0.0;
+#pragma unroll
+  for (int u = 0; u < CG_RPT; ++u) {
+    const int i = t + u * WG;
+    const double bi = i < m ? -a[i] : 0.0;
+    x[u] = 0.0;
+    r[u] = bi;
+    an += bi * bi;
+  }
+  an = sqrt(blk_sum(an, red));
+  const double atol = 1e-5 * an;
+  double done = an == 0.0 ? 2.0 : 0.0, it = 0.0, rho_prev = 1.0;
+  while (done == 0.0) {   // uniform: every thread holds the same scalars
+    if (it >= 10.0 * m) {
+      done = 3.0;
+      break;
+    }
+    double rr = 0.0;
+#pragma unroll
+    for (int u = 0; u < CG_RPT; ++u) rr += r[u] * r[u];   // zero past m
+    rr = blk_sum(rr, red);
+    if (sqrt(rr) < atol) {
+      done = 1.0;
+      break;
+    }
+    const double rho = rr;
+    const double beta = it > 0.0 ? rho / rho_prev : 0.0;
+#pragma unroll
+    for (int u = 0; u < CG_RPT; ++u) {
+      const int i = t + u * WG;
+      if (i < m) ps[i] = it > 0.0 ? ps[i] * beta + r[u] : r[u];
+    }
+    __syncthreads();
+    wg_matvec(A, lda, m, ps, qs);
+    __syncthreads();
+    double pq = 0.0;
+#pragma unroll
+    for (int u = 0; u < CG_RPT; ++u) {
+      const int i = t + u * WG;
+      if (i < m) pq += ps[i] * qs[i];
+    }
+    pq = blk_sum(pq, red);
+    const double alpha = rho / pq;
+#pragma unroll
+    for (int u = 0; u < CG_RPT; ++u) {
+      const int i = t + u * WG;
+      if (i < m) {
+        x[u] += alpha * ps[i];
+        r[u] -= alpha * qs[i];
+      }
+    }
+    rho_prev = rho;
+    it += 1.0;
+  }
+  // the final test needs A x: x through LDS
+  __syncthreads();
+#pragma unroll
+  for (int u = 0; u < CG_RPT; ++u) {
+    const int i = t + u * WG;
+    if (i < m) {
+      ps[i] = x[u];
+      q.v[VS_CGX][i] = x[u];
+    }
+  }
+  __syncthreads();
+  wg_matvec(A, lda, m, ps, qs);
+  __syncthreads();
+  double v0 = 0.0, v1 = 0.0, v2 = 0.0, v3 = 0.0;
+#pragma unroll
+  for (int u = 0; u < CG_RPT; ++u) {
+    const int i = t + u * WG;
+    if (i < m) {
+      const double res = qs[i] + a[i];
+      v0 += res * res;
+      v1 += x[u] * x[u];
+      v2 += x[u] * qs[i];
+      v3 += a[i] * x[u];
+    }
+  }
+  if (t == 0) {
+    q.sc[SC_AN] = an;
+    q.sc[SC_ATOL] = atol;
+    q.sc[SC_IT] = it;
+    q.sc[SC_DONE] = done;
+  }
+  cg_final_terms(red, q.sc, an, D[(int64_t)B.ids[k] * dstride], v0, v1, v2, v3);
+}
+
+// grid-wide CG, one launch each step for all slots (grid.y = slot)
+__global__ void __launch_bounds__(WG) k_cg_init(Bat B, int m) {
+  __shared__ double red[WG / 64];
+  const Slot q = slot_at(B, blockIdx.y);
+  const double* a = q.v[VS_A];
   double an = 0.0;
   for (int i = threadIdx.x; i < m; i += WG) {
     const double bi = -a[i];
-    cgx[i] = 0.0;
-    r[i] = bi;
+    q.v[VS_CGX][i] = 0.0;
+    q.v[VS_R][i] = bi;
     an += bi * bi;
   }
   an = sqrt(blk_sum(an, red));
   if (threadIdx.x == 0) {
+    double* sc = q.sc;
     sc[SC_AN] = an;
     sc[SC_ATOL] = 1e-5 * an;
     sc[SC_IT] = 0.0;
@@ -256,8 +445,12 @@ __global__ void __launch_bounds__(WG) k_cg_init(int m, const double* a, double* 
 }
 
 // top of a CG iteration: the convergence test, then the direction
-__global__ void __launch_bounds__(WG) k_cg_dir(int m, const double* r, double* p, double* sc) {
+__global__ void __launch_bounds__(WG) k_cg_dir(Bat B, int m) {
   __shared__ double red[WG / 64];
+  const Slot q = slot_at(B, blockIdx.y);
+  double* sc = q.sc;
+  const double *r = q.v[VS_R];
+  double* p = q.v[VS_P];
   if (sc[SC_DONE] != 0.0) return;
   const double it = sc[SC_IT];
   if (it >= 10.0 * m) {   // maxiter = 10 n
@@ -277,17 +470,20 @@ __global__ void __launch_bounds__(WG) k_cg_dir(int m, const double* r, double* p
   if (threadIdx.x == 0) sc[SC_RHO] = rho;
 }
 
-__global__ void __launch_bounds__(WG) k_cg_upd(int m, const double* p, const double* q, double* cgx, double* r,
-                                               double* sc) {
+__global__ void __launch_bounds__(WG) k_cg_upd(Bat B, int m) {
   __shared__ double red[WG / 64];
+  const Slot q = slot_at(B, blockIdx.y);
+  double* sc = q.sc;
+  const double *p = q.v[VS_P], *qv = q.v[VS_Q];
+  double *cgx = q.v[VS_CGX], *r = q.v[VS_R];
   if (sc[SC_DONE] != 0.0) return;
   double pq = 0.0;
-  for (int i = threadIdx.x; i < m; i += WG) pq += p[i] * q[i];
+  for (int i = threadIdx.x; i < m; i += WG) pq += p[i] * qv[i];
   pq = blk_sum(pq, red);
   const double alpha = sc[SC_RHO] / pq;
   for (int i = threadIdx.x; i < m; i += WG) {
     cgx[i] += alpha * p[i];
-    r[i] -= alpha * q[i];
+    r[i] -= alpha * qv[i];
   }
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -296,37 +492,39 @@ __global__ void __launch_bounds__(WG) k_cg_upd(int m, const double* p, const dou
   }
 }
 
-// ||A p1 + a|| / ||a|| < 1e-5 and p1^T p1 < Delta^2 (RIPTRM.py:246-251); p1's model value
-__global__ void __launch_bounds__(WG) k_cg_final(int m, const double* a, const double* cgx, const double* q,
-                                                 const double* Delta, double* sc) {
+// flag[0] = 1 when every slot of the pass has left the CG loop
+__global__ void k_cg_alldone(Bat B, int cnt, int32_t* flag) {
+  if (threadIdx.x != 0) return;
+  int all = 1;
+  for (int k = 0; k < cnt; ++k) all &= slot_at(B, k).sc[SC_DONE] != 0.0;
+  flag[0] = all;
+}
+
+__global__ void __launch_bounds__(WG) k_cg_final(Bat B, int m, const double* D, int64_t dstride) {
   __shared__ double red[WG / 64];
+  const int k = blockIdx.y;
+  const Slot q = slot_at(B, k);
+  const double *a = q.v[VS_A], *cgx = q.v[VS_CGX], *qv = q.v[VS_Q];
   double v0 = 0.0, v1 = 0.0, v2 = 0.0, v3 = 0.0;
   for (int i = threadIdx.x; i < m; i += WG) {
-    const double res = q[i] + a[i];
+    const double res = qv[i] + a[i];
     v0 += res * res;
     v1 += cgx[i] * cgx[i];
-    v2 += cgx[i] * q[i];
+    v2 += cgx[i] * qv[i];
     v3 += a[i] * cgx[i];
   }
-  v0 = blk_sum(v0, red);
-  v1 = blk_sum(v1, red);
-  v2 = blk_sum(v2, red);
-  v3 = blk_sum(v3, red);
-  if (threadIdx.x == 0) {
-    const double an = sc[SC_AN];
-    const double D = *Delta;
-    sc[SC_CG_OK] = (an != 0.0 && sqrt(v0) / an < 1e-5 && v1 < D * D) ? 1.0 : 0.0;
-    sc[SC_P1OBJ] = 0.5 * v2 + v3;
-    sc[SC_DELTA] = D;
-  }
+  cg_final_terms(red, q.sc, q.sc[SC_AN], D[(int64_t)B.ids[k] * dstride], v0, v1, v2, v3);
 }
 
 // After dsyevd (ev ascending) and g = Q^T a: the hard case / secular Newton / interior choice of
 // riptrm_trs::trs_solve; writes the eigen coordinates pe of the boundary / hard-case candidate and
 // the result scalars
-__global__ void __launch_bounds__(WG) k_secular(int m, const double* ev, const double* g, double* pe, double tolhc,
-                                                double* sc) {
+__global__ void __launch_bounds__(WG) k_secular(Bat B, int m, double tolhc) {
   __shared__ double red[WG / 64];
+  const Slot q = slot_at(B, blockIdx.y);
+  const double *ev = q.v[VS_EV], *g = q.v[VS_G];
+  double* pe = q.v[VS_PE];
+  double* sc = q.sc;
   const double Delta = sc[SC_DELTA];
   const double D2 = Delta * Delta;
   const double lmin = ev[0];   // ascending: the lowest index of the minimum
@@ -418,59 +616,70 @@ __global__ void __launch_bounds__(WG) k_secular(int m, const double* ev, const d
 }
 
 // x <- cgx when the interior candidate won (x = Q pe was computed before)
-__global__ void __launch_bounds__(256) k_pick(int m, const double* cgx, double* x, const double* sc) {
+__global__ void __launch_bounds__(256) k_pick(Bat B, int m) {
+  const Slot q = slot_at(B, blockIdx.y);
   const int i = blockIdx.x * 256 + threadIdx.x;
-  if (i < m && sc[SC_INTERIOR] != 0.0) x[i] = cgx[i];
+  if (i < m && q.sc[SC_INTERIOR] != 0.0) q.v[VS_X][i] = q.v[VS_CGX][i];
 }
 
 // eta = H [0; x] (RIPTRM.py:442-444 in the Householder frame), the direction type, j = -1, and the
 // instance resumes at PH_TRS_END
-__global__ void __launch_bounds__(WG) k_finish_dir(DevParams P, int b, const double* w, const double* x, const double* sc,
-                                                   const int32_t* info) {
+__global__ void __launch_bounds__(WG) k_finish_dir(DevParams P, Bat B) {
   __shared__ double red[WG / 64];
+  const int k = blockIdx.y, b = B.ids[k];
+  const Slot q = slot_at(B, k);
+  const double *w = q.v[VS_W], *x = q.v[VS_X];
   const int n = P.n;
   double wz = 0.0;
-  for (int k = threadIdx.x + 1; k < n; k += WG) wz += w[k] * x[k - 1];
+  for (int i = threadIdx.x + 1; i < n; i += WG) wz += w[i] * x[i - 1];
   wz = blk_sum(wz, red);
-  const double tau = sc[SC_TAU];
+  const double tau = q.sc[SC_TAU];
   double* E = P.vec + ((int64_t)V_ETA * P.batch + b) * P.ld;
   for (int i = threadIdx.x; i < n; i += WG) E[i] = (i == 0 ? 0.0 : x[i - 1]) - tau * w[i] * wz;
   if (threadIdx.x == 0) {
     double* s = P.st + (int64_t)b * ST_N;
     // dsyevd did not converge (info > 0): scipy.linalg.eig would raise LinAlgError inside
     // outer_step (RIPTRM.py:961-966); the machine stops the instance at PH_TRS_END
-    s[ST_TCG_STOP] = *info != 0 ? (double)RIPTRM_TCG_EIGFAIL : RIPTRM_TRS_BOUNDARY + sc[SC_KIND];
+    s[ST_TCG_STOP] = *q.info != 0 ? (double)RIPTRM_TCG_EIGFAIL : RIPTRM_TRS_BOUNDARY + q.sc[SC_KIND];
     s[ST_J] = -1.0;
     s[ST_PHASE] = PH_TRS_END;
   }
 }
 
-__global__ void k_finish_mineig(DevParams P, int b, const double* ev, const int32_t* info) {
-  double* s = P.st + (int64_t)b * ST_N;
-  s[ST_MINEIG] = *info != 0 ? NAN : ev[0];   // non-converged dsyevd: the machine stops the instance
+__global__ void k_finish_mineig(DevParams P, Bat B, int cnt) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= cnt) return;
+  const Slot q = slot_at(B, k);
+  double* s = P.st + (int64_t)B.ids[k] * ST_N;
+  s[ST_MINEIG] = *q.info != 0 ? NAN : q.v[VS_EV][0];   // non-converged dsyevd: the machine stops the instance
   s[ST_PHASE] = PH_MINEIG_END;
 }
 
-// riptrm_trs_gep outputs for one subproblem
-__global__ void __launch_bounds__(256) k_gep_out(int m, const double* x, const double* sc, const double* ev, double* xo,
-                                                 double* lam1, int32_t* kind, double* mineig) {
+// riptrm_trs_gep outputs of slot blockIdx.y (subproblem ids[k])
+__global__ void __launch_bounds__(256) k_gep_out(Bat B, int m, int64_t ldv, double* xo, double* lam1, int32_t* kind,
+                                                 double* mineig) {
+  const int k = blockIdx.y, b = B.ids[k];
+  const Slot q = slot_at(B, k);
   const int i = blockIdx.x * 256 + threadIdx.x;
-  if (i < m) xo[i] = x[i];
+  if (i < m) xo[(int64_t)b * ldv + i] = q.v[VS_X][i];
   if (i == 0) {
-    *lam1 = sc[SC_LAM1];
-    *kind = RIPTRM_TRS_BOUNDARY + (int32_t)sc[SC_KIND];
-    if (mineig) *mineig = ev[0];
+    lam1[b] = q.sc[SC_LAM1];
+    kind[b] = RIPTRM_TRS_BOUNDARY + (int32_t)q.sc[SC_KIND];
+    if (mineig) mineig[b] = q.v[VS_EV][0];
   }
 }
 
-// copy an m x m block (row-major, lda) into the slot's matrix (lda m) and a into the slot
-__global__ void __launch_bounds__(256) k_load(int m, const double* A, int64_t lda, const double* a, double* M, double* av) {
+// copy subproblem ids[k]'s m x m block (row-major, lda) into slot k's matrix (lda m) and a
+__global__ void __launch_bounds__(256) k_load(Bat B, int m, const double* A, int64_t lda, int64_t a_stride,
+                                              const double* a, int64_t ldv) {
+  const int k = blockIdx.y, b = B.ids[k];
+  const Slot q = slot_at(B, k);
   const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (e < (int64_t)m * m) {
     const int i = (int)(e / m), j = (int)(e - (int64_t)i * m);
-    M[e] = A[(int64_t)i * lda + j];
+    q.M[e] = A[(int64_t)b * a_stride + (int64_t)i * lda + j];
   }
-  if (e < m) av[e] = a[e];
+  if (e < m) q.v[VS_A][e] = a[(int64_t)b * ldv + e];
 }
 
 // ---- rocSOLVER, loaded on first use (no link-time dependency of the library) -----------------------
@@ -479,8 +688,11 @@ __global__ void __launch_bounds__(256) k_load(int m, const double* A, int64_t ld
 typedef int (*fn_create_t)(void**);
 typedef int (*fn_set_stream_t)(void*, hipStream_t);
 typedef int (*fn_destroy_t)(void*);
-typedef int (*fn_syevd_t)(void*, int, int, int, double*, int, double*, double*, int*);
-constexpr int EVECT_ORIGINAL = 211, EVECT_NONE = 213, FILL_UPPER = 121;
+typedef int (*fn_syevd_sb_t)(void*, int, int, int, double*, int, int64_t, double*, int64_t, double*, int64_t, int*, int);
+typedef int (*fn_syevj_sb_t)(void*, int, int, int, int, double*, int, int64_t, double, double*, int, int*, double*, int64_t,
+                             int*, int);
+typedef int (*fn_syevdj_sb_t)(void*, int, int, int, double*, int, int64_t, double*, int64_t, int*, int);
+constexpr int EVECT_ORIGINAL = 211, EVECT_NONE = 213, FILL_UPPER = 121, ESORT_ASCENDING = 252;
 
 struct Solver {
   bool tried = false, ok = false;
@@ -488,7 +700,9 @@ struct Solver {
   fn_create_t create = nullptr;
   fn_set_stream_t set_stream = nullptr;
   fn_destroy_t destroy = nullptr;
-  fn_syevd_t syevd = nullptr;
+  fn_syevd_sb_t syevd_sb = nullptr;
+  fn_syevj_sb_t syevj_sb = nullptr;     // A/B only (RIPTRM_BIG_EIG)
+  fn_syevdj_sb_t syevdj_sb = nullptr;
 };
 
 static Solver& solver() {
@@ -516,9 +730,12 @@ static Solver& solver() {
   s.create = (fn_create_t)dlsym(blas, "rocblas_create_handle");
   s.set_stream = (fn_set_stream_t)dlsym(blas, "rocblas_set_stream");
   s.destroy = (fn_destroy_t)dlsym(blas, "rocblas_destroy_handle");
-  s.syevd = (fn_syevd_t)dlsym(sol, "rocsolver_dsyevd");
-  s.ok = s.create && s.set_stream && s.destroy && s.syevd;
-  if (!s.ok) s.why = "rocBLAS / rocSOLVER lack rocblas_create_handle / rocblas_set_stream / rocsolver_dsyevd";
+  s.syevd_sb = (fn_syevd_sb_t)dlsym(sol, "rocsolver_dsyevd_strided_batched");
+  s.syevj_sb = (fn_syevj_sb_t)dlsym(sol, "rocsolver_dsyevj_strided_batched");
+  s.syevdj_sb = (fn_syevdj_sb_t)dlsym(sol, "rocsolver_dsyevdj_strided_batched");
+  s.ok = s.create && s.set_stream && s.destroy && s.syevd_sb;
+  if (!s.ok)
+    s.why = "rocBLAS / rocSOLVER lack rocblas_create_handle / rocblas_set_stream / rocsolver_dsyevd_strided_batched";
   return s;
 }
 
@@ -548,68 +765,133 @@ void riptrm_big_release(riptrm_ctx* c) {
   }
 }
 
-// The subproblem min x^T A x / 2 + a^T x s.t. ||x|| <= Delta on the slot: A = q.M + off with leading
-// dimension lda (m x m), a = q.v[VS_A].  CG (interior candidate), dsyevd, secular solve; the
-// solution lands in q.v[VS_X], the scalars in q.sc.  A is destroyed (eigenvectors).
-static int big_solve(riptrm_ctx* c, Slot& q, double* A, int lda, int m, const double* Delta_dev, double tolhc) {
-  hipStream_t st = c->stream;
-  double* a = q.v[VS_A];
-  hipLaunchKernelGGL(k_cg_init, dim3(1), dim3(WG), 0, st, m, a, q.v[VS_CGX], q.v[VS_R], q.sc);
-  HIPCHK(c, hipGetLastError());
-  double done = 0.0;
-  for (int it = 0; it < 10 * m + 1; it += CG_POLL) {
-    for (int k = 0; k < CG_POLL; ++k) {
-      hipLaunchKernelGGL(k_cg_dir, dim3(1), dim3(WG), 0, st, m, q.v[VS_R], q.v[VS_P], q.sc);
-      hipLaunchKernelGGL(k_gemv, dim3(blocks_of(m, GV / 64)), dim3(GV), 0, st, A, (int64_t)lda, m, m, q.v[VS_P],
-                         q.v[VS_Q], q.sc + SC_DONE);
-      hipLaunchKernelGGL(k_cg_upd, dim3(1), dim3(WG), 0, st, m, q.v[VS_P], q.v[VS_Q], q.v[VS_CGX], q.v[VS_R], q.sc);
-    }
-    HIPCHK(c, hipGetLastError());
-    HIPCHK(c, hipMemcpyAsync(&done, q.sc + SC_DONE, sizeof(double), hipMemcpyDeviceToHost, st));
-    HIPCHK(c, hipStreamSynchronize(st));
-    if (done != 0.0) break;
-  }
-  hipLaunchKernelGGL(k_gemv, dim3(blocks_of(m, GV / 64)), dim3(GV), 0, st, A, (int64_t)lda, m, m, q.v[VS_CGX],
-                     q.v[VS_Q], nullptr);
-  hipLaunchKernelGGL(k_cg_final, dim3(1), dim3(WG), 0, st, m, a, q.v[VS_CGX], q.v[VS_Q], Delta_dev, q.sc);
-  HIPCHK(c, hipGetLastError());
+// the workspace's pass descriptor and its id / flag arrays (after the slots)
+static Bat bat_of(riptrm_ctx* c) {
+  const int64_t N = c->big_order, sd = slot_doubles(N);
+  double* base = (double*)c->big_ws;
+  int32_t* tail = (int32_t*)(base + sd * c->big_slots);
+  return Bat{base, N, sd, tail + c->big_slots, tail};
+}
+static int32_t* tail_of(riptrm_ctx* c) { return (int32_t*)((double*)c->big_ws + slot_doubles(c->big_order) * c->big_slots); }
+static int32_t* flag_of(riptrm_ctx* c) { return tail_of(c) + 2 * c->big_slots; }
+
+// A = Q diag(lam) Q^T for the pass's cnt slots (A at slot offset aoff, lda; eigenvalues ascending into
+// VS_EV, eigenvectors over A when vectors): rocSOLVER dsyevd (default) or, for A/B measurements
+// (RIPTRM_BIG_EIG=j / dj), its Jacobi dsyevj / dsyevdj
+static int eig_batched(riptrm_ctx* c, const Bat& B, int cnt, bool vectors, int m, int64_t aoff, int lda) {
   if (int rc = big_handle(c)) return rc;
-  if (solver().syevd(c->big_handle, EVECT_ORIGINAL, FILL_UPPER, m, A, lda, q.v[VS_EV], q.v[VS_EW], q.info) != 0)
-    return fail(c, RIPTRM_E_HIP, "rocsolver_dsyevd failed");
+  Solver& s = solver();
+  const int ev = vectors ? EVECT_ORIGINAL : EVECT_NONE;
+  double* A = B.base + aoff;
+  double* W = B.base + off_vec(B.N, VS_EV);
+  const char* e = getenv("RIPTRM_BIG_EIG");
+  int st;
+  if (e && e[0] == 'j' && s.syevj_sb) {
+    int32_t* sweeps = tail_of(c) + 2 * c->big_slots + 8;
+    double* resid = (double*)(tail_of(c) + tail_ints(c->big_slots));
+    st = s.syevj_sb(c->big_handle, ESORT_ASCENDING, ev, FILL_UPPER, m, A, lda, B.sd, 0.0, resid, 100, sweeps, W, B.sd,
+                    B.infos, cnt);
+  } else if (e && e[0] == 'd' && e[1] == 'j' && s.syevdj_sb) {
+    st = s.syevdj_sb(c->big_handle, ev, FILL_UPPER, m, A, lda, B.sd, W, B.sd, B.infos, cnt);
+  } else {
+    st = s.syevd_sb(c->big_handle, ev, FILL_UPPER, m, A, lda, B.sd, W, B.sd, B.base + off_vec(B.N, VS_EW), B.sd, B.infos,
+                    cnt);
+  }
+  if (st != 0) return fail(c, RIPTRM_E_HIP, "rocsolver batched symmetric eigensolver failed (status " + std::to_string(st) + ")");
+  return RIPTRM_OK;
+}
+
+// this pass's ids -> the workspace (stream-ordered after the previous pass; synchronises)
+static int put_ids(riptrm_ctx* c, const Bat& B, const int32_t* ids, int cnt) {
+  HIPCHK(c, hipMemcpyAsync(const_cast<int32_t*>(B.ids), ids, (size_t)cnt * sizeof(int32_t), hipMemcpyHostToDevice,
+                           c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return RIPTRM_OK;
+}
+
+// the one-workgroup CG when its per-iteration time (A streamed by one CU, ~60 GB/s, or a ~3 us
+// latency floor) beats the grid-wide form's (3 launches ~12 us + the pass's matrices at ~5 TB/s)
+static bool cg_one_workgroup(int m, int cnt) {
+  if (m > CG_WG_MAX) return false;
+  const char* e = getenv("RIPTRM_BIG_CG");   // "wg" / "grid": force one form (A/B measurements)
+  if (e && e[0] == 'w') return true;
+  if (e && e[0] == 'g') return false;
+  const double bytes = (double)m * m * 8.0;
+  const double t_wg = fmax(3e-6, bytes / 60e9);
+  const double t_grid = 12e-6 + cnt * bytes / 5e12;
+  return t_wg <= t_grid;
+}
+
+// The subproblems min x^T A x / 2 + a^T x s.t. ||x|| <= Delta of the pass's cnt slots: A at slot
+// offset aoff with leading dimension lda (m x m), a = v[VS_A], Delta of slot k at D[ids[k] dstride].
+// CG (interior candidate), batched dsyevd, secular solve; the solution lands in v[VS_X], the
+// scalars in sc.  A is destroyed (eigenvectors).
+static int big_solve(riptrm_ctx* c, const Bat& B, int cnt, int64_t aoff, int lda, int m, const double* D, int64_t dstride,
+                     double tolhc) {
+  hipStream_t st = c->stream;
+  const int64_t N = B.N;
+  const dim3 one(1, cnt), rows(blocks_of(m, GV / 64), cnt);
+  if (cg_one_workgroup(m, cnt)) {
+    hipLaunchKernelGGL(k_cg_wg, one, dim3(WG), 0, st, B, m, aoff, (int64_t)lda, D, dstride);
+    HIPCHK(c, hipGetLastError());
+  } else {
+    hipLaunchKernelGGL(k_cg_init, one, dim3(WG), 0, st, B, m);
+    HIPCHK(c, hipGetLastError());
+    int32_t* flag = flag_of(c);
+    int32_t all = 0;
+    for (int it = 0; it < 10 * m + 1; it += CG_POLL) {
+      for (int k = 0; k < CG_POLL; ++k) {
+        hipLaunchKernelGGL(k_cg_dir, one, dim3(WG), 0, st, B, m);
+        hipLaunchKernelGGL(k_gemv, rows, dim3(GV), 0, st, B, aoff, (int64_t)lda, m, m, off_vec(N, VS_P), off_vec(N, VS_Q),
+                           off_sc(N) + SC_DONE);
+        hipLaunchKernelGGL(k_cg_upd, one, dim3(WG), 0, st, B, m);
+      }
+      hipLaunchKernelGGL(k_cg_alldone, dim3(1), dim3(64), 0, st, B, cnt, flag);
+      HIPCHK(c, hipGetLastError());
+      HIPCHK(c, hipMemcpyAsync(&all, flag, sizeof(int32_t), hipMemcpyDeviceToHost, st));
+      HIPCHK(c, hipStreamSynchronize(st));
+      if (all) break;
+    }
+    hipLaunchKernelGGL(k_gemv, rows, dim3(GV), 0, st, B, aoff, (int64_t)lda, m, m, off_vec(N, VS_CGX), off_vec(N, VS_Q),
+                       (int64_t)-1);
+    hipLaunchKernelGGL(k_cg_final, one, dim3(WG), 0, st, B, m, D, dstride);
+    HIPCHK(c, hipGetLastError());
+  }
+  if (int rc = eig_batched(c, B, cnt, true, m, aoff, lda)) return rc;
   // eigenvector k = row k of the row-major view (column k of dsyevd's column-major output)
-  hipLaunchKernelGGL(k_gemv, dim3(blocks_of(m, GV / 64)), dim3(GV), 0, st, A, (int64_t)lda, m, m, a, q.v[VS_G], nullptr);
-  hipLaunchKernelGGL(k_secular, dim3(1), dim3(WG), 0, st, m, q.v[VS_EV], q.v[VS_G], q.v[VS_PE], tolhc, q.sc);
-  hipLaunchKernelGGL(k_gemv_t, dim3(blocks_of(m, 256)), dim3(256), 0, st, A, (int64_t)lda, m, m, q.v[VS_PE], q.v[VS_X]);
-  hipLaunchKernelGGL(k_pick, dim3(blocks_of(m, 256)), dim3(256), 0, st, m, q.v[VS_CGX], q.v[VS_X], q.sc);
+  hipLaunchKernelGGL(k_gemv, rows, dim3(GV), 0, st, B, aoff, (int64_t)lda, m, m, off_vec(N, VS_A), off_vec(N, VS_G),
+                     (int64_t)-1);
+  hipLaunchKernelGGL(k_secular, one, dim3(WG), 0, st, B, m, tolhc);
+  hipLaunchKernelGGL(k_gemv_t, dim3(blocks_of(m, 256), cnt), dim3(256), 0, st, B, aoff, (int64_t)lda, m, m,
+                     off_vec(N, VS_PE), off_vec(N, VS_X));
+  hipLaunchKernelGGL(k_pick, dim3(blocks_of(m, 256), cnt), dim3(256), 0, st, B, m);
   HIPCHK(c, hipGetLastError());
   return RIPTRM_OK;
 }
 
-// matrix of HwCur (trial = 0: at (x, y), the subproblem's linear term from cxCur) or of HwNew
-// (trial = 1: at (x_new, y_new)) for NonnegPCA instance b, in the slot: A at q.M + n + 1, lda n
-static int big_nonnegpca_matrix(riptrm_ctx* c, Slot& q, int b, int trial) {
+// matrices of HwCur (trial = 0: at (x, y), the subproblem's linear term from cxCur) or of HwNew
+// (trial = 1: at (x_new, y_new)) for the pass's NonnegPCA instances: A at M + n + 1, lda n
+static int big_nonnegpca_matrix(riptrm_ctx* c, const Bat& B, int cnt, int trial) {
   hipStream_t st = c->stream;
   const DevParams& P = c->P;
   const int n = P.n;
+  const int64_t N = B.N;
   const int xk = trial ? V_IN1 : V_X, yk = trial ? V_YNEW : V_Y;
-  hipLaunchKernelGGL(k_dense, dim3(blocks_of((int64_t)n * n, 256)), dim3(256), 0, st, P, b, xk, yk, q.M);
-  hipLaunchKernelGGL(k_house, dim3(1), dim3(WG), 0, st, P, b, xk, yk, q.v[VS_W], q.sc);
-  hipLaunchKernelGGL(k_gemv, dim3(blocks_of(n, GV / 64)), dim3(GV), 0, st, q.M, (int64_t)n, n, n, q.v[VS_W], q.v[VS_U],
-                     nullptr);
-  const double* Xv = P.vec + ((int64_t)xk * P.batch + b) * P.ld;
+  const dim3 one(1, cnt), rows(blocks_of(n, GV / 64), cnt);
+  hipLaunchKernelGGL(k_dense, dim3(blocks_of((int64_t)n * n, 256), cnt), dim3(256), 0, st, P, B, xk, yk);
+  hipLaunchKernelGGL(k_house, one, dim3(WG), 0, st, P, B, xk, yk);
+  hipLaunchKernelGGL(k_gemv, rows, dim3(GV), 0, st, B, (int64_t)0, (int64_t)n, n, n, off_vec(N, VS_W), off_vec(N, VS_U),
+                     (int64_t)-1);
   if (trial)   // M x_new for x^T S x
-    hipLaunchKernelGGL(k_gemv, dim3(blocks_of(n, GV / 64)), dim3(GV), 0, st, q.M, (int64_t)n, n, n, Xv, q.v[VS_Q],
-                       nullptr);
-  hipLaunchKernelGGL(k_repmat_vec, dim3(1), dim3(WG), 0, st, P, b, xk, trial ? -1 : (int)V_C, q.v[VS_W], q.v[VS_U],
-                     q.v[VS_Q], q.v[VS_A], q.sc, trial);
-  hipLaunchKernelGGL(k_transform, dim3(blocks_of((int64_t)(n - 1) * (n - 1), 256)), dim3(256), 0, st, n, q.M, q.v[VS_W],
-                     q.v[VS_U], q.sc);
+    hipLaunchKernelGGL(k_gemv_x, rows, dim3(GV), 0, st, P, B, xk);
+  hipLaunchKernelGGL(k_repmat_vec, one, dim3(WG), 0, st, P, B, xk, trial ? -1 : (int)V_C, trial);
+  hipLaunchKernelGGL(k_transform, dim3(blocks_of((int64_t)(n - 1) * (n - 1), 256), cnt), dim3(256), 0, st, n, B);
   HIPCHK(c, hipGetLastError());
   return RIPTRM_OK;
 }
 
-// Serve every instance parked at PH_TRS_HOST / PH_MINEIG_HOST (one at a time, slot 0).  Returns the
-// number of instances resumed in *served.  Synchronises.
+// Serve every instance parked at PH_TRS_HOST / PH_MINEIG_HOST, up to big_slots per pass.  Returns
+// the number of instances resumed in *served.  Synchronises.
 int riptrm_big_service(riptrm_ctx* c, int* served) {
   *served = 0;
   const DevParams& P = c->P;
@@ -617,51 +899,61 @@ int riptrm_big_service(riptrm_ctx* c, int* served) {
   std::vector<double> st((size_t)B * RIPTRM_STAT_NFIELDS);
   HIPCHK(c, hipMemcpyAsync(st.data(), P.stats, st.size() * sizeof(double), hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
+  std::vector<int32_t> ids[2];   // [0] subproblems, [1] trial eigenvalues
   for (int b = 0; b < B; ++b) {
     const int ph = (int)st[(size_t)b * RIPTRM_STAT_NFIELDS + RIPTRM_STAT_PHASE];
-    if (ph != PH_TRS_HOST && ph != PH_MINEIG_HOST) continue;
-    if (!c->big_ws || c->big_order < n || c->big_slots < 1)
-      return fail(c, RIPTRM_E_STATE, "Exact_RepMat above dim 96 needs riptrm_trs_bind_workspace (order >= n)");
-    Slot q = slot_at(c->big_ws, c->big_order, 0);
-    const int trial = ph == PH_MINEIG_HOST;
-    if (int rc = big_nonnegpca_matrix(c, q, b, trial)) return rc;
-    double* A = q.M + n + 1;   // rows / columns 1.. of the n x n buffer
-    if (trial) {
-      if (int rc = big_handle(c)) return rc;
-      if (solver().syevd(c->big_handle, EVECT_NONE, FILL_UPPER, n - 1, A, n, q.v[VS_EV], q.v[VS_EW], q.info) != 0)
-        return fail(c, RIPTRM_E_HIP, "rocsolver_dsyevd failed");
-      hipLaunchKernelGGL(k_finish_mineig, dim3(1), dim3(1), 0, c->stream, P, b, q.v[VS_EV], q.info);
-    } else {
-      const double* Delta = P.st + (int64_t)b * ST_N + ST_DELTA;
-      if (int rc = big_solve(c, q, A, n, n - 1, Delta, P.opt.trs_tolhardcase)) return rc;
-      hipLaunchKernelGGL(k_finish_dir, dim3(1), dim3(WG), 0, c->stream, P, b, q.v[VS_W], q.v[VS_X], q.sc, q.info);
+    if (ph == PH_TRS_HOST) ids[0].push_back(b);
+    if (ph == PH_MINEIG_HOST) ids[1].push_back(b);
+  }
+  if (ids[0].empty() && ids[1].empty()) return RIPTRM_OK;
+  if (!c->big_ws || c->big_order < n || c->big_slots < 1)
+    return fail(c, RIPTRM_E_STATE, "Exact_RepMat above dim 96 needs riptrm_trs_bind_workspace (order >= n)");
+  const Bat Bt = bat_of(c);
+  for (int trial = 0; trial < 2; ++trial) {
+    const std::vector<int32_t>& L = ids[trial];
+    for (size_t k0 = 0; k0 < L.size(); k0 += (size_t)c->big_slots) {
+      const int cnt = (int)std::min<size_t>((size_t)c->big_slots, L.size() - k0);
+      if (int rc = put_ids(c, Bt, L.data() + k0, cnt)) return rc;
+      if (int rc = big_nonnegpca_matrix(c, Bt, cnt, trial)) return rc;
+      const int64_t aoff = n + 1;   // rows / columns 1.. of the n x n buffer
+      if (trial) {
+        if (int rc = eig_batched(c, Bt, cnt, false, n - 1, aoff, n)) return rc;
+        hipLaunchKernelGGL(k_finish_mineig, dim3(blocks_of(cnt, 64)), dim3(64), 0, c->stream, P, Bt, cnt);
+      } else {
+        if (int rc = big_solve(c, Bt, cnt, aoff, n, n - 1, P.st + ST_DELTA, ST_N, P.opt.trs_tolhardcase)) return rc;
+        hipLaunchKernelGGL(k_finish_dir, dim3(1, cnt), dim3(WG), 0, c->stream, P, Bt);
+      }
+      HIPCHK(c, hipGetLastError());
+      *served += cnt;
     }
-    HIPCHK(c, hipGetLastError());
-    ++*served;
   }
   return RIPTRM_OK;
 }
 
-// riptrm_trs_gep for dim > RIPTRM_TRS_DIM_MAX: one subproblem at a time through slot 0
+// riptrm_trs_gep for dim > RIPTRM_TRS_DIM_MAX: up to big_slots subproblems per pass
 int riptrm_big_trs_gep(riptrm_ctx* c, int dim, int batch, const double* A, int64_t lda, int64_t a_stride, const double* a,
                        int64_t ldv, const double* Delta, double tolhc, double* x, double* lam1, int32_t* kind,
                        double* mineig) {
   if (!c->big_ws || c->big_order < dim || c->big_slots < 1)
     return fail(c, RIPTRM_E_STATE, "trs_gep above dim 96 needs riptrm_trs_bind_workspace (order >= dim)");
-  Slot q = slot_at(c->big_ws, c->big_order, 0);
-  for (int b = 0; b < batch; ++b) {
-    hipLaunchKernelGGL(k_load, dim3(blocks_of((int64_t)dim * dim, 256)), dim3(256), 0, c->stream, dim,
-                       A + (int64_t)b * a_stride, lda, a + (int64_t)b * ldv, q.M, q.v[VS_A]);
+  const Bat Bt = bat_of(c);
+  std::vector<int32_t> ids(c->big_slots), info(c->big_slots);
+  for (int b0 = 0; b0 < batch; b0 += c->big_slots) {
+    const int cnt = std::min(c->big_slots, batch - b0);
+    for (int k = 0; k < cnt; ++k) ids[k] = b0 + k;
+    if (int rc = put_ids(c, Bt, ids.data(), cnt)) return rc;
+    hipLaunchKernelGGL(k_load, dim3(blocks_of((int64_t)dim * dim, 256), cnt), dim3(256), 0, c->stream, Bt, dim, A, lda,
+                       a_stride, a, ldv);
     HIPCHK(c, hipGetLastError());
-    if (int rc = big_solve(c, q, q.M, dim, dim, Delta + b, tolhc)) return rc;
-    int32_t info = 0;
-    HIPCHK(c, hipMemcpyAsync(&info, q.info, sizeof(info), hipMemcpyDeviceToHost, c->stream));
+    if (int rc = big_solve(c, Bt, cnt, 0, dim, dim, Delta, 1, tolhc)) return rc;
+    HIPCHK(c, hipMemcpyAsync(info.data(), Bt.infos, (size_t)cnt * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
-    if (info != 0)   // scipy.linalg.eig raises LinAlgError here
-      return fail(c, RIPTRM_E_HIP, "trs_gep: rocsolver_dsyevd did not converge (info " + std::to_string(info) +
-                                       ") on subproblem " + std::to_string(b));
-    hipLaunchKernelGGL(k_gep_out, dim3(blocks_of(dim, 256)), dim3(256), 0, c->stream, dim, q.v[VS_X], q.sc, q.v[VS_EV],
-                       x + (int64_t)b * ldv, lam1 + b, kind + b, mineig ? mineig + b : nullptr);
+    for (int k = 0; k < cnt; ++k)
+      if (info[k] != 0)   // scipy.linalg.eig raises LinAlgError here
+        return fail(c, RIPTRM_E_HIP, "trs_gep: rocsolver_dsyevd did not converge (info " + std::to_string(info[k]) +
+                                         ") on subproblem " + std::to_string(b0 + k));
+    hipLaunchKernelGGL(k_gep_out, dim3(blocks_of(dim, 256), cnt), dim3(256), 0, c->stream, Bt, dim, ldv, x, lam1, kind,
+                       mineig);
     HIPCHK(c, hipGetLastError());
   }
   return RIPTRM_OK;
@@ -672,7 +964,7 @@ extern "C" {
 int riptrm_trs_backend_status(char* msg, int32_t len) {
   Solver& s = solver();
   if (msg && len > 0) {
-    const std::string t = s.ok ? std::string("rocBLAS + rocSOLVER dsyevd loaded") : s.why;
+    const std::string t = s.ok ? std::string("rocBLAS + rocSOLVER dsyevd_strided_batched loaded") : s.why;
     std::strncpy(msg, t.c_str(), (size_t)len - 1);
     msg[len - 1] = 0;
   }
@@ -681,7 +973,7 @@ int riptrm_trs_backend_status(char* msg, int32_t len) {
 
 int64_t riptrm_trs_workspace_bytes(int32_t order, int32_t slots) {
   if (order < 1 || slots < 1) return 0;
-  return slot_doubles(order) * 8 * (int64_t)slots + 256;
+  return slot_doubles(order) * 8 * (int64_t)slots + tail_bytes(slots) + 256;
 }
 
 int riptrm_trs_bind_workspace(riptrm_ctx* ctx, void* ws, int64_t bytes, int32_t order, int32_t slots) {

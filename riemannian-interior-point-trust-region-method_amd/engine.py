@@ -213,6 +213,19 @@ def _stream_handle(device: torch.device) -> int:
     return torch.cuda.current_stream(device).cuda_stream
 
 
+EXACT_BIG_CHUNK = 4        # lock-step iterations per advance on the HBM Exact_RepMat path
+TRS_WS_BUDGET = 16 << 30   # bytes of HBM the Exact_RepMat scratch may take (RIPTRM_TRS_WS_GB overrides)
+
+
+def trs_workspace_slots(lib, order: int, want: int) -> int:
+    """Slots of order `order` for the HBM Exact_RepMat path: one per subproblem served in the same
+    pass (`want`), as many as the budget holds, at least one."""
+    import os
+    budget = int(float(os.environ.get("RIPTRM_TRS_WS_GB", TRS_WS_BUDGET / 2 ** 30)) * 2 ** 30)
+    per = int(lib.riptrm_trs_workspace_bytes(int(order), 1))
+    return max(1, min(int(want), budget // max(per, 1)))
+
+
 LAYOUTS = {"full": C["RIPTRM_LAYOUT_FULL"], "sym": C["RIPTRM_LAYOUT_SYMTILE"], "shared": C["RIPTRM_LAYOUT_SHARED"]}
 
 
@@ -502,15 +515,17 @@ class NonnegPCABatch:
         assert self.bound
         ro = resolve_options(option, math.pi, self.cap, restart_every)
         if ro.exact and self.n - 1 > C["RIPTRM_TRS_DIM_MAX"]:
-            # Exact_RepMat beyond the LDS solver: the frame matrix (n x n) lives in HBM scratch
-            # (riptrm_trs_bind_workspace; csrc/riptrm_trs_big.hip)
+            # Exact_RepMat beyond the LDS solver: the frame matrices (n x n) live in HBM scratch, one
+            # slot per instance served in the same pass (riptrm_trs_bind_workspace;
+            # csrc/riptrm_trs_big.hip), as many as trs_workspace_slots allows
+            slots = trs_workspace_slots(self.lib, self.n, self.batch)
             if self._trs_ws is None:
-                nbytes = int(self.lib.riptrm_trs_workspace_bytes(self.n, 1))
+                nbytes = int(self.lib.riptrm_trs_workspace_bytes(self.n, slots))
                 self._trs_ws = torch.empty(nbytes + 256, dtype=torch.uint8, device=self.device)
             base = self._trs_ws.data_ptr()
             ptr = base + (-base) % 256
             self.ctx.check(self.lib.riptrm_trs_bind_workspace(self.ctx.h, ctypes.c_void_p(ptr),
-                                                              self._trs_ws.numel() - (ptr - base), self.n, 1),
+                                                              self._trs_ws.numel() - (ptr - base), self.n, slots),
                            "riptrm_trs_bind_workspace")
         X, Y = self._padded(x0), self._padded(y0)
         tabs = ro.device_tables(self.device)
@@ -541,6 +556,11 @@ class NonnegPCABatch:
         most one record per instance on the tCG path) and the device log is drained once half full."""
         chunk, t0 = 4, time.time()
         cap = min(self.cap, int(self.ro.c_opt.log_capacity))
+        if self.ro.exact and self.n - 1 > C["RIPTRM_TRS_DIM_MAX"]:
+            # the HBM Exact_RepMat path parks every instance a few lock-step iterations after each
+            # service (subproblem -> trial point -> trial eigenvalue): short chunks, so the parked
+            # instances are served as soon as they all wait
+            max_chunk = min(max_chunk, EXACT_BIG_CHUNK)
         if self.drain:
             max_chunk = max(1, min(max_chunk, cap // 4))
         act = self.advance(0, outer_target)

@@ -3,8 +3,8 @@
 ``TRSgep(A, a, B, Del, tolhardcase)`` keeps the reference's signature and return value
 (src/solver/RIPTRM.py:218-299: ``(x, lam1, type)``); ``trs_gep_batched`` solves a batch of
 subproblems held as torch tensors on the GPU (dim <= RIPTRM_TRS_DIM_MAX: one launch, the matrix in
-LDS; larger: the HBM path — SciPy CG restated, rocSOLVER dsyevd, secular Newton — one subproblem
-after another).  Only B = I is supported — the one call site passes ``np.eye(xdim)``
+LDS; larger: the HBM path — SciPy CG restated, batched rocSOLVER dsyevd, secular Newton — every
+subproblem of the batch in one pass when the scratch budget allows).  Only B = I is supported — the one call site passes ``np.eye(xdim)``
 (RIPTRM.py:441).  No CPU fallback.
 """
 from __future__ import annotations
@@ -16,7 +16,7 @@ import numpy as np
 import torch
 
 import riptrm_native as N
-from engine import _stream_handle
+from engine import _stream_handle, trs_workspace_slots
 
 C = N.CONST
 KIND_NAMES = {C["RIPTRM_TRS_BOUNDARY"]: "boundary", C["RIPTRM_TRS_INTERIOR"]: "interior",
@@ -71,8 +71,8 @@ def trs_gep_batched(A: torch.Tensor, a: torch.Tensor, Delta: torch.Tensor, tolha
     if dim < 1:
         raise ValueError("dim must be >= 1")
     ctx = _context(dev)
-    if dim > DIM_MAX:   # HBM path: scratch for one subproblem of order dim (riptrm_trs_workspace_bytes)
-        bind_trs_workspace(ctx, dev, dim)
+    if dim > DIM_MAX:   # HBM path: one slot of order dim per subproblem of a pass (riptrm_trs_workspace_bytes)
+        bind_trs_workspace(ctx, dev, dim, trs_workspace_slots(ctx.lib, dim, B))
     x = torch.empty((B, dim), dtype=torch.float64, device=dev)
     lam1 = torch.empty(B, dtype=torch.float64, device=dev)
     kind = torch.empty(B, dtype=torch.int32, device=dev)

@@ -20,6 +20,7 @@
 #   stiefel_pmc      FETCH_SIZE / WRITE_SIZE of the Stiefel kernels (tools/stiefel_stamps)
 #   stiefel_stamps   in-kernel phase stamps of the Stiefel kernels (tools/stiefel_stamps)
 #   exact            bench.py --trs Exact_RepMat --dim 200 --batch 64    -> bench_exact_200.json
+#   exact_prof       rocprofv3 stats of the same
 #   dist2            bench.py --gpus 2 --same-device --backend gloo at the configs[3] per-rank shape
 set -u
 cd "$GRAFT_REPO_ROOT"
@@ -63,7 +64,8 @@ step() {
     python scripts/pmc_summarize.py $(find $O/spmc_FETCH_SIZE -name "*counter_collection.csv" | head -1) \
       $(find $O/spmc_WRITE_SIZE -name "*counter_collection.csv" | head -1) $O/r4_pmc_spass_sup.json $O/r4_traffic_spass_sup.json \
       --n 4000 --batch 128 --instances 64 \
-      --source "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate passes, of python bench.py --cpu-budget 0 --warmup 1 --steps 2 ($O)" ;;
+      --source "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate passes, of python bench.py --cpu-budget 0 --warmup 1 --steps 2 ($O)" \
+      && cp $O/r4_traffic_spass_sup.json profiles/ ;;   # the later headline step in this call reads it (bench.py --traffic-json)
   cfg1)
     timeout -k 10 240 python bench.py --dim 1000 --batch 1 > $O/bench_cfg1.json 2> $O/bench_cfg1.err || { tail $O/bench_cfg1.err; return 1; }
     val $O/bench_cfg1.json cfg1 ;;
@@ -112,6 +114,10 @@ for b in (256, 2048):
     timeout -k 10 420 python bench.py --trs Exact_RepMat --dim 200 --batch 64 --steps 4 --warmup 1 --cpu-budget 60 \
       > $O/bench_exact_200.json 2> $O/bench_exact.err || { tail $O/bench_exact.err; return 1; }
     val $O/bench_exact_200.json exact200 ;;
+  exact_prof)
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/exact -o exact -- python bench.py --trs Exact_RepMat \
+      --dim 200 --batch 64 --steps 4 --warmup 1 --cpu-budget 0 > $O/bench_exact_rocprof.json 2> $O/exact_rocprof.log || return 1
+    note "exact rocprof ok" ;;
   dist2)
     timeout -k 10 500 python bench.py --gpus 2 --same-device --backend gloo --batch 128 --warmup 1 --steps 2 --cpu-budget 0 \
       > $O/bench_dist2.json 2> $O/bench_dist2.err || { tail $O/bench_dist2.err; return 1; }
@@ -120,6 +126,15 @@ for b in (256, 2048):
     echo "unknown step $1"; return 2 ;;
   esac
 }
+
+# gpurun copies gpurun_out/ back only under 64 MiB: keep the rocprofv3 summaries (stats, PMC
+# summaries), drop the per-dispatch traces and raw counter rows once the steps have read them
+prune() {
+  find $O \( -name "*kernel_trace.csv" -o -name "*counter_collection.csv" -o -name "*memory_copy_trace.csv" \
+    -o -name "*.db" \) -delete 2>/dev/null
+  du -sh $O 2>/dev/null | tail -1
+}
+trap prune EXIT
 
 SEL="$*"
 for s in $STEPS; do

@@ -339,7 +339,7 @@ def si_perturb(x, y, eps, rs):
     return xp, y * (1.0 + eps * rs.randn(y.shape[0]))
 
 
-def classify_flip(step, P, states, gl, rl, flip, trials=8, seed=0, perturb=sphere_perturb):
+def classify_flip(step, P, states, gl, rl, flip, trials=8, seed=0, perturb=sphere_perturb, drift=None):
     """A branch flip at log row `flip[0]` (key flip[1]) is a rounding-driven one if the GPU's decision
     is reachable from the ORACLE's own state at that inner step perturbed at any size from 1e-14 up
     to the drift the two trajectories had accumulated before it on their outer iterates
@@ -355,7 +355,7 @@ def classify_flip(step, P, states, gl, rl, flip, trials=8, seed=0, perturb=spher
     if row < 1 or row - 1 >= len(states):
         return None
     x, y, mu, Delta, it, iopt = states[row - 1]
-    drift = max(prefix_deviation(gl, rl, row), 1e-14)
+    drift = max(prefix_deviation(gl, rl, row) if drift is None else min(drift, DRIFT_CAP), 1e-14)
     want = gl[key][row]
     rs = np.random.RandomState(seed)
     sizes = np.logspace(-14, np.log10(drift), max(1, int(np.ceil(np.log10(drift) + 14)) + 1))
@@ -482,10 +482,65 @@ def decision_tie(step, P, states, gl, rl, flip):
     return margin / err if margin <= err else None
 
 
-def check_against(gl, ra, states, variants, P, step, gpu_x=None, gpu_tcg=None):
+def forced_outer_flip(gl, flip, P, opt, resume):
+    """Teacher forcing at the outer boundary, for a flip the classifiers above cannot reproduce from
+    the ORACLE's state because the two trajectories have drifted apart over many outer iterations
+    (within the order variants' envelope, but past DRIFT_CAP): the GPU's own iterate at the head of
+    the flip's outer iteration k (`resume(k - 1)` -> x, y, mu, Delta of the device solve paused
+    there) goes into the oracle's inner_run for outer iteration k (RIPTRM.py:785-847).  From the
+    same state, the oracle must take the GPU's branches on every row of iteration k through the
+    flip row, with values within the calibrated bar (compare_logs) -- i.e. the GPU's decision is
+    the reference's decision at the GPU's own state -- or its own first flip against the GPU there
+    must be a classified rounding tie (classify_flip with the drift of iteration k's earlier rows,
+    decision_tie, is_radius_tie).  Returns (k, row, eps) or None."""
+    from oracle import riptrm_oracle as O
+    row = flip[0]
+    k = int(gl["iteration"][row])
+    rows_k = [i for i in range(1, len(gl["iteration"])) if gl["iteration"][i] == k]
+    if k < 1 or not rows_k or rows_k != list(range(rows_k[0], rows_k[-1] + 1)):
+        return None
+    h = rows_k[0] - 1
+    x, y, mu_dev, delta = resume(k - 1)
+    orc = O.RIPTRMOracle(opt)
+    rec = StateRecorder(orc)
+    o = orc.option
+    mu = O.mu_schedule(opt, k)[k - 1]
+    assert abs(mu - mu_dev) <= 1e-14 * mu, (mu, mu_dev)
+    Delta = max(float(delta), o['minimal_initial_TR_radius'])
+    inner_option = {"stopping_criterion_Lagrangian": o['forcing_function_Lagrangian'](mu),
+                    "stopping_criterion_complementarity": o['forcing_function_complementarity'](mu)}
+    x = np.asarray(x, np.float64)
+    y = np.asarray(y, np.float64)
+    t0 = orc.clock()
+    orc.add_log(0, t0, orc.evaluation(P, x, x, y), orc.solver_status(y, mu, True, None))   # a head row (dropped)
+    orc.inner_run(P, k, t0, x, y, mu, Delta, inner_option)
+    # the GPU's own rows 0..h in front of both (identical: the columns keep their scale, and the
+    # continuation's row i is global row h + i)
+    keys = [key for key in orc.log if key in gl]
+    sub_g = {key: list(gl[key][:h + 1]) + [gl[key][i] for i in rows_k] for key in keys}
+    sub_o = {key: list(gl[key][:h + 1]) + list(orc.log[key][1:]) for key in keys}
+    states = [None] * h + rec.states
+    f = first_branch_flip(sub_g, sub_o)
+    if f is None or f[0] > row:
+        compare_logs(_prefix(sub_g, row + 1), _prefix(sub_o, row + 1))
+        return (k, row, 0.0)
+    if f[0] > h + 1:
+        compare_logs(_prefix(sub_g, f[0]), _prefix(sub_o, f[0]))
+    pre = lambda lg: {key: v[h + 1:f[0]] for key, v in lg.items()}   # noqa: E731
+    drift = max([column_deviation(pre(sub_g), pre(sub_o), key) for key in ("cost", "residual")] + [0.0])
+    eps = classify_flip(rec.step, P, states, sub_g, sub_o, f, drift=drift)
+    if eps is None and decision_tie(rec.step, P, states, sub_g, sub_o, f) is not None:
+        eps = 0.0
+    if eps is None and f[1] == "radius_update" and is_radius_tie(sub_g, sub_o, f[0]):
+        eps = 0.0
+    return None if eps is None else (k, f[0], eps)
+
+
+def check_against(gl, ra, states, variants, P, step, gpu_x=None, gpu_tcg=None, resume=None, opt=None):
     """check_instance's bar, given the oracle's reference run `ra` (its inner steps' starting
     states recorded: StateRecorder), the order-perturbed runs `variants` (order_variants), the
-    oracle problem P and its unwrapped inner step (classify_flip's probe)."""
+    oracle problem P and its unwrapped inner step (classify_flip's probe).  resume (with opt, the
+    oracle's options): the GPU state at an outer-iteration head, for forced_outer_flip."""
     exc = []
     env = None
 
@@ -507,18 +562,38 @@ def check_against(gl, ra, states, variants, P, step, gpu_x=None, gpu_tcg=None):
             eps = 0.0   # the oracle's own summation-order variants leave its branches there (no perturbation)
         if eps is None and decision_tie(step, P, states, gl, ra.log, flip) is not None:
             eps = 0.0   # the decision's margin is inside the evaluation error of ared / pred
-        assert eps is not None, ("branch flip neither reachable within the accumulated drift nor left by the "
-                                 "oracle's order variants", flip, gl[flip[1]][flip[0]], ra.log[flip[1]][flip[0]])
-        compare_outer(gl, ra.log)
-        # the rows before the flip still meet the envelope bar (and their tCG exit indices)
+        forced = None
+        if eps is None and resume is not None:
+            forced = forced_outer_flip(gl, flip, P, opt, resume)
+            if forced is not None:
+                eps = forced[2]
+        if eps is None:
+            row = flip[0]
+            m = decision_margins(step, P, states[row - 1]) if 1 <= row <= len(states) else None
+            raise AssertionError(("branch flip neither reachable within the accumulated drift nor left by the "
+                                  "oracle's order variants", flip, gl[flip[1]][row], ra.log[flip[1]][row],
+                                  "drift", prefix_deviation(gl, ra.log, row), "margins", m,
+                                  "gpu rows", {k: gl[k][max(0, row - 2):row + 2] for k in
+                                               ("iteration", "inner_status", "radius_update", "cost", "residual")},
+                                  "ref rows", {k: ra.log[k][max(0, row - 2):row + 2] for k in
+                                               ("iteration", "inner_status", "radius_update", "cost", "residual")}))
         row = flip[0]
+        if forced is None:
+            compare_outer(gl, ra.log)
+        else:
+            # outer-level agreement up to the head of the forced iteration (past it the GPU's rows
+            # were checked against the oracle from the GPU's own state)
+            head = next(i for i in range(1, len(gl["iteration"])) if gl["iteration"][i] == forced[0]) - 1
+            compare_outer(_prefix(gl, head + 1), _prefix(ra.log, head + 1))
+            flip = flip + ("forced at outer %d" % forced[0],)
+        # the rows before the flip still meet the envelope bar (and their tCG exit indices)
         if row > 1:
             env = env if env is not None else envelope(ra, variants)
             compare_logs(_prefix(gl, row), _prefix(ra.log, row), envelope=env, excursions=exc)
             if gpu_tcg is not None:
                 pre = type("Pre", (), {"trace": ra.trace[:row - 1]})()
                 compare_tcg_iters(list(gpu_tcg)[:row - 1], pre, {"_tcg": env["_tcg"][:row - 1]}, reachable=reachable)
-        return ("flip", flip + (eps, len(gl["iteration"]), exc))
+        return ("flip", flip[:2] + (eps, len(gl["iteration"]), exc) + flip[2:])
     if gpu_x is not None:
         np.testing.assert_allclose(gpu_x, ra.x, atol=1e-6)
     return ("excursion", exc) if exc else None
@@ -611,8 +686,12 @@ def check_instances_parallel(items, opt, workers=16, progress=print, every_s=20.
                         S = np.load(paths[k])
                         P = O.NonnegPCAVectorized(S, S=S)
                         name = it.get("name", k)
-                        r = check_against(it["gl"], ra, states, variants, P, O.RIPTRMOracle(opt).inner_step,
-                                          gpu_x=it.get("gpu_x"), gpu_tcg=it.get("gpu_tcg"))
+                        try:
+                            r = check_against(it["gl"], ra, states, variants, P, O.RIPTRMOracle(opt).inner_step,
+                                              gpu_x=it.get("gpu_x"), gpu_tcg=it.get("gpu_tcg"),
+                                              resume=it.get("resume"), opt=opt)
+                        except AssertionError as e:
+                            raise AssertionError((f"instance {name}",) + tuple(e.args)) from e
                         results[name] = r
                         progress(f"[parity] instance {name}: {r} ({time.time() - t0:.0f} s)")
                         for q in need:
@@ -636,12 +715,13 @@ def check_budget(results, B, late_ties_free=False):
     excursion_budget(B) may show an envelope excursion (before a flip, for flipped ones).
     late_ties_free: flips in the last quarter of an instance's rows reproduced by a perturbation
     <= 1e-12 (the tie regime of small-mu iterations: |normdx - Delta| <= 1e-15 with a tiny Delta,
-    RIPTRM.py:672) do not count against the B/2."""
+    RIPTRM.py:672) do not count against the B/2; flips classified by forced_outer_flip (drift-driven:
+    the GPU's decision is the oracle's at the GPU's own state) always count."""
     flips = {b: r[1] for b, r in results.items() if r and r[0] == "flip"}
     exc = {b: r[1] for b, r in results.items() if r and r[0] == "excursion"}
     exc.update({b: f[4] for b, f in flips.items() if f[4]})   # flip = (row, key, eps, rows, excursions)
     print("classified flips:", flips, "envelope excursions:", exc)
     counted = {b: f for b, f in flips.items()
-               if not (late_ties_free and f[0] >= 0.75 * f[3] and f[2] <= 1e-12)}
+               if not (late_ties_free and f[0] >= 0.75 * f[3] and f[2] <= 1e-12 and len(f) < 6)}
     assert len(counted) <= B // 2, flips
     assert len(exc) <= excursion_budget(B), exc

@@ -513,6 +513,54 @@ def test_exact_repmat_above_lds_size_matches_oracle(sos):
     compare_until_flip(gl, ref.log)
 
 
+@pytest.mark.timeout(600)
+def test_exact_repmat_above_lds_size_batched(monkeypatch):
+    """The HBM Exact_RepMat service over a batch (csrc/riptrm_trs_big.hip: every parked instance in
+    one pass, one workspace slot each, batched dsyevd): six n = 200 instances with the second-order
+    test.  Each instance's trajectory is the one it has solved alone (a slot's arithmetic does not
+    depend on the pass it shares), whichever CG form serves it (one workgroup per slot or the
+    grid-wide launches: the same sums in the same order) and however many slots the scratch budget
+    allows (one slot: six passes); instance 0 also meets the oracle bar of the solo test above."""
+    from parity import compare_until_flip
+    B, K = 6, 3
+    insts = [G.generate_instance(200, 90 + b) for b in range(B)]
+    Zs = np.stack([z for z, _, _ in insts])
+    xs = np.stack([x for _, x, _ in insts])
+    ys = np.stack([y for _, _, y in insts])
+    opt = _gpu_opt(TRS_solver="Exact_RepMat", second_order_stationarity=True, maxiter=K)
+
+    def run(Z, x, y, cg=None, gb=None):
+        if cg:
+            monkeypatch.setenv("RIPTRM_BIG_CG", cg)
+        else:
+            monkeypatch.delenv("RIPTRM_BIG_CG", raising=False)
+        if gb:
+            monkeypatch.setenv("RIPTRM_TRS_WS_GB", gb)
+        else:
+            monkeypatch.delenv("RIPTRM_TRS_WS_GB", raising=False)
+        r = _engine(Z).solve(x, y, opt)
+        return r
+
+    base = run(Zs, xs, ys)
+    for b in range(B):
+        lg = base.log(b)
+        assert max(lg["iteration"]) == K, (b, max(lg["iteration"]))
+        assert all(v is not None for v in lg["mineigvalHw"][1:]), b
+    variants = {"grid CG": run(Zs, xs, ys, cg="grid"), "one-workgroup CG": run(Zs, xs, ys, cg="wg"),
+                "one slot": run(Zs, xs, ys, gb="0.0004")}
+    for b in (0, 3):
+        variants[f"instance {b} alone"] = run(Zs[b:b + 1], xs[b:b + 1], ys[b:b + 1])
+    for name, r in variants.items():
+        ids = [0] if name == "instance 0 alone" else [3] if name == "instance 3 alone" else range(B)
+        for k, b in enumerate(ids):
+            ra, rb = r.log(k), base.log(b)
+            for key in ("cost", "residual", "normdx", "mineigvalHw"):
+                assert ra[key] == rb[key], (name, b, key)
+            np.testing.assert_array_equal(r.x[k].cpu().numpy(), base.x[b].cpu().numpy(), err_msg=f"{name} instance {b}")
+    ref = O.solve(Zs[0], xs[0], ys[0], _oracle_opt(TRS_solver="Exact_RepMat", second_order_stationarity=True, maxiter=K))
+    compare_until_flip(base.log(0), ref.log)
+
+
 @pytest.mark.timeout(900)
 def test_exact_repmat_configs1_size_drop_in(monkeypatch):
     """BASELINE configs[1] size (n = 1000) with the reference's class defaults (Exact_RepMat +

@@ -391,3 +391,36 @@ def test_decision_margins_reproduce_the_logged_ratio():
         fake = {k: list(v) for k, v in r.log.items()}
         fake["inner_status"][row] = "unsuccessful" if r.log["inner_status"][row] == "successful" else "successful"
         assert decision_tie(rec.step, P, rec.states, fake, r.log, (row, "inner_status")) is None
+
+
+def test_forced_outer_flip_reproduces_own_state_and_rejects_margins():
+    """parity.forced_outer_flip: the 'GPU' log is the reference-structured oracle's, resumed at the
+    head of its outer iteration k from its OWN state (x, y, mu, Delta recorded at the inner_run
+    call).  From that state the vectorised oracle takes the same branches through any row of
+    iteration k (a flip there is accepted as the GPU's own decision); a fabricated decision with a
+    real margin ('unsuccessful' on a step with ared/pred > 0.5) is not."""
+    import copy
+    from parity import forced_outer_flip
+    Z, x0, y0 = G.generate_instance(37, 100)
+    opt = dict(OPT, maxiter=8)
+    heads = {}
+    oa = O.RIPTRMOracle(opt)
+    inner = oa.inner_run
+
+    def rec(P_, it, start, x, y, mu, Delta, iopt):
+        heads[it - 1] = (x.copy(), y.copy(), mu, Delta)
+        return inner(P_, it, start, x, y, mu, Delta, iopt)
+
+    oa.inner_run = rec
+    a = oa.run(O.NonnegPCAStructured(Z), x0, y0)
+    P = O.NonnegPCAVectorized(Z)
+    k = 6
+    rows_k = [i for i, it in enumerate(a.log["iteration"]) if it == k and i > 0]
+    assert len(rows_k) >= 2
+    got = forced_outer_flip(a.log, (rows_k[-1], "inner_status"), P, opt, lambda kk: heads[kk])
+    assert got is not None and got[0] == k and got[2] == 0.0, got
+    clear = [r for r in rows_k if a.log["inner_status"][r] == "successful" and a.log["ared/pred"][r] > 0.5]
+    assert clear
+    fake = copy.deepcopy(a.log)
+    fake["inner_status"][clear[0]] = "unsuccessful"
+    assert forced_outer_flip(fake, (clear[0], "inner_status"), P, opt, lambda kk: heads[kk]) is None
