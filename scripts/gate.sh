@@ -12,8 +12,8 @@
 #                    -> r4_pmc_spass_sup.json + the traffic json bench.py reads
 #   cfg1             bench.py --dim 1000 --batch 1 (configs[1])          -> bench_cfg1.json
 #   cfg1_trace       scripts/persist_trace.py (k_persist phase stamps at configs[1])
-#   shared           bench.py --layout shared (multi-start, MFMA S-pass) -> bench_shared.json
-#   shared_prof      rocprofv3 stats of the shared bench
+#   shared           bench.py --layout shared (multi-start, MFMA S-pass), 128 and 256 starts -> bench_shared*.json
+#   shared_prof      rocprofv3 stats of the shared bench (256 starts)
 #   si               bench.py --problem si --batch 256                   -> bench_si_b256.json
 #   stiefel          bench.py --problem stiefel at (200,50) x 256 and x 2048
 #   stiefel_prof     rocprofv3 stats of the 256 and 2048 Stiefel benches
@@ -74,10 +74,13 @@ step() {
     tail -5 $O/cfg1_trace.txt ;;
   shared)
     timeout -k 10 300 python bench.py --layout shared > $O/bench_shared.json 2> $O/bench_shared.err || { tail $O/bench_shared.err; return 1; }
-    val $O/bench_shared.json shared ;;
+    val $O/bench_shared.json shared
+    timeout -k 10 300 python bench.py --layout shared --batch 256 > $O/bench_shared_b256.json 2> $O/bench_shared_b256.err \
+      || { tail $O/bench_shared_b256.err; return 1; }
+    val $O/bench_shared_b256.json shared256 ;;
   shared_prof)
     timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/shared -o shared -- python bench.py --layout shared \
-      --cpu-budget 0 > $O/bench_shared_rocprof.json 2> $O/shared_rocprof.log || return 1
+      --batch 256 --cpu-budget 0 > $O/bench_shared_rocprof.json 2> $O/shared_rocprof.log || return 1
     note "shared rocprof ok" ;;
   si)
     timeout -k 10 300 python bench.py --problem si --batch 256 > $O/bench_si_b256.json 2> $O/bench_si.err || { tail $O/bench_si.err; return 1; }

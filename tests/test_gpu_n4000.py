@@ -247,5 +247,8 @@ def test_n4000_b128_headline_pipeline_matches_oracle(capsys):
     for k, r in results.items():
         say(f"[n4000] instance {k}: " + ("no flip, no excursion" if r is None else
                                          f"first flip (row, key, eps) = {r[1][:3]} of {r[1][3]} rows, excursions {r[1][4]}"
-                                         if r[0] == "flip" else f"excursions {r[1]}"))
+                                         if r[0] == "flip" else
+                                         f"no flip; order variants leave the reference at row {r[1][0]}: rows before it "
+                                         f"on the envelope bar, outer iterates compared (excursions {r[1][1]})"
+                                         if r[0] == "unstable" else f"excursions {r[1]}"))
     check_budget(results, len(ids), late_ties_free=True)

@@ -424,3 +424,28 @@ def test_forced_outer_flip_reproduces_own_state_and_rejects_margins():
     fake = copy.deepcopy(a.log)
     fake["inner_status"][clear[0]] = "unsuccessful"
     assert forced_outer_flip(fake, (clear[0], "inner_status"), P, opt, lambda kk: heads[kk]) is None
+
+
+def test_variant_decorrelation_classifier():
+    """parity.variant_decorrelated: an order variant that keeps the reference's branches but carries
+    a radius 1% away before the flip row marks the reference's later branches as no target; a
+    variant within rounding (1e-14) does not, nor does a deviation only after the flip row."""
+    from parity import BRANCH_KEYS, variant_decorrelated
+    rows = 8
+
+    def run(tr):
+        log = {k: [0] * rows for k in BRANCH_KEYS}
+        log["TR_radius"] = list(tr)
+        log["cost"] = [1.0] * rows
+        obj = type("R", (), {})()
+        obj.log, obj.trace = log, [{"tcg_iters": 1}] * (rows - 1)
+        return obj
+
+    base = np.full(rows, 0.25)
+    ref = run(base)
+    near = run(base * (1 + 1e-14))
+    early = base.copy(); early[3] *= 1.01
+    late = base.copy(); late[6] *= 1.01
+    assert variant_decorrelated(ref, [near, run(early)], (5, "inner_status"))
+    assert not variant_decorrelated(ref, [near], (5, "inner_status"))
+    assert not variant_decorrelated(ref, [near, run(late)], (5, "inner_status"))
