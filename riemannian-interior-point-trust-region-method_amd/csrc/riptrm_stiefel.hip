@@ -301,12 +301,14 @@ __device__ __forceinline__ void p3_gram(const lds_f64* Xs, const lds_f64* Us, in
 // behind its own branch; measured 21.9k ticks for the update at (200, 50))
 // units (independent accumulator chains) per wave per step of the update; measured at (200, 50):
 // 2 / 3 / 4 -> 22.9k / 22.9k / 23.5k ticks (4 spills): the update is not bound by its chains
-template <int P16, int P4T, int UMAX>
+// hk(q) after every step q (all waves; k_st_proj4 frees X's rows there)
+template <int P16, int P4T, int UMAX, class HK>
 __device__ __forceinline__ void p3_update(const lds_f64* Xs, const double (&bk)[4 * P16], const double (&cv)[UMAX][4],
-                                          double* out, int n, int p, int w, int c, int kk, int J, int nunits) {
+                                          double* out, int n, int p, int w, int c, int kk, int J, int nunits, HK hk) {
   constexpr int UB = 2;
 #pragma unroll
   for (int q = 0; q < UMAX; q += UB) {
+    if (q > 0) hk(q - UB);
     if (w + NW * q >= nunits) continue;   // wave-uniform (no break: the loop stays unrolled)
     int R[UB];
     bool on[UB];
@@ -344,46 +346,19 @@ __device__ __forceinline__ void p3_update(const lds_f64* Xs, const double (&bk)[
         if (on[b] && i < n && j < p) out[(int64_t)i * p + j] = cv[q + b < UMAX ? q + b : UMAX - 1][g] - acc[b][g];
       }
   }
+  hk((UMAX - 1) / UB * UB);
 }
 
-template <int P16>
-__global__ void __launch_bounds__(T) k_st_proj3(int n, int p, int64_t stride, const double* X, const double* U,
-                                                double* out) {
+// one projection out of LDS (X at Xs, U at Us, M over U's rows): the Gram, M, and the update; `pf()`
+// runs once every wave holds its operands of the update in registers and U's LDS area (M included)
+// is free -- k_st_proj4 starts the next point's U copy there
+template <int P16, class PF, class HK>
+__device__ __forceinline__ void p3_body(int n, int p, const lds_f64* Xs, lds_f64* Us, double* outp, PF pf, HK hk) {
   constexpr int S = 16 * P16;
-  constexpr int UL = 10;   // 16-B copies per thread per matrix in flight
-  extern __shared__ double lds[];
-  lds_f64* Xs = (lds_f64*)lds;
-  lds_f64* Us = Xs + n * p;
   lds_f64* Ms = (n * p >= S * S) ? Us : Us + n * p;   // M over U's rows once they are consumed
   const int t = threadIdx.x, l = t & 63, w = t >> 6, c = l & 15, kk = l >> 4;
-  const int64_t o = (int64_t)blockIdx.x * stride;
-  ST_STAMP(0);
-  {   // X, U -> LDS: np / 2 16-byte chunks each, every load of a batch in flight together (loading the
-      // second row half while the Gram runs over the first measured slower: 33.8 vs 31.3 us)
-    const int nc = n * p / 2;
-    const dbl2* Xg = (const dbl2*)(X + o);
-    const dbl2* Ug = (const dbl2*)(U + o);
-    for (int e0 = 0; e0 < nc; e0 += T * UL) {
-      dbl2 vx[UL], vu[UL];
-#pragma unroll
-      for (int u = 0; u < UL; ++u) {
-        const int e = e0 + u * T + t;
-        const int ec = e < nc ? e : nc - 1;
-        vx[u] = Xg[ec];
-        vu[u] = Ug[ec];
-      }
-#pragma unroll
-      for (int u = 0; u < UL; ++u) {
-        const int e = e0 + u * T + t;
-        if (e < nc) {
-          *(__attribute__((address_space(3))) dbl2*)(Xs + 2 * e) = vx[u];
-          *(__attribute__((address_space(3))) dbl2*)(Us + 2 * e) = vu[u];
-        }
-      }
-    }
-  }
-  __syncthreads();
-  ST_STAMP(1);
+  (void)t;
+  (void)l;
   // Gram: this wave's two blocks over all n rows
   int I0, J0, I1, J1;
   p3_unit<P16>(w, I0, J0, I1, J1);
@@ -441,13 +416,120 @@ __global__ void __launch_bounds__(T) k_st_proj3(int n, int p, int64_t stride, co
     // (16 lanes on 16 rows of one column) is bank-conflict free (unswizzled: 16-way)
     bk[s] = 0.5 * (Ms[k * S + (j ^ (k & 15))] + Ms[j * S + (k ^ (j & 15))]);
   }
+  pf();
   switch (P4) {   // the update specialised on the k steps, so no MFMA sits behind a per-step branch
-    case 13: p3_update<P16, 13, UMAX>(Xs, bk, cv, out + o, n, p, w, c, kk, J, nunits); break;
-    case 14: p3_update<P16, 14, UMAX>(Xs, bk, cv, out + o, n, p, w, c, kk, J, nunits); break;
-    case 15: p3_update<P16, 15, UMAX>(Xs, bk, cv, out + o, n, p, w, c, kk, J, nunits); break;
-    default: p3_update<P16, 16, UMAX>(Xs, bk, cv, out + o, n, p, w, c, kk, J, nunits); break;
+    case 13: p3_update<P16, 13, UMAX>(Xs, bk, cv, outp, n, p, w, c, kk, J, nunits, hk); break;
+    case 14: p3_update<P16, 14, UMAX>(Xs, bk, cv, outp, n, p, w, c, kk, J, nunits, hk); break;
+    case 15: p3_update<P16, 15, UMAX>(Xs, bk, cv, outp, n, p, w, c, kk, J, nunits, hk); break;
+    default: p3_update<P16, 16, UMAX>(Xs, bk, cv, outp, n, p, w, c, kk, J, nunits, hk); break;
   }
   ST_STAMP(4);
+}
+
+template <int P16>
+__global__ void __launch_bounds__(T) k_st_proj3(int n, int p, int64_t stride, const double* X, const double* U,
+                                                double* out) {
+  constexpr int UL = 10;   // 16-B copies per thread per matrix in flight
+  extern __shared__ double lds[];
+  lds_f64* Xs = (lds_f64*)lds;
+  lds_f64* Us = Xs + n * p;
+  const int t = threadIdx.x;
+  const int64_t o = (int64_t)blockIdx.x * stride;
+  ST_STAMP(0);
+  {   // X, U -> LDS: np / 2 16-byte chunks each, every load of a batch in flight together (loading the
+      // second row half while the Gram runs over the first measured slower: 33.8 vs 31.3 us)
+    const int nc = n * p / 2;
+    const dbl2* Xg = (const dbl2*)(X + o);
+    const dbl2* Ug = (const dbl2*)(U + o);
+    for (int e0 = 0; e0 < nc; e0 += T * UL) {
+      dbl2 vx[UL], vu[UL];
+#pragma unroll
+      for (int u = 0; u < UL; ++u) {
+        const int e = e0 + u * T + t;
+        const int ec = e < nc ? e : nc - 1;
+        vx[u] = Xg[ec];
+        vu[u] = Ug[ec];
+      }
+#pragma unroll
+      for (int u = 0; u < UL; ++u) {
+        const int e = e0 + u * T + t;
+        if (e < nc) {
+          *(__attribute__((address_space(3))) dbl2*)(Xs + 2 * e) = vx[u];
+          *(__attribute__((address_space(3))) dbl2*)(Us + 2 * e) = vu[u];
+        }
+      }
+    }
+  }
+  __syncthreads();
+  ST_STAMP(1);
+  p3_body<P16>(n, p, Xs, Us, out + o, [] {}, [](int) {});
+}
+
+// n p / 2 16-byte chunks from global memory into LDS (lane-linear image) by LDS-DMA: wave w's
+// instruction k copies chunks 64 (w + NW k) .. + 63; no VGPR destination, nothing waits on them until
+// the caller's vmcnt(0) (a __syncthreads()).  Chunks past nc are not issued (exec mask).
+__device__ __forceinline__ void p4_dma(const double* g, lds_f64* l, int c0, int c1) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  for (int e0 = c0 + 64 * w; e0 < c1; e0 += 64 * NW) {
+    const int e = e0 + lane;
+    if (e < c1)
+      __builtin_amdgcn_global_load_lds((const void*)(g + 2 * (int64_t)e), (__attribute__((address_space(3))) void*)(l + 2 * e0),
+                                       16, 0, 0);
+  }
+}
+
+// a workgroup barrier that leaves LDS-DMA copies in flight: this wave's LDS reads are complete
+// (lgkmcnt(0)), no vmcnt wait (a __syncthreads() would drain the copies); the memory clobber keeps
+// the compiler from moving LDS accesses across it
+__device__ __forceinline__ void p4_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// k_st_proj3 as a persistent loop over the points b = blockIdx.x, + gridDim.x, ... (one workgroup per
+// CU, the point resident in LDS): the next point's U is copied into U's LDS area by LDS-DMA while the
+// update runs (M and the update's operands are in registers by then), and its X once the update has
+// read X; the copies run beside the update's matrix-core work instead of in front of the Gram.
+template <int P16>
+__global__ void __launch_bounds__(T) k_st_proj4(int n, int p, int64_t stride, int batch, const double* X,
+                                                const double* U, double* out) {
+  extern __shared__ double lds[];
+  lds_f64* Xs = (lds_f64*)lds;
+  lds_f64* Us = Xs + n * p;
+  const int nc = n * p / 2;
+  int b = blockIdx.x;
+  if (b >= batch) return;
+  p4_dma(X + (int64_t)b * stride, Xs, 0, nc);
+  p4_dma(U + (int64_t)b * stride, Us, 0, nc);
+  __syncthreads();   // vmcnt(0): this point's copies landed
+  for (; b < batch; b += gridDim.x) {
+    const int nb = b + (int)gridDim.x;
+    // opaque per iteration: keeps the body's per-lane LDS addresses from being hoisted out of the loop
+    // (live across it they pushed the inlined body past 256 VGPRs)
+    int n_ = n, p_ = p;
+    asm volatile("" : "+s"(n_), "+s"(p_));
+    const double* Xn = X + (int64_t)nb * stride;
+    int rdone = 0;   // rows of X whose next-point copy is issued
+    ST_STAMP(0);
+    ST_STAMP(1);
+    p3_body<P16>(n_, p_, Xs, Us, out + (int64_t)b * stride, [&] {
+      if (nb < batch) {
+        __syncthreads();   // every wave's M reads are done: U's area is free
+        p4_dma(U + (int64_t)nb * stride, Us, 0, nc);
+      }
+    }, [&](int q) {
+      // after update step q every unit u < NW (q + 2) is done: X's rows below 16 (NW (q + 2) / P16)
+      // are read for good, and the next point's rows go there while the update goes on
+      if (nb < batch) {
+        int r1 = 16 * ((NW * (q + 2)) / P16);
+        r1 = r1 < n_ ? r1 & ~1 : n_;   // whole 16-B chunks (n p even; an even row count keeps r p even)
+        if (r1 > rdone) {
+          p4_barrier();
+          p4_dma(Xn, Xs, rdone * p_ / 2, r1 * p_ / 2);
+          rdone = r1;
+        }
+      }
+    });
+    if (nb < batch) __syncthreads();   // vmcnt(0): the next point's copies landed
+    ST_STAMP(5);
+  }
 }
 
 template <int P16>
@@ -1306,7 +1388,7 @@ static int st_check(riptrm_ctx* c, int32_t n, int32_t p, int32_t batch, int64_t 
     HIPCHK(c, hipFuncSetAttribute((const void*)k_st_retr_r, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   (int)(LDS_DOUBLES_R * sizeof(double))));
     const void* fr[] = {(const void*)k_st_retr2<1>, (const void*)k_st_retr2<2>, (const void*)k_st_retr2<3>,
-                        (const void*)k_st_retr2<4>, (const void*)k_st_proj3<4>};
+                        (const void*)k_st_retr2<4>, (const void*)k_st_proj3<4>, (const void*)k_st_proj4<4>};
     for (const void* f : fr) HIPCHK(c, hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, R2_LDS_MAX));
     if (c->device >= 0 && c->device < 64) attr[c->device] = true;
   }
@@ -1376,8 +1458,15 @@ int riptrm_stiefel_proj(riptrm_ctx* ctx, int32_t n, int32_t p, int32_t batch, in
   int rc = st_check(ctx, n, p, batch, stride);
   if (rc) return rc;
   if (proj3_ok(n, p, stride)) {
-    hipLaunchKernelGGL(k_st_proj3<4>, dim3(batch), dim3(T), (size_t)p3_lds_doubles(n, p, 4) * sizeof(double),
-                       ctx->stream, n, p, stride, X, U, out);
+    const size_t shm = (size_t)p3_lds_doubles(n, p, 4) * sizeof(double);
+    const int ncu = ctx->ncu > 0 ? ctx->ncu : 256;
+    // (a Gram that left the 2-column tail of p = 50 to the VALU and split the 9 remaining MFMA blocks
+    // over two k halves measured slower: 29.98 vs 27.62 us at 256 points, 246 vs 191 us at 2048)
+    const char* e = getenv("RIPTRM_STIEFEL_PROJ");   // "p3": one point per workgroup always (A/B)
+    if (batch > ncu && !(e && e[0] == 'p' && e[1] == '3'))   // several points per CU: the prefetching loop
+      hipLaunchKernelGGL(k_st_proj4<4>, dim3(ncu), dim3(T), shm, ctx->stream, n, p, stride, batch, X, U, out);
+    else
+      hipLaunchKernelGGL(k_st_proj3<4>, dim3(batch), dim3(T), shm, ctx->stream, n, p, stride, X, U, out);
     HIPCHK(ctx, hipGetLastError());
     return RIPTRM_OK;
   }

@@ -29,7 +29,8 @@ def _t(a):
                                      # every specialisation of the projection update (ceil(p/4) = 13..16)
                                      # and of the retraction's last-block k steps (1..4)
                                      (200, 55, 3), (200, 59, 3), (100, 27, 3), (96, 61, 2),
-                                     (200, 50, 256)])   # BASELINE configs[4]: (200, 50) x 256
+                                     (200, 50, 256),    # BASELINE configs[4]: (200, 50) x 256
+                                     (200, 49, 3), (200, 51, 3), (200, 52, 3), (172, 52, 2)])
 def test_stiefel_ops_match_oracle(n, p, B):
     from stiefel import StiefelBatch
     M, X, U, W = _data(n, p, B, seed=n)
@@ -65,6 +66,36 @@ def test_stiefel_retraction_kernels_agree(n, p, monkeypatch):
     assert np.abs(R2 - R1).max() <= 1e-13
     for b in range(8):
         assert np.abs(R2[b].T @ R2[b] - np.eye(p)).max() <= 1e-13
+
+
+@pytest.mark.parametrize("n,p,B", [(200, 50, 600), (200, 50, 2048), (208, 64, 513), (200, 51, 300)])
+def test_stiefel_projection_persistent_loop(n, p, B, monkeypatch):
+    """More points than CUs run k_st_proj4 (one workgroup per CU loops over its points, copying the
+    next point into LDS by LDS-DMA during the update): bitwise the one-point-per-workgroup k_st_proj3
+    (RIPTRM_STIEFEL_PROJ=p3, the same arithmetic), in place (out = U) too, and against torch fp64 at
+    a sample of points (ragged: B not a multiple of the CU count)."""
+    from stiefel import StiefelBatch
+    g = torch.Generator(device="cuda")
+    g.manual_seed(B)
+    X = torch.linalg.qr(torch.randn(B, n, p, dtype=torch.float64, device="cuda", generator=g))[0].contiguous()
+    W = torch.randn(B, n, p, dtype=torch.float64, device="cuda", generator=g)
+    st = StiefelBatch(n, p)
+    P4 = st.projection(X, W)
+    monkeypatch.setenv("RIPTRM_STIEFEL_PROJ", "p3")
+    P3 = st.projection(X, W)
+    monkeypatch.delenv("RIPTRM_STIEFEL_PROJ")
+    assert torch.equal(P4, P3)
+    Wc = W.clone()
+    st.ctx.check(st.lib.riptrm_stiefel_proj(st.ctx.h, n, p, B, n * p, st._ptr(X), st._ptr(Wc), st._ptr(Wc)),
+                 "riptrm_stiefel_proj")   # out = U
+    torch.cuda.synchronize()
+    assert torch.equal(Wc, P4)
+    idx = torch.tensor([0, 1, 255, 256, 257, B // 2, B - 2, B - 1], device="cuda").clamp(max=B - 1)
+    Xs, Ws = X[idx], W[idx]
+    M = Xs.transpose(1, 2) @ Ws
+    ref = Ws - Xs @ ((M + M.transpose(1, 2)) / 2)
+    err = ((P4[idx] - ref).flatten(1).norm(dim=1) / ref.flatten(1).norm(dim=1)).max().item()
+    assert err <= 1e-12, err
 
 
 def test_stiefel_rejects_bad_shapes():
