@@ -589,7 +589,14 @@ def main():
                        "state_kernel_ms": prof["state_ms"], "state_launches": prof["state_launches"],
                        "gemv_launches": prof["gemv_launches"],
                        "state_kernel_roofline": state_roofline,
-                       **({"spass_calibration": cal} if cal.get("ms_per_launch_tile") else {})},
+                       **({"spass_calibration": cal} if cal.get("ms_per_launch_tile") else {}),
+                       **({"exact_repmat_note": (
+                           "manifold.dim > 96: the subproblems are served in batched passes between lock-step "
+                           "chunks (csrc/riptrm_trs_big.hip); the pass, not the S-pass priced in `roofline`, sets "
+                           "this line's time: rocprofv3 puts ~75% of GPU time in rocSOLVER's batched dsyevd "
+                           "(tridiagonalisation + divide and conquer on (n-1) x (n-1) matrices, latency-bound; "
+                           "profiles/r4_exact_rocprofv3_kernel_stats.csv)")}
+                          if args.trs == "Exact_RepMat" and n - 1 > engine.C["RIPTRM_TRS_DIM_MAX"] else {})},
         }
         print(json.dumps(out), flush=True)
     if world > 1:
@@ -641,16 +648,21 @@ def bench_stiefel(args, world, rank, dev, dist):
     proj_kernel = ("k_st_proj3" if -(-p // 16) == 4 and n * p % 2 == 0 and -(-n // 16) <= 14 and
                    2 * n * p + (0 if n * p >= 64 * 64 else 64 * 64) <= 160 * 1024 // 8 and
                    os.environ.get("RIPTRM_STIEFEL_PROJ", "") != "r2" else "k_st_proj")
+    # more points than CUs: the persistent k_st_proj4 (same arithmetic, next point copied in during the update)
+    if proj_kernel == "k_st_proj3" and B > torch.cuda.get_device_properties(dev).multi_processor_count and \
+            os.environ.get("RIPTRM_STIEFEL_PROJ", "") != "p3":
+        proj_kernel = "k_st_proj4"
     # HBM bytes per launch from the committed PMC passes of this exact shape (FETCH_SIZE doubled
     # per MI355X_MICROARCH.md, + WRITE_SIZE); None for any other shape
+    # (profiles/r4_stiefel_pmc.json: 2048 points; bytes per point scaled to this batch)
     traffic = {}
-    pmc_path = os.path.join(ROOT, "profiles", "r3_stiefel_pmc.json")
+    pmc_path = os.path.join(ROOT, "profiles", "r4_stiefel_pmc.json")
     if os.path.exists(pmc_path):
         pm = json.load(open(pmc_path))
-        if (pm.get("n"), pm.get("p"), pm.get("B")) == (n, p, B * 1):
+        if (pm.get("n"), pm.get("p")) == (n, p) and pm.get("B"):
             for kname, m in pm["kernels"].items():
                 if "read_bytes_corrected" in m and "write_bytes" in m:
-                    traffic[kname.split("::")[-1].split("<")[0]] = m["read_bytes_corrected"] + m["write_bytes"]
+                    traffic[kname.split("::")[-1].split("<")[0]] = (m["read_bytes_corrected"] + m["write_bytes"]) / pm["B"] * B
     # CPU baseline: the pymanopt restatement (oracle/stiefel_oracle.py, NumPy) on the host, over the
     # same points until ~2 s have passed (a bounded sample; BLAS threads as configured)
     from oracle.stiefel_oracle import Stiefel as _CpuStiefel
@@ -685,7 +697,9 @@ def bench_stiefel(args, world, rank, dev, dist):
                      "hbm_floor_us": hbm_floor * 1e6, "mfma_floor_us": mfma_floor * 1e6,
                      "mfma_achieved_tflops": tfs,
                      "traffic": traffic.get(proj_kernel),
-                     "kernel": f"{proj_kernel} (U - X sym(X^T U), one workgroup per point)"},
+                     "kernel": f"{proj_kernel} (U - X sym(X^T U), " + ("one workgroup per CU looping over its points, the next "
+                                                                      "point copied into LDS during the update)"
+                                                                      if proj_kernel == "k_st_proj4" else "one workgroup per point)")},
         "cpu_baseline": cpu,
         "detail": {"retractions_per_s": B * world / tr, "retraction_ms": tr * 1e3,
                    "retraction_roofline": {"bound": "hbm", "achieved": 3.0 * n * p * 8 * B / tr / 1e9,

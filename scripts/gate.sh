@@ -108,7 +108,7 @@ for b in (256, 2048):
       note "stiefel pmc $c ok"
     done
     python scripts/stiefel_pmc_summary.py $(find $O/stpmc_FETCH_SIZE -name "*counter_collection.csv" | head -1) \
-      $(find $O/stpmc_WRITE_SIZE -name "*counter_collection.csv" | head -1) $O/stiefel_pmc.json ;;
+      $(find $O/stpmc_WRITE_SIZE -name "*counter_collection.csv" | head -1) $O/stiefel_pmc.json --batch ${ST_B:-2048} ;;
   stiefel_stamps)
     stamps_tool || return 3
     timeout -k 10 60 /tmp/stamps 200 50 ${ST_B:-256} > $O/stiefel_stamps.txt 2>&1 || return 1
