@@ -383,9 +383,10 @@ int riptrm_si_solve(riptrm_ctx* ctx, const riptrm_options* opt, const double* x0
  * lda), a / x at a + b*ldv, x + b*ldv; Delta, lam1, mineig: batch doubles; kind: batch int32
  * (RIPTRM_TRS_*).  mineig (may be NULL) = the smallest eigenvalue of A (RIPTRM.py:611).
  * dim <= RIPTRM_TRS_DIM_MAX: one workgroup per instance, A staged in LDS, asynchronous.
- * dim > RIPTRM_TRS_DIM_MAX: needs riptrm_trs_bind_workspace(order >= dim); the instances are solved
- * one after another on the HBM-resident matrix (SciPy CG restated, rocSOLVER dsyevd, secular
- * Newton on one workgroup); synchronises. */
+ * dim > RIPTRM_TRS_DIM_MAX: needs riptrm_trs_bind_workspace(order >= dim); up to `slots` subproblems
+ * per pass on HBM-resident matrices (SciPy CG restated, rocSOLVER dsyevd_strided_batched, secular
+ * Newton on one workgroup per subproblem); synchronises.  A non-converged eigensolve fails the call
+ * (RIPTRM_E_HIP naming the subproblem: scipy.linalg.eig raises there). */
 int riptrm_trs_gep(riptrm_ctx* ctx, int32_t dim, int32_t batch, const double* A, int64_t lda, int64_t a_stride,
                    const double* a, int64_t ldv, const double* Delta, double tolhardcase, double* x,
                    double* lam1, int32_t* kind, double* mineig);
@@ -393,11 +394,14 @@ int riptrm_trs_gep(riptrm_ctx* ctx, int32_t dim, int32_t batch, const double* A,
 /* Scratch of the HBM path of Exact_RepMat (manifold.dim > RIPTRM_TRS_DIM_MAX; RIPTRM.py:433-444,
  * :599-617 and TRSgep :218-299 at any size): `slots` subproblems of matrix order `order` (NonnegPCA:
  * order = n, the n x n frame matrix; riptrm_trs_gep: order = dim).  Bytes for riptrm_trs_bind_workspace,
- * caller-owned device memory (256-byte aligned).  The eigendecomposition is rocSOLVER's dsyevd,
- * loaded at first use (dlopen of librocsolver.so.0); rocSOLVER manages its own internal workspace.
- * In a NonnegPCA solve an instance that reaches the subproblem (or, with the second-order test, a
- * trial point) parks; riptrm_solve_advance serves parked instances after its lock-step chunk and
- * synchronises then.  Binding NULL unbinds. */
+ * caller-owned device memory (256-byte aligned).  Each subproblem of a pass takes one slot; with
+ * fewer slots than subproblems the pass repeats, with bitwise the same results.  The
+ * eigendecomposition is rocSOLVER's dsyevd_strided_batched, loaded at first use (dlopen of
+ * librocsolver.so.0); rocSOLVER manages its own internal workspace.  In a NonnegPCA solve an
+ * instance that reaches the subproblem (or, with the second-order test, a trial point) parks;
+ * riptrm_solve_advance serves every parked instance in batched passes after its lock-step chunk and
+ * synchronises then; an eigensolve that does not converge stops that instance (RIPTRM_ERR_EIGEN).
+ * Binding NULL unbinds. */
 int64_t riptrm_trs_workspace_bytes(int32_t order, int32_t slots);
 /* Whether the HBM path's eigensolver could be loaded (host only, no device work): RIPTRM_OK, or
  * RIPTRM_E_HIP with the dlopen message in msg (len bytes, NUL-terminated).  The libraries are
