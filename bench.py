@@ -593,9 +593,11 @@ def main():
                        **({"exact_repmat_note": (
                            "manifold.dim > 96: the subproblems are served in batched passes between lock-step "
                            "chunks (csrc/riptrm_trs_big.hip); the pass, not the S-pass priced in `roofline`, sets "
-                           "this line's time: rocprofv3 puts ~75% of GPU time in rocSOLVER's batched dsyevd "
-                           "(tridiagonalisation + divide and conquer on (n-1) x (n-1) matrices, latency-bound; "
-                           "profiles/r4_exact_rocprofv3_kernel_stats.csv)")}
+                           "this line's time: rocSOLVER's batched dsyevd (tridiagonalisation + divide and conquer "
+                           "on (n-1) x (n-1) matrices, latency-bound) takes most of the GPU time "
+                           "(profiles/r4_exact_rocprofv3_kernel_stats.csv); a subproblem at an accepted trial "
+                           "point reuses that point's eigenpairs (riptrm_trs_bind_cache)"),
+                           "trs_cache": dict(zip(("hits", "subproblems"), eng.trs_cache_stats()))}
                           if args.trs == "Exact_RepMat" and n - 1 > engine.C["RIPTRM_TRS_DIM_MAX"] else {})},
         }
         print(json.dumps(out), flush=True)

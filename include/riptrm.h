@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define RIPTRM_ABI_VERSION 9
+#define RIPTRM_ABI_VERSION 10
 
 /* status codes */
 #define RIPTRM_OK 0
@@ -408,6 +408,19 @@ int64_t riptrm_trs_workspace_bytes(int32_t order, int32_t slots);
  * librocblas.so.5 / librocsolver.so.0 unless RIPTRM_ROCBLAS_LIB / RIPTRM_ROCSOLVER_LIB name others. */
 int riptrm_trs_backend_status(char* msg, int32_t len);
 int riptrm_trs_bind_workspace(riptrm_ctx* ctx, void* ws, int64_t bytes, int32_t order, int32_t slots);
+/* Eigendecomposition cache of the HBM path in a NonnegPCA solve with the second-order test
+ * (RIPTRM.py:599-617 computes the trial point's eigenpairs; :686-692 keeps HwNewmatrix for the next
+ * subproblem when the step was accepted without dual clipping).  One entry per instance (order >= n,
+ * batch >= the bound batch): the trial point's eigenvectors / eigenvalues keyed by its (x, y).  A
+ * subproblem whose (x, y) equals its instance's key bitwise builds the same matrix bits, so it runs
+ * CG and the secular step on the cached eigenpairs without an eigensolve: results are bitwise those
+ * of the uncached solve.  Caller-owned device memory, riptrm_trs_cache_bytes(order, batch) bytes,
+ * 256-byte aligned; binding invalidates every entry, and so does riptrm_solve_begin.  Binding NULL
+ * unbinds.  riptrm_trs_cache_stats: hits and subproblems served since riptrm_solve_begin (either
+ * pointer may be NULL). */
+int64_t riptrm_trs_cache_bytes(int32_t order, int32_t batch);
+int riptrm_trs_bind_cache(riptrm_ctx* ctx, void* cache, int64_t bytes, int32_t order, int32_t batch);
+int riptrm_trs_cache_stats(riptrm_ctx* ctx, int64_t* hits, int64_t* subproblems);
 
 /* ==== Stiefel(n, p) manifold operations =========================================
  * Not in the reference (north_star / BASELINE configs[4] ask for them): pymanopt 2.x formulas,

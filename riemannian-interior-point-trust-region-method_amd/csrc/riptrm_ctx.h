@@ -70,6 +70,11 @@ struct riptrm_ctx {
   char* big_ws = nullptr;
   int big_order = 0, big_slots = 0;
   void* big_handle = nullptr;
+  // per-instance cache of the trial point's eigendecomposition (riptrm_trs_bind_cache): the next
+  // subproblem at the same (x, y) reuses it, as the reference reuses HwNewmatrix (RIPTRM.py:686-692)
+  char* big_cache = nullptr;
+  int big_cache_order = 0, big_cache_batch = 0;
+  int64_t big_cache_hits = 0, big_subproblems = 0;   // since the solve began (riptrm_trs_cache_stats)
 };
 
 // riptrm_trs_big.hip
@@ -78,6 +83,7 @@ int riptrm_big_trs_gep(riptrm_ctx* c, int dim, int batch, const double* A, int64
                        int64_t ldv, const double* Delta, double tolhc, double* x, double* lam1, int32_t* kind,
                        double* mineig);
 void riptrm_big_release(riptrm_ctx* c);
+int riptrm_big_reset_cache(riptrm_ctx* c);
 
 
 inline int fail(riptrm_ctx* c, int code, const std::string& msg) {

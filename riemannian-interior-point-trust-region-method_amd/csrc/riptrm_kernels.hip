@@ -3749,6 +3749,7 @@ int riptrm_solve_begin(riptrm_ctx* ctx, const riptrm_options* opt, const double*
   if (int rc0 = persist_init(ctx, x0, y0, ldv, nullptr, nullptr, (int)MODE_SOLVE)) return rc0;
   reset_groups(ctx);
   HIPCHK(ctx, hipMemsetAsync(P.cnt, 0, 4 * sizeof(int32_t), ctx->stream));
+  if (int rc0 = riptrm_big_reset_cache(ctx)) return rc0;
   ctx->solving = true;
   return kick(ctx);
 }

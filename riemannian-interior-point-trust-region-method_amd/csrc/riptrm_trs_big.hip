@@ -61,11 +61,15 @@ constexpr int NVS = 12;        // vectors per slot
 enum Vs : int { VS_W = 0, VS_U, VS_A, VS_CGX, VS_R, VS_P, VS_Q, VS_EV, VS_EW, VS_G, VS_PE, VS_X };
 
 // one slot for matrices of order N: [N x N][NVS vectors of vpad(N)][NSC scalars]; after the slots:
-// int32 info[slots], ids[slots], flag[8], sweeps[slots] (+ pad), double residual[slots]
+// int32 info[slots], ids[slots], flag[8], sweeps[slots], hits[slots] (+ pad), double residual[slots]
 __host__ __device__ inline int64_t slot_doubles(int64_t N) { return N * N + NVS * vpad(N) + NSC; }
 __host__ __device__ inline int64_t off_vec(int64_t N, int k) { return N * N + k * vpad(N); }
 __host__ __device__ inline int64_t off_sc(int64_t N) { return N * N + NVS * vpad(N); }
-inline int64_t tail_ints(int64_t slots) { return (3 * slots + 8 + 1) / 2 * 2; }   // even: the doubles stay aligned
+inline int64_t tail_ints(int64_t slots) { return (4 * slots + 8 + 1) / 2 * 2; }   // even: the doubles stay aligned
+
+// the per-instance eigendecomposition cache (riptrm_trs_bind_cache), order N: [Q: N x N][ev][x key]
+// [y key][valid] (vectors vpad(N))
+__host__ __device__ inline int64_t cache_doubles(int64_t N) { return N * N + 3 * vpad(N) + 8; }
 inline int64_t tail_bytes(int64_t slots) { return tail_ints(slots) * 4 + slots * 8; }
 
 // the slots of one pass: slot k (blockIdx.y) holds instance / subproblem ids[k]
@@ -226,9 +230,11 @@ __global__ void __launch_bounds__(256) k_gemv_t(Bat B, int64_t aoff, int64_t lda
   base[ooff + i] = s;
 }
 
-// gam = w^T u, then (iterate) a_k = c_k - tau w_k (w^T c) for k >= 1 and coef from the state,
-// or (trial) coef = (x^T S x + y^T x) x^T x with x^T S x = -x^T (M x) + y^T x (M = -S + diag(y/x))
-__global__ void __launch_bounds__(WG) k_repmat_vec(DevParams P, Bat B, int xk, int ck, int trial) {
+// gam = w^T u, then (iterate) a_k = c_k - tau w_k (w^T c) for k >= 1; coef = (x^T S x + y^T x) x^T x
+// with x^T S x = -x^T (M x) + y^T x (M = -S + diag(y/x)) at the iterate and at the trial point
+// alike, so the two matrices of the same (x, y) are the same bits (the trial point's
+// eigendecomposition serves the next subproblem there: riptrm_trs_bind_cache)
+__global__ void __launch_bounds__(WG) k_repmat_vec(DevParams P, Bat B, int xk, int ck) {
   __shared__ double red[WG / 64];
   const int k = blockIdx.y, b = B.ids[k];
   const Slot q = slot_at(B, k);
@@ -242,7 +248,7 @@ __global__ void __launch_bounds__(WG) k_repmat_vec(DevParams P, Bat B, int xk, i
   for (int i = threadIdx.x; i < n; i += WG) {
     gam += w[i] * u[i];
     if (Cv) wc += w[i] * Cv[i];
-    if (trial) xmx += X[i] * mx[i];
+    xmx += X[i] * mx[i];
   }
   gam = blk_sum(gam, red);
   wc = blk_sum(wc, red);
@@ -253,13 +259,9 @@ __global__ void __launch_bounds__(WG) k_repmat_vec(DevParams P, Bat B, int xk, i
   if (threadIdx.x == 0) {
     sc[SC_GAM] = gam;
     sc[SC_WC] = wc;
-    if (trial) {
-      const double xSx = -xmx + sc[SC_YX];
-      sc[SC_XSX] = xSx;
-      sc[SC_COEF] = (xSx + sc[SC_YX]) * sc[SC_XX];
-    } else {
-      sc[SC_COEF] = P.st[(int64_t)b * ST_N + ST_COEF];
-    }
+    const double xSx = -xmx + sc[SC_YX];
+    sc[SC_XSX] = xSx;
+    sc[SC_COEF] = (xSx + sc[SC_YX]) * sc[SC_XX];
   }
 }
 
@@ -682,6 +684,57 @@ __global__ void __launch_bounds__(256) k_load(Bat B, int m, const double* A, int
   if (e < m) q.v[VS_A][e] = a[(int64_t)b * ldv + e];
 }
 
+// ---- the per-instance eigendecomposition cache (riptrm_trs_bind_cache) ------------------------------
+__device__ __forceinline__ double* cache_of(double* cache, int64_t N, int b) { return cache + (int64_t)b * cache_doubles(N); }
+
+// after the trial point's eigensolve: slot k's eigenvectors (the n x n buffer), eigenvalues and the
+// trial point (x_new, y_new) -> instance ids[k]'s cache entry; valid iff the eigensolve converged
+__global__ void __launch_bounds__(256) k_cache_store(DevParams P, Bat B, double* cache, int64_t N) {
+  const int k = blockIdx.y, b = B.ids[k];
+  const Slot q = slot_at(B, k);
+  double* C = cache_of(cache, N, b);
+  const int n = P.n;
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e < (int64_t)n * n) C[e] = q.M[e];
+  if (e < n - 1) C[N * N + e] = q.v[VS_EV][e];
+  if (e < n) {
+    C[N * N + vpad(N) + e] = vec_of(P, V_IN1, b)[e];
+    C[N * N + 2 * vpad(N) + e] = vec_of(P, V_YNEW, b)[e];
+  }
+  if (e == 0) C[N * N + 3 * vpad(N)] = *q.info == 0 ? 1.0 : 0.0;
+}
+
+// hits[k] = 1 iff instance ids[k]'s cache entry is valid and was taken at exactly this (x, y): then
+// its matrix is the same bits as the one this subproblem would build (k_repmat_vec)
+__global__ void __launch_bounds__(256) k_cache_check(DevParams P, Bat B, const double* cache, int64_t N, int32_t* hits) {
+  const int k = blockIdx.y, b = B.ids[k];
+  const double* C = cache + (int64_t)b * cache_doubles(N);
+  const int n = P.n;
+  const double *X = vec_of(P, V_X, b), *Y = vec_of(P, V_Y, b);
+  int ok = C[N * N + 3 * vpad(N)] == 1.0;
+  for (int i = threadIdx.x; i < n; i += 256)
+    ok &= (X[i] == C[N * N + vpad(N) + i]) & (Y[i] == C[N * N + 2 * vpad(N) + i]);
+  ok = __syncthreads_and(ok);
+  if (threadIdx.x == 0) hits[k] = ok;
+}
+
+// a cache hit: the cached eigenvectors / eigenvalues -> slot k (after its CG used the matrix)
+__global__ void __launch_bounds__(256) k_cache_load(DevParams P, Bat B, const double* cache, int64_t N) {
+  const int k = blockIdx.y, b = B.ids[k];
+  const Slot q = slot_at(B, k);
+  const double* C = cache + (int64_t)b * cache_doubles(N);
+  const int n = P.n;
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e < (int64_t)n * n) q.M[e] = C[e];
+  if (e < n - 1) q.v[VS_EV][e] = C[N * N + e];
+  if (e == 0) *q.info = 0;
+}
+
+__global__ void k_cache_invalidate(double* cache, int64_t N, int batch) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b < batch) cache[(int64_t)b * cache_doubles(N) + N * N + 3 * vpad(N)] = 0.0;
+}
+
 // ---- rocSOLVER, loaded on first use (no link-time dependency of the library) -----------------------
 // (RIPTRM_ROCBLAS_LIB / RIPTRM_ROCSOLVER_LIB in the environment name other libraries: a host whose
 // ROCm is elsewhere, or a test that checks the failure path)
@@ -826,8 +879,7 @@ static bool cg_one_workgroup(int m, int cnt) {
 // offset aoff with leading dimension lda (m x m), a = v[VS_A], Delta of slot k at D[ids[k] dstride].
 // CG (interior candidate), batched dsyevd, secular solve; the solution lands in v[VS_X], the
 // scalars in sc.  A is destroyed (eigenvectors).
-static int big_solve(riptrm_ctx* c, const Bat& B, int cnt, int64_t aoff, int lda, int m, const double* D, int64_t dstride,
-                     double tolhc) {
+static int big_cg(riptrm_ctx* c, const Bat& B, int cnt, int64_t aoff, int lda, int m, const double* D, int64_t dstride) {
   hipStream_t st = c->stream;
   const int64_t N = B.N;
   const dim3 one(1, cnt), rows(blocks_of(m, GV / 64), cnt);
@@ -857,7 +909,14 @@ static int big_solve(riptrm_ctx* c, const Bat& B, int cnt, int64_t aoff, int lda
     hipLaunchKernelGGL(k_cg_final, one, dim3(WG), 0, st, B, m, D, dstride);
     HIPCHK(c, hipGetLastError());
   }
-  if (int rc = eig_batched(c, B, cnt, true, m, aoff, lda)) return rc;
+  return RIPTRM_OK;
+}
+
+// after the eigendecomposition (eigenvectors over the matrix): g = Q^T a, the secular solve, x
+static int big_after_eig(riptrm_ctx* c, const Bat& B, int cnt, int64_t aoff, int lda, int m, double tolhc) {
+  hipStream_t st = c->stream;
+  const int64_t N = B.N;
+  const dim3 one(1, cnt), rows(blocks_of(m, GV / 64), cnt);
   // eigenvector k = row k of the row-major view (column k of dsyevd's column-major output)
   hipLaunchKernelGGL(k_gemv, rows, dim3(GV), 0, st, B, aoff, (int64_t)lda, m, m, off_vec(N, VS_A), off_vec(N, VS_G),
                      (int64_t)-1);
@@ -867,6 +926,13 @@ static int big_solve(riptrm_ctx* c, const Bat& B, int cnt, int64_t aoff, int lda
   hipLaunchKernelGGL(k_pick, dim3(blocks_of(m, 256), cnt), dim3(256), 0, st, B, m);
   HIPCHK(c, hipGetLastError());
   return RIPTRM_OK;
+}
+
+static int big_solve(riptrm_ctx* c, const Bat& B, int cnt, int64_t aoff, int lda, int m, const double* D, int64_t dstride,
+                     double tolhc) {
+  if (int rc = big_cg(c, B, cnt, aoff, lda, m, D, dstride)) return rc;
+  if (int rc = eig_batched(c, B, cnt, true, m, aoff, lda)) return rc;
+  return big_after_eig(c, B, cnt, aoff, lda, m, tolhc);
 }
 
 // matrices of HwCur (trial = 0: at (x, y), the subproblem's linear term from cxCur) or of HwNew
@@ -882,9 +948,8 @@ static int big_nonnegpca_matrix(riptrm_ctx* c, const Bat& B, int cnt, int trial)
   hipLaunchKernelGGL(k_house, one, dim3(WG), 0, st, P, B, xk, yk);
   hipLaunchKernelGGL(k_gemv, rows, dim3(GV), 0, st, B, (int64_t)0, (int64_t)n, n, n, off_vec(N, VS_W), off_vec(N, VS_U),
                      (int64_t)-1);
-  if (trial)   // M x_new for x^T S x
-    hipLaunchKernelGGL(k_gemv_x, rows, dim3(GV), 0, st, P, B, xk);
-  hipLaunchKernelGGL(k_repmat_vec, one, dim3(WG), 0, st, P, B, xk, trial ? -1 : (int)V_C, trial);
+  hipLaunchKernelGGL(k_gemv_x, rows, dim3(GV), 0, st, P, B, xk);   // M x for x^T S x (k_repmat_vec)
+  hipLaunchKernelGGL(k_repmat_vec, one, dim3(WG), 0, st, P, B, xk, trial ? -1 : (int)V_C);
   hipLaunchKernelGGL(k_transform, dim3(blocks_of((int64_t)(n - 1) * (n - 1), 256), cnt), dim3(256), 0, st, n, B);
   HIPCHK(c, hipGetLastError());
   return RIPTRM_OK;
@@ -892,6 +957,15 @@ static int big_nonnegpca_matrix(riptrm_ctx* c, const Bat& B, int cnt, int trial)
 
 // Serve every instance parked at PH_TRS_HOST / PH_MINEIG_HOST, up to big_slots per pass.  Returns
 // the number of instances resumed in *served.  Synchronises.
+static bool cache_on(const riptrm_ctx* c) {
+  return c->big_cache && c->big_cache_order >= c->P.n && c->big_cache_batch >= c->P.batch;
+}
+
+// Serve every instance parked at PH_TRS_HOST / PH_MINEIG_HOST, up to big_slots per pass.  With the
+// cache bound, the trial point's pass keeps its eigendecomposition per instance, and a subproblem at
+// exactly that (x, y) (the step was accepted without dual clipping) builds its matrix and runs CG
+// but takes the cached eigenpairs instead of an eigensolve -- the same bits, as the matrices are
+// the same bits.  Returns the number of instances resumed in *served.  Synchronises.
 int riptrm_big_service(riptrm_ctx* c, int* served) {
   *served = 0;
   const DevParams& P = c->P;
@@ -909,24 +983,70 @@ int riptrm_big_service(riptrm_ctx* c, int* served) {
   if (!c->big_ws || c->big_order < n || c->big_slots < 1)
     return fail(c, RIPTRM_E_STATE, "Exact_RepMat above dim 96 needs riptrm_trs_bind_workspace (order >= n)");
   const Bat Bt = bat_of(c);
-  for (int trial = 0; trial < 2; ++trial) {
-    const std::vector<int32_t>& L = ids[trial];
-    for (size_t k0 = 0; k0 < L.size(); k0 += (size_t)c->big_slots) {
-      const int cnt = (int)std::min<size_t>((size_t)c->big_slots, L.size() - k0);
+  const bool cached = cache_on(c);
+  double* cache = (double*)c->big_cache;
+  const int64_t CN = c->big_cache_order;
+  const int64_t aoff = n + 1;   // rows / columns 1.. of the n x n buffer
+  const int S = c->big_slots;
+  // subproblems: split into cache hits and misses
+  std::vector<int32_t> miss, hit;
+  if (cached && !ids[0].empty()) {
+    int32_t* hits = tail_of(c) + 3 * S + 8;
+    std::vector<int32_t> h(S);
+    for (size_t k0 = 0; k0 < ids[0].size(); k0 += (size_t)S) {
+      const int cnt = (int)std::min<size_t>((size_t)S, ids[0].size() - k0);
+      if (int rc = put_ids(c, Bt, ids[0].data() + k0, cnt)) return rc;
+      hipLaunchKernelGGL(k_cache_check, dim3(1, cnt), dim3(256), 0, c->stream, P, Bt, cache, CN, hits);
+      HIPCHK(c, hipGetLastError());
+      HIPCHK(c, hipMemcpyAsync(h.data(), hits, (size_t)cnt * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+      HIPCHK(c, hipStreamSynchronize(c->stream));
+      for (int k = 0; k < cnt; ++k) (h[k] ? hit : miss).push_back(ids[0][k0 + k]);
+    }
+  } else {
+    miss = ids[0];
+  }
+  // pass kinds: 0 subproblem with its eigensolve, 1 subproblem on cached eigenpairs, 2 trial eigenvalues
+  const std::vector<int32_t>* lists[3] = {&miss, &hit, &ids[1]};
+  for (int kind = 0; kind < 3; ++kind) {
+    const std::vector<int32_t>& L = *lists[kind];
+    for (size_t k0 = 0; k0 < L.size(); k0 += (size_t)S) {
+      const int cnt = (int)std::min<size_t>((size_t)S, L.size() - k0);
       if (int rc = put_ids(c, Bt, L.data() + k0, cnt)) return rc;
-      if (int rc = big_nonnegpca_matrix(c, Bt, cnt, trial)) return rc;
-      const int64_t aoff = n + 1;   // rows / columns 1.. of the n x n buffer
-      if (trial) {
-        if (int rc = eig_batched(c, Bt, cnt, false, n - 1, aoff, n)) return rc;
+      if (int rc = big_nonnegpca_matrix(c, Bt, cnt, kind == 2)) return rc;
+      if (kind == 2) {
+        // eigenvectors too (the next subproblem at this point reuses them); the value is the same
+        // computation with or without the cache
+        if (int rc = eig_batched(c, Bt, cnt, true, n - 1, aoff, n)) return rc;
         hipLaunchKernelGGL(k_finish_mineig, dim3(blocks_of(cnt, 64)), dim3(64), 0, c->stream, P, Bt, cnt);
+        if (cached)
+          hipLaunchKernelGGL(k_cache_store, dim3(blocks_of((int64_t)n * n, 256), cnt), dim3(256), 0, c->stream, P, Bt, cache,
+                             CN);
       } else {
-        if (int rc = big_solve(c, Bt, cnt, aoff, n, n - 1, P.st + ST_DELTA, ST_N, P.opt.trs_tolhardcase)) return rc;
+        if (int rc = big_cg(c, Bt, cnt, aoff, n, n - 1, P.st + ST_DELTA, ST_N)) return rc;
+        if (kind == 1)
+          hipLaunchKernelGGL(k_cache_load, dim3(blocks_of((int64_t)n * n, 256), cnt), dim3(256), 0, c->stream, P, Bt, cache,
+                             CN);
+        else if (int rc = eig_batched(c, Bt, cnt, true, n - 1, aoff, n))
+          return rc;
+        if (int rc = big_after_eig(c, Bt, cnt, aoff, n, n - 1, P.opt.trs_tolhardcase)) return rc;
         hipLaunchKernelGGL(k_finish_dir, dim3(1, cnt), dim3(WG), 0, c->stream, P, Bt);
       }
       HIPCHK(c, hipGetLastError());
       *served += cnt;
     }
   }
+  if (cached) c->big_cache_hits += (int64_t)hit.size();
+  c->big_subproblems += (int64_t)ids[0].size();
+  return RIPTRM_OK;
+}
+
+// a new solve: no cache entry is valid (same (x, y) on other data would otherwise hit)
+int riptrm_big_reset_cache(riptrm_ctx* c) {
+  c->big_cache_hits = c->big_subproblems = 0;
+  if (!c->big_cache) return RIPTRM_OK;
+  hipLaunchKernelGGL(k_cache_invalidate, dim3(blocks_of(c->big_cache_batch, 256)), dim3(256), 0, c->stream,
+                     (double*)c->big_cache, (int64_t)c->big_cache_order, c->big_cache_batch);
+  HIPCHK(c, hipGetLastError());
   return RIPTRM_OK;
 }
 
@@ -974,6 +1094,34 @@ int riptrm_trs_backend_status(char* msg, int32_t len) {
 int64_t riptrm_trs_workspace_bytes(int32_t order, int32_t slots) {
   if (order < 1 || slots < 1) return 0;
   return slot_doubles(order) * 8 * (int64_t)slots + tail_bytes(slots) + 256;
+}
+
+int64_t riptrm_trs_cache_bytes(int32_t order, int32_t batch) {
+  if (order < 1 || batch < 1) return 0;
+  return cache_doubles(order) * 8 * (int64_t)batch;
+}
+
+int riptrm_trs_bind_cache(riptrm_ctx* ctx, void* cache, int64_t bytes, int32_t order, int32_t batch) {
+  if (!ctx) return RIPTRM_E_ARG;
+  if (!cache) {   // unbind
+    ctx->big_cache = nullptr;
+    ctx->big_cache_order = ctx->big_cache_batch = 0;
+    return RIPTRM_OK;
+  }
+  if (order < 1 || batch < 1 || bytes < riptrm_trs_cache_bytes(order, batch) || ((uintptr_t)cache % 256) != 0)
+    return fail(ctx, RIPTRM_E_ARG, "trs_bind_cache: need order, batch >= 1, 256-byte alignment and "
+                                   "riptrm_trs_cache_bytes(order, batch) bytes");
+  ctx->big_cache = (char*)cache;
+  ctx->big_cache_order = order;
+  ctx->big_cache_batch = batch;
+  return riptrm_big_reset_cache(ctx);
+}
+
+int riptrm_trs_cache_stats(riptrm_ctx* ctx, int64_t* hits, int64_t* subproblems) {
+  if (!ctx) return RIPTRM_E_ARG;
+  if (hits) *hits = ctx->big_cache_hits;
+  if (subproblems) *subproblems = ctx->big_subproblems;
+  return RIPTRM_OK;
 }
 
 int riptrm_trs_bind_workspace(riptrm_ctx* ctx, void* ws, int64_t bytes, int32_t order, int32_t slots) {

@@ -226,6 +226,20 @@ def trs_workspace_slots(lib, order: int, want: int) -> int:
     return max(1, min(int(want), budget // max(per, 1)))
 
 
+TRS_CACHE_BUDGET = 16 << 30   # bytes of HBM the eigendecomposition cache may take (RIPTRM_TRS_CACHE_GB)
+
+
+def trs_cache_wanted(lib, order: int, batch: int) -> int:
+    """Bytes of the HBM Exact_RepMat path's eigendecomposition cache (riptrm_trs_bind_cache), or 0
+    when RIPTRM_TRS_CACHE=0 or the whole batch does not fit the budget (the cache is all or none)."""
+    import os
+    if os.environ.get("RIPTRM_TRS_CACHE", "1") == "0":
+        return 0
+    budget = int(float(os.environ.get("RIPTRM_TRS_CACHE_GB", TRS_CACHE_BUDGET / 2 ** 30)) * 2 ** 30)
+    nbytes = int(lib.riptrm_trs_cache_bytes(int(order), int(batch)))
+    return nbytes if 0 < nbytes <= budget else 0
+
+
 LAYOUTS = {"full": C["RIPTRM_LAYOUT_FULL"], "sym": C["RIPTRM_LAYOUT_SYMTILE"], "shared": C["RIPTRM_LAYOUT_SHARED"]}
 
 
@@ -270,6 +284,7 @@ class NonnegPCABatch:
         self.bound = False
         self._keep: List[torch.Tensor] = []
         self._trs_ws: Optional[torch.Tensor] = None   # Exact_RepMat above RIPTRM_TRS_DIM_MAX
+        self._trs_cache: Optional[torch.Tensor] = None   # its eigendecomposition cache
         # log records copied to the host by drain_logs() (riptrm_log_rebase), per instance
         self.drain = bool(drain_logs)
         self._drained: List[List[np.ndarray]] = [[] for _ in range(self.batch)]
@@ -527,6 +542,19 @@ class NonnegPCABatch:
             self.ctx.check(self.lib.riptrm_trs_bind_workspace(self.ctx.h, ctypes.c_void_p(ptr),
                                                               self._trs_ws.numel() - (ptr - base), self.n, slots),
                            "riptrm_trs_bind_workspace")
+            # with the second-order test every trial point's eigenpairs are computed anyway; a
+            # subproblem at that same point (step accepted without dual clipping) then skips its
+            # eigensolve (RIPTRM.py:686-692 keeps HwNewmatrix the same way)
+            cbytes = trs_cache_wanted(self.lib, self.n, self.batch) if ro.c_opt.second_order_stationarity else 0
+            if cbytes and (self._trs_cache is None or self._trs_cache.numel() < cbytes + 256):
+                self._trs_cache = torch.empty(cbytes + 256, dtype=torch.uint8, device=self.device)
+            if cbytes:
+                base = self._trs_cache.data_ptr()
+                ptr = base + (-base) % 256
+                self.ctx.check(self.lib.riptrm_trs_bind_cache(self.ctx.h, ctypes.c_void_p(ptr), cbytes, self.n,
+                                                              self.batch), "riptrm_trs_bind_cache")
+            else:
+                self.ctx.check(self.lib.riptrm_trs_bind_cache(self.ctx.h, None, 0, 0, 0), "riptrm_trs_bind_cache")
         X, Y = self._padded(x0), self._padded(y0)
         tabs = ro.device_tables(self.device)
         self._keep = [X, Y] + tabs
@@ -541,6 +569,13 @@ class NonnegPCABatch:
         self._drained = [[] for _ in range(self.batch)]
         self._dropped = np.zeros(self.batch, dtype=np.int64)
         return ro
+
+    def trs_cache_stats(self):
+        """(cache hits, subproblems served) of the HBM Exact_RepMat path since begin()."""
+        h, t = ctypes.c_int64(0), ctypes.c_int64(0)
+        self.ctx.check(self.lib.riptrm_trs_cache_stats(self.ctx.h, ctypes.byref(h), ctypes.byref(t)),
+                       "riptrm_trs_cache_stats")
+        return int(h.value), int(t.value)
 
     def advance(self, steps: int, outer_target: Optional[int] = None) -> int:
         tgt = 2 ** 31 - 1 if outer_target is None else int(outer_target)

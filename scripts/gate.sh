@@ -117,6 +117,10 @@ for b in (256, 2048):
     timeout -k 10 420 python bench.py --trs Exact_RepMat --dim 200 --batch 64 --steps 4 --warmup 1 --cpu-budget 60 \
       > $O/bench_exact_200.json 2> $O/bench_exact.err || { tail $O/bench_exact.err; return 1; }
     val $O/bench_exact_200.json exact200 ;;
+  exact1000)
+    timeout -k 10 600 python bench.py --trs Exact_RepMat --dim 1000 --batch ${EX_B:-1} --steps 3 --warmup 1 --cpu-budget 0 \
+      > $O/bench_exact_1000.json 2> $O/bench_exact1000.err || { tail $O/bench_exact1000.err; return 1; }
+    val $O/bench_exact_1000.json exact1000 ;;
   exact_prof)
     timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/exact -o exact -- python bench.py --trs Exact_RepMat \
       --dim 200 --batch 64 --steps 4 --warmup 1 --cpu-budget 0 > $O/bench_exact_rocprof.json 2> $O/exact_rocprof.log || return 1

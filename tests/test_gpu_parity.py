@@ -519,8 +519,10 @@ def test_exact_repmat_above_lds_size_batched(monkeypatch):
     one pass, one workspace slot each, batched dsyevd): six n = 200 instances with the second-order
     test.  Each instance's trajectory is the one it has solved alone (a slot's arithmetic does not
     depend on the pass it shares), whichever CG form serves it (one workgroup per slot or the
-    grid-wide launches: the same sums in the same order) and however many slots the scratch budget
-    allows (one slot: six passes); instance 0 also meets the oracle bar of the solo test above."""
+    grid-wide launches: the same sums in the same order), however many slots the scratch budget
+    allows (one slot: six passes) and whether the eigendecomposition cache serves the subproblems at
+    an accepted trial point (riptrm_trs_bind_cache: same matrix bits, so the same eigenpairs);
+    instance 0 also meets the oracle bar of the solo test above."""
     from parity import compare_until_flip
     B, K = 6, 3
     insts = [G.generate_instance(200, 90 + b) for b in range(B)]
@@ -529,7 +531,13 @@ def test_exact_repmat_above_lds_size_batched(monkeypatch):
     ys = np.stack([y for _, _, y in insts])
     opt = _gpu_opt(TRS_solver="Exact_RepMat", second_order_stationarity=True, maxiter=K)
 
-    def run(Z, x, y, cg=None, gb=None):
+    stats = {}
+
+    def run(Z, x, y, cg=None, gb=None, cache=None):
+        if cache:
+            monkeypatch.setenv("RIPTRM_TRS_CACHE", cache)
+        else:
+            monkeypatch.delenv("RIPTRM_TRS_CACHE", raising=False)
         if cg:
             monkeypatch.setenv("RIPTRM_BIG_CG", cg)
         else:
@@ -538,16 +546,22 @@ def test_exact_repmat_above_lds_size_batched(monkeypatch):
             monkeypatch.setenv("RIPTRM_TRS_WS_GB", gb)
         else:
             monkeypatch.delenv("RIPTRM_TRS_WS_GB", raising=False)
-        r = _engine(Z).solve(x, y, opt)
+        e = _engine(Z)
+        r = e.solve(x, y, opt)
+        stats[(cg, gb, cache, len(Z))] = e.trs_cache_stats()
         return r
 
     base = run(Zs, xs, ys)
+    hits, total = stats[(None, None, None, B)]
+    print(f"eigendecomposition cache: {hits} of {total} subproblems")
+    assert total > 0 and 0 < hits <= total, (hits, total)
     for b in range(B):
         lg = base.log(b)
         assert max(lg["iteration"]) == K, (b, max(lg["iteration"]))
         assert all(v is not None for v in lg["mineigvalHw"][1:]), b
     variants = {"grid CG": run(Zs, xs, ys, cg="grid"), "one-workgroup CG": run(Zs, xs, ys, cg="wg"),
-                "one slot": run(Zs, xs, ys, gb="0.0004")}
+                "one slot": run(Zs, xs, ys, gb="0.0004"), "no cache": run(Zs, xs, ys, cache="0")}
+    assert stats[(None, None, "0", B)][0] == 0
     for b in (0, 3):
         variants[f"instance {b} alone"] = run(Zs[b:b + 1], xs[b:b + 1], ys[b:b + 1])
     for name, r in variants.items():
