@@ -372,7 +372,13 @@ int riptrm_si_profile_enable(riptrm_ctx* ctx, int32_t on);
 int riptrm_si_profile_read(riptrm_ctx* ctx, double* seconds);
 
 /* Whole RIPTRM solves (RIPTRM.py:909-976) from x0 (batch x 3 d d), y0 (batch x m); tables as in
- * riptrm_solve_begin.  One launch, asynchronous: synchronise the stream, then read the workspace. */
+ * riptrm_solve_begin.  One launch, asynchronous: synchronise the stream, then read the workspace.
+ * Exact_RepMat with manifold.dim = d(d-1)/2 + d(d+1) > RIPTRM_TRS_DIM_MAX (d >= 8): needs
+ * riptrm_trs_bind_workspace(order >= manifold.dim) first; an instance builds its subproblem's matrix
+ * (manifold.dim HVPs) in the SI workspace and parks, the call serves every parked instance in
+ * batched passes (the HBM path of riptrm_trs_gep; with the second-order test also HwNew's smallest
+ * eigenvalue) and relaunches until every instance has finished: synchronous then.  A non-converged
+ * eigensolve fails the call (RIPTRM_E_HIP). */
 int riptrm_si_solve(riptrm_ctx* ctx, const riptrm_options* opt, const double* x0, const double* y0,
                     const double* mu_table, const double* tolL_table, const double* tolC_table,
                     int32_t table_len);

@@ -84,6 +84,9 @@ int riptrm_big_trs_gep(riptrm_ctx* c, int dim, int batch, const double* A, int64
                        double* mineig);
 void riptrm_big_release(riptrm_ctx* c);
 int riptrm_big_reset_cache(riptrm_ctx* c);
+int riptrm_big_gep_ids(riptrm_ctx* c, int dim, const int32_t* sel, int count, const double* A, int64_t lda,
+                       int64_t a_stride, const double* a, int64_t ldv, const double* Delta, double tolhc, double* x,
+                       double* lam1, int32_t* kind, double* mineig, bool mineig_only);
 
 
 inline int fail(riptrm_ctx* c, int code, const std::string& msg) {

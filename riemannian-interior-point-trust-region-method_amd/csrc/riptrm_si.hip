@@ -26,6 +26,7 @@
 #include <math.h>
 #include <cstring>
 #include <string>
+#include <vector>
 #include "riptrm_ctx.h"
 #include "riptrm_wave.h"
 #include "riptrm_trs.h"
@@ -39,7 +40,7 @@ constexpr int DMAX = RIPTRM_SI_DMAX;
 constexpr int MMAX = RIPTRM_SI_MMAX;
 constexpr int CF = RIPTRM_SI_CONS_FIELDS;
 
-enum Mode : int { MODE_SOLVE = 0, MODE_HVP = 1, MODE_TCG = 2 };
+enum Mode : int { MODE_SOLVE = 0, MODE_HVP = 1, MODE_TCG = 2, MODE_RESUME = 3 };
 
 struct SIParams {
   int32_t d, N, m, batch, cap, mode, tab_len, pad;
@@ -66,14 +67,37 @@ struct SIParams {
   const double* mu_tab;
   const double* tolL_tab;
   const double* tolC_tab;
+  // Exact_RepMat above RIPTRM_TRS_DIM_MAX (si_hbm_trs): the parked subproblems and the resume records
+  double* trsA;      // batch x tdim x tdim   matrix of HwCur / HwNew in the tangent frame
+  double* trsw;      // batch x 2 tdp         unit vector / HVP coordinates (repmat scratch)
+  double* trsa;      // batch x tdp           coordinates of cxCur
+  double* trsx;      // batch x tdp           the subproblem's solution (host service)
+  double* trsD;      // batch                 Delta
+  double* trslam;    // batch                 lam1 (host service)
+  int32_t* trskind;  // batch                 RIPTRM_TRS_* (host service)
+  double* trsmin;    // batch                 smallest eigenvalue of HwNew's matrix (host service)
+  double* rs;        // batch x rs_doubles    resume records
+  int32_t tdim, tdp;
   riptrm_options opt;
 };
 
 struct Layout {
   int64_t off_x, off_y, off_eta, off_heta, off_escr, off_stats, off_log, total;
+  int64_t off_tA, off_tw, off_ta, off_tx, off_tD, off_tlam, off_tkind, off_tmin, off_rs;   // 0: no HBM subproblem path
 };
 
 inline int64_t rup(int64_t a, int64_t m) { return (a + m - 1) / m * m; }
+
+// manifold.dim of Product(Skew(d), SPD(d), SPD(d)) and whether its Exact_RepMat subproblem takes the
+// HBM path (parked instances served by the host's batched TRS service, riptrm_trs_big.hip)
+__host__ __device__ constexpr int si_manifold_dim(int d) { return d * (d - 1) / 2 + d * (d + 1); }
+__host__ __device__ constexpr bool si_hbm_trs(int d) { return si_manifold_dim(d) > RIPTRM_TRS_DIM_MAX; }
+__host__ __device__ constexpr int si_tdp(int d) { return (si_manifold_dim(d) + 31) / 32 * 32; }
+// resume record: 32 scalars (incl. the section ticks), then 21 rows of one double per thread
+// (x, xI, xPrev, xHead, x0, eta as 3 rows each; y, yI, y0)
+constexpr int RS_NSC = 32, RS_PT = 20, RS_ROWS = 21;
+__host__ __device__ constexpr int si_nt(int d) { return d <= 8 ? 64 : (d * d + 63) / 64 * 64; }
+__host__ __device__ constexpr int64_t si_rs_doubles(int d) { return RS_NSC + (int64_t)RS_ROWS * si_nt(d); }
 
 inline Layout make_layout(int d, int N, int m, int batch, int cap) {
   Layout L;
@@ -86,6 +110,19 @@ inline Layout make_layout(int d, int N, int m, int batch, int cap) {
   L.off_escr = o;  o = rup(o + 8LL * batch * d * N, 256);
   L.off_stats = o; o = rup(o + 8LL * batch * RIPTRM_STAT_NFIELDS, 256);
   L.off_log = o;   o = rup(o + 8LL * batch * cap * RIPTRM_LOG_NFIELDS, 256);
+  L.off_tA = L.off_tw = L.off_ta = L.off_tx = L.off_tD = L.off_tlam = L.off_tkind = L.off_tmin = L.off_rs = 0;
+  if (si_hbm_trs(d)) {
+    const int64_t td = si_manifold_dim(d), tp = si_tdp(d);
+    L.off_tA = o;    o = rup(o + 8 * batch * td * td, 256);
+    L.off_tw = o;    o = rup(o + 8 * batch * 2 * tp, 256);
+    L.off_ta = o;    o = rup(o + 8 * batch * tp, 256);
+    L.off_tx = o;    o = rup(o + 8 * batch * tp, 256);
+    L.off_tD = o;    o = rup(o + 8LL * batch, 256);
+    L.off_tlam = o;  o = rup(o + 8LL * batch, 256);
+    L.off_tkind = o; o = rup(o + 4LL * batch, 256);
+    L.off_tmin = o;  o = rup(o + 8LL * batch, 256);
+    L.off_rs = o;    o = rup(o + 8 * batch * si_rs_doubles(d), 256);
+  }
   L.total = o;
   return L;
 }
@@ -325,7 +362,7 @@ __device__ __forceinline__ double spd_dist_reg(const double (&A)[D * D], const d
 }
 
 // threads of the workgroup for block size D: one wave up to D = 8, one thread per element above
-__host__ __device__ constexpr int si_threads(int D) { return D <= 8 ? W : (D * D + 63) / 64 * 64; }
+__host__ __device__ constexpr int si_threads(int D) { return si_nt(D); }
 
 // LDS doubles a big-D workgroup needs besides its static arrays: the broadcast buffer, the
 // reduction buffers, the dense solvers' row / column buffers and the Jacobi work area
@@ -839,6 +876,8 @@ struct Eng {
   // the Cholesky factor L of the point: <L B L^T, L C L^T>_X = tr(B C).  The reference draws a random
   // basis (utils.py:388-397); the subproblem's solution does not depend on the basis.
   static constexpr int NS = D * (D - 1) / 2, NY = D * (D + 1) / 2, DIMM = NS + 2 * NY;
+  static constexpr bool HBMT = si_hbm_trs(D);   // the subproblem's matrix lives in HBM (host service)
+  static constexpr int TDP = si_tdp(D);
   static constexpr double RS2 = 0.7071067811865475;   // 1 / np.sqrt(2)
   __device__ __forceinline__ static int skew_idx(int i, int j) { return i * (2 * D - i - 1) / 2 + (j - i - 1); }
   __device__ __forceinline__ static int sym_idx(int i, int j) { return i * D - i * (i - 1) / 2 + (j - i); }
@@ -846,6 +885,15 @@ struct Eng {
     double Lr, Lq, Lri, Lqi;   // this lane's element of chol(R), chol(Q) and their inverses
   };
   __device__ __forceinline__ Frame frame(PV x) {
+    if constexpr (BIG) {   // the workgroup's Cholesky / Gauss-Jordan (one element per thread)
+      bool ok;
+      Frame F;
+      F.Lr = par_chol(x.r, ok);
+      F.Lq = par_chol(x.q, ok);
+      F.Lri = par_inv(F.Lr);
+      F.Lqi = par_inv(F.Lq);
+      return F;
+    }
     stage(0, x.r);
     stage(1, x.q);
     __syncthreads();
@@ -918,7 +966,7 @@ struct Eng {
   }
   // compute_direction's Exact_RepMat branch: returns the RIPTRM_TRS_* type
   __device__ __forceinline__ int trs_direction(const AtX& a, double Delta, PV& eta, double& hvps) {
-    if constexpr (BIG) {   // riptrm_si_solve refuses Exact_RepMat above d = 7 (manifold.dim > 96)
+    if constexpr (HBMT) {   // solve() parks instead (repmat_hbm)
       eta = PV{0.0, 0.0, 0.0};
       return RIPTRM_TRS_BOUNDARY;
     }
@@ -931,13 +979,50 @@ struct Eng {
   }
   // smallest eigenvalue of HwNew's matrix at (xN, yN, mu) (RIPTRM.py:599-613)
   __device__ __forceinline__ double mineig_at(PV xN, double yN, double mu, double& hvps) {
-    if constexpr (BIG) return 0.0;
+    if constexpr (HBMT) return 0.0;   // solve() parks instead (repmat_hbm)
     AtX aN;
     prepare(aN, xN, yN, mu);
     const Frame F = frame(xN);
     riptrm_trs::Work w = repmat(aN, F, hvps);
     riptrm_trs::Blk<W> B(nullptr);
     return riptrm_trs::min_eig<W>(B, w);
+  }
+
+  // manifold.dim > RIPTRM_TRS_DIM_MAX: selfadj_operator2matrix (utils.py:565-573) into this instance's
+  // HBM matrix (tdim x tdim, row-major), the same HVP per basis vector as repmat; with want_c the
+  // coordinates of cxCur too.  The host's batched service solves / eigensolves it while the instance
+  // is parked (RIPTRM.py:433-444, :599-617).
+  __device__ void repmat_hbm(const AtX& a, const Frame& F, double& hvps, bool want_c) {
+    double* A = P.trsA + (int64_t)b * DIMM * DIMM;
+    double* e = P.trsw + (int64_t)b * 2 * TDP;
+    double* q = e + TDP;
+    for (int j = 0; j < DIMM; ++j) {
+      for (int k = l; k < DIMM; k += NT) e[k] = (k == j) ? 1.0 : 0.0;
+      __syncthreads();
+      const PV bj = from_coords(F, e);
+      const PV h = hw(a, bj);
+      hvps += 1.0;
+      to_coords(F, h, q);
+      for (int k = l; k <= j; k += NT) {
+        A[(int64_t)k * DIMM + j] = q[k];
+        A[(int64_t)j * DIMM + k] = q[k];
+      }
+      __syncthreads();
+    }
+    if (want_c) to_coords(F, a.c, P.trsa + (int64_t)b * TDP);
+  }
+
+  // ---- resume records (HBM subproblem path) ------------------------------------------------
+  __device__ __forceinline__ double* rs_base() const { return P.rs + (int64_t)b * si_rs_doubles(D); }
+  __device__ __forceinline__ void rs_put(double* r, int row, double v) { r[RS_NSC + (int64_t)row * NT + l] = v; }
+  __device__ __forceinline__ double rs_get(const double* r, int row) const { return r[RS_NSC + (int64_t)row * NT + l]; }
+  __device__ __forceinline__ void rs_put_pv(double* r, int k, PV v) {
+    rs_put(r, 3 * k, v.j);
+    rs_put(r, 3 * k + 1, v.r);
+    rs_put(r, 3 * k + 2, v.q);
+  }
+  __device__ __forceinline__ PV rs_get_pv(const double* r, int k) const {
+    return PV{rs_get(r, 3 * k), rs_get(r, 3 * k + 1), rs_get(r, 3 * k + 2)};
   }
 
   // ---- evaluation, src/solver/utils.py:342-368 (+ compute_residual :269-340) ----------------
@@ -1048,27 +1133,74 @@ struct Eng {
   }
 
   // ---- the whole run: RIPTRM.run / outer_step / inner_run / inner_step ----------------------
-  __device__ __forceinline__ void solve() {
+  // resume = false: a new solve from P.in_x / P.in_y.  resume = true (HBM subproblem path only): an
+  // instance parked at PH_TRS_HOST / PH_MINEIG_HOST continues from its resume record with the host
+  // service's answer; every other instance returns at once.
+  __device__ __forceinline__ void solve(bool resume) {
     const int64_t v3 = 3LL * dd;
-    PV x = load_pv(P.in_x + b * v3);
-    double y = cact ? P.in_y[(int64_t)b * m + l] : 0.0;
-    const PV xI = x;
-    const double yI = y;
+    PV x, xI, xPrev, xHead, x0, eta_r;   // xPrev: inner_run's (RIPTRM.py:787); xHead: run's (:929, :947)
+    double y, yI, y0;
     double outer_it = 0.0, mu_idx = 0.0, mu = mu_at(0), Delta = P.opt.initial_tr_radius;
     double inner_total = 0.0, tcg_total = 0.0, hvps = 0.0, log_count = 0.0, log_over = 0.0;
     double stop_code = RIPTRM_STOP_NONE, stop_rt = 0.0, residual = 0.0, last_j = 0.0, last_stop = 0.0;
-    const double t_start = now();
-    const double t_tick0 = (double)wall_clock64();
-    PV xPrev = x;   // inner_run's xPrev (RIPTRM.py:787)
-    PV xHead = x;   // run's xPrev: the point at the previous outer head (RIPTRM.py:929, :947)
+    double t_start, t_tick0, Delta0 = 0.0, inner_it = 0.0, t_inner = 0.0;
+    int rph = 0;       // resumed: 1 with the subproblem's solution, 2 with HwNew's smallest eigenvalue
+    int tstop_r = 0;   // the direction type of a phase-2 resume
+    if (!resume) {
+      x = load_pv(P.in_x + b * v3);
+      y = cact ? P.in_y[(int64_t)b * m + l] : 0.0;
+      xI = xPrev = xHead = x0 = x;
+      yI = y0 = y;
+      eta_r = PV{0.0, 0.0, 0.0};
+      t_start = now();
+      t_tick0 = (double)wall_clock64();
+    } else {
+      if constexpr (!HBMT) {
+        return;
+      } else {
+        const double ph = P.stats[(int64_t)b * RIPTRM_STAT_NFIELDS + RIPTRM_STAT_PHASE];
+        if (ph != (double)riptrm::PH_TRS_HOST && ph != (double)riptrm::PH_MINEIG_HOST) return;
+        rph = ph == (double)riptrm::PH_TRS_HOST ? 1 : 2;
+        const double* r = rs_base();
+        outer_it = r[0], mu_idx = r[1], mu = r[2], Delta = r[3], inner_total = r[4], tcg_total = r[5];
+        hvps = r[6], log_count = r[7], log_over = r[8], residual = r[9], last_j = r[10], last_stop = r[11];
+        t_start = r[12], t_tick0 = r[13], inner_it = r[14], Delta0 = r[15], t_inner = r[16];
+        tstop_r = (int)r[17];
+        for (int k = 0; k < RIPTRM_SI_PROF_NFIELDS; ++k) pt[k] = r[RS_PT + k];
+        x = rs_get_pv(r, 0), xI = rs_get_pv(r, 1), xPrev = rs_get_pv(r, 2), xHead = rs_get_pv(r, 3);
+        x0 = rs_get_pv(r, 4), eta_r = rs_get_pv(r, 5);
+        y = rs_get(r, 18), yI = rs_get(r, 19), y0 = rs_get(r, 20);
+      }
+    }
+    // park at phase ph: the resume record, then the host serves the subproblem (riptrm_si_solve)
+    auto park = [&](int ph, int tstop_now, PV eta_now) {
+      double* r = rs_base();
+      if (l == 0) {
+        r[0] = outer_it, r[1] = mu_idx, r[2] = mu, r[3] = Delta, r[4] = inner_total, r[5] = tcg_total;
+        r[6] = hvps, r[7] = log_count, r[8] = log_over, r[9] = residual, r[10] = last_j, r[11] = last_stop;
+        r[12] = t_start, r[13] = t_tick0, r[14] = inner_it, r[15] = Delta0, r[16] = t_inner;
+        r[17] = (double)tstop_now;
+        for (int k = 0; k < RIPTRM_SI_PROF_NFIELDS; ++k) r[RS_PT + k] = pt[k];
+        P.trsD[b] = Delta;
+        double* o = P.stats + (int64_t)b * RIPTRM_STAT_NFIELDS;
+        o[RIPTRM_STAT_PHASE] = (double)ph;
+        o[RIPTRM_STAT_OUTER_ITERS] = outer_it;
+        o[RIPTRM_STAT_LOG_COUNT] = log_count;
+      }
+      rs_put_pv(r, 0, x), rs_put_pv(r, 1, xI), rs_put_pv(r, 2, xPrev), rs_put_pv(r, 3, xHead);
+      rs_put_pv(r, 4, x0), rs_put_pv(r, 5, eta_now);
+      rs_put(r, 18, y), rs_put(r, 19, yI), rs_put(r, 20, y0);
+    };
     Info info{};
-    bool have_info = false;
+    bool have_info = resume;   // a resumed instance is inside an inner iteration: info is set before use
     const bool save_inner = P.opt.save_inner_iteration != 0;
     while (true) {
-      // outer loop head, RIPTRM.py:931-959
       double ev[10];
+      double tn = 0.0;
+     if (rph == 0) {
+      // outer loop head, RIPTRM.py:931-959
       evaluation(xHead, x, y, ev);
-      double tn = now();
+      tn = now();
       if (outer_it == 0.0 || !save_inner)
         log_row(ev, outer_it, mu, (outer_it != 0.0 && have_info) ? &info : nullptr, last_j + 1.0, tn, t_start,
                 log_count, log_over);
@@ -1095,17 +1227,18 @@ struct Eng {
         Delta = P.opt.initial_tr_radius;
       }
       outer_it += 1.0;
+      x0 = x;
+      y0 = y;
+      Delta0 = Delta;
+      xPrev = x;
+      inner_it = 0.0;
+      t_inner = now();
+     }
       const int ti = (int)mu_idx < P.tab_len ? (int)mu_idx : P.tab_len - 1;
       const double tolL = P.tolL_tab[ti], tolC = P.tolC_tab[ti];
-      const PV x0 = x;
-      const double y0 = y;
-      const double Delta0 = Delta;
-      xPrev = x;
-      double inner_it = 0.0;
-      const double t_inner = now();
       while (true) {  // inner_run, RIPTRM.py:785-847
-        inner_it += 1.0;
-        const double DeltaStep = Delta;
+        if (rph == 0) inner_it += 1.0;
+        const double DeltaStep = Delta;   // a parked instance resumes with Delta unchanged
         double tq = tick();
         AtX a;
         prepare(a, x, y, mu);
@@ -1114,7 +1247,27 @@ struct Eng {
         PV eta, Heta;
         int jj = 0;
         const bool exact = P.opt.trs_solver == RIPTRM_TRS_SOLVER_EXACT_REPMAT;
-        const int tstop = exact ? trs_direction(a, Delta, eta, hvps) : tcg(a, Delta, eta, Heta, jj, hvps);
+        int tstop;
+        if constexpr (HBMT) {
+          if (exact && rph == 0) {   // the matrix to HBM, park; the host solves TRSgep
+            const Frame F = frame(a.x);
+            repmat_hbm(a, F, hvps, true);
+            park((int)riptrm::PH_TRS_HOST, 0, PV{0.0, 0.0, 0.0});
+            return;
+          }
+          if (exact && rph == 1) {
+            const Frame F = frame(a.x);
+            eta = from_coords(F, P.trsx + (int64_t)b * TDP);
+            tstop = P.trskind[b];
+          } else if (exact) {
+            eta = eta_r;
+            tstop = tstop_r;
+          } else {
+            tstop = tcg(a, Delta, eta, Heta, jj, hvps);
+          }
+        } else {
+          tstop = exact ? trs_direction(a, Delta, eta, hvps) : tcg(a, Delta, eta, Heta, jj, hvps);
+        }
         if (exact) jj = -1;   // no tCG iterations
         pt[RIPTRM_SI_PROF_TCG] += tick() - tq;
         tq = tick();
@@ -1141,12 +1294,26 @@ struct Eng {
         have_info = true;
         bool mineig_ok = true;
         if (exact && P.opt.second_order_stationarity) {   // RIPTRM.py:599-613
-          const double me = mineig_at(xN, yN, mu, hvps);
+          double me;
+          if constexpr (HBMT) {
+            if (rph != 2) {   // HwNew's matrix to HBM, park; the host computes its eigenvalues
+              AtX aN;
+              prepare(aN, xN, yN, mu);
+              const Frame F = frame(xN);
+              repmat_hbm(aN, F, hvps, false);
+              park((int)riptrm::PH_MINEIG_HOST, tstop, eta);
+              return;
+            }
+            me = P.trsmin[b];
+          } else {
+            me = mineig_at(xN, yN, mu, hvps);
+          }
           const double tol2 = P.opt.tol2_table ? P.opt.tol2_table[ti] : mu;
           mineig_ok = me >= -tol2;
           info.hasmin = 1.0;
           info.mineig = me;
         }
+        rph = 0;
         bool converged = false;
         double fN = 0.0, AN2 = 0.0;
         if (xfeas) {
@@ -1313,7 +1480,7 @@ __global__ void __launch_bounds__(si_threads(D)) k_si(SIParams P) {
   const int b = blockIdx.x;
   if (b >= P.batch) return;
   Eng<D> e(P, b, sh, ser, crs, ccs, trs_lds);
-  if (P.mode == MODE_SOLVE) e.solve();
+  if (P.mode == MODE_SOLVE || P.mode == MODE_RESUME) e.solve(P.mode == MODE_RESUME);
   else if (P.mode == MODE_HVP) e.op_hvp();
   else e.op_tcg();
 }
@@ -1365,6 +1532,19 @@ static SIParams si_params(riptrm_ctx* c, int mode) {
   P.stats = (double*)(s->ws + s->L.off_stats);
   P.log = (double*)(s->ws + s->L.off_log);
   P.prof = s->prof_on ? s->prof : nullptr;
+  if (si_hbm_trs(P.d)) {
+    P.trsA = (double*)(s->ws + s->L.off_tA);
+    P.trsw = (double*)(s->ws + s->L.off_tw);
+    P.trsa = (double*)(s->ws + s->L.off_ta);
+    P.trsx = (double*)(s->ws + s->L.off_tx);
+    P.trsD = (double*)(s->ws + s->L.off_tD);
+    P.trslam = (double*)(s->ws + s->L.off_tlam);
+    P.trskind = (int32_t*)(s->ws + s->L.off_tkind);
+    P.trsmin = (double*)(s->ws + s->L.off_tmin);
+    P.rs = (double*)(s->ws + s->L.off_rs);
+    P.tdim = si_manifold_dim(P.d);
+    P.tdp = si_tdp(P.d);
+  }
   P.opt.struct_size = (int32_t)sizeof(riptrm_options);
   P.opt.tcg_theta = 1.0;   // RIPTRM.py:330-332 defaults for the operator entry points
   P.opt.tcg_kappa = 0.1;
@@ -1372,13 +1552,12 @@ static SIParams si_params(riptrm_ctx* c, int mode) {
   return P;
 }
 
-static int si_manifold_dim(int d) { return d * (d - 1) / 2 + d * (d + 1); }
-
 template <int D>
 static int si_launch_d(riptrm_ctx* c, const SIParams& P) {
-  const bool exact = P.mode == MODE_SOLVE && P.opt.trs_solver == RIPTRM_TRS_SOLVER_EXACT_REPMAT;
+  const bool exact = (P.mode == MODE_SOLVE || P.mode == MODE_RESUME) && P.opt.trs_solver == RIPTRM_TRS_SOLVER_EXACT_REPMAT;
   const size_t shm = D > 8 ? (size_t)si_big_lds_doubles(D) * sizeof(double)
-                           : exact ? (size_t)riptrm_trs::work_doubles(si_manifold_dim(D)) * sizeof(double) : 0;
+                     : (exact && !si_hbm_trs(D)) ? (size_t)riptrm_trs::work_doubles(si_manifold_dim(D)) * sizeof(double)
+                                                 : 0;
   if (shm > 64 * 1024)
     HIPCHK(c, hipFuncSetAttribute((const void*)k_si<D>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm));
   hipLaunchKernelGGL(k_si<D>, dim3((unsigned)P.batch), dim3(si_threads(D)), shm, c->stream, P);
@@ -1503,8 +1682,11 @@ int riptrm_si_solve(riptrm_ctx* ctx, const riptrm_options* opt, const double* x0
   if (opt->log_capacity > ctx->si->cap) return fail(ctx, RIPTRM_E_ARG, "si_solve: log_capacity exceeds bound capacity");
   if (opt->trs_solver != RIPTRM_TRS_SOLVER_TCG && opt->trs_solver != RIPTRM_TRS_SOLVER_EXACT_REPMAT)
     return fail(ctx, RIPTRM_E_ARG, "si_solve: unknown trs_solver");
-  if (opt->trs_solver == RIPTRM_TRS_SOLVER_EXACT_REPMAT && si_manifold_dim(ctx->si->prob.d) > RIPTRM_TRS_DIM_MAX)
-    return fail(ctx, RIPTRM_E_ARG, "si_solve: Exact_RepMat needs manifold.dim <= RIPTRM_TRS_DIM_MAX (d <= 7)");
+  const int d = ctx->si->prob.d, tdim = si_manifold_dim(d);
+  const bool hbm = opt->trs_solver == RIPTRM_TRS_SOLVER_EXACT_REPMAT && si_hbm_trs(d);
+  if (hbm && (!ctx->big_ws || ctx->big_order < tdim || ctx->big_slots < 1))
+    return fail(ctx, RIPTRM_E_STATE, "si_solve: Exact_RepMat above RIPTRM_TRS_DIM_MAX (d >= 8) needs "
+                                     "riptrm_trs_bind_workspace(order >= manifold.dim) first");
   HIPCHK(ctx, hipSetDevice(ctx->device));
   SIParams P = si_params(ctx, MODE_SOLVE);
   P.opt = *opt;
@@ -1514,7 +1696,35 @@ int riptrm_si_solve(riptrm_ctx* ctx, const riptrm_options* opt, const double* x0
   P.tolL_tab = tolL_table;
   P.tolC_tab = tolC_table;
   P.tab_len = table_len;
-  return si_launch(ctx, P);
+  if (int rc = si_launch(ctx, P)) return rc;
+  if (!hbm) return RIPTRM_OK;
+  // HBM subproblem path: the kernel parks an instance at each subproblem (and each trial point's
+  // eigenvalue test); serve every parked instance in batched passes, resume, until none is parked
+  const int B = ctx->si->batch;
+  std::vector<double> st((size_t)B * RIPTRM_STAT_NFIELDS);
+  P.mode = MODE_RESUME;
+  while (true) {
+    HIPCHK(ctx, hipMemcpyAsync(st.data(), P.stats, st.size() * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    std::vector<int32_t> trs, mine;
+    for (int b = 0; b < B; ++b) {
+      const double ph = st[(size_t)b * RIPTRM_STAT_NFIELDS + RIPTRM_STAT_PHASE];
+      if (ph == (double)riptrm::PH_TRS_HOST) trs.push_back(b);
+      else if (ph == (double)riptrm::PH_MINEIG_HOST) mine.push_back(b);
+    }
+    if (trs.empty() && mine.empty()) break;
+    const int64_t tp = si_tdp(d);
+    if (!trs.empty())
+      if (int rc = riptrm_big_gep_ids(ctx, tdim, trs.data(), (int)trs.size(), P.trsA, tdim, (int64_t)tdim * tdim, P.trsa,
+                                      tp, P.trsD, opt->trs_tolhardcase, P.trsx, P.trslam, P.trskind, nullptr, false))
+        return rc;
+    if (!mine.empty())
+      if (int rc = riptrm_big_gep_ids(ctx, tdim, mine.data(), (int)mine.size(), P.trsA, tdim, (int64_t)tdim * tdim,
+                                      P.trsa, tp, P.trsD, opt->trs_tolhardcase, nullptr, nullptr, nullptr, P.trsmin, true))
+        return rc;
+    if (int rc = si_launch(ctx, P)) return rc;
+  }
+  return RIPTRM_OK;
 }
 
 int riptrm_si_profile_enable(riptrm_ctx* ctx, int32_t on) {

@@ -671,6 +671,13 @@ __global__ void __launch_bounds__(256) k_gep_out(Bat B, int m, int64_t ldv, doub
   }
 }
 
+// the smallest eigenvalue of slot k (eigenvalues ascending) -> mineig[ids[k]]
+__global__ void k_min_out(Bat B, int cnt, double* mineig) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= cnt) return;
+  mineig[B.ids[k]] = slot_at(B, k).v[VS_EV][0];
+}
+
 // copy subproblem ids[k]'s m x m block (row-major, lda) into slot k's matrix (lda m) and a
 __global__ void __launch_bounds__(256) k_load(Bat B, int m, const double* A, int64_t lda, int64_t a_stride,
                                               const double* a, int64_t ldv) {
@@ -1050,33 +1057,53 @@ int riptrm_big_reset_cache(riptrm_ctx* c) {
   return RIPTRM_OK;
 }
 
-// riptrm_trs_gep for dim > RIPTRM_TRS_DIM_MAX: up to big_slots subproblems per pass
-int riptrm_big_trs_gep(riptrm_ctx* c, int dim, int batch, const double* A, int64_t lda, int64_t a_stride, const double* a,
-                       int64_t ldv, const double* Delta, double tolhc, double* x, double* lam1, int32_t* kind,
-                       double* mineig) {
+// TRSgep for the subproblems ids[0..count) of a batch laid out as riptrm_trs_gep's arguments (or,
+// mineig_only, just the smallest eigenvalue of each A: RIPTRM.py:611), up to big_slots per pass.
+// A non-converged eigensolve fails the call naming the subproblem (scipy.linalg.eig raises there).
+// Synchronises.  Serves riptrm_trs_gep above dim 96 and the StableIdentification solve's parked
+// instances (riptrm_si.hip).
+int riptrm_big_gep_ids(riptrm_ctx* c, int dim, const int32_t* sel, int count, const double* A, int64_t lda,
+                       int64_t a_stride, const double* a, int64_t ldv, const double* Delta, double tolhc, double* x,
+                       double* lam1, int32_t* kind, double* mineig, bool mineig_only) {
   if (!c->big_ws || c->big_order < dim || c->big_slots < 1)
-    return fail(c, RIPTRM_E_STATE, "trs_gep above dim 96 needs riptrm_trs_bind_workspace (order >= dim)");
+    return fail(c, RIPTRM_E_STATE, "Exact_RepMat above dim 96 needs riptrm_trs_bind_workspace (order >= dim)");
   const Bat Bt = bat_of(c);
-  std::vector<int32_t> ids(c->big_slots), info(c->big_slots);
-  for (int b0 = 0; b0 < batch; b0 += c->big_slots) {
-    const int cnt = std::min(c->big_slots, batch - b0);
-    for (int k = 0; k < cnt; ++k) ids[k] = b0 + k;
-    if (int rc = put_ids(c, Bt, ids.data(), cnt)) return rc;
+  std::vector<int32_t> info(c->big_slots);
+  for (int b0 = 0; b0 < count; b0 += c->big_slots) {
+    const int cnt = std::min(c->big_slots, count - b0);
+    if (int rc = put_ids(c, Bt, sel + b0, cnt)) return rc;
     hipLaunchKernelGGL(k_load, dim3(blocks_of((int64_t)dim * dim, 256), cnt), dim3(256), 0, c->stream, Bt, dim, A, lda,
                        a_stride, a, ldv);
     HIPCHK(c, hipGetLastError());
-    if (int rc = big_solve(c, Bt, cnt, 0, dim, dim, Delta, 1, tolhc)) return rc;
+    if (mineig_only) {
+      if (int rc = eig_batched(c, Bt, cnt, false, dim, 0, dim)) return rc;
+    } else if (int rc = big_solve(c, Bt, cnt, 0, dim, dim, Delta, 1, tolhc)) {
+      return rc;
+    }
     HIPCHK(c, hipMemcpyAsync(info.data(), Bt.infos, (size_t)cnt * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     for (int k = 0; k < cnt; ++k)
-      if (info[k] != 0)   // scipy.linalg.eig raises LinAlgError here
-        return fail(c, RIPTRM_E_HIP, "trs_gep: rocsolver_dsyevd did not converge (info " + std::to_string(info[k]) +
-                                         ") on subproblem " + std::to_string(b0 + k));
-    hipLaunchKernelGGL(k_gep_out, dim3(blocks_of(dim, 256), cnt), dim3(256), 0, c->stream, Bt, dim, ldv, x, lam1, kind,
-                       mineig);
+      if (info[k] != 0)
+        return fail(c, RIPTRM_E_HIP, "Exact_RepMat: rocsolver_dsyevd did not converge (info " + std::to_string(info[k]) +
+                                         ") on subproblem " + std::to_string(sel[b0 + k]));
+    if (mineig_only)
+      hipLaunchKernelGGL(k_min_out, dim3(blocks_of(cnt, 64)), dim3(64), 0, c->stream, Bt, cnt, mineig);
+    else
+      hipLaunchKernelGGL(k_gep_out, dim3(blocks_of(dim, 256), cnt), dim3(256), 0, c->stream, Bt, dim, ldv, x, lam1, kind,
+                         mineig);
     HIPCHK(c, hipGetLastError());
   }
   return RIPTRM_OK;
+}
+
+// riptrm_trs_gep for dim > RIPTRM_TRS_DIM_MAX
+int riptrm_big_trs_gep(riptrm_ctx* c, int dim, int batch, const double* A, int64_t lda, int64_t a_stride, const double* a,
+                       int64_t ldv, const double* Delta, double tolhc, double* x, double* lam1, int32_t* kind,
+                       double* mineig) {
+  std::vector<int32_t> ids(batch);
+  for (int b = 0; b < batch; ++b) ids[b] = b;
+  return riptrm_big_gep_ids(c, dim, ids.data(), batch, A, lda, a_stride, a, ldv, Delta, tolhc, x, lam1, kind, mineig,
+                            false);
 }
 
 extern "C" {

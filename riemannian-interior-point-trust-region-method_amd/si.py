@@ -274,6 +274,7 @@ class SIBatch:
         self.ws_bytes = nbytes
         self._keep: List[torch.Tensor] = []
         self.ro: Optional[ResolvedOptions] = None
+        self._trs_ws: Optional[torch.Tensor] = None   # Exact_RepMat at d >= 8 (manifold.dim > 96)
 
     def _view(self, kind: int, shape):
         off = int(self.lib.riptrm_si_workspace_offset(self.d, self.N, self.m, self.batch, self.cap, kind))
@@ -359,9 +360,21 @@ class SIBatch:
         ro = resolve_options(option, typical, self.cap, restart_every, manvio_classifier=si_manvio_kind)
         X = self._dev(x0, (self.batch, 3, d, d))
         Y = self._dev(y0, (self.batch, self.m))
-        if ro.exact and d * (d - 1) // 2 + d * (d + 1) > C["RIPTRM_TRS_DIM_MAX"]:
-            raise NotImplementedError(f"TRS_solver='Exact_RepMat' on the GPU needs manifold.dim <= "
-                                      f"{C['RIPTRM_TRS_DIM_MAX']} (d <= 7)")
+        tdim = d * (d - 1) // 2 + d * (d + 1)
+        if ro.exact and tdim > C["RIPTRM_TRS_DIM_MAX"]:
+            # d >= 8: the subproblem's matrix (manifold.dim squared) no longer fits LDS; instances park
+            # at each subproblem and the host's batched service (riptrm_trs_big.hip) solves them in
+            # caller-owned HBM scratch, one slot per instance of a pass (riptrm_trs_bind_workspace)
+            from engine import trs_workspace_slots
+            slots = trs_workspace_slots(self.lib, tdim, self.batch)
+            if self._trs_ws is None:
+                nbytes = int(self.lib.riptrm_trs_workspace_bytes(tdim, slots))
+                self._trs_ws = torch.empty(nbytes + 256, dtype=torch.uint8, device=self.device)
+            base = self._trs_ws.data_ptr()
+            ptr = base + (-base) % 256
+            self.ctx.check(self.lib.riptrm_trs_bind_workspace(self.ctx.h, ctypes.c_void_p(ptr),
+                                                              self._trs_ws.numel() - (ptr - base), tdim, slots),
+                           "riptrm_trs_bind_workspace")
         tabs = ro.device_tables(self.device)
         self._keep = [X, Y] + tabs
         self.ctx.set_stream(_stream_handle(self.device))

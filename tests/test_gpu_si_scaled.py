@@ -129,3 +129,36 @@ def test_si_scaled_trajectory_matches_oracle(d):
                 dg = column_deviation(pre(gl), pre(ref.log), key)
                 dc = column_deviation(pre(ref2.log), pre(ref.log), key)
                 assert dg <= 10.0 * dc + 1e-12, (d, b, flip, f2, key, dg, dc)
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("d,sos,inner", [(8, True, 6), (16, False, 2)])
+def test_si_scaled_exact_repmat_hbm(d, sos, inner):
+    """TRS_solver = 'Exact_RepMat' past d = 7 (RIPTRM.py:433-444, :599-617 with TRSgep :218-299):
+    manifold.dim = 100 (d = 8) / 392 (d = 16) > RIPTRM_TRS_DIM_MAX, so each instance builds the matrix
+    of HwCur (manifold.dim HVPs) in HBM and parks; riptrm_si_solve serves the parked instances in
+    batched passes of the NonnegPCA HBM path (SciPy CG, rocSOLVER dsyevd, secular solve) and
+    relaunches.  Bars: an instance's trajectory is bitwise the one it has solved alone (a slot's
+    arithmetic does not depend on its pass), and each instance's rows meet compare_until_flip's bar
+    against the oracle (trs_oracle: the reference's 2n x 2n pencil).  One outer iteration with a
+    few inner ones: the oracle's own cost at these sizes (~2 s per inner iteration at d = 8 with the
+    second-order test, ~14 s at d = 16) bounds the window."""
+    import si
+    from parity import compare_until_flip
+    data, st = _inst(d, 2)
+    xs = np.stack([x for x, _ in st])
+    ys = np.stack([y for _, y in st])
+    opt = {"maxiter": 1, "inner_maxiter": inner, "tolresid": 0.0, "maxtime": 1e9, "TRS_solver": "Exact_RepMat",
+           "second_order_stationarity": sos}
+    res = _batch(data, 2).solve(xs, ys, dict(opt, manviofun=si.si_manviofun))
+    alone = _batch(data, 1).solve(xs[1:], ys[1:], dict(opt, manviofun=si.si_manviofun))
+    for key in ("cost", "residual", "normdx", "mineigvalHw", "dxtype"):
+        assert res.log(1)[key] == alone.log(0)[key], key
+    np.testing.assert_array_equal(res.x[1].cpu().numpy(), alone.x[0].cpu().numpy())
+    for b in range(2):
+        gl = res.log(b)
+        kinds = [k for k in gl["dxtype"] if k is not None]
+        assert 0 < len(kinds) <= inner and all(k in ("boundary", "interior", "hardcase_1") for k in kinds), kinds
+        assert (len([v for v in gl["mineigvalHw"] if v is not None]) > 0) == sos
+        ref = SI.solve(data, xs[b], ys[b], dict(opt, manviofun=SI.si_manvio))
+        compare_until_flip(gl, ref.log)
