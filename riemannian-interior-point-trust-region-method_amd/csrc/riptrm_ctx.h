@@ -86,7 +86,7 @@ void riptrm_big_release(riptrm_ctx* c);
 int riptrm_big_reset_cache(riptrm_ctx* c);
 int riptrm_big_gep_ids(riptrm_ctx* c, int dim, const int32_t* sel, int count, const double* A, int64_t lda,
                        int64_t a_stride, const double* a, int64_t ldv, const double* Delta, double tolhc, double* x,
-                       double* lam1, int32_t* kind, double* mineig, bool mineig_only);
+                       double* lam1, int32_t* kind, double* mineig, bool mineig_only, bool per_instance);
 
 
 inline int fail(riptrm_ctx* c, int code, const std::string& msg) {

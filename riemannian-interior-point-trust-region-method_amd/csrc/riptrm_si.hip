@@ -1146,6 +1146,7 @@ struct Eng {
     double t_start, t_tick0, Delta0 = 0.0, inner_it = 0.0, t_inner = 0.0;
     int rph = 0;       // resumed: 1 with the subproblem's solution, 2 with HwNew's smallest eigenvalue
     int tstop_r = 0;   // the direction type of a phase-2 resume
+    int err = RIPTRM_ERR_NONE;   // RIPTRM_ERR_EIGEN: the host's eigensolve failed (RIPTRM.py:961-966 break)
     if (!resume) {
       x = load_pv(P.in_x + b * v3);
       y = cact ? P.in_y[(int64_t)b * m + l] : 0.0;
@@ -1255,6 +1256,10 @@ struct Eng {
             park((int)riptrm::PH_TRS_HOST, 0, PV{0.0, 0.0, 0.0});
             return;
           }
+          if (exact && rph == 1 && P.trskind[b] == RIPTRM_TCG_EIGFAIL) {
+            err = RIPTRM_ERR_EIGEN;   // scipy.linalg.eig raised inside outer_step
+            break;
+          }
           if (exact && rph == 1) {
             const Frame F = frame(a.x);
             eta = from_coords(F, P.trsx + (int64_t)b * TDP);
@@ -1305,6 +1310,10 @@ struct Eng {
               return;
             }
             me = P.trsmin[b];
+            if (!isfinite(me)) {   // the eigensolve failed (scipy raises inside outer_step)
+              err = RIPTRM_ERR_EIGEN;
+              break;
+            }
           } else {
             me = mineig_at(xN, yN, mu, hvps);
           }
@@ -1406,6 +1415,12 @@ struct Eng {
         }
         if (exitflag) break;
       }
+      if (err != RIPTRM_ERR_NONE) {   // the reference's do_exit_on_error break: the outer step's start
+        x = x0;
+        y = y0;
+        stop_rt = (now() - t_start) / P.clock_hz;
+        break;
+      }
       // outer_step tail, RIPTRM.py:889-896
       mu_idx += 1.0;
       mu = mu_at((int)mu_idx);
@@ -1426,7 +1441,8 @@ struct Eng {
       o[RIPTRM_STAT_FINAL_RESIDUAL] = residual;
       o[RIPTRM_STAT_LOG_COUNT] = log_count;
       o[RIPTRM_STAT_LOG_OVERFLOW] = log_over;
-      o[RIPTRM_STAT_PHASE] = riptrm::PH_DONE;
+      o[RIPTRM_STAT_PHASE] = err != RIPTRM_ERR_NONE ? riptrm::PH_ERROR : riptrm::PH_DONE;
+      o[RIPTRM_STAT_ERROR] = err;
       o[RIPTRM_STAT_MU] = mu;
       o[RIPTRM_STAT_TR_RADIUS] = Delta;
       o[RIPTRM_STAT_TCG_LAST_J] = last_j;
@@ -1716,11 +1732,13 @@ int riptrm_si_solve(riptrm_ctx* ctx, const riptrm_options* opt, const double* x0
     const int64_t tp = si_tdp(d);
     if (!trs.empty())
       if (int rc = riptrm_big_gep_ids(ctx, tdim, trs.data(), (int)trs.size(), P.trsA, tdim, (int64_t)tdim * tdim, P.trsa,
-                                      tp, P.trsD, opt->trs_tolhardcase, P.trsx, P.trslam, P.trskind, nullptr, false))
+                                      tp, P.trsD, opt->trs_tolhardcase, P.trsx, P.trslam, P.trskind, nullptr, false,
+                                      true))
         return rc;
     if (!mine.empty())
       if (int rc = riptrm_big_gep_ids(ctx, tdim, mine.data(), (int)mine.size(), P.trsA, tdim, (int64_t)tdim * tdim,
-                                      P.trsa, tp, P.trsD, opt->trs_tolhardcase, nullptr, nullptr, nullptr, P.trsmin, true))
+                                      P.trsa, tp, P.trsD, opt->trs_tolhardcase, nullptr, nullptr, nullptr, P.trsmin, true,
+                                      true))
         return rc;
     if (int rc = si_launch(ctx, P)) return rc;
   }

@@ -671,11 +671,13 @@ __global__ void __launch_bounds__(256) k_gep_out(Bat B, int m, int64_t ldv, doub
   }
 }
 
-// the smallest eigenvalue of slot k (eigenvalues ascending) -> mineig[ids[k]]
+// the smallest eigenvalue of slot k (eigenvalues ascending) -> mineig[ids[k]]; NaN when the
+// eigensolve did not converge
 __global__ void k_min_out(Bat B, int cnt, double* mineig) {
   const int k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= cnt) return;
-  mineig[B.ids[k]] = slot_at(B, k).v[VS_EV][0];
+  const Slot q = slot_at(B, k);
+  mineig[B.ids[k]] = *q.info != 0 ? NAN : q.v[VS_EV][0];
 }
 
 // copy subproblem ids[k]'s m x m block (row-major, lda) into slot k's matrix (lda m) and a
@@ -1059,12 +1061,13 @@ int riptrm_big_reset_cache(riptrm_ctx* c) {
 
 // TRSgep for the subproblems ids[0..count) of a batch laid out as riptrm_trs_gep's arguments (or,
 // mineig_only, just the smallest eigenvalue of each A: RIPTRM.py:611), up to big_slots per pass.
-// A non-converged eigensolve fails the call naming the subproblem (scipy.linalg.eig raises there).
-// Synchronises.  Serves riptrm_trs_gep above dim 96 and the StableIdentification solve's parked
+// A non-converged eigensolve fails the call naming the subproblem (scipy.linalg.eig raises there),
+// or, with per_instance, only marks that subproblem: kind = RIPTRM_TCG_EIGFAIL / mineig = NaN (the
+// caller stops that instance, RIPTRM_ERR_EIGEN).  Synchronises.  Serves riptrm_trs_gep above dim 96 and the StableIdentification solve's parked
 // instances (riptrm_si.hip).
 int riptrm_big_gep_ids(riptrm_ctx* c, int dim, const int32_t* sel, int count, const double* A, int64_t lda,
                        int64_t a_stride, const double* a, int64_t ldv, const double* Delta, double tolhc, double* x,
-                       double* lam1, int32_t* kind, double* mineig, bool mineig_only) {
+                       double* lam1, int32_t* kind, double* mineig, bool mineig_only, bool per_instance) {
   if (!c->big_ws || c->big_order < dim || c->big_slots < 1)
     return fail(c, RIPTRM_E_STATE, "Exact_RepMat above dim 96 needs riptrm_trs_bind_workspace (order >= dim)");
   const Bat Bt = bat_of(c);
@@ -1083,7 +1086,7 @@ int riptrm_big_gep_ids(riptrm_ctx* c, int dim, const int32_t* sel, int count, co
     HIPCHK(c, hipMemcpyAsync(info.data(), Bt.infos, (size_t)cnt * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     for (int k = 0; k < cnt; ++k)
-      if (info[k] != 0)
+      if (info[k] != 0 && !per_instance)
         return fail(c, RIPTRM_E_HIP, "Exact_RepMat: rocsolver_dsyevd did not converge (info " + std::to_string(info[k]) +
                                          ") on subproblem " + std::to_string(sel[b0 + k]));
     if (mineig_only)
@@ -1092,6 +1095,12 @@ int riptrm_big_gep_ids(riptrm_ctx* c, int dim, const int32_t* sel, int count, co
       hipLaunchKernelGGL(k_gep_out, dim3(blocks_of(dim, 256), cnt), dim3(256), 0, c->stream, Bt, dim, ldv, x, lam1, kind,
                          mineig);
     HIPCHK(c, hipGetLastError());
+    if (!mineig_only) {
+      static const int32_t eigfail = RIPTRM_TCG_EIGFAIL;
+      for (int k = 0; k < cnt; ++k)
+        if (info[k] != 0)
+          HIPCHK(c, hipMemcpyAsync(kind + sel[b0 + k], &eigfail, sizeof(int32_t), hipMemcpyHostToDevice, c->stream));
+    }
   }
   return RIPTRM_OK;
 }
@@ -1103,7 +1112,7 @@ int riptrm_big_trs_gep(riptrm_ctx* c, int dim, int batch, const double* A, int64
   std::vector<int32_t> ids(batch);
   for (int b = 0; b < batch; ++b) ids[b] = b;
   return riptrm_big_gep_ids(c, dim, ids.data(), batch, A, lda, a_stride, a, ldv, Delta, tolhc, x, lam1, kind, mineig,
-                            false);
+                            false, false);
 }
 
 extern "C" {

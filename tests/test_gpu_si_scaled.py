@@ -162,3 +162,33 @@ def test_si_scaled_exact_repmat_hbm(d, sos, inner):
         assert (len([v for v in gl["mineigvalHw"] if v is not None]) > 0) == sos
         ref = SI.solve(data, xs[b], ys[b], dict(opt, manviofun=SI.si_manvio))
         compare_until_flip(gl, ref.log)
+
+
+@pytest.mark.timeout(600)
+def test_si_exact_hbm_eigensolve_failure_stops_one_instance():
+    """bench.si_starts' start 30 at d = 8 drives the subproblem's eigensolve to non-convergence
+    within two outer iterations -- on the CPU as well: there the oracle's scipy.linalg.eig raises
+    LinAlgError (LAPACK ggev info 111) on the reference's pencil.  The reference's do_exit_on_error
+    break (RIPTRM.py:961-966) ends that run with the iterate its outer step started from; the device
+    stops only that instance (stats.error = RIPTRM_ERR_EIGEN), and the healthy instance of the same
+    batch is bitwise the one solved alone."""
+    import bench
+    import si
+    from engine import C
+    xs, ys, (X, XP, h, constset) = bench.si_starts(2, [30, 1], 8)
+    cons = si.expand_constset(constset)
+    opt = {"maxiter": 2, "tolresid": 0.0, "maxtime": 1e9, "TRS_solver": "Exact_RepMat",
+           "second_order_stationarity": True, "manviofun": si.si_manviofun}
+
+    def run(sel):
+        eng = si.SIBatch(8, X.shape[1], cons.shape[0], len(sel), log_capacity=1024)
+        eng.load(X, XP, h, cons)
+        return eng.solve(xs[sel], ys[sel], opt)
+
+    both, alone = run([0, 1]), run([1])
+    assert int(both.stats[0, C["RIPTRM_STAT_ERROR"]]) == C["RIPTRM_ERR_EIGEN"]
+    assert int(both.stats[1, C["RIPTRM_STAT_ERROR"]]) == C["RIPTRM_ERR_NONE"]
+    assert np.all(np.isfinite(both.x[0].cpu().numpy()))
+    for key in ("cost", "residual", "normdx", "mineigvalHw"):
+        assert both.log(1)[key] == alone.log(0)[key], key
+    np.testing.assert_array_equal(both.x[1].cpu().numpy(), alone.x[0].cpu().numpy())
