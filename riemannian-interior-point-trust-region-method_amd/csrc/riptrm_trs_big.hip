@@ -754,6 +754,7 @@ typedef int (*fn_syevd_sb_t)(void*, int, int, int, double*, int, int64_t, double
 typedef int (*fn_syevj_sb_t)(void*, int, int, int, int, double*, int, int64_t, double, double*, int, int*, double*, int64_t,
                              int*, int);
 typedef int (*fn_syevdj_sb_t)(void*, int, int, int, double*, int, int64_t, double*, int64_t, int*, int);
+typedef int (*fn_syevd_t)(void*, int, int, int, double*, int, double*, double*, int*);
 constexpr int EVECT_ORIGINAL = 211, EVECT_NONE = 213, FILL_UPPER = 121, ESORT_ASCENDING = 252;
 
 struct Solver {
@@ -765,6 +766,7 @@ struct Solver {
   fn_syevd_sb_t syevd_sb = nullptr;
   fn_syevj_sb_t syevj_sb = nullptr;     // A/B only (RIPTRM_BIG_EIG)
   fn_syevdj_sb_t syevdj_sb = nullptr;
+  fn_syevd_t syevd = nullptr;           // one matrix per call (large orders)
 };
 
 static Solver& solver() {
@@ -795,6 +797,7 @@ static Solver& solver() {
   s.syevd_sb = (fn_syevd_sb_t)dlsym(sol, "rocsolver_dsyevd_strided_batched");
   s.syevj_sb = (fn_syevj_sb_t)dlsym(sol, "rocsolver_dsyevj_strided_batched");
   s.syevdj_sb = (fn_syevdj_sb_t)dlsym(sol, "rocsolver_dsyevdj_strided_batched");
+  s.syevd = (fn_syevd_t)dlsym(sol, "rocsolver_dsyevd");
   s.ok = s.create && s.set_stream && s.destroy && s.syevd_sb;
   if (!s.ok)
     s.why = "rocBLAS / rocSOLVER lack rocblas_create_handle / rocblas_set_stream / rocsolver_dsyevd_strided_batched";
@@ -855,6 +858,11 @@ static int eig_batched(riptrm_ctx* c, const Bat& B, int cnt, bool vectors, int m
                     B.infos, cnt);
   } else if (e && e[0] == 'd' && e[1] == 'j' && s.syevdj_sb) {
     st = s.syevdj_sb(c->big_handle, ev, FILL_UPPER, m, A, lda, B.sd, W, B.sd, B.infos, cnt);
+  } else if (e && e[0] == 's' && s.syevd) {   // one rocsolver_dsyevd call per matrix
+    st = 0;
+    for (int k = 0; k < cnt && st == 0; ++k)
+      st = s.syevd(c->big_handle, ev, FILL_UPPER, m, A + k * B.sd, lda, W + k * B.sd, B.base + off_vec(B.N, VS_EW) + k * B.sd,
+                   B.infos + k);
   } else {
     st = s.syevd_sb(c->big_handle, ev, FILL_UPPER, m, A, lda, B.sd, W, B.sd, B.base + off_vec(B.N, VS_EW), B.sd, B.infos,
                     cnt);
