@@ -105,6 +105,33 @@ def test_layout_functions(built_lib):
     assert built_lib.riptrm_nonnegpca_s_elems(10, 5) == -1
 
 
+def test_exact_hbm_scratch_sizes(built_lib, monkeypatch):
+    """Host-side sizing of the HBM Exact_RepMat path: the per-instance eigendecomposition cache
+    (n^2 + 3 vpad(n) + 8 doubles per instance, vpad = n rounded up to 64), the engine's all-or-none cache budget, and the SI
+    workspace's extra regions once manifold.dim = d(d-1)/2 + d(d+1) exceeds RIPTRM_TRS_DIM_MAX
+    (d >= 8: the subproblem matrix, coordinates, service outputs and resume records)."""
+    import engine
+    vpad = lambda n: -(-n // 64) * 64
+    for n, B in ((98, 1), (200, 64), (1000, 3)):
+        assert built_lib.riptrm_trs_cache_bytes(n, B) == (n * n + 3 * vpad(n) + 8) * 8 * B
+    assert built_lib.riptrm_trs_cache_bytes(0, 4) == 0 and built_lib.riptrm_trs_cache_bytes(4, 0) == 0
+    assert engine.trs_cache_wanted(built_lib, 200, 64) == built_lib.riptrm_trs_cache_bytes(200, 64)
+    monkeypatch.setenv("RIPTRM_TRS_CACHE_GB", "0.001")
+    assert engine.trs_cache_wanted(built_lib, 200, 64) == 0   # the whole batch or nothing
+    monkeypatch.delenv("RIPTRM_TRS_CACHE_GB")
+    monkeypatch.setenv("RIPTRM_TRS_CACHE", "0")
+    assert engine.trs_cache_wanted(built_lib, 200, 64) == 0
+    ws = lambda d: built_lib.riptrm_si_workspace_bytes(d, 95, 16, 4, 64)
+    dim = lambda d: d * (d - 1) // 2 + d * (d + 1)
+    assert dim(7) <= N.CONST["RIPTRM_TRS_DIM_MAX"] < dim(8)
+    nt = lambda d: 64 if d <= 8 else -(-d * d // 64) * 64
+    for d in (8, 12, 16):
+        # at least the 4 subproblem matrices and 4 resume records on top of the tCG layout's share
+        extra = 4 * 8 * (dim(d) ** 2 + 32 + 21 * nt(d))
+        assert ws(d) >= extra, d
+    assert ws(8) - ws(7) > 4 * 8 * dim(8) ** 2
+
+
 @pytest.mark.parametrize("cls,cname", [("RiptrmOptions", "riptrm_options"), ("RiptrmSIProblem", "riptrm_si_problem")])
 def test_options_struct_layout_matches_c(tmp_path, cls, cname):
     """ctypes mirrors == the C structs (sizeof and every offset), compiled with gcc."""
