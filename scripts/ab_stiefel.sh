@@ -1,19 +1,15 @@
+#!/bin/bash
+# Same-box A/B of a Stiefel knob: bench.py --problem stiefel alternating the default and $VAR=$ALT.
+#   OUT=r4p5 VAR=RIPTRM_STIEFEL_PROJ ALT=p3 B="256 2048" bash scripts/ab_stiefel.sh
 set -e
 cd "$GRAFT_REPO_ROOT"
-O=gpurun_out/${OUT:-r4st}; mkdir -p $O
-timeout -k 10 300 python -u -m pytest tests/test_gpu_stiefel.py -x -q --timeout 200 > $O/stiefel_tests.log 2>&1 || { tail -30 $O/stiefel_tests.log; exit 1; }
-tail -2 $O/stiefel_tests.log
-for B in 256 2048; do
-  timeout -k 10 180 python bench.py --problem stiefel --dim 200 --batch $B --cpu-budget 0 > $O/st_p4_b$B.json 2> $O/st_p4_b$B.err
-  RIPTRM_STIEFEL_PROJ=p3 timeout -k 10 180 python bench.py --problem stiefel --dim 200 --batch $B --cpu-budget 0 > $O/st_p3_b$B.json 2> $O/st_p3_b$B.err
-  python -c "
-import json
-for v in ('p4','p3'):
-    d=json.load(open('$O/st_%s_b$B.json' % v)); print(v, $B, 'proj us', round(d['ms_per_step']*1e3,2), 'frac', round(d['roofline']['frac'],3))"
-done
-for B in 256 2048; do
-  RIPTRM_STIEFEL_PROJ=nt timeout -k 10 180 python bench.py --problem stiefel --dim 200 --batch $B --cpu-budget 0 > $O/st_nt_b$B.json 2> $O/st_nt_b$B.err
-  python -c "
-import json
-d=json.load(open('$O/st_nt_b$B.json')); print('no-tail', $B, 'proj us', round(d['ms_per_step']*1e3,2), 'frac', round(d['roofline']['frac'],3))"
+O=gpurun_out/${OUT:-ab_stiefel}; mkdir -p $O
+for b in ${B:-256}; do
+  for r in 1 2; do
+    for v in default alt; do
+      if [ $v = alt ]; then export ${VAR}=${ALT}; else unset ${VAR}; fi
+      timeout -k 10 300 python bench.py --problem stiefel --dim ${DIM:-200} --batch $b --cpu-budget 0 > $O/st_${b}_${v}_$r.json 2> $O/st_${b}_${v}_$r.err || { tail $O/st_${b}_${v}_$r.err; exit 1; }
+      python -c "import json; d=json.load(open('$O/st_${b}_${v}_$r.json')); dd=d['detail']; print('B=$b $v run $r proj_us', round(d['ms_per_step'] * 1e3, 2), 'frac', d['roofline']['frac'], 'kernel', d['roofline'].get('kernel'), 'retr_us', round(dd['retraction_ms'] * 1e3, 2))"
+    done
+  done
 done
