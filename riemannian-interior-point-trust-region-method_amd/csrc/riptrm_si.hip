@@ -69,7 +69,8 @@ struct SIParams {
   const double* tolC_tab;
   // Exact_RepMat above RIPTRM_TRS_DIM_MAX (si_hbm_trs): the parked subproblems and the resume records
   double* trsA;      // batch x tdim x tdim   matrix of HwCur / HwNew in the tangent frame
-  double* trsw;      // batch x 2 tdp         unit vector / HVP coordinates (repmat scratch)
+  double* trsP;      // batch x (3dd + m + 1) the point (x, y) and mu of the parked subproblem's matrix
+  int32_t* trsids;   // 2 batch                the instances of a k_si_repmat launch
   double* trsa;      // batch x tdp           coordinates of cxCur
   double* trsx;      // batch x tdp           the subproblem's solution (host service)
   double* trsD;      // batch                 Delta
@@ -83,7 +84,7 @@ struct SIParams {
 
 struct Layout {
   int64_t off_x, off_y, off_eta, off_heta, off_escr, off_stats, off_log, total;
-  int64_t off_tA, off_tw, off_ta, off_tx, off_tD, off_tlam, off_tkind, off_tmin, off_rs;   // 0: no HBM subproblem path
+  int64_t off_tA, off_tP, off_tids, off_ta, off_tx, off_tD, off_tlam, off_tkind, off_tmin, off_rs;   // 0: no HBM subproblem path
 };
 
 inline int64_t rup(int64_t a, int64_t m) { return (a + m - 1) / m * m; }
@@ -110,11 +111,12 @@ inline Layout make_layout(int d, int N, int m, int batch, int cap) {
   L.off_escr = o;  o = rup(o + 8LL * batch * d * N, 256);
   L.off_stats = o; o = rup(o + 8LL * batch * RIPTRM_STAT_NFIELDS, 256);
   L.off_log = o;   o = rup(o + 8LL * batch * cap * RIPTRM_LOG_NFIELDS, 256);
-  L.off_tA = L.off_tw = L.off_ta = L.off_tx = L.off_tD = L.off_tlam = L.off_tkind = L.off_tmin = L.off_rs = 0;
+  L.off_tA = L.off_tP = L.off_tids = L.off_ta = L.off_tx = L.off_tD = L.off_tlam = L.off_tkind = L.off_tmin = L.off_rs = 0;
   if (si_hbm_trs(d)) {
     const int64_t td = si_manifold_dim(d), tp = si_tdp(d);
     L.off_tA = o;    o = rup(o + 8 * batch * td * td, 256);
-    L.off_tw = o;    o = rup(o + 8 * batch * 2 * tp, 256);
+    L.off_tP = o;    o = rup(o + 8LL * batch * (3LL * d * d + m + 1), 256);
+    L.off_tids = o;  o = rup(o + 4LL * 2 * batch, 256);
     L.off_ta = o;    o = rup(o + 8 * batch * tp, 256);
     L.off_tx = o;    o = rup(o + 8 * batch * tp, 256);
     L.off_tD = o;    o = rup(o + 8LL * batch, 256);
@@ -966,7 +968,7 @@ struct Eng {
   }
   // compute_direction's Exact_RepMat branch: returns the RIPTRM_TRS_* type
   __device__ __forceinline__ int trs_direction(const AtX& a, double Delta, PV& eta, double& hvps) {
-    if constexpr (HBMT) {   // solve() parks instead (repmat_hbm)
+    if constexpr (HBMT) {   // solve() parks instead (k_si_repmat)
       eta = PV{0.0, 0.0, 0.0};
       return RIPTRM_TRS_BOUNDARY;
     }
@@ -979,7 +981,7 @@ struct Eng {
   }
   // smallest eigenvalue of HwNew's matrix at (xN, yN, mu) (RIPTRM.py:599-613)
   __device__ __forceinline__ double mineig_at(PV xN, double yN, double mu, double& hvps) {
-    if constexpr (HBMT) return 0.0;   // solve() parks instead (repmat_hbm)
+    if constexpr (HBMT) return 0.0;   // solve() parks instead (k_si_repmat)
     AtX aN;
     prepare(aN, xN, yN, mu);
     const Frame F = frame(xN);
@@ -988,26 +990,39 @@ struct Eng {
     return riptrm_trs::min_eig<W>(B, w);
   }
 
-  // manifold.dim > RIPTRM_TRS_DIM_MAX: selfadj_operator2matrix (utils.py:565-573) into this instance's
-  // HBM matrix (tdim x tdim, row-major), the same HVP per basis vector as repmat; with want_c the
-  // coordinates of cxCur too.  The host's batched service solves / eigensolves it while the instance
-  // is parked (RIPTRM.py:433-444, :599-617).
-  __device__ void repmat_hbm(const AtX& a, const Frame& F, double& hvps, bool want_c) {
+  // manifold.dim > RIPTRM_TRS_DIM_MAX: selfadj_operator2matrix (utils.py:565-573) into HBM by
+  // k_si_repmat, one workgroup per basis vector j: the point of the parked subproblem (park_point),
+  // the frame, column j's HVP and its coordinates, written as repmat writes them (entries (k, j) and
+  // (j, k) for k <= j: HVP j's coordinate k), so the matrix is the sequential loop's bit for bit.
+  // With want_c, also the coordinates of cxCur (RIPTRM.py:438-440).  uv: 2 TDP doubles of LDS.
+  // (cost_grad's residual scratch E is shared by the instance's workgroups: they all write the same
+  // values at the same point.)
+  __device__ __forceinline__ int64_t tp_stride() const { return 3LL * dd + m + 1; }
+  __device__ __forceinline__ void park_point(PV px, double py, double mu) {
+    double* t = P.trsP + (int64_t)b * tp_stride();
+    store_pv(t, px);
+    if (cact) t[3 * dd + l] = py;
+    if (l == 0) t[3 * dd + m] = mu;
+  }
+  __device__ void repmat_col(int j, bool want_c, double* uv) {
+    const double* t = P.trsP + (int64_t)b * tp_stride();
+    const PV x = load_pv(t);
+    const double y = cact ? t[3 * dd + l] : 0.0;
+    const double mu = t[3 * dd + m];
+    AtX a;
+    prepare(a, x, y, mu);
+    const Frame F = frame(x);
+    double* e = uv;
+    double* q = uv + TDP;
+    for (int k = l; k < DIMM; k += NT) e[k] = (k == j) ? 1.0 : 0.0;
+    __syncthreads();
+    const PV bj = from_coords(F, e);
+    const PV h = hw(a, bj);
+    to_coords(F, h, q);
     double* A = P.trsA + (int64_t)b * DIMM * DIMM;
-    double* e = P.trsw + (int64_t)b * 2 * TDP;
-    double* q = e + TDP;
-    for (int j = 0; j < DIMM; ++j) {
-      for (int k = l; k < DIMM; k += NT) e[k] = (k == j) ? 1.0 : 0.0;
-      __syncthreads();
-      const PV bj = from_coords(F, e);
-      const PV h = hw(a, bj);
-      hvps += 1.0;
-      to_coords(F, h, q);
-      for (int k = l; k <= j; k += NT) {
-        A[(int64_t)k * DIMM + j] = q[k];
-        A[(int64_t)j * DIMM + k] = q[k];
-      }
-      __syncthreads();
+    for (int k = l; k <= j; k += NT) {
+      A[(int64_t)k * DIMM + j] = q[k];
+      A[(int64_t)j * DIMM + k] = q[k];
     }
     if (want_c) to_coords(F, a.c, P.trsa + (int64_t)b * TDP);
   }
@@ -1250,9 +1265,9 @@ struct Eng {
         const bool exact = P.opt.trs_solver == RIPTRM_TRS_SOLVER_EXACT_REPMAT;
         int tstop;
         if constexpr (HBMT) {
-          if (exact && rph == 0) {   // the matrix to HBM, park; the host solves TRSgep
-            const Frame F = frame(a.x);
-            repmat_hbm(a, F, hvps, true);
+          if (exact && rph == 0) {   // park; the host builds the matrix (k_si_repmat) and solves TRSgep
+            park_point(x, y, mu);
+            hvps += (double)DIMM;
             park((int)riptrm::PH_TRS_HOST, 0, PV{0.0, 0.0, 0.0});
             return;
           }
@@ -1301,11 +1316,9 @@ struct Eng {
         if (exact && P.opt.second_order_stationarity) {   // RIPTRM.py:599-613
           double me;
           if constexpr (HBMT) {
-            if (rph != 2) {   // HwNew's matrix to HBM, park; the host computes its eigenvalues
-              AtX aN;
-              prepare(aN, xN, yN, mu);
-              const Frame F = frame(xN);
-              repmat_hbm(aN, F, hvps, false);
+            if (rph != 2) {   // park; the host builds HwNew's matrix and computes its eigenvalues
+              park_point(xN, yN, mu);
+              hvps += (double)DIMM;
               park((int)riptrm::PH_MINEIG_HOST, tstop, eta);
               return;
             }
@@ -1501,6 +1514,20 @@ __global__ void __launch_bounds__(si_threads(D)) k_si(SIParams P) {
   else e.op_tcg();
 }
 
+// the parked instances' subproblem matrices (ids[blockIdx.y], basis vector blockIdx.x): Eng::repmat_col
+template <int D>
+__global__ void __launch_bounds__(si_threads(D)) k_si_repmat(SIParams P, int32_t ids_off, int want_c) {
+  constexpr int NT = si_threads(D);
+  __shared__ double sh[2 * NT];
+  __shared__ double ser[NT == W ? 8 * W : 1];
+  __shared__ int crs[NT], ccs[NT];
+  __shared__ double uv[2 * si_tdp(D)];
+  extern __shared__ double trs_lds[];   // big D: si_big_lds_doubles
+  const int b = P.trsids[ids_off + blockIdx.y];
+  Eng<D> e(P, b, sh, ser, crs, ccs, trs_lds);
+  if constexpr (si_hbm_trs(D)) e.repmat_col((int)blockIdx.x, want_c != 0 && blockIdx.x == 0, uv);
+}
+
 struct Bound {
   riptrm_si_problem prob;
   int batch = 0, cap = 0;
@@ -1550,7 +1577,8 @@ static SIParams si_params(riptrm_ctx* c, int mode) {
   P.prof = s->prof_on ? s->prof : nullptr;
   if (si_hbm_trs(P.d)) {
     P.trsA = (double*)(s->ws + s->L.off_tA);
-    P.trsw = (double*)(s->ws + s->L.off_tw);
+    P.trsP = (double*)(s->ws + s->L.off_tP);
+    P.trsids = (int32_t*)(s->ws + s->L.off_tids);
     P.trsa = (double*)(s->ws + s->L.off_ta);
     P.trsx = (double*)(s->ws + s->L.off_tx);
     P.trsD = (double*)(s->ws + s->L.off_tD);
@@ -1600,6 +1628,40 @@ static int si_launch(riptrm_ctx* c, const SIParams& P) {
     case 15: return si_launch_d<15>(c, P);
     default: return si_launch_d<16>(c, P);
   }
+}
+
+template <int D>
+static int si_repmat_d(riptrm_ctx* c, const SIParams& P, int ids_off, int cnt, int want_c) {
+  const size_t shm = D > 8 ? (size_t)si_big_lds_doubles(D) * sizeof(double) : 0;
+  if (shm > 64 * 1024)
+    HIPCHK(c, hipFuncSetAttribute((const void*)k_si_repmat<D>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm));
+  hipLaunchKernelGGL(k_si_repmat<D>, dim3((unsigned)si_manifold_dim(D), (unsigned)cnt), dim3(si_threads(D)), shm, c->stream,
+                     P, ids_off, want_c);
+  HIPCHK(c, hipGetLastError());
+  return RIPTRM_OK;
+}
+
+// the subproblem matrices of the parked instances ids (HBM path: d >= 8), one workgroup per entry of
+// the tangent basis
+static int si_repmat(riptrm_ctx* c, const SIParams& P, const std::vector<int32_t>& ids, int ids_off, int want_c) {
+  if (ids.empty()) return RIPTRM_OK;
+  HIPCHK(c, hipMemcpyAsync(P.trsids + ids_off, ids.data(), ids.size() * sizeof(int32_t), hipMemcpyHostToDevice, c->stream));
+  const int cnt = (int)ids.size();
+  int rc;
+  switch (P.d) {
+    case 8: rc = si_repmat_d<8>(c, P, ids_off, cnt, want_c); break;
+    case 9: rc = si_repmat_d<9>(c, P, ids_off, cnt, want_c); break;
+    case 10: rc = si_repmat_d<10>(c, P, ids_off, cnt, want_c); break;
+    case 11: rc = si_repmat_d<11>(c, P, ids_off, cnt, want_c); break;
+    case 12: rc = si_repmat_d<12>(c, P, ids_off, cnt, want_c); break;
+    case 13: rc = si_repmat_d<13>(c, P, ids_off, cnt, want_c); break;
+    case 14: rc = si_repmat_d<14>(c, P, ids_off, cnt, want_c); break;
+    case 15: rc = si_repmat_d<15>(c, P, ids_off, cnt, want_c); break;
+    default: rc = si_repmat_d<16>(c, P, ids_off, cnt, want_c); break;
+  }
+  if (rc) return rc;
+  HIPCHK(c, hipStreamSynchronize(c->stream));   // ids (host memory) may go after the copy has run
+  return RIPTRM_OK;
 }
 
 extern "C" {
@@ -1730,6 +1792,8 @@ int riptrm_si_solve(riptrm_ctx* ctx, const riptrm_options* opt, const double* x0
     }
     if (trs.empty() && mine.empty()) break;
     const int64_t tp = si_tdp(d);
+    if (int rc = si_repmat(ctx, P, trs, 0, 1)) return rc;
+    if (int rc = si_repmat(ctx, P, mine, B, 0)) return rc;
     if (!trs.empty())
       if (int rc = riptrm_big_gep_ids(ctx, tdim, trs.data(), (int)trs.size(), P.trsA, tdim, (int64_t)tdim * tdim, P.trsa,
                                       tp, P.trsD, opt->trs_tolhardcase, P.trsx, P.trslam, P.trskind, nullptr, false,
