@@ -71,6 +71,7 @@ struct SIParams {
   double* trsA;      // batch x tdim x tdim   matrix of HwCur / HwNew in the tangent frame
   double* trsP;      // batch x (3dd + m + 1) the point (x, y) and mu of the parked subproblem's matrix
   int32_t* trsids;   // 2 batch                the instances of a k_si_repmat launch
+  double* trsE;      // batch x tdim x d x N   k_si_repmat's residual scratch when d N does not fit LDS
   double* trsa;      // batch x tdp           coordinates of cxCur
   double* trsx;      // batch x tdp           the subproblem's solution (host service)
   double* trsD;      // batch                 Delta
@@ -84,7 +85,7 @@ struct SIParams {
 
 struct Layout {
   int64_t off_x, off_y, off_eta, off_heta, off_escr, off_stats, off_log, total;
-  int64_t off_tA, off_tP, off_tids, off_ta, off_tx, off_tD, off_tlam, off_tkind, off_tmin, off_rs;   // 0: no HBM subproblem path
+  int64_t off_tA, off_tP, off_tids, off_tE, off_ta, off_tx, off_tD, off_tlam, off_tkind, off_tmin, off_rs;   // 0: no HBM subproblem path
 };
 
 inline int64_t rup(int64_t a, int64_t m) { return (a + m - 1) / m * m; }
@@ -97,6 +98,11 @@ __host__ __device__ constexpr int si_tdp(int d) { return (si_manifold_dim(d) + 3
 // resume record: 32 scalars (incl. the section ticks), then 21 rows of one double per thread
 // (x, xI, xPrev, xHead, x0, eta as 3 rows each; y, yI, y0)
 constexpr int RS_NSC = 32, RS_PT = 20, RS_ROWS = 21;
+// k_si_repmat keeps each workgroup's residual E (d x N) in LDS up to this size, else in its own
+// slice of an HBM scratch (every workgroup of an instance computes the same E: a shared one would
+// be a race on identical values)
+constexpr int SI_REPMAT_E_LDS = 48 * 1024;
+__host__ __device__ constexpr bool si_repmat_e_lds(int d, int N) { return (int64_t)d * N * 8 <= SI_REPMAT_E_LDS; }
 __host__ __device__ constexpr int si_nt(int d) { return d <= 8 ? 64 : (d * d + 63) / 64 * 64; }
 __host__ __device__ constexpr int64_t si_rs_doubles(int d) { return RS_NSC + (int64_t)RS_ROWS * si_nt(d); }
 
@@ -111,12 +117,15 @@ inline Layout make_layout(int d, int N, int m, int batch, int cap) {
   L.off_escr = o;  o = rup(o + 8LL * batch * d * N, 256);
   L.off_stats = o; o = rup(o + 8LL * batch * RIPTRM_STAT_NFIELDS, 256);
   L.off_log = o;   o = rup(o + 8LL * batch * cap * RIPTRM_LOG_NFIELDS, 256);
-  L.off_tA = L.off_tP = L.off_tids = L.off_ta = L.off_tx = L.off_tD = L.off_tlam = L.off_tkind = L.off_tmin = L.off_rs = 0;
+  L.off_tA = L.off_tP = L.off_tids = L.off_tE = L.off_ta = L.off_tx = L.off_tD = L.off_tlam = L.off_tkind = L.off_tmin = L.off_rs = 0;
   if (si_hbm_trs(d)) {
     const int64_t td = si_manifold_dim(d), tp = si_tdp(d);
     L.off_tA = o;    o = rup(o + 8 * batch * td * td, 256);
     L.off_tP = o;    o = rup(o + 8LL * batch * (3LL * d * d + m + 1), 256);
     L.off_tids = o;  o = rup(o + 4LL * 2 * batch, 256);
+    if (!si_repmat_e_lds(d, N)) {
+      L.off_tE = o;  o = rup(o + 8 * batch * td * d * N, 256);
+    }
     L.off_ta = o;    o = rup(o + 8 * batch * tp, 256);
     L.off_tx = o;    o = rup(o + 8 * batch * tp, 256);
     L.off_tD = o;    o = rup(o + 8LL * batch, 256);
@@ -995,8 +1004,7 @@ struct Eng {
   // the frame, column j's HVP and its coordinates, written as repmat writes them (entries (k, j) and
   // (j, k) for k <= j: HVP j's coordinate k), so the matrix is the sequential loop's bit for bit.
   // With want_c, also the coordinates of cxCur (RIPTRM.py:438-440).  uv: 2 TDP doubles of LDS.
-  // (cost_grad's residual scratch E is shared by the instance's workgroups: they all write the same
-  // values at the same point.)
+  // Each workgroup has its own residual scratch E (k_si_repmat sets it: LDS or an HBM slice).
   __device__ __forceinline__ int64_t tp_stride() const { return 3LL * dd + m + 1; }
   __device__ __forceinline__ void park_point(PV px, double py, double mu) {
     double* t = P.trsP + (int64_t)b * tp_stride();
@@ -1522,9 +1530,12 @@ __global__ void __launch_bounds__(si_threads(D)) k_si_repmat(SIParams P, int32_t
   __shared__ double ser[NT == W ? 8 * W : 1];
   __shared__ int crs[NT], ccs[NT];
   __shared__ double uv[2 * si_tdp(D)];
-  extern __shared__ double trs_lds[];   // big D: si_big_lds_doubles
+  extern __shared__ double trs_lds[];   // big D: si_big_lds_doubles; then E when it fits (si_repmat_e_lds)
   const int b = P.trsids[ids_off + blockIdx.y];
   Eng<D> e(P, b, sh, ser, crs, ccs, trs_lds);
+  const int64_t en = (int64_t)D * P.N;
+  e.E = P.trsE ? P.trsE + ((int64_t)b * si_manifold_dim(D) + blockIdx.x) * en
+               : trs_lds + (D > 8 ? si_big_lds_doubles(D) : 0);
   if constexpr (si_hbm_trs(D)) e.repmat_col((int)blockIdx.x, want_c != 0 && blockIdx.x == 0, uv);
 }
 
@@ -1579,6 +1590,7 @@ static SIParams si_params(riptrm_ctx* c, int mode) {
     P.trsA = (double*)(s->ws + s->L.off_tA);
     P.trsP = (double*)(s->ws + s->L.off_tP);
     P.trsids = (int32_t*)(s->ws + s->L.off_tids);
+    P.trsE = s->L.off_tE ? (double*)(s->ws + s->L.off_tE) : nullptr;
     P.trsa = (double*)(s->ws + s->L.off_ta);
     P.trsx = (double*)(s->ws + s->L.off_tx);
     P.trsD = (double*)(s->ws + s->L.off_tD);
@@ -1632,7 +1644,7 @@ static int si_launch(riptrm_ctx* c, const SIParams& P) {
 
 template <int D>
 static int si_repmat_d(riptrm_ctx* c, const SIParams& P, int ids_off, int cnt, int want_c) {
-  const size_t shm = D > 8 ? (size_t)si_big_lds_doubles(D) * sizeof(double) : 0;
+  const size_t shm = ((D > 8 ? (size_t)si_big_lds_doubles(D) : 0) + (P.trsE ? 0 : (size_t)D * P.N)) * sizeof(double);
   if (shm > 64 * 1024)
     HIPCHK(c, hipFuncSetAttribute((const void*)k_si_repmat<D>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm));
   hipLaunchKernelGGL(k_si_repmat<D>, dim3((unsigned)si_manifold_dim(D), (unsigned)cnt), dim3(si_threads(D)), shm, c->stream,

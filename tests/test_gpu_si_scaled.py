@@ -192,3 +192,27 @@ def test_si_exact_hbm_eigensolve_failure_stops_one_instance():
     for key in ("cost", "residual", "normdx", "mineigvalHw"):
         assert both.log(1)[key] == alone.log(0)[key], key
     np.testing.assert_array_equal(both.x[1].cpu().numpy(), alone.x[0].cpu().numpy())
+
+
+@pytest.mark.timeout(600)
+def test_si_exact_hbm_many_columns():
+    """k_si_repmat keeps each workgroup's residual E = XP - (I + hA) X (d x N) in LDS while d N 8 <=
+    48 KiB and in its own slice of an HBM scratch beyond: d = 8 with the data columns replicated to
+    N = 855 takes the HBM slices.  Bar: the oracle's (compare_until_flip), as for the LDS case."""
+    import si
+    from parity import compare_until_flip
+    import copy
+    base, st = _inst(8, 1)
+    data = copy.copy(base)
+    data.X, data.XP = np.tile(base.X, (1, 9)), np.tile(base.XP, (1, 9))
+    data.N = data.X.shape[1]
+    assert data.N * 8 * 8 > 48 * 1024
+    xs = np.stack([x for x, _ in st])
+    ys = np.stack([y for _, y in st])
+    opt = {"maxiter": 1, "inner_maxiter": 3, "tolresid": 0.0, "maxtime": 1e9, "TRS_solver": "Exact_RepMat",
+           "second_order_stationarity": False}
+    res = _batch(data, 1).solve(xs, ys, dict(opt, manviofun=si.si_manviofun))
+    ref = SI.solve(data, xs[0], ys[0], dict(opt, manviofun=SI.si_manvio))
+    gl = res.log(0)
+    assert 0 < len([k for k in gl["dxtype"] if k is not None]) <= 3
+    compare_until_flip(gl, ref.log)
