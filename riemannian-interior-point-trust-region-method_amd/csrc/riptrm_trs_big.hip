@@ -301,39 +301,67 @@ __device__ __forceinline__ void cg_final_terms(double* red, double* sc, double a
   }
 }
 
-// q[row] = A[row] . v over rows m, 8 waves, FOUR rows at a time per wave (independent chains;
-// each row's own sum in k_gemv's order)
-__device__ __forceinline__ void wg_matvec(const double* __restrict__ A, int64_t lda, int m, const double* v,
-                                          double* out) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  for (int r0 = 4 * w; r0 < m; r0 += 4 * (WG / 64)) {
-    double s[4] = {0.0, 0.0, 0.0, 0.0};
-    const double* a0 = A + (int64_t)r0 * lda;
-    for (int j = lane; j < m; j += 64) {
-      const double vj = v[j];
+typedef __attribute__((address_space(3))) double lds_f64;
+
+// rows r0 .. r0 + 3 of A (leading dimension lda) . v: each row's own sum in k_gemv's order
+template <typename TA>
+__device__ __forceinline__ void wg_rows4(const TA* a0, int64_t lda, int r0, int m, const double* v, double* out) {
+  const int lane = threadIdx.x & 63;
+  double s[4] = {0.0, 0.0, 0.0, 0.0};
+  for (int j = lane; j < m; j += 64) {
+    const double vj = v[j];
 #pragma unroll
-      for (int u = 0; u < 4; ++u)
-        if (r0 + u < m) s[u] += a0[(int64_t)u * lda + j] * vj;
-    }
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const double t = riptrm_wave::wave_sum(s[u]);
-      if (lane == 0 && r0 + u < m) out[r0 + u] = t;
-    }
+    for (int u = 0; u < 4; ++u)
+      if (r0 + u < m) s[u] += a0[(int64_t)u * lda + j] * vj;
   }
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const double t = riptrm_wave::wave_sum(s[u]);
+    if (lane == 0 && r0 + u < m) out[r0 + u] = t;
+  }
+}
+
+// q[row] = A[row] . v over rows m, 8 waves, FOUR rows at a time per wave (independent chains).
+// Rows below rl (a multiple of 4) come from their LDS copy Al (leading dimension m): the same
+// values, so the same sums.
+__device__ __forceinline__ void wg_matvec(const double* __restrict__ A, int64_t lda, int m, const double* v,
+                                          double* out, const lds_f64* Al = nullptr, int rl = 0) {
+  const int w = threadIdx.x >> 6;
+  for (int r0 = 4 * w; r0 < m; r0 += 4 * (WG / 64)) {
+    if (r0 < rl) wg_rows4(Al + (int64_t)r0 * m, (int64_t)m, r0, m, v, out);
+    else wg_rows4(A + (int64_t)r0 * lda, lda, r0, m, v, out);
+  }
+}
+
+// rows of A the one-workgroup CG keeps in LDS (dynamic, next to its static p / q / red arrays): all
+// of them up to m ~ 120 (SciPy's CG runs to its 10 m iteration cap on indefinite subproblems, so the
+// per-iteration mat-vec latency is what counts there)
+constexpr int CG_LDS_BYTES = 124 * 1024;
+inline int cg_lds_rows(int m) {
+  const char* e = getenv("RIPTRM_CG_LDS");   // "0": stream every row (A/B measurements)
+  if (e && e[0] == '0') return 0;
+  const int r = std::min(m, CG_LDS_BYTES / (8 * m));
+  return r >= m ? m : r / 4 * 4;
 }
 
 // The whole CG (init, iterations, final test) for slot blockIdx.y, order m <= CG_WG_MAX; A at slot
 // offset aoff with leading dimension lda; Delta of the slot at D[ids[k] * dstride]
 __global__ void __launch_bounds__(WG) k_cg_wg(Bat B, int m, int64_t aoff, int64_t lda, const double* D,
-                                              int64_t dstride) {
+                                              int64_t dstride, int rl) {
   __shared__ double red[WG / 64];
   __shared__ double ps[CG_WG_MAX], qs[CG_WG_MAX];
+  extern __shared__ double arows[];   // rows 0 .. rl - 1 of A, leading dimension m
   const int k = blockIdx.y;
   const Slot q = slot_at(B, k);
   const double* A = q.M + aoff;
   const double* a = q.v[VS_A];
   const int t = threadIdx.x;
+  const lds_f64* Al = (const lds_f64*)arows;
+  for (int64_t e = t; e < (int64_t)rl * m; e += WG) {
+    const int i = (int)(e / m), j = (int)(e - (int64_t)i * m);
+    arows[e] = A[(int64_t)i * lda + j];
+  }
+  __syncthreads();
   double x[CG_RPT], r[CG_RPT];
   double an = 0.0;
 #pragma unroll
@@ -368,7 +396,7 @@ __global__ void __launch_bounds__(WG) k_cg_wg(Bat B, int m, int64_t aoff, int64_
       if (i < m) ps[i] = it > 0.0 ? ps[i] * beta + r[u] : r[u];
     }
     __syncthreads();
-    wg_matvec(A, lda, m, ps, qs);
+    wg_matvec(A, lda, m, ps, qs, Al, rl);
     __syncthreads();
     double pq = 0.0;
 #pragma unroll
@@ -400,7 +428,7 @@ __global__ void __launch_bounds__(WG) k_cg_wg(Bat B, int m, int64_t aoff, int64_
     }
   }
   __syncthreads();
-  wg_matvec(A, lda, m, ps, qs);
+  wg_matvec(A, lda, m, ps, qs, Al, rl);
   __syncthreads();
   double v0 = 0.0, v1 = 0.0, v2 = 0.0, v3 = 0.0;
 #pragma unroll
@@ -901,7 +929,11 @@ static int big_cg(riptrm_ctx* c, const Bat& B, int cnt, int64_t aoff, int lda, i
   const int64_t N = B.N;
   const dim3 one(1, cnt), rows(blocks_of(m, GV / 64), cnt);
   if (cg_one_workgroup(m, cnt)) {
-    hipLaunchKernelGGL(k_cg_wg, one, dim3(WG), 0, st, B, m, aoff, (int64_t)lda, D, dstride);
+    const int rl = cg_lds_rows(m);
+    const size_t shm = (size_t)rl * m * sizeof(double);
+    if (shm > 0)
+      HIPCHK(c, hipFuncSetAttribute((const void*)k_cg_wg, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm));
+    hipLaunchKernelGGL(k_cg_wg, one, dim3(WG), shm, st, B, m, aoff, (int64_t)lda, D, dstride, rl);
     HIPCHK(c, hipGetLastError());
   } else {
     hipLaunchKernelGGL(k_cg_init, one, dim3(WG), 0, st, B, m);
