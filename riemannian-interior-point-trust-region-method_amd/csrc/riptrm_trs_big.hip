@@ -346,16 +346,36 @@ inline int cg_lds_rows(int m) {
 
 // The whole CG (init, iterations, final test) for slot blockIdx.y, order m <= CG_WG_MAX; A at slot
 // offset aoff with leading dimension lda; Delta of the slot at D[ids[k] * dstride]
+// Aext (optional): A of slot k at Aext + ids[k] ext_stride instead of the slot (whose copy an
+// eigensolve has already overwritten).  skip_indef: the slot's eigenvalues are known (ascending, in
+// VS_EV); when A is clearly indefinite (lam_min < -1e-8 max |lam|) the interior candidate cannot win
+// -- the boundary solution's model value is below every interior point's then (RIPTRM.py:294-298
+// takes p1 only if p1obj <= xobj) -- so the CG is not run and the candidate is marked ineligible.
 __global__ void __launch_bounds__(WG) k_cg_wg(Bat B, int m, int64_t aoff, int64_t lda, const double* D,
-                                              int64_t dstride, int rl) {
+                                              int64_t dstride, int rl, const double* Aext = nullptr,
+                                              int64_t ext_stride = 0, int skip_indef = 0) {
   __shared__ double red[WG / 64];
   __shared__ double ps[CG_WG_MAX], qs[CG_WG_MAX];
   extern __shared__ double arows[];   // rows 0 .. rl - 1 of A, leading dimension m
   const int k = blockIdx.y;
   const Slot q = slot_at(B, k);
-  const double* A = q.M + aoff;
+  const double* A = Aext ? Aext + (int64_t)B.ids[k] * ext_stride : q.M + aoff;
   const double* a = q.v[VS_A];
   const int t = threadIdx.x;
+  if (skip_indef) {
+    const double* ev = q.v[VS_EV];
+    const double lmin = ev[0], lmax = fmax(fabs(ev[0]), fabs(ev[m - 1]));
+    if (*q.info == 0 && lmin < -1e-8 * lmax) {   // uniform over the workgroup
+      if (t == 0) {
+        q.sc[SC_CG_OK] = 0.0;
+        q.sc[SC_P1OBJ] = 0.0;
+        q.sc[SC_IT] = 0.0;
+        q.sc[SC_DONE] = 4.0;
+        q.sc[SC_DELTA] = D[(int64_t)B.ids[k] * dstride];
+      }
+      return;
+    }
+  }
   const lds_f64* Al = (const lds_f64*)arows;
   for (int64_t e = t; e < (int64_t)rl * m; e += WG) {
     const int i = (int)(e / m), j = (int)(e - (int64_t)i * m);
@@ -837,6 +857,10 @@ static Solver& solver() {
 using namespace riptrm_big;
 
 static unsigned blocks_of(int64_t n, int per) { return (unsigned)((n + per - 1) / per); }
+static bool getenv_is(const char* name, char v) {
+  const char* e = getenv(name);
+  return e && e[0] == v;
+}
 
 static int big_handle(riptrm_ctx* c) {
   Solver& s = solver();
@@ -1120,6 +1144,18 @@ int riptrm_big_gep_ids(riptrm_ctx* c, int dim, const int32_t* sel, int count, co
     HIPCHK(c, hipGetLastError());
     if (mineig_only) {
       if (int rc = eig_batched(c, Bt, cnt, false, dim, 0, dim)) return rc;
+    } else if (per_instance && cg_one_workgroup(dim, cnt) && !getenv_is("RIPTRM_CG_SKIP", '0')) {
+      // eigenpairs first; the CG then reads A from the caller's array and is skipped where A is
+      // clearly indefinite (k_cg_wg: the interior candidate cannot win there)
+      if (int rc = eig_batched(c, Bt, cnt, true, dim, 0, dim)) return rc;
+      const int rl = cg_lds_rows(dim);
+      const size_t shm = (size_t)rl * dim * sizeof(double);
+      if (shm > 0)
+        HIPCHK(c, hipFuncSetAttribute((const void*)k_cg_wg, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm));
+      hipLaunchKernelGGL(k_cg_wg, dim3(1, cnt), dim3(WG), shm, c->stream, Bt, dim, (int64_t)0, lda, Delta, (int64_t)1, rl,
+                         A, a_stride, 1);
+      HIPCHK(c, hipGetLastError());
+      if (int rc = big_after_eig(c, Bt, cnt, 0, dim, dim, tolhc)) return rc;
     } else if (int rc = big_solve(c, Bt, cnt, 0, dim, dim, Delta, 1, tolhc)) {
       return rc;
     }
