@@ -77,8 +77,9 @@ extern "C" {
 #define RIPTRM_TRS_SOLVER_TCG 0
 #define RIPTRM_TRS_SOLVER_EXACT_REPMAT 1
 /* Exact_RepMat works on the dim x dim matrix of HwCur in LDS up to manifold.dim = this
- * (NonnegPCA n <= 97, StableIdentification d <= 7); larger NonnegPCA problems keep the matrix in
- * HBM scratch bound with riptrm_trs_bind_workspace (below) */
+ * (NonnegPCA n <= 97, StableIdentification d <= 7); larger problems (NonnegPCA in
+ * riptrm_solve_advance, StableIdentification d >= 8 in riptrm_si_solve) keep the matrix in HBM
+ * scratch bound with riptrm_trs_bind_workspace (below) */
 #define RIPTRM_TRS_DIM_MAX 96
 
 /* inner_status codes (RIPTRM.py:763,770,678,698,829,837); 0 = None */
