@@ -236,11 +236,12 @@ def rank_census(dist, world: int, rank: int, dev):
     with one all_gather, so the JSON line shows which collective backend really ran with how many
     ranks on which devices.  World 1: just this process."""
     import torch
-    backend = dist.get_backend() if world > 1 else None
-    me = torch.tensor([rank, dist.get_world_size() if world > 1 else 1, dev.index if dev.index is not None else 0,
+    on = dist.is_initialized()
+    backend = dist.get_backend() if on else None
+    me = torch.tensor([rank, dist.get_world_size() if on else 1, dev.index if dev.index is not None else 0,
                        1 if backend == "nccl" else 0], dtype=torch.int64,
                       device=dev if backend == "nccl" else "cpu")
-    if world == 1:
+    if not on:
         rows = [me]
     else:
         rows = [torch.empty_like(me) for _ in range(world)]
@@ -326,6 +327,8 @@ def main():
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend (nccl = RCCL)")
     ap.add_argument("--dump", default="",
                     help="rank 0 writes the gathered x, y and stats of every global instance to this .npz")
+    ap.add_argument("--dist-at-1", action="store_true",
+                    help="with --gpus 1: still initialise a (one-rank) process group, so the collectives run")
     ap.add_argument("--same-device", action="store_true",
                     help="rehearsal only: every rank on cuda:0 (use with --backend gloo on a 1-GPU box)")
     args = ap.parse_args()
@@ -345,8 +348,14 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; launch one rank per GPU")
-    if world > 1:
+    if world > 1 or args.dist_at_1:
+        # --dist-at-1: a one-rank process group on the one GPU, so every collective call site of
+        # the N-GPU path (rank census, timing all_reduce, final all_gather) runs over RCCL
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if world == 1:
+            os.environ.setdefault("RANK", "0")
+            os.environ.setdefault("WORLD_SIZE", "1")
+            os.environ.setdefault("MASTER_PORT", str(_free_port()))
         dev_idx = 0 if args.same_device else local
         torch.cuda.set_device(dev_idx)
         if args.backend == "nccl":
@@ -360,12 +369,12 @@ def main():
 
     if args.problem == "stiefel":
         bench_stiefel(args, world, rank, dev, dist)
-        if world > 1:
+        if dist.is_initialized():
             dist.destroy_process_group()
         return
     if args.problem == "si":
         bench_si(args, world, rank, dev, dist)
-        if world > 1:
+        if dist.is_initialized():
             dist.destroy_process_group()
         return
 
@@ -393,14 +402,14 @@ def main():
     graph_mode = (args.layout == "shared") or (B * eng.inst_stride * 8 < 2e8)
     if not graph_mode:
         engine.profile_enable(eng, True)
-    if world > 1:
+    if dist.is_initialized():
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     eng.run_until(W + K)
     torch.cuda.synchronize(dev)
     el = time.perf_counter() - t0
-    if world > 1:
+    if dist.is_initialized():
         dist.barrier()
     st1 = eng.stats()
     if graph_mode:
@@ -421,7 +430,7 @@ def main():
                           dtype=torch.float64, device=dev)
     tmax = torch.tensor([el], dtype=torch.float64, device=dev)
     ranks_seen = rank_census(dist, world, rank, dev)
-    if world > 1:
+    if dist.is_initialized():
         from distributed import gather_rows
         dist.all_reduce(counts, op=dist.ReduceOp.SUM)
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
@@ -577,7 +586,7 @@ def main():
                        "n": n, "batch_per_gpu": B, "global_batch": B * world,
                        "outer_window": [W + 1, W + K], "restart_every": args.cycle, "layout": args.layout,
                        "parallelism": f"instance-sharded x{world}", "world_size": world,
-                       "backend": dist.get_backend() if world > 1 else None, "ranks": ranks_seen},
+                       "backend": dist.get_backend() if dist.is_initialized() else None, "ranks": ranks_seen},
             "roofline": roofline,
             "cpu_baseline": cpu,
             "detail": {"inner_iterations_per_s": inner_all / T, "tcg_iterations_per_s": tcg_all / T,
@@ -601,7 +610,7 @@ def main():
                           if args.trs == "Exact_RepMat" and n - 1 > engine.C["RIPTRM_TRS_DIM_MAX"] else {})},
         }
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 
@@ -622,7 +631,7 @@ def bench_stiefel(args, world, rank, dev, dist):
     for name, fn in (("projection", lambda: st.projection(X, W)), ("retraction", lambda: st.retraction(X, U))):
         for _ in range(max(1, args.warmup)):
             fn()
-        if world > 1:
+        if dist.is_initialized():
             dist.barrier()
         torch.cuda.synchronize(dev)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -633,7 +642,7 @@ def bench_stiefel(args, world, rank, dev, dist):
         torch.cuda.synchronize(dev)
         res[name] = e0.elapsed_time(e1) / 1e3 / args.steps
     t = torch.tensor([res["projection"], res["retraction"]], dtype=torch.float64, device=dev)
-    if world > 1:
+    if dist.is_initialized():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     tp, tr = [float(v) for v in t.tolist()]
     if rank != 0:
@@ -826,7 +835,7 @@ def bench_si(args, world, rank, dev, dist):
            "maxiter": max(1, W), "save_inner_iteration": True, **trs_options(args.trs)}
     eng.solve(xs, ys, opt)          # warmup launch (W outer iterations), untimed
     opt["maxiter"] = K
-    if world > 1:
+    if dist.is_initialized():
         dist.barrier()
     torch.cuda.synchronize(dev)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -836,7 +845,7 @@ def bench_si(args, world, rank, dev, dist):
     e1.record()
     torch.cuda.synchronize(dev)
     el = time.perf_counter() - t0
-    if world > 1:
+    if dist.is_initialized():
         dist.barrier()
     kern_s = e0.elapsed_time(e1) / 1e3
     st = eng.stats()
@@ -851,7 +860,7 @@ def bench_si(args, world, rank, dev, dist):
     counts = torch.tensor([tot("OUTER_ITERS"), tot("INNER_ITERS"), tot("TCG_ITERS"), tot("PASSES")],
                           dtype=torch.float64, device=dev)
     tmax = torch.tensor([el], dtype=torch.float64, device=dev)
-    if world > 1:
+    if dist.is_initialized():
         dist.all_reduce(counts, op=dist.ReduceOp.SUM)
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
     outer, inner, tcg, hvps = [float(v) for v in counts.tolist()]

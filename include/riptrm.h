@@ -379,7 +379,9 @@ int riptrm_si_profile_read(riptrm_ctx* ctx, double* seconds);
  * (manifold.dim HVPs) in the SI workspace and parks, the call serves every parked instance in
  * batched passes (the HBM path of riptrm_trs_gep; with the second-order test also HwNew's smallest
  * eigenvalue) and relaunches until every instance has finished: synchronous then.  A non-converged
- * eigensolve fails the call (RIPTRM_E_HIP). */
+ * eigensolve stops only its instance (stats error = RIPTRM_ERR_EIGEN, x and y back to the start of
+ * its outer step: the reference's do_exit_on_error break, RIPTRM.py:961-966); the call still returns
+ * RIPTRM_OK and the other instances continue. */
 int riptrm_si_solve(riptrm_ctx* ctx, const riptrm_options* opt, const double* x0, const double* y0,
                     const double* mu_table, const double* tolL_table, const double* tolC_table,
                     int32_t table_len);
@@ -428,6 +430,13 @@ int riptrm_trs_bind_workspace(riptrm_ctx* ctx, void* ws, int64_t bytes, int32_t 
 int64_t riptrm_trs_cache_bytes(int32_t order, int32_t batch);
 int riptrm_trs_bind_cache(riptrm_ctx* ctx, void* cache, int64_t bytes, int32_t order, int32_t batch);
 int riptrm_trs_cache_stats(riptrm_ctx* ctx, int64_t* hits, int64_t* subproblems);
+/* StableIdentification Exact_RepMat above dim 96 (riptrm_si_solve's service): subproblems whose
+ * SciPy CG (RIPTRM.py:246-251) was decided on the eigenpairs, and how many of them skipped it because
+ * a bound from those eigenpairs shows that no CG iterate passing RIPTRM.py:246-251 can have a model
+ * value <= the boundary solution's (RIPTRM.py:294-298); the choice, and every result, is the one the
+ * CG would have given (RIPTRM_CG_SKIP=0 in the environment: always run it).  Since the context was
+ * created; either pointer may be NULL. */
+int riptrm_trs_skip_stats(riptrm_ctx* ctx, int64_t* checked, int64_t* skipped);
 
 /* ==== Stiefel(n, p) manifold operations =========================================
  * Not in the reference (north_star / BASELINE configs[4] ask for them): pymanopt 2.x formulas,

@@ -75,6 +75,7 @@ struct riptrm_ctx {
   char* big_cache = nullptr;
   int big_cache_order = 0, big_cache_batch = 0;
   int64_t big_cache_hits = 0, big_subproblems = 0;   // since the solve began (riptrm_trs_cache_stats)
+  int64_t big_cg_checked = 0, big_cg_skipped = 0;    // since the context was created (riptrm_trs_skip_stats)
 };
 
 // riptrm_trs_big.hip

@@ -53,7 +53,8 @@ constexpr int CG_RPT = CG_WG_MAX / WG;     // x / r elements per thread there
 // scalar slots
 enum Sc : int {
   SC_TAU = 0, SC_GAM, SC_XX, SC_COEF, SC_WC, SC_AN, SC_ATOL, SC_RHO, SC_RHO_PREV, SC_IT, SC_DONE,
-  SC_CG_OK, SC_P1OBJ, SC_KIND, SC_LAM1, SC_MINEIG, SC_INTERIOR, SC_DELTA, SC_XSX, SC_YX
+  SC_CG_OK, SC_P1OBJ, SC_KIND, SC_LAM1, SC_MINEIG, SC_INTERIOR, SC_DELTA, SC_XSX, SC_YX,
+  SC_XOBJ, SC_BKIND, SC_BLAM1   // the boundary / hard-case candidate, before the interior choice
 };
 
 __host__ __device__ inline int64_t vpad(int64_t n) { return (n + 63) / 64 * 64; }
@@ -347,10 +348,16 @@ inline int cg_lds_rows(int m) {
 // The whole CG (init, iterations, final test) for slot blockIdx.y, order m <= CG_WG_MAX; A at slot
 // offset aoff with leading dimension lda; Delta of the slot at D[ids[k] * dstride]
 // Aext (optional): A of slot k at Aext + ids[k] ext_stride instead of the slot (whose copy an
-// eigensolve has already overwritten).  skip_indef: the slot's eigenvalues are known (ascending, in
-// VS_EV); when A is clearly indefinite (lam_min < -1e-8 max |lam|) the interior candidate cannot win
-// -- the boundary solution's model value is below every interior point's then (RIPTRM.py:294-298
-// takes p1 only if p1obj <= xobj) -- so the CG is not run and the candidate is marked ineligible.
+// eigensolve has already overwritten).  skip_indef: the eigenpairs (ev ascending, g = Q^T a) and the
+// boundary candidate's model value xobj (k_secular, choose = 0) are known.  The CG is not run, and
+// its candidate marked ineligible, only where a bound computed from them shows that no iterate it can
+// return passes RIPTRM.py:294-298 (residual < 1e-5 ||a||, ||p1|| < Delta, p1obj <= xobj): with
+// A p1 = -a + r, ||r|| <= 1e-5 ||a|| =: e, lam_s = min |lam_i| > 0,
+//   ||p1|| >= ||p*|| - e / lam_s            (p* = -A^-1 a: ||p*||^2 = sum g_i^2 / lam_i^2)
+//   p1obj = q(p*) + r^T A^-1 r / 2 >= -sum g_i^2 / lam_i / 2 - e^2 / (2 lam_s)
+// so the skip needs ||p*|| (1 - 1e-6) - e / lam_s >= Delta, or that lower bound on p1obj above xobj
+// by more than a rounding allowance; A indefinite (lam_min < -1e-8 max |lam|) and not nearly
+// singular (lam_s > 1e-8 max |lam|).  Otherwise the CG runs (the same iterate as without the skip).
 __global__ void __launch_bounds__(WG) k_cg_wg(Bat B, int m, int64_t aoff, int64_t lda, const double* D,
                                               int64_t dstride, int rl, const double* Aext = nullptr,
                                               int64_t ext_stride = 0, int skip_indef = 0) {
@@ -363,9 +370,30 @@ __global__ void __launch_bounds__(WG) k_cg_wg(Bat B, int m, int64_t aoff, int64_
   const double* a = q.v[VS_A];
   const int t = threadIdx.x;
   if (skip_indef) {
-    const double* ev = q.v[VS_EV];
+    const double *ev = q.v[VS_EV], *g = q.v[VS_G];
     const double lmin = ev[0], lmax = fmax(fabs(ev[0]), fabs(ev[m - 1]));
-    if (*q.info == 0 && lmin < -1e-8 * lmax) {   // uniform over the workgroup
+    double lsm = INFINITY, s1 = 0.0, s2 = 0.0, aa = 0.0;
+    for (int i = t; i < m; i += WG) {
+      const double l = ev[i], gi = g[i];
+      lsm = fmin(lsm, fabs(l));
+      s1 += (gi / l) * (gi / l);
+      s2 += gi * gi / l;
+      aa += a[i] * a[i];
+    }
+    lsm = -blk_max(-lsm, red);
+    s1 = blk_sum(s1, red);
+    s2 = blk_sum(s2, red);
+    const double e = 1e-5 * sqrt(blk_sum(aa, red));
+    const double Dl = D[(int64_t)B.ids[k] * dstride];
+    bool skip = *q.info == 0 && lmin < -1e-8 * lmax && lsm > 1e-8 * lmax;
+    if (skip) {
+      const double xobj = q.sc[SC_XOBJ];
+      const bool far = sqrt(s1) * (1.0 - 1e-6) - e / lsm >= Dl;
+      const double p1lo = -0.5 * s2 - 0.5 * e * e / lsm;
+      const bool worse = p1lo - xobj > 1e-6 * (fabs(s2) + fabs(xobj)) + 1e-10 * (e * 1e5) * Dl;
+      skip = far || worse;
+    }
+    if (skip) {   // uniform over the workgroup
       if (t == 0) {
         q.sc[SC_CG_OK] = 0.0;
         q.sc[SC_P1OBJ] = 0.0;
@@ -569,7 +597,9 @@ __global__ void __launch_bounds__(WG) k_cg_final(Bat B, int m, const double* D, 
 // After dsyevd (ev ascending) and g = Q^T a: the hard case / secular Newton / interior choice of
 // riptrm_trs::trs_solve; writes the eigen coordinates pe of the boundary / hard-case candidate and
 // the result scalars
-__global__ void __launch_bounds__(WG) k_secular(Bat B, int m, double tolhc) {
+// choose = 0 (the StableIdentification service's certified CG skip, which needs xobj before it
+// decides on the CG): only the candidate and xobj; k_choose makes the interior choice after the CG.
+__global__ void __launch_bounds__(WG) k_secular(Bat B, int m, double tolhc, int choose = 1) {
   __shared__ double red[WG / 64];
   const Slot q = slot_at(B, blockIdx.y);
   const double *ev = q.v[VS_EV], *g = q.v[VS_G];
@@ -656,6 +686,15 @@ __global__ void __launch_bounds__(WG) k_secular(Bat B, int m, double tolhc) {
     o1 += g[i] * c;
   }
   const double xobj = 0.5 * blk_sum(o0, red) + blk_sum(o1, red);
+  if (!choose) {
+    if (threadIdx.x == 0) {
+      sc[SC_XOBJ] = xobj;
+      sc[SC_BKIND] = (double)kind;
+      sc[SC_BLAM1] = lam1;
+      sc[SC_MINEIG] = lmin;
+    }
+    return;
+  }
   const bool interior = sc[SC_CG_OK] != 0.0 && sc[SC_P1OBJ] <= xobj;   // RIPTRM.py:294-298
   if (threadIdx.x == 0) {
     sc[SC_INTERIOR] = interior ? 1.0 : 0.0;
@@ -663,6 +702,25 @@ __global__ void __launch_bounds__(WG) k_secular(Bat B, int m, double tolhc) {
     sc[SC_LAM1] = interior ? 0.0 : lam1;
     sc[SC_MINEIG] = lmin;
   }
+}
+
+// the interior choice of k_secular (RIPTRM.py:294-298) after a deferred (choose = 0) secular solve
+__global__ void k_choose(Bat B, int cnt) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= cnt) return;
+  double* sc = slot_at(B, k).sc;
+  const bool interior = sc[SC_CG_OK] != 0.0 && sc[SC_P1OBJ] <= sc[SC_XOBJ];
+  sc[SC_INTERIOR] = interior ? 1.0 : 0.0;
+  sc[SC_KIND] = interior ? 1.0 : sc[SC_BKIND];
+  sc[SC_LAM1] = interior ? 0.0 : sc[SC_BLAM1];
+}
+
+// Delta of slot k -> sc[SC_DELTA] (the CG's final terms write it otherwise; the deferred secular
+// solve runs before the CG)
+__global__ void k_set_delta(Bat B, int cnt, const double* D, int64_t dstride) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= cnt) return;
+  slot_at(B, k).sc[SC_DELTA] = D[(int64_t)B.ids[k] * dstride];
 }
 
 // x <- cgx when the interior candidate won (x = Q pe was computed before)
@@ -1136,8 +1194,10 @@ int riptrm_big_gep_ids(riptrm_ctx* c, int dim, const int32_t* sel, int count, co
     return fail(c, RIPTRM_E_STATE, "Exact_RepMat above dim 96 needs riptrm_trs_bind_workspace (order >= dim)");
   const Bat Bt = bat_of(c);
   std::vector<int32_t> info(c->big_slots);
+  std::vector<double> skip_done;   // SC_DONE of the pass's slots (4 = CG skipped by k_cg_wg's bound)
   for (int b0 = 0; b0 < count; b0 += c->big_slots) {
     const int cnt = std::min(c->big_slots, count - b0);
+    skip_done.clear();
     if (int rc = put_ids(c, Bt, sel + b0, cnt)) return rc;
     hipLaunchKernelGGL(k_load, dim3(blocks_of((int64_t)dim * dim, 256), cnt), dim3(256), 0, c->stream, Bt, dim, A, lda,
                        a_stride, a, ldv);
@@ -1145,22 +1205,37 @@ int riptrm_big_gep_ids(riptrm_ctx* c, int dim, const int32_t* sel, int count, co
     if (mineig_only) {
       if (int rc = eig_batched(c, Bt, cnt, false, dim, 0, dim)) return rc;
     } else if (per_instance && cg_one_workgroup(dim, cnt) && !getenv_is("RIPTRM_CG_SKIP", '0')) {
-      // eigenpairs first; the CG then reads A from the caller's array and is skipped where A is
-      // clearly indefinite (k_cg_wg: the interior candidate cannot win there)
+      // eigenpairs, g = Q^T a and the boundary candidate first; the CG then reads A from the
+      // caller's array and is skipped where the eigenpairs prove the interior candidate cannot win
+      // (k_cg_wg's bound), so the choice is the one the CG-first order makes (RIPTRM_CG_SKIP=0)
       if (int rc = eig_batched(c, Bt, cnt, true, dim, 0, dim)) return rc;
+      hipStream_t st = c->stream;
+      const int64_t N = Bt.N;
+      hipLaunchKernelGGL(k_gemv, dim3(blocks_of(dim, GV / 64), cnt), dim3(GV), 0, st, Bt, (int64_t)0, (int64_t)dim, dim,
+                         dim, off_vec(N, VS_A), off_vec(N, VS_G), (int64_t)-1);
+      hipLaunchKernelGGL(k_set_delta, dim3(blocks_of(cnt, 64)), dim3(64), 0, st, Bt, cnt, Delta, (int64_t)1);
+      hipLaunchKernelGGL(k_secular, dim3(1, cnt), dim3(WG), 0, st, Bt, dim, tolhc, 0);
       const int rl = cg_lds_rows(dim);
       const size_t shm = (size_t)rl * dim * sizeof(double);
       if (shm > 0)
         HIPCHK(c, hipFuncSetAttribute((const void*)k_cg_wg, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm));
-      hipLaunchKernelGGL(k_cg_wg, dim3(1, cnt), dim3(WG), shm, c->stream, Bt, dim, (int64_t)0, lda, Delta, (int64_t)1, rl,
-                         A, a_stride, 1);
+      hipLaunchKernelGGL(k_cg_wg, dim3(1, cnt), dim3(WG), shm, st, Bt, dim, (int64_t)0, lda, Delta, (int64_t)1, rl, A,
+                         a_stride, 1);
+      skip_done.resize(cnt);
+      HIPCHK(c, hipMemcpy2DAsync(skip_done.data(), sizeof(double), Bt.base + off_sc(N) + SC_DONE, (size_t)Bt.sd * sizeof(double),
+                                 sizeof(double), cnt, hipMemcpyDeviceToHost, st));
+      hipLaunchKernelGGL(k_choose, dim3(blocks_of(cnt, 64)), dim3(64), 0, st, Bt, cnt);
+      hipLaunchKernelGGL(k_gemv_t, dim3(blocks_of(dim, 256), cnt), dim3(256), 0, st, Bt, (int64_t)0, (int64_t)dim, dim, dim,
+                         off_vec(N, VS_PE), off_vec(N, VS_X));
+      hipLaunchKernelGGL(k_pick, dim3(blocks_of(dim, 256), cnt), dim3(256), 0, st, Bt, dim);
       HIPCHK(c, hipGetLastError());
-      if (int rc = big_after_eig(c, Bt, cnt, 0, dim, dim, tolhc)) return rc;
     } else if (int rc = big_solve(c, Bt, cnt, 0, dim, dim, Delta, 1, tolhc)) {
       return rc;
     }
     HIPCHK(c, hipMemcpyAsync(info.data(), Bt.infos, (size_t)cnt * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
+    c->big_cg_checked += (int64_t)skip_done.size();
+    for (double v : skip_done) c->big_cg_skipped += v == 4.0;
     for (int k = 0; k < cnt; ++k)
       if (info[k] != 0 && !per_instance)
         return fail(c, RIPTRM_E_HIP, "Exact_RepMat: rocsolver_dsyevd did not converge (info " + std::to_string(info[k]) +
@@ -1233,6 +1308,13 @@ int riptrm_trs_cache_stats(riptrm_ctx* ctx, int64_t* hits, int64_t* subproblems)
   if (!ctx) return RIPTRM_E_ARG;
   if (hits) *hits = ctx->big_cache_hits;
   if (subproblems) *subproblems = ctx->big_subproblems;
+  return RIPTRM_OK;
+}
+
+int riptrm_trs_skip_stats(riptrm_ctx* ctx, int64_t* checked, int64_t* skipped) {
+  if (!ctx) return RIPTRM_E_ARG;
+  if (checked) *checked = ctx->big_cg_checked;
+  if (skipped) *skipped = ctx->big_cg_skipped;
   return RIPTRM_OK;
 }
 

@@ -217,6 +217,23 @@ EXACT_BIG_CHUNK = 4        # lock-step iterations per advance on the HBM Exact_R
 TRS_WS_BUDGET = 16 << 30   # bytes of HBM the Exact_RepMat scratch may take (RIPTRM_TRS_WS_GB overrides)
 
 
+def bind_trs_scratch(ctx, lib, device, have, order: int, slots: int):
+    """Bind the HBM scratch of Exact_RepMat above RIPTRM_TRS_DIM_MAX (riptrm_trs_bind_workspace) for
+    `slots` matrices of order `order`.  `have` is the (buffer, order, slots) this caller bound before
+    (or None): it is reused when it is large enough and reallocated otherwise (a later begin() may ask
+    for more slots once RIPTRM_TRS_WS_GB or the batch changed).  Returns the (buffer, order, slots)
+    to keep."""
+    if have is None or have[1] < order or have[2] < slots:
+        nbytes = int(lib.riptrm_trs_workspace_bytes(int(order), int(slots)))
+        have = (torch.empty(nbytes + 256, dtype=torch.uint8, device=device), int(order), int(slots))
+    buf = have[0]
+    base = buf.data_ptr()
+    ptr = base + (-base) % 256
+    ctx.check(lib.riptrm_trs_bind_workspace(ctx.h, ctypes.c_void_p(ptr), buf.numel() - (ptr - base), int(order),
+                                            int(slots)), "riptrm_trs_bind_workspace")
+    return have
+
+
 def trs_workspace_slots(lib, order: int, want: int) -> int:
     """Slots of order `order` for the HBM Exact_RepMat path: one per subproblem served in the same
     pass (`want`), as many as the budget holds, at least one."""
@@ -283,7 +300,7 @@ class NonnegPCABatch:
         self.ws_bytes = nbytes
         self.bound = False
         self._keep: List[torch.Tensor] = []
-        self._trs_ws: Optional[torch.Tensor] = None   # Exact_RepMat above RIPTRM_TRS_DIM_MAX
+        self._trs_ws = None   # (buffer, order, slots) of Exact_RepMat above RIPTRM_TRS_DIM_MAX
         self._trs_cache: Optional[torch.Tensor] = None   # its eigendecomposition cache
         # log records copied to the host by drain_logs() (riptrm_log_rebase), per instance
         self.drain = bool(drain_logs)
@@ -534,14 +551,7 @@ class NonnegPCABatch:
             # slot per instance served in the same pass (riptrm_trs_bind_workspace;
             # csrc/riptrm_trs_big.hip), as many as trs_workspace_slots allows
             slots = trs_workspace_slots(self.lib, self.n, self.batch)
-            if self._trs_ws is None:
-                nbytes = int(self.lib.riptrm_trs_workspace_bytes(self.n, slots))
-                self._trs_ws = torch.empty(nbytes + 256, dtype=torch.uint8, device=self.device)
-            base = self._trs_ws.data_ptr()
-            ptr = base + (-base) % 256
-            self.ctx.check(self.lib.riptrm_trs_bind_workspace(self.ctx.h, ctypes.c_void_p(ptr),
-                                                              self._trs_ws.numel() - (ptr - base), self.n, slots),
-                           "riptrm_trs_bind_workspace")
+            self._trs_ws = bind_trs_scratch(self.ctx, self.lib, self.device, self._trs_ws, self.n, slots)
             # with the second-order test every trial point's eigenpairs are computed anyway; a
             # subproblem at that same point (step accepted without dual clipping) then skips its
             # eigensolve (RIPTRM.py:686-692 keeps HwNewmatrix the same way)

@@ -274,7 +274,7 @@ class SIBatch:
         self.ws_bytes = nbytes
         self._keep: List[torch.Tensor] = []
         self.ro: Optional[ResolvedOptions] = None
-        self._trs_ws: Optional[torch.Tensor] = None   # Exact_RepMat at d >= 8 (manifold.dim > 96)
+        self._trs_ws = None   # (buffer, order, slots): Exact_RepMat at d >= 8 (manifold.dim > 96)
 
     def _view(self, kind: int, shape):
         off = int(self.lib.riptrm_si_workspace_offset(self.d, self.N, self.m, self.batch, self.cap, kind))
@@ -365,16 +365,9 @@ class SIBatch:
             # d >= 8: the subproblem's matrix (manifold.dim squared) no longer fits LDS; instances park
             # at each subproblem and the host's batched service (riptrm_trs_big.hip) solves them in
             # caller-owned HBM scratch, one slot per instance of a pass (riptrm_trs_bind_workspace)
-            from engine import trs_workspace_slots
+            from engine import bind_trs_scratch, trs_workspace_slots
             slots = trs_workspace_slots(self.lib, tdim, self.batch)
-            if self._trs_ws is None:
-                nbytes = int(self.lib.riptrm_trs_workspace_bytes(tdim, slots))
-                self._trs_ws = torch.empty(nbytes + 256, dtype=torch.uint8, device=self.device)
-            base = self._trs_ws.data_ptr()
-            ptr = base + (-base) % 256
-            self.ctx.check(self.lib.riptrm_trs_bind_workspace(self.ctx.h, ctypes.c_void_p(ptr),
-                                                              self._trs_ws.numel() - (ptr - base), tdim, slots),
-                           "riptrm_trs_bind_workspace")
+            self._trs_ws = bind_trs_scratch(self.ctx, self.lib, self.device, self._trs_ws, tdim, slots)
         tabs = ro.device_tables(self.device)
         self._keep = [X, Y] + tabs
         self.ctx.set_stream(_stream_handle(self.device))
@@ -384,6 +377,13 @@ class SIBatch:
                                                 len(ro.mu_tab)), "riptrm_si_solve")
         self.ro = ro
         return ro
+
+    def trs_skip_stats(self):
+        """(subproblems whose CG was decided on their eigenpairs, CGs skipped) since the context was
+        created (riptrm_trs_skip_stats)."""
+        a, b = ctypes.c_int64(0), ctypes.c_int64(0)
+        self.ctx.check(self.lib.riptrm_trs_skip_stats(self.ctx.h, ctypes.byref(a), ctypes.byref(b)), "riptrm_trs_skip_stats")
+        return int(a.value), int(b.value)
 
     def profile_enable(self, on: bool = True):
         self.ctx.check(self.lib.riptrm_si_profile_enable(self.ctx.h, 1 if on else 0), "riptrm_si_profile_enable")

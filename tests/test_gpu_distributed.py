@@ -156,3 +156,40 @@ def test_bench_configs3_per_rank_shape_two_ranks():
     for k, i in enumerate(ids):
         np.testing.assert_array_equal(gx[i], rx[k], err_msg=f"global instance {i}")
         np.testing.assert_array_equal(gy[i], ry[k], err_msg=f"global instance {i}")
+
+
+def test_bench_rccl_one_rank_matches_no_dist_bitwise():
+    """Every RCCL call site of the N-GPU bench path, executed on the one GPU: `bench.py --gpus 1
+    --dist-at-1` initialises a one-rank "nccl" (RCCL) process group with device_id, so rank_census's
+    device-tensor all_gather, the timing all_reduce(SUM / MAX) and distributed.gather_rows' final
+    all_gather of x, y and the stats all run over RCCL at the configs[3] per-rank shape (n = 4000,
+    128 instances).  The gathered x / y / stats must equal a run without a process group bitwise
+    (the reference's multi-run axis, src/NonnegPCA/config_simulation.yaml:35-42)."""
+    import json
+    import subprocess
+    import sys
+    import tempfile
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    base = [sys.executable, "-u", os.path.join(root, "bench.py"), "--gpus", "1", "--dim", "4000", "--batch", "128",
+            "--warmup", "1", "--steps", "2", "--cpu-budget", "0"]
+    with tempfile.TemporaryDirectory() as td:
+        outs, dumps = [], []
+        for extra in (["--dist-at-1"], []):
+            dumps.append(os.path.join(td, f"g{len(dumps)}.npz"))
+            r = subprocess.run(base + extra + ["--dump", dumps[-1]], env=env, capture_output=True, text=True, timeout=400)
+            assert r.returncode == 0, r.stderr[-3000:]
+            lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+            assert len(lines) == 1, r.stdout
+            outs.append(json.loads(lines[0]))
+        a, b = np.load(dumps[0]), np.load(dumps[1])
+        for key in ("x", "y"):
+            np.testing.assert_array_equal(a[key], b[key], err_msg=key)
+        import engine
+        keep = [i for i in range(a["stats"].shape[1]) if i != engine.C["RIPTRM_STAT_STOP_RUNTIME"]]   # a clock
+        np.testing.assert_array_equal(a["stats"][:, keep], b["stats"][:, keep], err_msg="stats")
+    cfg = outs[0]["config"]
+    assert cfg["backend"] == "nccl", cfg
+    assert cfg["ranks"] == [{"rank": 0, "world_size_seen": 1, "device": 0, "rccl": True}], cfg["ranks"]
+    assert outs[1]["config"]["backend"] is None and outs[1]["config"]["ranks"][0]["rccl"] is False
+    assert outs[0]["n_gpus"] == 1 and outs[0]["config"]["global_batch"] == 128

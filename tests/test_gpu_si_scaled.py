@@ -216,3 +216,51 @@ def test_si_exact_hbm_many_columns():
     gl = res.log(0)
     assert 0 < len([k for k in gl["dxtype"] if k is not None]) <= 3
     compare_until_flip(gl, ref.log)
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("d,sos,bench_starts", [(8, True, True), (8, False, False), (16, True, False)])
+def test_si_exact_cg_skip_is_bitwise_neutral(d, sos, bench_starts, monkeypatch):
+    """The StableIdentification HBM service decides on the eigenpairs whether SciPy's CG
+    (RIPTRM.py:246-251) can matter: it skips the CG only where a bound from them shows no CG iterate
+    that passes the reference's residual / radius test can have p1obj <= xobj (RIPTRM.py:294-298;
+    riptrm_trs_big.hip k_cg_wg).  So the default and RIPTRM_CG_SKIP=0 (always run the CG, in the
+    order the NonnegPCA path uses) must give the same logs (cost, residual, normdx, dxtype,
+    mineigvalHw) and x / y bit for bit; on the bench's own d = 8 starts some CGs must really be
+    skipped (the test is not vacuous)."""
+    import bench
+    import si
+    if bench_starts:
+        xs, ys, (X, XP, h, constset) = bench.si_starts(8, list(range(8)), d)
+        cons = si.expand_constset(constset)
+        mk = lambda: _load(si.SIBatch(d, X.shape[1], cons.shape[0], len(xs), log_capacity=1024), X, XP, h, cons)   # noqa: E731
+        opt = {"maxiter": 3, "tolresid": 0.0, "maxtime": 1e9}
+    else:
+        data, st = _inst(d, 2)
+        xs = np.stack([x for x, _ in st])
+        ys = np.stack([y for _, y in st])
+        mk = lambda: _batch(data, len(xs))   # noqa: E731
+        opt = {"maxiter": 1, "inner_maxiter": 4, "tolresid": 0.0, "maxtime": 1e9}
+    opt.update(TRS_solver="Exact_RepMat", second_order_stationarity=sos, manviofun=si.si_manviofun)
+    monkeypatch.delenv("RIPTRM_CG_SKIP", raising=False)
+    e1 = mk()
+    r1 = e1.solve(xs, ys, opt)
+    checked, skipped = e1.trs_skip_stats()
+    monkeypatch.setenv("RIPTRM_CG_SKIP", "0")
+    e0 = mk()
+    r0 = e0.solve(xs, ys, opt)
+    assert e0.trs_skip_stats() == (0, 0)
+    print(f"d={d} sos={sos}: {checked} subproblems decided on their eigenpairs, {skipped} CGs skipped")
+    assert checked > 0
+    if bench_starts:
+        assert skipped > 0
+    for b in range(len(xs)):
+        for key in ("cost", "residual", "normdx", "dxtype", "mineigvalHw", "inner_status", "radius_update"):
+            assert r1.log(b)[key] == r0.log(b)[key], (b, key)
+    np.testing.assert_array_equal(r1.x.cpu().numpy(), r0.x.cpu().numpy())
+    np.testing.assert_array_equal(r1.y.cpu().numpy(), r0.y.cpu().numpy())
+
+
+def _load(eng, X, XP, h, cons):
+    eng.load(X, XP, h, cons)
+    return eng
