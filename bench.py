@@ -77,7 +77,9 @@ def _oracle_positions(n: int, seed: int, pmax: int, budget_s: float, trs: str, s
     except O.BudgetExceeded:
         pass
     h = orc.outer_heads
-    return {p: h[p] - h[p - 1] for p in range(1, pmax + 1) if p in h and p - 1 in h}
+    durs = {p: h[p] - h[p - 1] for p in range(1, pmax + 1) if p in h and p - 1 in h}
+    _oracle_positions.inner_durations = list(orc.inner_durations)
+    return durs
 
 
 def _window_rate(durs, positions):
@@ -96,15 +98,34 @@ def _blas_threads():
         return int(os.environ.get("OMP_NUM_THREADS", "1"))
 
 
-def cpu_baseline(n: int, positions, budget_s: float, trs: str = "tCG"):
+def _inner_sampled(idurs, inner_per_outer, procs, cores, n, trs, who, budget_s):
+    """A window the CPU cannot finish in its budget (Exact_RepMat at n = 1000: one 2n x 2n pencil
+    per inner step): the solver seconds of the inner steps it completed, converted to outer
+    iterations/s with the GPU window's own inner iterations per outer iteration."""
+    if not idurs or not inner_per_outer:
+        return None
+    per_inner = sum(idurs) / len(idurs)
+    return {"value": procs / (per_inner * inner_per_outer), "unit": "outer iterations/s", "cores": int(cores),
+            "kind": "port",
+            "sample": (f"oracle/riptrm_oracle.py NonnegPCAVectorized, {who}, n={n}"
+                       + (", TRS_solver=Exact_RepMat (trs_oracle: 2n x 2n pencil, scipy.linalg.eig)" if trs != "tCG" else "")
+                       + f": the window does not complete in the {budget_s:.0f} s budget, so the rate is sampled per inner "
+                         f"step -- {len(idurs)} inner steps of outer iteration 1.. at {per_inner:.2f} s each (evaluation "
+                         f"excluded) -- times the GPU window's {inner_per_outer:.2f} inner iterations per outer iteration"
+                       + (f", x {procs} processes" if procs > 1 else "")),
+            "sampled_inner_s": per_inner}
+
+
+def cpu_baseline(n: int, positions, budget_s: float, trs: str = "tCG", inner_per_outer=None):
     """SURVEY.md §8d variant (V), one process with all BLAS threads: the oracle (vectorised NumPy +
     OpenBLAS dsymv) on one instance, timed over the GPU window's own outer iterations."""
     from oracle import nonnegpca_gen as G
     durs = _oracle_positions(n, G.SEED0, max(positions), budget_s, trs)
     rate = _window_rate(durs, positions)
-    if rate is None:
-        return None
     cores = _blas_threads()
+    if rate is None:
+        return _inner_sampled(_oracle_positions.inner_durations, inner_per_outer, 1, cores, n, trs,
+                              f"1 instance (seed {G.SEED0}), {cores} BLAS threads", budget_s)
     return {"value": rate, "unit": "outer iterations/s", "cores": int(cores), "kind": "port",
             "sample": (f"oracle/riptrm_oracle.py NonnegPCAVectorized, 1 instance n={n} (reference generator recipe, "
                        f"seed {G.SEED0}), timed over the GPU window's own outer-iteration positions "
@@ -130,10 +151,12 @@ def _cpu_worker(argv):
     """One single-threaded oracle instance (run in its own process by cpu_baseline_pool)."""
     n, seed, pmax, budget, trs = int(argv[0]), int(argv[1]), int(argv[2]), float(argv[3]), argv[4]
     durs = _oracle_positions(n, seed, pmax, budget, trs)
-    print(json.dumps({str(k): v for k, v in durs.items()}), flush=True)
+    out = {str(k): v for k, v in durs.items()}
+    out["inner"] = _oracle_positions.inner_durations
+    print(json.dumps(out), flush=True)
 
 
-def cpu_baseline_pool(n: int, positions, budget_s: float, procs: int, trs: str = "tCG"):
+def cpu_baseline_pool(n: int, positions, budget_s: float, procs: int, trs: str = "tCG", inner_per_outer=None):
     """SURVEY.md §8d variant (V) as a pool: `procs` single-threaded oracle processes, one instance
     each (seeds SEED0 + i), run concurrently, each timed over the GPU window's own positions;
     aggregate = sum of the per-process rates, over processes that completed the whole window."""
@@ -143,18 +166,21 @@ def cpu_baseline_pool(n: int, positions, budget_s: float, procs: int, trs: str =
     ps = [subprocess.Popen([sys.executable, os.path.abspath(__file__), "--cpu-worker", str(n), str(G.SEED0 + i),
                             str(max(positions)), str(budget_s), trs], stdout=subprocess.PIPE,
                            stderr=subprocess.DEVNULL, env=env, text=True) for i in range(procs)]
-    rates = []
+    rates, inner = [], []
     for p in ps:
         out, _ = p.communicate(timeout=budget_s + 600)
         try:
-            durs = {int(k): v for k, v in json.loads(out.strip().splitlines()[-1]).items()}
+            rec = json.loads(out.strip().splitlines()[-1])
+            inner.extend(rec.pop("inner", []))
+            durs = {int(k): v for k, v in rec.items()}
         except Exception:
             continue
         r = _window_rate(durs, positions)
         if r is not None:
             rates.append(r)
     if not rates:
-        return None
+        return _inner_sampled(inner, inner_per_outer, procs, procs, n, trs,
+                              f"{procs} single-threaded processes, one instance each (seeds {G.SEED0}..)", budget_s)
     # every process runs the same amount of work, so the complete ones are a fair sample; scale the
     # aggregate to all `procs` cores (incomplete processes ran on cores too)
     agg = sum(rates) / len(rates) * procs
@@ -186,14 +212,19 @@ def cpu_reference_structured(n: int, budget_s: float):
 
 def host_cpu_info() -> dict:
     """lscpu model name and os.cpu_count() of the host the CPU legs ran on."""
-    model = None
+    model, cores_per_socket, sockets = None, None, None
     try:
         import subprocess
         out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
         for line in out.splitlines():
-            if line.split(":")[0].strip() == "Model name":
-                model = line.split(":", 1)[1].strip()
-                break
+            key, _, val = line.partition(":")
+            key, val = key.strip(), val.strip()
+            if key == "Model name" and model is None:
+                model = val
+            elif key == "Core(s) per socket":
+                cores_per_socket = int(val)
+            elif key == "Socket(s)":
+                sockets = int(val)
     except Exception:
         pass
     if model is None:
@@ -204,7 +235,26 @@ def host_cpu_info() -> dict:
                     break
         except Exception:
             pass
-    return {"cpu_model": model, "os_cpu_count": os.cpu_count()}
+    phys = cores_per_socket * sockets if cores_per_socket and sockets else None
+    return {"cpu_model": model, "os_cpu_count": os.cpu_count(), "physical_cores": phys}
+
+
+def core_rationale(cpu: dict, gpus_per_node: int = 8) -> dict:
+    """Why the CPU legs use the cores they use, and what the whole host would give (SURVEY.md §8d:
+    the baseline is context, not the target).  The GPU box leases this job one GPU and 16 of the
+    host's CPUs (OMP_NUM_THREADS / MAX_JOBS are 16 there, and its process limits are sized for 16
+    workers), which is also one GPU's share of an 8-GPU node's physical cores on the pool's hosts; a
+    pool over the whole host is outside the lease, so it is extrapolated, not timed."""
+    phys = cpu.get("physical_cores")
+    out = {"core_rationale": (f"{cpu['cores']} cores = the CPU share the GPU box leases to one GPU's job (OMP_NUM_THREADS="
+                              f"{os.environ.get('OMP_NUM_THREADS', '?')} there)"
+                              + (f"; the host has {phys} physical cores / {cpu.get('os_cpu_count')} threads for "
+                                 f"{gpus_per_node} GPUs = {phys / gpus_per_node:g} cores per GPU" if phys else "")
+                              + "; a whole-host pool is outside the lease: whole_host_estimate scales the pool linearly "
+                                "to every physical core (an upper bound, not measured)")}
+    if phys and cpu.get("cores"):
+        out["whole_host_estimate"] = cpu["value"] * phys / cpu["cores"]
+    return out
 
 
 def pick_cpu_baseline(threaded, pool):
@@ -547,17 +597,19 @@ def main():
         if args.cpu_budget > 0 and world == 1:
             positions = window_positions(W, K, args.cycle)
             log(f"CPU baseline (oracle) over positions {_pos_text(positions)} ...")
-            threaded = cpu_baseline(n, positions, args.cpu_budget, args.trs)
+            ipo = (inner_all / outer_all) if outer_all > 0 else None
+            threaded = cpu_baseline(n, positions, args.cpu_budget, args.trs, ipo)
             # the pool runs one instance per process: never more processes than the workload has
             # instances (configs[1] is ONE instance; 16 processes would time 16x its work)
             procs = min(args.cpu_procs, B)
             pool = None
             if procs > 0:
                 log(f"CPU baseline, {procs} single-threaded processes ...")
-                pool = cpu_baseline_pool(n, positions, args.cpu_pool_budget, procs, args.trs)
+                pool = cpu_baseline_pool(n, positions, args.cpu_pool_budget, procs, args.trs, ipo)
             cpu = pick_cpu_baseline(threaded, pool)
             if cpu is not None:
                 cpu.update(host_cpu_info())
+                cpu.update(core_rationale(cpu))
                 cpu["gpu_over_cpu"] = (outer_all / T) / cpu["value"]
                 if args.ref_structured_dim > 0:
                     log(f"CPU reference-structured variant (R), n={args.ref_structured_dim} ...")
@@ -883,6 +935,7 @@ def bench_si(args, world, rank, dev, dist):
         cpu = pick_cpu_baseline(cpu, pool)
         if cpu is not None:
             cpu.update(host_cpu_info())
+            cpu.update(core_rationale(cpu))
             cpu["gpu_over_cpu"] = (outer / T) / cpu["value"]
     print(json.dumps({
         "metric": f"outer RIPTRM iterations/sec, StableIdentification d={d} (Product(Skew,SPD,SPD)), batch {B}/GPU",

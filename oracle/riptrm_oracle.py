@@ -523,6 +523,7 @@ class RIPTRMOracle:
         self.passes = 1        # GPU pass accounting: S.x0 once, then see inner_step
         self.deadline = deadline
         self.outer_heads: Dict[int, float] = {}
+        self.inner_durations: List[float] = []   # solver seconds of each completed inner step
 
     # base_solver.py:58-76
     def add_log(self, it, start_time, ev, status):
@@ -704,7 +705,9 @@ class RIPTRMOracle:
             it += 1
             if self.deadline is not None and self.clock() > self.deadline:
                 raise BudgetExceeded()
+            t_step = self.clock()
             exitflag, x, y, Delta, info = self.inner_step(P, x, y, mu, Delta, it, inner_option)
+            self.inner_durations.append(self.clock() - t_step)
             self.inner_total += 1
             if o['save_inner_iteration']:
                 t0 = self.clock()

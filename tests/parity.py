@@ -693,10 +693,13 @@ def _oracle_job(job):
         return O.RIPTRMOracle(opt).run(O.NonnegPCAVectorized(S, S=S, symv=False), x0, y0), None
     p = np.random.RandomState(seed).permutation(S.shape[0])
     Sp = np.ascontiguousarray(S[p][:, p])
-    return O.RIPTRMOracle(opt).run(O.NonnegPCAVectorized(Sp, S=Sp), x0[p], y0[p]), None
+    r = O.RIPTRMOracle(opt).run(O.NonnegPCAVectorized(Sp, S=Sp), x0[p], y0[p])
+    inv = np.argsort(p)
+    r.x, r.y = np.asarray(r.x)[inv], np.asarray(r.y)[inv]   # back to the instance's own order
+    return r, None
 
 
-def check_instances_parallel(items, opt, workers=16, progress=print, every_s=20.0):
+def check_instances_parallel(items, opt, workers=16, progress=print, every_s=20.0, null=False):
     """check_instance for many instances with the 6 oracle runs of each (reference + the 5
     order variants) spread over a pool of `workers` single-threaded processes.  items: dicts with
     gl (the GPU log), S (n x n, the device's own S), x0, y0 and optionally gpu_x, gpu_tcg, name.
@@ -744,13 +747,19 @@ def check_instances_parallel(items, opt, workers=16, progress=print, every_s=20.
                         P = O.NonnegPCAVectorized(S, S=S)
                         name = it.get("name", k)
                         try:
-                            r = check_against(it["gl"], ra, states, variants, P, O.RIPTRMOracle(opt).inner_step,
-                                              gpu_x=it.get("gpu_x"), gpu_tcg=it.get("gpu_tcg"),
-                                              resume=it.get("resume"), opt=opt)
+                            if null:
+                                r = check_null(it["gl"], ra, variants, it["gpu_x"], it["gpu_y"], it.get("gpu_tcg"))
+                            else:
+                                r = check_against(it["gl"], ra, states, variants, P, O.RIPTRMOracle(opt).inner_step,
+                                                  gpu_x=it.get("gpu_x"), gpu_tcg=it.get("gpu_tcg"),
+                                                  resume=it.get("resume"), opt=opt)
                         except AssertionError as e:
                             raise AssertionError((f"instance {name}",) + tuple(e.args)) from e
                         results[name] = r
-                        progress(f"[parity] instance {name}: {r} ({time.time() - t0:.0f} s)")
+                        progress(f"[parity] instance {name}: "
+                                 + (f"GPU div row {r['gpu']['div_row']} of {r['gpu']['rows']}, variants "
+                                    f"{[v['div_row'] for v in r['variants']]}" if null else f"{r}")
+                                 + f" ({time.time() - t0:.0f} s)")
                         for q in need:
                             out.pop(q)
                         last = time.time()
@@ -783,3 +792,195 @@ def check_budget(results, B, late_ties_free=False):
                if not (late_ties_free and f[0] >= 0.75 * f[3] and f[2] <= 1e-12 and len(f) < 6)}
     assert len(counted) <= B // 2, flips
     assert len(exc) <= excursion_budget(B), exc
+
+
+# ---- null calibration: the GPU as one more summation-order variant (round 5) ------------------
+#
+# The bar above judges the GPU's trajectory against the reference run with classifiers for the
+# rows where the two leave each other.  The null test below asks the question those classifiers
+# answer indirectly: does the GPU leave the reference run the way a further CPU order variant of
+# the same arithmetic does (order_variants: dgemv, dsymv on symmetric permutations), or worse?
+# Each run m (the GPU, and every variant) is measured against the reference run R by
+#   div_row   the first row whose branch decisions differ (the log length if none);
+#   dx, dy    ||x_m - x_R|| and ||y_m - y_R|| / ||y_R|| at the end of the window;
+#   outer_dev the largest relative deviation of the KKT residual at the end of each outer iteration.
+# Per instance the GPU's dx, dy and outer_dev must be within MULT x the largest variant's (plus a
+# rounding floor).  Over the instances of a test, the GPU's divergence row must rank among the
+# variants' like one more exchangeable variant: under that null its mid-rank percentile u (0 = it
+# diverges before every variant, 1 = after every one) has mean 1/2, and P(u = 0 strictly) <=
+# 1/(K+1) per instance; the test fails at level NULL_ALPHA if the mean is too low or there are too
+# many strictly-earliest instances.  tests/test_oracle.py calibrates this on the CPU (a variant in
+# the GPU's place passes; a run with a 1e-9 relative Hessian error, a real defect far below what a
+# trajectory comparison sees by eye, fails).
+
+NULL_MULT = 10.0
+NULL_ALPHA = 0.01
+NULL_FLOOR_X = 1e-10      # ||x|| = 1: rounding of a K = 20 window is ~1e-13
+NULL_FLOOR_Y = 1e-10      # relative
+NULL_FLOOR_OUTER = 1e-9   # relative
+
+
+def outer_residuals(log):
+    """{outer iteration k: KKT residual of its last row} (row 0 for k = 0)."""
+    it = log["iteration"]
+    return {int(it[r]): float(log["residual"][r]) for r in outer_rows(log)}
+
+
+def run_divergence(log, x, y, ref_log, ref_x, ref_y):
+    """One run's distance from the reference run (see above)."""
+    f = first_branch_flip(log, ref_log)
+    nrows = len(ref_log["iteration"])
+    ro, mo = outer_residuals(ref_log), outer_residuals(log)
+    ks = sorted(set(ro) & set(mo))
+    od = max([abs(mo[k] - ro[k]) / max(abs(ro[k]), 1e-300) for k in ks] + [0.0])
+    x, y, rx, ry = (np.asarray(v, float).ravel() for v in (x, y, ref_x, ref_y))
+    return {"div_row": nrows if f is None else int(f[0]), "flip": None if f is None else [int(f[0]), f[1]],
+            "rows": nrows, "dx": float(np.linalg.norm(x - rx)),
+            "dy": float(np.linalg.norm(y - ry) / max(np.linalg.norm(ry), 1e-300)), "outer_dev": float(od)}
+
+
+def null_row(gpu, variants, mult=NULL_MULT):
+    """The GPU's run_divergence against its variants' (a list): mid-rank percentile u of the
+    divergence row, whether it is strictly the earliest, and the per-instance bars' ratios."""
+    K = len(variants)
+    dg = gpu["div_row"]
+    below = sum(1 for v in variants if v["div_row"] < dg)
+    ties = sum(1 for v in variants if v["div_row"] == dg)
+    row = {"gpu": gpu, "variants": variants, "u": (below + 0.5 * ties) / K if K else 0.5,
+           "earliest": below == 0 and ties == 0}
+    for key, floor in (("dx", NULL_FLOOR_X), ("dy", NULL_FLOOR_Y), ("outer_dev", NULL_FLOOR_OUTER)):
+        vmax = max([v[key] for v in variants] + [0.0])
+        row[key + "_limit"] = mult * vmax + floor
+        row[key + "_ok"] = bool(gpu[key] <= row[key + "_limit"])
+    return row
+
+
+def binom_upper(n, p, alpha):
+    """Smallest q with P(Binomial(n, p) > q) <= alpha."""
+    from math import comb
+    tail = 1.0
+    for q in range(n + 1):
+        tail -= comb(n, q) * p ** q * (1 - p) ** (n - q)
+        if tail <= alpha:
+            return q
+    return n
+
+
+def null_summary(rows, alpha=NULL_ALPHA):
+    """Aggregate of null_row over a test's instances (see above); ok = every bar holds."""
+    from statistics import NormalDist
+    n = len(rows)
+    K = min(len(r["variants"]) for r in rows)
+    mean_u = sum(r["u"] for r in rows) / n
+    # the mid-rank of one exchangeable run among K + 1 has variance <= (K + 2) / (12 K) (ties only shrink it)
+    sd = ((K + 2) / (12.0 * K * n)) ** 0.5
+    u_min = 0.5 - NormalDist().inv_cdf(1 - alpha) * sd
+    earliest = sum(1 for r in rows if r["earliest"])
+    q = binom_upper(n, 1.0 / (K + 1), alpha)
+    per = {k: [i for i, r in enumerate(rows) if not r[k + "_ok"]] for k in ("dx", "dy", "outer_dev")}
+    ok = mean_u >= u_min and earliest <= q and not any(per.values())
+    return {"instances": n, "variants": K, "mean_u": mean_u, "mean_u_min": u_min, "earliest": earliest,
+            "earliest_max": q, "failed_bars": per, "ok": bool(ok)}
+
+
+def leave_one_out(variant_runs, mult=NULL_MULT):
+    """The null's own behaviour: each CPU variant in the GPU's place against the others (K - 1).
+    variant_runs: per instance, the list of run_divergence dicts of its K variants.  Returns the
+    null_summary of all (instance, variant) rows plus the per-row list."""
+    rows = []
+    for runs in variant_runs:
+        for j in range(len(runs)):
+            rows.append(null_row(runs[j], runs[:j] + runs[j + 1:], mult))
+    return rows
+
+
+def check_null(gl, ra, variants, gpu_x, gpu_y, gpu_tcg=None):
+    """One instance's GPU trajectory under the round-5 bar: the rows on which the reference run is
+    reproducible under summation order (before every variant's first branch flip) and before the
+    GPU's own first flip meet the envelope bar (compare_logs(envelope=...), compare_tcg_iters);
+    past them the trajectory is summarised by run_divergence, against the variants', in null_row
+    (the per-instance MULT bars here, the rank test over the instances in null_summary).  Returns
+    the null_row dict (+ the envelope excursions and the number of rows compared row by row)."""
+    env = envelope(ra, variants)
+    nrows = len(ra.log["iteration"])
+    fv = min([f[0] for f in env["_flips"] if f is not None], default=nrows)
+    fg = first_branch_flip(gl, ra.log)
+    upto = min(fv, nrows if fg is None else fg[0])
+    exc = []
+    if upto > 0:
+        compare_logs(_prefix(gl, upto), _prefix(ra.log, upto), envelope=env, excursions=exc)
+    if gpu_tcg is not None and upto > 1:
+        pre = type("Pre", (), {"trace": ra.trace[:upto - 1]})()
+        compare_tcg_iters(list(gpu_tcg)[:upto - 1], pre, {"_tcg": env["_tcg"][:upto - 1]})
+    vr = [run_divergence(v.log, v.x, v.y, ra.log, ra.x, ra.y) for v in variants]
+    row = null_row(run_divergence(gl, gpu_x, gpu_y, ra.log, ra.x, ra.y), vr)
+    row.update(excursions=exc, rows_compared=int(upto))
+    return row
+
+
+def null_table(rows, names, summary, path=None):
+    """The per-instance table of a null test (GPU vs variants: divergence rows, final distances,
+    outer deviation) as JSON-able dict; written to `path` when given."""
+    import json
+    out = {"summary": summary, "instances": []}
+    for name, r in zip(names, rows):
+        g = r["gpu"]
+        out["instances"].append({
+            "name": name, "rows": g["rows"], "gpu_first_flip": g["flip"], "gpu_div_row": g["div_row"],
+            "variant_div_rows": [v["div_row"] for v in r["variants"]], "u": r["u"], "earliest": r["earliest"],
+            "gpu_dx": g["dx"], "variant_dx_max": max(v["dx"] for v in r["variants"]),
+            "gpu_dy": g["dy"], "variant_dy_max": max(v["dy"] for v in r["variants"]),
+            "gpu_outer_dev": g["outer_dev"], "variant_outer_dev_max": max(v["outer_dev"] for v in r["variants"]),
+            "rows_compared_row_by_row": r.get("rows_compared"), "excursions": r.get("excursions")})
+    if path:
+        import os
+        os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
+        json.dump(out, open(path, "w"), indent=1, default=str)
+    return out
+
+
+def assert_null(rows, names, path=None, budget=None):
+    """null_summary over a test's rows; the table goes to `path`; fails on any bar (and on more
+    envelope excursions than excursion_budget)."""
+    summary = null_summary(rows)
+    tab = null_table(rows, names, summary, path)
+    for it in tab["instances"]:
+        print("[null]", it["name"], "gpu div row", it["gpu_div_row"], "of", it["rows"], "variants", it["variant_div_rows"],
+              "u %.2f" % it["u"], "dx %.1e (variants %.1e)" % (it["gpu_dx"], it["variant_dx_max"]),
+              "outer %.1e (%.1e)" % (it["gpu_outer_dev"], it["variant_outer_dev_max"]), flush=True)
+    print("[null] summary", summary, flush=True)
+    exc = [n for n, r in zip(names, rows) if r.get("excursions")]
+    assert len(exc) <= (excursion_budget(len(rows)) if budget is None else budget), exc
+    assert summary["ok"], summary
+    return summary
+
+
+def si_order_variants(data, x0, y0, opt, seeds=(1, 2, 3), structured=True):
+    """StableIdentification runs that are the same arithmetic in another summation order: the
+    reference-structured wiring (SIStructured: per-constraint loops, RIPTRM.py:475-571), and the
+    vectorised oracle on a coordinate permutation Pi (X, XP -> Pi X, Pi XP; J, R, Q -> Pi J Pi^T ...;
+    the constraints on A_rc -> A'_{pi(r) pi(c)}, their order shuffled too), which leaves the cost,
+    the constraints, the SPD metric and every logged quantity invariant (A' = Pi A Pi^T, E' = Pi E).
+    x and y of the permuted runs are mapped back.  The SI analogue of order_variants."""
+    import copy
+    from oracle import si_oracle as SI
+    out = []
+    if structured:
+        out.append(SI.solve(data, x0, y0, opt, structured=True))
+    d, m = data.d, data.m
+    for sd in seeds:
+        rs = np.random.RandomState(sd)
+        p = rs.permutation(d)
+        inv = np.argsort(p)
+        sig = rs.permutation(m)
+        dp = copy.copy(data)
+        dp.X, dp.XP = np.ascontiguousarray(data.X[p]), np.ascontiguousarray(data.XP[p])
+        dp.cons = [(k, int(inv[r]), int(inv[c]), p0, p1) for (k, r, c, p0, p1) in (data.cons[i] for i in sig)]
+        xp = np.stack([np.asarray(x0)[k][p][:, p] for k in range(3)])
+        r = SI.solve(dp, xp, np.asarray(y0)[sig], opt)
+        r.x = np.stack([np.asarray(r.x)[k][inv][:, inv] for k in range(3)])
+        yy = np.empty(m)
+        yy[sig] = np.asarray(r.y)
+        r.y = yy
+        out.append(r)
+    return out

@@ -79,56 +79,46 @@ def test_si_scaled_tcg_teacher_forced(d):
         assert err <= 1e-8, (d, b, j, err)
 
 
-@pytest.mark.parametrize("d", DS)
-def test_si_scaled_trajectory_matches_oracle(d):
-    """Two starts, two outer iterations with at most 25 inner iterations each (inner_maxiter's reset
-    to the outer start point, RIPTRM.py:835-842, is part of the path): every row before the first
-    branch flip (at most 20 compared) within the NonnegPCA bounds, or -- where those calibrated
-    bounds do not hold even for the CPU back-ends -- within 10x the CPU back-ends' own spread
-    (compare_until_flip's bar up to
-    the flip; past it these trajectories are chaotic: at d = 16 even the two CPU back-ends end the
-    first outer iteration 3x apart in the residual, so no outer-level bar holds).  The first flip must be a radius-expansion rounding
-    tie, come late (row >= 20), or come after drift within the CPU's own rounding spread: on the
-    rows before it the GPU's cost and KKT residual deviate from the oracle's by at
-    most 10x what the oracle's other back-end (SIStructured: the same arithmetic in another
-    summation order) shows there.  These instances amplify rounding fast (at d = 12 the two CPU
-    back-ends, with identical branches, are 2e-5 apart in the cost and 60% in the residual by row
-    13), so an early flip -- the tCG residual target, RIPTRM.py:183, crossed on an erratic CG
-    plateau -- is expected once the trajectories have drifted that far."""
+@pytest.mark.timeout(600)
+def test_si_scaled_trajectory_matches_oracle():
+    """At d = 8, 12 and 16, four starts each (12 instances pooled into one rank test), two outer
+    iterations with at most 25 inner iterations each (inner_maxiter's reset
+    to the outer start point, RIPTRM.py:835-842, is part of the path), under the null-calibrated bar
+    (tests/parity.py check_null / null_summary; RIPTRM.py:631-705, 785-976): these trajectories
+    amplify rounding fast (at d = 12 two CPU back-ends with identical branches are 2e-5 apart in the
+    cost and 60% in the residual by row 13, and their first branch flip comes after 9-50 rows), so
+    the GPU is compared row by row only where the reference run is reproducible under summation
+    order -- before every order variant's first flip (parity.si_order_variants: the
+    reference-structured wiring and three coordinate / constraint-order permutations) and before
+    its own -- and over the whole window it must leave the reference run like one more such
+    variant: final x, y and the outer iterates' KKT residuals within 10x the farthest variant, its
+    first divergence row ranked among theirs as an exchangeable run would be."""
     import si
-    from parity import column_deviation, compare_logs, first_branch_flip, is_radius_tie
-    data, st = _inst(d, 2)
-    xs = np.stack([x for x, _ in st])
-    ys = np.stack([y for _, y in st])
+    from parity import assert_null, check_null, si_order_variants
     opt = {"maxiter": 2, "inner_maxiter": 25, "tolresid": 0.0, "maxtime": 1e9}
-    res = _batch(data, len(st)).solve(xs, ys, dict(opt, TRS_solver="tCG", second_order_stationarity=False,
-                                                       manviofun=si.si_manviofun))
-    for b in range(len(st)):
-        ref = SI.solve(data, xs[b], ys[b], dict(opt, manviofun=SI.si_manvio))
-        gl = res.log(b)
-        assert abs(gl["residual"][0] - ref.log["residual"][0]) <= 1e-12 * ref.log["residual"][0]
-        assert len(gl["iteration"]) > 5
-        flip = first_branch_flip(gl, ref.log)
-        nrow = 20 if flip is None else min(flip[0], 20)
-        early = flip is not None and flip[0] < 20 and not (flip[1] == "radius_update" and is_radius_tie(gl, ref.log, flip[0]))
-        try:
-            if nrow > 0:
-                compare_logs({k: v[:nrow] for k, v in gl.items()}, {k: v[:nrow] for k, v in ref.log.items()})
-            calibrated = True
-        except AssertionError:
-            calibrated = False
-        if early or not calibrated:
-            # the oracle's other back-end (the same arithmetic in another order) shows how far
-            # rounding alone moves this trajectory; on the rows before the GPU's flip (and before
-            # the back-ends' own first flip) the GPU's values stay within 10x that spread
-            ref2 = SI.solve(data, xs[b], ys[b], dict(opt, manviofun=SI.si_manvio), structured=True)
-            f2 = first_branch_flip(ref2.log, ref.log)
-            rows = min(nrow, f2[0] if f2 is not None else nrow)
-            pre = lambda lg: {k: v[:rows] for k, v in lg.items()}
-            for key in ("cost", "residual", "gradnorm", "normdx"):
-                dg = column_deviation(pre(gl), pre(ref.log), key)
-                dc = column_deviation(pre(ref2.log), pre(ref.log), key)
-                assert dg <= 10.0 * dc + 1e-12, (d, b, flip, f2, key, dg, dc)
+    rows, names = [], []
+    for d in DS:
+        data, st = _inst(d, 4)
+        xs = np.stack([x for x, _ in st])
+        ys = np.stack([y for _, y in st])
+        res = _batch(data, len(st)).solve(xs, ys, dict(opt, TRS_solver="tCG", second_order_stationarity=False,
+                                                           manviofun=si.si_manviofun))
+        gx, gy = res.x.cpu().numpy(), res.y.cpu().numpy()
+        for b in range(len(st)):
+            ref = SI.solve(data, xs[b], ys[b], dict(opt, manviofun=SI.si_manvio))
+            gl = res.log(b)
+            assert abs(gl["residual"][0] - ref.log["residual"][0]) <= 1e-12 * ref.log["residual"][0]
+            assert len(gl["iteration"]) > 5
+            vs = si_order_variants(data, xs[b], ys[b], dict(opt, manviofun=SI.si_manvio))
+            rows.append(check_null(gl, ref, vs, gx[b].reshape(3, d, d), gy[b][:data.m]))
+            names.append(f"d={d} start {b}")
+            print(f"[si null] d={d} start {b} done", flush=True)
+    assert_null(rows, names, _table("si_scaled"))
+
+
+def _table(name):
+    import os
+    return os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "gpurun_out", "parity", name + ".json")
 
 
 @pytest.mark.timeout(600)
@@ -251,7 +241,9 @@ def test_si_exact_cg_skip_is_bitwise_neutral(d, sos, bench_starts, monkeypatch):
     r0 = e0.solve(xs, ys, opt)
     assert e0.trs_skip_stats() == (0, 0)
     print(f"d={d} sos={sos}: {checked} subproblems decided on their eigenpairs, {skipped} CGs skipped")
-    assert checked > 0
+    # manifold.dim 100 (d = 8) runs the one-workgroup CG, where the skip is decided; 392 (d = 16)
+    # the grid-wide CG, which always runs
+    assert (checked > 0) == (d == 8), checked
     if bench_starts:
         assert skipped > 0
     for b in range(len(xs)):

@@ -449,3 +449,53 @@ def test_variant_decorrelation_classifier():
     assert variant_decorrelated(ref, [near, run(early)], (5, "inner_status"))
     assert not variant_decorrelated(ref, [near], (5, "inner_status"))
     assert not variant_decorrelated(ref, [near, run(late)], (5, "inner_status"))
+
+
+class _HessianError(O.NonnegPCAVectorized):
+    """Negative control for the null test: every S.v carries a fixed relative error of size `rel`
+    (elementwise factors 1 +- rel), a systematic defect a kernel could have while still passing an
+    operator-level 1e-8 check."""
+
+    def __init__(self, S, rel, seed):
+        super().__init__(S, S=S)
+        self.w = 1.0 + rel * np.random.RandomState(seed).choice([-1.0, 1.0], size=S.shape[0])
+
+    def Sv(self, v):
+        return super().Sv(v) * self.w
+
+
+def test_null_calibration_accepts_variants_and_rejects_hessian_error():
+    """parity.null_row / null_summary, the round-5 bar of the GPU trajectory tests, calibrated on the
+    CPU over the regime the bench window lives in (K = 20 outer iterations, mu down to 1.4e-8, where
+    every summation-order variant leaves the reference run's branches somewhere: n = 100, 12
+    instances, 6 variants each):
+    * null: each variant in the GPU's place against the other five (leave_one_out) passes -- the
+      bar's false-alarm level is what it claims;
+    * power: a run whose Hessian action carries a 1e-9 relative error (_HessianError) fails -- it
+      leaves the reference run earlier than the variants do (measured while choosing the bar: mean
+      percentile 0.08-0.13 at 1e-10 .. 1e-8 against a 0.28 limit; 1e-12 passes at 0.35, a rounding-
+      level error)."""
+    from parity import leave_one_out, null_row, null_summary, run_divergence
+    opt = dict(OPT, maxiter=20)
+    variants, bad = [], []
+    for s in range(12):
+        Z, x0, y0 = G.generate_instance(100, 7000 + s)
+        S = Z + Z.T
+        ref = O.RIPTRMOracle(opt).run(O.NonnegPCAVectorized(S, S=S), x0, y0)
+        runs = []
+        r = O.RIPTRMOracle(opt).run(O.NonnegPCAVectorized(S, S=S, symv=False), x0, y0)
+        runs.append(run_divergence(r.log, r.x, r.y, ref.log, ref.x, ref.y))
+        for sd in (1, 2, 6, 7, 3):
+            p = np.random.RandomState(sd).permutation(100)
+            inv = np.argsort(p)
+            Sp = np.ascontiguousarray(S[p][:, p])
+            r = O.RIPTRMOracle(opt).run(O.NonnegPCAVectorized(Sp, S=Sp), x0[p], y0[p])
+            runs.append(run_divergence(r.log, r.x[inv], r.y[inv], ref.log, ref.x, ref.y))
+        variants.append(runs)
+        r = O.RIPTRMOracle(opt).run(_HessianError(S, 1e-9, 7000 + s), x0, y0)
+        bad.append(null_row(run_divergence(r.log, r.x, r.y, ref.log, ref.x, ref.y), runs))
+    assert all(v["div_row"] < v["rows"] for runs in variants for v in runs)   # the flip regime
+    null = null_summary(leave_one_out(variants))
+    assert null["ok"], null
+    neg = null_summary(bad)
+    assert not neg["ok"] and neg["mean_u"] < neg["mean_u_min"], neg
