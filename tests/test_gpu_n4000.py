@@ -134,27 +134,6 @@ def _say(capsys):
     return say
 
 
-def _resume(make, K):
-    """parity.forced_outer_flip's hook: the device solve of one instance alone (bitwise the batch's,
-    test_n4000_b128_headline_pipeline_matches_oracle) paused at the head of outer iteration
-    k_head + 1 -> its x, y, mu and radius there.  make() -> (engine, x0, y0) for that instance."""
-    import engine
-    C = engine.C
-
-    def at(k_head):
-        one, xa, ya = make()
-        one.begin(xa, ya, _gpu_opt(maxiter=K))
-        one.run_until(k_head)
-        r = one.result()
-        st = one.stats()[0]
-        assert int(st[C["RIPTRM_STAT_OUTER_ITERS"]]) == k_head
-        out = (r.x[0].cpu().numpy()[:N], r.y[0].cpu().numpy()[:N], float(st[C["RIPTRM_STAT_MU"]]),
-               float(st[C["RIPTRM_STAT_TR_RADIUS"]]))
-        del one
-        return out
-    return at
-
-
 def _table(name):
     """Where a null test writes its per-instance table (merged back from the GPU box)."""
     import os
@@ -191,7 +170,7 @@ def test_n4000_solve_matches_oracle(capsys):
         items.append(dict(gl=res.log(b), S=Z + Z.T, x0=x0, y0=y0, gpu_x=xs[b][:N], gpu_y=ys[b][:N],
                           gpu_tcg=res.tcg_iters_per_row(b)[1:], name=f"host seed {4000 + b}"))
     assert max(res.tcg_iters_per_row(0)) >= 1000   # the expensive late iterations are in the window
-    results = check_instances_parallel(items, _oracle_opt(maxiter=K), progress=say, null=True)
+    results = check_instances_parallel(items, _oracle_opt(maxiter=K), progress=say, )
     names = [it["name"] for it in items]
     with capsys.disabled():
         assert_null([results[n] for n in names], names, _table("n4000_host"))
@@ -239,7 +218,7 @@ def test_n4000_b128_headline_pipeline_matches_oracle(capsys):
         S = big.unpack(k)
         items.append(dict(gl=res.log(k), S=S, x0=xs0[k][:N], y0=ys0[k][:N], gpu_x=xs[k][:N], gpu_y=ysr[k][:N],
                           gpu_tcg=res.tcg_iters_per_row(k)[1:], name=f"bench id {k}"))
-    results = check_instances_parallel(items, _oracle_opt(maxiter=K), progress=say, null=True)
+    results = check_instances_parallel(items, _oracle_opt(maxiter=K), progress=say, )
     names = [it["name"] for it in items]
     with capsys.disabled():
         assert_null([results[n] for n in names], names, _table("n4000_bench"))

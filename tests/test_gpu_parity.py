@@ -142,32 +142,34 @@ def test_fixture_reaches_published_residual_on_gpu(fixture_n50):
     assert res[conv][-1] < 2e-14
 
 
-def _check_instance(gl, Z, x0, y0, K, gpu_x=None, S=None, gpu_tcg=None, option=None):
+def _check_instance(gl, Z, x0, y0, K, gpu_x, gpu_y, S=None, gpu_tcg=None, option=None):
     from parity import check_instance
-    return check_instance(gl, Z, x0, y0, _oracle_opt(maxiter=K, **(option or {})), gpu_x=gpu_x, S=S, gpu_tcg=gpu_tcg)
+    return check_instance(gl, Z, x0, y0, _oracle_opt(maxiter=K, **(option or {})), gpu_x[:len(x0)], gpu_y[:len(x0)], S=S,
+                          gpu_tcg=gpu_tcg)
 
 
 def _budget(results, B):
-    from parity import check_budget
-    check_budget(results, B)
+    """The null-calibrated bar over a test's instances (tests/parity.py assert_null)."""
+    from parity import assert_null
+    names = sorted(results)
+    assert_null([results[b] for b in names], [f"instance {b}" for b in names])
 
 
 @pytest.mark.timeout(900)
 @pytest.mark.parametrize("n,B,K,layout", [(37, 5, 10, "sym"), (200, 4, 12, "sym"), (1000, 2, 10, "sym"),
                                           (300, 3, 10, "sym2"), (1000, 2, 10, "sym2")])
 def test_batched_solve_matches_oracle(n, B, K, layout):
-    """Per instance (_check_instance): identical branches and values within tests/parity.py's bar; a
-    flip only where classify_flip shows it is rounding-driven.  (Replaces round 1's "at most B/2
-    instances may flip" allowance.)"""
+    """Per instance (_check_instance): the envelope bar row by row where the reference run is
+    reproducible under summation order, and the null-calibrated bar over the whole window
+    (tests/parity.py check_null / assert_null)."""
     insts = [G.generate_instance(n, 100 + b) for b in range(B)]
     eng = _engine(np.stack([z for z, _, _ in insts]), layout=layout)
     res = eng.solve(np.stack([x for _, x, _ in insts]), np.stack([y for _, _, y in insts]), _gpu_opt(maxiter=K))
-    xs = res.x.cpu().numpy()
+    xs, ys = res.x.cpu().numpy(), res.y.cpu().numpy()
     results = {}
     for b, (Z, x0, y0) in enumerate(insts):
-        results[b] = _check_instance(res.log(b), Z, x0, y0, K, gpu_x=xs[b], gpu_tcg=res.tcg_iters_per_row(b)[1:])
-        if not (results[b] and results[b][0] == "flip"):
-            assert int(res.stat(b, "OUTER_ITERS")) == K
+        assert int(res.stat(b, "OUTER_ITERS")) == K
+        results[b] = _check_instance(res.log(b), Z, x0, y0, K, xs[b], ys[b], gpu_tcg=res.tcg_iters_per_row(b)[1:])
     _budget(results, B)
 
 
@@ -398,11 +400,10 @@ def test_shared_multistart_solve_matches_oracle(n, B, K):
         starts.append(x0 / np.linalg.norm(x0))
     eng = _shared_engine(Z, B)
     res = eng.solve(np.stack(starts), np.stack([y0] * B), _gpu_opt(maxiter=K))
-    xs = res.x.cpu().numpy()
+    xs, ys = res.x.cpu().numpy(), res.y.cpu().numpy()
     results = {}
     for b in range(B):
-        results[b] = _check_instance(res.log(b), Z, starts[b], y0, K, gpu_x=xs[b],
-                                     gpu_tcg=res.tcg_iters_per_row(b)[1:])
+        results[b] = _check_instance(res.log(b), Z, starts[b], y0, K, xs[b], ys[b], gpu_tcg=res.tcg_iters_per_row(b)[1:])
     _budget(results, B)
 
 

@@ -230,28 +230,6 @@ def test_euclidean_branch_options_agree(lincomb, embedded):
     assert np.linalg.norm(P.gradlag(x, y) - Q.gradlag(x, y)) <= 1e-12 * np.linalg.norm(Q.gradlag(x, y))
 
 
-def test_flip_classifier_accepts_rounding_ties_and_rejects_real_differences():
-    """parity.classify_flip (used by the GPU batch tests instead of round 1's 'B/2 may flip'):
-    on an instance where the two CPU oracles' inner branches differ (seed 125, n = 37), the flip is
-    reachable from the reference oracle's own state perturbed by the drift accumulated before it;
-    a fabricated decision at an early, well-separated row is not."""
-    import copy
-    from parity import StateRecorder, classify_flip, first_branch_flip
-    Z, x0, y0 = G.generate_instance(37, 125)
-    P = O.NonnegPCAVectorized(Z)
-    oa = O.RIPTRMOracle(dict(OPT, maxiter=10))
-    rec = StateRecorder(oa)
-    ra = oa.run(P, x0, y0)
-    b = O.solve(Z, x0, y0, dict(OPT, maxiter=10), structured=True)
-    flip = first_branch_flip(b.log, ra.log)
-    assert flip is not None
-    assert classify_flip(rec.step, P, rec.states, b.log, ra.log, flip) is not None
-    fake = copy.deepcopy(ra.log)
-    row = next(r for r in range(1, len(fake["inner_status"])) if fake["inner_status"][r] == "successful")
-    fake["inner_status"][row] = "unsuccessful"
-    assert classify_flip(rec.step, P, rec.states, fake, ra.log, (row, "inner_status")) is None
-
-
 def test_envelope_calibration():
     """parity.compare_logs(envelope=...) as the GPU solve tests use it, with CPU stand-ins for the
     GPU: further order variants (dsymv on other permutations) and the reference-structured oracle
@@ -291,164 +269,28 @@ def test_envelope_calibration():
     assert len(exc) <= excursion_budget(compared), exc
 
 
-def test_flip_classifier_rejects_late_decision_with_margin():
-    """the classifier's perturbation is the OUTER-iterate drift before the flip, capped at
-    1e-8 relative, so a late row cannot borrow O(1) trial-row drift.  Fabricated decisions at the
-    last outer iteration whose real margins are large must not be reproduced: 'unsuccessful' on a
-    step with ared/pred > 0.5 (the test is ared > rho pred, rho = 0.1, RIPTRM.py:676), and
-    'expanded' on a step far inside the radius (needs |normdx - Delta| <= 1e-15, :672)."""
-    import copy
-    from parity import DRIFT_CAP, StateRecorder, classify_flip, prefix_deviation
-    Z, x0, y0 = G.generate_instance(37, 100)
-    P = O.NonnegPCAVectorized(Z)
-    oa = O.RIPTRMOracle(dict(OPT, maxiter=10))
-    rec = StateRecorder(oa)
-    ra = oa.run(P, x0, y0)
-    b = O.solve(Z, x0, y0, dict(OPT, maxiter=10), structured=True)
-    rows = len(ra.log["iteration"])
-    assert prefix_deviation(b.log, ra.log, rows) <= DRIFT_CAP
-    last = max(ra.log["iteration"])
-    late = [r for r in range(rows) if ra.log["iteration"][r] == last and ra.log["inner_status"][r] == "successful"
-            and ra.log["ared/pred"][r] > 0.5 and ra.log["normdx"][r] < 0.5 * ra.log["TR_radius"][r]]
-    assert late, "no late row with a clear decision"
-    row = late[-1]
-    for key, value in (("inner_status", "unsuccessful"), ("radius_update", "expanded")):
-        fake = copy.deepcopy(ra.log)
-        fake[key][row] = value
-        assert classify_flip(rec.step, P, rec.states, fake, ra.log, (row, key)) is None, key
-
-
 def test_parallel_checker_matches_sequential():
     """parity.check_instances_parallel (the n = 4000 GPU tests' pool of single-threaded oracle
     processes) reaches the same verdict as parity.check_instance: here the 'GPU' log is the
     reference-structured oracle's, one instance that agrees and one whose branches flip (seed 125,
     test_outer_comparator_on_branch_flips)."""
-    from parity import check_instance, check_instances_parallel
+    from parity import check_instance, check_instances_parallel, null_summary
     opt = dict(OPT, maxiter=10)
     items = []
     for n, seed in ((37, 100), (37, 125)):
         Z, x0, y0 = G.generate_instance(n, seed)
         a = O.solve(Z, x0, y0, opt, structured=True)
-        items.append(dict(gl=a.log, S=Z + Z.T, x0=x0, y0=y0, gpu_x=a.x, name=seed, Z=Z))
+        items.append(dict(gl=a.log, S=Z + Z.T, x0=x0, y0=y0, gpu_x=a.x, gpu_y=a.y, name=seed, Z=Z))
     msgs = []
     par = check_instances_parallel(items, opt, workers=2, progress=msgs.append)
     assert len(msgs) >= 2
     for it in items:
-        seq = check_instance(it["gl"], it["Z"], it["x0"], it["y0"], opt, gpu_x=it["gpu_x"])
-        assert (seq is None) == (par[it["name"]] is None)
-        if seq is not None:
-            assert seq[0] == par[it["name"]][0]
-            if seq[0] == "flip":
-                assert seq[1][:2] == par[it["name"]][1][:2]
-    assert par[125] is not None and par[125][0] == "flip"
-
-
-def test_variant_support_for_flips():
-    """parity.variant_supports_flip: a GPU flip at row r counts as rounding-driven when an order
-    variant of the oracle takes the same decision at r, or already leaves the reference's branches
-    at a row <= r; a variant that agrees with the reference everywhere supports nothing."""
-    from parity import variant_supports_flip
-    keys = ("iteration", "num_inner", "inner_status", "dxtype", "radius_update", "dual_clipping")
-
-    def log(status):
-        return {k: (list(status) if k == "inner_status" else [0] * len(status)) for k in keys}
-
-    ref = log(["successful"] * 6)
-    gpu = log(["successful"] * 4 + ["unsuccessful", "successful"])
-    V = type("V", (), {})
-    same = V(); same.log = log(["successful"] * 6)
-    assert not variant_supports_flip([same], gpu, ref, (4, "inner_status"))
-    at = V(); at.log = log(["successful"] * 4 + ["unsuccessful", "successful"])
-    assert variant_supports_flip([same, at], gpu, ref, (4, "inner_status"))
-    other = V(); other.log = log(["successful"] * 4 + ["converged", "successful"])
-    assert not variant_supports_flip([other], gpu, ref, (4, "inner_status"))
-    earlier = V(); earlier.log = log(["successful"] * 2 + ["unsuccessful"] + ["successful"] * 3)
-    assert variant_supports_flip([earlier], gpu, ref, (4, "inner_status"))
-    later = V(); later.log = log(["successful"] * 5 + ["unsuccessful"])
-    assert not variant_supports_flip([later], gpu, ref, (4, "inner_status"))
-
-
-def test_decision_margins_reproduce_the_logged_ratio():
-    """parity.decision_margins re-runs one inner step of the oracle from its recorded state and
-    returns ared / pred (their ratio is the logged 'ared/pred' bit for bit) with the forward error
-    of both; a decision with a margin far above that error is not a tie."""
-    from parity import StateRecorder, decision_margins, decision_tie
-    Z, x0, y0 = G.generate_instance(37, 100)
-    P = O.NonnegPCAVectorized(Z)
-    oa = O.RIPTRMOracle(dict(OPT, maxiter=6))
-    rec = StateRecorder(oa)
-    r = oa.run(P, x0, y0)
-    rows = [i for i, s in enumerate(r.log["inner_status"]) if s in ("successful", "unsuccessful")]
-    assert rows
-    for row in rows[:4]:
-        m = decision_margins(rec.step, P, rec.states[row - 1])
-        assert m["ared"] / m["pred"] == r.log["ared/pred"][row]
-        assert 0 < m["err_ared"] < 1e-10 and 0 <= m["err_pred"] < 1e-10
-    # a well-separated decision is not a tie (the flipped log claims the other outcome)
-    row = rows[0]
-    m = decision_margins(rec.step, P, rec.states[row - 1])
-    if abs(m["ared"] - 0.1 * m["pred"]) > 10 * (m["err_ared"] + 0.1 * m["err_pred"]):
-        fake = {k: list(v) for k, v in r.log.items()}
-        fake["inner_status"][row] = "unsuccessful" if r.log["inner_status"][row] == "successful" else "successful"
-        assert decision_tie(rec.step, P, rec.states, fake, r.log, (row, "inner_status")) is None
-
-
-def test_forced_outer_flip_reproduces_own_state_and_rejects_margins():
-    """parity.forced_outer_flip: the 'GPU' log is the reference-structured oracle's, resumed at the
-    head of its outer iteration k from its OWN state (x, y, mu, Delta recorded at the inner_run
-    call).  From that state the vectorised oracle takes the same branches through any row of
-    iteration k (a flip there is accepted as the GPU's own decision); a fabricated decision with a
-    real margin ('unsuccessful' on a step with ared/pred > 0.5) is not."""
-    import copy
-    from parity import forced_outer_flip
-    Z, x0, y0 = G.generate_instance(37, 100)
-    opt = dict(OPT, maxiter=8)
-    heads = {}
-    oa = O.RIPTRMOracle(opt)
-    inner = oa.inner_run
-
-    def rec(P_, it, start, x, y, mu, Delta, iopt):
-        heads[it - 1] = (x.copy(), y.copy(), mu, Delta)
-        return inner(P_, it, start, x, y, mu, Delta, iopt)
-
-    oa.inner_run = rec
-    a = oa.run(O.NonnegPCAStructured(Z), x0, y0)
-    P = O.NonnegPCAVectorized(Z)
-    k = 6
-    rows_k = [i for i, it in enumerate(a.log["iteration"]) if it == k and i > 0]
-    assert len(rows_k) >= 2
-    got = forced_outer_flip(a.log, (rows_k[-1], "inner_status"), P, opt, lambda kk: heads[kk])
-    assert got is not None and got[0] == k and got[2] == 0.0, got
-    clear = [r for r in rows_k if a.log["inner_status"][r] == "successful" and a.log["ared/pred"][r] > 0.5]
-    assert clear
-    fake = copy.deepcopy(a.log)
-    fake["inner_status"][clear[0]] = "unsuccessful"
-    assert forced_outer_flip(fake, (clear[0], "inner_status"), P, opt, lambda kk: heads[kk]) is None
-
-
-def test_variant_decorrelation_classifier():
-    """parity.variant_decorrelated: an order variant that keeps the reference's branches but carries
-    a radius 1% away before the flip row marks the reference's later branches as no target; a
-    variant within rounding (1e-14) does not, nor does a deviation only after the flip row."""
-    from parity import BRANCH_KEYS, variant_decorrelated
-    rows = 8
-
-    def run(tr):
-        log = {k: [0] * rows for k in BRANCH_KEYS}
-        log["TR_radius"] = list(tr)
-        log["cost"] = [1.0] * rows
-        obj = type("R", (), {})()
-        obj.log, obj.trace = log, [{"tcg_iters": 1}] * (rows - 1)
-        return obj
-
-    base = np.full(rows, 0.25)
-    ref = run(base)
-    near = run(base * (1 + 1e-14))
-    early = base.copy(); early[3] *= 1.01
-    late = base.copy(); late[6] *= 1.01
-    assert variant_decorrelated(ref, [near, run(early)], (5, "inner_status"))
-    assert not variant_decorrelated(ref, [near], (5, "inner_status"))
-    assert not variant_decorrelated(ref, [near, run(late)], (5, "inner_status"))
+        seq = check_instance(it["gl"], it["Z"], it["x0"], it["y0"], opt, it["gpu_x"], it["gpu_y"])
+        for key in ("div_row", "dx", "dy", "outer_dev"):
+            assert seq["gpu"][key] == par[it["name"]]["gpu"][key], key
+            assert seq["u_" + key] == par[it["name"]]["u_" + key], key
+    assert par[125]["gpu"]["flip"] is not None and par[100]["gpu"]["flip"] is None
+    assert null_summary([par[100], par[125]])["ok"]
 
 
 class _HessianError(O.NonnegPCAVectorized):
@@ -473,7 +315,7 @@ def test_null_calibration_accepts_variants_and_rejects_hessian_error():
       bar's false-alarm level is what it claims;
     * power: a run whose Hessian action carries a 1e-9 relative error (_HessianError) fails -- it
       leaves the reference run earlier than the variants do (measured while choosing the bar: mean
-      percentile 0.08-0.13 at 1e-10 .. 1e-8 against a 0.28 limit; 1e-12 passes at 0.35, a rounding-
+      percentile 0.08-0.13 at 1e-10 .. 1e-8 against a 0.23 limit; 1e-12 passes at 0.35, a rounding-
       level error)."""
     from parity import leave_one_out, null_row, null_summary, run_divergence
     opt = dict(OPT, maxiter=20)
