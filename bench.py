@@ -374,6 +374,8 @@ def main():
                     help="k_persist for small batches: 1 = cooperative launch (default), 2 = plain launch (A/B), 0 = off")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r4_traffic_spass_sup.json"),
                     help="per instance-pass HBM bytes of the S-pass from a committed rocprofv3 PMC summary (scripts/gate.sh pmc_spass)")
+    ap.add_argument("--si-pmc-json", default=os.path.join(ROOT, "profiles", "r5_si_pmc.json"),
+                    help="k_si issue-rate PMC summary (scripts/si_pmc_summary.py) for --problem si's roofline")
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend (nccl = RCCL)")
     ap.add_argument("--dump", default="",
                     help="rank 0 writes the gathered x, y and stats of every global instance to this .npz")
@@ -870,6 +872,34 @@ def si_cpu_pool(K: int, budget_s: float, procs: int, trs: str, d: int = 5):
                        f"rate x {procs}, evaluation time excluded as RIPTRM.py:932-941")}
 
 
+def si_roofline(args, d, hvps, kern_s, sec, passes):
+    """The SI line's roof.  k_si runs each instance's whole solve on one wave: a dependent chain of
+    d x d products, LDS round trips and wave reductions, no HBM stream and no matrix-core work worth
+    pricing, so its bound is the issue rate of one wave (one instruction per cycle).  achieved =
+    SQ_ACTIVE_INST_ANY / SQ_WAVE_CYCLES from a committed rocprofv3 PMC pass of this d
+    (scripts/si_pmc_summary.py -> --si-pmc-json), the fraction of each wave's lifetime in which it
+    issues; peak 1.  The latency floor per instance-step is stated beside it: device time per HVP per
+    instance, from the instrumented launch's section clocks."""
+    issue = None
+    if os.path.exists(args.si_pmc_json):
+        try:
+            pm = json.load(open(args.si_pmc_json))
+            if pm.get("d") == d and pm.get("issue_frac") is not None:
+                issue = pm
+        except Exception as e:  # pragma: no cover
+            log(f"si pmc json unreadable: {e}")
+    us_hvp = sec["hvp"] / max(1.0, passes) * 1e6
+    return {"bound": "issue", "achieved": issue["issue_frac"] if issue else None, "peak": 1.0,
+            "unit": "instructions issued per wave-cycle (one wave per instance)",
+            "frac": issue["issue_frac"] if issue else None, "traffic": None,
+            "pmc": ({k: issue[k] for k in ("wait_frac", "wait_inst_frac", "valu_insts_per_wave_cycle", "source")}
+                    if issue else None),
+            "latency_floor_us_per_hvp_per_instance": us_hvp,
+            "hvps_per_s_M": hvps / kern_s / 1e6,
+            "kernel": "k_si (one 64-lane workgroup per instance, whole solve per launch)", "kernel_ms": kern_s * 1e3,
+            "why": "latency-bound single-wave chains; HBM traffic is the problem data only (no roof applies)"}
+
+
 def bench_si(args, world, rank, dev, dist):
     """StableIdentification throughput: one HIP launch runs every instance's whole solve
     (maxiter = warmup + steps); the timed launch is bracketed by barriers + syncs."""
@@ -950,10 +980,7 @@ def bench_si(args, world, rank, dev, dist):
                                + ("" if args.trs == "tCG" else ", TRS_solver=Exact_RepMat + second-order test"),
                    "trs_solver": args.trs,
                    "global_batch": B * world, "parallelism": f"instance-sharded x{world}", "world_size": world},
-        "roofline": {"bound": "latency", "achieved": hvps / kern_s / 1e6, "peak": None, "unit": "M HVP/s",
-                     "frac": None, "traffic": None,
-                     "kernel": "k_si (one 64-lane workgroup per instance, whole solve per launch)",
-                     "kernel_ms": kern_s * 1e3},
+        "roofline": si_roofline(args, d, hvps, kern_s, sec, tot("PASSES")),
         "cpu_baseline": cpu,
         "detail": {"inner_iterations_per_s": inner / T, "tcg_iterations_per_s": tcg / T, "hvps_per_s": hvps / T,
                    "section_fraction": secfrac, "us_per_hvp_per_instance": sec["hvp"] / max(1.0, tot("PASSES")) * 1e6},

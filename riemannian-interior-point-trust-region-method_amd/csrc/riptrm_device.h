@@ -217,6 +217,7 @@ struct DevParams {
   int32_t tab_len;
   int32_t outer_target;
   double clock_hz;
+  int32_t trs_hbm;      // 1: Exact_RepMat's subproblems on the HBM path at every n (RIPTRM_TRS_HBM=1; A/B)
   riptrm_options opt;
 };
 

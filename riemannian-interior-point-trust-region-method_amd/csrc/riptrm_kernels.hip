@@ -1484,7 +1484,7 @@ struct MachineT {
 
   // Exact_RepMat beyond the LDS solver's size: the host serves the subproblem and the trial-point
   // eigenvalue from HBM (riptrm_trs_big.hip)
-  __device__ __forceinline__ bool trs_big() const { return n - 1 > riptrm_trs::DIM_MAX; }
+  __device__ __forceinline__ bool trs_big() const { return n - 1 > riptrm_trs::DIM_MAX || P.trs_hbm; }
 
   // Error stop (include/riptrm.h RIPTRM_ERR_NONFINITE / RIPTRM_ERR_EIGEN; RIPTRM.py:961-966):
   // stop the instance; inside an outer step (restore) hand back the iterate that step started
@@ -3715,6 +3715,10 @@ int riptrm_tcg(riptrm_ctx* ctx, const double* x, const double* y, int64_t ldv, c
   return RIPTRM_OK;
 }
 
+// the subproblems of Exact_RepMat go to the HBM service (riptrm_trs_big.hip): above the LDS solver's
+// size, or everywhere with RIPTRM_TRS_HBM=1 (read at riptrm_solve_begin)
+static bool big_trs_path(const riptrm_ctx* c) { return c->P.n - 1 > RIPTRM_TRS_DIM_MAX || c->P.trs_hbm; }
+
 int riptrm_solve_begin(riptrm_ctx* ctx, const riptrm_options* opt, const double* x0, const double* y0, int64_t ldv,
                        const double* mu_table, const double* tolL_table, const double* tolC_table, int32_t table_len) {
   if (!ctx) return RIPTRM_E_ARG;
@@ -3725,7 +3729,11 @@ int riptrm_solve_begin(riptrm_ctx* ctx, const riptrm_options* opt, const double*
     return fail(ctx, RIPTRM_E_ARG, "solve_begin: unknown trs_solver");
   if (opt->trs_solver == RIPTRM_TRS_SOLVER_EXACT_REPMAT && ctx->P.n < 2)
     return fail(ctx, RIPTRM_E_ARG, "solve_begin: Exact_RepMat needs n >= 2");
-  if (opt->trs_solver == RIPTRM_TRS_SOLVER_EXACT_REPMAT && ctx->P.n - 1 > RIPTRM_TRS_DIM_MAX &&
+  {   // A/B: the HBM subproblem path below its size limit too (comparisons with the LDS solver)
+    const char* e = getenv("RIPTRM_TRS_HBM");
+    ctx->P.trs_hbm = (e && e[0] == '1') ? 1 : 0;
+  }
+  if (opt->trs_solver == RIPTRM_TRS_SOLVER_EXACT_REPMAT && big_trs_path(ctx) &&
       (!ctx->big_ws || ctx->big_order < ctx->P.n || ctx->big_slots < 1))
     return fail(ctx, RIPTRM_E_STATE, "solve_begin: Exact_RepMat above RIPTRM_TRS_DIM_MAX + 1 needs "
                                      "riptrm_trs_bind_workspace(order >= n) first");
@@ -3858,7 +3866,7 @@ int riptrm_solve_advance(riptrm_ctx* ctx, int32_t steps, int32_t outer_target, i
   }
   int act = 0;
   if (int rc = run_steps(ctx, steps, &act)) return rc;
-  if (ctx->P.opt.trs_solver == RIPTRM_TRS_SOLVER_EXACT_REPMAT && ctx->P.n - 1 > RIPTRM_TRS_DIM_MAX) {
+  if (ctx->P.opt.trs_solver == RIPTRM_TRS_SOLVER_EXACT_REPMAT && big_trs_path(ctx)) {
     // instances parked for a host-served subproblem / trial eigenvalue (riptrm_trs_big.hip): serve
     // them and let them run on from PH_TRS_END / PH_MINEIG_END with the next chunk
     int served = 0;

@@ -217,6 +217,13 @@ EXACT_BIG_CHUNK = 4        # lock-step iterations per advance on the HBM Exact_R
 TRS_WS_BUDGET = 16 << 30   # bytes of HBM the Exact_RepMat scratch may take (RIPTRM_TRS_WS_GB overrides)
 
 
+def trs_hbm_path(n: int) -> bool:
+    """Exact_RepMat's subproblems go to the HBM service: above the LDS solver's size (manifold.dim =
+    n - 1 > RIPTRM_TRS_DIM_MAX), or at every n with RIPTRM_TRS_HBM=1 (A/B; riptrm_solve_begin reads it)."""
+    import os
+    return n - 1 > C["RIPTRM_TRS_DIM_MAX"] or os.environ.get("RIPTRM_TRS_HBM", "") == "1"
+
+
 def bind_trs_scratch(ctx, lib, device, have, order: int, slots: int):
     """Bind the HBM scratch of Exact_RepMat above RIPTRM_TRS_DIM_MAX (riptrm_trs_bind_workspace) for
     `slots` matrices of order `order`.  `have` is the (buffer, order, slots) this caller bound before
@@ -546,7 +553,7 @@ class NonnegPCABatch:
     def begin(self, x0, y0, option: Dict[str, Any], restart_every: int = 0) -> ResolvedOptions:
         assert self.bound
         ro = resolve_options(option, math.pi, self.cap, restart_every)
-        if ro.exact and self.n - 1 > C["RIPTRM_TRS_DIM_MAX"]:
+        if ro.exact and trs_hbm_path(self.n):
             # Exact_RepMat beyond the LDS solver: the frame matrices (n x n) live in HBM scratch, one
             # slot per instance served in the same pass (riptrm_trs_bind_workspace;
             # csrc/riptrm_trs_big.hip), as many as trs_workspace_slots allows
@@ -601,7 +608,7 @@ class NonnegPCABatch:
         most one record per instance on the tCG path) and the device log is drained once half full."""
         chunk, t0 = 4, time.time()
         cap = min(self.cap, int(self.ro.c_opt.log_capacity))
-        if self.ro.exact and self.n - 1 > C["RIPTRM_TRS_DIM_MAX"]:
+        if self.ro.exact and trs_hbm_path(self.n):
             # the HBM Exact_RepMat path parks every instance a few lock-step iterations after each
             # service (subproblem -> trial point -> trial eigenvalue): short chunks, so the parked
             # instances are served as soon as they all wait

@@ -515,6 +515,31 @@ def test_exact_repmat_above_lds_size_matches_oracle(sos):
 
 
 @pytest.mark.timeout(600)
+def test_exact_repmat_lds_and_hbm_paths_agree_near_97(monkeypatch):
+    """the two Exact_RepMat paths at the size where they meet.  n = 97 (manifold.dim 96,
+    the LDS solver's limit: Householder frame matrix, parallel Jacobi in LDS) solved again with
+    RIPTRM_TRS_HBM=1 (the HBM service: densified frame matrix, coef = -x^T (M x) + y^T x in
+    k_repmat_vec, rocSOLVER dsyevd, the eigenpair cache) -- the same reference step (RIPTRM.py:433-444,
+    599-617, TRSgep :218-299) in two arithmetics, so their trajectories must agree with the bar the
+    solo Exact test uses against the oracle (parity.compare_until_flip), and both against the oracle."""
+    from parity import compare_until_flip
+    Z, x0, y0 = G.generate_instance(97, 78)
+    opt = dict(TRS_solver="Exact_RepMat", second_order_stationarity=True, maxiter=4)
+    monkeypatch.delenv("RIPTRM_TRS_HBM", raising=False)
+    lds = _engine(Z).solve(x0[None], y0[None], _gpu_opt(**opt))
+    monkeypatch.setenv("RIPTRM_TRS_HBM", "1")
+    e = _engine(Z)
+    hbm = e.solve(x0[None], y0[None], _gpu_opt(**opt))
+    assert e.trs_cache_stats()[1] > 0   # the HBM service really served the subproblems
+    ref = O.solve(Z, x0, y0, _oracle_opt(**opt))
+    for gl in (lds.log(0), hbm.log(0)):
+        kinds = [k for k in gl["dxtype"] if k is not None]
+        assert kinds and all(k in ("boundary", "interior", "hardcase_1") for k in kinds), kinds
+        compare_until_flip(gl, ref.log)
+    compare_until_flip(hbm.log(0), lds.log(0))
+
+
+@pytest.mark.timeout(600)
 def test_exact_repmat_above_lds_size_batched(monkeypatch):
     """The HBM Exact_RepMat service over a batch (csrc/riptrm_trs_big.hip: every parked instance in
     one pass, one workspace slot each, batched dsyevd): six n = 200 instances with the second-order
