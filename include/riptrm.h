@@ -437,6 +437,17 @@ int riptrm_trs_cache_stats(riptrm_ctx* ctx, int64_t* hits, int64_t* subproblems)
  * CG would have given (RIPTRM_CG_SKIP=0 in the environment: always run it).  Since the context was
  * created; either pointer may be NULL. */
 int riptrm_trs_skip_stats(riptrm_ctx* ctx, int64_t* checked, int64_t* skipped);
+/* Batched symmetric eigendecomposition, hand-written for gfx950 (csrc/riptrm_eig.h): the spectrum
+ * TRSgep (RIPTRM.py:218-299) and the second-order test (RIPTRM.py:599-617; scipy.linalg.eigh there)
+ * take of the Exact_RepMat matrix; the HBM service uses it for manifold.dim 97..199.  One workgroup
+ * per matrix, the matrix resident in LDS: Householder tridiagonalisation, bisection, twisted
+ * factorisations, back-transformation.  batch matrices of order dim (1 <= dim <= 199) at
+ * A + k a_stride (leading dimension lda; the lower triangle is read): eigenvalues ascending into
+ * w + k w_stride and, with vectors != 0, eigenvector j into row j of the matrix (overwritten).
+ * info[k] = 0, or 1 for a non-finite input (its eigenvalues are NaN).  Asynchronous on the
+ * context's stream; the context keeps a small scratch (3 dim doubles per matrix). */
+int riptrm_sym_eig(riptrm_ctx* ctx, int32_t dim, int32_t batch, double* A, int64_t lda, int64_t a_stride, double* w,
+                   int64_t w_stride, int32_t* info, int32_t vectors);
 
 /* ==== Stiefel(n, p) manifold operations =========================================
  * Not in the reference (north_star / BASELINE configs[4] ask for them): pymanopt 2.x formulas,

@@ -76,6 +76,8 @@ struct riptrm_ctx {
   int big_cache_order = 0, big_cache_batch = 0;
   int64_t big_cache_hits = 0, big_subproblems = 0;   // since the solve began (riptrm_trs_cache_stats)
   int64_t big_cg_checked = 0, big_cg_skipped = 0;    // since the context was created (riptrm_trs_skip_stats)
+  void* eig_scratch = nullptr;   // riptrm_sym_eig's d / e / tau vectors (context-owned)
+  size_t eig_scratch_bytes = 0;
 };
 
 // riptrm_trs_big.hip

@@ -1,0 +1,315 @@
+// riptrm_eig.h — batched symmetric eigensolver for the HBM Exact_RepMat service, one workgroup per
+// matrix, the matrix resident in LDS (orders up to EIG_LDS_MAX; csrc/riptrm_trs_big.hip eig_batched).
+//
+// Reference: TRSgep (src/solver/RIPTRM.py:218-299) needs the spectrum of the subproblem's matrix
+// (the rightmost eigenpair of its 2n x 2n pencil; the build takes A = Q diag(lam) Q^T and solves the
+// secular equation in that basis, riptrm_trs_big.hip k_secular), and the second-order test
+// (RIPTRM.py:599-617) its smallest eigenvalue.  Rounds 3-4 called rocSOLVER dsyevd_strided_batched
+// for orders above 96: ~78% of the n = 200 Exact line's GPU time (sytd2 + divide and conquer on
+// 199 x 199 matrices, latency-bound).  This is the hand-written replacement:
+//   1. Householder tridiagonalisation (LAPACK dsytd2, lower) with the lower triangle PACKED in LDS
+//      (m (m + 1) / 2 doubles: 159 KB at m = 199), the reflectors stored in place of the columns
+//      they annihilate; per column one wave forms the reflector, the workgroup runs the symmetric
+//      mat-vec (wave per row, both halves of the packed triangle) and the rank-two update;
+//   2. eigenvalues of the tridiagonal T by bisection on Sturm counts, one thread per eigenvalue
+//      (absolute accuracy eps ||T||, the tridiagonalisation's own error);
+//   3. eigenvectors of T by twisted factorisations (the LDL^T and UDU^T of T - lam I meet at the
+//      index of the smallest |gamma|), one thread per eigenvector, in its output row;
+//   4. back-transformation q = H_0 ... H_{m-2} z with the reflectors from LDS, a wave per group of
+//      four vectors (each vector spread over the wave's lanes, wave reductions for the dots).
+// Output as rocSOLVER's: eigenvalues ascending, eigenvector k in row k of the row-major view of the
+// input (column k of the column-major matrix), info = 0 (non-finite input: info = 1).  Fixed
+// reduction orders: a matrix's results do not depend on the batch it is in.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <float.h>
+#include <math.h>
+#include "riptrm_wave.h"
+
+namespace riptrm_eig {
+
+#pragma clang fp contract(off)
+
+constexpr int EW = 512;                    // threads per matrix
+constexpr int EIG_LDS_MAX = 199;           // packed lower triangle + two vectors fit 160 KiB
+constexpr int EIG_MAX_M = 256;             // four elements per lane in the back-transformation
+
+__host__ __device__ constexpr int poff(int i) { return i * (i + 1) / 2; }
+__host__ __device__ constexpr int vpad_eig(int m) { return (m + 7) / 8 * 8; }
+__host__ __device__ constexpr size_t eig_lds_bytes(int m) {
+  return ((size_t)poff(m) + 2 * (size_t)vpad_eig(m)) * sizeof(double);
+}
+
+typedef __attribute__((address_space(3))) double lds_t;
+
+// the number of eigenvalues of T (diagonal d, off-diagonal e) below x (Sturm count, LAPACK dlaneg's
+// recurrence with pivmin guarding zero pivots)
+__device__ __forceinline__ int sturm_count(const lds_t* d, const lds_t* e, int m, double x, double pivmin) {
+  double q = d[0] - x;
+  if (fabs(q) < pivmin) q = -pivmin;
+  int c = q < 0.0;
+  for (int j = 1; j < m; ++j) {
+    const double ej = e[j - 1];
+    q = (d[j] - x) - (ej * ej) / q;
+    if (fabs(q) < pivmin) q = -pivmin;
+    c += q < 0.0;
+  }
+  return c;
+}
+
+// Matrix k = blockIdx.x: the m x m symmetric matrix at A0 + k a_stride (leading dimension lda; the
+// lower triangle is read) -> eigenvalues ascending at ev0 + k ev_stride, eigenvectors (vectors != 0)
+// in the rows of the same matrix.  Scratch per matrix (three vectors of >= m doubles, k sc_stride
+// apart): d at d0, e at e0, tau at t0.
+__global__ void __launch_bounds__(EW) k_eig_lds(double* A0, int64_t a_stride, int lda, int m, double* ev0,
+                                                int64_t ev_stride, double* d0, double* e0, double* t0,
+                                                int64_t sc_stride, int32_t* infos, int vectors) {
+  extern __shared__ double smem[];
+  __shared__ double scal[2];
+  __shared__ int bad;
+  lds_t* P = (lds_t*)smem;                    // packed lower triangle, row i at poff(i)
+  lds_t* vb = P + poff(m);                    // the reflector (phase 1), then d (phases 2-3)
+  lds_t* pb = vb + vpad_eig(m);               // p (phase 1), then e (phases 2-3), then tau (phase 4)
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  constexpr int NW = EW / 64;
+  const int k = blockIdx.x;
+  double* A = A0 + (int64_t)k * a_stride;
+  double* ev = ev0 + (int64_t)k * ev_stride;
+  double* dg = d0 + (int64_t)k * sc_stride;
+  double* eg = e0 + (int64_t)k * sc_stride;
+  double* tg = t0 + (int64_t)k * sc_stride;
+  if (tid == 0) bad = 0;
+  __syncthreads();
+  for (int64_t q = tid; q < (int64_t)m * m; q += EW) {
+    const int i = (int)(q / m), j = (int)(q - (int64_t)i * m);
+    if (j <= i) {
+      const double a = A[(int64_t)i * lda + j];
+      if (!isfinite(a)) bad = 1;
+      P[poff(i) + j] = a;
+    }
+  }
+  __syncthreads();
+  if (bad) {
+    if (tid == 0) infos[k] = 1;
+    for (int i = tid; i < m; i += EW) ev[i] = NAN;
+    return;
+  }
+  if (tid == 0) infos[k] = 0;
+
+  // ---- 1. tridiagonalisation (dsytd2, lower) ----------------------------------------------------
+  for (int i = 0; i < m - 1; ++i) {
+    const int r = m - i - 1;   // the trailing rows / columns i + 1 .. m - 1
+    if (w == 0) {
+      double s = 0.0;
+      for (int j = i + 2 + lane; j < m; j += 64) {
+        const double x = P[poff(j) + i];
+        s += x * x;
+      }
+      s = riptrm_wave::wave_sum(s);
+      const double alpha = P[poff(i + 1) + i];
+      double tau = 0.0, beta = alpha, scl = 0.0;
+      if (s != 0.0) {   // dlarfg: H (alpha, x) = (beta, 0), H = I - tau v v^T, v(0) = 1
+        beta = -copysign(sqrt(alpha * alpha + s), alpha);
+        tau = (beta - alpha) / beta;
+        scl = 1.0 / (alpha - beta);
+      }
+      for (int l = lane; l < r; l += 64) {
+        double v = 1.0;
+        if (l > 0) {
+          v = P[poff(i + 1 + l) + i] * scl;
+          P[poff(i + 1 + l) + i] = v;   // the reflector replaces the column it annihilates
+        }
+        vb[l] = v;
+      }
+      if (lane == 0) {
+        scal[0] = tau;
+        P[poff(i + 1) + i] = beta;
+        eg[i] = beta;
+        tg[i] = tau;
+      }
+    }
+    __syncthreads();
+    const double tau = scal[0];
+    if (tau != 0.0) {   // uniform
+      // p = tau A22 v: a wave per row, the row's lower part and its column below the diagonal
+      for (int l = w; l < r; l += NW) {
+        const int gl = i + 1 + l;
+        double acc = 0.0;
+        for (int j = lane; j < r; j += 64) {
+          const int gj = i + 1 + j;
+          const double a = j <= l ? P[poff(gl) + gj] : P[poff(gj) + gl];
+          acc += a * vb[j];
+        }
+        acc = riptrm_wave::wave_sum(acc);
+        if (lane == 0) pb[l] = tau * acc;
+      }
+      __syncthreads();
+      // alpha2 = -tau (p . v) / 2 (every wave the same tree), w = p + alpha2 v, A22 -= v w^T + w v^T
+      double s = 0.0;
+      for (int l = lane; l < r; l += 64) s += pb[l] * vb[l];
+      s = riptrm_wave::wave_sum(s);
+      const double a2 = -0.5 * tau * s;
+      for (int l = w; l < r; l += NW) {
+        const double vl = vb[l], wl = pb[l] + a2 * vl;
+        lds_t* row = P + poff(i + 1 + l) + i + 1;
+        for (int j = lane; j <= l; j += 64) {
+          const double vj = vb[j];
+          const double wj = pb[j] + a2 * vj;
+          row[j] = row[j] - (vl * wj + wl * vj);
+        }
+      }
+    }
+    __syncthreads();
+  }
+  // d, e into LDS (vb, pb) and the slot
+  for (int i = tid; i < m; i += EW) {
+    const double di = P[poff(i) + i];
+    vb[i] = di;
+    dg[i] = di;
+    if (i < m - 1) pb[i] = P[poff(i + 1) + i];
+  }
+  __syncthreads();
+  const lds_t* d = vb;
+  const lds_t* e = pb;
+
+  // ---- 2. eigenvalues: bisection on Sturm counts, one thread per eigenvalue ------------------------
+  double tnorm = 0.0, glo = INFINITY, ghi = -INFINITY, emax2 = 0.0;
+  for (int j = 0; j < m; ++j) {   // every thread the same (broadcast LDS reads)
+    const double r0 = j > 0 ? fabs(e[j - 1]) : 0.0, r1 = j < m - 1 ? fabs(e[j]) : 0.0;
+    glo = fmin(glo, d[j] - r0 - r1);
+    ghi = fmax(ghi, d[j] + r0 + r1);
+    tnorm = fmax(tnorm, fabs(d[j]) + r0 + r1);
+    if (j < m - 1) emax2 = fmax(emax2, e[j] * e[j]);
+  }
+  const double eps = DBL_EPSILON;
+  const double pivmin = DBL_MIN * fmax(1.0, emax2);
+  const double fudge = 2.0 * eps * tnorm + 2.0 * pivmin;
+  double lam = 0.0;
+  if (tid < m) {
+    double lo = glo - fudge, hi = ghi + fudge;
+    for (int it = 0; it < 128; ++it) {
+      const double tol = fmax(2.0 * eps * fmax(fabs(lo), fabs(hi)), eps * tnorm);
+      if (hi - lo <= tol) break;
+      const double mid = 0.5 * (lo + hi);
+      if (mid <= lo || mid >= hi) break;
+      if (sturm_count(d, e, m, mid, pivmin) > tid) hi = mid;
+      else lo = mid;
+    }
+    lam = 0.5 * (lo + hi);
+    ev[tid] = lam;
+  }
+  if (!vectors) return;
+
+  // ---- 3. eigenvectors of T: twisted factorisation at lam, in the thread's output row ---------------
+  if (tid < m) {
+    double* Z = A + (int64_t)tid * lda;
+    const double tiny = pivmin;
+    double dp = d[0] - lam;
+    if (fabs(dp) < tiny) dp = -tiny;
+    Z[0] = dp;   // D+_j (LDL^T of T - lam I)
+    for (int j = 1; j < m; ++j) {
+      const double ej = e[j - 1];
+      dp = (d[j] - lam) - (ej * ej) / dp;
+      if (fabs(dp) < tiny) dp = -tiny;
+      Z[j] = dp;
+    }
+    // UDU^T from the bottom; gamma_j = D+_j + D-_j - (d_j - lam), the twist at min |gamma|
+    double dm = d[m - 1] - lam;
+    if (fabs(dm) < tiny) dm = -tiny;
+    double best = fabs(Z[m - 1]);
+    int r = m - 1;
+    for (int j = m - 2; j >= 0; --j) {
+      const double ej = e[j];
+      dm = (d[j] - lam) - (ej * ej) / dm;
+      if (fabs(dm) < tiny) dm = -tiny;
+      const double g = fabs(Z[j] + dm - (d[j] - lam));
+      if (g < best) {
+        best = g;
+        r = j;
+      }
+    }
+    // D-_j for j > r into the row (D+ is kept below the twist)
+    dm = d[m - 1] - lam;
+    if (fabs(dm) < tiny) dm = -tiny;
+    for (int j = m - 1; j > r; --j) {
+      if (j < m - 1) {
+        const double ej = e[j];
+        dm = (d[j] - lam) - (ej * ej) / dm;
+        if (fabs(dm) < tiny) dm = -tiny;
+      }
+      Z[j] = dm;
+    }
+    double z = 1.0, nrm = 1.0;
+    for (int j = r + 1; j < m; ++j) {   // z_j = -(e_{j-1} / D-_j) z_{j-1}
+      z = -(e[j - 1] / Z[j]) * z;
+      Z[j] = z;
+      nrm += z * z;
+    }
+    z = 1.0;
+    for (int j = r - 1; j >= 0; --j) {  // z_j = -(e_j / D+_j) z_{j+1}
+      z = -(e[j] / Z[j]) * z;
+      Z[j] = z;
+      nrm += z * z;
+    }
+    Z[r] = 1.0;
+    const double inv = 1.0 / sqrt(nrm);
+    for (int j = 0; j < m; ++j) Z[j] = Z[j] * inv;
+  }
+  __syncthreads();
+  for (int i = tid; i < m - 1; i += EW) pb[i] = tg[i];   // tau into LDS (e is done with)
+  __threadfence_block();
+  __syncthreads();
+
+  // ---- 4. back-transformation q = H_0 H_1 ... H_{m-2} z, four vectors per wave at a time ----------
+  constexpr int NV = 4;
+  for (int v0 = w * NV; v0 < m; v0 += NW * NV) {
+    double z[NV][4];
+    double* R[NV];
+#pragma unroll
+    for (int u = 0; u < NV; ++u) {
+      const int t = v0 + u < m ? v0 + u : m - 1;
+      R[u] = A + (int64_t)t * lda;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int j = lane + 64 * q;
+        z[u][q] = j < m ? R[u][j] : 0.0;
+      }
+    }
+    for (int i = m - 2; i >= 0; --i) {
+      const double tau = pb[i];
+      if (tau == 0.0) continue;   // uniform
+      double v[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int j = lane + 64 * q;
+        v[q] = j == i + 1 ? 1.0 : ((j > i + 1 && j < m) ? P[poff(j) + i] : 0.0);
+      }
+      double s[NV];
+#pragma unroll
+      for (int u = 0; u < NV; ++u) {
+        s[u] = 0.0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) s[u] += v[q] * z[u][q];
+      }
+#pragma unroll
+      for (int u = 0; u < NV; ++u) s[u] = riptrm_wave::wave_sum(s[u]);
+#pragma unroll
+      for (int u = 0; u < NV; ++u) {
+        const double f = tau * s[u];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) z[u][q] = z[u][q] - f * v[q];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < NV; ++u) {
+      if (v0 + u >= m) continue;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int j = lane + 64 * q;
+        if (j < m) R[u][j] = z[u][q];
+      }
+    }
+  }
+}
+
+}  // namespace riptrm_eig

@@ -35,6 +35,7 @@
 #include <string>
 #include <vector>
 #include "riptrm_ctx.h"
+#include "riptrm_eig.h"
 #include "riptrm_wave.h"
 
 using namespace riptrm;
@@ -933,6 +934,11 @@ static int big_handle(riptrm_ctx* c) {
 }
 
 void riptrm_big_release(riptrm_ctx* c) {
+  if (c && c->eig_scratch) {
+    (void)hipFree(c->eig_scratch);
+    c->eig_scratch = nullptr;
+    c->eig_scratch_bytes = 0;
+  }
   if (c && c->big_handle) {
     Solver& s = solver();
     if (s.ok) (void)s.destroy(c->big_handle);
@@ -954,12 +960,24 @@ static int32_t* flag_of(riptrm_ctx* c) { return tail_of(c) + 2 * c->big_slots; }
 // VS_EV, eigenvectors over A when vectors): rocSOLVER dsyevd (default) or, for A/B measurements
 // (RIPTRM_BIG_EIG=j / dj), its Jacobi dsyevj / dsyevdj
 static int eig_batched(riptrm_ctx* c, const Bat& B, int cnt, bool vectors, int m, int64_t aoff, int lda) {
+  const char* e = getenv("RIPTRM_BIG_EIG");
+  if (m <= riptrm_eig::EIG_LDS_MAX && !(e && e[0] != 'h')) {
+    // hand-written: one workgroup per matrix, the matrix in LDS (riptrm_eig.h); RIPTRM_BIG_EIG=r (or
+    // j / dj / s) keeps rocSOLVER for A/B
+    const size_t shm = riptrm_eig::eig_lds_bytes(m);
+    HIPCHK(c, hipFuncSetAttribute((const void*)riptrm_eig::k_eig_lds, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)shm));
+    hipLaunchKernelGGL(riptrm_eig::k_eig_lds, dim3(cnt), dim3(riptrm_eig::EW), shm, c->stream, B.base + aoff, B.sd, lda, m,
+                       B.base + off_vec(B.N, VS_EV), B.sd, B.base + off_vec(B.N, VS_R), B.base + off_vec(B.N, VS_EW),
+                       B.base + off_vec(B.N, VS_Q), B.sd, B.infos, vectors ? 1 : 0);
+    HIPCHK(c, hipGetLastError());
+    return RIPTRM_OK;
+  }
   if (int rc = big_handle(c)) return rc;
   Solver& s = solver();
   const int ev = vectors ? EVECT_ORIGINAL : EVECT_NONE;
   double* A = B.base + aoff;
   double* W = B.base + off_vec(B.N, VS_EV);
-  const char* e = getenv("RIPTRM_BIG_EIG");
   int st;
   if (e && e[0] == 'j' && s.syevj_sb) {
     int32_t* sweeps = tail_of(c) + 2 * c->big_slots + 8;
@@ -1308,6 +1326,32 @@ int riptrm_trs_cache_stats(riptrm_ctx* ctx, int64_t* hits, int64_t* subproblems)
   if (!ctx) return RIPTRM_E_ARG;
   if (hits) *hits = ctx->big_cache_hits;
   if (subproblems) *subproblems = ctx->big_subproblems;
+  return RIPTRM_OK;
+}
+
+int riptrm_sym_eig(riptrm_ctx* ctx, int32_t dim, int32_t batch, double* A, int64_t lda, int64_t a_stride, double* w,
+                   int64_t w_stride, int32_t* info, int32_t vectors) {
+  if (!ctx) return RIPTRM_E_ARG;
+  if (dim < 1 || dim > riptrm_eig::EIG_LDS_MAX || batch < 1 || !A || !w || !info || lda < dim ||
+      a_stride < (int64_t)dim * lda || w_stride < dim)
+    return fail(ctx, RIPTRM_E_ARG, "sym_eig: need 1 <= dim <= " + std::to_string(riptrm_eig::EIG_LDS_MAX) +
+                                       ", batch >= 1, lda >= dim, a_stride >= dim * lda, w_stride >= dim");
+  HIPCHK(ctx, hipSetDevice(ctx->device));
+  const int64_t sc = riptrm_eig::vpad_eig(dim);
+  const size_t need = (size_t)3 * sc * batch * sizeof(double);
+  if (ctx->eig_scratch_bytes < need) {
+    if (ctx->eig_scratch) HIPCHK(ctx, hipFree(ctx->eig_scratch));
+    ctx->eig_scratch = nullptr;
+    ctx->eig_scratch_bytes = 0;
+    HIPCHK(ctx, hipMalloc(&ctx->eig_scratch, need));
+    ctx->eig_scratch_bytes = need;
+  }
+  double* s = (double*)ctx->eig_scratch;
+  const size_t shm = riptrm_eig::eig_lds_bytes(dim);
+  HIPCHK(ctx, hipFuncSetAttribute((const void*)riptrm_eig::k_eig_lds, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm));
+  hipLaunchKernelGGL(riptrm_eig::k_eig_lds, dim3(batch), dim3(riptrm_eig::EW), shm, ctx->stream, A, a_stride, (int)lda, dim, w,
+                     w_stride, s, s + sc, s + 2 * sc, 3 * sc, info, vectors ? 1 : 0);
+  HIPCHK(ctx, hipGetLastError());
   return RIPTRM_OK;
 }
 

@@ -96,3 +96,23 @@ def TRSgep(A, a, B, Del, tolhardcase=1e-4):
     torch.cuda.synchronize(dev)
     k = int(kind[0])
     return x[0].cpu().numpy(), (0 if k == C["RIPTRM_TRS_INTERIOR"] else float(lam1[0])), KIND_NAMES[k]
+
+
+def sym_eig(A: torch.Tensor, vectors: bool = True) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+    """Batched symmetric eigendecomposition on the GPU (riptrm_sym_eig, csrc/riptrm_eig.h: the
+    eigensolver the Exact_RepMat HBM service uses for manifold.dim 97..199).  A: (batch, dim, dim)
+    symmetric float64 on one GPU, dim <= 199.  Returns (w (batch, dim) ascending, V (batch, dim, dim)
+    with eigenvector j in row j -- V[k] @ A[k] @ V[k].T = diag(w[k]) -- or None, info (batch,))."""
+    if not torch.cuda.is_available():
+        raise RuntimeError("sym_eig needs a ROCm GPU (gfx950); there is no CPU fallback")
+    if A.dim() != 3 or A.shape[1] != A.shape[2] or A.dtype != torch.float64 or not A.is_cuda:
+        raise ValueError("expected A (batch, dim, dim) float64 on a GPU")
+    B, dim = A.shape[0], A.shape[1]
+    V = A.contiguous().clone()
+    w = torch.empty((B, dim), dtype=torch.float64, device=A.device)
+    info = torch.empty(B, dtype=torch.int32, device=A.device)
+    ctx = _context(A.device)
+    p = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    ctx.check(ctx.lib.riptrm_sym_eig(ctx.h, dim, B, p(V), dim, dim * dim, p(w), dim, p(info), 1 if vectors else 0),
+              "riptrm_sym_eig")
+    return w, (V if vectors else None), info

@@ -161,3 +161,56 @@ def test_trs_gep_hard_case_above_lds_size():
             assert _obj(A, a, x[b]) <= _obj(A, a, xr) + 1e-10 * abs(_obj(A, a, xr))
             xe, le, ke = T.trs_eigh(A, a, Del, 1e-8)
             assert ke == "hardcase_1" and np.isclose(_obj(A, a, x[b]), _obj(A, a, xe), rtol=1e-10)
+
+
+def _clustered(m, rs, gaps):
+    """Q diag(lam) Q^T with prescribed eigenvalue clusters: lam has exact doubles, near-doubles at the
+    given relative gaps and a triple at the bottom (the hard case's multiplicity)."""
+    lam = np.sort(rs.randn(m) * 3.0)
+    lam[1] = lam[0]
+    lam[2] = lam[0]
+    for k, g in enumerate(gaps):
+        i = 10 + 7 * k
+        lam[i + 1] = lam[i] * (1.0 + g)
+    lam = np.sort(lam)
+    Q, _ = np.linalg.qr(rs.randn(m, m))
+    A = (Q * lam) @ Q.T
+    return (A + A.T) / 2
+
+
+@pytest.mark.parametrize("m", [1, 2, 3, 50, 97, 100, 150, 199])
+def test_sym_eig_matches_lapack(m):
+    """The hand-written batched eigensolver (riptrm_sym_eig, csrc/riptrm_eig.h) against LAPACK
+    (numpy.linalg.eigh): random symmetric matrices, the kind of matrix Exact_RepMat builds (a
+    shifted frame matrix with a few huge diagonal entries y_i / x_i) and clustered spectra (exact and
+    near-multiple eigenvalues, a triple at the bottom).  Eigenvalues within 1e-13 ||A||, residual
+    ||A v - lam v|| and orthogonality ||V V^T - I|| within 1e-12 (scaled)."""
+    import trs
+    rs = np.random.RandomState(m)
+    mats = [rs.randn(m, m)]
+    mats[0] = mats[0] + mats[0].T
+    D = rs.randn(m, m) / np.sqrt(m)
+    D = D + D.T + np.diag(np.where(rs.rand(m) < 0.3, 10.0 ** rs.uniform(2, 6, m), 0.0))
+    mats.append(D)
+    if m >= 40:
+        mats.append(_clustered(m, rs, (1e-4, 1e-8, 1e-12)))
+    A = torch.tensor(np.stack(mats), dtype=torch.float64, device="cuda")
+    w, V, info = trs.sym_eig(A)
+    torch.cuda.synchronize()
+    w, V, info = w.cpu().numpy(), V.cpu().numpy(), info.cpu().numpy()
+    assert (info == 0).all()
+    for k, M in enumerate(mats):
+        nrm = np.linalg.norm(M, 2)
+        ref = np.linalg.eigvalsh(M)
+        assert np.max(np.abs(w[k] - ref)) <= 1e-13 * max(nrm, 1e-300) * max(1.0, np.sqrt(m) / 4), (k, np.max(np.abs(w[k] - ref)) / nrm)
+        R = V[k] @ M - w[k][:, None] * V[k]
+        assert np.max(np.linalg.norm(R, axis=1)) <= 1e-12 * nrm, (k, np.max(np.linalg.norm(R, axis=1)) / nrm)
+        O = V[k] @ V[k].T - np.eye(m)
+        assert np.max(np.abs(O)) <= 1e-12, (k, np.max(np.abs(O)))
+    w2, V2, _ = trs.sym_eig(A, vectors=False)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(w2.cpu().numpy(), w)     # the same bisection with or without vectors
+    w3, V3, _ = trs.sym_eig(A[-1:].contiguous())
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(w3.cpu().numpy()[0], w[-1])   # batch-independent bits
+    np.testing.assert_array_equal(V3.cpu().numpy()[0], V[-1])
