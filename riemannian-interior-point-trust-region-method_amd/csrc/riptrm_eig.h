@@ -16,7 +16,11 @@
 //   3. eigenvectors of T by twisted factorisations (the LDL^T and UDU^T of T - lam I meet at the
 //      index of the smallest |gamma|), one thread per eigenvector, in its output row;
 //   4. back-transformation q = H_0 ... H_{m-2} z with the reflectors from LDS, a wave per group of
-//      four vectors (each vector spread over the wave's lanes, wave reductions for the dots).
+//      four vectors (each vector spread over the wave's lanes, wave reductions for the dots);
+//   5. block Gram-Schmidt among eigenvectors of close eigenvalues (the twisted vectors are
+//      orthogonal only to eps ||T|| / gap), first order inside a block.
+// Numerically multiple eigenvalues: T is split where e_j^2 <= eps^2 |d_j d_{j+1}| and each member of
+// such a run takes its vector on a different block.
 // Output as rocSOLVER's: eigenvalues ascending, eigenvector k in row k of the row-major view of the
 // input (column k of the column-major matrix), info = 0 (non-finite input: info = 1).  Fixed
 // reduction orders: a matrix's results do not depend on the batch it is in.
@@ -36,8 +40,13 @@ constexpr int EIG_MAX_M = 256;             // four elements per lane in the back
 
 __host__ __device__ constexpr int poff(int i) { return i * (i + 1) / 2; }
 __host__ __device__ constexpr int vpad_eig(int m) { return (m + 7) / 8 * 8; }
+constexpr int GB = 32;                     // row block of the Gram-Schmidt phase
+// dynamic LDS: the packed triangle + d / e (phases 1-4), or two GB-row blocks + their Gram (phase 5)
 __host__ __device__ constexpr size_t eig_lds_bytes(int m) {
-  return ((size_t)poff(m) + 2 * (size_t)vpad_eig(m)) * sizeof(double);
+  return (poff(m) + 2 * (size_t)vpad_eig(m) > 2 * (size_t)GB * vpad_eig(m) + GB * (GB + 1)
+              ? poff(m) + 2 * (size_t)vpad_eig(m)
+              : 2 * (size_t)GB * vpad_eig(m) + GB * (GB + 1)) *
+         sizeof(double);
 }
 
 typedef __attribute__((address_space(3))) double lds_t;
@@ -169,6 +178,14 @@ __global__ void __launch_bounds__(EW) k_eig_lds(double* A0, int64_t a_stride, in
     if (i < m - 1) pb[i] = P[poff(i + 1) + i];
   }
   __syncthreads();
+  const double eps = DBL_EPSILON;
+  // splitting (LAPACK dstebz): e_j -> 0 where e_j^2 <= eps^2 |d_j d_{j+1}| (eigenvalues move by
+  // O(eps |d|)); a numerically multiple eigenvalue then lives in separate blocks
+  for (int j = tid; j < m - 1; j += EW) {
+    const double ej = pb[j];
+    if (ej * ej <= (eps * eps) * fabs(vb[j] * vb[j + 1]) + DBL_MIN) pb[j] = 0.0;
+  }
+  __syncthreads();
   const lds_t* d = vb;
   const lds_t* e = pb;
 
@@ -181,7 +198,6 @@ __global__ void __launch_bounds__(EW) k_eig_lds(double* A0, int64_t a_stride, in
     tnorm = fmax(tnorm, fabs(d[j]) + r0 + r1);
     if (j < m - 1) emax2 = fmax(emax2, e[j] * e[j]);
   }
-  const double eps = DBL_EPSILON;
   const double pivmin = DBL_MIN * fmax(1.0, emax2);
   const double fudge = 2.0 * eps * tnorm + 2.0 * pivmin;
   double lam = 0.0;
@@ -199,26 +215,59 @@ __global__ void __launch_bounds__(EW) k_eig_lds(double* A0, int64_t a_stride, in
     ev[tid] = lam;
   }
   if (!vectors) return;
+  __syncthreads();   // every eigenvalue in ev (the block assignment below reads its neighbours)
 
-  // ---- 3. eigenvectors of T: twisted factorisation at lam, in the thread's output row ---------------
+  // ---- 3. eigenvectors of T: twisted factorisation at lam on its block, in the thread's row ----------
   if (tid < m) {
     double* Z = A + (int64_t)tid * lda;
     const double tiny = pivmin;
-    double dp = d[0] - lam;
+    // numerically equal eigenvalues (within delta) take distinct blocks: member k of the run
+    // i0 .. takes the block where the running count of block eigenvalues in [lam - delta,
+    // lam + delta] passes k (per-block Sturm counts at both ends)
+    const double delta = 16.0 * eps * tnorm;
+    int i0 = tid;
+    while (i0 > 0 && lam - ev[i0 - 1] <= delta) --i0;
+    const int kk = tid - i0;
+    int blo = 0, bhi = m - 1, acc = 0, bs = 0, ca = 0, cb = 0;
+    bool found = false;
+    double qa = 0.0, qb = 0.0;
+    for (int j = 0; j < m; ++j) {
+      const bool start = j == bs;
+      const double ej2 = start ? 0.0 : e[j - 1] * e[j - 1];
+      qa = (d[j] - (lam - delta)) - (start ? 0.0 : ej2 / qa);
+      if (fabs(qa) < pivmin) qa = -pivmin;
+      qb = (d[j] - (lam + delta)) - (start ? 0.0 : ej2 / qb);
+      if (fabs(qb) < pivmin) qb = -pivmin;
+      ca += qa < 0.0;
+      cb += qb < 0.0;
+      if (j == m - 1 || e[j] == 0.0) {   // block bs .. j ends
+        if (!found && acc + (cb - ca) > kk) {
+          found = true;
+          blo = bs;
+          bhi = j;
+        }
+        acc += cb - ca;
+        ca = cb = 0;
+        bs = j + 1;
+      }
+    }
+    for (int j = 0; j < blo; ++j) Z[j] = 0.0;
+    for (int j = bhi + 1; j < m; ++j) Z[j] = 0.0;
+    double dp = d[blo] - lam;
     if (fabs(dp) < tiny) dp = -tiny;
-    Z[0] = dp;   // D+_j (LDL^T of T - lam I)
-    for (int j = 1; j < m; ++j) {
+    Z[blo] = dp;   // D+_j (LDL^T of T - lam I on the block)
+    for (int j = blo + 1; j <= bhi; ++j) {
       const double ej = e[j - 1];
       dp = (d[j] - lam) - (ej * ej) / dp;
       if (fabs(dp) < tiny) dp = -tiny;
       Z[j] = dp;
     }
-    // UDU^T from the bottom; gamma_j = D+_j + D-_j - (d_j - lam), the twist at min |gamma|
-    double dm = d[m - 1] - lam;
+    // UDU^T from the block's bottom; gamma_j = D+_j + D-_j - (d_j - lam), the twist at min |gamma|
+    double dm = d[bhi] - lam;
     if (fabs(dm) < tiny) dm = -tiny;
-    double best = fabs(Z[m - 1]);
-    int r = m - 1;
-    for (int j = m - 2; j >= 0; --j) {
+    double best = fabs(Z[bhi]);
+    int r = bhi;
+    for (int j = bhi - 1; j >= blo; --j) {
       const double ej = e[j];
       dm = (d[j] - lam) - (ej * ej) / dm;
       if (fabs(dm) < tiny) dm = -tiny;
@@ -229,10 +278,10 @@ __global__ void __launch_bounds__(EW) k_eig_lds(double* A0, int64_t a_stride, in
       }
     }
     // D-_j for j > r into the row (D+ is kept below the twist)
-    dm = d[m - 1] - lam;
+    dm = d[bhi] - lam;
     if (fabs(dm) < tiny) dm = -tiny;
-    for (int j = m - 1; j > r; --j) {
-      if (j < m - 1) {
+    for (int j = bhi; j > r; --j) {
+      if (j < bhi) {
         const double ej = e[j];
         dm = (d[j] - lam) - (ej * ej) / dm;
         if (fabs(dm) < tiny) dm = -tiny;
@@ -240,20 +289,20 @@ __global__ void __launch_bounds__(EW) k_eig_lds(double* A0, int64_t a_stride, in
       Z[j] = dm;
     }
     double z = 1.0, nrm = 1.0;
-    for (int j = r + 1; j < m; ++j) {   // z_j = -(e_{j-1} / D-_j) z_{j-1}
+    for (int j = r + 1; j <= bhi; ++j) {   // z_j = -(e_{j-1} / D-_j) z_{j-1}
       z = -(e[j - 1] / Z[j]) * z;
       Z[j] = z;
       nrm += z * z;
     }
     z = 1.0;
-    for (int j = r - 1; j >= 0; --j) {  // z_j = -(e_j / D+_j) z_{j+1}
+    for (int j = r - 1; j >= blo; --j) {  // z_j = -(e_j / D+_j) z_{j+1}
       z = -(e[j] / Z[j]) * z;
       Z[j] = z;
       nrm += z * z;
     }
     Z[r] = 1.0;
     const double inv = 1.0 / sqrt(nrm);
-    for (int j = 0; j < m; ++j) Z[j] = Z[j] * inv;
+    for (int j = blo; j <= bhi; ++j) Z[j] = Z[j] * inv;
   }
   __syncthreads();
   for (int i = tid; i < m - 1; i += EW) pb[i] = tg[i];   // tau into LDS (e is done with)
@@ -309,6 +358,88 @@ __global__ void __launch_bounds__(EW) k_eig_lds(double* A0, int64_t a_stride, in
         if (j < m) R[u][j] = z[u][q];
       }
     }
+  }
+  __threadfence_block();
+  __syncthreads();
+
+  // ---- 5. orthogonality: block Gram-Schmidt over close eigenvalues ---------------------------------
+  // The twisted vectors are orthogonal to ~eps ||T|| / gap: ~1e-9 for the frame matrices of
+  // Exact_RepMat (a few diagonal entries y_i / x_i ~ 1e6 over O(1) eigenvalues).  Row blocks of GB
+  // vectors, in order: block J loses its components along every earlier block I that holds
+  // eigenvalues within CTOL ||T|| of its own (classical GS against the already orthonormal rows,
+  // E = Q_I Q_J^T), then its own Gram E = Q_J Q_J^T - I is removed to first order (Q_J <- (I -
+  // tril(E, -1) - diag(E) / 2) Q_J: exact to O(E^2), E ~ 1e-9 here).  A block whose |E| exceeds
+  // 1e-4 (no reliable first-order fix) reports info = 2.
+  {
+    const double ctol = 1e-2 * tnorm;
+    const int nb = (m + GB - 1) / GB;
+    const int mp = vpad_eig(m);
+    lds_t* QJ = P;                         // [GB][mp]
+    lds_t* QI = P + GB * mp;               // [GB][mp]
+    lds_t* E = P + 2 * GB * mp;            // [GB][GB + 1]
+    __shared__ int eflag;
+    if (tid == 0) eflag = 0;
+    for (int J = 0; J < nb; ++J) {
+      const int j0 = J * GB, jn = min(GB, m - j0);
+      __syncthreads();
+      for (int q = tid; q < GB * mp; q += EW) {
+        const int a = q / mp, c = q - a * mp;
+        QJ[q] = (a < jn && c < m) ? A[(int64_t)(j0 + a) * lda + c] : 0.0;
+      }
+      for (int I = 0; I <= J; ++I) {
+        const int i0b = I * GB, in = min(GB, m - i0b);
+        // eigenvalues sorted: block I is close to block J iff its last one is within ctol of J's first
+        if (I < J && ev[j0] - ev[i0b + in - 1] > ctol) continue;   // uniform
+        __syncthreads();
+        if (I < J)
+          for (int q = tid; q < GB * mp; q += EW) {
+            const int a = q / mp, c = q - a * mp;
+            QI[q] = (a < in && c < m) ? A[(int64_t)(i0b + a) * lda + c] : 0.0;
+          }
+        __syncthreads();
+        const lds_t* QA = I < J ? QI : QJ;
+        // E[a][b] = Q_I[a] . Q_J[b] (a 2 x 1 register block per thread: GB x GB / 512)
+        for (int q = tid; q < GB * GB; q += EW) {
+          const int a = q / GB, b = q - a * GB;
+          double sacc = 0.0;
+          for (int c = 0; c < m; ++c) sacc += QA[a * mp + c] * QJ[b * mp + c];
+          E[a * (GB + 1) + b] = (I == J && a == b) ? sacc - 1.0 : sacc;
+        }
+        __syncthreads();
+        if (I == J) {
+          for (int q = tid; q < GB * GB; q += EW) {
+            const int a = q / GB, b = q - a * GB;
+            if (a < jn && b < jn && fabs(E[a * (GB + 1) + b]) > 1e-4) eflag = 1;
+          }
+          // Q_J[b] <- Q_J[b] - sum_{a < b} E[a][b] Q_J[a] - E[b][b] / 2 Q_J[b] (old rows on the right)
+          for (int q = tid; q < GB * mp; q += EW) {
+            const int b = q / mp, c = q - b * mp;
+            double v = QJ[b * mp + c];
+            double corr = 0.5 * E[b * (GB + 1) + b] * v;
+            for (int a = 0; a < b; ++a) corr += E[a * (GB + 1) + b] * QJ[a * mp + c];
+            QI[b * mp + c] = v - corr;   // QI is free here (I == J is the last of the loop)
+          }
+          __syncthreads();
+          for (int q = tid; q < GB * mp; q += EW) QJ[q] = QI[q];
+        } else {
+          // Q_J[b] -= sum_a E[a][b] Q_I[a]
+          for (int q = tid; q < GB * mp; q += EW) {
+            const int b = q / mp, c = q - b * mp;
+            double corr = 0.0;
+            for (int a = 0; a < in; ++a) corr += E[a * (GB + 1) + b] * QI[a * mp + c];
+            QJ[q] = QJ[q] - corr;
+          }
+        }
+      }
+      __syncthreads();
+      for (int q = tid; q < jn * m; q += EW) {
+        const int a = q / m, c = q - a * m;
+        A[(int64_t)(j0 + a) * lda + c] = QJ[a * mp + c];
+      }
+      __threadfence_block();
+    }
+    __syncthreads();
+    if (tid == 0 && eflag) infos[k] = 2;
   }
 }
 
