@@ -179,12 +179,15 @@ __global__ void __launch_bounds__(EW) k_eig_lds(double* A0, int64_t a_stride, in
   }
   __syncthreads();
   const double eps = DBL_EPSILON;
-  // splitting (LAPACK dstebz): e_j -> 0 where e_j^2 <= eps^2 |d_j d_{j+1}| (eigenvalues move by
-  // O(eps |d|)); a numerically multiple eigenvalue then lives in separate blocks
-  for (int j = tid; j < m - 1; j += EW) {
-    const double ej = pb[j];
-    if (ej * ej <= (eps * eps) * fabs(vb[j] * vb[j + 1]) + DBL_MIN) pb[j] = 0.0;
-  }
+  // splitting: e_j -> 0 where |e_j| <= 4 eps ||T|| (the tridiagonalisation's own rounding level, so
+  // the eigenvalues move by no more than its error); a multiple eigenvalue of A then lives in
+  // separate blocks of T (an unreduced tridiagonal has simple eigenvalues)
+  double tn0 = 0.0;
+  for (int j = 0; j < m; ++j)
+    tn0 = fmax(tn0, fabs(vb[j]) + (j > 0 ? fabs(pb[j - 1]) : 0.0) + (j < m - 1 ? fabs(pb[j]) : 0.0));
+  __syncthreads();
+  for (int j = tid; j < m - 1; j += EW)
+    if (fabs(pb[j]) <= 4.0 * eps * tn0) pb[j] = 0.0;
   __syncthreads();
   const lds_t* d = vb;
   const lds_t* e = pb;
@@ -368,8 +371,9 @@ __global__ void __launch_bounds__(EW) k_eig_lds(double* A0, int64_t a_stride, in
   // vectors, in order: block J loses its components along every earlier block I that holds
   // eigenvalues within CTOL ||T|| of its own (classical GS against the already orthonormal rows,
   // E = Q_I Q_J^T), then its own Gram E = Q_J Q_J^T - I is removed to first order (Q_J <- (I -
-  // tril(E, -1) - diag(E) / 2) Q_J: exact to O(E^2), E ~ 1e-9 here).  A block whose |E| exceeds
-  // 1e-4 (no reliable first-order fix) reports info = 2.
+  // tril(E, -1) - diag(E) / 2) Q_J: exact to O(E^2), E ~ 1e-9 here).  The sweep repeats while
+  // some |E| exceeded 1e-8 (the first-order fix leaves O(E^2)), at most three times; vectors as
+  // good as parallel (|E| > 0.5) report info = 2.
   {
     const double ctol = 1e-2 * tnorm;
     const int nb = (m + GB - 1) / GB;
@@ -377,8 +381,11 @@ __global__ void __launch_bounds__(EW) k_eig_lds(double* A0, int64_t a_stride, in
     lds_t* QJ = P;                         // [GB][mp]
     lds_t* QI = P + GB * mp;               // [GB][mp]
     lds_t* E = P + 2 * GB * mp;            // [GB][GB + 1]
-    __shared__ int eflag;
+    __shared__ int eflag, again;
     if (tid == 0) eflag = 0;
+    for (int pass = 0; pass < 3; ++pass) {
+    __syncthreads();
+    if (tid == 0) again = 0;
     for (int J = 0; J < nb; ++J) {
       const int j0 = J * GB, jn = min(GB, m - j0);
       __syncthreads();
@@ -403,14 +410,15 @@ __global__ void __launch_bounds__(EW) k_eig_lds(double* A0, int64_t a_stride, in
           const int a = q / GB, b = q - a * GB;
           double sacc = 0.0;
           for (int c = 0; c < m; ++c) sacc += QA[a * mp + c] * QJ[b * mp + c];
-          E[a * (GB + 1) + b] = (I == J && a == b) ? sacc - 1.0 : sacc;
+          const double eab = (I == J && a == b) ? sacc - 1.0 : sacc;
+          E[a * (GB + 1) + b] = eab;
+          if (a < in && b < jn) {
+            if (fabs(eab) > 1e-8) again = 1;
+            if (fabs(eab) > 0.5 && !(I == J && a == b)) eflag = 1;
+          }
         }
         __syncthreads();
         if (I == J) {
-          for (int q = tid; q < GB * GB; q += EW) {
-            const int a = q / GB, b = q - a * GB;
-            if (a < jn && b < jn && fabs(E[a * (GB + 1) + b]) > 1e-4) eflag = 1;
-          }
           // Q_J[b] <- Q_J[b] - sum_{a < b} E[a][b] Q_J[a] - E[b][b] / 2 Q_J[b] (old rows on the right)
           for (int q = tid; q < GB * mp; q += EW) {
             const int b = q / mp, c = q - b * mp;
@@ -439,6 +447,8 @@ __global__ void __launch_bounds__(EW) k_eig_lds(double* A0, int64_t a_stride, in
       __threadfence_block();
     }
     __syncthreads();
+    if (!again) break;   // uniform
+    }
     if (tid == 0 && eflag) infos[k] = 2;
   }
 }
