@@ -18,7 +18,7 @@
 //   4. back-transformation q = H_0 ... H_{m-2} z with the reflectors from LDS, a wave per group of
 //      four vectors (each vector spread over the wave's lanes, wave reductions for the dots);
 //   5. block Gram-Schmidt among eigenvectors of close eigenvalues (the twisted vectors are
-//      orthogonal only to eps ||T|| / gap), first order inside a block.
+//      orthogonal only to eps ||T|| / gap), Cholesky-QR inside a block.
 // Numerically multiple eigenvalues: T is split where e_j^2 <= eps^2 |d_j d_{j+1}| and each member of
 // such a run takes its vector on a different block.
 // Output as rocSOLVER's: eigenvalues ascending, eigenvector k in row k of the row-major view of the
@@ -41,11 +41,12 @@ constexpr int EIG_MAX_M = 256;             // four elements per lane in the back
 __host__ __device__ constexpr int poff(int i) { return i * (i + 1) / 2; }
 __host__ __device__ constexpr int vpad_eig(int m) { return (m + 7) / 8 * 8; }
 constexpr int GB = 32;                     // row block of the Gram-Schmidt phase
-// dynamic LDS: the packed triangle + d / e (phases 1-4), or two GB-row blocks + their Gram (phase 5)
+// dynamic LDS: the packed triangle + d / e (phases 1-4), or two GB-row blocks + their Gram and its
+// Cholesky inverse (phase 5)
 __host__ __device__ constexpr size_t eig_lds_bytes(int m) {
-  return (poff(m) + 2 * (size_t)vpad_eig(m) > 2 * (size_t)GB * vpad_eig(m) + GB * (GB + 1)
+  return (poff(m) + 2 * (size_t)vpad_eig(m) > 2 * (size_t)GB * vpad_eig(m) + 2 * GB * (GB + 1)
               ? poff(m) + 2 * (size_t)vpad_eig(m)
-              : 2 * (size_t)GB * vpad_eig(m) + GB * (GB + 1)) *
+              : 2 * (size_t)GB * vpad_eig(m) + 2 * GB * (GB + 1)) *
          sizeof(double);
 }
 
@@ -370,10 +371,10 @@ __global__ void __launch_bounds__(EW) k_eig_lds(double* A0, int64_t a_stride, in
   // Exact_RepMat (a few diagonal entries y_i / x_i ~ 1e6 over O(1) eigenvalues).  Row blocks of GB
   // vectors, in order: block J loses its components along every earlier block I that holds
   // eigenvalues within CTOL ||T|| of its own (classical GS against the already orthonormal rows,
-  // E = Q_I Q_J^T), then its own Gram E = Q_J Q_J^T - I is removed to first order (Q_J <- (I -
-  // tril(E, -1) - diag(E) / 2) Q_J: exact to O(E^2), E ~ 1e-9 here).  The sweep repeats while
-  // some |E| exceeded 1e-8 (the first-order fix leaves O(E^2)), at most three times; vectors as
-  // good as parallel (|E| > 0.5) report info = 2.
+  // E = Q_I Q_J^T), then is orthonormalised itself (Cholesky-QR of its Gram).  The sweep repeats
+  // while some |E| exceeded 1e-8, at most three times; a row that is (numerically) in the span of
+  // its block's earlier rows is rebuilt from the orthogonal complement of all the others; if that
+  // fails, info = 2.
   {
     const double ctol = 1e-2 * tnorm;
     const int nb = (m + GB - 1) / GB;
@@ -381,11 +382,12 @@ __global__ void __launch_bounds__(EW) k_eig_lds(double* A0, int64_t a_stride, in
     lds_t* QJ = P;                         // [GB][mp]
     lds_t* QI = P + GB * mp;               // [GB][mp]
     lds_t* E = P + 2 * GB * mp;            // [GB][GB + 1]
-    __shared__ int eflag, again;
+    __shared__ int eflag, again, ndrop;
+    __shared__ int dropped[16];
     if (tid == 0) eflag = 0;
     for (int pass = 0; pass < 3; ++pass) {
     __syncthreads();
-    if (tid == 0) again = 0;
+    if (tid == 0) again = 0, ndrop = 0;
     for (int J = 0; J < nb; ++J) {
       const int j0 = J * GB, jn = min(GB, m - j0);
       __syncthreads();
@@ -414,18 +416,55 @@ __global__ void __launch_bounds__(EW) k_eig_lds(double* A0, int64_t a_stride, in
           E[a * (GB + 1) + b] = eab;
           if (a < in && b < jn) {
             if (fabs(eab) > 1e-8) again = 1;
-            if (fabs(eab) > 0.5 && !(I == J && a == b)) eflag = 1;
           }
         }
         __syncthreads();
         if (I == J) {
-          // Q_J[b] <- Q_J[b] - sum_{a < b} E[a][b] Q_J[a] - E[b][b] / 2 Q_J[b] (old rows on the right)
+          // exact orthonormalisation of the block: G = Q_J Q_J^T = L L^T (wave 0, right-looking, lane c
+          // owns row c), Q_J <- L^-1 Q_J.  A pivot below 1/4 (a vector nearly in the span of the
+          // block's earlier ones: a numerically multiple eigenvalue T did not split) drops the row;
+          // it is rebuilt from the orthogonal complement of all other vectors after the sweep.
+          lds_t* Li = E + GB * (GB + 1);   // L^-1, [GB][GB + 1]
+          if (w == 0 && lane < GB) {
+            const int c = lane;
+            E[c * (GB + 1) + c] += 1.0;   // G = E + I
+            if (c >= jn) E[c * (GB + 1) + c] = 1.0;   // padding rows: identity
+            for (int kk = 0; kk < GB; ++kk) {
+              const double piv = E[kk * (GB + 1) + kk];
+              const bool drop = kk < jn && piv < 0.25;
+              if (drop && c == 0) dropped[ndrop < 16 ? ndrop : 15] = j0 + kk, ndrop = ndrop + 1;
+              const double sq = drop ? 1.0 : sqrt(piv);
+              double lck = 0.0;
+              if (c > kk) lck = drop ? 0.0 : E[c * (GB + 1) + kk] / sq;
+              asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // lanes exchange through LDS
+              if (c == kk) E[c * (GB + 1) + kk] = sq;
+              if (c > kk) {
+                E[c * (GB + 1) + kk] = lck;
+                for (int c2 = kk + 1; c2 <= c; ++c2) {
+                  // L[c2][kk] of another lane: read after every lane wrote its column entry
+                  const double l2 = c2 == c ? lck : E[c2 * (GB + 1) + kk];
+                  E[c * (GB + 1) + c2] -= lck * l2;
+                }
+              }
+              asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // lanes exchange through LDS
+            }
+            // column c of L^-1 (lower)
+            for (int rr = 0; rr < GB; ++rr) Li[rr * (GB + 1) + c] = 0.0;
+            Li[c * (GB + 1) + c] = 1.0 / E[c * (GB + 1) + c];
+            for (int rr = c + 1; rr < GB; ++rr) {
+              double acc = 0.0;
+              for (int ss = c; ss < rr; ++ss) acc += E[rr * (GB + 1) + ss] * Li[ss * (GB + 1) + c];
+              Li[rr * (GB + 1) + c] = -acc / E[rr * (GB + 1) + rr];
+            }
+          }
+          __syncthreads();
           for (int q = tid; q < GB * mp; q += EW) {
             const int b = q / mp, c = q - b * mp;
-            double v = QJ[b * mp + c];
-            double corr = 0.5 * E[b * (GB + 1) + b] * v;
-            for (int a = 0; a < b; ++a) corr += E[a * (GB + 1) + b] * QJ[a * mp + c];
-            QI[b * mp + c] = v - corr;   // QI is free here (I == J is the last of the loop)
+            double v = 0.0;
+            for (int a = 0; a <= b; ++a) v += Li[b * (GB + 1) + a] * QJ[a * mp + c];
+            bool dr = false;
+            for (int z2 = 0; z2 < (ndrop < 16 ? ndrop : 16); ++z2) dr |= dropped[z2] == j0 + b;
+            QI[b * mp + c] = dr ? 0.0 : v;   // QI is free here (I == J is the last of the loop)
           }
           __syncthreads();
           for (int q = tid; q < GB * mp; q += EW) QJ[q] = QI[q];
@@ -445,6 +484,48 @@ __global__ void __launch_bounds__(EW) k_eig_lds(double* A0, int64_t a_stride, in
         A[(int64_t)(j0 + a) * lda + c] = QJ[a * mp + c];
       }
       __threadfence_block();
+    }
+    __syncthreads();
+    if (ndrop > 16) eflag = 1;
+    // dropped rows: a unit vector made orthogonal (twice) to every other row spans what the others
+    // leave of the eigenspace -- an eigenvector when they are eigenvectors
+    for (int z2 = 0; z2 < (ndrop < 16 ? ndrop : 16); ++z2) {
+      const int t = dropped[z2];
+      lds_t* u = QI;   // [mp]
+      lds_t* cf = QJ;  // coefficients [m]
+      for (int tr = 0; tr < 4; ++tr) {
+        const int e1 = (t * 131 + 7 + 53 * tr) % m;
+        for (int c = tid; c < mp; c += EW) u[c] = c == e1 ? 1.0 : 0.0;
+        __syncthreads();
+        for (int rep = 0; rep < 2; ++rep) {
+          for (int rr = w; rr < m; rr += NW) {   // cf[rr] = q_rr . u (row t itself is zero)
+            double acc = 0.0;
+            for (int c = lane; c < m; c += 64) acc += A[(int64_t)rr * lda + c] * u[c];
+            acc = riptrm_wave::wave_sum(acc);
+            if (lane == 0) cf[rr] = rr == t ? 0.0 : acc;
+          }
+          __syncthreads();
+          for (int c = tid; c < m; c += EW) {
+            double acc = 0.0;
+            for (int rr = 0; rr < m; ++rr) acc += cf[rr] * A[(int64_t)rr * lda + c];
+            u[c] = u[c] - acc;
+          }
+          __syncthreads();
+        }
+        double nn = 0.0;
+        for (int c = lane; c < m; c += 64) nn += u[c] * u[c];
+        nn = riptrm_wave::wave_sum(nn);   // every wave the same
+        if (nn > 1e-2) {   // uniform
+          const double inv = 1.0 / sqrt(nn);
+          for (int c = tid; c < m; c += EW) A[(int64_t)t * lda + c] = u[c] * inv;
+          __threadfence_block();
+          __syncthreads();
+          break;
+        }
+        if (tr == 3 && tid == 0) eflag = 1;
+        __syncthreads();
+      }
+      if (tid == 0) again = 1;   // verify with another sweep
     }
     __syncthreads();
     if (!again) break;   // uniform

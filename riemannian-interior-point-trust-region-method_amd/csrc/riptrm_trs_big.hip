@@ -500,6 +500,175 @@ __global__ void __launch_bounds__(WG) k_cg_wg(Bat B, int m, int64_t aoff, int64_
   cg_final_terms(red, q.sc, an, D[(int64_t)B.ids[k] * dstride], v0, v1, v2, v3);
 }
 
+// The same SciPy CG on ONE wave for orders m <= CGW_MAX (StableIdentification at d = 8: m = 100,
+// where indefinite subproblems run the CG to its 10 m iteration cap): A in LDS with an odd row stride
+// (each lane reads its own rows, conflict-free), two rows per lane, p broadcast from LDS, the dot
+// products as wave reductions -- no workgroup barrier in the loop (k_cg_wg pays three per
+// iteration).  Its own fixed summation order (four partial sums per row); skip_indef as k_cg_wg.
+constexpr int CGW_MAX = 128;
+inline size_t cg_wave_lds(int m) { return ((size_t)m * (m + 1) + CGW_MAX) * sizeof(double); }
+__global__ void __launch_bounds__(64) k_cg_wave(Bat B, int m, int64_t aoff, int64_t lda, const double* D,
+                                                int64_t dstride, const double* Aext = nullptr, int64_t ext_stride = 0,
+                                                int skip_indef = 0) {
+  extern __shared__ double cgs[];
+  const int k = blockIdx.y;
+  const Slot q = slot_at(B, k);
+  const double* A = Aext ? Aext + (int64_t)B.ids[k] * ext_stride : q.M + aoff;
+  const double* a = q.v[VS_A];
+  const int l = threadIdx.x;
+  const double Dl = D[(int64_t)B.ids[k] * dstride];
+  if (skip_indef) {   // k_cg_wg's certified skip, with wave reductions
+    const double *ev = q.v[VS_EV], *g = q.v[VS_G];
+    const double lmin = ev[0], lmax = fmax(fabs(ev[0]), fabs(ev[m - 1]));
+    double lsm = INFINITY, s1 = 0.0, s2 = 0.0, aa = 0.0;
+    for (int i = l; i < m; i += 64) {
+      const double lv = ev[i], gi = g[i];
+      lsm = fmin(lsm, fabs(lv));
+      s1 += (gi / lv) * (gi / lv);
+      s2 += gi * gi / lv;
+      aa += a[i] * a[i];
+    }
+    lsm = riptrm_wave::wave_min(lsm);
+    s1 = riptrm_wave::wave_sum(s1);
+    s2 = riptrm_wave::wave_sum(s2);
+    const double e = 1e-5 * sqrt(riptrm_wave::wave_sum(aa));
+    bool skip = *q.info == 0 && lmin < -1e-8 * lmax && lsm > 1e-8 * lmax;
+    if (skip) {
+      const double xobj = q.sc[SC_XOBJ];
+      const bool far = sqrt(s1) * (1.0 - 1e-6) - e / lsm >= Dl;
+      const double p1lo = -0.5 * s2 - 0.5 * e * e / lsm;
+      const bool worse = p1lo - xobj > 1e-6 * (fabs(s2) + fabs(xobj)) + 1e-10 * (e * 1e5) * Dl;
+      skip = far || worse;
+    }
+    if (skip) {
+      if (l == 0) {
+        q.sc[SC_CG_OK] = 0.0;
+        q.sc[SC_P1OBJ] = 0.0;
+        q.sc[SC_IT] = 0.0;
+        q.sc[SC_DONE] = 4.0;
+        q.sc[SC_DELTA] = Dl;
+      }
+      return;
+    }
+  }
+  const int ms = m + 1;
+  lds_f64* Al = (lds_f64*)cgs;
+  lds_f64* ps = Al + (int64_t)m * ms;
+  for (int64_t e = l; e < (int64_t)m * m; e += 64) {
+    const int i = (int)(e / m), j = (int)(e - (int64_t)i * m);
+    Al[i * ms + j] = A[(int64_t)i * lda + j];
+  }
+  double x[2] = {0.0, 0.0}, r[2];
+  double an = 0.0;
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int i = l + 64 * u;
+    const double bi = i < m ? -a[i] : 0.0;
+    r[u] = bi;
+    an += bi * bi;
+  }
+  an = sqrt(riptrm_wave::wave_sum(an));
+  const double atol = 1e-5 * an;
+  double done = an == 0.0 ? 2.0 : 0.0, it = 0.0, rho_prev = 1.0;
+  __syncthreads();
+  // rows i = l and l + 64 of A . p, each with four partial sums (j mod 4), then (s0 + s1) + (s2 + s3)
+  auto matvec = [&](double* qv) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int i = l + 64 * u < m ? l + 64 * u : m - 1;
+      const lds_f64* row = Al + i * ms;
+      double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+      int j = 0;
+      for (; j + 3 < m; j += 4) {
+        s0 += row[j] * ps[j];
+        s1 += row[j + 1] * ps[j + 1];
+        s2 += row[j + 2] * ps[j + 2];
+        s3 += row[j + 3] * ps[j + 3];
+      }
+      if (j < m) s0 += row[j] * ps[j];
+      if (j + 1 < m) s1 += row[j + 1] * ps[j + 1];
+      if (j + 2 < m) s2 += row[j + 2] * ps[j + 2];
+      qv[u] = l + 64 * u < m ? (s0 + s1) + (s2 + s3) : 0.0;
+    }
+  };
+  while (done == 0.0) {   // uniform
+    if (it >= 10.0 * m) {
+      done = 3.0;
+      break;
+    }
+    const double rr = riptrm_wave::wave_sum(r[0] * r[0] + r[1] * r[1]);   // zero past m
+    if (sqrt(rr) < atol) {
+      done = 1.0;
+      break;
+    }
+    const double rho = rr;
+    const double beta = it > 0.0 ? rho / rho_prev : 0.0;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int i = l + 64 * u;
+      if (i < m) ps[i] = it > 0.0 ? ps[i] * beta + r[u] : r[u];
+    }
+    __syncthreads();
+    double qv[2];
+    matvec(qv);
+    double pq = 0.0;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int i = l + 64 * u;
+      if (i < m) pq += ps[i] * qv[u];
+    }
+    pq = riptrm_wave::wave_sum(pq);
+    const double alpha = rho / pq;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      if (l + 64 * u < m) {
+        x[u] += alpha * ps[l + 64 * u];
+        r[u] -= alpha * qv[u];
+      }
+    }
+    rho_prev = rho;
+    it += 1.0;
+    __syncthreads();
+  }
+  __syncthreads();
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int i = l + 64 * u;
+    if (i < m) {
+      ps[i] = x[u];
+      q.v[VS_CGX][i] = x[u];
+    }
+  }
+  __syncthreads();
+  double qv[2];
+  matvec(qv);
+  double v0 = 0.0, v1 = 0.0, v2 = 0.0, v3 = 0.0;
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int i = l + 64 * u;
+    if (i < m) {
+      const double res = qv[u] + a[i];
+      v0 += res * res;
+      v1 += x[u] * x[u];
+      v2 += x[u] * qv[u];
+      v3 += a[i] * x[u];
+    }
+  }
+  v0 = riptrm_wave::wave_sum(v0);
+  v1 = riptrm_wave::wave_sum(v1);
+  v2 = riptrm_wave::wave_sum(v2);
+  v3 = riptrm_wave::wave_sum(v3);
+  if (l == 0) {
+    q.sc[SC_AN] = an;
+    q.sc[SC_ATOL] = atol;
+    q.sc[SC_IT] = it;
+    q.sc[SC_DONE] = done;
+    q.sc[SC_CG_OK] = (an != 0.0 && sqrt(v0) / an < 1e-5 && v1 < Dl * Dl) ? 1.0 : 0.0;   // RIPTRM.py:246-251
+    q.sc[SC_P1OBJ] = 0.5 * v2 + v3;
+    q.sc[SC_DELTA] = Dl;
+  }
+}
+
 // grid-wide CG, one launch each step for all slots (grid.y = slot)
 __global__ void __launch_bounds__(WG) k_cg_init(Bat B, int m) {
   __shared__ double red[WG / 64];
@@ -1028,7 +1197,12 @@ static int big_cg(riptrm_ctx* c, const Bat& B, int cnt, int64_t aoff, int lda, i
   hipStream_t st = c->stream;
   const int64_t N = B.N;
   const dim3 one(1, cnt), rows(blocks_of(m, GV / 64), cnt);
-  if (cg_one_workgroup(m, cnt)) {
+  if (m <= CGW_MAX && cg_one_workgroup(m, cnt) && !getenv_is("RIPTRM_CG_WAVE", '0')) {
+    const size_t shm = cg_wave_lds(m);
+    HIPCHK(c, hipFuncSetAttribute((const void*)k_cg_wave, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm));
+    hipLaunchKernelGGL(k_cg_wave, one, dim3(64), shm, st, B, m, aoff, (int64_t)lda, D, dstride, nullptr, (int64_t)0, 0);
+    HIPCHK(c, hipGetLastError());
+  } else if (cg_one_workgroup(m, cnt)) {
     const int rl = cg_lds_rows(m);
     const size_t shm = (size_t)rl * m * sizeof(double);
     if (shm > 0)
@@ -1233,12 +1407,19 @@ int riptrm_big_gep_ids(riptrm_ctx* c, int dim, const int32_t* sel, int count, co
                          dim, off_vec(N, VS_A), off_vec(N, VS_G), (int64_t)-1);
       hipLaunchKernelGGL(k_set_delta, dim3(blocks_of(cnt, 64)), dim3(64), 0, st, Bt, cnt, Delta, (int64_t)1);
       hipLaunchKernelGGL(k_secular, dim3(1, cnt), dim3(WG), 0, st, Bt, dim, tolhc, 0);
-      const int rl = cg_lds_rows(dim);
-      const size_t shm = (size_t)rl * dim * sizeof(double);
-      if (shm > 0)
-        HIPCHK(c, hipFuncSetAttribute((const void*)k_cg_wg, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm));
-      hipLaunchKernelGGL(k_cg_wg, dim3(1, cnt), dim3(WG), shm, st, Bt, dim, (int64_t)0, lda, Delta, (int64_t)1, rl, A,
-                         a_stride, 1);
+      if (dim <= CGW_MAX && !getenv_is("RIPTRM_CG_WAVE", '0')) {
+        const size_t shm = cg_wave_lds(dim);
+        HIPCHK(c, hipFuncSetAttribute((const void*)k_cg_wave, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm));
+        hipLaunchKernelGGL(k_cg_wave, dim3(1, cnt), dim3(64), shm, st, Bt, dim, (int64_t)0, lda, Delta, (int64_t)1, A,
+                           a_stride, 1);
+      } else {
+        const int rl = cg_lds_rows(dim);
+        const size_t shm = (size_t)rl * dim * sizeof(double);
+        if (shm > 0)
+          HIPCHK(c, hipFuncSetAttribute((const void*)k_cg_wg, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm));
+        hipLaunchKernelGGL(k_cg_wg, dim3(1, cnt), dim3(WG), shm, st, Bt, dim, (int64_t)0, lda, Delta, (int64_t)1, rl, A,
+                           a_stride, 1);
+      }
       skip_done.resize(cnt);
       HIPCHK(c, hipMemcpy2DAsync(skip_done.data(), sizeof(double), Bt.base + off_sc(N) + SC_DONE, (size_t)Bt.sd * sizeof(double),
                                  sizeof(double), cnt, hipMemcpyDeviceToHost, st));

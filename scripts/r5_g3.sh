@@ -1,6 +1,6 @@
 set -u
 cd "$GRAFT_REPO_ROOT"
-O=gpurun_out/${OUT:-r5f}
+O=gpurun_out/${OUT:-r5g}
 mkdir -p $O
 export TMPDIR=/tmp
 timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu -s tests/test_gpu_trs.py > $O/trs_tests.log 2>&1 || { tail -60 $O/trs_tests.log; exit 1; }
