@@ -41,16 +41,29 @@ constexpr int EIG_MAX_M = 256;             // four elements per lane in the back
 __host__ __device__ constexpr int poff(int i) { return i * (i + 1) / 2; }
 __host__ __device__ constexpr int vpad_eig(int m) { return (m + 7) / 8 * 8; }
 constexpr int GB = 32;                     // row block of the Gram-Schmidt phase
-// dynamic LDS: the packed triangle + d / e (phases 1-4), or two GB-row blocks + their Gram and its
-// Cholesky inverse (phase 5)
+constexpr int ZB = 64;                     // eigenvectors per block of the twisted + back-transform phase
+constexpr int RB = 16;                     // reflectors staged in LDS at a time
+__host__ __device__ constexpr int ms_of(int m) { return vpad_eig(m) + 1; }   // odd LDS row stride
+__host__ __device__ constexpr size_t smax(size_t a, size_t b) { return a > b ? a : b; }
+// doubles before d / e / tau: the packed triangle (phase 1) or a ZB-vector block + a reflector stage
+__host__ __device__ constexpr size_t de_off(int m) { return smax((size_t)poff(m), (size_t)(ZB + RB) * ms_of(m)); }
+__host__ __device__ constexpr size_t refl_doubles(int m) { return ((size_t)poff(m) + 7) / 8 * 8; }
+// dynamic LDS: phases 1-4 (packed triangle or vector block + stage, then d, e, tau), or phase 5
+// (two GB-row blocks + their Gram and its Cholesky inverse)
 __host__ __device__ constexpr size_t eig_lds_bytes(int m) {
-  return (poff(m) + 2 * (size_t)vpad_eig(m) > 2 * (size_t)GB * vpad_eig(m) + 2 * GB * (GB + 1)
-              ? poff(m) + 2 * (size_t)vpad_eig(m)
-              : 2 * (size_t)GB * vpad_eig(m) + 2 * GB * (GB + 1)) *
-         sizeof(double);
+  return smax(de_off(m) + 3 * (size_t)vpad_eig(m), 2 * (size_t)GB * ms_of(m) + 2 * GB * (GB + 1)) * sizeof(double);
 }
 
 typedef __attribute__((address_space(3))) double lds_t;
+
+// 1 / q by v_rcp_f64 and two Newton steps (a shorter dependent chain than the IEEE division)
+__device__ __forceinline__ double rcp_nr(double q) {
+  double r = __builtin_amdgcn_rcp(q);
+  double t = fma(-q, r, 1.0);
+  r = fma(r, t, r);
+  t = fma(-q, r, 1.0);
+  return fma(r, t, r);
+}
 
 // the number of eigenvalues of T (diagonal d, off-diagonal e) below x (Sturm count, LAPACK dlaneg's
 // recurrence with pivmin guarding zero pivots)
@@ -58,9 +71,26 @@ __device__ __forceinline__ int sturm_count(const lds_t* d, const lds_t* e, int m
   double q = d[0] - x;
   if (fabs(q) < pivmin) q = -pivmin;
   int c = q < 0.0;
-  for (int j = 1; j < m; ++j) {
+  int j = 1;
+  for (; j + 3 < m; j += 4) {   // the next four entries' loads issued ahead of the dependent chain
+    const double d0 = d[j], d1 = d[j + 1], d2 = d[j + 2], d3 = d[j + 3];
+    const double f0 = e[j - 1], f1 = e[j], f2 = e[j + 1], f3 = e[j + 2];
+    q = (d0 - x) - (f0 * f0) * rcp_nr(q);
+    if (fabs(q) < pivmin) q = -pivmin;
+    c += q < 0.0;
+    q = (d1 - x) - (f1 * f1) * rcp_nr(q);
+    if (fabs(q) < pivmin) q = -pivmin;
+    c += q < 0.0;
+    q = (d2 - x) - (f2 * f2) * rcp_nr(q);
+    if (fabs(q) < pivmin) q = -pivmin;
+    c += q < 0.0;
+    q = (d3 - x) - (f3 * f3) * rcp_nr(q);
+    if (fabs(q) < pivmin) q = -pivmin;
+    c += q < 0.0;
+  }
+  for (; j < m; ++j) {
     const double ej = e[j - 1];
-    q = (d[j] - x) - (ej * ej) / q;
+    q = (d[j] - x) - (ej * ej) * rcp_nr(q);
     if (fabs(q) < pivmin) q = -pivmin;
     c += q < 0.0;
   }
@@ -70,16 +100,18 @@ __device__ __forceinline__ int sturm_count(const lds_t* d, const lds_t* e, int m
 // Matrix k = blockIdx.x: the m x m symmetric matrix at A0 + k a_stride (leading dimension lda; the
 // lower triangle is read) -> eigenvalues ascending at ev0 + k ev_stride, eigenvectors (vectors != 0)
 // in the rows of the same matrix.  Scratch per matrix (three vectors of >= m doubles, k sc_stride
-// apart): d at d0, e at e0, tau at t0.
+// apart): d at d0, e at e0, tau at t0; the reflectors (refl_doubles(m)) at R0 + k r_stride.
 __global__ void __launch_bounds__(EW) k_eig_lds(double* A0, int64_t a_stride, int lda, int m, double* ev0,
                                                 int64_t ev_stride, double* d0, double* e0, double* t0,
-                                                int64_t sc_stride, int32_t* infos, int vectors) {
+                                                int64_t sc_stride, double* R0, int64_t r_stride, int32_t* infos,
+                                                int vectors, long long* stamps = nullptr) {
   extern __shared__ double smem[];
   __shared__ double scal[2];
   __shared__ int bad;
   lds_t* P = (lds_t*)smem;                    // packed lower triangle, row i at poff(i)
-  lds_t* vb = P + poff(m);                    // the reflector (phase 1), then d (phases 2-3)
-  lds_t* pb = vb + vpad_eig(m);               // p (phase 1), then e (phases 2-3), then tau (phase 4)
+  lds_t* vb = P + de_off(m);                  // the reflector (phase 1), then d (phases 2-3)
+  lds_t* pb = vb + vpad_eig(m);               // p (phase 1), then e (phases 2-3)
+  lds_t* tb = pb + vpad_eig(m);               // tau (phase 4)
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   constexpr int NW = EW / 64;
   const int k = blockIdx.x;
@@ -88,7 +120,10 @@ __global__ void __launch_bounds__(EW) k_eig_lds(double* A0, int64_t a_stride, in
   double* dg = d0 + (int64_t)k * sc_stride;
   double* eg = e0 + (int64_t)k * sc_stride;
   double* tg = t0 + (int64_t)k * sc_stride;
+  double* Rg = R0 + (int64_t)k * r_stride;
   if (tid == 0) bad = 0;
+  long long* stp = (stamps && tid == 0) ? stamps + (int64_t)k * 8 : nullptr;   // phase clocks (diagnostics)
+  if (stp) stp[0] = clock64();
   __syncthreads();
   for (int64_t q = tid; q < (int64_t)m * m; q += EW) {
     const int i = (int)(q / m), j = (int)(q - (int64_t)i * m);
@@ -141,36 +176,78 @@ __global__ void __launch_bounds__(EW) k_eig_lds(double* A0, int64_t a_stride, in
     __syncthreads();
     const double tau = scal[0];
     if (tau != 0.0) {   // uniform
-      // p = tau A22 v: a wave per row, the row's lower part and its column below the diagonal
-      for (int l = w; l < r; l += NW) {
-        const int gl = i + 1 + l;
-        double acc = 0.0;
-        for (int j = lane; j < r; j += 64) {
-          const int gj = i + 1 + j;
-          const double a = j <= l ? P[poff(gl) + gj] : P[poff(gj) + gl];
-          acc += a * vb[j];
+      // p = tau A22 v: two threads per row (r <= 256), each over half the row -- its part of the
+      // packed row (contiguous) and, past the diagonal, its part of the column below the diagonal
+      // (an incremental offset, no multiplies) -- then the partner's half (lane ^ 1: a + b on both)
+      {
+        const int l = tid >> 1, h = tid & 1;
+        const int half = (r + 1) >> 1;
+        double acc0 = 0.0, acc1 = 0.0;
+        if (l < r) {
+          const int gl = i + 1 + l;
+          const int jb = h * half, je = min(r, jb + half);
+          const int jm = max(jb, min(je, l + 1));
+          const lds_t* rowp = P + poff(gl) + i + 1;
+          double acc2 = 0.0, acc3 = 0.0;
+          int j = jb;
+          for (; j + 3 < jm; j += 4) {
+            acc0 += rowp[j] * vb[j];
+            acc1 += rowp[j + 1] * vb[j + 1];
+            acc2 += rowp[j + 2] * vb[j + 2];
+            acc3 += rowp[j + 3] * vb[j + 3];
+          }
+          for (; j < jm; ++j) acc0 += rowp[j] * vb[j];
+          int off = poff(i + 1 + j) + gl;   // element (i + 1 + j, gl) of the packed lower triangle
+          for (; j + 3 < je; j += 4) {
+            const int o1 = off + i + 1 + j + 1;   // poff(k + 1) = poff(k) + k + 1
+            const int o2 = o1 + i + 1 + j + 2;
+            const int o3 = o2 + i + 1 + j + 3;
+            acc0 += P[off] * vb[j];
+            acc1 += P[o1] * vb[j + 1];
+            acc2 += P[o2] * vb[j + 2];
+            acc3 += P[o3] * vb[j + 3];
+            off = o3 + i + 1 + j + 4;
+          }
+          for (; j < je; ++j) {
+            acc0 += P[off] * vb[j];
+            off += i + 1 + j + 1;
+          }
+          acc0 = (acc0 + acc1) + (acc2 + acc3);
+          acc1 = 0.0;
         }
-        acc = riptrm_wave::wave_sum(acc);
-        if (lane == 0) pb[l] = tau * acc;
+        double acc = acc0 + acc1;
+        acc = acc + riptrm_wave::dpp<riptrm_wave::DPP_XOR1>(acc);
+        if (l < r && h == 0) pb[l] = tau * acc;
       }
       __syncthreads();
-      // alpha2 = -tau (p . v) / 2 (every wave the same tree), w = p + alpha2 v, A22 -= v w^T + w v^T
+      // alpha2 = -tau (p . v) / 2 (every wave the same tree), w = p + alpha2 v, A22 -= v w^T + w v^T:
+      // lanes over columns (v_j, w_j in registers), waves over rows
       double s = 0.0;
       for (int l = lane; l < r; l += 64) s += pb[l] * vb[l];
       s = riptrm_wave::wave_sum(s);
       const double a2 = -0.5 * tau * s;
+      double vj[4], wj[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int j = lane + 64 * q;
+        vj[q] = j < r ? vb[j] : 0.0;
+        wj[q] = j < r ? pb[j] + a2 * vj[q] : 0.0;
+      }
       for (int l = w; l < r; l += NW) {
         const double vl = vb[l], wl = pb[l] + a2 * vl;
         lds_t* row = P + poff(i + 1 + l) + i + 1;
-        for (int j = lane; j <= l; j += 64) {
-          const double vj = vb[j];
-          const double wj = pb[j] + a2 * vj;
-          row[j] = row[j] - (vl * wj + wl * vj);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int j = lane + 64 * q;
+          if (j <= l) row[j] = row[j] - (vl * wj[q] + wl * vj[q]);
         }
       }
     }
     __syncthreads();
   }
+  if (stp) stp[1] = clock64();
+  if (vectors)   // the reflectors (below the subdiagonal of the packed triangle) for the back-transformation
+    for (int q = tid; q < poff(m); q += EW) Rg[q] = P[q];
   // d, e into LDS (vb, pb) and the slot
   for (int i = tid; i < m; i += EW) {
     const double di = P[poff(i) + i];
@@ -204,167 +281,179 @@ __global__ void __launch_bounds__(EW) k_eig_lds(double* A0, int64_t a_stride, in
   }
   const double pivmin = DBL_MIN * fmax(1.0, emax2);
   const double fudge = 2.0 * eps * tnorm + 2.0 * pivmin;
-  double lam = 0.0;
-  if (tid < m) {
-    double lo = glo - fudge, hi = ghi + fudge;
-    for (int it = 0; it < 128; ++it) {
-      const double tol = fmax(2.0 * eps * fmax(fabs(lo), fabs(hi)), eps * tnorm);
-      if (hi - lo <= tol) break;
-      const double mid = 0.5 * (lo + hi);
-      if (mid <= lo || mid >= hi) break;
-      if (sturm_count(d, e, m, mid, pivmin) > tid) hi = mid;
-      else lo = mid;
-    }
-    lam = 0.5 * (lo + hi);
-    ev[tid] = lam;
-  }
-  if (!vectors) return;
-  __syncthreads();   // every eigenvalue in ev (the block assignment below reads its neighbours)
-
-  // ---- 3. eigenvectors of T: twisted factorisation at lam on its block, in the thread's row ----------
-  if (tid < m) {
-    double* Z = A + (int64_t)tid * lda;
-    const double tiny = pivmin;
-    // numerically equal eigenvalues (within delta) take distinct blocks: member k of the run
-    // i0 .. takes the block where the running count of block eigenvalues in [lam - delta,
-    // lam + delta] passes k (per-block Sturm counts at both ends)
-    const double delta = 16.0 * eps * tnorm;
-    int i0 = tid;
-    while (i0 > 0 && lam - ev[i0 - 1] <= delta) --i0;
-    const int kk = tid - i0;
-    int blo = 0, bhi = m - 1, acc = 0, bs = 0, ca = 0, cb = 0;
-    bool found = false;
-    double qa = 0.0, qb = 0.0;
-    for (int j = 0; j < m; ++j) {
-      const bool start = j == bs;
-      const double ej2 = start ? 0.0 : e[j - 1] * e[j - 1];
-      qa = (d[j] - (lam - delta)) - (start ? 0.0 : ej2 / qa);
-      if (fabs(qa) < pivmin) qa = -pivmin;
-      qb = (d[j] - (lam + delta)) - (start ? 0.0 : ej2 / qb);
-      if (fabs(qb) < pivmin) qb = -pivmin;
-      ca += qa < 0.0;
-      cb += qb < 0.0;
-      if (j == m - 1 || e[j] == 0.0) {   // block bs .. j ends
-        if (!found && acc + (cb - ca) > kk) {
-          found = true;
-          blo = bs;
-          bhi = j;
+  // multisection: kq (1, 2, 4 or 8) consecutive lanes per eigenvalue test kq points of its interval
+  // at once and keep the sub-interval the counts select (the same on every lane of the group)
+  {
+    int kq = EW / m;
+    kq = kq >= 8 ? 8 : (kq >= 4 ? 4 : (kq >= 2 ? 2 : 1));
+    const int ei = tid / kq, sub = tid - ei * kq, base = (int)(threadIdx.x & 63) - sub;
+    if (ei < m) {
+      double lo = glo - fudge, hi = ghi + fudge;
+      for (int it = 0; it < 128; ++it) {
+        const double tol = fmax(2.0 * eps * fmax(fabs(lo), fabs(hi)), eps * tnorm);
+        if (hi - lo <= tol) break;   // uniform over the group
+        const double step = (hi - lo) / (kq + 1);
+        const double x = lo + step * (sub + 1);
+        const int c = (x > lo && x < hi) ? sturm_count(d, e, m, x, pivmin) : (x <= lo ? 0 : m);
+        double nlo = lo, nhi = hi;
+        for (int s2 = 0; s2 < kq; ++s2) {
+          const int cs = __shfl(c, base + s2);
+          const double xs = lo + step * (s2 + 1);
+          if (cs > ei) nhi = fmin(nhi, xs);
+          else nlo = fmax(nlo, xs);
         }
-        acc += cb - ca;
-        ca = cb = 0;
-        bs = j + 1;
+        if (nlo >= nhi || (nlo == lo && nhi == hi)) break;
+        lo = nlo;
+        hi = nhi;
       }
+      if (sub == 0) ev[ei] = 0.5 * (lo + hi);
     }
-    for (int j = 0; j < blo; ++j) Z[j] = 0.0;
-    for (int j = bhi + 1; j < m; ++j) Z[j] = 0.0;
-    double dp = d[blo] - lam;
-    if (fabs(dp) < tiny) dp = -tiny;
-    Z[blo] = dp;   // D+_j (LDL^T of T - lam I on the block)
-    for (int j = blo + 1; j <= bhi; ++j) {
-      const double ej = e[j - 1];
-      dp = (d[j] - lam) - (ej * ej) / dp;
-      if (fabs(dp) < tiny) dp = -tiny;
-      Z[j] = dp;
-    }
-    // UDU^T from the block's bottom; gamma_j = D+_j + D-_j - (d_j - lam), the twist at min |gamma|
-    double dm = d[bhi] - lam;
-    if (fabs(dm) < tiny) dm = -tiny;
-    double best = fabs(Z[bhi]);
-    int r = bhi;
-    for (int j = bhi - 1; j >= blo; --j) {
-      const double ej = e[j];
-      dm = (d[j] - lam) - (ej * ej) / dm;
-      if (fabs(dm) < tiny) dm = -tiny;
-      const double g = fabs(Z[j] + dm - (d[j] - lam));
-      if (g < best) {
-        best = g;
-        r = j;
-      }
-    }
-    // D-_j for j > r into the row (D+ is kept below the twist)
-    dm = d[bhi] - lam;
-    if (fabs(dm) < tiny) dm = -tiny;
-    for (int j = bhi; j > r; --j) {
-      if (j < bhi) {
-        const double ej = e[j];
-        dm = (d[j] - lam) - (ej * ej) / dm;
-        if (fabs(dm) < tiny) dm = -tiny;
-      }
-      Z[j] = dm;
-    }
-    double z = 1.0, nrm = 1.0;
-    for (int j = r + 1; j <= bhi; ++j) {   // z_j = -(e_{j-1} / D-_j) z_{j-1}
-      z = -(e[j - 1] / Z[j]) * z;
-      Z[j] = z;
-      nrm += z * z;
-    }
-    z = 1.0;
-    for (int j = r - 1; j >= blo; --j) {  // z_j = -(e_j / D+_j) z_{j+1}
-      z = -(e[j] / Z[j]) * z;
-      Z[j] = z;
-      nrm += z * z;
-    }
-    Z[r] = 1.0;
-    const double inv = 1.0 / sqrt(nrm);
-    for (int j = blo; j <= bhi; ++j) Z[j] = Z[j] * inv;
   }
   __syncthreads();
-  for (int i = tid; i < m - 1; i += EW) pb[i] = tg[i];   // tau into LDS (e is done with)
-  __threadfence_block();
-  __syncthreads();
+  const double lam = tid < m ? ev[tid] : 0.0;
+  if (stp) stp[2] = clock64();
+  if (!vectors) return;
 
-  // ---- 4. back-transformation q = H_0 H_1 ... H_{m-2} z, four vectors per wave at a time ----------
-  constexpr int NV = 4;
-  for (int v0 = w * NV; v0 < m; v0 += NW * NV) {
-    double z[NV][4];
-    double* R[NV];
-#pragma unroll
-    for (int u = 0; u < NV; ++u) {
-      const int t = v0 + u < m ? v0 + u : m - 1;
-      R[u] = A + (int64_t)t * lda;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int j = lane + 64 * q;
-        z[u][q] = j < m ? R[u][j] : 0.0;
+  // ---- 3 + 4. per block of ZB eigenvectors, in LDS: the twisted vectors of T, then q = H_0 ... H_{m-2} z
+  const int ms = ms_of(m);
+  lds_t* Zb = P;                 // [ZB][ms]
+  lds_t* St = P + ZB * ms;       // [RB][ms]: reflectors i_hi - RB + 1 .. i_hi, v_i[j] dense
+  for (int i = tid; i < m - 1; i += EW) tb[i] = tg[i];
+  const double delta = 16.0 * eps * tnorm;
+  for (int t0 = 0; t0 < m; t0 += ZB) {
+    __syncthreads();   // the previous block's rows are out, tau is in
+    if (tid < ZB && t0 + tid < m) {
+      const int t = t0 + tid;
+      const double lt = ev[t];
+      lds_t* Z = Zb + tid * ms;
+      const double tiny = pivmin;
+      // numerically equal eigenvalues (within delta) take distinct blocks of the split T: member kk
+      // of the run i0 .. takes the block where the running count of block eigenvalues in
+      // [lt - delta, lt + delta] passes kk (per-block Sturm counts at both ends)
+      int i0 = t;
+      while (i0 > 0 && lt - ev[i0 - 1] <= delta) --i0;
+      const int kk = t - i0;
+      int blo = 0, bhi = m - 1, acc = 0, bs = 0, ca = 0, cb = 0;
+      bool found = false;
+      double qa = 0.0, qb = 0.0;
+      for (int j = 0; j < m; ++j) {
+        const bool start = j == bs;
+        const double ej2 = start ? 0.0 : e[j - 1] * e[j - 1];
+        qa = (d[j] - (lt - delta)) - (start ? 0.0 : ej2 / qa);
+        if (fabs(qa) < pivmin) qa = -pivmin;
+        qb = (d[j] - (lt + delta)) - (start ? 0.0 : ej2 / qb);
+        if (fabs(qb) < pivmin) qb = -pivmin;
+        ca += qa < 0.0;
+        cb += qb < 0.0;
+        if (j == m - 1 || e[j] == 0.0) {   // block bs .. j ends
+          if (!found && acc + (cb - ca) > kk) {
+            found = true;
+            blo = bs;
+            bhi = j;
+          }
+          acc += cb - ca;
+          ca = cb = 0;
+          bs = j + 1;
+        }
+      }
+      for (int j = 0; j < blo; ++j) Z[j] = 0.0;
+      for (int j = bhi + 1; j < m; ++j) Z[j] = 0.0;
+      double dp = d[blo] - lt;
+      if (fabs(dp) < tiny) dp = -tiny;
+      Z[blo] = dp;   // D+_j (LDL^T of T - lt I on the block)
+      for (int j = blo + 1; j <= bhi; ++j) {
+        const double ej = e[j - 1];
+        dp = (d[j] - lt) - (ej * ej) / dp;
+        if (fabs(dp) < tiny) dp = -tiny;
+        Z[j] = dp;
+      }
+      // UDU^T from the block's bottom; gamma_j = D+_j + D-_j - (d_j - lt), the twist at min |gamma|
+      double dm = d[bhi] - lt;
+      if (fabs(dm) < tiny) dm = -tiny;
+      double best = fabs(Z[bhi]);
+      int r = bhi;
+      for (int j = bhi - 1; j >= blo; --j) {
+        const double ej = e[j];
+        dm = (d[j] - lt) - (ej * ej) / dm;
+        if (fabs(dm) < tiny) dm = -tiny;
+        const double g = fabs(Z[j] + dm - (d[j] - lt));
+        if (g < best) {
+          best = g;
+          r = j;
+        }
+      }
+      // D-_j for j > r into the row (D+ is kept below the twist)
+      dm = d[bhi] - lt;
+      if (fabs(dm) < tiny) dm = -tiny;
+      for (int j = bhi; j > r; --j) {
+        if (j < bhi) {
+          const double ej = e[j];
+          dm = (d[j] - lt) - (ej * ej) / dm;
+          if (fabs(dm) < tiny) dm = -tiny;
+        }
+        Z[j] = dm;
+      }
+      double z = 1.0, nrm = 1.0;
+      for (int j = r + 1; j <= bhi; ++j) {   // z_j = -(e_{j-1} / D-_j) z_{j-1}
+        z = -(e[j - 1] / Z[j]) * z;
+        Z[j] = z;
+        nrm += z * z;
+      }
+      z = 1.0;
+      for (int j = r - 1; j >= blo; --j) {  // z_j = -(e_j / D+_j) z_{j+1}
+        z = -(e[j] / Z[j]) * z;
+        Z[j] = z;
+        nrm += z * z;
+      }
+      Z[r] = 1.0;
+      const double inv = 1.0 / sqrt(nrm);
+      for (int j = blo; j <= bhi; ++j) Z[j] = Z[j] * inv;
+    }
+    // back-transformation of the block: reflectors i = m - 2 .. 0, RB at a time staged from Rg; eight
+    // lanes per vector (lane c8 takes j = c8, c8 + 8, ...: its own elements only, so the wave needs
+    // no LDS ordering between reflectors), the dot product closed by three butterfly steps
+    const int u = tid >> 3, c8 = tid & 7;
+    for (int ihi = m - 2; ihi >= 0; ihi -= RB) {
+      const int ilo = ihi - RB + 1 > 0 ? ihi - RB + 1 : 0;
+      __syncthreads();   // the block's vectors are in; the previous stage is done with
+      for (int q = tid; q < (ihi - ilo + 1) * ms; q += EW) {
+        const int ii = q / ms, j = q - ii * ms;
+        const int i = ilo + ii;
+        St[q] = j == i + 1 ? 1.0 : ((j > i + 1 && j < m) ? Rg[poff(j) + i] : 0.0);
+      }
+      __syncthreads();
+      if (t0 + u < m) {
+        lds_t* Zu = Zb + u * ms;
+        for (int i = ihi; i >= ilo; --i) {
+          const double tau = tb[i];
+          if (tau == 0.0) continue;   // uniform
+          const lds_t* vi = St + (i - ilo) * ms;
+          const int jb = i + 1 + ((c8 - (i + 1)) & 7);   // my first j >= i + 1
+          double s0 = 0.0, s1 = 0.0;
+          int j = jb;
+          for (; j + 8 < m; j += 16) {
+            s0 += vi[j] * Zu[j];
+            s1 += vi[j + 8] * Zu[j + 8];
+          }
+          if (j < m) s0 += vi[j] * Zu[j];
+          double sv = s0 + s1;
+          sv = sv + riptrm_wave::dpp<riptrm_wave::DPP_XOR1>(sv);
+          sv = sv + riptrm_wave::dpp<riptrm_wave::DPP_XOR2>(sv);
+          sv = sv + riptrm_wave::dpp<riptrm_wave::DPP_HALF_MIRROR>(sv);   // lane ^ 7 within the row of 8
+          const double f = tau * sv;
+          for (j = jb; j < m; j += 8) Zu[j] = Zu[j] - f * vi[j];
+        }
       }
     }
-    for (int i = m - 2; i >= 0; --i) {
-      const double tau = pb[i];
-      if (tau == 0.0) continue;   // uniform
-      double v[4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int j = lane + 64 * q;
-        v[q] = j == i + 1 ? 1.0 : ((j > i + 1 && j < m) ? P[poff(j) + i] : 0.0);
-      }
-      double s[NV];
-#pragma unroll
-      for (int u = 0; u < NV; ++u) {
-        s[u] = 0.0;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) s[u] += v[q] * z[u][q];
-      }
-#pragma unroll
-      for (int u = 0; u < NV; ++u) s[u] = riptrm_wave::wave_sum(s[u]);
-#pragma unroll
-      for (int u = 0; u < NV; ++u) {
-        const double f = tau * s[u];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) z[u][q] = z[u][q] - f * v[q];
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < NV; ++u) {
-      if (v0 + u >= m) continue;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int j = lane + 64 * q;
-        if (j < m) R[u][j] = z[u][q];
-      }
+    __syncthreads();
+    for (int q = tid; q < ZB * m; q += EW) {
+      const int uu = q / m, c = q - uu * m;
+      if (t0 + uu < m) A[(int64_t)(t0 + uu) * lda + c] = Zb[uu * ms + c];
     }
   }
   __threadfence_block();
   __syncthreads();
+  if (stp) stp[3] = stp[4] = clock64();
 
   // ---- 5. orthogonality: block Gram-Schmidt over close eigenvalues ---------------------------------
   // The twisted vectors are orthogonal to ~eps ||T|| / gap: ~1e-9 for the frame matrices of
@@ -378,7 +467,7 @@ __global__ void __launch_bounds__(EW) k_eig_lds(double* A0, int64_t a_stride, in
   {
     const double ctol = 1e-2 * tnorm;
     const int nb = (m + GB - 1) / GB;
-    const int mp = vpad_eig(m);
+    const int mp = vpad_eig(m) + 1;        // odd row stride: a wave's 32 rows at one column hit distinct banks
     lds_t* QJ = P;                         // [GB][mp]
     lds_t* QI = P + GB * mp;               // [GB][mp]
     lds_t* E = P + 2 * GB * mp;            // [GB][GB + 1]
@@ -410,8 +499,18 @@ __global__ void __launch_bounds__(EW) k_eig_lds(double* A0, int64_t a_stride, in
         // E[a][b] = Q_I[a] . Q_J[b] (a 2 x 1 register block per thread: GB x GB / 512)
         for (int q = tid; q < GB * GB; q += EW) {
           const int a = q / GB, b = q - a * GB;
-          double sacc = 0.0;
-          for (int c = 0; c < m; ++c) sacc += QA[a * mp + c] * QJ[b * mp + c];
+          double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+          const lds_t* xa = QA + a * mp;
+          const lds_t* xb = QJ + b * mp;
+          int c = 0;
+          for (; c + 3 < m; c += 4) {
+            s0 += xa[c] * xb[c];
+            s1 += xa[c + 1] * xb[c + 1];
+            s2 += xa[c + 2] * xb[c + 2];
+            s3 += xa[c + 3] * xb[c + 3];
+          }
+          for (; c < m; ++c) s0 += xa[c] * xb[c];
+          const double sacc = (s0 + s1) + (s2 + s3);
           const double eab = (I == J && a == b) ? sacc - 1.0 : sacc;
           E[a * (GB + 1) + b] = eab;
           if (a < in && b < jn) {
@@ -419,7 +518,28 @@ __global__ void __launch_bounds__(EW) k_eig_lds(double* A0, int64_t a_stride, in
           }
         }
         __syncthreads();
+        __shared__ int bigE;
         if (I == J) {
+          if (tid == 0) bigE = 0;
+          __syncthreads();
+          for (int q = tid; q < GB * GB; q += EW) {
+            const int a = q / GB, b = q - a * GB;
+            if (a < jn && b < jn && fabs(E[a * (GB + 1) + b]) > 1e-6) bigE = 1;
+          }
+          __syncthreads();
+        }
+        if (I == J && !bigE) {   // uniform: |E| <= 1e-6, first order (the dropped terms are <= 1e-12)
+          // Q_J[b] <- Q_J[b] - sum_{a < b} E[a][b] Q_J[a] - E[b][b] / 2 Q_J[b]
+          for (int q = tid; q < GB * mp; q += EW) {
+            const int b = q / mp, c = q - b * mp;
+            const double v = QJ[b * mp + c];
+            double corr = 0.5 * E[b * (GB + 1) + b] * v;
+            for (int a = 0; a < b; ++a) corr += E[a * (GB + 1) + b] * QJ[a * mp + c];
+            QI[b * mp + c] = v - corr;
+          }
+          __syncthreads();
+          for (int q = tid; q < GB * mp; q += EW) QJ[q] = QI[q];
+        } else if (I == J) {
           // exact orthonormalisation of the block: G = Q_J Q_J^T = L L^T (wave 0, right-looking, lane c
           // owns row c), Q_J <- L^-1 Q_J.  A pivot below 1/4 (a vector nearly in the span of the
           // block's earlier ones: a numerically multiple eigenvalue T did not split) drops the row;
@@ -515,7 +635,7 @@ __global__ void __launch_bounds__(EW) k_eig_lds(double* A0, int64_t a_stride, in
         double nn = 0.0;
         for (int c = lane; c < m; c += 64) nn += u[c] * u[c];
         nn = riptrm_wave::wave_sum(nn);   // every wave the same
-        if (nn > 1e-2) {   // uniform
+        if (nn > 1e-8) {   // uniform (a unit vector's share of a one-dimensional complement is ~1 / m)
           const double inv = 1.0 / sqrt(nn);
           for (int c = tid; c < m; c += EW) A[(int64_t)t * lda + c] = u[c] * inv;
           __threadfence_block();
@@ -532,6 +652,7 @@ __global__ void __launch_bounds__(EW) k_eig_lds(double* A0, int64_t a_stride, in
     }
     if (tid == 0 && eflag) infos[k] = 2;
   }
+  if (stp) stp[5] = clock64();
 }
 
 }  // namespace riptrm_eig

@@ -30,6 +30,7 @@
 #include <dlfcn.h>
 #include <math.h>
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <string>
@@ -64,9 +65,14 @@ enum Vs : int { VS_W = 0, VS_U, VS_A, VS_CGX, VS_R, VS_P, VS_Q, VS_EV, VS_EW, VS
 
 // one slot for matrices of order N: [N x N][NVS vectors of vpad(N)][NSC scalars]; after the slots:
 // int32 info[slots], ids[slots], flag[8], sweeps[slots], hits[slots] (+ pad), double residual[slots]
-__host__ __device__ inline int64_t slot_doubles(int64_t N) { return N * N + NVS * vpad(N) + NSC; }
+// ... then [the eigensolver's reflectors: riptrm_eig::refl_doubles(N)] (orders it serves)
+__host__ __device__ inline int64_t refl_of(int64_t N) {
+  return N <= riptrm_eig::EIG_LDS_MAX ? (int64_t)riptrm_eig::refl_doubles((int)N) : 0;
+}
+__host__ __device__ inline int64_t slot_doubles(int64_t N) { return N * N + NVS * vpad(N) + NSC + refl_of(N); }
 __host__ __device__ inline int64_t off_vec(int64_t N, int k) { return N * N + k * vpad(N); }
 __host__ __device__ inline int64_t off_sc(int64_t N) { return N * N + NVS * vpad(N); }
+__host__ __device__ inline int64_t off_refl(int64_t N) { return N * N + NVS * vpad(N) + NSC; }
 inline int64_t tail_ints(int64_t slots) { return (4 * slots + 8 + 1) / 2 * 2; }   // even: the doubles stay aligned
 
 // the per-instance eigendecomposition cache (riptrm_trs_bind_cache), order N: [Q: N x N][ev][x key]
@@ -1136,9 +1142,10 @@ static int eig_batched(riptrm_ctx* c, const Bat& B, int cnt, bool vectors, int m
     const size_t shm = riptrm_eig::eig_lds_bytes(m);
     HIPCHK(c, hipFuncSetAttribute((const void*)riptrm_eig::k_eig_lds, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   (int)shm));
+    if (refl_of(B.N) < (int64_t)riptrm_eig::refl_doubles(m)) return fail(c, RIPTRM_E_STATE, "eig: slot too small");
     hipLaunchKernelGGL(riptrm_eig::k_eig_lds, dim3(cnt), dim3(riptrm_eig::EW), shm, c->stream, B.base + aoff, B.sd, lda, m,
                        B.base + off_vec(B.N, VS_EV), B.sd, B.base + off_vec(B.N, VS_R), B.base + off_vec(B.N, VS_EW),
-                       B.base + off_vec(B.N, VS_Q), B.sd, B.infos, vectors ? 1 : 0);
+                       B.base + off_vec(B.N, VS_Q), B.sd, B.base + off_refl(B.N), B.sd, B.infos, vectors ? 1 : 0);
     HIPCHK(c, hipGetLastError());
     return RIPTRM_OK;
   }
@@ -1519,7 +1526,8 @@ int riptrm_sym_eig(riptrm_ctx* ctx, int32_t dim, int32_t batch, double* A, int64
                                        ", batch >= 1, lda >= dim, a_stride >= dim * lda, w_stride >= dim");
   HIPCHK(ctx, hipSetDevice(ctx->device));
   const int64_t sc = riptrm_eig::vpad_eig(dim);
-  const size_t need = (size_t)3 * sc * batch * sizeof(double);
+  const int64_t per = 3 * sc + (int64_t)riptrm_eig::refl_doubles(dim);   // d, e, tau, reflectors
+  const size_t need = (size_t)per * batch * sizeof(double);
   if (ctx->eig_scratch_bytes < need) {
     if (ctx->eig_scratch) HIPCHK(ctx, hipFree(ctx->eig_scratch));
     ctx->eig_scratch = nullptr;
@@ -1530,9 +1538,21 @@ int riptrm_sym_eig(riptrm_ctx* ctx, int32_t dim, int32_t batch, double* A, int64
   double* s = (double*)ctx->eig_scratch;
   const size_t shm = riptrm_eig::eig_lds_bytes(dim);
   HIPCHK(ctx, hipFuncSetAttribute((const void*)riptrm_eig::k_eig_lds, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm));
+  long long* stamps = nullptr;   // RIPTRM_EIG_STAMPS=1: per-phase clocks of matrix 0 on stderr (diagnostics)
+  const bool want_stamps = getenv_is("RIPTRM_EIG_STAMPS", '1');
+  if (want_stamps) HIPCHK(ctx, hipMalloc(&stamps, (size_t)batch * 8 * sizeof(long long)));
   hipLaunchKernelGGL(riptrm_eig::k_eig_lds, dim3(batch), dim3(riptrm_eig::EW), shm, ctx->stream, A, a_stride, (int)lda, dim, w,
-                     w_stride, s, s + sc, s + 2 * sc, 3 * sc, info, vectors ? 1 : 0);
+                     w_stride, s, s + sc, s + 2 * sc, per, s + 3 * sc, per, info, vectors ? 1 : 0, stamps);
   HIPCHK(ctx, hipGetLastError());
+  if (want_stamps) {
+    std::vector<long long> h((size_t)batch * 8);
+    HIPCHK(ctx, hipMemcpyAsync(h.data(), stamps, h.size() * sizeof(long long), hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    (void)hipFree(stamps);
+    const long long* t = h.data();
+    fprintf(stderr, "[eig stamps] m=%d load+tridiag %lld bisect %lld vectors(twisted+backtransform) %lld+%lld orthog %lld total %lld\n",
+            dim, t[1] - t[0], t[2] - t[1], t[3] - t[2], t[4] - t[3], t[5] - t[4], t[5] - t[0]);
+  }
   return RIPTRM_OK;
 }
 
