@@ -21,6 +21,11 @@
 #   stiefel_stamps   in-kernel phase stamps of the Stiefel kernels (tools/stiefel_stamps)
 #   exact            bench.py --trs Exact_RepMat --dim 200 --batch 64    -> bench_exact_200.json
 #   exact_prof       rocprofv3 stats of the same
+#   exact1000        bench.py --trs Exact_RepMat --dim 1000 --batch 1 with its (sampled) CPU baseline
+#   si_pmc           issue-rate PMC pass of k_si (SQ_*) -> profiles/r5_si_pmc.json, read by the si step
+#   si_prof          rocprofv3 stats of the SI bench
+#   si_d8_exact      bench.py --problem si --si-dim 8 --trs Exact_RepMat --batch 64 with its CPU baseline
+#   si_d8_exact_prof rocprofv3 stats of the same
 #   dist2            bench.py --gpus 2 --same-device --backend gloo at the configs[3] per-rank shape
 set -u
 cd "$GRAFT_REPO_ROOT"
@@ -118,9 +123,28 @@ for b in (256, 2048):
       > $O/bench_exact_200.json 2> $O/bench_exact.err || { tail $O/bench_exact.err; return 1; }
     val $O/bench_exact_200.json exact200 ;;
   exact1000)
-    timeout -k 10 600 python bench.py --trs Exact_RepMat --dim 1000 --batch ${EX_B:-1} --steps 3 --warmup 1 --cpu-budget 0 \
-      > $O/bench_exact_1000.json 2> $O/bench_exact1000.err || { tail $O/bench_exact1000.err; return 1; }
+    timeout -k 10 900 python bench.py --trs Exact_RepMat --dim 1000 --batch ${EX_B:-1} --steps 3 --warmup 1 --cpu-budget 120 \
+      --cpu-pool-budget 150 > $O/bench_exact_1000.json 2> $O/bench_exact1000.err || { tail $O/bench_exact1000.err; return 1; }
     val $O/bench_exact_1000.json exact1000 ;;
+  si_pmc)
+    timeout -s KILL 240 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_INSTS_VALU \
+      --output-format csv -d $O/sipmc -o p -- python bench.py --problem si --batch 256 --cpu-budget 0 > $O/sipmc.log 2>&1 \
+      || { tail $O/sipmc.log; return 1; }
+    python scripts/si_pmc_summary.py $(find $O/sipmc -name "*counter_collection.csv" | head -1) $O/r5_si_pmc.json --d 5 \
+      --source "rocprofv3 --pmc SQ_WAVE_CYCLES SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_INSTS_VALU -- python bench.py --problem si --batch 256 --cpu-budget 0 ($O)" \
+      && cp $O/r5_si_pmc.json profiles/ ;;   # the later si step in this call reads it (bench.py --si-pmc-json)
+  si_prof)
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/si -o si -- python bench.py --problem si \
+      --batch 256 --cpu-budget 0 > $O/bench_si_rocprof.json 2> $O/si_rocprof.log || return 1
+    note "si rocprof ok" ;;
+  si_d8_exact)
+    timeout -k 10 900 python bench.py --problem si --si-dim 8 --trs Exact_RepMat --batch 64 --cpu-budget 100 --cpu-pool-budget 150 \
+      > $O/bench_si_d8_exact.json 2> $O/bench_si_d8_exact.err || { tail $O/bench_si_d8_exact.err; return 1; }
+    val $O/bench_si_d8_exact.json si_d8_exact ;;
+  si_d8_exact_prof)
+    timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/sid8 -o sid8 -- python bench.py --problem si \
+      --si-dim 8 --trs Exact_RepMat --batch 64 --cpu-budget 0 > $O/bench_si_d8_rocprof.json 2> $O/sid8_rocprof.log || return 1
+    note "si d8 exact rocprof ok" ;;
   exact_prof)
     timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/exact -o exact -- python bench.py --trs Exact_RepMat \
       --dim 200 --batch 64 --steps 4 --warmup 1 --cpu-budget 0 > $O/bench_exact_rocprof.json 2> $O/exact_rocprof.log || return 1
