@@ -443,9 +443,11 @@ int riptrm_trs_skip_stats(riptrm_ctx* ctx, int64_t* checked, int64_t* skipped);
  * per matrix, the matrix resident in LDS: Householder tridiagonalisation, bisection, twisted
  * factorisations, back-transformation.  batch matrices of order dim (1 <= dim <= 199) at
  * A + k a_stride (leading dimension lda; the lower triangle is read): eigenvalues ascending into
- * w + k w_stride and, with vectors != 0, eigenvector j into row j of the matrix (overwritten).
- * info[k] = 0, or 1 for a non-finite input (its eigenvalues are NaN).  Asynchronous on the
- * context's stream; the context keeps a small scratch (3 dim doubles per matrix). */
+ * w + k w_stride and, with vectors = 1, eigenvector j into row j of the matrix (overwritten);
+ * vectors = 2 leaves the eigenvectors of the tridiagonal form there instead (the compact form the
+ * service keeps, back-transformed per vector; for timing).  info[k] = 0, 1 for a non-finite input
+ * (its eigenvalues are NaN), 2 when the eigenvectors could not be orthonormalised.  Asynchronous on
+ * the context's stream; the context keeps a scratch (2 dim + dim (dim + 1) / 2 doubles per matrix). */
 int riptrm_sym_eig(riptrm_ctx* ctx, int32_t dim, int32_t batch, double* A, int64_t lda, int64_t a_stride, double* w,
                    int64_t w_stride, int32_t* info, int32_t vectors);
 

@@ -47,12 +47,24 @@ __host__ __device__ constexpr int ms_of(int m) { return vpad_eig(m) + 1; }   // 
 __host__ __device__ constexpr size_t smax(size_t a, size_t b) { return a > b ? a : b; }
 // doubles before d / e / tau: the packed triangle (phase 1) or a ZB-vector block + a reflector stage
 __host__ __device__ constexpr size_t de_off(int m) { return smax((size_t)poff(m), (size_t)(ZB + RB) * ms_of(m)); }
+// the reflectors in HBM (vectors != 0): reflector i (v_{i+1} = 1, ..., v_{m-1}) contiguous from
+// refl_col(m, i), then tau from refl_tau(m); m (m + 1) / 2 doubles in all, rounded to 8
+__host__ __device__ constexpr int refl_col(int m, int i) { return i * (m - 1) - i * (i - 1) / 2; }
+__host__ __device__ constexpr int refl_tau(int m) { return m * (m - 1) / 2; }
 __host__ __device__ constexpr size_t refl_doubles(int m) { return ((size_t)poff(m) + 7) / 8 * 8; }
+// tau (phase 4 only): in the triangle's space behind the vector block + stage when that fits (m = 199:
+// the triangle is dead by then), else behind d and e
+__host__ __device__ constexpr size_t tau_off(int m) {
+  return (size_t)(ZB + RB) * ms_of(m) + vpad_eig(m) <= de_off(m) ? (size_t)(ZB + RB) * ms_of(m)
+                                                                   : de_off(m) + 2 * (size_t)vpad_eig(m);
+}
 // dynamic LDS: phases 1-4 (packed triangle or vector block + stage, then d, e, tau), or phase 5
 // (two GB-row blocks + their Gram and its Cholesky inverse)
 __host__ __device__ constexpr size_t eig_lds_bytes(int m) {
-  return smax(de_off(m) + 3 * (size_t)vpad_eig(m), 2 * (size_t)GB * ms_of(m) + 2 * GB * (GB + 1)) * sizeof(double);
+  return smax(smax(de_off(m) + 2 * (size_t)vpad_eig(m), tau_off(m) + vpad_eig(m)),
+              2 * (size_t)GB * ms_of(m) + 2 * GB * (GB + 1)) * sizeof(double);
 }
+static_assert(eig_lds_bytes(EIG_LDS_MAX) <= 160 * 1024, "EIG_LDS_MAX exceeds the LDS");
 
 typedef __attribute__((address_space(3))) double lds_t;
 
@@ -98,20 +110,22 @@ __device__ __forceinline__ int sturm_count(const lds_t* d, const lds_t* e, int m
 }
 
 // Matrix k = blockIdx.x: the m x m symmetric matrix at A0 + k a_stride (leading dimension lda; the
-// lower triangle is read) -> eigenvalues ascending at ev0 + k ev_stride, eigenvectors (vectors != 0)
-// in the rows of the same matrix.  Scratch per matrix (three vectors of >= m doubles, k sc_stride
-// apart): d at d0, e at e0, tau at t0; the reflectors (refl_doubles(m)) at R0 + k r_stride.
+// lower triangle is read) -> eigenvalues ascending at ev0 + k ev_stride and, with vectors, in the
+// rows of the same matrix: vectors = 1 the eigenvectors of A; vectors = 2 those of the tridiagonal
+// T = H^T A H (compact form: an eigenvector of A is H z = H_0 ... H_{m-2} z, applied by the caller,
+// k_refl_apply).  Scratch per matrix (two vectors of >= m doubles, k sc_stride apart): d at d0, e at
+// e0; the reflectors and tau (refl_doubles(m), layout refl_col / refl_tau) at R0 + k r_stride.
 __global__ void __launch_bounds__(EW) k_eig_lds(double* A0, int64_t a_stride, int lda, int m, double* ev0,
-                                                int64_t ev_stride, double* d0, double* e0, double* t0,
-                                                int64_t sc_stride, double* R0, int64_t r_stride, int32_t* infos,
-                                                int vectors, long long* stamps = nullptr) {
+                                                int64_t ev_stride, double* d0, double* e0, int64_t sc_stride,
+                                                double* R0, int64_t r_stride, int32_t* infos, int vectors,
+                                                long long* stamps = nullptr) {
   extern __shared__ double smem[];
   __shared__ double scal[2];
   __shared__ int bad;
   lds_t* P = (lds_t*)smem;                    // packed lower triangle, row i at poff(i)
   lds_t* vb = P + de_off(m);                  // the reflector (phase 1), then d (phases 2-3)
   lds_t* pb = vb + vpad_eig(m);               // p (phase 1), then e (phases 2-3)
-  lds_t* tb = pb + vpad_eig(m);               // tau (phase 4)
+  lds_t* tb = P + tau_off(m);                 // tau (phase 4)
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   constexpr int NW = EW / 64;
   const int k = blockIdx.x;
@@ -119,7 +133,6 @@ __global__ void __launch_bounds__(EW) k_eig_lds(double* A0, int64_t a_stride, in
   double* ev = ev0 + (int64_t)k * ev_stride;
   double* dg = d0 + (int64_t)k * sc_stride;
   double* eg = e0 + (int64_t)k * sc_stride;
-  double* tg = t0 + (int64_t)k * sc_stride;
   double* Rg = R0 + (int64_t)k * r_stride;
   if (tid == 0) bad = 0;
   long long* stp = (stamps && tid == 0) ? stamps + (int64_t)k * 8 : nullptr;   // phase clocks (diagnostics)
@@ -165,12 +178,13 @@ __global__ void __launch_bounds__(EW) k_eig_lds(double* A0, int64_t a_stride, in
           P[poff(i + 1 + l) + i] = v;   // the reflector replaces the column it annihilates
         }
         vb[l] = v;
+        if (vectors) Rg[refl_col(m, i) + l] = v;
       }
       if (lane == 0) {
         scal[0] = tau;
         P[poff(i + 1) + i] = beta;
         eg[i] = beta;
-        tg[i] = tau;
+        if (vectors) Rg[refl_tau(m) + i] = tau;
       }
     }
     __syncthreads();
@@ -246,8 +260,6 @@ __global__ void __launch_bounds__(EW) k_eig_lds(double* A0, int64_t a_stride, in
     __syncthreads();
   }
   if (stp) stp[1] = clock64();
-  if (vectors)   // the reflectors (below the subdiagonal of the packed triangle) for the back-transformation
-    for (int q = tid; q < poff(m); q += EW) Rg[q] = P[q];
   // d, e into LDS (vb, pb) and the slot
   for (int i = tid; i < m; i += EW) {
     const double di = P[poff(i) + i];
@@ -318,7 +330,7 @@ __global__ void __launch_bounds__(EW) k_eig_lds(double* A0, int64_t a_stride, in
   const int ms = ms_of(m);
   lds_t* Zb = P;                 // [ZB][ms]
   lds_t* St = P + ZB * ms;       // [RB][ms]: reflectors i_hi - RB + 1 .. i_hi, v_i[j] dense
-  for (int i = tid; i < m - 1; i += EW) tb[i] = tg[i];
+  for (int i = tid; i < m - 1; i += EW) tb[i] = Rg[refl_tau(m) + i];
   const double delta = 16.0 * eps * tnorm;
   for (int t0 = 0; t0 < m; t0 += ZB) {
     __syncthreads();   // the previous block's rows are out, tau is in
@@ -413,13 +425,13 @@ __global__ void __launch_bounds__(EW) k_eig_lds(double* A0, int64_t a_stride, in
     // lanes per vector (lane c8 takes j = c8, c8 + 8, ...: its own elements only, so the wave needs
     // no LDS ordering between reflectors), the dot product closed by three butterfly steps
     const int u = tid >> 3, c8 = tid & 7;
-    for (int ihi = m - 2; ihi >= 0; ihi -= RB) {
+    for (int ihi = vectors == 1 ? m - 2 : -1; ihi >= 0; ihi -= RB) {
       const int ilo = ihi - RB + 1 > 0 ? ihi - RB + 1 : 0;
       __syncthreads();   // the block's vectors are in; the previous stage is done with
       for (int q = tid; q < (ihi - ilo + 1) * ms; q += EW) {
         const int ii = q / ms, j = q - ii * ms;
         const int i = ilo + ii;
-        St[q] = j == i + 1 ? 1.0 : ((j > i + 1 && j < m) ? Rg[poff(j) + i] : 0.0);
+        St[q] = (j > i && j < m) ? Rg[refl_col(m, i) + j - i - 1] : 0.0;
       }
       __syncthreads();
       if (t0 + u < m) {

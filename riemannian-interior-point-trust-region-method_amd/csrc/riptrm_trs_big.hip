@@ -66,8 +66,9 @@ enum Vs : int { VS_W = 0, VS_U, VS_A, VS_CGX, VS_R, VS_P, VS_Q, VS_EV, VS_EW, VS
 // one slot for matrices of order N: [N x N][NVS vectors of vpad(N)][NSC scalars]; after the slots:
 // int32 info[slots], ids[slots], flag[8], sweeps[slots], hits[slots] (+ pad), double residual[slots]
 // ... then [the eigensolver's reflectors: riptrm_eig::refl_doubles(N)] (orders it serves)
+// (every order m <= min(N, EIG_LDS_MAX) the hand-written eigensolver serves)
 __host__ __device__ inline int64_t refl_of(int64_t N) {
-  return N <= riptrm_eig::EIG_LDS_MAX ? (int64_t)riptrm_eig::refl_doubles((int)N) : 0;
+  return (int64_t)riptrm_eig::refl_doubles((int)(N < riptrm_eig::EIG_LDS_MAX ? N : riptrm_eig::EIG_LDS_MAX));
 }
 __host__ __device__ inline int64_t slot_doubles(int64_t N) { return N * N + NVS * vpad(N) + NSC + refl_of(N); }
 __host__ __device__ inline int64_t off_vec(int64_t N, int k) { return N * N + k * vpad(N); }
@@ -77,7 +78,7 @@ inline int64_t tail_ints(int64_t slots) { return (4 * slots + 8 + 1) / 2 * 2; } 
 
 // the per-instance eigendecomposition cache (riptrm_trs_bind_cache), order N: [Q: N x N][ev][x key]
 // [y key][valid] (vectors vpad(N))
-__host__ __device__ inline int64_t cache_doubles(int64_t N) { return N * N + 3 * vpad(N) + 8; }
+__host__ __device__ inline int64_t cache_doubles(int64_t N) { return N * N + 3 * vpad(N) + 8 + refl_of(N); }
 inline int64_t tail_bytes(int64_t slots) { return tail_ints(slots) * 4 + slots * 8; }
 
 // the slots of one pass: slot k (blockIdx.y) holds instance / subproblem ids[k]
@@ -975,6 +976,51 @@ __global__ void __launch_bounds__(256) k_load(Bat B, int m, const double* A, int
   if (e < m) q.v[VS_A][e] = a[(int64_t)b * ldv + e];
 }
 
+// v <- H^T v = H_{m-2} ... H_0 v (backward = 0) or H v = H_0 ... H_{m-2} v (backward = 1), H the
+// tridiagonalisation's reflectors of the slot's matrix (compact eigenvectors: q_k = H z_k, riptrm_eig.h),
+// from slot offset voff to ooff (may be the same).  One workgroup per slot: the reflectors and tau are
+// staged into LDS by all threads, then one wave runs the m - 1 reflections with v in registers (lane l
+// owns elements l, l + 64, l + 128, l + 192; each dot product in lane order, then the wave tree).
+static_assert(riptrm_eig::EIG_LDS_MAX <= 256, "k_refl_apply holds four elements per lane");
+__global__ void __launch_bounds__(256) k_refl_apply(Bat B, int m, int64_t voff, int64_t ooff, int backward) {
+  extern __shared__ double smem[];
+  riptrm_eig::lds_t* R = (riptrm_eig::lds_t*)smem;
+  double* base = B.base + (int64_t)blockIdx.y * B.sd;
+  const double* Rg = base + off_refl(B.N);
+  const int nt = riptrm_eig::refl_tau(m), nr = nt + m - 1;
+  for (int q = threadIdx.x; q < nr; q += 256) R[q] = Rg[q];
+  __syncthreads();
+  if (threadIdx.x >= 64) return;
+  const int lane = threadIdx.x;
+  double v[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int j = lane + 64 * q;
+    v[q] = j < m ? base[voff + j] : 0.0;
+  }
+  for (int t = 0; t < m - 1; ++t) {
+    const int i = backward ? m - 2 - t : t;
+    const double tau = R[nt + i];
+    if (tau == 0.0) continue;   // uniform
+    const int c = riptrm_eig::refl_col(m, i) - i - 1;   // element j > i of reflector i at c + j
+    double u[4], s = 0.0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int j = lane + 64 * q;
+      u[q] = (j > i && j < m) ? R[c + j] : 0.0;
+      s += u[q] * v[q];
+    }
+    const double f = tau * riptrm_wave::wave_sum(s);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) v[q] = v[q] - f * u[q];
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int j = lane + 64 * q;
+    if (j < m) base[ooff + j] = v[q];
+  }
+}
+
 // ---- the per-instance eigendecomposition cache (riptrm_trs_bind_cache) ------------------------------
 __device__ __forceinline__ double* cache_of(double* cache, int64_t N, int b) { return cache + (int64_t)b * cache_doubles(N); }
 
@@ -993,6 +1039,9 @@ __global__ void __launch_bounds__(256) k_cache_store(DevParams P, Bat B, double*
     C[N * N + 2 * vpad(N) + e] = vec_of(P, V_YNEW, b)[e];
   }
   if (e == 0) C[N * N + 3 * vpad(N)] = *q.info == 0 ? 1.0 : 0.0;
+  // the reflectors of the compact eigenvectors (riptrm_eig.h), when the hand-written solver made them
+  if (n - 1 <= riptrm_eig::EIG_LDS_MAX && e < (int64_t)riptrm_eig::refl_doubles(n - 1))
+    C[N * N + 3 * vpad(N) + 8 + e] = B.base[(int64_t)k * B.sd + off_refl(B.N) + e];
 }
 
 // hits[k] = 1 iff instance ids[k]'s cache entry is valid and was taken at exactly this (x, y): then
@@ -1018,6 +1067,8 @@ __global__ void __launch_bounds__(256) k_cache_load(DevParams P, Bat B, const do
   const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (e < (int64_t)n * n) q.M[e] = C[e];
   if (e < n - 1) q.v[VS_EV][e] = C[N * N + e];
+  if (n - 1 <= riptrm_eig::EIG_LDS_MAX && e < (int64_t)riptrm_eig::refl_doubles(n - 1))
+    B.base[(int64_t)k * B.sd + off_refl(B.N) + e] = C[N * N + 3 * vpad(N) + 8 + e];
   if (e == 0) *q.info = 0;
 }
 
@@ -1134,18 +1185,32 @@ static int32_t* flag_of(riptrm_ctx* c) { return tail_of(c) + 2 * c->big_slots; }
 // A = Q diag(lam) Q^T for the pass's cnt slots (A at slot offset aoff, lda; eigenvalues ascending into
 // VS_EV, eigenvectors over A when vectors): rocSOLVER dsyevd (default) or, for A/B measurements
 // (RIPTRM_BIG_EIG=j / dj), its Jacobi dsyevj / dsyevdj
+// the hand-written eigensolver serves order m (riptrm_eig.h; RIPTRM_BIG_EIG=r, or j / dj / s, keeps
+// rocSOLVER for A/B measurements): its eigenvectors are compact (those of the tridiagonal form over
+// the matrix, the reflectors in the slot), applied through k_refl_apply
+static bool eig_compact(int m) {
+  const char* e = getenv("RIPTRM_BIG_EIG");
+  return m <= riptrm_eig::EIG_LDS_MAX && !(e && e[0] != 'h');
+}
+
+static int refl_apply(riptrm_ctx* c, const Bat& B, int cnt, int m, int64_t voff, int64_t ooff, int backward) {
+  const size_t shm = (size_t)(riptrm_eig::refl_tau(m) + m) * sizeof(double);
+  HIPCHK(c, hipFuncSetAttribute((const void*)k_refl_apply, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm));
+  hipLaunchKernelGGL(k_refl_apply, dim3(1, cnt), dim3(256), shm, c->stream, B, m, voff, ooff, backward);
+  HIPCHK(c, hipGetLastError());
+  return RIPTRM_OK;
+}
+
 static int eig_batched(riptrm_ctx* c, const Bat& B, int cnt, bool vectors, int m, int64_t aoff, int lda) {
   const char* e = getenv("RIPTRM_BIG_EIG");
-  if (m <= riptrm_eig::EIG_LDS_MAX && !(e && e[0] != 'h')) {
-    // hand-written: one workgroup per matrix, the matrix in LDS (riptrm_eig.h); RIPTRM_BIG_EIG=r (or
-    // j / dj / s) keeps rocSOLVER for A/B
+  if (eig_compact(m)) {
+    // hand-written: one workgroup per matrix, the matrix in LDS
     const size_t shm = riptrm_eig::eig_lds_bytes(m);
     HIPCHK(c, hipFuncSetAttribute((const void*)riptrm_eig::k_eig_lds, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   (int)shm));
-    if (refl_of(B.N) < (int64_t)riptrm_eig::refl_doubles(m)) return fail(c, RIPTRM_E_STATE, "eig: slot too small");
     hipLaunchKernelGGL(riptrm_eig::k_eig_lds, dim3(cnt), dim3(riptrm_eig::EW), shm, c->stream, B.base + aoff, B.sd, lda, m,
-                       B.base + off_vec(B.N, VS_EV), B.sd, B.base + off_vec(B.N, VS_R), B.base + off_vec(B.N, VS_EW),
-                       B.base + off_vec(B.N, VS_Q), B.sd, B.base + off_refl(B.N), B.sd, B.infos, vectors ? 1 : 0);
+                       B.base + off_vec(B.N, VS_EV), B.sd, B.base + off_vec(B.N, VS_R), B.base + off_vec(B.N, VS_EW), B.sd,
+                       B.base + off_refl(B.N), B.sd, B.infos, vectors ? 2 : 0);
     HIPCHK(c, hipGetLastError());
     return RIPTRM_OK;
   }
@@ -1247,12 +1312,18 @@ static int big_after_eig(riptrm_ctx* c, const Bat& B, int cnt, int64_t aoff, int
   hipStream_t st = c->stream;
   const int64_t N = B.N;
   const dim3 one(1, cnt), rows(blocks_of(m, GV / 64), cnt);
-  // eigenvector k = row k of the row-major view (column k of dsyevd's column-major output)
-  hipLaunchKernelGGL(k_gemv, rows, dim3(GV), 0, st, B, aoff, (int64_t)lda, m, m, off_vec(N, VS_A), off_vec(N, VS_G),
-                     (int64_t)-1);
+  // eigenvector k = row k of the row-major view (column k of dsyevd's column-major output); compact:
+  // Q^T a = Z^T (H^T a), Q y = H (Z y)
+  const bool cpt = eig_compact(m);
+  if (cpt)
+    if (int rc = refl_apply(c, B, cnt, m, off_vec(N, VS_A), off_vec(N, VS_PE), 0)) return rc;
+  hipLaunchKernelGGL(k_gemv, rows, dim3(GV), 0, st, B, aoff, (int64_t)lda, m, m, off_vec(N, cpt ? VS_PE : VS_A),
+                     off_vec(N, VS_G), (int64_t)-1);
   hipLaunchKernelGGL(k_secular, one, dim3(WG), 0, st, B, m, tolhc);
   hipLaunchKernelGGL(k_gemv_t, dim3(blocks_of(m, 256), cnt), dim3(256), 0, st, B, aoff, (int64_t)lda, m, m,
                      off_vec(N, VS_PE), off_vec(N, VS_X));
+  if (cpt)
+    if (int rc = refl_apply(c, B, cnt, m, off_vec(N, VS_X), off_vec(N, VS_X), 1)) return rc;
   hipLaunchKernelGGL(k_pick, dim3(blocks_of(m, 256), cnt), dim3(256), 0, st, B, m);
   HIPCHK(c, hipGetLastError());
   return RIPTRM_OK;
@@ -1410,8 +1481,11 @@ int riptrm_big_gep_ids(riptrm_ctx* c, int dim, const int32_t* sel, int count, co
       if (int rc = eig_batched(c, Bt, cnt, true, dim, 0, dim)) return rc;
       hipStream_t st = c->stream;
       const int64_t N = Bt.N;
+      const bool cpt = eig_compact(dim);
+      if (cpt)
+        if (int rc = refl_apply(c, Bt, cnt, dim, off_vec(N, VS_A), off_vec(N, VS_PE), 0)) return rc;
       hipLaunchKernelGGL(k_gemv, dim3(blocks_of(dim, GV / 64), cnt), dim3(GV), 0, st, Bt, (int64_t)0, (int64_t)dim, dim,
-                         dim, off_vec(N, VS_A), off_vec(N, VS_G), (int64_t)-1);
+                         dim, off_vec(N, cpt ? VS_PE : VS_A), off_vec(N, VS_G), (int64_t)-1);
       hipLaunchKernelGGL(k_set_delta, dim3(blocks_of(cnt, 64)), dim3(64), 0, st, Bt, cnt, Delta, (int64_t)1);
       hipLaunchKernelGGL(k_secular, dim3(1, cnt), dim3(WG), 0, st, Bt, dim, tolhc, 0);
       if (dim <= CGW_MAX && !getenv_is("RIPTRM_CG_WAVE", '0')) {
@@ -1433,6 +1507,8 @@ int riptrm_big_gep_ids(riptrm_ctx* c, int dim, const int32_t* sel, int count, co
       hipLaunchKernelGGL(k_choose, dim3(blocks_of(cnt, 64)), dim3(64), 0, st, Bt, cnt);
       hipLaunchKernelGGL(k_gemv_t, dim3(blocks_of(dim, 256), cnt), dim3(256), 0, st, Bt, (int64_t)0, (int64_t)dim, dim, dim,
                          off_vec(N, VS_PE), off_vec(N, VS_X));
+      if (cpt)
+        if (int rc = refl_apply(c, Bt, cnt, dim, off_vec(N, VS_X), off_vec(N, VS_X), 1)) return rc;
       hipLaunchKernelGGL(k_pick, dim3(blocks_of(dim, 256), cnt), dim3(256), 0, st, Bt, dim);
       HIPCHK(c, hipGetLastError());
     } else if (int rc = big_solve(c, Bt, cnt, 0, dim, dim, Delta, 1, tolhc)) {
@@ -1526,7 +1602,7 @@ int riptrm_sym_eig(riptrm_ctx* ctx, int32_t dim, int32_t batch, double* A, int64
                                        ", batch >= 1, lda >= dim, a_stride >= dim * lda, w_stride >= dim");
   HIPCHK(ctx, hipSetDevice(ctx->device));
   const int64_t sc = riptrm_eig::vpad_eig(dim);
-  const int64_t per = 3 * sc + (int64_t)riptrm_eig::refl_doubles(dim);   // d, e, tau, reflectors
+  const int64_t per = 2 * sc + (int64_t)riptrm_eig::refl_doubles(dim);   // d, e, reflectors + tau
   const size_t need = (size_t)per * batch * sizeof(double);
   if (ctx->eig_scratch_bytes < need) {
     if (ctx->eig_scratch) HIPCHK(ctx, hipFree(ctx->eig_scratch));
@@ -1542,7 +1618,7 @@ int riptrm_sym_eig(riptrm_ctx* ctx, int32_t dim, int32_t batch, double* A, int64
   const bool want_stamps = getenv_is("RIPTRM_EIG_STAMPS", '1');
   if (want_stamps) HIPCHK(ctx, hipMalloc(&stamps, (size_t)batch * 8 * sizeof(long long)));
   hipLaunchKernelGGL(riptrm_eig::k_eig_lds, dim3(batch), dim3(riptrm_eig::EW), shm, ctx->stream, A, a_stride, (int)lda, dim, w,
-                     w_stride, s, s + sc, s + 2 * sc, per, s + 3 * sc, per, info, vectors ? 1 : 0, stamps);
+                     w_stride, s, s + sc, per, s + 2 * sc, per, info, vectors == 2 ? 2 : (vectors ? 1 : 0), stamps);
   HIPCHK(ctx, hipGetLastError());
   if (want_stamps) {
     std::vector<long long> h((size_t)batch * 8);

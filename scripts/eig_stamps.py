@@ -26,11 +26,19 @@ def main():
             D += np.diag(np.where(rs.rand(m) < 0.3, 10.0 ** rs.uniform(2, 6, m), 0.0))
         mats.append(D)
     A = torch.tensor(np.stack(mats), dtype=torch.float64, device="cuda")
-    for kind in ("vectors", "values"):
+    import ctypes
+    ctx = trs._context(A.device)
+    V = A.clone()
+    w = torch.empty((B, m), dtype=torch.float64, device=A.device)
+    info = torch.empty(B, dtype=torch.int32, device=A.device)
+    p = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    # vectors 1: eigenvectors of A; 2: of the tridiagonal form (the service's compact eigenvectors)
+    for kind, mode in (("vectors", 1), ("compact", 2), ("values", 0)):
         for _ in range(3):
+            V.copy_(A)
             torch.cuda.synchronize()
             t0 = time.perf_counter()
-            trs.sym_eig(A, vectors=kind == "vectors")
+            ctx.check(ctx.lib.riptrm_sym_eig(ctx.h, m, B, p(V), m, m * m, p(w), m, p(info), mode), "riptrm_sym_eig")
             torch.cuda.synchronize()
             print(f"{kind}: m={m} batch={B} {1e3 * (time.perf_counter() - t0):.3f} ms", flush=True)
 
