@@ -34,7 +34,7 @@ namespace riptrm_eig {
 
 #pragma clang fp contract(off)
 
-constexpr int EW = 512;                    // threads per matrix
+constexpr int EW = 512;                    // threads per matrix (the default; k_eig_lds<TW> takes 512 or 1024)
 constexpr int EIG_LDS_MAX = 199;           // packed lower triangle + two vectors fit 160 KiB
 constexpr int EIG_MAX_M = 256;             // four elements per lane in the back-transformation
 
@@ -45,8 +45,17 @@ constexpr int ZB = 64;                     // eigenvectors per block of the twis
 constexpr int RB = 16;                     // reflectors staged in LDS at a time
 __host__ __device__ constexpr int ms_of(int m) { return vpad_eig(m) + 1; }   // odd LDS row stride
 __host__ __device__ constexpr size_t smax(size_t a, size_t b) { return a > b ? a : b; }
-// doubles before d / e / tau: the packed triangle (phase 1) or a ZB-vector block + a reflector stage
-__host__ __device__ constexpr size_t de_off(int m) { return smax((size_t)poff(m), (size_t)(ZB + RB) * ms_of(m)); }
+// compact eigenvectors (vectors = 2, no back-transformation): blocks of zc_of(m) vectors, row stride
+// msc_of(m) (odd), as many as fit beside d and e
+__host__ __device__ constexpr int msc_of(int m) { return m | 1; }
+__host__ __device__ constexpr int zc_of(int m) {
+  return m < (20480 - 2 * vpad_eig(m) - 16) / msc_of(m) ? m : (20480 - 2 * vpad_eig(m) - 16) / msc_of(m);
+}
+// doubles before d / e / tau: the packed triangle (phase 1), a ZB-vector block + a reflector stage
+// (vectors = 1) or a zc-vector block (vectors = 2)
+__host__ __device__ constexpr size_t de_off(int m) {
+  return smax(smax((size_t)poff(m), (size_t)(ZB + RB) * ms_of(m)), (size_t)zc_of(m) * msc_of(m));
+}
 // the reflectors in HBM (vectors != 0): reflector i (v_{i+1} = 1, ..., v_{m-1}) contiguous from
 // refl_col(m, i), then tau from refl_tau(m); m (m + 1) / 2 doubles in all, rounded to 8
 __host__ __device__ constexpr int refl_col(int m, int i) { return i * (m - 1) - i * (i - 1) / 2; }
@@ -77,36 +86,129 @@ __device__ __forceinline__ double rcp_nr(double q) {
   return fma(r, t, r);
 }
 
-// the number of eigenvalues of T (diagonal d, off-diagonal e) below x (Sturm count, LAPACK dlaneg's
-// recurrence with pivmin guarding zero pivots)
+// the number of eigenvalues of T (diagonal d, off-diagonal e; split where e_j = 0) below x: the sign
+// changes of p_j = det(T_{0..j} - x I) = (d_j - x) p_{j-1} - e_{j-1}^2 p_{j-2} (a new block restarts
+// at p = 1), i.e. the negative pivots q_j = p_j / p_{j-1} of LAPACK dlaneg's recurrence, with its guard:
+// |q_j| < pivmin counts as q_j = -pivmin.  No division on the dependent chain (a multiply and an FMA per
+// step); p_{j-1}, p_j are rescaled by a power of two every four steps (|d_j - x| <= 4 ||T|| per step; the larger to ~1).
+__device__ __forceinline__ void sturm_step(double dx, double f, double& p0, double& p1, int& c, double pivmin) {
+  double pn = fma(-(f * f), p0, dx * p1);
+  double pv = p1;
+  if (f == 0.0) {   // a new block of the split T
+    pn = dx;
+    pv = 1.0;
+  }
+  if (pn == 0.0 || fabs(pn) < pivmin * fabs(pv)) pn = -(pivmin * pv);   // (may underflow to a signed zero)
+  c += signbit(pn) != signbit(pv);
+  p0 = pv;
+  p1 = pn;
+}
 __device__ __forceinline__ int sturm_count(const lds_t* d, const lds_t* e, int m, double x, double pivmin) {
-  double q = d[0] - x;
-  if (fabs(q) < pivmin) q = -pivmin;
-  int c = q < 0.0;
+  double p0 = 1.0, p1 = d[0] - x;
+  if (p1 == 0.0 || fabs(p1) < pivmin) p1 = -pivmin;
+  int c = signbit(p1) ? 1 : 0;
   int j = 1;
   for (; j + 3 < m; j += 4) {   // the next four entries' loads issued ahead of the dependent chain
-    const double d0 = d[j], d1 = d[j + 1], d2 = d[j + 2], d3 = d[j + 3];
+    const double d0 = d[j] - x, d1 = d[j + 1] - x, d2 = d[j + 2] - x, d3 = d[j + 3] - x;
     const double f0 = e[j - 1], f1 = e[j], f2 = e[j + 1], f3 = e[j + 2];
-    q = (d0 - x) - (f0 * f0) * rcp_nr(q);
-    if (fabs(q) < pivmin) q = -pivmin;
-    c += q < 0.0;
-    q = (d1 - x) - (f1 * f1) * rcp_nr(q);
-    if (fabs(q) < pivmin) q = -pivmin;
-    c += q < 0.0;
-    q = (d2 - x) - (f2 * f2) * rcp_nr(q);
-    if (fabs(q) < pivmin) q = -pivmin;
-    c += q < 0.0;
-    q = (d3 - x) - (f3 * f3) * rcp_nr(q);
-    if (fabs(q) < pivmin) q = -pivmin;
-    c += q < 0.0;
+    sturm_step(d0, f0, p0, p1, c, pivmin);
+    sturm_step(d1, f1, p0, p1, c, pivmin);
+    sturm_step(d2, f2, p0, p1, c, pivmin);
+    sturm_step(d3, f3, p0, p1, c, pivmin);
+    int ex;   // the larger of the two to ~1 (a signed-zero or subnormal p_j keeps its sign)
+    (void)frexp(fmax(fabs(p0), fabs(p1)), &ex);
+    p0 = ldexp(p0, -ex);
+    p1 = ldexp(p1, -ex);
   }
-  for (; j < m; ++j) {
-    const double ej = e[j - 1];
-    q = (d[j] - x) - (ej * ej) * rcp_nr(q);
-    if (fabs(q) < pivmin) q = -pivmin;
-    c += q < 0.0;
-  }
+  for (; j < m; ++j) sturm_step(d[j] - x, e[j - 1], p0, p1, c, pivmin);
   return c;
+}
+
+// The eigenvector of T (d, e; split where e_j = 0) for eigenvalue t (lt = ev[t], ev ascending) into
+// Z[0 .. m): the twisted factorisation of T - lt I (LAPACK dlar1v's), z_r = 1 at the twist r where
+// |gamma_r| is least.  Numerically equal eigenvalues (within delta) take distinct blocks of the split T:
+// member kk of the run i0 .. t takes the block where the running count of block eigenvalues in
+// [lt - delta, lt + delta] passes kk.  Passes: forward (the Sturm counts at lt -+ delta and D+, which
+// restarts at every split: three independent chains), backward over the block (D- and gamma; D- over
+// D+), forward again below the twist (D+), then the solve outward from r and the normalisation.
+__device__ __forceinline__ void twisted_vector(lds_t* Z, const lds_t* d, const lds_t* e, const double* ev, int m, int t,
+                                               double delta, double pivmin) {
+  const double lt = ev[t];
+  int i0 = t;
+  while (i0 > 0 && lt - ev[i0 - 1] <= delta) --i0;
+  const int kk = t - i0;
+  const double xa = lt - delta, xb = lt + delta;
+  int blo = 0, bhi = m - 1, acc = 0, bs = 0, ca = 0, cb = 0;
+  bool found = false;
+  double qa = 0.0, qb = 0.0, dp = 0.0;
+  for (int j = 0; j < m; ++j) {
+    const bool start = j == bs;
+    const double dj = d[j];
+    const double ej2 = start ? 0.0 : e[j - 1] * e[j - 1];
+    qa = (dj - xa) - (start ? 0.0 : ej2 * rcp_nr(qa));
+    qb = (dj - xb) - (start ? 0.0 : ej2 * rcp_nr(qb));
+    dp = (dj - lt) - (start ? 0.0 : ej2 * rcp_nr(dp));
+    if (fabs(qa) < pivmin) qa = -pivmin;
+    if (fabs(qb) < pivmin) qb = -pivmin;
+    if (fabs(dp) < pivmin) dp = -pivmin;
+    Z[j] = dp;
+    ca += qa < 0.0;
+    cb += qb < 0.0;
+    if (j == m - 1 || e[j] == 0.0) {   // block bs .. j ends
+      if (!found && acc + (cb - ca) > kk) {
+        found = true;
+        blo = bs;
+        bhi = j;
+      }
+      acc += cb - ca;
+      ca = cb = 0;
+      bs = j + 1;
+    }
+  }
+  // gamma_j = D+_j + D-_j - (d_j - lt); gamma_bhi = D+_bhi
+  double dm = d[bhi] - lt;
+  if (fabs(dm) < pivmin) dm = -pivmin;
+  double best = fabs(Z[bhi]);
+  int r = bhi;
+  Z[bhi] = dm;
+  for (int j = bhi - 1; j >= blo; --j) {
+    const double ej = e[j];
+    const double djl = d[j] - lt;
+    dm = djl - (ej * ej) * rcp_nr(dm);
+    if (fabs(dm) < pivmin) dm = -pivmin;
+    const double g = fabs(Z[j] + dm - djl);
+    Z[j] = dm;
+    if (g < best) {
+      best = g;
+      r = j;
+    }
+  }
+  if (r > blo) {   // D+ below the twist
+    dp = d[blo] - lt;
+    if (fabs(dp) < pivmin) dp = -pivmin;
+    Z[blo] = dp;
+    for (int j = blo + 1; j < r; ++j) {
+      const double ej = e[j - 1];
+      dp = (d[j] - lt) - (ej * ej) * rcp_nr(dp);
+      if (fabs(dp) < pivmin) dp = -pivmin;
+      Z[j] = dp;
+    }
+  }
+  double z = 1.0, nrm = 1.0;
+  for (int j = r + 1; j <= bhi; ++j) {   // z_j = -(e_{j-1} / D-_j) z_{j-1}
+    z = -(e[j - 1] / Z[j]) * z;
+    Z[j] = z;
+    nrm += z * z;
+  }
+  z = 1.0;
+  for (int j = r - 1; j >= blo; --j) {   // z_j = -(e_j / D+_j) z_{j+1}
+    z = -(e[j] / Z[j]) * z;
+    Z[j] = z;
+    nrm += z * z;
+  }
+  Z[r] = 1.0;
+  const double inv = 1.0 / sqrt(nrm);
+  for (int j = 0; j < m; ++j) Z[j] = (j < blo || j > bhi) ? 0.0 : Z[j] * inv;
 }
 
 // Matrix k = blockIdx.x: the m x m symmetric matrix at A0 + k a_stride (leading dimension lda; the
@@ -115,10 +217,13 @@ __device__ __forceinline__ int sturm_count(const lds_t* d, const lds_t* e, int m
 // T = H^T A H (compact form: an eigenvector of A is H z = H_0 ... H_{m-2} z, applied by the caller,
 // k_refl_apply).  Scratch per matrix (two vectors of >= m doubles, k sc_stride apart): d at d0, e at
 // e0; the reflectors and tau (refl_doubles(m), layout refl_col / refl_tau) at R0 + k r_stride.
-__global__ void __launch_bounds__(EW) k_eig_lds(double* A0, int64_t a_stride, int lda, int m, double* ev0,
+template <int TW>
+__global__ void __launch_bounds__(TW) k_eig_lds(double* A0, int64_t a_stride, int lda, int m, double* ev0,
                                                 int64_t ev_stride, double* d0, double* e0, int64_t sc_stride,
                                                 double* R0, int64_t r_stride, int32_t* infos, int vectors,
                                                 long long* stamps = nullptr) {
+  constexpr int EW = TW;
+  static_assert(TW == 512 || TW == 1024, "k_eig_lds: 512 or 1024 threads");
   extern __shared__ double smem[];
   __shared__ double scal[2];
   __shared__ int bad;
@@ -190,12 +295,13 @@ __global__ void __launch_bounds__(EW) k_eig_lds(double* A0, int64_t a_stride, in
     __syncthreads();
     const double tau = scal[0];
     if (tau != 0.0) {   // uniform
-      // p = tau A22 v: two threads per row (r <= 256), each over half the row -- its part of the
-      // packed row (contiguous) and, past the diagonal, its part of the column below the diagonal
-      // (an incremental offset, no multiplies) -- then the partner's half (lane ^ 1: a + b on both)
+      // p = tau A22 v: TPR = EW / 256 threads per row (r <= 256), each over a part of the row -- its
+      // part of the packed row (contiguous) and, past the diagonal, its part of the column below the
+      // diagonal (an incremental offset, no multiplies) -- then the partners' parts (DPP xor 1, 2)
       {
-        const int l = tid >> 1, h = tid & 1;
-        const int half = (r + 1) >> 1;
+        constexpr int TPR = EW / 256;
+        const int l = tid / TPR, h = tid % TPR;
+        const int half = (r + TPR - 1) / TPR;
         double acc0 = 0.0, acc1 = 0.0;
         if (l < r) {
           const int gl = i + 1 + l;
@@ -231,6 +337,7 @@ __global__ void __launch_bounds__(EW) k_eig_lds(double* A0, int64_t a_stride, in
         }
         double acc = acc0 + acc1;
         acc = acc + riptrm_wave::dpp<riptrm_wave::DPP_XOR1>(acc);
+        if (TPR == 4) acc = acc + riptrm_wave::dpp<riptrm_wave::DPP_XOR2>(acc);
         if (l < r && h == 0) pb[l] = tau * acc;
       }
       __syncthreads();
@@ -326,101 +433,20 @@ __global__ void __launch_bounds__(EW) k_eig_lds(double* A0, int64_t a_stride, in
   if (stp) stp[2] = clock64();
   if (!vectors) return;
 
-  // ---- 3 + 4. per block of ZB eigenvectors, in LDS: the twisted vectors of T, then q = H_0 ... H_{m-2} z
+  // ---- 3 + 4. per block of eigenvectors, in LDS: the twisted vectors of T, then (vectors = 1)
+  // q = H_0 ... H_{m-2} z
   const int ms = ms_of(m);
-  lds_t* Zb = P;                 // [ZB][ms]
-  lds_t* St = P + ZB * ms;       // [RB][ms]: reflectors i_hi - RB + 1 .. i_hi, v_i[j] dense
-  for (int i = tid; i < m - 1; i += EW) tb[i] = Rg[refl_tau(m) + i];
+  const bool cpt = vectors == 2;
+  const int zs = cpt ? msc_of(m) : ms;   // row stride of the block
+  const int zb = cpt ? zc_of(m) : ZB;    // vectors per block
+  lds_t* Zb = P;                         // [zb][zs]
+  lds_t* St = P + ZB * ms;               // [RB][ms]: reflectors i_hi - RB + 1 .. i_hi, v_i[j] dense
+  if (!cpt)
+    for (int i = tid; i < m - 1; i += EW) tb[i] = Rg[refl_tau(m) + i];
   const double delta = 16.0 * eps * tnorm;
-  for (int t0 = 0; t0 < m; t0 += ZB) {
+  for (int t0 = 0; t0 < m; t0 += zb) {
     __syncthreads();   // the previous block's rows are out, tau is in
-    if (tid < ZB && t0 + tid < m) {
-      const int t = t0 + tid;
-      const double lt = ev[t];
-      lds_t* Z = Zb + tid * ms;
-      const double tiny = pivmin;
-      // numerically equal eigenvalues (within delta) take distinct blocks of the split T: member kk
-      // of the run i0 .. takes the block where the running count of block eigenvalues in
-      // [lt - delta, lt + delta] passes kk (per-block Sturm counts at both ends)
-      int i0 = t;
-      while (i0 > 0 && lt - ev[i0 - 1] <= delta) --i0;
-      const int kk = t - i0;
-      int blo = 0, bhi = m - 1, acc = 0, bs = 0, ca = 0, cb = 0;
-      bool found = false;
-      double qa = 0.0, qb = 0.0;
-      for (int j = 0; j < m; ++j) {
-        const bool start = j == bs;
-        const double ej2 = start ? 0.0 : e[j - 1] * e[j - 1];
-        qa = (d[j] - (lt - delta)) - (start ? 0.0 : ej2 / qa);
-        if (fabs(qa) < pivmin) qa = -pivmin;
-        qb = (d[j] - (lt + delta)) - (start ? 0.0 : ej2 / qb);
-        if (fabs(qb) < pivmin) qb = -pivmin;
-        ca += qa < 0.0;
-        cb += qb < 0.0;
-        if (j == m - 1 || e[j] == 0.0) {   // block bs .. j ends
-          if (!found && acc + (cb - ca) > kk) {
-            found = true;
-            blo = bs;
-            bhi = j;
-          }
-          acc += cb - ca;
-          ca = cb = 0;
-          bs = j + 1;
-        }
-      }
-      for (int j = 0; j < blo; ++j) Z[j] = 0.0;
-      for (int j = bhi + 1; j < m; ++j) Z[j] = 0.0;
-      double dp = d[blo] - lt;
-      if (fabs(dp) < tiny) dp = -tiny;
-      Z[blo] = dp;   // D+_j (LDL^T of T - lt I on the block)
-      for (int j = blo + 1; j <= bhi; ++j) {
-        const double ej = e[j - 1];
-        dp = (d[j] - lt) - (ej * ej) / dp;
-        if (fabs(dp) < tiny) dp = -tiny;
-        Z[j] = dp;
-      }
-      // UDU^T from the block's bottom; gamma_j = D+_j + D-_j - (d_j - lt), the twist at min |gamma|
-      double dm = d[bhi] - lt;
-      if (fabs(dm) < tiny) dm = -tiny;
-      double best = fabs(Z[bhi]);
-      int r = bhi;
-      for (int j = bhi - 1; j >= blo; --j) {
-        const double ej = e[j];
-        dm = (d[j] - lt) - (ej * ej) / dm;
-        if (fabs(dm) < tiny) dm = -tiny;
-        const double g = fabs(Z[j] + dm - (d[j] - lt));
-        if (g < best) {
-          best = g;
-          r = j;
-        }
-      }
-      // D-_j for j > r into the row (D+ is kept below the twist)
-      dm = d[bhi] - lt;
-      if (fabs(dm) < tiny) dm = -tiny;
-      for (int j = bhi; j > r; --j) {
-        if (j < bhi) {
-          const double ej = e[j];
-          dm = (d[j] - lt) - (ej * ej) / dm;
-          if (fabs(dm) < tiny) dm = -tiny;
-        }
-        Z[j] = dm;
-      }
-      double z = 1.0, nrm = 1.0;
-      for (int j = r + 1; j <= bhi; ++j) {   // z_j = -(e_{j-1} / D-_j) z_{j-1}
-        z = -(e[j - 1] / Z[j]) * z;
-        Z[j] = z;
-        nrm += z * z;
-      }
-      z = 1.0;
-      for (int j = r - 1; j >= blo; --j) {  // z_j = -(e_j / D+_j) z_{j+1}
-        z = -(e[j] / Z[j]) * z;
-        Z[j] = z;
-        nrm += z * z;
-      }
-      Z[r] = 1.0;
-      const double inv = 1.0 / sqrt(nrm);
-      for (int j = blo; j <= bhi; ++j) Z[j] = Z[j] * inv;
-    }
+    if (tid < zb && t0 + tid < m) twisted_vector(Zb + tid * zs, d, e, ev, m, t0 + tid, delta, pivmin);
     // back-transformation of the block: reflectors i = m - 2 .. 0, RB at a time staged from Rg; eight
     // lanes per vector (lane c8 takes j = c8, c8 + 8, ...: its own elements only, so the wave needs
     // no LDS ordering between reflectors), the dot product closed by three butterfly steps
@@ -434,8 +460,8 @@ __global__ void __launch_bounds__(EW) k_eig_lds(double* A0, int64_t a_stride, in
         St[q] = (j > i && j < m) ? Rg[refl_col(m, i) + j - i - 1] : 0.0;
       }
       __syncthreads();
-      if (t0 + u < m) {
-        lds_t* Zu = Zb + u * ms;
+      if (u < ZB && t0 + u < m) {   // (1024 threads: the upper half idles)
+        lds_t* Zu = Zb + u * zs;
         for (int i = ihi; i >= ilo; --i) {
           const double tau = tb[i];
           if (tau == 0.0) continue;   // uniform
@@ -458,9 +484,9 @@ __global__ void __launch_bounds__(EW) k_eig_lds(double* A0, int64_t a_stride, in
       }
     }
     __syncthreads();
-    for (int q = tid; q < ZB * m; q += EW) {
+    for (int q = tid; q < zb * m; q += EW) {
       const int uu = q / m, c = q - uu * m;
-      if (t0 + uu < m) A[(int64_t)(t0 + uu) * lda + c] = Zb[uu * ms + c];
+      if (t0 + uu < m) A[(int64_t)(t0 + uu) * lda + c] = Zb[uu * zs + c];
     }
   }
   __threadfence_block();

@@ -1201,18 +1201,34 @@ static int refl_apply(riptrm_ctx* c, const Bat& B, int cnt, int m, int64_t voff,
   return RIPTRM_OK;
 }
 
+// k_eig_lds with 1024 threads per matrix (16 waves: the symv and rank-2 update of the
+// tridiagonalisation hide more LDS latency), or 512 (RIPTRM_EIG_THREADS=512, A/B)
+static int launch_eig(riptrm_ctx* c, int cnt, int m, double* A, int64_t a_stride, int lda, double* ev, int64_t ev_stride,
+                      double* d, double* e, int64_t sc_stride, double* R, int64_t r_stride, int32_t* infos, int vectors,
+                      long long* stamps) {
+  const size_t shm = riptrm_eig::eig_lds_bytes(m);
+  const char* t = getenv("RIPTRM_EIG_THREADS");
+  if (!(t && atoi(t) == 512)) {
+    HIPCHK(c, hipFuncSetAttribute((const void*)riptrm_eig::k_eig_lds<1024>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)shm));
+    hipLaunchKernelGGL(riptrm_eig::k_eig_lds<1024>, dim3(cnt), dim3(1024), shm, c->stream, A, a_stride, lda, m, ev, ev_stride,
+                       d, e, sc_stride, R, r_stride, infos, vectors, stamps);
+  } else {
+    HIPCHK(c, hipFuncSetAttribute((const void*)riptrm_eig::k_eig_lds<512>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)shm));
+    hipLaunchKernelGGL(riptrm_eig::k_eig_lds<512>, dim3(cnt), dim3(512), shm, c->stream, A, a_stride, lda, m, ev, ev_stride,
+                       d, e, sc_stride, R, r_stride, infos, vectors, stamps);
+  }
+  HIPCHK(c, hipGetLastError());
+  return RIPTRM_OK;
+}
+
 static int eig_batched(riptrm_ctx* c, const Bat& B, int cnt, bool vectors, int m, int64_t aoff, int lda) {
   const char* e = getenv("RIPTRM_BIG_EIG");
   if (eig_compact(m)) {
     // hand-written: one workgroup per matrix, the matrix in LDS
-    const size_t shm = riptrm_eig::eig_lds_bytes(m);
-    HIPCHK(c, hipFuncSetAttribute((const void*)riptrm_eig::k_eig_lds, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)shm));
-    hipLaunchKernelGGL(riptrm_eig::k_eig_lds, dim3(cnt), dim3(riptrm_eig::EW), shm, c->stream, B.base + aoff, B.sd, lda, m,
-                       B.base + off_vec(B.N, VS_EV), B.sd, B.base + off_vec(B.N, VS_R), B.base + off_vec(B.N, VS_EW), B.sd,
-                       B.base + off_refl(B.N), B.sd, B.infos, vectors ? 2 : 0);
-    HIPCHK(c, hipGetLastError());
-    return RIPTRM_OK;
+    return launch_eig(c, cnt, m, B.base + aoff, B.sd, lda, B.base + off_vec(B.N, VS_EV), B.sd, B.base + off_vec(B.N, VS_R),
+                      B.base + off_vec(B.N, VS_EW), B.sd, B.base + off_refl(B.N), B.sd, B.infos, vectors ? 2 : 0, nullptr);
   }
   if (int rc = big_handle(c)) return rc;
   Solver& s = solver();
@@ -1612,14 +1628,12 @@ int riptrm_sym_eig(riptrm_ctx* ctx, int32_t dim, int32_t batch, double* A, int64
     ctx->eig_scratch_bytes = need;
   }
   double* s = (double*)ctx->eig_scratch;
-  const size_t shm = riptrm_eig::eig_lds_bytes(dim);
-  HIPCHK(ctx, hipFuncSetAttribute((const void*)riptrm_eig::k_eig_lds, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm));
   long long* stamps = nullptr;   // RIPTRM_EIG_STAMPS=1: per-phase clocks of matrix 0 on stderr (diagnostics)
   const bool want_stamps = getenv_is("RIPTRM_EIG_STAMPS", '1');
   if (want_stamps) HIPCHK(ctx, hipMalloc(&stamps, (size_t)batch * 8 * sizeof(long long)));
-  hipLaunchKernelGGL(riptrm_eig::k_eig_lds, dim3(batch), dim3(riptrm_eig::EW), shm, ctx->stream, A, a_stride, (int)lda, dim, w,
-                     w_stride, s, s + sc, per, s + 2 * sc, per, info, vectors == 2 ? 2 : (vectors ? 1 : 0), stamps);
-  HIPCHK(ctx, hipGetLastError());
+  if (int rc = launch_eig(ctx, batch, dim, A, a_stride, (int)lda, w, w_stride, s, s + sc, per, s + 2 * sc, per, info,
+                          vectors == 2 ? 2 : (vectors ? 1 : 0), stamps))
+    return rc;
   if (want_stamps) {
     std::vector<long long> h((size_t)batch * 8);
     HIPCHK(ctx, hipMemcpyAsync(h.data(), stamps, h.size() * sizeof(long long), hipMemcpyDeviceToHost, ctx->stream));
