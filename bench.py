@@ -98,7 +98,7 @@ def _blas_threads():
         return int(os.environ.get("OMP_NUM_THREADS", "1"))
 
 
-def _inner_sampled(idurs, inner_per_outer, procs, cores, n, trs, who, budget_s):
+def _inner_sampled(idurs, inner_per_outer, procs, cores, n, trs, who, budget_s, what=None):
     """A window the CPU cannot finish in its budget (Exact_RepMat at n = 1000: one 2n x 2n pencil
     per inner step): the solver seconds of the inner steps it completed, converted to outer
     iterations/s with the GPU window's own inner iterations per outer iteration."""
@@ -107,7 +107,7 @@ def _inner_sampled(idurs, inner_per_outer, procs, cores, n, trs, who, budget_s):
     per_inner = sum(idurs) / len(idurs)
     return {"value": procs / (per_inner * inner_per_outer), "unit": "outer iterations/s", "cores": int(cores),
             "kind": "port",
-            "sample": (f"oracle/riptrm_oracle.py NonnegPCAVectorized, {who}, n={n}"
+            "sample": ((what or f"oracle/riptrm_oracle.py NonnegPCAVectorized, {who}, n={n}")
                        + (", TRS_solver=Exact_RepMat (trs_oracle: 2n x 2n pencil, scipy.linalg.eig)" if trs != "tCG" else "")
                        + f": the window does not complete in the {budget_s:.0f} s budget, so the rate is sampled per inner "
                          f"step -- {len(idurs)} inner steps of outer iteration 1.. at {per_inner:.2f} s each (evaluation "
@@ -833,6 +833,7 @@ def _si_oracle_window(gid: int, K: int, budget_s: float, trs: str, d: int = 5):
         pass
     heads = orc.outer_heads
     last = max(heads)
+    _si_oracle_window.inner_durations = list(orc.inner_durations)
     return (last, heads[last]) if last > 0 and heads[last] > 0 else None
 
 
@@ -840,30 +841,36 @@ def _si_cpu_worker(argv):
     """One single-threaded SI oracle process (run by si_cpu_pool)."""
     gid, K, budget, trs, d = int(argv[0]), int(argv[1]), float(argv[2]), argv[3], int(argv[4])
     r = _si_oracle_window(gid, K, budget, trs, d)
-    print(json.dumps(None if r is None else {"outer": r[0], "secs": r[1]}), flush=True)
+    print(json.dumps({"outer": r[0] if r else 0, "secs": r[1] if r else 0.0,
+                      "inner": _si_oracle_window.inner_durations}), flush=True)
 
 
-def si_cpu_pool(K: int, budget_s: float, procs: int, trs: str, d: int = 5):
+def si_cpu_pool(K: int, budget_s: float, procs: int, trs: str, d: int = 5, inner_per_outer=None):
     """The StableIdentification analogue of cpu_baseline_pool: `procs` single-threaded oracle
     processes run concurrently, process i solving the GPU batch's start i (si_starts) over the
-    same outer window 1..K; aggregate = mean complete per-process rate x procs."""
+    same outer window 1..K; aggregate = mean complete per-process rate x procs.  When no process
+    completes the window (Exact_RepMat at d >= 8), the rate is sampled per inner step
+    (_inner_sampled, with the GPU window's inner iterations per outer iteration)."""
     import subprocess
     env = dict(os.environ, OMP_NUM_THREADS="1", OPENBLAS_NUM_THREADS="1", MKL_NUM_THREADS="1")
     ps = [subprocess.Popen([sys.executable, os.path.abspath(__file__), "--si-cpu-worker", str(i), str(K),
                             str(budget_s), trs, str(d)], stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, env=env,
                            text=True)
           for i in range(procs)]
-    rates = []
+    rates, inner = [], []
     for p in ps:
         out, _ = p.communicate(timeout=budget_s + 600)
         try:
             r = json.loads(out.strip().splitlines()[-1])
         except Exception:
             continue
-        if r is not None and r["outer"] == K:
+        inner.extend(r.get("inner", []))
+        if r["outer"] == K and r["secs"] > 0:
             rates.append(r["outer"] / r["secs"])
     if not rates:
-        return None
+        return _inner_sampled(inner, inner_per_outer, procs, procs, None, trs, None, budget_s,
+                              what=(f"oracle/si_oracle.py SIVectorized, d={d}, {procs} single-threaded processes, process i "
+                                    f"solving the GPU batch's start i"))
     return {"value": sum(rates) / len(rates) * procs, "unit": "outer iterations/s", "cores": int(procs),
             "kind": "port",
             "sample": (f"oracle/si_oracle.py SIVectorized, {procs} single-threaded processes, process i solving the GPU "
@@ -951,7 +958,11 @@ def bench_si(args, world, rank, dev, dist):
         return
     cpu = None
     if args.cpu_budget > 0 and world == 1:
+        ipo = inner / outer if outer > 0 else None
         one = _si_oracle_window(0, K, args.cpu_budget, args.trs, d)
+        if one is None:   # not one outer iteration within the budget: sampled per inner step
+            cpu = _inner_sampled(_si_oracle_window.inner_durations, ipo, 1, 1, None, args.trs, None, args.cpu_budget,
+                                 what=f"oracle/si_oracle.py SIVectorized (NumPy, closed-form Lagrangian), d={d}, start 0")
         if one is not None:
             last, secs = one
             cpu = {"value": last / secs, "unit": "outer iterations/s", "cores": 1, "kind": "port",
@@ -961,7 +972,7 @@ def bench_si(args, world, rank, dev, dist):
         pool = None
         if procs > 0:
             log(f"SI CPU baseline, {procs} single-threaded processes ...")
-            pool = si_cpu_pool(K, args.cpu_pool_budget, procs, args.trs, d)
+            pool = si_cpu_pool(K, args.cpu_pool_budget, procs, args.trs, d, ipo)
         cpu = pick_cpu_baseline(cpu, pool)
         if cpu is not None:
             cpu.update(host_cpu_info())

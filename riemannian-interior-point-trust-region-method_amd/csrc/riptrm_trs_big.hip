@@ -508,12 +508,18 @@ __global__ void __launch_bounds__(WG) k_cg_wg(Bat B, int m, int64_t aoff, int64_
 }
 
 // The same SciPy CG on ONE wave for orders m <= CGW_MAX (StableIdentification at d = 8: m = 100,
-// where indefinite subproblems run the CG to its 10 m iteration cap): A in LDS with an odd row stride
-// (each lane reads its own rows, conflict-free), two rows per lane, p broadcast from LDS, the dot
-// products as wave reductions -- no workgroup barrier in the loop (k_cg_wg pays three per
-// iteration).  Its own fixed summation order (four partial sums per row); skip_indef as k_cg_wg.
+// where ill-conditioned subproblems run the CG to its 10 m iteration cap): A in LDS, two rows per
+// lane, p broadcast from LDS, the dot products as wave reductions -- no workgroup barrier in the loop
+// (k_cg_wg pays three per iteration).  Rows are zero-padded to a multiple of four and read 16 bytes at
+// a time; the row stride cgw_stride(m) = 2 mod 4 doubles puts a 16-lane phase of those reads on
+// distinct banks.  Its own fixed summation order (four partial sums per row, j mod 4, then
+// (s0 + s1) + (s2 + s3)); skip_indef as k_cg_wg.
 constexpr int CGW_MAX = 128;
-inline size_t cg_wave_lds(int m) { return ((size_t)m * (m + 1) + CGW_MAX) * sizeof(double); }
+typedef double cgw_d2 __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(3))) cgw_d2 lds_d2;
+__host__ __device__ inline int cgw_m4(int m) { return (m + 3) / 4 * 4; }
+__host__ __device__ inline int cgw_stride(int m) { return cgw_m4(m) + 2; }
+inline size_t cg_wave_lds(int m) { return ((size_t)m * cgw_stride(m) + CGW_MAX) * sizeof(double); }
 __global__ void __launch_bounds__(64) k_cg_wave(Bat B, int m, int64_t aoff, int64_t lda, const double* D,
                                                 int64_t dstride, const double* Aext = nullptr, int64_t ext_stride = 0,
                                                 int skip_indef = 0) {
@@ -558,13 +564,14 @@ __global__ void __launch_bounds__(64) k_cg_wave(Bat B, int m, int64_t aoff, int6
       return;
     }
   }
-  const int ms = m + 1;
+  const int ms = cgw_stride(m), m4 = cgw_m4(m);
   lds_f64* Al = (lds_f64*)cgs;
   lds_f64* ps = Al + (int64_t)m * ms;
-  for (int64_t e = l; e < (int64_t)m * m; e += 64) {
-    const int i = (int)(e / m), j = (int)(e - (int64_t)i * m);
-    Al[i * ms + j] = A[(int64_t)i * lda + j];
+  for (int64_t e = l; e < (int64_t)m * ms; e += 64) {
+    const int i = (int)(e / ms), j = (int)(e - (int64_t)i * ms);
+    Al[e] = j < m ? A[(int64_t)i * lda + j] : 0.0;
   }
+  for (int j = m + l; j < m4; j += 64) ps[j] = 0.0;
   double x[2] = {0.0, 0.0}, r[2];
   double an = 0.0;
 #pragma unroll
@@ -578,25 +585,28 @@ __global__ void __launch_bounds__(64) k_cg_wave(Bat B, int m, int64_t aoff, int6
   const double atol = 1e-5 * an;
   double done = an == 0.0 ? 2.0 : 0.0, it = 0.0, rho_prev = 1.0;
   __syncthreads();
-  // rows i = l and l + 64 of A . p, each with four partial sums (j mod 4), then (s0 + s1) + (s2 + s3)
+  // rows i = l and l + 64 of A . p, each with four partial sums (j mod 4), then (s0 + s1) + (s2 + s3);
+  // both rows in one loop (twelve 16-byte loads in flight per step of four)
   auto matvec = [&](double* qv) {
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int i = l + 64 * u < m ? l + 64 * u : m - 1;
-      const lds_f64* row = Al + i * ms;
-      double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
-      int j = 0;
-      for (; j + 3 < m; j += 4) {
-        s0 += row[j] * ps[j];
-        s1 += row[j + 1] * ps[j + 1];
-        s2 += row[j + 2] * ps[j + 2];
-        s3 += row[j + 3] * ps[j + 3];
-      }
-      if (j < m) s0 += row[j] * ps[j];
-      if (j + 1 < m) s1 += row[j + 1] * ps[j + 1];
-      if (j + 2 < m) s2 += row[j + 2] * ps[j + 2];
-      qv[u] = l + 64 * u < m ? (s0 + s1) + (s2 + s3) : 0.0;
+    const int i0 = l < m ? l : m - 1, i1 = l + 64 < m ? l + 64 : m - 1;
+    const lds_d2* r0 = (const lds_d2*)(Al + i0 * ms);
+    const lds_d2* r1 = (const lds_d2*)(Al + i1 * ms);
+    const lds_d2* pv = (const lds_d2*)ps;
+    double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0, b0 = 0.0, b1 = 0.0, b2 = 0.0, b3 = 0.0;
+#pragma unroll 2
+    for (int h = 0; h < m4 / 2; h += 2) {
+      const cgw_d2 x0 = r0[h], x1 = r0[h + 1], y0 = r1[h], y1 = r1[h + 1], p0 = pv[h], p1 = pv[h + 1];
+      a0 += x0.x * p0.x;
+      a1 += x0.y * p0.y;
+      a2 += x1.x * p1.x;
+      a3 += x1.y * p1.y;
+      b0 += y0.x * p0.x;
+      b1 += y0.y * p0.y;
+      b2 += y1.x * p1.x;
+      b3 += y1.y * p1.y;
     }
+    qv[0] = l < m ? (a0 + a1) + (a2 + a3) : 0.0;
+    qv[1] = l + 64 < m ? (b0 + b1) + (b2 + b3) : 0.0;
   };
   while (done == 0.0) {   // uniform
     if (it >= 10.0 * m) {
