@@ -994,7 +994,10 @@ def bench_si(args, world, rank, dev, dist):
         "roofline": si_roofline(args, d, hvps, kern_s, sec, tot("PASSES")),
         "cpu_baseline": cpu,
         "detail": {"inner_iterations_per_s": inner / T, "tcg_iterations_per_s": tcg / T, "hvps_per_s": hvps / T,
-                   "section_fraction": secfrac, "us_per_hvp_per_instance": sec["hvp"] / max(1.0, tot("PASSES")) * 1e6},
+                   "section_fraction": secfrac, "us_per_hvp_per_instance": sec["hvp"] / max(1.0, tot("PASSES")) * 1e6,
+                   # HBM TRS service (Exact_RepMat, d >= 8): subproblems whose CG was decided on their
+                   # eigenpairs, and CGs skipped by the certified bound (since the context was made)
+                   "trs_cg_checked_skipped": (list(eng.trs_skip_stats()) if args.trs != "tCG" else None)},
     }), flush=True)
 
 

@@ -364,8 +364,9 @@ inline int cg_lds_rows(int m) {
 //   ||p1|| >= ||p*|| - e / lam_s            (p* = -A^-1 a: ||p*||^2 = sum g_i^2 / lam_i^2)
 //   p1obj = q(p*) + r^T A^-1 r / 2 >= -sum g_i^2 / lam_i / 2 - e^2 / (2 lam_s)
 // so the skip needs ||p*|| (1 - 1e-6) - e / lam_s >= Delta, or that lower bound on p1obj above xobj
-// by more than a rounding allowance; A indefinite (lam_min < -1e-8 max |lam|) and not nearly
-// singular (lam_s > 1e-8 max |lam|).  Otherwise the CG runs (the same iterate as without the skip).
+// by more than a rounding allowance; A not nearly singular (lam_s > 1e-8 max |lam|; definite or
+// not: the bounds hold for any iterate with that residual).  Otherwise the CG runs (the same iterate
+// as without the skip).
 __global__ void __launch_bounds__(WG) k_cg_wg(Bat B, int m, int64_t aoff, int64_t lda, const double* D,
                                               int64_t dstride, int rl, const double* Aext = nullptr,
                                               int64_t ext_stride = 0, int skip_indef = 0) {
@@ -379,7 +380,7 @@ __global__ void __launch_bounds__(WG) k_cg_wg(Bat B, int m, int64_t aoff, int64_
   const int t = threadIdx.x;
   if (skip_indef) {
     const double *ev = q.v[VS_EV], *g = q.v[VS_G];
-    const double lmin = ev[0], lmax = fmax(fabs(ev[0]), fabs(ev[m - 1]));
+    const double lmax = fmax(fabs(ev[0]), fabs(ev[m - 1]));
     double lsm = INFINITY, s1 = 0.0, s2 = 0.0, aa = 0.0;
     for (int i = t; i < m; i += WG) {
       const double l = ev[i], gi = g[i];
@@ -393,7 +394,7 @@ __global__ void __launch_bounds__(WG) k_cg_wg(Bat B, int m, int64_t aoff, int64_
     s2 = blk_sum(s2, red);
     const double e = 1e-5 * sqrt(blk_sum(aa, red));
     const double Dl = D[(int64_t)B.ids[k] * dstride];
-    bool skip = *q.info == 0 && lmin < -1e-8 * lmax && lsm > 1e-8 * lmax;
+    bool skip = *q.info == 0 && lsm > 1e-8 * lmax;
     if (skip) {
       const double xobj = q.sc[SC_XOBJ];
       const bool far = sqrt(s1) * (1.0 - 1e-6) - e / lsm >= Dl;
@@ -532,7 +533,7 @@ __global__ void __launch_bounds__(64) k_cg_wave(Bat B, int m, int64_t aoff, int6
   const double Dl = D[(int64_t)B.ids[k] * dstride];
   if (skip_indef) {   // k_cg_wg's certified skip, with wave reductions
     const double *ev = q.v[VS_EV], *g = q.v[VS_G];
-    const double lmin = ev[0], lmax = fmax(fabs(ev[0]), fabs(ev[m - 1]));
+    const double lmax = fmax(fabs(ev[0]), fabs(ev[m - 1]));
     double lsm = INFINITY, s1 = 0.0, s2 = 0.0, aa = 0.0;
     for (int i = l; i < m; i += 64) {
       const double lv = ev[i], gi = g[i];
@@ -545,7 +546,7 @@ __global__ void __launch_bounds__(64) k_cg_wave(Bat B, int m, int64_t aoff, int6
     s1 = riptrm_wave::wave_sum(s1);
     s2 = riptrm_wave::wave_sum(s2);
     const double e = 1e-5 * sqrt(riptrm_wave::wave_sum(aa));
-    bool skip = *q.info == 0 && lmin < -1e-8 * lmax && lsm > 1e-8 * lmax;
+    bool skip = *q.info == 0 && lsm > 1e-8 * lmax;
     if (skip) {
       const double xobj = q.sc[SC_XOBJ];
       const bool far = sqrt(s1) * (1.0 - 1e-6) - e / lsm >= Dl;
