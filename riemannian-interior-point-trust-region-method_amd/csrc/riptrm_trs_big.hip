@@ -911,6 +911,128 @@ __global__ void k_set_delta(Bat B, int cnt, const double* D, int64_t dstride) {
   slot_at(B, k).sc[SC_DELTA] = D[(int64_t)B.ids[k] * dstride];
 }
 
+// SciPy's CG (RIPTRM.py:240-251; the loop of k_cg_wave, restated from scipy.sparse.linalg.cg) on
+// the subproblem's eigen-coordinates.  With A = Q diag(lam) Q^T (lam ascending at VS_EV, g = Q^T a at
+// VS_G), the CG on diag(lam) y = -g generates y_k = Q^T x_k of the CG on A x = -a: Krylov subspaces,
+// residual norms and step lengths are invariant under the orthogonal change of basis, so it is the
+// same iterate up to rounding, at O(m) per iteration instead of an m x m mat-vec.  The stopping test
+// uses ||a|| (atol = 1e-5 ||a||) and the final test the true residual diag(lam) y + g = Q^T (A x + a).
+// One wave per slot, element i on lane i mod 64 (m <= 256).  The candidate stays in eigen-coordinates
+// at VS_CGX (k_pick_eig).  skip_test: k_cg_wg's certified skip first.
+__global__ void __launch_bounds__(64) k_cg_diag(Bat B, int m, const double* D, int64_t dstride, int skip_test) {
+  const int k = blockIdx.y;
+  const Slot q = slot_at(B, k);
+  const double *ev = q.v[VS_EV], *g = q.v[VS_G], *a = q.v[VS_A];
+  const int l = threadIdx.x;
+  const double Dl = D[(int64_t)B.ids[k] * dstride];
+  double lam[4], x[4], r[4], p[4];
+  double an = 0.0, lsm = INFINITY, s1 = 0.0, s2 = 0.0;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int i = l + 64 * u;
+    const double ai = i < m ? a[i] : 0.0, gi = i < m ? g[i] : 0.0;
+    lam[u] = i < m ? ev[i] : 0.0;
+    r[u] = -gi;
+    x[u] = p[u] = 0.0;
+    an += ai * ai;
+    if (i < m) {
+      lsm = fmin(lsm, fabs(lam[u]));
+      s1 += (gi / lam[u]) * (gi / lam[u]);
+      s2 += gi * gi / lam[u];
+    }
+  }
+  an = sqrt(riptrm_wave::wave_sum(an));
+  if (skip_test) {   // k_cg_wg's certified skip (the bounds there)
+    const double lmax = fmax(fabs(ev[0]), fabs(ev[m - 1]));
+    lsm = riptrm_wave::wave_min(lsm);
+    s1 = riptrm_wave::wave_sum(s1);
+    s2 = riptrm_wave::wave_sum(s2);
+    const double e = 1e-5 * an;
+    bool skip = *q.info == 0 && lsm > 1e-8 * lmax;
+    if (skip) {
+      const double xobj = q.sc[SC_XOBJ];
+      const bool far = sqrt(s1) * (1.0 - 1e-6) - e / lsm >= Dl;
+      const double p1lo = -0.5 * s2 - 0.5 * e * e / lsm;
+      const bool worse = p1lo - xobj > 1e-6 * (fabs(s2) + fabs(xobj)) + 1e-10 * (e * 1e5) * Dl;
+      skip = far || worse;
+    }
+    if (skip) {
+      if (l == 0) {
+        q.sc[SC_CG_OK] = 0.0;
+        q.sc[SC_P1OBJ] = 0.0;
+        q.sc[SC_IT] = 0.0;
+        q.sc[SC_DONE] = 4.0;
+        q.sc[SC_DELTA] = Dl;
+      }
+      return;
+    }
+  }
+  const double atol = 1e-5 * an;
+  double done = an == 0.0 ? 2.0 : 0.0, it = 0.0, rho_prev = 1.0;
+  while (done == 0.0) {   // uniform
+    if (it >= 10.0 * m) {
+      done = 3.0;
+      break;
+    }
+    const double rr = riptrm_wave::wave_sum((r[0] * r[0] + r[1] * r[1]) + (r[2] * r[2] + r[3] * r[3]));
+    if (sqrt(rr) < atol) {
+      done = 1.0;
+      break;
+    }
+    const double rho = rr;
+    const double beta = it > 0.0 ? rho / rho_prev : 0.0;
+    double qv[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      p[u] = it > 0.0 ? p[u] * beta + r[u] : r[u];
+      qv[u] = lam[u] * p[u];
+    }
+    const double pq = riptrm_wave::wave_sum((p[0] * qv[0] + p[1] * qv[1]) + (p[2] * qv[2] + p[3] * qv[3]));
+    const double alpha = rho / pq;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      x[u] += alpha * p[u];
+      r[u] -= alpha * qv[u];
+    }
+    rho_prev = rho;
+    it += 1.0;
+  }
+  double v0 = 0.0, v1 = 0.0, v2 = 0.0, v3 = 0.0;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int i = l + 64 * u;
+    if (i < m) {
+      const double ax = lam[u] * x[u], gi = g[i];
+      const double res = ax + gi;
+      v0 += res * res;
+      v1 += x[u] * x[u];
+      v2 += x[u] * ax;
+      v3 += gi * x[u];
+      q.v[VS_CGX][i] = x[u];
+    }
+  }
+  v0 = riptrm_wave::wave_sum(v0);
+  v1 = riptrm_wave::wave_sum(v1);
+  v2 = riptrm_wave::wave_sum(v2);
+  v3 = riptrm_wave::wave_sum(v3);
+  if (l == 0) {
+    q.sc[SC_AN] = an;
+    q.sc[SC_ATOL] = atol;
+    q.sc[SC_IT] = it;
+    q.sc[SC_DONE] = done;
+    q.sc[SC_CG_OK] = (an != 0.0 && sqrt(v0) / an < 1e-5 && v1 < Dl * Dl) ? 1.0 : 0.0;   // RIPTRM.py:246-251
+    q.sc[SC_P1OBJ] = 0.5 * v2 + v3;
+    q.sc[SC_DELTA] = Dl;
+  }
+}
+
+// pe <- the CG's eigen-coordinates when the interior candidate won (then x = Q pe for either)
+__global__ void __launch_bounds__(256) k_pick_eig(Bat B, int m) {
+  const Slot q = slot_at(B, blockIdx.y);
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i < m && q.sc[SC_INTERIOR] != 0.0) q.v[VS_PE][i] = q.v[VS_CGX][i];
+}
+
 // x <- cgx when the interior candidate won (x = Q pe was computed before)
 __global__ void __launch_bounds__(256) k_pick(Bat B, int m) {
   const Slot q = slot_at(B, blockIdx.y);
@@ -1356,6 +1478,28 @@ static int big_after_eig(riptrm_ctx* c, const Bat& B, int cnt, int64_t aoff, int
   return RIPTRM_OK;
 }
 
+// The subproblems of the pass after the hand-written eigensolve (compact eigenvectors over the
+// matrix at aoff, lda; eig_compact(m)): g = Q^T a, the boundary candidate (k_secular, choose = 0), the
+// CG in eigen-coordinates (k_cg_diag; skip: its certified skip), the interior / boundary choice, and
+// x = Q pe.  The matrix itself is not read again.
+static int compact_trs(riptrm_ctx* c, const Bat& B, int cnt, int m, int64_t aoff, int lda, const double* D,
+                       int64_t dstride, double tolhc, bool skip) {
+  hipStream_t st = c->stream;
+  const int64_t N = B.N;
+  const dim3 one(1, cnt), rows(blocks_of(m, GV / 64), cnt), els(blocks_of(m, 256), cnt);
+  if (int rc = refl_apply(c, B, cnt, m, off_vec(N, VS_A), off_vec(N, VS_PE), 0)) return rc;
+  hipLaunchKernelGGL(k_gemv, rows, dim3(GV), 0, st, B, aoff, (int64_t)lda, m, m, off_vec(N, VS_PE), off_vec(N, VS_G),
+                     (int64_t)-1);
+  hipLaunchKernelGGL(k_set_delta, dim3(blocks_of(cnt, 64)), dim3(64), 0, st, B, cnt, D, dstride);
+  hipLaunchKernelGGL(k_secular, one, dim3(WG), 0, st, B, m, tolhc, 0);
+  hipLaunchKernelGGL(k_cg_diag, one, dim3(64), 0, st, B, m, D, dstride, skip ? 1 : 0);
+  hipLaunchKernelGGL(k_choose, dim3(blocks_of(cnt, 64)), dim3(64), 0, st, B, cnt);
+  hipLaunchKernelGGL(k_pick_eig, els, dim3(256), 0, st, B, m);
+  hipLaunchKernelGGL(k_gemv_t, els, dim3(256), 0, st, B, aoff, (int64_t)lda, m, m, off_vec(N, VS_PE), off_vec(N, VS_X));
+  HIPCHK(c, hipGetLastError());
+  return refl_apply(c, B, cnt, m, off_vec(N, VS_X), off_vec(N, VS_X), 1);
+}
+
 static int big_solve(riptrm_ctx* c, const Bat& B, int cnt, int64_t aoff, int lda, int m, const double* D, int64_t dstride,
                      double tolhc) {
   if (int rc = big_cg(c, B, cnt, aoff, lda, m, D, dstride)) return rc;
@@ -1449,6 +1593,16 @@ int riptrm_big_service(riptrm_ctx* c, int* served) {
         if (cached)
           hipLaunchKernelGGL(k_cache_store, dim3(blocks_of((int64_t)n * n, 256), cnt), dim3(256), 0, c->stream, P, Bt, cache,
                              CN);
+      } else if (eig_compact(n - 1)) {   // eigenpairs (or the cached ones), then the CG in eigen-coordinates
+        if (kind == 1)
+          hipLaunchKernelGGL(k_cache_load, dim3(blocks_of((int64_t)n * n, 256), cnt), dim3(256), 0, c->stream, P, Bt, cache,
+                             CN);
+        else if (int rc = eig_batched(c, Bt, cnt, true, n - 1, aoff, n))
+          return rc;
+        if (int rc = compact_trs(c, Bt, cnt, n - 1, aoff, n, P.st + ST_DELTA, ST_N, P.opt.trs_tolhardcase,
+                                 !getenv_is("RIPTRM_CG_SKIP", '0')))
+          return rc;
+        hipLaunchKernelGGL(k_finish_dir, dim3(1, cnt), dim3(WG), 0, c->stream, P, Bt);
       } else {
         if (int rc = big_cg(c, Bt, cnt, aoff, n, n - 1, P.st + ST_DELTA, ST_N)) return rc;
         if (kind == 1)
@@ -1501,6 +1655,17 @@ int riptrm_big_gep_ids(riptrm_ctx* c, int dim, const int32_t* sel, int count, co
     HIPCHK(c, hipGetLastError());
     if (mineig_only) {
       if (int rc = eig_batched(c, Bt, cnt, false, dim, 0, dim)) return rc;
+    } else if (eig_compact(dim)) {
+      // eigenpairs first, then the CG in eigen-coordinates (k_cg_diag), skipped where the certified
+      // bound shows its candidate cannot win (per_instance callers; RIPTRM_CG_SKIP=0: never)
+      const bool skip = per_instance && !getenv_is("RIPTRM_CG_SKIP", '0');
+      if (int rc = eig_batched(c, Bt, cnt, true, dim, 0, dim)) return rc;
+      if (int rc = compact_trs(c, Bt, cnt, dim, 0, dim, Delta, 1, tolhc, skip)) return rc;
+      if (skip) {
+        skip_done.resize(cnt);
+        HIPCHK(c, hipMemcpy2DAsync(skip_done.data(), sizeof(double), Bt.base + off_sc(Bt.N) + SC_DONE,
+                                   (size_t)Bt.sd * sizeof(double), sizeof(double), cnt, hipMemcpyDeviceToHost, c->stream));
+      }
     } else if (per_instance && cg_one_workgroup(dim, cnt) && !getenv_is("RIPTRM_CG_SKIP", '0')) {
       // eigenpairs, g = Q^T a and the boundary candidate first; the CG then reads A from the
       // caller's array and is skipped where the eigenpairs prove the interior candidate cannot win
