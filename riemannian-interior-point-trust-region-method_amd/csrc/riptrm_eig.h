@@ -86,41 +86,37 @@ __device__ __forceinline__ double rcp_nr(double q) {
   return fma(r, t, r);
 }
 
-// the number of eigenvalues of T (diagonal d, off-diagonal e; split where e_j = 0) below x: the sign
-// changes of p_j = det(T_{0..j} - x I) = (d_j - x) p_{j-1} - e_{j-1}^2 p_{j-2} (a new block restarts
-// at p = 1), i.e. the negative pivots q_j = p_j / p_{j-1} of LAPACK dlaneg's recurrence, with its guard:
-// |q_j| < pivmin counts as q_j = -pivmin.  No division on the dependent chain (a multiply and an FMA per
-// step); p_{j-1}, p_j are rescaled by a power of two every four steps (|d_j - x| <= 4 ||T|| per step; the larger to ~1).
-__device__ __forceinline__ void sturm_step(double dx, double f, double& p0, double& p1, int& c, double pivmin) {
-  double pn = fma(-(f * f), p0, dx * p1);
-  double pv = p1;
-  if (f == 0.0) {   // a new block of the split T
-    pn = dx;
-    pv = 1.0;
-  }
-  if (pn == 0.0 || fabs(pn) < pivmin * fabs(pv)) pn = -(pivmin * pv);   // (may underflow to a signed zero)
-  c += signbit(pn) != signbit(pv);
-  p0 = pv;
-  p1 = pn;
-}
+// the number of eigenvalues of T (diagonal d, off-diagonal e) below x (Sturm count, LAPACK dlaneg's
+// recurrence with pivmin guarding zero pivots).  (A division-free form -- the sign changes of
+// p_j = (d_j - x) p_{j-1} - e_{j-1}^2 p_{j-2}, rescaled every four steps -- measured 6-10% slower: it
+// issues more instructions per step, and the counts are issue-bound, not latency-bound.)
 __device__ __forceinline__ int sturm_count(const lds_t* d, const lds_t* e, int m, double x, double pivmin) {
-  double p0 = 1.0, p1 = d[0] - x;
-  if (p1 == 0.0 || fabs(p1) < pivmin) p1 = -pivmin;
-  int c = signbit(p1) ? 1 : 0;
+  double q = d[0] - x;
+  if (fabs(q) < pivmin) q = -pivmin;
+  int c = q < 0.0;
   int j = 1;
   for (; j + 3 < m; j += 4) {   // the next four entries' loads issued ahead of the dependent chain
-    const double d0 = d[j] - x, d1 = d[j + 1] - x, d2 = d[j + 2] - x, d3 = d[j + 3] - x;
+    const double d0 = d[j], d1 = d[j + 1], d2 = d[j + 2], d3 = d[j + 3];
     const double f0 = e[j - 1], f1 = e[j], f2 = e[j + 1], f3 = e[j + 2];
-    sturm_step(d0, f0, p0, p1, c, pivmin);
-    sturm_step(d1, f1, p0, p1, c, pivmin);
-    sturm_step(d2, f2, p0, p1, c, pivmin);
-    sturm_step(d3, f3, p0, p1, c, pivmin);
-    int ex;   // the larger of the two to ~1 (a signed-zero or subnormal p_j keeps its sign)
-    (void)frexp(fmax(fabs(p0), fabs(p1)), &ex);
-    p0 = ldexp(p0, -ex);
-    p1 = ldexp(p1, -ex);
+    q = (d0 - x) - (f0 * f0) * rcp_nr(q);
+    if (fabs(q) < pivmin) q = -pivmin;
+    c += q < 0.0;
+    q = (d1 - x) - (f1 * f1) * rcp_nr(q);
+    if (fabs(q) < pivmin) q = -pivmin;
+    c += q < 0.0;
+    q = (d2 - x) - (f2 * f2) * rcp_nr(q);
+    if (fabs(q) < pivmin) q = -pivmin;
+    c += q < 0.0;
+    q = (d3 - x) - (f3 * f3) * rcp_nr(q);
+    if (fabs(q) < pivmin) q = -pivmin;
+    c += q < 0.0;
   }
-  for (; j < m; ++j) sturm_step(d[j] - x, e[j - 1], p0, p1, c, pivmin);
+  for (; j < m; ++j) {
+    const double ej = e[j - 1];
+    q = (d[j] - x) - (ej * ej) * rcp_nr(q);
+    if (fabs(q) < pivmin) q = -pivmin;
+    c += q < 0.0;
+  }
   return c;
 }
 
@@ -209,6 +205,40 @@ __device__ __forceinline__ void twisted_vector(lds_t* Z, const lds_t* d, const l
   Z[r] = 1.0;
   const double inv = 1.0 / sqrt(nrm);
   for (int j = 0; j < m; ++j) Z[j] = (j < blo || j > bhi) ? 0.0 : Z[j] * inv;
+}
+
+// Block Gram-Schmidt algebra on the matrix cores (v_mfma_f64_16x16x4_f64: A operand lane (i = l & 15,
+// k = l >> 4), B operand (k = l >> 4, j = l & 15), D rows 4 q + (l >> 4), column l & 15).
+typedef double eig_d4 __attribute__((ext_vector_type(4)));
+// Out[b][c] = (SUB ? Base[b][c] : 0) -+ sum_a W[b][a] X[a][c] for the GB x m block (b < GB, c < m): W is
+// GB x GB at stride GB + 1 (TRANS: W[b][a] read as W[a][b]), X, Out, Base GB x m at stride mp (X's
+// columns past m are zero).  (2 x ceil(m / 16)) 16 x 16 tiles dealt to the NWV waves, K = GB in eight steps.
+template <bool TRANS, bool SUB, int NWV>
+__device__ __forceinline__ void gs_wmul(lds_t* Out, const lds_t* Base, const lds_t* W, const lds_t* X, int mp, int m,
+                                        int w, int lane) {
+  const int c16 = lane & 15, kk = lane >> 4;
+  const int nct = (m + 15) / 16;
+  for (int t = w; t < 2 * nct; t += NWV) {
+    const int b0 = (t & 1) * 16, c0 = (t >> 1) * 16;
+    const int col = c0 + c16 < mp ? c0 + c16 : mp - 1;
+    eig_d4 acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int a0 = 0; a0 < GB; a0 += 8) {
+      const double av0 = TRANS ? W[(a0 + kk) * (GB + 1) + b0 + c16] : W[(b0 + c16) * (GB + 1) + a0 + kk];
+      const double av1 = TRANS ? W[(a0 + 4 + kk) * (GB + 1) + b0 + c16] : W[(b0 + c16) * (GB + 1) + a0 + 4 + kk];
+      const double bv0 = X[(a0 + kk) * mp + col], bv1 = X[(a0 + 4 + kk) * mp + col];
+      acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(av0, bv0, acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(av1, bv1, acc1, 0, 0, 0);
+    }
+    if (c0 + c16 < m) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int b = b0 + kk + 4 * q;
+        const double v = acc0[q] + acc1[q];
+        Out[b * mp + c0 + c16] = SUB ? Base[b * mp + c0 + c16] - v : v;
+      }
+    }
+  }
 }
 
 // Matrix k = blockIdx.x: the m x m symmetric matrix at A0 + k a_stride (leading dimension lda; the
@@ -403,7 +433,7 @@ __global__ void __launch_bounds__(TW) k_eig_lds(double* A0, int64_t a_stride, in
   // multisection: kq (1, 2, 4 or 8) consecutive lanes per eigenvalue test kq points of its interval
   // at once and keep the sub-interval the counts select (the same on every lane of the group)
   {
-    int kq = EW / m;
+    int kq = 512 / m;   // ~512 lanes in all: the counts are issue-bound, more lanes only add work
     kq = kq >= 8 ? 8 : (kq >= 4 ? 4 : (kq >= 2 ? 2 : 1));
     const int ei = tid / kq, sub = tid - ei * kq, base = (int)(threadIdx.x & 63) - sub;
     if (ei < m) {
@@ -534,25 +564,26 @@ __global__ void __launch_bounds__(TW) k_eig_lds(double* A0, int64_t a_stride, in
           }
         __syncthreads();
         const lds_t* QA = I < J ? QI : QJ;
-        // E[a][b] = Q_I[a] . Q_J[b] (a 2 x 1 register block per thread: GB x GB / 512)
-        for (int q = tid; q < GB * GB; q += EW) {
-          const int a = q / GB, b = q - a * GB;
-          double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
-          const lds_t* xa = QA + a * mp;
-          const lds_t* xb = QJ + b * mp;
-          int c = 0;
-          for (; c + 3 < m; c += 4) {
-            s0 += xa[c] * xb[c];
-            s1 += xa[c + 1] * xb[c + 1];
-            s2 += xa[c + 2] * xb[c + 2];
-            s3 += xa[c + 3] * xb[c + 3];
+        // E[a][b] = Q_I[a] . Q_J[b] on the matrix cores: waves 0-3 one 16 x 16 tile each, the k steps
+        // over the columns (zero past m) alternating between two accumulators
+        if (w < 4) {
+          const int a0 = (w >> 1) * 16, b0 = (w & 1) * 16, c16 = lane & 15, kq = lane >> 4;
+          eig_d4 acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
+          const lds_t* xa = QA + (a0 + c16) * mp + kq;
+          const lds_t* xb = QJ + (b0 + c16) * mp + kq;
+          int k0 = 0;
+          for (; k0 + 4 < m; k0 += 8) {
+            acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(xa[k0], xb[k0], acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(xa[k0 + 4], xb[k0 + 4], acc1, 0, 0, 0);
           }
-          for (; c < m; ++c) s0 += xa[c] * xb[c];
-          const double sacc = (s0 + s1) + (s2 + s3);
-          const double eab = (I == J && a == b) ? sacc - 1.0 : sacc;
-          E[a * (GB + 1) + b] = eab;
-          if (a < in && b < jn) {
-            if (fabs(eab) > 1e-8) again = 1;
+          if (k0 < m) acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(xa[k0], xb[k0], acc0, 0, 0, 0);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int a = a0 + kq + 4 * q, b = b0 + c16;
+            const double sacc = acc0[q] + acc1[q];
+            const double eab = (I == J && a == b) ? sacc - 1.0 : sacc;
+            E[a * (GB + 1) + b] = eab;
+            if (a < in && b < jn && fabs(eab) > 1e-8) again = 1;
           }
         }
         __syncthreads();
@@ -567,16 +598,18 @@ __global__ void __launch_bounds__(TW) k_eig_lds(double* A0, int64_t a_stride, in
           __syncthreads();
         }
         if (I == J && !bigE) {   // uniform: |E| <= 1e-6, first order (the dropped terms are <= 1e-12)
-          // Q_J[b] <- Q_J[b] - sum_{a < b} E[a][b] Q_J[a] - E[b][b] / 2 Q_J[b]
-          for (int q = tid; q < GB * mp; q += EW) {
-            const int b = q / mp, c = q - b * mp;
-            const double v = QJ[b * mp + c];
-            double corr = 0.5 * E[b * (GB + 1) + b] * v;
-            for (int a = 0; a < b; ++a) corr += E[a * (GB + 1) + b] * QJ[a * mp + c];
-            QI[b * mp + c] = v - corr;
+          // Q_J[b] <- Q_J[b] - sum_{a < b} E[a][b] Q_J[a] - E[b][b] / 2 Q_J[b] = Q_J - W Q_J with
+          // W[b][a] = E[a][b] (a < b), E[b][b] / 2 (a = b)
+          lds_t* Wm = E + GB * (GB + 1);
+          for (int q = tid; q < GB * GB; q += EW) {
+            const int b = q / GB, a = q - b * GB;
+            Wm[b * (GB + 1) + a] = a < b ? E[a * (GB + 1) + b] : (a == b ? 0.5 * E[b * (GB + 1) + b] : 0.0);
           }
           __syncthreads();
-          for (int q = tid; q < GB * mp; q += EW) QJ[q] = QI[q];
+          gs_wmul<false, true, EW / 64>(QI, QJ, Wm, QJ, mp, m, w, lane);
+          __syncthreads();
+          for (int q = tid; q < GB * mp; q += EW)   // columns past m stay zero (the Gram's k steps read them)
+            if (q - (q / mp) * mp < m) QJ[q] = QI[q];
         } else if (I == J) {
           // exact orthonormalisation of the block: G = Q_J Q_J^T = L L^T (wave 0, right-looking, lane c
           // owns row c), Q_J <- L^-1 Q_J.  A pivot below 1/4 (a vector nearly in the span of the
@@ -616,24 +649,18 @@ __global__ void __launch_bounds__(TW) k_eig_lds(double* A0, int64_t a_stride, in
             }
           }
           __syncthreads();
+          gs_wmul<false, false, EW / 64>(QI, QI, Li, QJ, mp, m, w, lane);   // QI is free (I == J is the last)
+          __syncthreads();
           for (int q = tid; q < GB * mp; q += EW) {
-            const int b = q / mp, c = q - b * mp;
-            double v = 0.0;
-            for (int a = 0; a <= b; ++a) v += Li[b * (GB + 1) + a] * QJ[a * mp + c];
+            const int b = q / mp;
+            if (q - b * mp >= m) continue;   // columns past m stay zero
             bool dr = false;
             for (int z2 = 0; z2 < (ndrop < 16 ? ndrop : 16); ++z2) dr |= dropped[z2] == j0 + b;
-            QI[b * mp + c] = dr ? 0.0 : v;   // QI is free here (I == J is the last of the loop)
+            QJ[q] = dr ? 0.0 : QI[q];
           }
-          __syncthreads();
-          for (int q = tid; q < GB * mp; q += EW) QJ[q] = QI[q];
         } else {
-          // Q_J[b] -= sum_a E[a][b] Q_I[a]
-          for (int q = tid; q < GB * mp; q += EW) {
-            const int b = q / mp, c = q - b * mp;
-            double corr = 0.0;
-            for (int a = 0; a < in; ++a) corr += E[a * (GB + 1) + b] * QI[a * mp + c];
-            QJ[q] = QJ[q] - corr;
-          }
+          // Q_J[b] -= sum_a E[a][b] Q_I[a] (rows of Q_I past `in` are zero)
+          gs_wmul<true, true, EW / 64>(QJ, QJ, E, QI, mp, m, w, lane);
         }
       }
       __syncthreads();
