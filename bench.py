@@ -997,7 +997,9 @@ def bench_si(args, world, rank, dev, dist):
                    "section_fraction": secfrac, "us_per_hvp_per_instance": sec["hvp"] / max(1.0, tot("PASSES")) * 1e6,
                    # HBM TRS service (Exact_RepMat, d >= 8): subproblems whose CG was decided on their
                    # eigenpairs, and CGs skipped by the certified bound (since the context was made)
-                   "trs_cg_checked_skipped": (list(eng.trs_skip_stats()) if args.trs != "tCG" else None)},
+                   "trs_cg_checked_skipped": (list(eng.trs_skip_stats()) if args.trs != "tCG" else None),
+                   # subproblems served from the keyed eigendecomposition cache / served (last solve)
+                   "trs_cache_hits_subproblems": (list(eng.trs_cache_stats()) if args.trs != "tCG" else None)},
     }), flush=True)
 
 

@@ -87,9 +87,26 @@ int riptrm_big_trs_gep(riptrm_ctx* c, int dim, int batch, const double* A, int64
                        double* mineig);
 void riptrm_big_release(riptrm_ctx* c);
 int riptrm_big_reset_cache(riptrm_ctx* c);
+// A per-instance eigendecomposition cache keyed by the point each matrix was built at (the
+// StableIdentification service): the trial point's eigensolve stores its compact eigenpairs, a
+// subproblem built at exactly that point (bitwise) takes them instead of an eigensolve.
+struct KeyedEigCache {
+  const double* keys = nullptr;   // instance b's key at keys + b kstride, klen doubles
+  int64_t kstride = 0;
+  int klen = 0;
+  double* cache = nullptr;        // instance b's entry at cache + b cstride (riptrm_big_kcache_doubles)
+  int64_t cstride = 0;
+  int mode = 0;                   // 1: every subproblem of the call is a hit; 2: store after the eigensolve
+};
+constexpr int RIPTRM_EIG_COMPACT_MAX = 199;   // riptrm_eig::EIG_LDS_MAX: orders with compact eigenpairs
+int64_t riptrm_big_kcache_doubles(int dim, int klen);
+bool riptrm_big_kcache_usable(int dim);   // the hand-written eigensolver serves dim (compact eigenpairs)
+int riptrm_big_kcache_split(riptrm_ctx* c, int dim, const std::vector<int32_t>& ids, const KeyedEigCache& kc,
+                            std::vector<int32_t>& hit, std::vector<int32_t>& miss);
 int riptrm_big_gep_ids(riptrm_ctx* c, int dim, const int32_t* sel, int count, const double* A, int64_t lda,
                        int64_t a_stride, const double* a, int64_t ldv, const double* Delta, double tolhc, double* x,
-                       double* lam1, int32_t* kind, double* mineig, bool mineig_only, bool per_instance);
+                       double* lam1, int32_t* kind, double* mineig, bool mineig_only, bool per_instance,
+                       const KeyedEigCache* kc = nullptr);
 
 
 inline int fail(riptrm_ctx* c, int code, const std::string& msg) {

@@ -247,7 +247,12 @@ __device__ __forceinline__ void gs_wmul(lds_t* Out, const lds_t* Base, const lds
 // T = H^T A H (compact form: an eigenvector of A is H z = H_0 ... H_{m-2} z, applied by the caller,
 // k_refl_apply).  Scratch per matrix (two vectors of >= m doubles, k sc_stride apart): d at d0, e at
 // e0; the reflectors and tau (refl_doubles(m), layout refl_col / refl_tau) at R0 + k r_stride.
-template <int TW>
+// PH selects the phases one launch runs (bit 0 tridiagonalisation, 1 eigenvalues, 2 eigenvectors of T,
+// 3 orthogonality; 15: all, one workgroup per matrix).  The split launches (k_eig_split) run them as
+// four kernels so the eigenvalue and eigenvector phases spread over gridDim.y workgroups per matrix
+// (eigenvalues / vectors m y / Y .. m (y + 1) / Y of workgroup y): d and the split e travel through
+// the slot (d0, e0), the eigenvalues through ev, the vectors through A.
+template <int TW, int PH = 15>
 __global__ void __launch_bounds__(TW) k_eig_lds(double* A0, int64_t a_stride, int lda, int m, double* ev0,
                                                 int64_t ev_stride, double* d0, double* e0, int64_t sc_stride,
                                                 double* R0, int64_t r_stride, int32_t* infos, int vectors,
@@ -269,8 +274,18 @@ __global__ void __launch_bounds__(TW) k_eig_lds(double* A0, int64_t a_stride, in
   double* dg = d0 + (int64_t)k * sc_stride;
   double* eg = e0 + (int64_t)k * sc_stride;
   double* Rg = R0 + (int64_t)k * r_stride;
+  const double eps = DBL_EPSILON;
+  const int ylo = (int)((int64_t)m * blockIdx.y / gridDim.y), yhi = (int)((int64_t)m * (blockIdx.y + 1) / gridDim.y);
+  long long* stp = (PH == 15 && stamps && tid == 0) ? stamps + (int64_t)k * 8 : nullptr;   // phase clocks (diagnostics)
+  if constexpr ((PH & 1) == 0) {   // a later phase: d, split e from the slot
+    if (infos[k] == 1) return;     // non-finite input: the eigenvalues are NaN already
+    for (int i = tid; i < m; i += EW) {
+      vb[i] = dg[i];
+      if (i < m - 1) pb[i] = eg[i];
+    }
+    __syncthreads();
+  } else {
   if (tid == 0) bad = 0;
-  long long* stp = (stamps && tid == 0) ? stamps + (int64_t)k * 8 : nullptr;   // phase clocks (diagnostics)
   if (stp) stp[0] = clock64();
   __syncthreads();
   for (int64_t q = tid; q < (int64_t)m * m; q += EW) {
@@ -405,7 +420,6 @@ __global__ void __launch_bounds__(TW) k_eig_lds(double* A0, int64_t a_stride, in
     if (i < m - 1) pb[i] = P[poff(i + 1) + i];
   }
   __syncthreads();
-  const double eps = DBL_EPSILON;
   // splitting: e_j -> 0 where |e_j| <= 4 eps ||T|| (the tridiagonalisation's own rounding level, so
   // the eigenvalues move by no more than its error); a multiple eigenvalue of A then lives in
   // separate blocks of T (an unreduced tridiagonal has simple eigenvalues)
@@ -416,6 +430,11 @@ __global__ void __launch_bounds__(TW) k_eig_lds(double* A0, int64_t a_stride, in
   for (int j = tid; j < m - 1; j += EW)
     if (fabs(pb[j]) <= 4.0 * eps * tn0) pb[j] = 0.0;
   __syncthreads();
+  if constexpr (PH == 1) {   // the split e for the later launches
+    for (int j = tid; j < m - 1; j += EW) eg[j] = pb[j];
+    return;
+  }
+  }   // PH & 1
   const lds_t* d = vb;
   const lds_t* e = pb;
 
@@ -432,11 +451,14 @@ __global__ void __launch_bounds__(TW) k_eig_lds(double* A0, int64_t a_stride, in
   const double fudge = 2.0 * eps * tnorm + 2.0 * pivmin;
   // multisection: kq (1, 2, 4 or 8) consecutive lanes per eigenvalue test kq points of its interval
   // at once and keep the sub-interval the counts select (the same on every lane of the group)
-  {
-    int kq = 512 / m;   // ~512 lanes in all: the counts are issue-bound, more lanes only add work
+  if constexpr ((PH & 2) != 0) {
+    // ~512 lanes per workgroup: kq = 2 for all 199 eigenvalues of one launch (the counts are
+    // issue-bound there: more lanes only add work), 8 for the ~50 of a split launch's workgroup (every
+    // path the service and riptrm_sym_eig take is split: the same eigenvalues with or without vectors)
+    int kq = 512 / (yhi - ylo);
     kq = kq >= 8 ? 8 : (kq >= 4 ? 4 : (kq >= 2 ? 2 : 1));
-    const int ei = tid / kq, sub = tid - ei * kq, base = (int)(threadIdx.x & 63) - sub;
-    if (ei < m) {
+    const int ei = ylo + tid / kq, sub = tid % kq, base = (int)(threadIdx.x & 63) - sub;
+    if (ei < yhi) {
       double lo = glo - fudge, hi = ghi + fudge;
       for (int it = 0; it < 128; ++it) {
         const double tol = fmax(2.0 * eps * fmax(fabs(lo), fabs(hi)), eps * tnorm);
@@ -458,10 +480,10 @@ __global__ void __launch_bounds__(TW) k_eig_lds(double* A0, int64_t a_stride, in
       if (sub == 0) ev[ei] = 0.5 * (lo + hi);
     }
   }
+  __threadfence_block();
   __syncthreads();
-  const double lam = tid < m ? ev[tid] : 0.0;
   if (stp) stp[2] = clock64();
-  if (!vectors) return;
+  if (!vectors || (PH & 12) == 0) return;
 
   // ---- 3 + 4. per block of eigenvectors, in LDS: the twisted vectors of T, then (vectors = 1)
   // q = H_0 ... H_{m-2} z
@@ -474,9 +496,9 @@ __global__ void __launch_bounds__(TW) k_eig_lds(double* A0, int64_t a_stride, in
   if (!cpt)
     for (int i = tid; i < m - 1; i += EW) tb[i] = Rg[refl_tau(m) + i];
   const double delta = 16.0 * eps * tnorm;
-  for (int t0 = 0; t0 < m; t0 += zb) {
+  for (int t0 = (PH & 4) ? ylo : m; t0 < yhi; t0 += zb) {
     __syncthreads();   // the previous block's rows are out, tau is in
-    if (tid < zb && t0 + tid < m) twisted_vector(Zb + tid * zs, d, e, ev, m, t0 + tid, delta, pivmin);
+    if (tid < zb && t0 + tid < yhi) twisted_vector(Zb + tid * zs, d, e, ev, m, t0 + tid, delta, pivmin);
     // back-transformation of the block: reflectors i = m - 2 .. 0, RB at a time staged from Rg; eight
     // lanes per vector (lane c8 takes j = c8, c8 + 8, ...: its own elements only, so the wave needs
     // no LDS ordering between reflectors), the dot product closed by three butterfly steps
@@ -490,7 +512,7 @@ __global__ void __launch_bounds__(TW) k_eig_lds(double* A0, int64_t a_stride, in
         St[q] = (j > i && j < m) ? Rg[refl_col(m, i) + j - i - 1] : 0.0;
       }
       __syncthreads();
-      if (u < ZB && t0 + u < m) {   // (1024 threads: the upper half idles)
+      if (u < ZB && t0 + u < yhi) {   // (1024 threads: the upper half idles)
         lds_t* Zu = Zb + u * zs;
         for (int i = ihi; i >= ilo; --i) {
           const double tau = tb[i];
@@ -516,12 +538,13 @@ __global__ void __launch_bounds__(TW) k_eig_lds(double* A0, int64_t a_stride, in
     __syncthreads();
     for (int q = tid; q < zb * m; q += EW) {
       const int uu = q / m, c = q - uu * m;
-      if (t0 + uu < m) A[(int64_t)(t0 + uu) * lda + c] = Zb[uu * zs + c];
+      if (t0 + uu < yhi) A[(int64_t)(t0 + uu) * lda + c] = Zb[uu * zs + c];
     }
   }
   __threadfence_block();
   __syncthreads();
   if (stp) stp[3] = stp[4] = clock64();
+  if constexpr ((PH & 8) == 0) return;
 
   // ---- 5. orthogonality: block Gram-Schmidt over close eigenvalues ---------------------------------
   // The twisted vectors are orthogonal to ~eps ||T|| / gap: ~1e-9 for the frame matrices of

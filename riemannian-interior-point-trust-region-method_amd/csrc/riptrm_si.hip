@@ -79,6 +79,8 @@ struct SIParams {
   int32_t* trskind;  // batch                 RIPTRM_TRS_* (host service)
   double* trsmin;    // batch                 smallest eigenvalue of HwNew's matrix (host service)
   double* rs;        // batch x rs_doubles    resume records
+  double* trsC;      // batch x trsC_stride   the service's keyed eigendecomposition cache (tdim <= 199)
+  int64_t trsC_stride;
   int32_t tdim, tdp;
   riptrm_options opt;
 };
@@ -86,6 +88,7 @@ struct SIParams {
 struct Layout {
   int64_t off_x, off_y, off_eta, off_heta, off_escr, off_stats, off_log, total;
   int64_t off_tA, off_tP, off_tids, off_tE, off_ta, off_tx, off_tD, off_tlam, off_tkind, off_tmin, off_rs;   // 0: no HBM subproblem path
+  int64_t off_tC, tC_stride;   // the keyed eigendecomposition cache (0: none)
 };
 
 inline int64_t rup(int64_t a, int64_t m) { return (a + m - 1) / m * m; }
@@ -118,6 +121,7 @@ inline Layout make_layout(int d, int N, int m, int batch, int cap) {
   L.off_stats = o; o = rup(o + 8LL * batch * RIPTRM_STAT_NFIELDS, 256);
   L.off_log = o;   o = rup(o + 8LL * batch * cap * RIPTRM_LOG_NFIELDS, 256);
   L.off_tA = L.off_tP = L.off_tids = L.off_tE = L.off_ta = L.off_tx = L.off_tD = L.off_tlam = L.off_tkind = L.off_tmin = L.off_rs = 0;
+  L.off_tC = L.tC_stride = 0;
   if (si_hbm_trs(d)) {
     const int64_t td = si_manifold_dim(d), tp = si_tdp(d);
     L.off_tA = o;    o = rup(o + 8 * batch * td * td, 256);
@@ -133,6 +137,10 @@ inline Layout make_layout(int d, int N, int m, int batch, int cap) {
     L.off_tkind = o; o = rup(o + 4LL * batch, 256);
     L.off_tmin = o;  o = rup(o + 8LL * batch, 256);
     L.off_rs = o;    o = rup(o + 8 * batch * si_rs_doubles(d), 256);
+    if (td <= RIPTRM_EIG_COMPACT_MAX) {   // keyed by the park point (x, y, mu): 3dd + m + 1 doubles
+      L.tC_stride = rup(riptrm_big_kcache_doubles((int)td, 3 * d * d + m + 1), 32);
+      L.off_tC = o;  o = rup(o + 8 * batch * L.tC_stride, 256);
+    }
   }
   L.total = o;
   return L;
@@ -1012,7 +1020,7 @@ struct Eng {
     if (cact) t[3 * dd + l] = py;
     if (l == 0) t[3 * dd + m] = mu;
   }
-  __device__ void repmat_col(int j, bool want_c, double* uv) {
+  __device__ void repmat_col(int j, bool want_c, double* uv, bool only_c = false) {
     const double* t = P.trsP + (int64_t)b * tp_stride();
     const PV x = load_pv(t);
     const double y = cact ? t[3 * dd + l] : 0.0;
@@ -1020,6 +1028,10 @@ struct Eng {
     AtX a;
     prepare(a, x, y, mu);
     const Frame F = frame(x);
+    if (only_c) {   // a cached eigendecomposition serves the matrix: the coordinates of cxCur only
+      to_coords(F, a.c, P.trsa + (int64_t)b * TDP);
+      return;
+    }
     double* e = uv;
     double* q = uv + TDP;
     for (int k = l; k < DIMM; k += NT) e[k] = (k == j) ? 1.0 : 0.0;
@@ -1524,7 +1536,7 @@ __global__ void __launch_bounds__(si_threads(D)) k_si(SIParams P) {
 
 // the parked instances' subproblem matrices (ids[blockIdx.y], basis vector blockIdx.x): Eng::repmat_col
 template <int D>
-__global__ void __launch_bounds__(si_threads(D)) k_si_repmat(SIParams P, int32_t ids_off, int want_c) {
+__global__ void __launch_bounds__(si_threads(D)) k_si_repmat(SIParams P, int32_t ids_off, int want_c, int only_c) {
   constexpr int NT = si_threads(D);
   __shared__ double sh[2 * NT];
   __shared__ double ser[NT == W ? 8 * W : 1];
@@ -1536,7 +1548,7 @@ __global__ void __launch_bounds__(si_threads(D)) k_si_repmat(SIParams P, int32_t
   const int64_t en = (int64_t)D * P.N;
   e.E = P.trsE ? P.trsE + ((int64_t)b * si_manifold_dim(D) + blockIdx.x) * en
                : trs_lds + (D > 8 ? si_big_lds_doubles(D) : 0);
-  if constexpr (si_hbm_trs(D)) e.repmat_col((int)blockIdx.x, want_c != 0 && blockIdx.x == 0, uv);
+  if constexpr (si_hbm_trs(D)) e.repmat_col((int)blockIdx.x, want_c != 0 && blockIdx.x == 0, uv, only_c != 0);
 }
 
 struct Bound {
@@ -1598,6 +1610,8 @@ static SIParams si_params(riptrm_ctx* c, int mode) {
     P.trskind = (int32_t*)(s->ws + s->L.off_tkind);
     P.trsmin = (double*)(s->ws + s->L.off_tmin);
     P.rs = (double*)(s->ws + s->L.off_rs);
+    P.trsC = s->L.off_tC ? (double*)(s->ws + s->L.off_tC) : nullptr;
+    P.trsC_stride = s->L.tC_stride;
     P.tdim = si_manifold_dim(P.d);
     P.tdp = si_tdp(P.d);
   }
@@ -1643,33 +1657,35 @@ static int si_launch(riptrm_ctx* c, const SIParams& P) {
 }
 
 template <int D>
-static int si_repmat_d(riptrm_ctx* c, const SIParams& P, int ids_off, int cnt, int want_c) {
+static int si_repmat_d(riptrm_ctx* c, const SIParams& P, int ids_off, int cnt, int want_c, int only_c) {
   const size_t shm = ((D > 8 ? (size_t)si_big_lds_doubles(D) : 0) + (P.trsE ? 0 : (size_t)D * P.N)) * sizeof(double);
   if (shm > 64 * 1024)
     HIPCHK(c, hipFuncSetAttribute((const void*)k_si_repmat<D>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm));
-  hipLaunchKernelGGL(k_si_repmat<D>, dim3((unsigned)si_manifold_dim(D), (unsigned)cnt), dim3(si_threads(D)), shm, c->stream,
-                     P, ids_off, want_c);
+  hipLaunchKernelGGL(k_si_repmat<D>, dim3(only_c ? 1u : (unsigned)si_manifold_dim(D), (unsigned)cnt), dim3(si_threads(D)), shm,
+                     c->stream, P, ids_off, want_c, only_c);
   HIPCHK(c, hipGetLastError());
   return RIPTRM_OK;
 }
 
 // the subproblem matrices of the parked instances ids (HBM path: d >= 8), one workgroup per entry of
 // the tangent basis
-static int si_repmat(riptrm_ctx* c, const SIParams& P, const std::vector<int32_t>& ids, int ids_off, int want_c) {
+// (only_c: just the coordinates of cxCur, for subproblems a cached eigendecomposition serves)
+static int si_repmat(riptrm_ctx* c, const SIParams& P, const std::vector<int32_t>& ids, int ids_off, int want_c,
+                     int only_c = 0) {
   if (ids.empty()) return RIPTRM_OK;
   HIPCHK(c, hipMemcpyAsync(P.trsids + ids_off, ids.data(), ids.size() * sizeof(int32_t), hipMemcpyHostToDevice, c->stream));
   const int cnt = (int)ids.size();
   int rc;
   switch (P.d) {
-    case 8: rc = si_repmat_d<8>(c, P, ids_off, cnt, want_c); break;
-    case 9: rc = si_repmat_d<9>(c, P, ids_off, cnt, want_c); break;
-    case 10: rc = si_repmat_d<10>(c, P, ids_off, cnt, want_c); break;
-    case 11: rc = si_repmat_d<11>(c, P, ids_off, cnt, want_c); break;
-    case 12: rc = si_repmat_d<12>(c, P, ids_off, cnt, want_c); break;
-    case 13: rc = si_repmat_d<13>(c, P, ids_off, cnt, want_c); break;
-    case 14: rc = si_repmat_d<14>(c, P, ids_off, cnt, want_c); break;
-    case 15: rc = si_repmat_d<15>(c, P, ids_off, cnt, want_c); break;
-    default: rc = si_repmat_d<16>(c, P, ids_off, cnt, want_c); break;
+    case 8: rc = si_repmat_d<8>(c, P, ids_off, cnt, want_c, only_c); break;
+    case 9: rc = si_repmat_d<9>(c, P, ids_off, cnt, want_c, only_c); break;
+    case 10: rc = si_repmat_d<10>(c, P, ids_off, cnt, want_c, only_c); break;
+    case 11: rc = si_repmat_d<11>(c, P, ids_off, cnt, want_c, only_c); break;
+    case 12: rc = si_repmat_d<12>(c, P, ids_off, cnt, want_c, only_c); break;
+    case 13: rc = si_repmat_d<13>(c, P, ids_off, cnt, want_c, only_c); break;
+    case 14: rc = si_repmat_d<14>(c, P, ids_off, cnt, want_c, only_c); break;
+    case 15: rc = si_repmat_d<15>(c, P, ids_off, cnt, want_c, only_c); break;
+    default: rc = si_repmat_d<16>(c, P, ids_off, cnt, want_c, only_c); break;
   }
   if (rc) return rc;
   HIPCHK(c, hipStreamSynchronize(c->stream));   // ids (host memory) may go after the copy has run
@@ -1789,10 +1805,31 @@ int riptrm_si_solve(riptrm_ctx* ctx, const riptrm_options* opt, const double* x0
   if (int rc = si_launch(ctx, P)) return rc;
   if (!hbm) return RIPTRM_OK;
   // HBM subproblem path: the kernel parks an instance at each subproblem (and each trial point's
-  // eigenvalue test); serve every parked instance in batched passes, resume, until none is parked
+  // eigenvalue test); serve every parked instance in batched passes, resume, until none is parked.
+  // With the keyed cache (tdim <= 199, RIPTRM_SI_CACHE=1; off by default), the trial point's
+  // eigensolve keeps its compact eigenpairs keyed by the park point (x_new, y_new, mu), and a
+  // subproblem parked at exactly that point -- the step was accepted without dual clipping, mu
+  // unchanged -- is served from them: its matrix is not built (only the coordinates of cxCur) and
+  // not decomposed; the matrix would be the same bits (the same k_si_repmat arithmetic at the same
+  // point), so the solve is the uncached one bit for bit (RIPTRM.py:686-692 reuses HwNewmatrix the
+  // same way).  Measured (d = 8 x 64, `OUT=r5w`): 71% of the subproblems hit, yet the line runs at
+  // 246 vs 307 outer it/s without it -- the service is bound by each pass's latency, not by its
+  // number of matrices: a pass with one miss costs the eigensolve of a full one, and the hits' CG
+  // runs as a second pass.  Kept as an opt-in.
   const int B = ctx->si->batch;
   std::vector<double> st((size_t)B * RIPTRM_STAT_NFIELDS);
   P.mode = MODE_RESUME;
+  const char* ce = getenv("RIPTRM_SI_CACHE");
+  const bool cache = P.trsC && ce && ce[0] == '1' && riptrm_big_kcache_usable(tdim);
+  KeyedEigCache kc;
+  kc.keys = P.trsP;
+  kc.kstride = kc.klen = 3 * d * d + ctx->si->prob.m + 1;
+  kc.cache = P.trsC;
+  kc.cstride = P.trsC_stride;
+  ctx->big_cache_hits = ctx->big_subproblems = 0;
+  if (cache)   // no entry of an earlier solve is valid
+    HIPCHK(ctx, hipMemset2DAsync(P.trsC, (size_t)P.trsC_stride * sizeof(double), 0, sizeof(double), B, ctx->stream));
+  std::vector<int32_t> hit, miss;
   while (true) {
     HIPCHK(ctx, hipMemcpyAsync(st.data(), P.stats, st.size() * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
@@ -1804,18 +1841,36 @@ int riptrm_si_solve(riptrm_ctx* ctx, const riptrm_options* opt, const double* x0
     }
     if (trs.empty() && mine.empty()) break;
     const int64_t tp = si_tdp(d);
-    if (int rc = si_repmat(ctx, P, trs, 0, 1)) return rc;
+    if (cache) {
+      if (int rc = riptrm_big_kcache_split(ctx, tdim, trs, kc, hit, miss)) return rc;
+    } else {
+      miss = trs;
+      hit.clear();
+    }
+    ctx->big_cache_hits += (int64_t)hit.size();
+    ctx->big_subproblems += (int64_t)trs.size();
+    if (int rc = si_repmat(ctx, P, miss, 0, 1)) return rc;
+    if (int rc = si_repmat(ctx, P, hit, (int)miss.size(), 1, 1)) return rc;
     if (int rc = si_repmat(ctx, P, mine, B, 0)) return rc;
-    if (!trs.empty())
-      if (int rc = riptrm_big_gep_ids(ctx, tdim, trs.data(), (int)trs.size(), P.trsA, tdim, (int64_t)tdim * tdim, P.trsa,
+    if (!miss.empty())
+      if (int rc = riptrm_big_gep_ids(ctx, tdim, miss.data(), (int)miss.size(), P.trsA, tdim, (int64_t)tdim * tdim, P.trsa,
                                       tp, P.trsD, opt->trs_tolhardcase, P.trsx, P.trslam, P.trskind, nullptr, false,
                                       true))
         return rc;
-    if (!mine.empty())
+    if (!hit.empty()) {
+      kc.mode = 1;
+      if (int rc = riptrm_big_gep_ids(ctx, tdim, hit.data(), (int)hit.size(), P.trsA, tdim, (int64_t)tdim * tdim, P.trsa,
+                                      tp, P.trsD, opt->trs_tolhardcase, P.trsx, P.trslam, P.trskind, nullptr, false,
+                                      true, &kc))
+        return rc;
+    }
+    if (!mine.empty()) {
+      kc.mode = 2;
       if (int rc = riptrm_big_gep_ids(ctx, tdim, mine.data(), (int)mine.size(), P.trsA, tdim, (int64_t)tdim * tdim,
                                       P.trsa, tp, P.trsD, opt->trs_tolhardcase, nullptr, nullptr, nullptr, P.trsmin, true,
-                                      true))
+                                      true, cache ? &kc : nullptr))
         return rc;
+    }
     if (int rc = si_launch(ctx, P)) return rc;
   }
   return RIPTRM_OK;

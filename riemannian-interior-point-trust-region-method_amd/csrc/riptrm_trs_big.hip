@@ -1205,6 +1205,54 @@ __global__ void __launch_bounds__(256) k_cache_load(DevParams P, Bat B, const do
   if (e == 0) *q.info = 0;
 }
 
+// ---- the keyed per-instance cache of the StableIdentification service (KeyedEigCache) ------------
+// entry of order m, key length kl: [valid, 7 pad][key: kl to 8][ev: vpad(m)][Z: m x m][reflectors + tau]
+__host__ __device__ inline int64_t kc_kpad(int kl) { return (kl + 7) / 8 * 8; }
+__host__ __device__ inline int64_t kc_doubles(int m, int kl) {
+  return 8 + kc_kpad(kl) + vpad(m) + (int64_t)m * m + (int64_t)riptrm_eig::refl_doubles(m);
+}
+
+// hits[k] = 1 iff instance ids[k]'s entry is valid and its key equals the instance's key bit for bit
+__global__ void __launch_bounds__(256) k_kc_check(Bat B, const double* keys, int64_t kstride, int kl, const double* cache,
+                                                  int64_t cstride, int32_t* hits) {
+  const int k = blockIdx.y, b = B.ids[k];
+  const double* C = cache + (int64_t)b * cstride;
+  const double* K = keys + (int64_t)b * kstride;
+  int ok = C[0] == 1.0;
+  for (int i = threadIdx.x; i < kl; i += 256) ok &= K[i] == C[8 + i];
+  ok = __syncthreads_and(ok);
+  if (threadIdx.x == 0) hits[k] = ok;
+}
+
+// after an eigensolve with compact vectors: slot k's eigenvalues, Z (the slot's matrix, lda m), the
+// reflectors and instance ids[k]'s key -> its entry; valid iff the eigensolve succeeded
+__global__ void __launch_bounds__(256) k_kc_store(Bat B, int m, const double* keys, int64_t kstride, int kl, double* cache,
+                                                  int64_t cstride) {
+  const int k = blockIdx.y, b = B.ids[k];
+  const Slot q = slot_at(B, k);
+  double* C = cache + (int64_t)b * cstride;
+  const int64_t kp = kc_kpad(kl), e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const double* R = B.base + (int64_t)k * B.sd + off_refl(B.N);
+  if (e < kl) C[8 + e] = keys[(int64_t)b * kstride + e];
+  if (e < m) C[8 + kp + e] = q.v[VS_EV][e];
+  if (e < (int64_t)m * m) C[8 + kp + vpad(m) + e] = q.M[e];
+  if (e < (int64_t)riptrm_eig::refl_doubles(m)) C[8 + kp + vpad(m) + (int64_t)m * m + e] = R[e];
+  if (e == 0) C[0] = *q.info == 0 ? 1.0 : 0.0;
+}
+
+// a hit: instance ids[k]'s cached eigenvalues, Z and reflectors -> slot k
+__global__ void __launch_bounds__(256) k_kc_load(Bat B, int m, int kl, const double* cache, int64_t cstride) {
+  const int k = blockIdx.y, b = B.ids[k];
+  const Slot q = slot_at(B, k);
+  const double* C = cache + (int64_t)b * cstride;
+  const int64_t kp = kc_kpad(kl), e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  double* R = B.base + (int64_t)k * B.sd + off_refl(B.N);
+  if (e < m) q.v[VS_EV][e] = C[8 + kp + e];
+  if (e < (int64_t)m * m) q.M[e] = C[8 + kp + vpad(m) + e];
+  if (e < (int64_t)riptrm_eig::refl_doubles(m)) R[e] = C[8 + kp + vpad(m) + (int64_t)m * m + e];
+  if (e == 0) *q.info = 0;
+}
+
 __global__ void k_cache_invalidate(double* cache, int64_t N, int batch) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b < batch) cache[(int64_t)b * cache_doubles(N) + N * N + 3 * vpad(N)] = 0.0;
@@ -1341,7 +1389,31 @@ static int launch_eig(riptrm_ctx* c, int cnt, int m, double* A, int64_t a_stride
                       long long* stamps) {
   const size_t shm = riptrm_eig::eig_lds_bytes(m);
   const char* t = getenv("RIPTRM_EIG_THREADS");
-  if (!(t && atoi(t) == 512)) {
+  const char* sp = getenv("RIPTRM_EIG_SPLIT");
+  if (!stamps && !(sp && sp[0] == '0') && !(t && atoi(t) == 512)) {
+    // four launches: the tridiagonalisation (one workgroup per matrix), the eigenvalues and the
+    // vectors of T over ~50 indices per workgroup (four per matrix at m = 199: the whole chip for a
+    // batch of 64), the orthogonality pass (one per matrix).  The same arithmetic as one launch.
+    const int yv = (m + 49) / 50;
+    HIPCHK(c, hipFuncSetAttribute((const void*)riptrm_eig::k_eig_lds<1024, 1>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)shm));
+    hipLaunchKernelGGL((riptrm_eig::k_eig_lds<1024, 1>), dim3(cnt), dim3(1024), shm, c->stream, A, a_stride, lda, m, ev,
+                       ev_stride, d, e, sc_stride, R, r_stride, infos, vectors, nullptr);
+    HIPCHK(c, hipFuncSetAttribute((const void*)riptrm_eig::k_eig_lds<512, 2>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)shm));
+    hipLaunchKernelGGL((riptrm_eig::k_eig_lds<512, 2>), dim3(cnt, yv), dim3(512), shm,
+                       c->stream, A, a_stride, lda, m, ev, ev_stride, d, e, sc_stride, R, r_stride, infos, vectors, nullptr);
+    if (vectors) {
+      HIPCHK(c, hipFuncSetAttribute((const void*)riptrm_eig::k_eig_lds<512, 4>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)shm));
+      hipLaunchKernelGGL((riptrm_eig::k_eig_lds<512, 4>), dim3(cnt, yv), dim3(512), shm, c->stream, A, a_stride, lda, m, ev,
+                         ev_stride, d, e, sc_stride, R, r_stride, infos, vectors, nullptr);
+      HIPCHK(c, hipFuncSetAttribute((const void*)riptrm_eig::k_eig_lds<1024, 8>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)shm));
+      hipLaunchKernelGGL((riptrm_eig::k_eig_lds<1024, 8>), dim3(cnt), dim3(1024), shm, c->stream, A, a_stride, lda, m, ev,
+                         ev_stride, d, e, sc_stride, R, r_stride, infos, vectors, nullptr);
+    }
+  } else if (!(t && atoi(t) == 512)) {
     HIPCHK(c, hipFuncSetAttribute((const void*)riptrm_eig::k_eig_lds<1024>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   (int)shm));
     hipLaunchKernelGGL(riptrm_eig::k_eig_lds<1024>, dim3(cnt), dim3(1024), shm, c->stream, A, a_stride, lda, m, ev, ev_stride,
@@ -1638,28 +1710,68 @@ int riptrm_big_reset_cache(riptrm_ctx* c) {
 // or, with per_instance, only marks that subproblem: kind = RIPTRM_TCG_EIGFAIL / mineig = NaN (the
 // caller stops that instance, RIPTRM_ERR_EIGEN).  Synchronises.  Serves riptrm_trs_gep above dim 96 and the StableIdentification solve's parked
 // instances (riptrm_si.hip).
-int riptrm_big_gep_ids(riptrm_ctx* c, int dim, const int32_t* sel, int count, const double* A, int64_t lda,
-                       int64_t a_stride, const double* a, int64_t ldv, const double* Delta, double tolhc, double* x,
-                       double* lam1, int32_t* kind, double* mineig, bool mineig_only, bool per_instance) {
+static_assert(RIPTRM_EIG_COMPACT_MAX == riptrm_eig::EIG_LDS_MAX, "riptrm_ctx.h's copy of EIG_LDS_MAX");
+int64_t riptrm_big_kcache_doubles(int dim, int klen) { return kc_doubles(dim, klen); }
+bool riptrm_big_kcache_usable(int dim) { return eig_compact(dim); }
+
+// the instances ids whose cache entry matches their key (hit) and the others (miss).  Synchronises.
+int riptrm_big_kcache_split(riptrm_ctx* c, int dim, const std::vector<int32_t>& ids, const KeyedEigCache& kc,
+                            std::vector<int32_t>& hit, std::vector<int32_t>& miss) {
+  hit.clear();
+  miss.clear();
+  if (ids.empty()) return RIPTRM_OK;
   if (!c->big_ws || c->big_order < dim || c->big_slots < 1)
     return fail(c, RIPTRM_E_STATE, "Exact_RepMat above dim 96 needs riptrm_trs_bind_workspace (order >= dim)");
   const Bat Bt = bat_of(c);
+  const int S = c->big_slots;
+  int32_t* hits = tail_of(c) + 3 * S + 8;
+  std::vector<int32_t> h(S);
+  for (size_t k0 = 0; k0 < ids.size(); k0 += (size_t)S) {
+    const int cnt = (int)std::min<size_t>((size_t)S, ids.size() - k0);
+    if (int rc = put_ids(c, Bt, ids.data() + k0, cnt)) return rc;
+    hipLaunchKernelGGL(k_kc_check, dim3(1, cnt), dim3(256), 0, c->stream, Bt, kc.keys, kc.kstride, kc.klen, kc.cache,
+                       kc.cstride, hits);
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipMemcpyAsync(h.data(), hits, (size_t)cnt * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    for (int k = 0; k < cnt; ++k) (h[k] ? hit : miss).push_back(ids[k0 + k]);
+  }
+  return RIPTRM_OK;
+}
+
+int riptrm_big_gep_ids(riptrm_ctx* c, int dim, const int32_t* sel, int count, const double* A, int64_t lda,
+                       int64_t a_stride, const double* a, int64_t ldv, const double* Delta, double tolhc, double* x,
+                       double* lam1, int32_t* kind, double* mineig, bool mineig_only, bool per_instance,
+                       const KeyedEigCache* kc) {
+  if (!c->big_ws || c->big_order < dim || c->big_slots < 1)
+    return fail(c, RIPTRM_E_STATE, "Exact_RepMat above dim 96 needs riptrm_trs_bind_workspace (order >= dim)");
+  const Bat Bt = bat_of(c);
+  const int kmode = (kc && kc->cache && eig_compact(dim)) ? kc->mode : 0;
+  if (kmode == 1 && mineig_only) return fail(c, RIPTRM_E_STATE, "gep_ids: cached eigenpairs serve subproblems only");
   std::vector<int32_t> info(c->big_slots);
   std::vector<double> skip_done;   // SC_DONE of the pass's slots (4 = CG skipped by k_cg_wg's bound)
   for (int b0 = 0; b0 < count; b0 += c->big_slots) {
     const int cnt = std::min(c->big_slots, count - b0);
     skip_done.clear();
     if (int rc = put_ids(c, Bt, sel + b0, cnt)) return rc;
-    hipLaunchKernelGGL(k_load, dim3(blocks_of((int64_t)dim * dim, 256), cnt), dim3(256), 0, c->stream, Bt, dim, A, lda,
-                       a_stride, a, ldv);
+    // (a hit needs only a: the matrix's first dim entries are copied too and then replaced)
+    hipLaunchKernelGGL(k_load, dim3(blocks_of(kmode == 1 ? (int64_t)dim : (int64_t)dim * dim, 256), cnt), dim3(256), 0,
+                       c->stream, Bt, dim, A, lda, a_stride, a, ldv);
     HIPCHK(c, hipGetLastError());
     if (mineig_only) {
-      if (int rc = eig_batched(c, Bt, cnt, false, dim, 0, dim)) return rc;
+      if (int rc = eig_batched(c, Bt, cnt, kmode == 2, dim, 0, dim)) return rc;
+      if (kmode == 2)
+        hipLaunchKernelGGL(k_kc_store, dim3(blocks_of((int64_t)dim * dim, 256), cnt), dim3(256), 0, c->stream, Bt, dim,
+                           kc->keys, kc->kstride, kc->klen, kc->cache, kc->cstride);
     } else if (eig_compact(dim)) {
-      // eigenpairs first, then the CG in eigen-coordinates (k_cg_diag), skipped where the certified
-      // bound shows its candidate cannot win (per_instance callers; RIPTRM_CG_SKIP=0: never)
+      // eigenpairs first (or the cached ones), then the CG in eigen-coordinates (k_cg_diag), skipped
+      // where the certified bound shows its candidate cannot win (per_instance; RIPTRM_CG_SKIP=0: never)
       const bool skip = per_instance && !getenv_is("RIPTRM_CG_SKIP", '0');
-      if (int rc = eig_batched(c, Bt, cnt, true, dim, 0, dim)) return rc;
+      if (kmode == 1)
+        hipLaunchKernelGGL(k_kc_load, dim3(blocks_of((int64_t)dim * dim, 256), cnt), dim3(256), 0, c->stream, Bt, dim,
+                           kc->klen, kc->cache, kc->cstride);
+      else if (int rc = eig_batched(c, Bt, cnt, true, dim, 0, dim))
+        return rc;
       if (int rc = compact_trs(c, Bt, cnt, dim, 0, dim, Delta, 1, tolhc, skip)) return rc;
       if (skip) {
         skip_done.resize(cnt);

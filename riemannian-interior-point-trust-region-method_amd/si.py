@@ -385,6 +385,13 @@ class SIBatch:
         self.ctx.check(self.lib.riptrm_trs_skip_stats(self.ctx.h, ctypes.byref(a), ctypes.byref(b)), "riptrm_trs_skip_stats")
         return int(a.value), int(b.value)
 
+    def trs_cache_stats(self):
+        """(subproblems served from the keyed eigendecomposition cache, subproblems served) of the
+        last solve on the HBM Exact_RepMat path (riptrm_trs_cache_stats)."""
+        h, t = ctypes.c_int64(0), ctypes.c_int64(0)
+        self.ctx.check(self.lib.riptrm_trs_cache_stats(self.ctx.h, ctypes.byref(h), ctypes.byref(t)), "riptrm_trs_cache_stats")
+        return int(h.value), int(t.value)
+
     def profile_enable(self, on: bool = True):
         self.ctx.check(self.lib.riptrm_si_profile_enable(self.ctx.h, 1 if on else 0), "riptrm_si_profile_enable")
 

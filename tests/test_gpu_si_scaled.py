@@ -253,6 +253,42 @@ def test_si_exact_cg_skip_is_bitwise_neutral(d, sos, bench_starts, monkeypatch):
     np.testing.assert_array_equal(r1.y.cpu().numpy(), r0.y.cpu().numpy())
 
 
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("sos", [True, False])
+def test_si_exact_eigen_cache_is_bitwise_neutral(sos, monkeypatch):
+    """The SI service's keyed eigendecomposition cache (riptrm_si_solve, KeyedEigCache): a subproblem
+    parked at exactly the point of the trial eigen-test before it (accepted step, no dual clipping,
+    same mu) takes that eigensolve's compact eigenpairs and builds no matrix, as RIPTRM.py:686-692
+    reuses HwNewmatrix.  The matrix would be the same bits, so RIPTRM_SI_CACHE=1 (opt-in: the
+    lock-step service is pass-latency-bound) and the default must give the same logs and
+    x / y bit for bit; with the second-order test the bench's d = 8 starts must really hit (the test
+    is not vacuous)."""
+    import bench
+    import si
+    d = 8
+    xs, ys, (X, XP, h, constset) = bench.si_starts(8, list(range(8)), d)
+    cons = si.expand_constset(constset)
+    mk = lambda: _load(si.SIBatch(d, X.shape[1], cons.shape[0], len(xs), log_capacity=1024), X, XP, h, cons)   # noqa: E731
+    opt = {"maxiter": 3, "tolresid": 0.0, "maxtime": 1e9, "TRS_solver": "Exact_RepMat",
+           "second_order_stationarity": sos, "manviofun": si.si_manviofun}
+    monkeypatch.setenv("RIPTRM_SI_CACHE", "1")
+    e1 = mk()
+    r1 = e1.solve(xs, ys, opt)
+    hits, subs = e1.trs_cache_stats()
+    monkeypatch.setenv("RIPTRM_SI_CACHE", "0")
+    e0 = mk()
+    r0 = e0.solve(xs, ys, opt)
+    assert e0.trs_cache_stats()[0] == 0
+    print(f"sos={sos}: {hits} of {subs} subproblems served from the cache")
+    assert subs > 0
+    assert (hits > 0) == sos, hits   # without the second-order test there is no trial eigensolve to keep
+    for b in range(len(xs)):
+        for key in ("cost", "residual", "normdx", "dxtype", "mineigvalHw", "inner_status", "radius_update"):
+            assert r1.log(b)[key] == r0.log(b)[key], (b, key)
+    np.testing.assert_array_equal(r1.x.cpu().numpy(), r0.x.cpu().numpy())
+    np.testing.assert_array_equal(r1.y.cpu().numpy(), r0.y.cpu().numpy())
+
+
 def _load(eng, X, XP, h, cons):
     eng.load(X, XP, h, cons)
     return eng
