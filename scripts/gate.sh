@@ -26,6 +26,7 @@
 #   si_prof          rocprofv3 stats of the SI bench
 #   si_d8_exact      bench.py --problem si --si-dim 8 --trs Exact_RepMat --batch 64 with its CPU baseline
 #   si_d8_exact_prof rocprofv3 stats of the same
+#   (XB: extra bench.py arguments for the cfg1, shared and si steps, e.g. smaller CPU budgets)
 #   dist2            bench.py --gpus 2 --same-device --backend gloo at the configs[3] per-rank shape
 set -u
 cd "$GRAFT_REPO_ROOT"
@@ -72,15 +73,15 @@ step() {
       --source "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate passes, of python bench.py --cpu-budget 0 --warmup 1 --steps 2 ($O)" \
       && cp $O/r4_traffic_spass_sup.json profiles/ ;;   # the later headline step in this call reads it (bench.py --traffic-json)
   cfg1)
-    timeout -k 10 240 python bench.py --dim 1000 --batch 1 > $O/bench_cfg1.json 2> $O/bench_cfg1.err || { tail $O/bench_cfg1.err; return 1; }
+    timeout -k 10 400 python bench.py --dim 1000 --batch 1 ${XB:-} > $O/bench_cfg1.json 2> $O/bench_cfg1.err || { tail $O/bench_cfg1.err; return 1; }
     val $O/bench_cfg1.json cfg1 ;;
   cfg1_trace)
     timeout -k 10 120 python scripts/persist_trace.py 1000 > $O/cfg1_trace.txt 2>&1 || { tail $O/cfg1_trace.txt; return 1; }
     tail -5 $O/cfg1_trace.txt ;;
   shared)
-    timeout -k 10 300 python bench.py --layout shared > $O/bench_shared.json 2> $O/bench_shared.err || { tail $O/bench_shared.err; return 1; }
+    timeout -k 10 300 python bench.py --layout shared ${XB:-} > $O/bench_shared.json 2> $O/bench_shared.err || { tail $O/bench_shared.err; return 1; }
     val $O/bench_shared.json shared
-    timeout -k 10 300 python bench.py --layout shared --batch 256 > $O/bench_shared_b256.json 2> $O/bench_shared_b256.err \
+    timeout -k 10 300 python bench.py --layout shared --batch 256 ${XB:-} > $O/bench_shared_b256.json 2> $O/bench_shared_b256.err \
       || { tail $O/bench_shared_b256.err; return 1; }
     val $O/bench_shared_b256.json shared256 ;;
   shared_prof)
@@ -88,7 +89,7 @@ step() {
       --batch 256 --cpu-budget 0 > $O/bench_shared_rocprof.json 2> $O/shared_rocprof.log || return 1
     note "shared rocprof ok" ;;
   si)
-    timeout -k 10 300 python bench.py --problem si --batch 256 > $O/bench_si_b256.json 2> $O/bench_si.err || { tail $O/bench_si.err; return 1; }
+    timeout -k 10 400 python bench.py --problem si --batch 256 ${XB:-} > $O/bench_si_b256.json 2> $O/bench_si.err || { tail $O/bench_si.err; return 1; }
     val $O/bench_si_b256.json si ;;
   stiefel)
     timeout -k 10 180 python bench.py --problem stiefel --dim 200 --batch 256 > $O/bench_stiefel_b256.json 2> $O/st256.err || return 1
