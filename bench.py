@@ -595,6 +595,10 @@ def main():
                                                    "partial sums of every element the S-pass left"),
                               "kernel": "k_state (tCG step, Sphere projection / retraction, trial point, acceptance; "
                                         "runs beside the other stream group's S-pass)"}
+        spass_roofline = None
+        if args.trs == "Exact_RepMat" and 96 < n - 1 <= 199 and rank == 0:
+            # the eigensolver, not the S-pass, sets this line's time: price it, keep the S-pass in detail
+            spass_roofline, roofline = roofline, eig_roofline(n - 1, B, dev)
         cpu = None
         if args.cpu_budget > 0 and world == 1:
             positions = window_positions(W, K, args.cycle)
@@ -652,14 +656,15 @@ def main():
                        "state_kernel_ms": prof["state_ms"], "state_launches": prof["state_launches"],
                        "gemv_launches": prof["gemv_launches"],
                        "state_kernel_roofline": state_roofline,
+                       **({"spass_roofline": spass_roofline} if spass_roofline else {}),
                        **({"spass_calibration": cal} if cal.get("ms_per_launch_tile") else {}),
                        **({"exact_repmat_note": (
                            "manifold.dim > 96: the subproblems are served in batched passes between lock-step "
-                           "chunks (csrc/riptrm_trs_big.hip); the pass, not the S-pass priced in `roofline`, sets "
-                           "this line's time: rocSOLVER's batched dsyevd (tridiagonalisation + divide and conquer "
-                           "on (n-1) x (n-1) matrices, latency-bound) takes most of the GPU time "
-                           "(profiles/r4_exact_rocprofv3_kernel_stats.csv); a subproblem at an accepted trial "
-                           "point reuses that point's eigenpairs (riptrm_trs_bind_cache)"),
+                           "chunks (csrc/riptrm_trs_big.hip); the pass, not the S-pass (detail.spass_roofline), sets "
+                           "this line's time: the hand-written eigensolver (csrc/riptrm_eig.h, order <= 199; rocSOLVER "
+                           "dsyevd above) takes most of the GPU time (profiles/r5_exact_rocprofv3_kernel_stats.csv); "
+                           "the CG runs in its eigen-coordinates; a subproblem at an accepted trial point reuses that "
+                           "point's eigenpairs (riptrm_trs_bind_cache)"),
                            "trs_cache": dict(zip(("hits", "subproblems"), eng.trs_cache_stats()))}
                           if args.trs == "Exact_RepMat" and n - 1 > engine.C["RIPTRM_TRS_DIM_MAX"] else {})},
         }
@@ -879,6 +884,65 @@ def si_cpu_pool(K: int, budget_s: float, procs: int, trs: str, d: int = 5, inner
                        f"rate x {procs}, evaluation time excluded as RIPTRM.py:932-941")}
 
 
+LDS_BYTES_PER_CLK = 256       # MI355X_MICROARCH.md: LDS 64 dwords wide per clock per CU
+CLOCK_HZ = 2.4e9              # max engine clock
+
+
+def eig_roofline(m: int, B: int, dev, reps: int = 5):
+    """The Exact_RepMat HBM service's dominant kernel, the hand-written eigensolver (csrc/riptrm_eig.h,
+    manifold.dim <= 199), timed live with HIP events on the library's stream: B matrices of order m
+    shaped like the frame matrices (O(1) symmetric part plus diagonal barrier terms up to 1e6),
+    compact eigenpairs as the service takes them.  Bound: LDS of the CUs it occupies (one workgroup
+    per matrix holds it in LDS for the tridiagonalisation, its dominant phase); algorithmic bytes =
+    that phase's LDS traffic, per column with r trailing rows r^2 doubles read by the symmetric
+    mat-vec and r (r + 1) read + written by the rank-2 update."""
+    import ctypes
+
+    import numpy as np
+    import torch
+    import trs
+    rs = np.random.RandomState(m)
+    mats = []
+    for _ in range(B):
+        D = rs.randn(m, m) / np.sqrt(m)
+        D = D + D.T + np.diag(np.where(rs.rand(m) < 0.3, 10.0 ** rs.uniform(2, 6, m), 0.0))
+        mats.append(D)
+    A = torch.tensor(np.stack(mats), dtype=torch.float64, device=dev)
+    V = A.clone()
+    w = torch.empty((B, m), dtype=torch.float64, device=dev)
+    info = torch.empty(B, dtype=torch.int32, device=dev)
+    ctx = trs._context(A.device)
+    p = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    call = lambda: ctx.check(ctx.lib.riptrm_sym_eig(ctx.h, m, B, p(V), m, m * m, p(w), m, p(info), 2), "riptrm_sym_eig")  # noqa: E731
+    for _ in range(2):
+        V.copy_(A)
+        call()
+    ts = []
+    for _ in range(reps):
+        V.copy_(A)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        call()
+        e1.record()
+        torch.cuda.synchronize(dev)
+        ts.append(e0.elapsed_time(e1) / 1e3)
+    t = sorted(ts)[len(ts) // 2]
+    per = 8.0 * sum(2 * r * r + r for r in range(1, m))
+    cus = min(B, 256)
+    ach = B * per / t / 1e9
+    peak = cus * LDS_BYTES_PER_CLK * CLOCK_HZ / 1e9
+    return {"bound": "lds", "achieved": ach, "peak": peak, "unit": "GB/s", "frac": ach / peak, "traffic": None,
+            "kernel": (f"riptrm_eig (k_eig_lds: tridiagonalisation one 1024-thread workgroup per matrix, eigenvalues / "
+                       f"twisted vectors over ~50 indices per workgroup, MFMA Gram-Schmidt), {B} matrices of order {m}, "
+                       "compact eigenpairs"),
+            "bytes_definition": ("tridiagonalisation's LDS traffic per matrix, sum over columns of (2 r^2 + r) doubles "
+                                 f"(symmetric mat-vec + rank-2 update), {per / 1e6:.1f} MB at m={m}; peak = LDS of the "
+                                 f"{cus} CUs one workgroup per matrix occupies ({LDS_BYTES_PER_CLK} B/clock at 2.4 GHz)"),
+            "avg_launch_us": t * 1e6, "bytes_per_launch": B * per,
+            "why": ("no HBM / MFMA roof: the matrices live in LDS; the tridiagonalisation's dependent column steps "
+                    "(three workgroup barriers each) keep it latency-bound")}
+
+
 def si_roofline(args, d, hvps, kern_s, sec, passes):
     """The SI line's roof.  k_si runs each instance's whole solve on one wave: a dependent chain of
     d x d products, LDS round trips and wave reductions, no HBM stream and no matrix-core work worth
@@ -956,6 +1020,7 @@ def bench_si(args, world, rank, dev, dist):
     T = float(tmax.item())
     if rank != 0:
         return
+    tdim = d * (d - 1) // 2 + d * (d + 1)   # manifold.dim of Product(Skew(d), SPD(d), SPD(d))
     cpu = None
     if args.cpu_budget > 0 and world == 1:
         ipo = inner / outer if outer > 0 else None
@@ -992,6 +1057,8 @@ def bench_si(args, world, rank, dev, dist):
                    "trs_solver": args.trs,
                    "global_batch": B * world, "parallelism": f"instance-sharded x{world}", "world_size": world},
         "roofline": si_roofline(args, d, hvps, kern_s, sec, tot("PASSES")),
+        # the HBM TRS service's eigensolver at this manifold.dim (the line's other half: DESIGN 7b)
+        **({"service_eig_roofline": eig_roofline(tdim, B, dev)} if args.trs != "tCG" and 96 < tdim <= 199 else {}),
         "cpu_baseline": cpu,
         "detail": {"inner_iterations_per_s": inner / T, "tcg_iterations_per_s": tcg / T, "hvps_per_s": hvps / T,
                    "section_fraction": secfrac, "us_per_hvp_per_instance": sec["hvp"] / max(1.0, tot("PASSES")) * 1e6,

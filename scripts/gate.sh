@@ -24,6 +24,7 @@
 #   exact1000        bench.py --trs Exact_RepMat --dim 1000 --batch 1 with its (sampled) CPU baseline
 #   si_pmc           issue-rate PMC pass of k_si (SQ_*) -> profiles/r5_si_pmc.json, read by the si step
 #   si_prof          rocprofv3 stats of the SI bench
+#   si_d8_pmc        issue-rate PMC pass of k_si at d = 8 (Exact) -> profiles/r5_si_pmc_d8.json, read by si_d8_exact
 #   si_d8_exact      bench.py --problem si --si-dim 8 --trs Exact_RepMat --batch 64 with its CPU baseline
 #   si_d8_exact_prof rocprofv3 stats of the same
 #   (XB: extra bench.py arguments for the cfg1, shared and si steps, e.g. smaller CPU budgets)
@@ -138,8 +139,16 @@ for b in (256, 2048):
     timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/si -o si -- python bench.py --problem si \
       --batch 256 --cpu-budget 0 > $O/bench_si_rocprof.json 2> $O/si_rocprof.log || return 1
     note "si rocprof ok" ;;
+  si_d8_pmc)
+    timeout -s KILL 240 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_INSTS_VALU \
+      --output-format csv -d $O/sid8pmc -o p -- python bench.py --problem si --si-dim 8 --trs Exact_RepMat --batch 64 \
+      --cpu-budget 0 --steps 4 > $O/sid8pmc.log 2>&1 || { tail $O/sid8pmc.log; return 1; }
+    python scripts/si_pmc_summary.py $(find $O/sid8pmc -name "*counter_collection.csv" | head -1) $O/r5_si_pmc_d8.json --d 8 \
+      --source "rocprofv3 --pmc SQ_WAVE_CYCLES SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_INSTS_VALU -- python bench.py --problem si --si-dim 8 --trs Exact_RepMat --batch 64 --cpu-budget 0 --steps 4 ($O)" \
+      && cp $O/r5_si_pmc_d8.json profiles/ ;;
   si_d8_exact)
     timeout -k 10 900 python bench.py --problem si --si-dim 8 --trs Exact_RepMat --batch 64 --cpu-budget 100 --cpu-pool-budget 150 \
+      --si-pmc-json profiles/r5_si_pmc_d8.json \
       > $O/bench_si_d8_exact.json 2> $O/bench_si_d8_exact.err || { tail $O/bench_si_d8_exact.err; return 1; }
     val $O/bench_si_d8_exact.json si_d8_exact ;;
   si_d8_exact_prof)
