@@ -305,8 +305,10 @@ __global__ void __launch_bounds__(TW) k_eig_lds(double* A0, int64_t a_stride, in
   if (tid == 0) infos[k] = 0;
 
   // ---- 1. tridiagonalisation (dsytd2, lower) ----------------------------------------------------
+  long long acc_refl = 0, acc_symv = 0, tq = 0;   // stamps: cycles in the reflector / symv sections
   for (int i = 0; i < m - 1; ++i) {
     const int r = m - i - 1;   // the trailing rows / columns i + 1 .. m - 1
+    if (stp) tq = clock64();
     if (w == 0) {
       double s = 0.0;
       for (int j = i + 2 + lane; j < m; j += 64) {
@@ -338,6 +340,11 @@ __global__ void __launch_bounds__(TW) k_eig_lds(double* A0, int64_t a_stride, in
       }
     }
     __syncthreads();
+    if (stp) {
+      const long long t1 = clock64();
+      acc_refl += t1 - tq;
+      tq = t1;
+    }
     const double tau = scal[0];
     if (tau != 0.0) {   // uniform
       // p = tau A22 v: TPR = EW / 256 threads per row (r <= 256), each over a part of the row -- its
@@ -386,6 +393,7 @@ __global__ void __launch_bounds__(TW) k_eig_lds(double* A0, int64_t a_stride, in
         if (l < r && h == 0) pb[l] = tau * acc;
       }
       __syncthreads();
+      if (stp) acc_symv += clock64() - tq;
       // alpha2 = -tau (p . v) / 2 (every wave the same tree), w = p + alpha2 v, A22 -= v w^T + w v^T:
       // lanes over columns (v_j, w_j in registers), waves over rows
       double s = 0.0;
@@ -411,7 +419,11 @@ __global__ void __launch_bounds__(TW) k_eig_lds(double* A0, int64_t a_stride, in
     }
     __syncthreads();
   }
-  if (stp) stp[1] = clock64();
+  if (stp) {
+    stp[1] = clock64();
+    stp[6] = acc_refl;
+    stp[7] = acc_symv;
+  }
   // d, e into LDS (vb, pb) and the slot
   for (int i = tid; i < m; i += EW) {
     const double di = P[poff(i) + i];

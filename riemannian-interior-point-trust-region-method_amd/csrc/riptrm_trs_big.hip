@@ -1928,8 +1928,9 @@ int riptrm_sym_eig(riptrm_ctx* ctx, int32_t dim, int32_t batch, double* A, int64
     HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
     (void)hipFree(stamps);
     const long long* t = h.data();
-    fprintf(stderr, "[eig stamps] m=%d load+tridiag %lld bisect %lld vectors(twisted+backtransform) %lld+%lld orthog %lld total %lld\n",
-            dim, t[1] - t[0], t[2] - t[1], t[3] - t[2], t[4] - t[3], t[5] - t[4], t[5] - t[0]);
+    fprintf(stderr, "[eig stamps] m=%d load+tridiag %lld (reflector %lld symv %lld) bisect %lld vectors(twisted+backtransform) %lld "
+            "orthog %lld total %lld\n",
+            dim, t[1] - t[0], t[6], t[7], t[2] - t[1], t[3] - t[2], t[5] - t[4], t[5] - t[0]);
   }
   return RIPTRM_OK;
 }
