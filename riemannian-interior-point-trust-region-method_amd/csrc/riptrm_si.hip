@@ -79,6 +79,7 @@ struct SIParams {
   int32_t* trskind;  // batch                 RIPTRM_TRS_* (host service)
   double* trsmin;    // batch                 smallest eigenvalue of HwNew's matrix (host service)
   double* rs;        // batch x rs_doubles    resume records
+  double* trsW;      // batch x SI_PREP_F x nt the park point's prepare / frame / X X^T per lane (k_si_prep)
   double* trsC;      // batch x trsC_stride   the service's keyed eigendecomposition cache (tdim <= 199)
   int64_t trsC_stride;
   int32_t tdim, tdp;
@@ -89,6 +90,7 @@ struct Layout {
   int64_t off_x, off_y, off_eta, off_heta, off_escr, off_stats, off_log, total;
   int64_t off_tA, off_tP, off_tids, off_tE, off_ta, off_tx, off_tD, off_tlam, off_tkind, off_tmin, off_rs;   // 0: no HBM subproblem path
   int64_t off_tC, tC_stride;   // the keyed eigendecomposition cache (0: none)
+  int64_t off_tW;              // k_si_prep's per-lane records
 };
 
 inline int64_t rup(int64_t a, int64_t m) { return (a + m - 1) / m * m; }
@@ -108,6 +110,8 @@ constexpr int SI_REPMAT_E_LDS = 48 * 1024;
 __host__ __device__ constexpr bool si_repmat_e_lds(int d, int N) { return (int64_t)d * N * 8 <= SI_REPMAT_E_LDS; }
 __host__ __device__ constexpr int si_nt(int d) { return d <= 8 ? 64 : (d * d + 63) / 64 * 64; }
 __host__ __device__ constexpr int64_t si_rs_doubles(int d) { return RS_NSC + (int64_t)RS_ROWS * si_nt(d); }
+// k_si_prep's record per lane: AtX (x 3, metric 2, A Gf GL sgR sgQ f, s w y, c 3), Frame 4, M2
+constexpr int SI_PREP_F = 22;
 
 inline Layout make_layout(int d, int N, int m, int batch, int cap) {
   Layout L;
@@ -121,7 +125,7 @@ inline Layout make_layout(int d, int N, int m, int batch, int cap) {
   L.off_stats = o; o = rup(o + 8LL * batch * RIPTRM_STAT_NFIELDS, 256);
   L.off_log = o;   o = rup(o + 8LL * batch * cap * RIPTRM_LOG_NFIELDS, 256);
   L.off_tA = L.off_tP = L.off_tids = L.off_tE = L.off_ta = L.off_tx = L.off_tD = L.off_tlam = L.off_tkind = L.off_tmin = L.off_rs = 0;
-  L.off_tC = L.tC_stride = 0;
+  L.off_tC = L.tC_stride = L.off_tW = 0;
   if (si_hbm_trs(d)) {
     const int64_t td = si_manifold_dim(d), tp = si_tdp(d);
     L.off_tA = o;    o = rup(o + 8 * batch * td * td, 256);
@@ -137,6 +141,7 @@ inline Layout make_layout(int d, int N, int m, int batch, int cap) {
     L.off_tkind = o; o = rup(o + 4LL * batch, 256);
     L.off_tmin = o;  o = rup(o + 8LL * batch, 256);
     L.off_rs = o;    o = rup(o + 8 * batch * si_rs_doubles(d), 256);
+    L.off_tW = o;    o = rup(o + 8LL * batch * SI_PREP_F * si_nt(d), 256);
     if (td <= RIPTRM_EIG_COMPACT_MAX) {   // keyed by the park point (x, y, mu): 3dd + m + 1 doubles
       L.tC_stride = rup(riptrm_big_kcache_doubles((int)td, 3 * d * d + m + 1), 32);
       L.off_tC = o;  o = rup(o + 8 * batch * L.tC_stride, 256);
@@ -421,7 +426,8 @@ struct Eng {
   double* rowx;
   double* jw;      // big D: riptrm_trs Work area of the SPD distance's eigenvalues
 
-  __device__ __forceinline__ Eng(const SIParams& P_, int b_, double* sh_, double* ser_, int* crs, int* ccs, double* tl_)
+  __device__ __forceinline__ Eng(const SIParams& P_, int b_, double* sh_, double* ser_, int* crs, int* ccs, double* tl_,
+                                 bool with_m2 = true)
       : P(P_), b(b_), l((int)threadIdx.x), m(P_.m), N(P_.N),
         li((int)threadIdx.x / D), lj((int)threadIdx.x % D), act((int)threadIdx.x < D * D),
         cact((int)threadIdx.x < P_.m), sh(sh_), ser(ser_), cr_s(crs), cc_s(ccs), tl(tl_),
@@ -447,7 +453,7 @@ struct Eng {
     }
     // X X^T (f's Hessian, coordinator.py:92-98)
     double acc = 0.0;
-    if (act)
+    if (act && with_m2)   // (k_si_repmat on k_si_prep's record takes M2 from there)
       for (int t = 0; t < N; ++t) acc = acc + Xd[li * N + t] * Xd[lj * N + t];
     M2 = acc;
 #pragma unroll
@@ -1020,7 +1026,10 @@ struct Eng {
     if (cact) t[3 * dd + l] = py;
     if (l == 0) t[3 * dd + m] = mu;
   }
-  __device__ void repmat_col(int j, bool want_c, double* uv, bool only_c = false) {
+  // k_si_prep: prepare / frame at the park point (and X X^T) once per instance, one record per lane,
+  // so the matrix's tdim workgroups load them instead of each recomputing the same values
+  __device__ __forceinline__ double* prep_rec() const { return P.trsW + (int64_t)b * SI_PREP_F * NT; }
+  __device__ void prep_park() {
     const double* t = P.trsP + (int64_t)b * tp_stride();
     const PV x = load_pv(t);
     const double y = cact ? t[3 * dd + l] : 0.0;
@@ -1028,6 +1037,38 @@ struct Eng {
     AtX a;
     prepare(a, x, y, mu);
     const Frame F = frame(x);
+    double* r = prep_rec() + l;
+    const double v[SI_PREP_F] = {a.x.j, a.x.r, a.x.q, a.g.XiR, a.g.XiQ, a.A, a.Gf, a.GL, a.sgR, a.sgQ, a.f,
+                                 a.s, a.w, a.y, a.c.j, a.c.r, a.c.q, F.Lr, F.Lq, F.Lri, F.Lqi, M2};
+#pragma unroll
+    for (int k = 0; k < SI_PREP_F; ++k) r[(int64_t)k * NT] = v[k];
+  }
+  __device__ void prep_load(AtX& a, Frame& F) {
+    const double* r = prep_rec() + l;
+    double v[SI_PREP_F];
+#pragma unroll
+    for (int k = 0; k < SI_PREP_F; ++k) v[k] = r[(int64_t)k * NT];
+    a.x = PV{v[0], v[1], v[2]};
+    a.g.XiR = v[3], a.g.XiQ = v[4];
+    a.A = v[5], a.Gf = v[6], a.GL = v[7], a.sgR = v[8], a.sgQ = v[9], a.f = v[10];
+    a.s = v[11], a.w = v[12], a.y = v[13];
+    a.c = PV{v[14], v[15], v[16]};
+    F.Lr = v[17], F.Lq = v[18], F.Lri = v[19], F.Lqi = v[20];
+    M2 = v[21];
+  }
+  __device__ void repmat_col(int j, bool want_c, double* uv, bool only_c = false, bool pre = false) {
+    AtX a;
+    Frame F;
+    if (pre) {
+      prep_load(a, F);
+    } else {
+      const double* t = P.trsP + (int64_t)b * tp_stride();
+      const PV x = load_pv(t);
+      const double y = cact ? t[3 * dd + l] : 0.0;
+      const double mu = t[3 * dd + m];
+      prepare(a, x, y, mu);
+      F = frame(x);
+    }
     if (only_c) {   // a cached eigendecomposition serves the matrix: the coordinates of cxCur only
       to_coords(F, a.c, P.trsa + (int64_t)b * TDP);
       return;
@@ -1534,9 +1575,26 @@ __global__ void __launch_bounds__(si_threads(D)) k_si(SIParams P) {
   else e.op_tcg();
 }
 
-// the parked instances' subproblem matrices (ids[blockIdx.y], basis vector blockIdx.x): Eng::repmat_col
+// the parked instances' prepare / frame / X X^T records (ids[blockIdx.y]): Eng::prep_park (its E is
+// the first column workgroup's slice, free until k_si_repmat runs)
 template <int D>
-__global__ void __launch_bounds__(si_threads(D)) k_si_repmat(SIParams P, int32_t ids_off, int want_c, int only_c) {
+__global__ void __launch_bounds__(si_threads(D)) k_si_prep(SIParams P, int32_t ids_off) {
+  constexpr int NT = si_threads(D);
+  __shared__ double sh[2 * NT];
+  __shared__ double ser[NT == W ? 8 * W : 1];
+  __shared__ int crs[NT], ccs[NT];
+  extern __shared__ double trs_lds[];
+  const int b = P.trsids[ids_off + blockIdx.y];
+  Eng<D> e(P, b, sh, ser, crs, ccs, trs_lds);
+  const int64_t en = (int64_t)D * P.N;
+  e.E = P.trsE ? P.trsE + (int64_t)b * si_manifold_dim(D) * en : trs_lds + (D > 8 ? si_big_lds_doubles(D) : 0);
+  if constexpr (si_hbm_trs(D)) e.prep_park();
+}
+
+// the parked instances' subproblem matrices (ids[blockIdx.y], basis vector blockIdx.x): Eng::repmat_col;
+// pre: on k_si_prep's records
+template <int D>
+__global__ void __launch_bounds__(si_threads(D)) k_si_repmat(SIParams P, int32_t ids_off, int want_c, int only_c, int pre) {
   constexpr int NT = si_threads(D);
   __shared__ double sh[2 * NT];
   __shared__ double ser[NT == W ? 8 * W : 1];
@@ -1544,11 +1602,11 @@ __global__ void __launch_bounds__(si_threads(D)) k_si_repmat(SIParams P, int32_t
   __shared__ double uv[2 * si_tdp(D)];
   extern __shared__ double trs_lds[];   // big D: si_big_lds_doubles; then E when it fits (si_repmat_e_lds)
   const int b = P.trsids[ids_off + blockIdx.y];
-  Eng<D> e(P, b, sh, ser, crs, ccs, trs_lds);
+  Eng<D> e(P, b, sh, ser, crs, ccs, trs_lds, pre == 0);
   const int64_t en = (int64_t)D * P.N;
   e.E = P.trsE ? P.trsE + ((int64_t)b * si_manifold_dim(D) + blockIdx.x) * en
                : trs_lds + (D > 8 ? si_big_lds_doubles(D) : 0);
-  if constexpr (si_hbm_trs(D)) e.repmat_col((int)blockIdx.x, want_c != 0 && blockIdx.x == 0, uv, only_c != 0);
+  if constexpr (si_hbm_trs(D)) e.repmat_col((int)blockIdx.x, want_c != 0 && blockIdx.x == 0, uv, only_c != 0, pre != 0);
 }
 
 struct Bound {
@@ -1610,6 +1668,7 @@ static SIParams si_params(riptrm_ctx* c, int mode) {
     P.trskind = (int32_t*)(s->ws + s->L.off_tkind);
     P.trsmin = (double*)(s->ws + s->L.off_tmin);
     P.rs = (double*)(s->ws + s->L.off_rs);
+    P.trsW = (double*)(s->ws + s->L.off_tW);
     P.trsC = s->L.off_tC ? (double*)(s->ws + s->L.off_tC) : nullptr;
     P.trsC_stride = s->L.tC_stride;
     P.tdim = si_manifold_dim(P.d);
@@ -1661,8 +1720,17 @@ static int si_repmat_d(riptrm_ctx* c, const SIParams& P, int ids_off, int cnt, i
   const size_t shm = ((D > 8 ? (size_t)si_big_lds_doubles(D) : 0) + (P.trsE ? 0 : (size_t)D * P.N)) * sizeof(double);
   if (shm > 64 * 1024)
     HIPCHK(c, hipFuncSetAttribute((const void*)k_si_repmat<D>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm));
+  // prepare / frame once per instance (k_si_prep), then the tdim column workgroups on its records;
+  // RIPTRM_SI_PREP=0: every workgroup recomputes them (A/B; the same values)
+  const char* pe = getenv("RIPTRM_SI_PREP");
+  const int pre = (pe && pe[0] == '0') ? 0 : 1;
+  if (pre) {
+    if (shm > 64 * 1024)
+      HIPCHK(c, hipFuncSetAttribute((const void*)k_si_prep<D>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm));
+    hipLaunchKernelGGL(k_si_prep<D>, dim3(1u, (unsigned)cnt), dim3(si_threads(D)), shm, c->stream, P, ids_off);
+  }
   hipLaunchKernelGGL(k_si_repmat<D>, dim3(only_c ? 1u : (unsigned)si_manifold_dim(D), (unsigned)cnt), dim3(si_threads(D)), shm,
-                     c->stream, P, ids_off, want_c, only_c);
+                     c->stream, P, ids_off, want_c, only_c, pre);
   HIPCHK(c, hipGetLastError());
   return RIPTRM_OK;
 }

@@ -1,7 +1,7 @@
 # SI d=8 Exact A/B: keyed cache and split eigensolver on/off, plus a rocprofv3 summary of the default
 set -u
 cd "$GRAFT_REPO_ROOT"
-O=gpurun_out/${OUT:-r5w}
+O=gpurun_out/${OUT:-absi}
 mkdir -p $O
 export TMPDIR=/tmp
 run() {

@@ -1,7 +1,7 @@
 # split eigensolver timing (m = 100, 199) + the TRS eigensolver tests + the two Exact benches
 set -u
 cd "$GRAFT_REPO_ROOT"
-O=gpurun_out/${OUT:-r5s2}
+O=gpurun_out/${OUT:-eigab}
 mkdir -p $O
 export TMPDIR=/tmp
 for m in 100 199; do

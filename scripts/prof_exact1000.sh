@@ -1,7 +1,7 @@
 # rocprofv3 of the Exact_RepMat line at configs[1]'s size (n = 1000, one instance, class defaults)
 set -u
 cd "$GRAFT_REPO_ROOT"
-O=gpurun_out/${OUT:-r5y}
+O=gpurun_out/${OUT:-p1000}
 mkdir -p $O
 export TMPDIR=/tmp
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/p1000 -o p -- python bench.py --trs Exact_RepMat \

@@ -289,6 +289,30 @@ def test_si_exact_eigen_cache_is_bitwise_neutral(sos, monkeypatch):
     np.testing.assert_array_equal(r1.y.cpu().numpy(), r0.y.cpu().numpy())
 
 
+@pytest.mark.timeout(600)
+def test_si_exact_prep_records_are_bitwise_neutral(monkeypatch):
+    """k_si_prep computes each parked instance's prepare / frame / X X^T once and the matrix's column
+    workgroups load them (RIPTRM.py:720-730 at the park point); RIPTRM_SI_PREP=0 has every workgroup
+    recompute them.  The same code on the same inputs: logs and x / y bit for bit."""
+    import bench
+    import si
+    d = 8
+    xs, ys, (X, XP, h, constset) = bench.si_starts(8, list(range(8)), d)
+    cons = si.expand_constset(constset)
+    mk = lambda: _load(si.SIBatch(d, X.shape[1], cons.shape[0], len(xs), log_capacity=1024), X, XP, h, cons)   # noqa: E731
+    opt = {"maxiter": 2, "tolresid": 0.0, "maxtime": 1e9, "TRS_solver": "Exact_RepMat",
+           "second_order_stationarity": True, "manviofun": si.si_manviofun}
+    monkeypatch.delenv("RIPTRM_SI_PREP", raising=False)
+    r1 = mk().solve(xs, ys, opt)
+    monkeypatch.setenv("RIPTRM_SI_PREP", "0")
+    r0 = mk().solve(xs, ys, opt)
+    for b in range(len(xs)):
+        for key in ("cost", "residual", "normdx", "dxtype", "mineigvalHw", "inner_status", "radius_update"):
+            assert r1.log(b)[key] == r0.log(b)[key], (b, key)
+    np.testing.assert_array_equal(r1.x.cpu().numpy(), r0.x.cpu().numpy())
+    np.testing.assert_array_equal(r1.y.cpu().numpy(), r0.y.cpu().numpy())
+
+
 def _load(eng, X, XP, h, cons):
     eng.load(X, XP, h, cons)
     return eng
