@@ -347,12 +347,13 @@ __global__ void __launch_bounds__(TW) k_eig_lds(double* A0, int64_t a_stride, in
     }
     const double tau = scal[0];
     if (tau != 0.0) {   // uniform
-      // p = tau A22 v: TPR = EW / 256 threads per row (r <= 256), each over a part of the row -- its
-      // part of the packed row (contiguous) and, past the diagonal, its part of the column below the
-      // diagonal (an incremental offset, no multiplies) -- then the partners' parts (DPP xor 1, 2)
+      // p = tau A22 v: TPR threads per row (EW / 256, or 8 once r <= 128 on 1024 threads), each over
+      // a part of the row -- its part of the packed row (contiguous) and, past the diagonal, its part
+      // of the column below the diagonal (an incremental offset, no multiplies) -- then the partners'
+      // parts (DPP xor 1, xor 2, half mirror)
       {
-        constexpr int TPR = EW / 256;
-        const int l = tid / TPR, h = tid % TPR;
+        const int TPR = (EW == 1024 && r <= 128) ? 8 : EW / 256;   // uniform
+        const int l = tid / TPR, h = tid & (TPR - 1);
         const int half = (r + TPR - 1) / TPR;
         double acc0 = 0.0, acc1 = 0.0;
         if (l < r) {
@@ -389,7 +390,8 @@ __global__ void __launch_bounds__(TW) k_eig_lds(double* A0, int64_t a_stride, in
         }
         double acc = acc0 + acc1;
         acc = acc + riptrm_wave::dpp<riptrm_wave::DPP_XOR1>(acc);
-        if (TPR == 4) acc = acc + riptrm_wave::dpp<riptrm_wave::DPP_XOR2>(acc);
+        if (TPR >= 4) acc = acc + riptrm_wave::dpp<riptrm_wave::DPP_XOR2>(acc);
+        if (TPR == 8) acc = acc + riptrm_wave::dpp<riptrm_wave::DPP_HALF_MIRROR>(acc);   // lane ^ 7 of the 8
         if (l < r && h == 0) pb[l] = tau * acc;
       }
       __syncthreads();
