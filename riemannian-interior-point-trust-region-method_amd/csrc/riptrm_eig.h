@@ -241,6 +241,37 @@ __device__ __forceinline__ void gs_wmul(lds_t* Out, const lds_t* Base, const lds
   }
 }
 
+// rows r0 .. r0 + rn - 1 of A (m columns, leading dimension lda) -> X [GB][mp], zero past rn / m:
+// unconditional loads of clamped addresses, eight in flight per thread, (row, column) stepped
+// incrementally (NT threads = qs mp + rs)
+template <int NT>
+__device__ __forceinline__ void gs_load(lds_t* X, const double* A, int64_t lda, int r0, int rn, int m, int mp, int tid) {
+  const int tot = GB * mp, qs = NT / mp, rs = NT - qs * mp;
+  int a0 = tid / mp, c0 = tid - (tid / mp) * mp;
+  for (int q0 = 0; q0 < tot; q0 += NT * 8) {
+    double v[8];
+    int aa[8], cc[8];
+    int a = a0, c = c0;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      aa[u] = a;
+      cc[u] = c;
+      v[u] = A[(a < rn && c < m) ? (int64_t)(r0 + a) * lda + c : (int64_t)r0 * lda];
+      c += rs;
+      a += qs;
+      if (c >= mp) {
+        c -= mp;
+        ++a;
+      }
+    }
+    a0 = a;
+    c0 = c;
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (aa[u] < GB) X[aa[u] * mp + cc[u]] = (aa[u] < rn && cc[u] < m) ? v[u] : 0.0;
+  }
+}
+
 // Matrix k = blockIdx.x: the m x m symmetric matrix at A0 + k a_stride (leading dimension lda; the
 // lower triangle is read) -> eigenvalues ascending at ev0 + k ev_stride and, with vectors, in the
 // rows of the same matrix: vectors = 1 the eigenvectors of A; vectors = 2 those of the tridiagonal
@@ -288,12 +319,37 @@ __global__ void __launch_bounds__(TW) k_eig_lds(double* A0, int64_t a_stride, in
   if (tid == 0) bad = 0;
   if (stp) stp[0] = clock64();
   __syncthreads();
-  for (int64_t q = tid; q < (int64_t)m * m; q += EW) {
-    const int i = (int)(q / m), j = (int)(q - (int64_t)i * m);
-    if (j <= i) {
-      const double a = A[(int64_t)i * lda + j];
-      if (!isfinite(a)) bad = 1;
-      P[poff(i) + j] = a;
+  // the lower triangle into the packed LDS image, eight loads in flight per thread (a load-then-store
+  // loop waits out one memory latency per element); element q = i m + j of thread tid, u-th of a
+  // batch, stepped incrementally (EW = qs m + rs)
+  {
+    const int mm2 = m * m, qs = EW / m, rs = EW - qs * m;
+    int i0 = tid / m, j0 = tid - (tid / m) * m;   // element tid
+    for (int q0 = 0; q0 < mm2; q0 += EW * 8) {
+      double v[8];
+      int ii[8], jj[8];
+      int i = i0, j = j0;
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        ii[u] = i;
+        jj[u] = j;
+        // an unconditional load of a clamped address (a guarded load is sunk into a branch that waits)
+        v[u] = A[(i < m && j <= i) ? (int64_t)i * lda + j : 0];
+        j += rs;
+        i += qs;
+        if (j >= m) {
+          j -= m;
+          ++i;
+        }
+      }
+      i0 = i;
+      j0 = j;
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (ii[u] < m && jj[u] <= ii[u]) {
+          if (!isfinite(v[u])) bad = 1;
+          P[poff(ii[u]) + jj[u]] = v[u];
+        }
     }
   }
   __syncthreads();
@@ -585,20 +641,14 @@ __global__ void __launch_bounds__(TW) k_eig_lds(double* A0, int64_t a_stride, in
     for (int J = 0; J < nb; ++J) {
       const int j0 = J * GB, jn = min(GB, m - j0);
       __syncthreads();
-      for (int q = tid; q < GB * mp; q += EW) {
-        const int a = q / mp, c = q - a * mp;
-        QJ[q] = (a < jn && c < m) ? A[(int64_t)(j0 + a) * lda + c] : 0.0;
-      }
+      gs_load<EW>(QJ, A, lda, j0, jn, m, mp, tid);
       for (int I = 0; I <= J; ++I) {
         const int i0b = I * GB, in = min(GB, m - i0b);
         // eigenvalues sorted: block I is close to block J iff its last one is within ctol of J's first
         if (I < J && ev[j0] - ev[i0b + in - 1] > ctol) continue;   // uniform
         __syncthreads();
         if (I < J)
-          for (int q = tid; q < GB * mp; q += EW) {
-            const int a = q / mp, c = q - a * mp;
-            QI[q] = (a < in && c < m) ? A[(int64_t)(i0b + a) * lda + c] : 0.0;
-          }
+          gs_load<EW>(QI, A, lda, i0b, in, m, mp, tid);
         __syncthreads();
         const lds_t* QA = I < J ? QI : QJ;
         // E[a][b] = Q_I[a] . Q_J[b] on the matrix cores: waves 0-3 one 16 x 16 tile each, the k steps

@@ -1121,7 +1121,21 @@ __global__ void __launch_bounds__(256) k_refl_apply(Bat B, int m, int64_t voff, 
   double* base = B.base + (int64_t)blockIdx.y * B.sd;
   const double* Rg = base + off_refl(B.N);
   const int nt = riptrm_eig::refl_tau(m), nr = nt + m - 1;
-  for (int q = threadIdx.x; q < nr; q += 256) R[q] = Rg[q];
+  // staged with sixteen loads in flight per thread (a load-then-store loop waits out one memory
+  // latency per element: ~78 of them at m = 199)
+  for (int q0 = 0; q0 < nr; q0 += 256 * 16) {
+    double v[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int q = q0 + u * 256 + (int)threadIdx.x;
+      v[u] = Rg[q < nr ? q : nr - 1];
+    }
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int q = q0 + u * 256 + (int)threadIdx.x;
+      if (q < nr) R[q] = v[u];
+    }
+  }
   __syncthreads();
   if (threadIdx.x >= 64) return;
   const int lane = threadIdx.x;
