@@ -394,6 +394,25 @@ __host__ __device__ constexpr int si_big_lds_doubles(int D) {
   return si_threads(D) + 2 * (si_threads(D) / 64) + 4 * D + riptrm_trs::work_doubles(D);
 }
 
+// sum_t a_t b_t in t order (one sequential chain), the loads issued eight at a time: a loop of
+// load, wait, multiply-add waits out one memory latency per term (N = 95 terms on the data)
+__device__ __forceinline__ double dot_seq(const double* a, const double* b, int N) {
+  double acc = 0.0;
+  int t = 0;
+  for (; t + 8 <= N; t += 8) {
+    double x[8], y[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      x[u] = a[t + u];
+      y[u] = b[t + u];
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) acc = acc + x[u] * y[u];
+  }
+  for (; t < N; ++t) acc = acc + a[t] * b[t];
+  return acc;
+}
+
 template <int D, int NT = si_threads(D)>
 struct Eng {
   static constexpr int d = D, dd = D * D;
@@ -454,7 +473,7 @@ struct Eng {
     // X X^T (f's Hessian, coordinator.py:92-98)
     double acc = 0.0;
     if (act && with_m2)   // (k_si_repmat on k_si_prep's record takes M2 from there)
-      for (int t = 0; t < N; ++t) acc = acc + Xd[li * N + t] * Xd[lj * N + t];
+      acc = dot_seq(Xd + li * N, Xd + lj * N, N);
     M2 = acc;
 #pragma unroll
     for (int k = 0; k < RIPTRM_SI_PROF_NFIELDS; ++k) pt[k] = 0.0;
@@ -737,8 +756,7 @@ struct Eng {
     __syncthreads();
     f = rsum(part) / (double)N;
     double g = 0.0;
-    if (act)
-      for (int t = 0; t < N; ++t) g = g + E[li * N + t] * Xd[lj * N + t];
+    if (act) g = dot_seq(E + li * N, Xd + lj * N, N);
     Gf = act ? -(2.0 * P.h / (double)N) * g : 0.0;
     __syncthreads();
   }
