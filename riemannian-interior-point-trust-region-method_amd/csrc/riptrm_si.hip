@@ -451,7 +451,8 @@ struct Eng {
         li((int)threadIdx.x / D), lj((int)threadIdx.x % D), act((int)threadIdx.x < D * D),
         cact((int)threadIdx.x < P_.m), sh(sh_), ser(ser_), cr_s(crs), cc_s(ccs), tl(tl_),
         bc(tl_), blk(BIG ? tl_ + NT : nullptr) {
-    colv = tl_ + NT + 2 * (NT / 64);
+    // one wave: the row / column buffers of par_inv in the serial solvers' spare slot 6 of ser
+    colv = BIG ? tl_ + NT + 2 * (NT / 64) : ser_ + 6 * W;
     rowa = colv + D;
     rowo = rowa + D;
     rowx = rowo + D;
@@ -618,9 +619,11 @@ struct Eng {
     return ok ? sqrt(s2) : NAN;
   }
 
-  // R^-1 and Q^-1 at once: lane 0 inverts slot 0, lane 1 slot 1 (Gauss-Jordan, partial pivoting)
+  // R^-1 and Q^-1 at once: lane 0 inverts slot 0, lane 1 slot 1 (Gauss-Jordan, partial pivoting).
+  // From D = 6 on the serial form's two D x D register arrays live in scratch memory (k_si<8>: 832
+  // bytes per lane), so those sizes take par_inv: the same arithmetic, one element per lane
   __device__ __forceinline__ void inv2(double r, double q, double& ri, double& qi) {
-    if constexpr (BIG) {
+    if constexpr (BIG || D >= 6) {
       ri = par_inv(r);
       qi = par_inv(q);
       return;
@@ -745,7 +748,32 @@ struct Eng {
     __syncthreads();
     double part = 0.0;
     const int tot = d * N;
-    for (int e = l; e < tot; e += NT) {
+    int e = l;
+    // two residual entries per step: both entries' data loads issued before either's sums (the same
+    // sums in the same order as one at a time)
+    for (; e + NT < tot; e += 2 * NT) {
+      const int e2 = e + NT;
+      const int i = e / N, t = e - i * N, i2 = e2 / N, t2 = e2 - i2 * N;
+      double xa[D], xb[D];
+#pragma unroll
+      for (int k = 0; k < D; ++k) {
+        xa[k] = Xd[k * N + t];
+        xb[k] = Xd[k * N + t2];
+      }
+      const double pa = XPd[i * N + t], pb = XPd[i2 * N + t2];
+      double s = 0.0, s2 = 0.0;
+#pragma unroll
+      for (int k = 0; k < D; ++k) {
+        s = s + sh[i * d + k] * xa[k];
+        s2 = s2 + sh[i2 * d + k] * xb[k];
+      }
+      const double ev = pa - s, ev2 = pb - s2;
+      E[e] = ev;
+      E[e2] = ev2;
+      part = part + ev * ev;
+      part = part + ev2 * ev2;
+    }
+    for (; e < tot; e += NT) {
       const int i = e / N, t = e - i * N;
       double s = 0.0;
       for (int k = 0; k < d; ++k) s = s + sh[i * d + k] * Xd[k * N + t];
