@@ -597,6 +597,27 @@ struct Eng {
     }
     return L;
   }
+  // L^-1 of this lane's element of lower-triangular L, chol_inv_reg's arithmetic: Li_jj = 1 / L_jj,
+  // Li_ij = (0 - sum_{k = j .. i-1} L_ik Li_kj) / L_ii (k ascending), one row of Li per step
+  __device__ __forceinline__ double par_trinv(double L) {
+    sh[l] = act ? L : 0.0;
+    double v = 0.0;
+    __syncthreads();
+    for (int i = 0; i < D; ++i) {
+      if (act && li == i && lj <= i) {
+        if (lj == i) {
+          v = 1.0 / sh[i * d + i];
+        } else {
+          double t = 0.0;
+          for (int k = lj; k < i; ++k) t -= sh[i * d + k] * sh[NT + k * d + lj];
+          v = t / sh[i * d + i];
+        }
+        sh[NT + i * d + lj] = v;
+      }
+      __syncthreads();
+    }
+    return v;
+  }
   // pymanopt SPD dist ||logm(C^-1 B C^-T)||_F, C = cholesky(A) (spd_dist_reg on the workgroup;
   // the eigenvalues by riptrm_trs.h's parallel Jacobi); NaN if A is not PD
   __device__ __forceinline__ double par_dist(double A, double Bm) {
@@ -963,6 +984,19 @@ struct Eng {
       F.Lq = par_chol(x.q, ok);
       F.Lri = par_inv(F.Lr);
       F.Lqi = par_inv(F.Lq);
+      return F;
+    } else if constexpr (D >= 6) {
+      // one wave from D = 6: chol_inv_reg's arithmetic one element per lane (par_chol is its
+      // Cholesky step for step; par_trinv its triangular inverse), not two lanes' scratch-resident
+      // arrays; NaN factors for a non-PD point as chol_inv_reg's sqrt gives them
+      bool okr, okq;
+      Frame F;
+      F.Lr = par_chol(x.r, okr);
+      F.Lq = par_chol(x.q, okq);
+      if (!okr) F.Lr = NAN;
+      if (!okq) F.Lq = NAN;
+      F.Lri = par_trinv(F.Lr);   // every lane (barriers inside); 0 above the diagonal and off the block
+      F.Lqi = par_trinv(F.Lq);
       return F;
     }
     stage(0, x.r);
