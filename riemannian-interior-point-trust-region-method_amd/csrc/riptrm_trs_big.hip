@@ -1415,7 +1415,13 @@ static int launch_eig(riptrm_ctx* c, int cnt, int m, double* A, int64_t a_stride
                        ev_stride, d, e, sc_stride, R, r_stride, infos, vectors, nullptr);
     HIPCHK(c, hipFuncSetAttribute((const void*)riptrm_eig::k_eig_lds<512, 2>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   (int)shm));
-    hipLaunchKernelGGL((riptrm_eig::k_eig_lds<512, 2>), dim3(cnt, yv), dim3(512), shm,
+    // the bisection over ~25 eigenvalues per workgroup up to order 128 (four waves of eight-lane
+    // groups instead of seven; kq stays 8 for any range <= 64, so the same arithmetic).
+    // RIPTRM_EIG_BIS=n (1..64): ~n per workgroup at every order (A/B)
+    const char* bs = getenv("RIPTRM_EIG_BIS");
+    const int bn = bs ? atoi(bs) : 0;
+    const int yb = (bn >= 1 && bn <= 64) ? (m + bn - 1) / bn : (m <= 128 ? (m + 24) / 25 : yv);
+    hipLaunchKernelGGL((riptrm_eig::k_eig_lds<512, 2>), dim3(cnt, yb), dim3(512), shm,
                        c->stream, A, a_stride, lda, m, ev, ev_stride, d, e, sc_stride, R, r_stride, infos, vectors, nullptr);
     if (vectors) {
       HIPCHK(c, hipFuncSetAttribute((const void*)riptrm_eig::k_eig_lds<512, 4>, hipFuncAttributeMaxDynamicSharedMemorySize,
