@@ -406,6 +406,7 @@ NULL_FLOOR_X = 1e-8       # ||x|| = 1; a late-window branch flip moves x by ~1e-
 NULL_FLOOR_Y = 1e-8       # relative
 NULL_FLOOR_OUTER = 1e-6   # relative
 NULL_KEYS = ("div_row", "dx", "dy", "outer_dev")   # div_row: earlier is worse; the others: larger is worse
+NULL_U_MIN_FLOOR = 0.2    # a pooled rank test's mean-u limit must exceed this (assert_null)
 
 
 def outer_residuals(log):
@@ -548,10 +549,21 @@ def null_table(rows, names, summary, path=None):
     return out
 
 
-def assert_null(rows, names, path=None, budget=None):
+def assert_null(rows, names, path=None, budget=None, variants_move=False):
     """null_summary over a test's rows; the table goes to `path`; fails on any bar (and on more
-    envelope excursions than excursion_budget)."""
+    envelope excursions than excursion_budget).  A rank test over too few instances cannot fail
+    (its mean-u limit sinks towards 0: 0.11 at 6 instances with 5 variants), so a test must pool
+    enough instances that the limit exceeds NULL_U_MIN_FLOOR (11 with 4 or 5 variants); the power
+    of the bar at those sizes is tests/test_oracle.py::test_null_calibration_accepts_variants_and_rejects_hessian_error.
+    variants_move: every instance's variants must end away from the reference run (dx, dy > 0),
+    so that the final-point statistics are not vacuous (a window that ends at the start point)."""
     summary = null_summary(rows)
+    assert summary["mean_u_min"] > NULL_U_MIN_FLOOR, ("too few instances for the rank test", summary["instances"],
+                                                      summary["variants"], summary["mean_u_min"])
+    if variants_move:
+        still = [n for n, r in zip(names, rows)
+                 if max(v["dx"] for v in r["variants"]) <= 0.0 or max(v["dy"] for v in r["variants"]) <= 0.0]
+        assert not still, ("variants end at the reference run's final point: vacuous dx / dy", still)
     tab = null_table(rows, names, summary, path)
     for it in tab["instances"]:
         print("[null]", it["name"], "gpu div row", it["gpu_div_row"], "of", it["rows"], "variants", it["variant_div_rows"],
@@ -564,32 +576,101 @@ def assert_null(rows, names, path=None, budget=None):
     return summary
 
 
-def si_order_variants(data, x0, y0, opt, seeds=(1, 2, 3), structured=True):
-    """StableIdentification runs that are the same arithmetic in another summation order: the
-    reference-structured wiring (SIStructured: per-constraint loops, RIPTRM.py:475-571), and the
-    vectorised oracle on a coordinate permutation Pi (X, XP -> Pi X, Pi XP; J, R, Q -> Pi J Pi^T ...;
-    the constraints on A_rc -> A'_{pi(r) pi(c)}, their order shuffled too), which leaves the cost,
-    the constraints, the SPD metric and every logged quantity invariant (A' = Pi A Pi^T, E' = Pi E).
-    x and y of the permuted runs are mapped back.  The SI analogue of order_variants."""
+def si_variant(data, x0, y0, opt, which):
+    """One StableIdentification run of the oracle: which = "ref" (the vectorised oracle, the
+    reference run R), "structured" (the reference-structured wiring, SIStructured: per-constraint
+    loops, RIPTRM.py:475-571) or an int seed: the vectorised oracle on a coordinate permutation Pi
+    (X, XP -> Pi X, Pi XP; J, R, Q -> Pi J Pi^T ...; the constraints on A_rc -> A'_{pi(r) pi(c)}, their
+    order shuffled too), which leaves the cost, the constraints, the SPD metric and every logged
+    quantity invariant (A' = Pi A Pi^T, E' = Pi E); x and y of a permuted run are mapped back."""
     import copy
     from oracle import si_oracle as SI
-    out = []
-    if structured:
-        out.append(SI.solve(data, x0, y0, opt, structured=True))
+    if which == "ref":
+        return SI.solve(data, x0, y0, opt)
+    if which == "structured":
+        return SI.solve(data, x0, y0, opt, structured=True)
     d, m = data.d, data.m
-    for sd in seeds:
-        rs = np.random.RandomState(sd)
-        p = rs.permutation(d)
-        inv = np.argsort(p)
-        sig = rs.permutation(m)
-        dp = copy.copy(data)
-        dp.X, dp.XP = np.ascontiguousarray(data.X[p]), np.ascontiguousarray(data.XP[p])
-        dp.cons = [(k, int(inv[r]), int(inv[c]), p0, p1) for (k, r, c, p0, p1) in (data.cons[i] for i in sig)]
-        xp = np.stack([np.asarray(x0)[k][p][:, p] for k in range(3)])
-        r = SI.solve(dp, xp, np.asarray(y0)[sig], opt)
-        r.x = np.stack([np.asarray(r.x)[k][inv][:, inv] for k in range(3)])
-        yy = np.empty(m)
-        yy[sig] = np.asarray(r.y)
-        r.y = yy
-        out.append(r)
-    return out
+    rs = np.random.RandomState(int(which))
+    p = rs.permutation(d)
+    inv = np.argsort(p)
+    sig = rs.permutation(m)
+    dp = copy.copy(data)
+    dp.X, dp.XP = np.ascontiguousarray(data.X[p]), np.ascontiguousarray(data.XP[p])
+    dp.cons = [(k, int(inv[r]), int(inv[c]), p0, p1) for (k, r, c, p0, p1) in (data.cons[i] for i in sig)]
+    xp = np.stack([np.asarray(x0)[k][p][:, p] for k in range(3)])
+    r = SI.solve(dp, xp, np.asarray(y0)[sig], opt)
+    r.x = np.stack([np.asarray(r.x)[k][inv][:, inv] for k in range(3)])
+    yy = np.empty(m)
+    yy[sig] = np.asarray(r.y)
+    r.y = yy
+    return r
+
+
+def si_order_variants(data, x0, y0, opt, seeds=(1, 2, 3), structured=True):
+    """StableIdentification runs that are the same arithmetic in another summation order
+    (si_variant): the reference-structured wiring and coordinate / constraint-order permutations.
+    The SI analogue of order_variants."""
+    return [si_variant(data, x0, y0, opt, w) for w in ((["structured"] if structured else []) + list(seeds))]
+
+
+def _si_job(job):
+    data, x0, y0, opt, which = job
+    from oracle import si_oracle as SI
+    opt = dict(opt, manviofun=SI.si_manvio)
+    return si_variant(data, x0, y0, opt, which)
+
+
+def check_si_parallel(items, workers=16, progress=print, every_s=20.0):
+    """check_null for StableIdentification instances with the oracle runs (the reference run and the
+    variants `item["variants"]`, a list of si_variant `which` values) spread over a pool of
+    single-threaded processes.  items: dicts with data (SIData), x0, y0, opt (without manviofun),
+    gl (the GPU log), gpu_x (3 x d x d), gpu_y, variants, name.  Returns {name: null_row}."""
+    import concurrent.futures as cf
+    import multiprocessing as mp
+    import os
+    import time
+    keep = {k: os.environ.get(k) for k in ("OMP_NUM_THREADS", "OPENBLAS_NUM_THREADS", "MKL_NUM_THREADS")}
+    results = {}
+    for v in keep:
+        os.environ[v] = "1"
+    try:
+        with cf.ProcessPoolExecutor(max_workers=workers, mp_context=mp.get_context("spawn")) as ex:
+            futs = {}
+            # the longest runs first (items in the order given; callers list the large d first)
+            for k, it in enumerate(items):
+                for w in ["ref"] + list(it["variants"]):
+                    futs[ex.submit(_si_job, (it["data"], it["x0"], it["y0"], it["opt"], w))] = (k, w)
+            out, pending, t0, last = {}, set(futs), time.time(), time.time()
+            done = set()
+            while pending:
+                fin, pending = cf.wait(pending, timeout=every_s, return_when=cf.FIRST_COMPLETED)
+                for f in fin:
+                    out[futs[f]] = f.result()
+                for k, it in enumerate(items):
+                    need = [(k, w) for w in ["ref"] + list(it["variants"])]
+                    if k in done or any(q not in out for q in need):
+                        continue
+                    done.add(k)
+                    ra, vs = out[need[0]], [out[q] for q in need[1:]]
+                    try:
+                        r = check_null(it["gl"], ra, vs, it["gpu_x"], it["gpu_y"])
+                    except AssertionError as e:
+                        raise AssertionError((f"instance {it['name']}",) + tuple(e.args)) from e
+                    r["ref_residual0"] = float(ra.log["residual"][0])
+                    results[it["name"]] = r
+                    progress(f"[si null] {it['name']}: GPU div row {r['gpu']['div_row']} of {r['gpu']['rows']}, "
+                             f"variants {[v['div_row'] for v in r['variants']]} ({time.time() - t0:.0f} s)")
+                    for q in need:
+                        out.pop(q)
+                    last = time.time()
+                if time.time() - last >= every_s:
+                    progress(f"[si null] {len(done)}/{len(items)} instances checked, {len(pending)} oracle runs pending "
+                             f"({time.time() - t0:.0f} s)")
+                    last = time.time()
+    finally:
+        for v, val in keep.items():
+            if val is None:
+                os.environ.pop(v, None)
+            else:
+                os.environ[v] = val
+    return results

@@ -170,3 +170,53 @@ def test_two_persistent_solves_on_concurrent_streams():
         for b in range(B):
             assert res.stat(b, "ERROR") == 0
         _assert_same(res, refs[k], B)
+
+
+@pytest.mark.timeout(900)
+def test_cfg1_bench_window_matches_oracle(capsys):
+    """BASELINE configs[1] as `bench.py --dim 1000 --batch 1 --warmup 5 --steps 20` runs it: one
+    instance at n = 1000 drawn on the device (seed 20251212 + id), the persistent k_persist path
+    (asserted active), options maxiter = 45 and restart_every = 20, paused at outer targets as the
+    bench's warm-up / timed regions do.  The bench times positions 6..20 and, after the restart, 1..5:
+    * the first 20 outer iterations (every position the bench times) against the oracle built from
+      the device's own S under the null-calibrated bar (tests/parity.py check_null / assert_null),
+      twelve instances (ids 0..11; id 0 is the bench's own) pooled into one rank test;
+    * the restart: x, y after outer iteration 25 (restart position 5) are bitwise the x, y after outer
+      iteration 5 of the same run (RIPTRM.py:785-976 from (x0, y0, mu0, Delta0) again).
+    RIPTRM.py:98-214 (tCG), 631-705 (acceptance), 785-976 (loops)."""
+    import engine
+    from parity import assert_null, check_instances_parallel
+    from problems import manviofun
+    import os
+    n, K, ids = 1000, 20, list(range(12))
+    oracle_opt = dict(tolresid=0.0, maxtime=1e9, maxiter=K)
+    from oracle import riptrm_oracle as O
+    oracle_opt["manviofun"] = O.sphere_manvio
+    opt = {"maxiter": 45, "tolresid": 0.0, "maxtime": 1e9, "manviofun": manviofun, "TRS_solver": "tCG",
+           "second_order_stationarity": False}
+    items = []
+    for k in ids:
+        eng = engine.NonnegPCABatch(n, 1, log_capacity=2048, drain_logs=False)
+        x0, y0 = eng.generate_synthetic(20251212, ids=[k])
+        eng.begin(x0, y0, opt, restart_every=20)
+        eng.run_until(5)
+        torch.cuda.synchronize()
+        st = eng.persistent_state()
+        assert st["possible"] and st["active"] and st["fallbacks"] == 0, st
+        x5, y5 = eng.vec(0).clone(), eng.vec(1).clone()
+        eng.run_until(K)
+        res = eng.result()
+        assert int(res.stat(0, "OUTER_ITERS")) == K
+        eng.run_until(25)
+        torch.cuda.synchronize()
+        assert torch.equal(eng.vec(0), x5) and torch.equal(eng.vec(1), y5), k
+        items.append(dict(gl=res.log(0), S=eng.unpack(0), x0=x0[0].cpu().numpy(), y0=y0[0].cpu().numpy(),
+                          gpu_x=res.x[0].cpu().numpy()[:n], gpu_y=res.y[0].cpu().numpy()[:n],
+                          gpu_tcg=res.tcg_iters_per_row(0)[1:], name=f"bench id {k}"))
+        del eng
+    with capsys.disabled():
+        print("[cfg1] 12 GPU solves done", flush=True)
+        results = check_instances_parallel(items, oracle_opt, progress=lambda m: print(m, flush=True))
+        names = [it["name"] for it in items]
+        path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "gpurun_out", "parity", "cfg1.json")
+        assert_null([results[nm] for nm in names], names, path)

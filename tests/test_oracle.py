@@ -309,18 +309,21 @@ class _HessianError(O.NonnegPCAVectorized):
 def test_null_calibration_accepts_variants_and_rejects_hessian_error():
     """parity.null_row / null_summary, the round-5 bar of the GPU trajectory tests, calibrated on the
     CPU over the regime the bench window lives in (K = 20 outer iterations, mu down to 1.4e-8, where
-    every summation-order variant leaves the reference run's branches somewhere: n = 100, 12
+    every summation-order variant leaves the reference run's branches somewhere: n = 100, 14
     instances, 6 variants each):
     * null: each variant in the GPU's place against the other five (leave_one_out) passes -- the
       bar's false-alarm level is what it claims;
-    * power: a run whose Hessian action carries a 1e-9 relative error (_HessianError) fails -- it
-      leaves the reference run earlier than the variants do (measured while choosing the bar: mean
-      percentile 0.08-0.13 at 1e-10 .. 1e-8 against a 0.23 limit; 1e-12 passes at 0.35, a rounding-
-      level error)."""
-    from parity import leave_one_out, null_row, null_summary, run_divergence
+    * power at the sizes the GPU tests use: a run whose Hessian action carries a 1e-9 relative error
+      (_HessianError) fails against 4 variants (the SI test) and 5 (the NonnegPCA tests) at 11, 12
+      and 14 instances (the pooled GPU tests: 12 SI / configs[1] / multi-start instances, 14 at
+      n = 4000, 16 batched), and even at 6 and 8 (it is the strictly earliest-diverging run on nearly
+      every instance).  assert_null refuses fewer instances than give a mean-u limit above 0.2
+      (parity.NULL_U_MIN_FLOOR).  Measured while choosing the pooling (16 instances): a 1e-10 error
+      fails from 8 instances on, a 1e-12 one (rounding level) passes at every size."""
+    from parity import NULL_U_MIN_FLOOR, leave_one_out, null_row, null_summary, run_divergence
     opt = dict(OPT, maxiter=20)
     variants, bad = [], []
-    for s in range(12):
+    for s in range(14):
         Z, x0, y0 = G.generate_instance(100, 7000 + s)
         S = Z + Z.T
         ref = O.RIPTRMOracle(opt).run(O.NonnegPCAVectorized(S, S=S), x0, y0)
@@ -335,9 +338,13 @@ def test_null_calibration_accepts_variants_and_rejects_hessian_error():
             runs.append(run_divergence(r.log, r.x[inv], r.y[inv], ref.log, ref.x, ref.y))
         variants.append(runs)
         r = O.RIPTRMOracle(opt).run(_HessianError(S, 1e-9, 7000 + s), x0, y0)
-        bad.append(null_row(run_divergence(r.log, r.x, r.y, ref.log, ref.x, ref.y), runs))
+        bad.append(run_divergence(r.log, r.x, r.y, ref.log, ref.x, ref.y))
     assert all(v["div_row"] < v["rows"] for runs in variants for v in runs)   # the flip regime
     null = null_summary(leave_one_out(variants))
     assert null["ok"], null
-    neg = null_summary(bad)
-    assert not neg["ok"] and neg["mean_u"] < neg["mean_u_min"], neg
+    for K in (4, 5, 6):
+        for n in (6, 8, 11, 12, 14):
+            neg = null_summary([null_row(b, runs[:K]) for b, runs in zip(bad[:n], variants[:n])])
+            assert not neg["ok"], (K, n, neg)
+            assert (neg["mean_u_min"] > NULL_U_MIN_FLOOR) == (n >= 11), (K, n, neg["mean_u_min"])
+        assert null_summary(leave_one_out([runs[:K + 1] for runs in variants]))["ok"], K
