@@ -78,6 +78,9 @@ struct riptrm_ctx {
   int64_t big_cg_checked = 0, big_cg_skipped = 0;    // since the context was created (riptrm_trs_skip_stats)
   void* eig_scratch = nullptr;   // riptrm_sym_eig's d / e / tau vectors (context-owned)
   size_t eig_scratch_bytes = 0;
+  void* tri_grid = nullptr;      // the distributed tridiagonalisation's granules (riptrm_tri.h, context-owned)
+  size_t tri_grid_bytes = 0;
+  int64_t tri_fallbacks = 0;     // subproblems the tridiagonal path handed to the eigendecomposition path
 };
 
 // riptrm_trs_big.hip

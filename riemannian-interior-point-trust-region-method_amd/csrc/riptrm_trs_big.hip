@@ -37,6 +37,7 @@
 #include <vector>
 #include "riptrm_ctx.h"
 #include "riptrm_eig.h"
+#include "riptrm_tri.h"
 #include "riptrm_wave.h"
 
 using namespace riptrm;
@@ -56,7 +57,8 @@ constexpr int CG_RPT = CG_WG_MAX / WG;     // x / r elements per thread there
 enum Sc : int {
   SC_TAU = 0, SC_GAM, SC_XX, SC_COEF, SC_WC, SC_AN, SC_ATOL, SC_RHO, SC_RHO_PREV, SC_IT, SC_DONE,
   SC_CG_OK, SC_P1OBJ, SC_KIND, SC_LAM1, SC_MINEIG, SC_INTERIOR, SC_DELTA, SC_XSX, SC_YX,
-  SC_XOBJ, SC_BKIND, SC_BLAM1   // the boundary / hard-case candidate, before the interior choice
+  SC_XOBJ, SC_BKIND, SC_BLAM1,  // the boundary / hard-case candidate, before the interior choice
+  SC_TRI_FB                      // the tridiagonal path handed this subproblem to the eigendecomposition path
 };
 
 __host__ __device__ inline int64_t vpad(int64_t n) { return (n + 63) / 64 * 64; }
@@ -66,9 +68,9 @@ enum Vs : int { VS_W = 0, VS_U, VS_A, VS_CGX, VS_R, VS_P, VS_Q, VS_EV, VS_EW, VS
 // one slot for matrices of order N: [N x N][NVS vectors of vpad(N)][NSC scalars]; after the slots:
 // int32 info[slots], ids[slots], flag[8], sweeps[slots], hits[slots] (+ pad), double residual[slots]
 // ... then [the eigensolver's reflectors: riptrm_eig::refl_doubles(N)] (orders it serves)
-// (every order m <= min(N, EIG_LDS_MAX) the hand-written eigensolver serves)
+// (every order m <= N the hand-written eigensolver or the tridiagonal path serves: N <= TRI_MAX)
 __host__ __device__ inline int64_t refl_of(int64_t N) {
-  return (int64_t)riptrm_eig::refl_doubles((int)(N < riptrm_eig::EIG_LDS_MAX ? N : riptrm_eig::EIG_LDS_MAX));
+  return (int64_t)riptrm_eig::refl_doubles((int)(N <= riptrm_tri::TRI_MAX ? N : riptrm_eig::EIG_LDS_MAX));
 }
 __host__ __device__ inline int64_t slot_doubles(int64_t N) { return N * N + NVS * vpad(N) + NSC + refl_of(N); }
 __host__ __device__ inline int64_t off_vec(int64_t N, int k) { return N * N + k * vpad(N); }
@@ -1173,21 +1175,29 @@ __device__ __forceinline__ double* cache_of(double* cache, int64_t N, int b) { r
 
 // after the trial point's eigensolve: slot k's eigenvectors (the n x n buffer), eigenvalues and the
 // trial point (x_new, y_new) -> instance ids[k]'s cache entry; valid iff the eigensolve converged
-__global__ void __launch_bounds__(256) k_cache_store(DevParams P, Bat B, double* cache, int64_t N) {
+// tri: the tridiagonal path's T (d, e: the first two rows of the eigenvector area) instead of Q
+__global__ void __launch_bounds__(256) k_cache_store(DevParams P, Bat B, double* cache, int64_t N, int tri) {
   const int k = blockIdx.y, b = B.ids[k];
   const Slot q = slot_at(B, k);
   double* C = cache_of(cache, N, b);
   const int n = P.n;
   const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (e < (int64_t)n * n) C[e] = q.M[e];
+  if (tri) {
+    if (e < n - 1) {
+      C[e] = q.v[VS_R][e];
+      C[N + e] = q.v[VS_P][e];
+    }
+  } else if (e < (int64_t)n * n) {
+    C[e] = q.M[e];
+  }
   if (e < n - 1) C[N * N + e] = q.v[VS_EV][e];
   if (e < n) {
     C[N * N + vpad(N) + e] = vec_of(P, V_IN1, b)[e];
     C[N * N + 2 * vpad(N) + e] = vec_of(P, V_YNEW, b)[e];
   }
   if (e == 0) C[N * N + 3 * vpad(N)] = *q.info == 0 ? 1.0 : 0.0;
-  // the reflectors of the compact eigenvectors (riptrm_eig.h), when the hand-written solver made them
-  if (n - 1 <= riptrm_eig::EIG_LDS_MAX && e < (int64_t)riptrm_eig::refl_doubles(n - 1))
+  // the reflectors of the compact eigenvectors (riptrm_eig.h) or of T, when the hand-written paths made them
+  if ((n - 1 <= riptrm_eig::EIG_LDS_MAX || tri) && e < (int64_t)riptrm_eig::refl_doubles(n - 1))
     C[N * N + 3 * vpad(N) + 8 + e] = B.base[(int64_t)k * B.sd + off_refl(B.N) + e];
 }
 
@@ -1206,15 +1216,22 @@ __global__ void __launch_bounds__(256) k_cache_check(DevParams P, Bat B, const d
 }
 
 // a cache hit: the cached eigenvectors / eigenvalues -> slot k (after its CG used the matrix)
-__global__ void __launch_bounds__(256) k_cache_load(DevParams P, Bat B, const double* cache, int64_t N) {
+__global__ void __launch_bounds__(256) k_cache_load(DevParams P, Bat B, const double* cache, int64_t N, int tri) {
   const int k = blockIdx.y, b = B.ids[k];
   const Slot q = slot_at(B, k);
   const double* C = cache + (int64_t)b * cache_doubles(N);
   const int n = P.n;
   const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (e < (int64_t)n * n) q.M[e] = C[e];
+  if (tri) {
+    if (e < n - 1) {
+      q.v[VS_R][e] = C[e];
+      q.v[VS_P][e] = C[N + e];
+    }
+  } else if (e < (int64_t)n * n) {
+    q.M[e] = C[e];
+  }
   if (e < n - 1) q.v[VS_EV][e] = C[N * N + e];
-  if (n - 1 <= riptrm_eig::EIG_LDS_MAX && e < (int64_t)riptrm_eig::refl_doubles(n - 1))
+  if ((n - 1 <= riptrm_eig::EIG_LDS_MAX || tri) && e < (int64_t)riptrm_eig::refl_doubles(n - 1))
     B.base[(int64_t)k * B.sd + off_refl(B.N) + e] = C[N * N + 3 * vpad(N) + 8 + e];
   if (e == 0) *q.info = 0;
 }
@@ -1355,6 +1372,11 @@ static int big_handle(riptrm_ctx* c) {
 }
 
 void riptrm_big_release(riptrm_ctx* c) {
+  if (c && c->tri_grid) {
+    (void)hipFree(c->tri_grid);
+    c->tri_grid = nullptr;
+    c->tri_grid_bytes = 0;
+  }
   if (c && c->eig_scratch) {
     (void)hipFree(c->eig_scratch);
     c->eig_scratch = nullptr;
@@ -1396,6 +1418,14 @@ static int refl_apply(riptrm_ctx* c, const Bat& B, int cnt, int m, int64_t voff,
   return RIPTRM_OK;
 }
 
+// the distributed tridiagonalisation (riptrm_tri.h) for the hand-written eigensolver's first phase:
+// RIPTRM_EIG_TRI=1 (A/B; orders >= 64)
+static int tri_launch(riptrm_ctx* c, const riptrm_tri::TriArgs& a, int cnt, int m);
+static bool eig_tri_front(int m) {
+  const char* e = getenv("RIPTRM_EIG_TRI");
+  return m >= 64 && e && e[0] == '1';
+}
+
 // k_eig_lds with 1024 threads per matrix (16 waves: the symv and rank-2 update of the
 // tridiagonalisation hide more LDS latency), or 512 (RIPTRM_EIG_THREADS=512, A/B)
 static int launch_eig(riptrm_ctx* c, int cnt, int m, double* A, int64_t a_stride, int lda, double* ev, int64_t ev_stride,
@@ -1409,10 +1439,25 @@ static int launch_eig(riptrm_ctx* c, int cnt, int m, double* A, int64_t a_stride
     // vectors of T over ~50 indices per workgroup (four per matrix at m = 199: the whole chip for a
     // batch of 64), the orthogonality pass (one per matrix).  The same arithmetic as one launch.
     const int yv = (m + 49) / 50;
-    HIPCHK(c, hipFuncSetAttribute((const void*)riptrm_eig::k_eig_lds<1024, 1>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)shm));
-    hipLaunchKernelGGL((riptrm_eig::k_eig_lds<1024, 1>), dim3(cnt), dim3(1024), shm, c->stream, A, a_stride, lda, m, ev,
-                       ev_stride, d, e, sc_stride, R, r_stride, infos, vectors, nullptr);
+    if (eig_tri_front(m)) {   // T across the chip, then phase 1's split / non-finite test
+      riptrm_tri::TriArgs ta{};
+      ta.A0 = A;
+      ta.a_stride = a_stride;
+      ta.lda = lda;
+      ta.d0 = d;
+      ta.e0 = e;
+      ta.de_stride = sc_stride;
+      ta.R0 = R;
+      ta.r_stride = r_stride;
+      ta.infos = infos;
+      if (int rc = tri_launch(c, ta, cnt, m)) return rc;
+      hipLaunchKernelGGL(riptrm_tri::k_tri_split, dim3(cnt), dim3(256), 0, c->stream, d, e, sc_stride, m, infos, ev, ev_stride);
+    } else {
+      HIPCHK(c, hipFuncSetAttribute((const void*)riptrm_eig::k_eig_lds<1024, 1>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)shm));
+      hipLaunchKernelGGL((riptrm_eig::k_eig_lds<1024, 1>), dim3(cnt), dim3(1024), shm, c->stream, A, a_stride, lda, m, ev,
+                         ev_stride, d, e, sc_stride, R, r_stride, infos, vectors, nullptr);
+    }
     HIPCHK(c, hipFuncSetAttribute((const void*)riptrm_eig::k_eig_lds<512, 2>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   (int)shm));
     // the bisection over ~25 eigenvalues per workgroup up to order 128 (four waves of eight-lane
@@ -1592,6 +1637,130 @@ static int compact_trs(riptrm_ctx* c, const Bat& B, int cnt, int m, int64_t aoff
   return refl_apply(c, B, cnt, m, off_vec(N, VS_X), off_vec(N, VS_X), 1);
 }
 
+// ---- the tridiagonal path (riptrm_tri.h): orders above the one-workgroup eigensolver ------------------
+// RIPTRM_BIG_EIG unset (or 'h'): orders TRI_MIN .. TRI_MAX take it; otherwise rocSOLVER (A/B)
+static bool tri_mode(int m) {
+  const char* e = getenv("RIPTRM_BIG_EIG");
+  return m >= riptrm_tri::TRI_MIN && m <= riptrm_tri::TRI_MAX && !(e && e[0] != 'h');
+}
+
+template <int EL>
+static int tri_launch_el(riptrm_ctx* c, riptrm_tri::TriArgs a, int cnt, int m) {
+  constexpr int RW = 32 / EL;
+  const int G = riptrm_tri::tri_groups(m);
+  auto kern = riptrm_tri::k_tridiag_dist<EL, RW>;
+  int nb = 0;
+  HIPCHK(c, hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kern, riptrm_tri::TT, 0));
+  const int64_t cap = (int64_t)nb * c->ncu;
+  if (nb < 1 || cap < G) return fail(c, RIPTRM_E_HIP, "tridiagonalisation: " + std::to_string(G) + " workgroups per matrix do not fit");
+  const int per = (int)std::min<int64_t>(cnt, cap / G);   // matrices per cooperative launch
+  const size_t gbytes = (size_t)riptrm_tri::tri_granules(m) * 16 * per;
+  if (c->tri_grid_bytes < gbytes) {
+    if (c->tri_grid) HIPCHK(c, hipFree(c->tri_grid));
+    c->tri_grid = nullptr;
+    c->tri_grid_bytes = 0;
+    HIPCHK(c, hipMalloc(&c->tri_grid, gbytes));
+    c->tri_grid_bytes = gbytes;
+  }
+  HIPCHK(c, hipMemsetAsync(a.infos, 0, (size_t)cnt * sizeof(int32_t), c->stream));
+  for (int k0 = 0; k0 < cnt; k0 += per) {
+    const int nk = std::min(per, cnt - k0);
+    HIPCHK(c, hipMemsetAsync(c->tri_grid, 0, (size_t)riptrm_tri::tri_granules(m) * 16 * nk, c->stream));
+    a.k0 = k0;
+    a.grid = c->tri_grid;
+    a.grid_bytes = (int64_t)c->tri_grid_bytes;
+    a.m = m;
+    a.G = G;
+    void* args[] = {&a};
+    HIPCHK(c, hipLaunchCooperativeKernel((const void*)kern, dim3(G, nk), dim3(riptrm_tri::TT), args, 0, c->stream));
+  }
+  return RIPTRM_OK;
+}
+
+// k_tridiag_dist over cnt matrices (a's pointers and strides; infos zeroed first, 3: an exchange
+// timed out)
+static int tri_launch(riptrm_ctx* c, const riptrm_tri::TriArgs& a, int cnt, int m) {
+  switch (riptrm_tri::tri_el(m)) {
+    case 4: return tri_launch_el<4>(c, a, cnt, m);
+    case 8: return tri_launch_el<8>(c, a, cnt, m);
+    default: return tri_launch_el<16>(c, a, cnt, m);
+  }
+}
+
+// T = H^T A H of the pass's cnt slots (A at slot offset aoff, leading dimension lda): d -> VS_R, e ->
+// VS_P, the reflectors at off_refl; infos zeroed first (3: an exchange timed out)
+static int tri_tridiag(riptrm_ctx* c, const Bat& B, int cnt, int m, int64_t aoff, int64_t lda) {
+  riptrm_tri::TriArgs a{};
+  a.A0 = B.base + aoff;
+  a.a_stride = B.sd;
+  a.lda = lda;
+  a.d0 = B.base + off_vec(B.N, VS_R);
+  a.e0 = B.base + off_vec(B.N, VS_P);
+  a.de_stride = B.sd;
+  a.R0 = B.base + off_refl(B.N);
+  a.r_stride = B.sd;
+  a.infos = B.infos;
+  return tri_launch(c, a, cnt, m);
+}
+
+static int tri_refl(riptrm_ctx* c, const Bat& B, int cnt, int m, int64_t voff, int64_t ooff, int backward) {
+  const dim3 grid(1, cnt);
+  switch (riptrm_tri::tri_el(m)) {
+    case 4: hipLaunchKernelGGL(riptrm_tri::k_refl_big<4>, grid, dim3(64), 0, c->stream, B.base, B.sd, 0, m, off_refl(B.N), voff, ooff, backward); break;
+    case 8: hipLaunchKernelGGL(riptrm_tri::k_refl_big<8>, grid, dim3(64), 0, c->stream, B.base, B.sd, 0, m, off_refl(B.N), voff, ooff, backward); break;
+    default: hipLaunchKernelGGL(riptrm_tri::k_refl_big<16>, grid, dim3(64), 0, c->stream, B.base, B.sd, 0, m, off_refl(B.N), voff, ooff, backward); break;
+  }
+  HIPCHK(c, hipGetLastError());
+  return RIPTRM_OK;
+}
+
+template <int EL>
+static int tri_solve_el(riptrm_ctx* c, const Bat& B, int cnt, int m, const double* D, int64_t dstride, double tolhc, int mode) {
+  const int64_t N = B.N;
+  const size_t shm = (size_t)8 * 64 * EL * sizeof(double);
+  auto kern = riptrm_tri::k_tri_solve<EL>;
+  HIPCHK(c, hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm));
+  const riptrm_tri::TriSc S{SC_CG_OK, SC_P1OBJ, SC_KIND, SC_LAM1, SC_MINEIG, SC_INTERIOR, SC_DELTA, SC_AN, SC_ATOL, SC_IT,
+                            SC_DONE, SC_TRI_FB};
+  hipLaunchKernelGGL(kern, dim3(1, cnt), dim3(256), shm, c->stream, B.base, B.sd, B.infos, m, off_vec(N, VS_R),
+                     off_vec(N, VS_P), off_vec(N, VS_G), off_vec(N, VS_A), off_vec(N, VS_PE), off_vec(N, VS_CGX),
+                     off_vec(N, VS_EV), off_sc(N), S, D, dstride, B.ids, tolhc, mode);
+  HIPCHK(c, hipGetLastError());
+  return RIPTRM_OK;
+}
+
+// after tri_tridiag (or a cache load of T): mode 1 the smallest eigenvalue only (-> VS_EV[0]); mode 0
+// the subproblem min x^T A x / 2 + a^T x, ||x|| <= Delta (a at VS_A): b = H^T a, k_tri_solve, x = H pe
+// -> VS_X and the result scalars.  Subproblems it cannot serve set SC_TRI_FB (tri_fallback_ids).
+static int tri_finish(riptrm_ctx* c, const Bat& B, int cnt, int m, const double* D, int64_t dstride, double tolhc, int mode) {
+  const int64_t N = B.N;
+  if (mode == 0)
+    if (int rc = tri_refl(c, B, cnt, m, off_vec(N, VS_A), off_vec(N, VS_G), 0)) return rc;
+  int rc;
+  switch (riptrm_tri::tri_el(m)) {
+    case 4: rc = tri_solve_el<4>(c, B, cnt, m, D, dstride, tolhc, mode); break;
+    case 8: rc = tri_solve_el<8>(c, B, cnt, m, D, dstride, tolhc, mode); break;
+    default: rc = tri_solve_el<16>(c, B, cnt, m, D, dstride, tolhc, mode); break;
+  }
+  if (rc) return rc;
+  if (mode == 0) return tri_refl(c, B, cnt, m, off_vec(N, VS_PE), off_vec(N, VS_X), 1);
+  return RIPTRM_OK;
+}
+
+// the ids of the pass whose subproblem set SC_TRI_FB (a hard case or a multiple smallest eigenvalue).
+// Synchronises.
+static int tri_fallback_ids(riptrm_ctx* c, const Bat& B, int cnt, const int32_t* ids, std::vector<int32_t>& out) {
+  out.clear();
+  std::vector<double> fb(cnt);
+  HIPCHK(c, hipMemcpy2DAsync(fb.data(), sizeof(double), B.base + off_sc(B.N) + SC_TRI_FB, (size_t)B.sd * sizeof(double),
+                             sizeof(double), cnt, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  for (int k = 0; k < cnt; ++k)
+    if (fb[k] != 0.0) out.push_back(ids[k]);
+  c->tri_fallbacks += (int64_t)out.size();
+  return RIPTRM_OK;
+}
+
 static int big_solve(riptrm_ctx* c, const Bat& B, int cnt, int64_t aoff, int lda, int m, const double* D, int64_t dstride,
                      double tolhc) {
   if (int rc = big_cg(c, B, cnt, aoff, lda, m, D, dstride)) return rc;
@@ -1677,18 +1846,43 @@ int riptrm_big_service(riptrm_ctx* c, int* served) {
       const int cnt = (int)std::min<size_t>((size_t)S, L.size() - k0);
       if (int rc = put_ids(c, Bt, L.data() + k0, cnt)) return rc;
       if (int rc = big_nonnegpca_matrix(c, Bt, cnt, kind == 2)) return rc;
+      const bool tri = tri_mode(n - 1);
       if (kind == 2) {
         // eigenvectors too (the next subproblem at this point reuses them); the value is the same
-        // computation with or without the cache
-        if (int rc = eig_batched(c, Bt, cnt, true, n - 1, aoff, n)) return rc;
+        // computation with or without the cache.  Tridiagonal path: T and its reflectors are kept.
+        if (tri) {
+          if (int rc = tri_tridiag(c, Bt, cnt, n - 1, aoff, n)) return rc;
+          if (int rc = tri_finish(c, Bt, cnt, n - 1, P.st + ST_DELTA, ST_N, P.opt.trs_tolhardcase, 1)) return rc;
+        } else if (int rc = eig_batched(c, Bt, cnt, true, n - 1, aoff, n)) {
+          return rc;
+        }
         hipLaunchKernelGGL(k_finish_mineig, dim3(blocks_of(cnt, 64)), dim3(64), 0, c->stream, P, Bt, cnt);
         if (cached)
           hipLaunchKernelGGL(k_cache_store, dim3(blocks_of((int64_t)n * n, 256), cnt), dim3(256), 0, c->stream, P, Bt, cache,
-                             CN);
+                             CN, tri ? 1 : 0);
+      } else if (tri) {   // T (or the cached one), then the subproblem in T's coordinates
+        if (kind == 1)
+          hipLaunchKernelGGL(k_cache_load, dim3(blocks_of((int64_t)n * n, 256), cnt), dim3(256), 0, c->stream, P, Bt, cache,
+                             CN, 1);
+        else if (int rc = tri_tridiag(c, Bt, cnt, n - 1, aoff, n))
+          return rc;
+        if (int rc = tri_finish(c, Bt, cnt, n - 1, P.st + ST_DELTA, ST_N, P.opt.trs_tolhardcase, 0)) return rc;
+        hipLaunchKernelGGL(k_finish_dir, dim3(1, cnt), dim3(WG), 0, c->stream, P, Bt);
+        std::vector<int32_t> fbi;
+        if (int rc = tri_fallback_ids(c, Bt, cnt, L.data() + k0, fbi)) return rc;
+        for (size_t f0 = 0; f0 < fbi.size(); f0 += (size_t)S) {   // hard cases: the eigendecomposition path
+          const int fc = (int)std::min<size_t>((size_t)S, fbi.size() - f0);
+          if (int rc = put_ids(c, Bt, fbi.data() + f0, fc)) return rc;
+          if (int rc = big_nonnegpca_matrix(c, Bt, fc, 0)) return rc;
+          if (int rc = big_cg(c, Bt, fc, aoff, n, n - 1, P.st + ST_DELTA, ST_N)) return rc;
+          if (int rc = eig_batched(c, Bt, fc, true, n - 1, aoff, n)) return rc;
+          if (int rc = big_after_eig(c, Bt, fc, aoff, n, n - 1, P.opt.trs_tolhardcase)) return rc;
+          hipLaunchKernelGGL(k_finish_dir, dim3(1, fc), dim3(WG), 0, c->stream, P, Bt);
+        }
       } else if (eig_compact(n - 1)) {   // eigenpairs (or the cached ones), then the CG in eigen-coordinates
         if (kind == 1)
           hipLaunchKernelGGL(k_cache_load, dim3(blocks_of((int64_t)n * n, 256), cnt), dim3(256), 0, c->stream, P, Bt, cache,
-                             CN);
+                             CN, 0);
         else if (int rc = eig_batched(c, Bt, cnt, true, n - 1, aoff, n))
           return rc;
         if (int rc = compact_trs(c, Bt, cnt, n - 1, aoff, n, P.st + ST_DELTA, ST_N, P.opt.trs_tolhardcase,
@@ -1699,7 +1893,7 @@ int riptrm_big_service(riptrm_ctx* c, int* served) {
         if (int rc = big_cg(c, Bt, cnt, aoff, n, n - 1, P.st + ST_DELTA, ST_N)) return rc;
         if (kind == 1)
           hipLaunchKernelGGL(k_cache_load, dim3(blocks_of((int64_t)n * n, 256), cnt), dim3(256), 0, c->stream, P, Bt, cache,
-                             CN);
+                             CN, 0);
         else if (int rc = eig_batched(c, Bt, cnt, true, n - 1, aoff, n))
           return rc;
         if (int rc = big_after_eig(c, Bt, cnt, aoff, n, n - 1, P.opt.trs_tolhardcase)) return rc;
@@ -1778,7 +1972,11 @@ int riptrm_big_gep_ids(riptrm_ctx* c, int dim, const int32_t* sel, int count, co
     hipLaunchKernelGGL(k_load, dim3(blocks_of(kmode == 1 ? (int64_t)dim : (int64_t)dim * dim, 256), cnt), dim3(256), 0,
                        c->stream, Bt, dim, A, lda, a_stride, a, ldv);
     HIPCHK(c, hipGetLastError());
-    if (mineig_only) {
+    std::vector<int32_t> fb_ids;   // subproblems the tridiagonal path hands to the eigendecomposition path
+    if (mineig_only && tri_mode(dim)) {
+      if (int rc = tri_tridiag(c, Bt, cnt, dim, 0, dim)) return rc;
+      if (int rc = tri_finish(c, Bt, cnt, dim, Delta, 1, tolhc, 1)) return rc;
+    } else if (mineig_only) {
       if (int rc = eig_batched(c, Bt, cnt, kmode == 2, dim, 0, dim)) return rc;
       if (kmode == 2)
         hipLaunchKernelGGL(k_kc_store, dim3(blocks_of((int64_t)dim * dim, 256), cnt), dim3(256), 0, c->stream, Bt, dim,
@@ -1798,6 +1996,10 @@ int riptrm_big_gep_ids(riptrm_ctx* c, int dim, const int32_t* sel, int count, co
         HIPCHK(c, hipMemcpy2DAsync(skip_done.data(), sizeof(double), Bt.base + off_sc(Bt.N) + SC_DONE,
                                    (size_t)Bt.sd * sizeof(double), sizeof(double), cnt, hipMemcpyDeviceToHost, c->stream));
       }
+    } else if (tri_mode(dim)) {   // T = H^T A H across the chip, the subproblem in T's coordinates
+      if (int rc = tri_tridiag(c, Bt, cnt, dim, 0, dim)) return rc;
+      if (int rc = tri_finish(c, Bt, cnt, dim, Delta, 1, tolhc, 0)) return rc;
+      if (int rc = tri_fallback_ids(c, Bt, cnt, sel + b0, fb_ids)) return rc;
     } else if (per_instance && cg_one_workgroup(dim, cnt) && !getenv_is("RIPTRM_CG_SKIP", '0')) {
       // eigenpairs, g = Q^T a and the boundary candidate first; the CG then reads A from the
       // caller's array and is skipped where the eigenpairs prove the interior candidate cannot win
@@ -1857,6 +2059,28 @@ int riptrm_big_gep_ids(riptrm_ctx* c, int dim, const int32_t* sel, int count, co
       for (int k = 0; k < cnt; ++k)
         if (info[k] != 0)
           HIPCHK(c, hipMemcpyAsync(kind + sel[b0 + k], &eigfail, sizeof(int32_t), hipMemcpyHostToDevice, c->stream));
+    }
+    // hard cases of the tridiagonal path: the eigendecomposition path (rocSOLVER dsyevd), one more pass
+    if (!fb_ids.empty()) {
+      const int fc = (int)fb_ids.size();   // <= cnt <= big_slots
+      if (int rc = put_ids(c, Bt, fb_ids.data(), fc)) return rc;
+      hipLaunchKernelGGL(k_load, dim3(blocks_of((int64_t)dim * dim, 256), fc), dim3(256), 0, c->stream, Bt, dim, A, lda,
+                         a_stride, a, ldv);
+      HIPCHK(c, hipGetLastError());
+      if (int rc = big_solve(c, Bt, fc, 0, dim, dim, Delta, 1, tolhc)) return rc;
+      HIPCHK(c, hipMemcpyAsync(info.data(), Bt.infos, (size_t)fc * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+      HIPCHK(c, hipStreamSynchronize(c->stream));
+      for (int k = 0; k < fc; ++k)
+        if (info[k] != 0 && !per_instance)
+          return fail(c, RIPTRM_E_HIP, "Exact_RepMat: rocsolver_dsyevd did not converge (info " + std::to_string(info[k]) +
+                                           ") on subproblem " + std::to_string(fb_ids[k]));
+      hipLaunchKernelGGL(k_gep_out, dim3(blocks_of(dim, 256), fc), dim3(256), 0, c->stream, Bt, dim, ldv, x, lam1, kind,
+                         mineig);
+      HIPCHK(c, hipGetLastError());
+      static const int32_t eigfail2 = RIPTRM_TCG_EIGFAIL;
+      for (int k = 0; k < fc; ++k)
+        if (info[k] != 0)
+          HIPCHK(c, hipMemcpyAsync(kind + fb_ids[k], &eigfail2, sizeof(int32_t), hipMemcpyHostToDevice, c->stream));
     }
   }
   return RIPTRM_OK;

@@ -514,14 +514,17 @@ def test_exact_repmat_reference_defaults_drop_in(fixture_n50):
 
 
 @pytest.mark.timeout(600)
+@pytest.mark.parametrize("n", [200, 260])
 @pytest.mark.parametrize("sos", [True, False])
-def test_exact_repmat_above_lds_size_matches_oracle(sos):
-    """NonnegPCA n = 200 (manifold.dim 199) with Exact_RepMat: the HBM path (frame matrix densified
-    from S, SciPy CG, rocSOLVER dsyevd, the trial-point eigenvalue with the second-order test) against
-    the oracle (the reference's 2n x 2n pencil per inner step, trs_oracle.trs_gep; its per-constraint
-    HVPs build the matrix), with the Exact_RepMat trajectory bar (parity.compare_until_flip)."""
+def test_exact_repmat_above_lds_size_matches_oracle(sos, n):
+    """NonnegPCA n = 200 / 260 (manifold.dim 199 / 259) with Exact_RepMat: the HBM path (frame matrix
+    densified from S; at 199 the hand-written eigensolver and the CG in its eigen-coordinates, at 259
+    the distributed tridiagonalisation and the subproblem in T's coordinates, riptrm_tri.h; the
+    trial-point eigenvalue with the second-order test) against the oracle (the reference's 2n x 2n
+    pencil per inner step, trs_oracle.trs_gep; its per-constraint HVPs build the matrix), with the
+    Exact_RepMat trajectory bar (parity.compare_until_flip)."""
     from parity import compare_until_flip
-    Z, x0, y0 = G.generate_instance(200, 77)
+    Z, x0, y0 = G.generate_instance(n, 77)
     opt = dict(TRS_solver="Exact_RepMat", second_order_stationarity=sos, maxiter=4)
     eng = _engine(Z)
     res = eng.solve(x0[None], y0[None], _gpu_opt(**opt))
@@ -559,10 +562,12 @@ def test_exact_repmat_lds_and_hbm_paths_agree_near_97(monkeypatch):
 
 
 @pytest.mark.timeout(600)
-def test_exact_repmat_above_lds_size_batched(monkeypatch):
+@pytest.mark.parametrize("n", [200, 260])
+def test_exact_repmat_above_lds_size_batched(monkeypatch, n):
     """The HBM Exact_RepMat service over a batch (csrc/riptrm_trs_big.hip: every parked instance in
-    one pass, one workspace slot each, batched dsyevd): six n = 200 instances with the second-order
-    test.  Each instance's trajectory is the one it has solved alone (a slot's arithmetic does not
+    one pass, one workspace slot each; n = 200 the batched hand-written eigensolver, n = 260 the
+    distributed tridiagonalisation, several matrices per cooperative launch): six instances with the
+    second-order test.  Each instance's trajectory is the one it has solved alone (a slot's arithmetic does not
     depend on the pass it shares), whichever CG form serves it (one workgroup per slot or the
     grid-wide launches: the same sums in the same order), however many slots the scratch budget
     allows (one slot: six passes) and whether the eigendecomposition cache serves the subproblems at
@@ -570,7 +575,7 @@ def test_exact_repmat_above_lds_size_batched(monkeypatch):
     instance 0 also meets the oracle bar of the solo test above."""
     from parity import compare_until_flip
     B, K = 6, 3
-    insts = [G.generate_instance(200, 90 + b) for b in range(B)]
+    insts = [G.generate_instance(n, 90 + b) for b in range(B)]
     Zs = np.stack([z for z, _, _ in insts])
     xs = np.stack([x for _, x, _ in insts])
     ys = np.stack([y for _, _, y in insts])
