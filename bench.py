@@ -599,6 +599,9 @@ def main():
         if args.trs == "Exact_RepMat" and 96 < n - 1 <= 199 and rank == 0:
             # the eigensolver, not the S-pass, sets this line's time: price it, keep the S-pass in detail
             spass_roofline, roofline = roofline, eig_roofline(n - 1, B, dev)
+        elif args.trs == "Exact_RepMat" and 199 < n - 1 <= 1024 and rank == 0:
+            # the tridiagonal path's subproblem service (riptrm_tri.h) sets this line's time
+            spass_roofline, roofline = roofline, tri_roofline(n - 1, dev)
         cpu = None
         if args.cpu_budget > 0 and world == 1:
             positions = window_positions(W, K, args.cycle)
@@ -661,10 +664,10 @@ def main():
                        **({"exact_repmat_note": (
                            "manifold.dim > 96: the subproblems are served in batched passes between lock-step "
                            "chunks (csrc/riptrm_trs_big.hip); the pass, not the S-pass (detail.spass_roofline), sets "
-                           "this line's time: the hand-written eigensolver (csrc/riptrm_eig.h, order <= 199; rocSOLVER "
-                           "dsyevd above) takes most of the GPU time (profiles/r5_exact_rocprofv3_kernel_stats.csv); "
-                           "the CG runs in its eigen-coordinates; a subproblem at an accepted trial point reuses that "
-                           "point's eigenpairs (riptrm_trs_bind_cache)"),
+                           "this line's time: up to order 199 the hand-written eigensolver (csrc/riptrm_eig.h) with the "
+                           "CG in its eigen-coordinates; 200..1024 the cooperative tridiagonalisation and the subproblem "
+                           "in T's coordinates (csrc/riptrm_tri.h); a subproblem at an accepted trial point reuses that "
+                           "point's eigenpairs / tridiagonal form (riptrm_trs_bind_cache)"),
                            "trs_cache": dict(zip(("hits", "subproblems"), eng.trs_cache_stats()))}
                           if args.trs == "Exact_RepMat" and n - 1 > engine.C["RIPTRM_TRS_DIM_MAX"] else {})},
         }
@@ -882,6 +885,47 @@ def si_cpu_pool(K: int, budget_s: float, procs: int, trs: str, d: int = 5, inner
                        f"batch's start i (fixture starts a.. in order) over outer iterations 1..{K} within a "
                        f"{budget_s:.0f} s budget; {len(rates)}/{procs} completed, aggregate = mean complete per-process "
                        f"rate x {procs}, evaluation time excluded as RIPTRM.py:932-941")}
+
+
+def tri_roofline(m: int, dev, reps: int = 5):
+    """The Exact_RepMat HBM service's work for one subproblem of order 200..1024 (csrc/riptrm_tri.h:
+    the cooperative tridiagonalisation k_tridiag_dist, then k_refl_big / k_tri_solve), timed live with
+    HIP events around riptrm_trs_gep on one frame-like matrix (O(1) symmetric part plus diagonal
+    barrier terms up to 1e6).  Bound: latency.  The tridiagonalisation's m - 1 columns are one all-to-all
+    exchange each (every workgroup publishes its rows' p = tau A v and polls every other's), a chain no
+    bandwidth can shorten; the floor is m - 1 hand-offs at the measured single hop
+    (MI355X_MICROARCH.md, handoff-1to1: ~1.0 us on an idle chip).  Its flops (4/3 m^3) at the FP64
+    vector peak are reported beside it (flops_frac)."""
+    import numpy as np
+    import torch
+    import trs
+    rs = np.random.RandomState(m)
+    D = rs.randn(m, m) / np.sqrt(m)
+    D = D + D.T + np.diag(np.where(rs.rand(m) < 0.3, 10.0 ** rs.uniform(2, 6, m), 0.0))
+    A = torch.tensor(D[None], dtype=torch.float64, device=dev)
+    a = torch.tensor(rs.randn(1, m), dtype=torch.float64, device=dev)
+    Del = torch.tensor([0.5], dtype=torch.float64, device=dev)
+    for _ in range(2):
+        trs.trs_gep_batched(A, a, Del, 1e-8)
+    ts = []
+    for _ in range(reps):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        trs.trs_gep_batched(A, a, Del, 1e-8)
+        e1.record()
+        torch.cuda.synchronize(dev)
+        ts.append(e0.elapsed_time(e1) / 1e3)
+    t = sorted(ts)[len(ts) // 2]
+    hop = 1.0e-6
+    ach = (m - 1) / t
+    return {"bound": "latency", "achieved": ach, "peak": 1.0 / hop, "unit": "columns/s", "frac": ach / (1.0 / hop),
+            "traffic": None, "avg_launch_us": t * 1e6,
+            "kernel": (f"riptrm_tri (k_tridiag_dist on {(m + 15) // 16 if m > 512 else (m + 31) // 32 if m > 256 else (m + 63) // 64} "
+                       "cooperative workgroups, k_refl_big, k_tri_solve): one TRSgep subproblem of order "
+                       f"{m} through riptrm_trs_gep"),
+            "flops_frac": (4.0 / 3.0 * m ** 3 / t) / 81.7e12,
+            "why": ("latency-bound: one all-to-all exchange per tridiagonalisation column; floor = m - 1 hand-offs "
+                    "at ~1.0 us (MI355X_MICROARCH.md handoff-1to1, idle chip)")}
 
 
 LDS_BYTES_PER_CLK = 256       # MI355X_MICROARCH.md: LDS 64 dwords wide per clock per CU

@@ -64,9 +64,10 @@ extern "C" {
  * A NaN / Inf KKT residual at the outer loop head also stops the instance, keeping x, y as they
  * are.  That site is a deliberate deviation: the reference raises nothing there (`residual <=
  * tolresid` is just False) and would keep iterating on the NaN iterate.
- * RIPTRM_ERR_EIGEN: the HBM Exact_RepMat path's eigendecomposition (rocSOLVER dsyevd) reported
- * info != 0, or the trial-point eigenvalue was not finite, where scipy.linalg.eig / eigh raises
- * LinAlgError inside outer_step: same break and restore as RIPTRM_ERR_NONFINITE. */
+ * RIPTRM_ERR_EIGEN: the HBM Exact_RepMat path's eigendecomposition (hand-written riptrm_eig.h /
+ * riptrm_tri.h, or rocSOLVER dsyevd) reported info != 0, or the trial-point eigenvalue was not finite,
+ * where scipy.linalg.eig / eigh raises LinAlgError inside outer_step: same break and restore as
+ * RIPTRM_ERR_NONFINITE. */
 #define RIPTRM_ERR_NONE 0
 #define RIPTRM_ERR_NO_TCG_ITER 1       /* manifold.dim = 0: tCG cannot iterate */
 #define RIPTRM_ERR_BARRIER_TIMEOUT 2   /* persistent mode: a peer workgroup never arrived (2 s) */
@@ -393,8 +394,10 @@ int riptrm_si_solve(riptrm_ctx* ctx, const riptrm_options* opt, const double* x0
  * (RIPTRM_TRS_*).  mineig (may be NULL) = the smallest eigenvalue of A (RIPTRM.py:611).
  * dim <= RIPTRM_TRS_DIM_MAX: one workgroup per instance, A staged in LDS, asynchronous.
  * dim > RIPTRM_TRS_DIM_MAX: needs riptrm_trs_bind_workspace(order >= dim); up to `slots` subproblems
- * per pass on HBM-resident matrices (SciPy CG restated, rocSOLVER dsyevd_strided_batched, secular
- * Newton on one workgroup per subproblem); synchronises.  A non-converged eigensolve fails the call
+ * per pass on HBM-resident matrices (dim <= 199: the hand-written eigensolver and SciPy's CG restated in
+ * its eigen-coordinates; 200 <= dim <= 1024: the cooperative tridiagonalisation T = H^T A H and the
+ * subproblem in T's coordinates, riptrm_tri.h; above, or for a hard case, rocSOLVER
+ * dsyevd_strided_batched and SciPy's CG on A; the secular Newton per subproblem); synchronises.  A non-converged eigensolve fails the call
  * (RIPTRM_E_HIP naming the subproblem: scipy.linalg.eig raises there). */
 int riptrm_trs_gep(riptrm_ctx* ctx, int32_t dim, int32_t batch, const double* A, int64_t lda, int64_t a_stride,
                    const double* a, int64_t ldv, const double* Delta, double tolhardcase, double* x,
@@ -404,9 +407,10 @@ int riptrm_trs_gep(riptrm_ctx* ctx, int32_t dim, int32_t batch, const double* A,
  * :599-617 and TRSgep :218-299 at any size): `slots` subproblems of matrix order `order` (NonnegPCA:
  * order = n, the n x n frame matrix; riptrm_trs_gep: order = dim).  Bytes for riptrm_trs_bind_workspace,
  * caller-owned device memory (256-byte aligned).  Each subproblem of a pass takes one slot; with
- * fewer slots than subproblems the pass repeats, with bitwise the same results.  The
- * eigendecomposition is rocSOLVER's dsyevd_strided_batched, loaded at first use (dlopen of
- * librocsolver.so.0); rocSOLVER manages its own internal workspace.  In a NonnegPCA solve an
+ * fewer slots than subproblems the pass repeats, with bitwise the same results.  Orders <= 199
+ * take the hand-written eigensolver (riptrm_eig.h), 200..1024 the tridiagonal path (riptrm_tri.h, no
+ * eigenvectors); rocSOLVER's dsyevd_strided_batched serves larger orders and the tridiagonal path's
+ * hard cases, loaded at first use (dlopen of librocsolver.so.0; it manages its own workspace).  In a NonnegPCA solve an
  * instance that reaches the subproblem (or, with the second-order test, a trial point) parks;
  * riptrm_solve_advance serves every parked instance in batched passes after its lock-step chunk and
  * synchronises then; an eigensolve that does not converge stops that instance (RIPTRM_ERR_EIGEN).
@@ -420,7 +424,8 @@ int riptrm_trs_bind_workspace(riptrm_ctx* ctx, void* ws, int64_t bytes, int32_t 
 /* Eigendecomposition cache of the HBM path in a NonnegPCA solve with the second-order test
  * (RIPTRM.py:599-617 computes the trial point's eigenpairs; :686-692 keeps HwNewmatrix for the next
  * subproblem when the step was accepted without dual clipping).  One entry per instance (order >= n,
- * batch >= the bound batch): the trial point's eigenvectors / eigenvalues keyed by its (x, y).  A
+ * batch >= the bound batch): the trial point's eigenvectors / eigenvalues (orders <= 199) or its
+ * tridiagonal form and reflectors (200..1024) keyed by its (x, y).  A
  * subproblem whose (x, y) equals its instance's key bitwise builds the same matrix bits, so it runs
  * CG and the secular step on the cached eigenpairs without an eigensolve: results are bitwise those
  * of the uncached solve.  Caller-owned device memory, riptrm_trs_cache_bytes(order, batch) bytes,

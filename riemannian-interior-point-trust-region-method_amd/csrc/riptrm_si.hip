@@ -988,7 +988,9 @@ struct Eng {
     } else if constexpr (D >= 6) {
       // one wave from D = 6: chol_inv_reg's arithmetic one element per lane (par_chol is its
       // Cholesky step for step; par_trinv its triangular inverse), not two lanes' scratch-resident
-      // arrays; NaN factors for a non-PD point as chol_inv_reg's sqrt gives them
+      // arrays.  At a non-PD point every lane's factor is NaN (above the diagonal and past the
+      // block too), where chol_inv_reg's are NaN from the failing pivot on and 0 above the diagonal:
+      // the same arithmetic on PD points only; either way the non-finite guard stops the instance
       bool okr, okq;
       Frame F;
       F.Lr = par_chol(x.r, okr);

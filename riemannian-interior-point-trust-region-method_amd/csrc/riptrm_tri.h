@@ -73,6 +73,8 @@ struct TriArgs {
   void* grid;            // granules, tri_granules(m) per launch slot (zeroed before the launch)
   int64_t grid_bytes;
   int m, G;
+  long long* stamps;     // diagnostics (RIPTRM_TRI_STAMPS=1): workgroup 0 of matrix 0 accumulates clock64
+                         // cycles in [0] the gather, [1] wave 0's section + barrier, [2] the update + publish
 };
 
 // the reflector of the column c[i+1 .. m) (dlarfg: H (alpha, x) = (beta, 0), v(i+1) = 1) into vo, by
@@ -104,6 +106,11 @@ __device__ __forceinline__ void make_reflector(const lds_t* c, int i, int m, lds
   }
 }
 
+// a workgroup barrier that waits for this wave's LDS accesses only: the granule / reflector stores in
+// flight need not complete here (__syncthreads() drains them with vmcnt(0): each write-through store is
+// a round trip to memory, ~1.5 us of the step at m = 999 by the phase stamps)
+__device__ __forceinline__ void bar_lds() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
 // dsytd2 (lower) of the m x m matrix of slot k0 + blockIdx.y on gridDim.x = G workgroups: d, e, the
 // reflectors and tau into the slot.  Row l lives on workgroup l mod G, wave (l / G) mod 8, register
 // row (l / G) / 8, lane j mod 64 holding columns j = lane + 64 q.
@@ -116,8 +123,10 @@ __global__ void __launch_bounds__(TT) k_tridiag_dist(TriArgs a) {
   // (a wave that finishes its rows early starts the next gather while others still read W, Vbuf: the
   // gather writes only GP and C, which nobody reads after the step's barrier)
   __shared__ double scal[2];
+  __shared__ int failflag;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int g = blockIdx.x, ks = blockIdx.y, k = a.k0 + ks;
+  if (tid == 0) failflag = 0;
   const int m = a.m, G = a.G;
   const double* A = a.A0 + (int64_t)k * a.a_stride;
   double* dv = a.d0 + (int64_t)k * a.de_stride;
@@ -197,6 +206,8 @@ __global__ void __launch_bounds__(TT) k_tridiag_dist(TriArgs a) {
 
   constexpr int NG = (2 * 64 * EL + 256 + TT - 1) / TT;   // granules polled per thread (upper bound)
   bool failed = false;
+  long long* stp = (a.stamps && g == 0 && k == 0 && tid == 0) ? a.stamps : nullptr;
+  long long acc0 = 0, acc1 = 0, acc2 = 0, tq = stp ? clock64() : 0, sa = 0, sb = 0, sc = 0, sd = 0;
   for (int i = 0; i <= m - 2; ++i) {
     const unsigned pass = (unsigned)(i + 1);
     const int64_t pb = gbase + (int64_t)(pass & 1) * par;
@@ -242,9 +253,16 @@ __global__ void __launch_bounds__(TT) k_tridiag_dist(TriArgs a) {
         __builtin_amdgcn_s_sleep(1);
       }
     }
-    if (__syncthreads_or(failed)) {
+    if (failed) failflag = 1;
+    bar_lds();
+    if (failflag) {   // uniform after the barrier (only ever set, then every wave returns)
       if (tid == 0) a.infos[k] = 3;
       return;
+    }
+    if (stp) {
+      const long long t1 = clock64();
+      acc0 += t1 - tq;
+      tq = t1;
     }
     // this workgroup has read pass i + 1: the parity of pass i + 2 (= pass i's) may be reused
     const int64_t pn = gbase + (int64_t)((pass + 1) & 1) * par;
@@ -253,31 +271,80 @@ __global__ void __launch_bounds__(TT) k_tridiag_dist(TriArgs a) {
     lds_t* Vc = (lds_t*)Vbuf[i & 1];
     lds_t* Vn = (lds_t*)Vbuf[(i + 1) & 1];
     if (w == 0) {
-      // w = p + a2 v, a2 = -tau (p . v) / 2; the column i + 1 of the updated matrix; its reflector
+      const long long q0s = stp ? clock64() : 0;
+      // w = p + a2 v, a2 = -tau (p . v) / 2; the column i + 1 of the updated matrix; its reflector.
+      // Every operand is loaded in one batch first (loads inside the selects were issued one
+      // latency at a time: 3 us of the 7.6 us step at m = 999), the column stays in registers.
+      const int i2 = i + 2 < m ? i + 2 : i + 1;
+      const double gp1 = GP[i + 1], vi1 = Vc[i + 1], cr1 = C[i + 1];
+      const double gp2 = GP[i2], vc2 = Vc[i2], cr2 = C[i2];
+      // (chunks of four columns: every chunk's loads in flight together, few registers live beside the rows)
       double s = 0.0;
 #pragma unroll
-      for (int q = 0; q < EL; ++q) {
-        const int j = lane + 64 * q;
-        s += (j > i && j < m) ? GP[j] * Vc[j] : 0.0;
+      for (int q0 = 0; q0 < EL; q0 += 4) {
+        double gp[4], vc[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          gp[u] = GP[lane + 64 * (q0 + u)];
+          vc[u] = Vc[lane + 64 * (q0 + u)];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int j = lane + 64 * (q0 + u);
+          s += (j > i && j < m) ? gp[u] * vc[u] : 0.0;
+        }
+        __builtin_amdgcn_sched_barrier(0);
       }
       s = riptrm_wave::wave_sum(s);
       const double a2 = -0.5 * tau_c * s;
-      const double vi1 = Vc[i + 1], wi1 = GP[i + 1] + a2 * vi1;
+      const long long q1s = stp ? clock64() : 0;
+      const double wi1 = gp1 + a2 * vi1;
+      double sn = 0.0;   // the reflector's sum over c_j^2, j >= i + 3
 #pragma unroll
-      for (int q = 0; q < EL; ++q) {
-        const int j = lane + 64 * q;
-        const double wj = (j > i && j < m) ? GP[j] + a2 * Vc[j] : 0.0;
-        const double cj = C[j] - (Vc[j] * wi1 + wj * vi1);   // the update of row j at column i + 1
-        W[j] = wj;
-        if (j > i + 1 && j < m) C[j] = cj;
+      for (int q0 = 0; q0 < EL; q0 += 4) {
+        double gp[4], vc[4], cr[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          gp[u] = GP[lane + 64 * (q0 + u)];
+          vc[u] = Vc[lane + 64 * (q0 + u)];
+          cr[u] = C[lane + 64 * (q0 + u)];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int j = lane + 64 * (q0 + u);
+          const double wj = (j > i && j < m) ? gp[u] + a2 * vc[u] : 0.0;
+          W[j] = wj;
+          const double cj = (j > i + 1 && j < m) ? cr[u] - (vc[u] * wi1 + wj * vi1) : 0.0;   // row j's update at column i + 1
+          C[j] = cj;
+          sn += j >= i + 3 ? cj * cj : 0.0;
+        }
+        __builtin_amdgcn_sched_barrier(0);   // keep the next chunk's loads behind this one (register pressure)
       }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the wave's lanes exchange through LDS
-      const double di1 = C[i + 1] - (vi1 * wi1 + wi1 * vi1);
+      const double di1 = cr1 - (vi1 * wi1 + wi1 * vi1);
+      const long long q2s = stp ? clock64() : 0;
       if (writer && lane == 0) dv[i + 1] = di1;
       if (more) {
-        double tau, beta, scl;
-        make_reflector<EL>((const lds_t*)C, i + 1, m, Vn, lane, tau, beta, scl);
+        // dlarfg on c[i+2 .. m): alpha = c[i+2] (its update formula, every lane), the sum over j >= i + 3
+        const double alpha = cr2 - (vc2 * wi1 + (gp2 + a2 * vc2) * vi1);
+        sn = riptrm_wave::wave_sum(sn);
+        double tau = 0.0, beta = alpha, scl = 0.0;
+        if (sn != 0.0) {
+          beta = -copysign(sqrt(alpha * alpha + sn), alpha);
+          tau = (beta - alpha) / beta;
+          scl = 1.0 / (alpha - beta);
+        }
+#pragma unroll
+        for (int q = 0; q < EL; ++q) {   // (each lane reads back its own c_j)
+          const int j = lane + 64 * q;
+          Vn[j] = (j <= i + 1 || j >= m) ? 0.0 : (j == i + 2 ? 1.0 : C[j] * scl);
+        }
         if (lane == 0) scal[(i + 1) & 1] = tau;
+        if (stp) {
+          const long long q3s = clock64();
+          sa += q1s - q0s;
+          sb += q2s - q1s;
+          sc += q3s - q2s;
+        }
         if (writer) {
           if (lane == 0) {
             ev[i + 1] = beta;
@@ -292,7 +359,12 @@ __global__ void __launch_bounds__(TT) k_tridiag_dist(TriArgs a) {
         }
       }
     }
-    __syncthreads();
+    bar_lds();
+    if (stp) {
+      const long long t1 = clock64();
+      acc1 += t1 - tq;
+      tq = t1;
+    }
     if (!more) break;
     const double tau_n = scal[(i + 1) & 1];
     // rank-two update of own rows l >= i + 2 (row i + 1 is finished: its diagonal is d_{i+1}), fused
@@ -323,6 +395,19 @@ __global__ void __launch_bounds__(TT) k_tridiag_dist(TriArgs a) {
       }
     }
     tau_c = tau_n;
+    if (stp) {
+      const long long t1 = clock64();
+      acc2 += t1 - tq;
+      tq = t1;
+    }
+  }
+  if (stp) {
+    stp[0] = acc0;
+    stp[1] = acc1;
+    stp[2] = acc2;
+    stp[4] = sa;
+    stp[5] = sb;
+    stp[6] = sc;
   }
 }
 
@@ -362,11 +447,13 @@ __global__ void __launch_bounds__(256) k_tri_split(double* d0, double* e0, int64
 
 // v <- H^T v (backward = 0: H_{m-2} ... H_0 v) or H v (backward = 1), H the reflectors of slot k0 +
 // blockIdx.y at r_off (riptrm_eig layout), from slot offset voff to ooff; one wave, lane l holding
-// elements l + 64 q (the k_refl_apply arithmetic); the next reflector's loads are issued before the
-// current one's reduction
+// elements l + 64 q (the k_refl_apply arithmetic).  The reflectors stream from HBM / L2 through a ring
+// of RD register sets: reflector t + RD is requested while t is applied (one reflection is ~0.2 us
+// of arithmetic against ~1-2 us of load latency).
 template <int EL>
 __global__ void __launch_bounds__(64) k_refl_big(double* base, int64_t sd, int k0, int m, int64_t r_off, int64_t voff,
                                                  int64_t ooff, int backward) {
+  constexpr int RD = EL <= 8 ? 8 : 4;   // ring depth (EL = 16: 4 x 16 doubles in flight per lane)
   double* sb = base + (int64_t)(k0 + blockIdx.y) * sd;
   const double* R = sb + r_off;
   const int lane = threadIdx.x;
@@ -376,34 +463,46 @@ __global__ void __launch_bounds__(64) k_refl_big(double* base, int64_t sd, int k
     const int j = lane + 64 * q;
     v[q] = j < m ? sb[voff + j] : 0.0;
   }
-  const int nt = riptrm_eig::refl_tau(m);
-  double un[EL], taun = 0.0;
-  auto fetch = [&](int t) {
+  const int nt = riptrm_eig::refl_tau(m), nr = m - 1;
+  double ring[RD][EL], rtau[RD];
+  auto fetch = [&](int t, double (&u)[EL], double& tau) {
     const int i = backward ? m - 2 - t : t;
-    taun = R[nt + i];
+    const bool live = t < nr;
+    tau = R[live ? nt + i : nt];
     const int c = riptrm_eig::refl_col(m, i) - i - 1;
 #pragma unroll
     for (int q = 0; q < EL; ++q) {
       const int j = lane + 64 * q;
-      const bool ok = j > i && j < m;
-      un[q] = R[ok ? c + j : nt];
-      un[q] = ok ? un[q] : 0.0;
+      const bool ok = live && j > i && j < m;
+      u[q] = R[ok ? c + j : nt];
     }
   };
-  if (m >= 2) fetch(0);
-  for (int t = 0; t < m - 1; ++t) {
-    double u[EL];
 #pragma unroll
-    for (int q = 0; q < EL; ++q) u[q] = un[q];
-    const double tau = taun;
-    if (t + 1 < m - 1) fetch(t + 1);
-    if (tau == 0.0) continue;   // uniform
-    double s = 0.0;
+  for (int r = 0; r < RD; ++r) fetch(r, ring[r], rtau[r]);
+  for (int t0 = 0; t0 < nr; t0 += RD) {
 #pragma unroll
-    for (int q = 0; q < EL; ++q) s += u[q] * v[q];
-    const double f = tau * riptrm_wave::wave_sum(s);
+    for (int r = 0; r < RD; ++r) {
+      const int t = t0 + r;
+      if (t < nr) {   // uniform
+        const int i = backward ? m - 2 - t : t;
+        double u[EL];
 #pragma unroll
-    for (int q = 0; q < EL; ++q) v[q] = v[q] - f * u[q];
+        for (int q = 0; q < EL; ++q) {
+          const int j = lane + 64 * q;
+          u[q] = (j > i && j < m) ? ring[r][q] : 0.0;
+        }
+        const double tau = rtau[r];
+        fetch(t + RD, ring[r], rtau[r]);   // the slot is free: request reflector t + RD
+        if (tau != 0.0) {   // uniform
+          double s = 0.0;
+#pragma unroll
+          for (int q = 0; q < EL; ++q) s += u[q] * v[q];
+          const double f = tau * riptrm_wave::wave_sum(s);
+#pragma unroll
+          for (int q = 0; q < EL; ++q) v[q] = v[q] - f * u[q];
+        }
+      }
+    }
   }
 #pragma unroll
   for (int q = 0; q < EL; ++q) {
@@ -412,10 +511,55 @@ __global__ void __launch_bounds__(64) k_refl_big(double* base, int64_t sd, int k
   }
 }
 
+// The number of eigenvalues of T below x by the sign changes of its leading principal minors
+// p_j = (d_j - x) p_{j-1} - e_{j-1}^2 p_{j-2} (p_{-1} = 1; e2 = e^2): two dependent operations per step
+// where riptrm_eig.h's LDL^T count (dlaneg) waits on a reciprocal (one thread's chain here, not the
+// issue-bound many-lane counts there: ~20 vs ~110 cycles per step).  Exact powers of two rescale
+// (p_j, p_{j-1}) every four steps; a zero minor takes the sign opposite to the previous one (a tiny
+// negative pivot: dlaneg's pivmin convention).
+__device__ __forceinline__ int sturm_count_df(const lds_t* d, const lds_t* e2, int m, double x) {
+  double pm = 1.0, p = d[0] - x;
+  if (p == 0.0) p = -DBL_MIN;
+  int c = p < 0.0;
+  int j = 1;
+  for (; j + 3 < m; j += 4) {
+    const double d0 = d[j], d1 = d[j + 1], d2 = d[j + 2], d3 = d[j + 3];
+    const double f0 = e2[j - 1], f1 = e2[j], f2 = e2[j + 1], f3 = e2[j + 2];
+    double pn = (d0 - x) * p - f0 * pm;
+    if (pn == 0.0) pn = -copysign(DBL_MIN, p);
+    c += (pn < 0.0) != (p < 0.0);
+    pm = p; p = pn;
+    pn = (d1 - x) * p - f1 * pm;
+    if (pn == 0.0) pn = -copysign(DBL_MIN, p);
+    c += (pn < 0.0) != (p < 0.0);
+    pm = p; p = pn;
+    pn = (d2 - x) * p - f2 * pm;
+    if (pn == 0.0) pn = -copysign(DBL_MIN, p);
+    c += (pn < 0.0) != (p < 0.0);
+    pm = p; p = pn;
+    pn = (d3 - x) * p - f3 * pm;
+    if (pn == 0.0) pn = -copysign(DBL_MIN, p);
+    c += (pn < 0.0) != (p < 0.0);
+    pm = p; p = pn;
+    int ex;
+    (void)frexp(p, &ex);
+    p = ldexp(p, -ex);
+    pm = ldexp(pm, -ex);
+  }
+  for (; j < m; ++j) {
+    double pn = (d[j] - x) * p - e2[j - 1] * pm;
+    if (pn == 0.0) pn = -copysign(DBL_MIN, p);
+    c += (pn < 0.0) != (p < 0.0);
+    pm = p;
+    p = pn;
+  }
+  return c;
+}
+
 // the smallest (hi = false) or largest eigenvalue of T by one wave's multisection (64 points per
 // step; riptrm_eig.h phase 2's tolerance max(2 eps |lambda|, eps ||T||))
-__device__ __forceinline__ double extreme_eig(const lds_t* d, const lds_t* e, int m, bool hi_end, double glo, double ghi,
-                                              double fudge, double tnorm, double pivmin, int lane) {
+__device__ __forceinline__ double extreme_eig(const lds_t* d, const lds_t* e2, int m, bool hi_end, double glo, double ghi,
+                                              double fudge, double tnorm, int lane) {
   const double eps = DBL_EPSILON;
   const int ei = hi_end ? m - 1 : 0;
   double lo = glo - fudge, hi = ghi + fudge;
@@ -424,7 +568,7 @@ __device__ __forceinline__ double extreme_eig(const lds_t* d, const lds_t* e, in
     if (hi - lo <= tol) break;   // uniform
     const double step = (hi - lo) / 65.0;
     const double x = lo + step * (lane + 1);
-    const int c = (x > lo && x < hi) ? riptrm_eig::sturm_count(d, e, m, x, pivmin) : (x <= lo ? 0 : m);
+    const int c = (x > lo && x < hi) ? sturm_count_df(d, e2, m, x) : (x <= lo ? 0 : m);
     // the new interval: the largest point with count <= ei, the smallest with count > ei
     const double nlo = riptrm_wave::wave_max(c > ei ? -INFINITY : x);
     const double nhi = riptrm_wave::wave_min(c > ei ? x : INFINITY);
@@ -436,67 +580,164 @@ __device__ __forceinline__ double extreme_eig(const lds_t* d, const lds_t* e, in
   return 0.5 * (lo + hi);
 }
 
-// y = (T + lam I)^-1 b for T + lam I positive definite (LDL^T without pivoting), L and 1/D kept in lf /
-// rd when factor (the solve with the same factor reuses them); one thread
-__device__ __forceinline__ void ldl_solve(const lds_t* d, const lds_t* e, int m, double lam, const lds_t* b, lds_t* y,
-                                          lds_t* lf, lds_t* rd, bool factor) {
-  if (factor) {
-    double D = d[0] + lam;
-    for (int j = 0; j + 1 < m; ++j) {
-      const double r = 1.0 / D;
-      rd[j] = r;
-      const double L = e[j] * r;
-      lf[j] = L;
-      D = (d[j + 1] + lam) - L * e[j];
-    }
-    rd[m - 1] = 1.0 / D;
+// One Newton step's solves of the secular equation, by one thread: (T + lam I) = L D L^T (no pivoting:
+// positive definite for lam > -lam_min), y = (T + lam I)^-1 b and, with second, t = (T + lam I)^-1 y;
+// returns s2 = y . y (and s3 = y . t).  The pivots come from the leading minors P_j = (d_j + lam)
+// P_{j-1} - e_{j-1}^2 P_{j-2} (D_j = P_j / P_{j-1}, 1 / D_j = P_{j-1} / P_j, L_j = e_j / D_j), so the dependent
+// chain is two operations per step and each reciprocal is off it (exact powers of two rescale the pair
+// every four steps: the ratios are unchanged).  Then the forward and backward sweeps (one FMA chain
+// each), their next four entries' loads issued ahead.  lf, rd: L and 1/D.
+__device__ __forceinline__ void ldl_newton(const lds_t* d, const lds_t* e, const lds_t* e2, int m, double lam,
+                                           const lds_t* b, lds_t* y, lds_t* t2, lds_t* lf, lds_t* rd, bool second,
+                                           double& s2, double& s3) {
+  double Pm = 1.0, P = d[0] + lam;
+  int j = 0;
+  for (; j + 4 < m; j += 4) {
+    const double d1 = d[j + 1], d2 = d[j + 2], d3 = d[j + 3], d4 = d[j + 4];
+    const double f0 = e2[j], f1 = e2[j + 1], f2 = e2[j + 2], f3 = e2[j + 3];
+    const double e0 = e[j], e1 = e[j + 1], ee2 = e[j + 2], e3 = e[j + 3];
+    const double P0 = P;
+    const double P1 = (d1 + lam) * P0 - f0 * Pm;
+    const double P2 = (d2 + lam) * P1 - f1 * P0;
+    const double P3 = (d3 + lam) * P2 - f2 * P1;
+    const double P4 = (d4 + lam) * P3 - f3 * P2;
+    const double r0 = Pm * riptrm_eig::rcp_nr(P0), r1 = P0 * riptrm_eig::rcp_nr(P1);
+    const double r2 = P1 * riptrm_eig::rcp_nr(P2), r3 = P2 * riptrm_eig::rcp_nr(P3);
+    rd[j] = r0; lf[j] = e0 * r0;
+    rd[j + 1] = r1; lf[j + 1] = e1 * r1;
+    rd[j + 2] = r2; lf[j + 2] = ee2 * r2;
+    rd[j + 3] = r3; lf[j + 3] = e3 * r3;
+    int ex;
+    (void)frexp(P4, &ex);
+    P = ldexp(P4, -ex);
+    Pm = ldexp(P3, -ex);
   }
+  for (; j + 1 < m; ++j) {
+    const double Pn = (d[j + 1] + lam) * P - e2[j] * Pm;
+    const double r = Pm * riptrm_eig::rcp_nr(P);
+    rd[j] = r;
+    lf[j] = e[j] * r;
+    Pm = P;
+    P = Pn;
+  }
+  rd[m - 1] = Pm * riptrm_eig::rcp_nr(P);
+  // forward: z_0 = b_0, z_{j+1} = b_{j+1} - L_j z_j (into y)
   double z = b[0];
   y[0] = z;
-  for (int j = 1; j < m; ++j) {
-    z = b[j] - lf[j - 1] * z;
-    y[j] = z;
+  j = 0;
+  for (; j + 4 < m; j += 4) {
+    const double l0 = lf[j], l1 = lf[j + 1], l2 = lf[j + 2], l3 = lf[j + 3];
+    const double b1 = b[j + 1], b2 = b[j + 2], b3 = b[j + 3], b4 = b[j + 4];
+    z = b1 - l0 * z; y[j + 1] = z;
+    z = b2 - l1 * z; y[j + 2] = z;
+    z = b3 - l2 * z; y[j + 3] = z;
+    z = b4 - l3 * z; y[j + 4] = z;
   }
+  for (; j + 1 < m; ++j) {
+    z = b[j + 1] - lf[j] * z;
+    y[j + 1] = z;
+  }
+  // backward: y_{m-1} = z_{m-1} / D_{m-1}, y_j = z_j / D_j - L_j y_{j+1}; s2
   double x = y[m - 1] * rd[m - 1];
   y[m - 1] = x;
-  for (int j = m - 2; j >= 0; --j) {
+  double a2 = x * x;
+  j = m - 2;
+  for (; j - 3 >= 0; j -= 4) {
+    const double z0 = y[j], z1 = y[j - 1], z2 = y[j - 2], z3 = y[j - 3];
+    const double r0 = rd[j], r1 = rd[j - 1], r2 = rd[j - 2], r3 = rd[j - 3];
+    const double l0 = lf[j], l1 = lf[j - 1], l2 = lf[j - 2], l3 = lf[j - 3];
+    x = z0 * r0 - l0 * x; y[j] = x; a2 += x * x;
+    x = z1 * r1 - l1 * x; y[j - 1] = x; a2 += x * x;
+    x = z2 * r2 - l2 * x; y[j - 2] = x; a2 += x * x;
+    x = z3 * r3 - l3 * x; y[j - 3] = x; a2 += x * x;
+  }
+  for (; j >= 0; --j) {
     x = y[j] * rd[j] - lf[j] * x;
     y[j] = x;
+    a2 += x * x;
   }
+  s2 = a2;
+  s3 = 0.0;
+  if (!second) return;
+  // t = (T + lam I)^-1 y with the same factor; s3 = y . t
+  z = y[0];
+  t2[0] = z;
+  j = 0;
+  for (; j + 4 < m; j += 4) {
+    const double l0 = lf[j], l1 = lf[j + 1], l2 = lf[j + 2], l3 = lf[j + 3];
+    const double y1 = y[j + 1], y2 = y[j + 2], y3 = y[j + 3], y4 = y[j + 4];
+    z = y1 - l0 * z; t2[j + 1] = z;
+    z = y2 - l1 * z; t2[j + 2] = z;
+    z = y3 - l2 * z; t2[j + 3] = z;
+    z = y4 - l3 * z; t2[j + 4] = z;
+  }
+  for (; j + 1 < m; ++j) {
+    z = y[j + 1] - lf[j] * z;
+    t2[j + 1] = z;
+  }
+  x = t2[m - 1] * rd[m - 1];
+  double a3 = y[m - 1] * x;
+  j = m - 2;
+  for (; j - 3 >= 0; j -= 4) {
+    const double z0 = t2[j], z1 = t2[j - 1], z2 = t2[j - 2], z3 = t2[j - 3];
+    const double r0 = rd[j], r1 = rd[j - 1], r2 = rd[j - 2], r3 = rd[j - 3];
+    const double l0 = lf[j], l1 = lf[j - 1], l2 = lf[j - 2], l3 = lf[j - 3];
+    const double y0 = y[j], y1 = y[j - 1], y2 = y[j - 2], y3 = y[j - 3];
+    x = z0 * r0 - l0 * x; a3 += y0 * x;
+    x = z1 * r1 - l1 * x; a3 += y1 * x;
+    x = z2 * r2 - l2 * x; a3 += y2 * x;
+    x = z3 * r3 - l3 * x; a3 += y3 * x;
+  }
+  for (; j >= 0; --j) {
+    x = t2[j] * rd[j] - lf[j] * x;
+    a3 += y[j] * x;
+  }
+  s3 = a3;
 }
 
 // scalar slots this header uses (riptrm_trs_big.hip Sc)
 struct TriSc {
-  int cg_ok, p1obj, kind, lam1, mineig, interior, delta, an, atol, it, done, fallback;
+  int cg_ok, p1obj, kind, lam1, mineig, interior, delta, an, atol, it, done, fallback, newton;
 };
 
-// After k_tridiag_dist (and k_refl_big: b = H^T a at boff): mode 0 the subproblem, mode 1 the smallest
-// eigenvalue only.  One workgroup of 256 threads per slot: wave 0 the secular Newton (lane 0) and the
-// hard-case test, wave 1 SciPy's CG on T y = -b, waves 2-3 the extreme eigenvalues first.  Writes the
-// boundary / interior candidate in T coordinates at peoff (the host applies H), lam_min at evoff[0].
+// After k_tridiag_dist (and the reflector application: b = H^T a at boff): mode 0 the subproblem, mode 1
+// the smallest eigenvalue only.  One workgroup of 256 threads per slot: waves 0 / 1 the extreme
+// eigenvalues; then, at once, wave 0 the secular Newton (lane 0), wave 1 SciPy's CG on T y = -b and
+// wave 2 the hard-case test (lam_min's multiplicity and the component of b on its twisted eigenvector;
+// a hard case discards the other two and sets the fallback flag).  Writes the boundary / interior
+// candidate in T coordinates at peoff (the host applies H), lam_min at evoff[0].
+constexpr int TRI_SOLVE_ARRAYS = 10;   // LDS vectors of 64 EL doubles
 template <int EL>
 __global__ void __launch_bounds__(256) k_tri_solve(double* base, int64_t sd, int32_t* infos, int m, int64_t d_off,
                                                    int64_t e_off, int64_t boff, int64_t aoff_vec, int64_t peoff,
                                                    int64_t cgxoff, int64_t evoff, int64_t scoff, TriSc S,
                                                    const double* Dg, int64_t dstride, const int32_t* ids, double tolhc,
-                                                   int mode) {
+                                                   int mode, long long* stamps) {
+  // stamps (diagnostics, RIPTRM_TRI_STAMPS=1; slot 0): clock64 at [0] start, [1] extreme eigenvalues,
+  // [2] hard-case test done (wave 2), [3] the Newton done (wave 0), [4] the CG done (wave 1), [5] end;
+  // [6] Newton steps, [7] CG iterations
+  long long* stp = (stamps && blockIdx.y == 0) ? stamps : nullptr;
+  if (stp && threadIdx.x == 0) stp[0] = clock64();
   extern __shared__ double smem[];
-  lds_t* d = (lds_t*)smem;           // [m] each
-  lds_t* e = d + 64 * EL;
-  lds_t* b = e + 64 * EL;
-  lds_t* y = b + 64 * EL;
-  lds_t* t2 = y + 64 * EL;
-  lds_t* lf = t2 + 64 * EL;
-  lds_t* rd = lf + 64 * EL;
-  lds_t* z = rd + 64 * EL;
+  constexpr int V = 64 * EL;
+  lds_t* d = (lds_t*)smem;
+  lds_t* e = d + V;
+  lds_t* e2 = e + V;   // e^2 (the Sturm counts and the minors)
+  lds_t* b = e2 + V;
+  lds_t* y = b + V;    // Newton: y, then the boundary candidate
+  lds_t* t2 = y + V;
+  lds_t* lf = t2 + V;
+  lds_t* rd = lf + V;
+  lds_t* z = rd + V;   // the twisted eigenvector
+  lds_t* cx = z + V;   // the CG's iterate
   __shared__ double red[8];
-  __shared__ double xs[8];   // lam_min, lam_max, multiplicity, xobj, lam1, CG ok, p1obj
+  __shared__ double xs[10];   // lam_min, lam_max, multiplicity, xobj, lam1, CG ok, p1obj, Newton steps, ghard
   const int k = blockIdx.y;
   double* sb = base + (int64_t)k * sd;
   double* sc = sb + scoff;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const double eps = DBL_EPSILON;
-  for (int j = tid; j < 64 * EL; j += 256) {
+  for (int j = tid; j < V; j += 256) {
     d[j] = j < m ? sb[d_off + j] : 0.0;
     e[j] = j < m - 1 ? sb[e_off + j] : 0.0;
     b[j] = (mode == 0 && j < m) ? sb[boff + j] : 0.0;
@@ -528,8 +769,12 @@ __global__ void __launch_bounds__(256) k_tri_solve(double* base, int64_t sd, int
   __syncthreads();
   tn0 = fmax(fmax(red[0], red[1]), fmax(red[2], red[3]));
   __syncthreads();
-  for (int j = tid; j < m - 1; j += 256)
-    if (fabs(e[j]) <= 4.0 * eps * tn0) e[j] = 0.0;
+  for (int j = tid; j < V; j += 256) {
+    double ej = e[j];
+    if (j < m - 1 && fabs(ej) <= 4.0 * eps * tn0) ej = 0.0;
+    e[j] = ej;
+    e2[j] = ej * ej;
+  }
   __syncthreads();
   double glo = INFINITY, ghi = -INFINITY, tnorm = 0.0, emax2 = 0.0;
   for (int j = tid; j < m; j += 256) {
@@ -559,11 +804,12 @@ __global__ void __launch_bounds__(256) k_tri_solve(double* base, int64_t sd, int
   const double fudge = 2.0 * eps * tnorm + 2.0 * pivmin;
   // lam_min (wave 0) and lam_max (wave 1)
   if (w < 2) {
-    const double lx = extreme_eig(d, e, m, w == 1, glo, ghi, fudge, tnorm, pivmin, lane);
+    const double lx = extreme_eig(d, e2, m, w == 1, glo, ghi, fudge, tnorm, lane);
     if (lane == 0) xs[w] = lx;
   }
   __syncthreads();
   const double lmin = xs[0], lmaxv = xs[1];
+  if (stp && tid == 0) stp[1] = clock64();
   __syncthreads();
   if (mode == 1) {
     if (tid == 0) {
@@ -592,45 +838,15 @@ __global__ void __launch_bounds__(256) k_tri_solve(double* base, int64_t sd, int
   an = sqrt((red[0] + red[1]) + (red[2] + red[3]));
   const double gn = sqrt((red[4] + red[5]) + (red[6] + red[7]));
   __syncthreads();
-  // hard-case test (k_secular): the component of b on the eigenspace of lam_min (eigenvalues within
-  // 1e-12 max(1, max |lambda|)); a multiple lam_min or a hard case goes to the eigendecomposition path
-  const double hard_tol = 1e-12 * fmax(1.0, fmax(fabs(lmin), fabs(lmaxv)));
-  if (tid == 0) {
-    const int mult = riptrm_eig::sturm_count(d, e, m, lmin + hard_tol, pivmin);
-    double evl[1] = {lmin};
-    riptrm_eig::twisted_vector(z, d, e, evl, m, 0, 16.0 * eps * tnorm, pivmin);
-    xs[2] = (double)mult;
-  }
-  __syncthreads();
-  double zb = 0.0;
-  for (int j = tid; j < m; j += 256) zb += z[j] * b[j];
-  zb = riptrm_wave::wave_sum(zb);
-  if (lane == 0) red[w] = zb;
-  __syncthreads();
-  const double ghard = fabs((red[0] + red[1]) + (red[2] + red[3]));
-  const bool fb = xs[2] > 1.5 || ghard <= tolhc * gn;
-  __syncthreads();
-  if (fb) {   // uniform
-    if (tid == 0) {
-      sc[S.fallback] = 1.0;
-      sb[evoff] = lmin;
-      infos[k] = 0;
-    }
-    return;
-  }
   if (w == 0) {
     // the secular Newton of k_secular: ||(T + l1 I)^-1 b|| = Delta from l1 = -lam_min + ||b|| / Delta
     if (lane == 0) {
       const double lo = -lmin;
       double l1 = lo + gn / Delta;
-      for (int itn = 0; itn < 100; ++itn) {
-        ldl_solve(d, e, m, l1, b, y, lf, rd, true);
-        ldl_solve(d, e, m, l1, y, t2, lf, rd, false);
-        double s2 = 0.0, s3 = 0.0;
-        for (int j = 0; j < m; ++j) {
-          s2 += y[j] * y[j];
-          s3 += y[j] * t2[j];
-        }
+      int itn = 0;
+      for (; itn < 100; ++itn) {
+        double s2, s3;
+        ldl_newton(d, e, e2, m, l1, b, y, t2, lf, rd, true, s2, s3);
         const double xn = sqrt(s2);
         const double f = 1.0 / xn - 1.0 / Delta;
         const double fp = s3 / (xn * xn * xn);
@@ -642,9 +858,8 @@ __global__ void __launch_bounds__(256) k_tri_solve(double* base, int64_t sd, int
         }
         l1 = nl;
       }
-      ldl_solve(d, e, m, l1, b, y, lf, rd, true);
-      double s2 = 0.0;
-      for (int j = 0; j < m; ++j) s2 += y[j] * y[j];
+      double s2, s3;
+      ldl_newton(d, e, e2, m, l1, b, y, t2, lf, rd, false, s2, s3);
       const double scl = Delta / sqrt(s2);
       double o0 = 0.0, o1 = 0.0;
       for (int j = 0; j < m; ++j) {
@@ -658,17 +873,26 @@ __global__ void __launch_bounds__(256) k_tri_solve(double* base, int64_t sd, int
       }
       xs[3] = 0.5 * o0 + o1;
       xs[4] = l1;
+      xs[7] = (double)itn;
+      if (stp) {
+        stp[3] = clock64();
+        stp[6] = itn;
+      }
     }
   } else if (w == 1) {
-    // SciPy's CG on T y = -b (k_cg_diag's loop; lane l owns elements l EL .. l EL + EL - 1)
-    double x[EL], r[EL], p[EL], tq[EL];
+    // SciPy's CG on T y = -b (k_cg_diag's loop; lane l owns elements l EL .. l EL + EL - 1, its diagonal
+    // and off-diagonal entries held in registers)
+    double x[EL], r[EL], p[EL], tq[EL], dg[EL], er[EL];
     const int j0 = lane * EL;
 #pragma unroll
     for (int u = 0; u < EL; ++u) {
       const int j = j0 + u;
       r[u] = j < m ? -b[j] : 0.0;
       x[u] = p[u] = 0.0;
+      dg[u] = j < m ? d[j] : 0.0;
+      er[u] = j < m - 1 ? e[j] : 0.0;
     }
+    const double el0 = j0 > 0 && j0 < m ? e[j0 - 1] : 0.0;   // the coupling to the previous lane's last element
     const double atol = 1e-5 * an;
     double done = an == 0.0 ? 2.0 : 0.0, it = 0.0, rho_prev = 1.0;
     auto tmul = [&](const double (&pv)[EL], double (&out)[EL]) {
@@ -676,11 +900,10 @@ __global__ void __launch_bounds__(256) k_tri_solve(double* base, int64_t sd, int
       const double right = __shfl(pv[0], lane < 63 ? lane + 1 : 63);     // element j0 + EL
 #pragma unroll
       for (int u = 0; u < EL; ++u) {
-        const int j = j0 + u;
         const double pl = u > 0 ? pv[u - 1] : (lane > 0 ? left : 0.0);
         const double pr = u < EL - 1 ? pv[u + 1] : (lane < 63 ? right : 0.0);
-        const double el = j > 0 && j < m ? e[j - 1] : 0.0, er = j < m - 1 ? e[j] : 0.0;
-        out[u] = j < m ? (el * pl + d[j] * pv[u]) + er * pr : 0.0;
+        const double el = u > 0 ? er[u - 1] : el0;
+        out[u] = (el * pl + dg[u] * pv[u]) + er[u] * pr;
       }
     };
     while (done == 0.0) {   // uniform
@@ -726,7 +949,7 @@ __global__ void __launch_bounds__(256) k_tri_solve(double* base, int64_t sd, int
         v2 += x[u] * tq[u];
         v3 += b[j] * x[u];
         sb[cgxoff + j] = x[u];
-        z[j] = x[u];   // (the twisted vector is no longer needed)
+        cx[j] = x[u];
       }
     }
     v0 = riptrm_wave::wave_sum(v0);
@@ -734,31 +957,111 @@ __global__ void __launch_bounds__(256) k_tri_solve(double* base, int64_t sd, int
     v2 = riptrm_wave::wave_sum(v2);
     v3 = riptrm_wave::wave_sum(v3);
     if (lane == 0) {
+      const double ok = (an != 0.0 && sqrt(v0) / an < 1e-5 && v1 < D2) ? 1.0 : 0.0;   // RIPTRM.py:246-251
       sc[S.an] = an;
       sc[S.atol] = atol;
       sc[S.it] = it;
       sc[S.done] = done;
-      const double ok = (an != 0.0 && sqrt(v0) / an < 1e-5 && v1 < D2) ? 1.0 : 0.0;   // RIPTRM.py:246-251
       sc[S.cg_ok] = ok;
       sc[S.p1obj] = 0.5 * v2 + v3;
       sc[S.delta] = Delta;
       xs[5] = ok;
       xs[6] = 0.5 * v2 + v3;
+      if (stp) {
+        stp[4] = clock64();
+        stp[7] = (long long)it;
+      }
+    }
+  } else if (w == 2) {
+    // hard-case test (k_secular): the component of b on the eigenspace of lam_min (eigenvalues within
+    // 1e-12 max(1, max |lambda|)); a multiple lam_min or a hard case goes to the eigendecomposition path
+    const double hard_tol = 1e-12 * fmax(1.0, fmax(fabs(lmin), fabs(lmaxv)));
+    if (lane == 0) {
+      xs[2] = (double)sturm_count_df(d, e2, m, lmin + hard_tol);
+      double evl[1] = {lmin};
+      riptrm_eig::twisted_vector(z, d, e, evl, m, 0, 16.0 * eps * tnorm, pivmin);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // lane 0's vector -> the wave
+    double zb = 0.0;
+    for (int j = lane; j < m; j += 64) zb += z[j] * b[j];
+    zb = riptrm_wave::wave_sum(zb);
+    if (lane == 0) {
+      xs[8] = fabs(zb);
+      if (stp) stp[2] = clock64();
     }
   }
   __syncthreads();
+  const bool fb = xs[2] > 1.5 || xs[8] <= tolhc * gn;
+  if (fb) {   // uniform
+    if (tid == 0) {
+      sc[S.fallback] = 1.0;
+      sb[evoff] = lmin;
+      infos[k] = 0;
+    }
+    return;
+  }
   // the interior / boundary choice (RIPTRM.py:294-298) and the candidate in T coordinates
   const bool interior = xs[5] != 0.0 && xs[6] <= xs[3];
-  for (int j = tid; j < m; j += 256) sb[peoff + j] = interior ? z[j] : y[j];
+  if (stp && tid == 0) stp[5] = clock64();
+  for (int j = tid; j < m; j += 256) sb[peoff + j] = interior ? cx[j] : y[j];
   if (tid == 0) {
     sc[S.interior] = interior ? 1.0 : 0.0;
     sc[S.kind] = interior ? 1.0 : 0.0;   // riptrm_trs::Kind: boundary 0, interior 1
     sc[S.lam1] = interior ? 0.0 : xs[4];
     sc[S.mineig] = lmin;
     sc[S.fallback] = 0.0;
+    sc[S.newton] = xs[7];
     sb[evoff] = lmin;
     infos[k] = 0;
   }
+}
+
+// v <- H^T v (backward = 0: H_{m-2} ... H_0 v) or H v (backward = 1) for orders up to 1024 on one
+// 1024-thread workgroup (element j on thread j): per reflection each wave's share of the dot product,
+// one workgroup barrier, the 16 wave partials added in a fixed order (two parities of the partial
+// buffer, so a wave may run one reflection ahead); reflector t + 8 is requested while t is applied.
+// ~0.1 us per reflection where one wave with the vector in registers waited on the reflectors' loads.
+__global__ void __launch_bounds__(1024) k_refl_wg(double* base, int64_t sd, int k0, int m, int64_t r_off, int64_t voff,
+                                                  int64_t ooff, int backward) {
+  constexpr int RD = 8;
+  __shared__ double red[2][16];
+  double* sb = base + (int64_t)(k0 + blockIdx.y) * sd;
+  const double* R = sb + r_off;
+  const int j = threadIdx.x, lane = j & 63, w = j >> 6;
+  double v = j < m ? sb[voff + j] : 0.0;
+  const int nt = riptrm_eig::refl_tau(m), nr = m - 1;
+  double ring[RD], rtau[RD];
+  auto fetch = [&](int t, double& u, double& tau) {
+    const int i = backward ? m - 2 - t : t;
+    const bool live = t < nr;
+    tau = R[live ? nt + i : nt];
+    const bool ok = live && j > i && j < m;
+    u = R[ok ? riptrm_eig::refl_col(m, i) - i - 1 + j : nt];
+  };
+#pragma unroll
+  for (int r = 0; r < RD; ++r) fetch(r, ring[r], rtau[r]);
+  for (int t0 = 0; t0 < nr; t0 += RD) {
+#pragma unroll
+    for (int r = 0; r < RD; ++r) {
+      const int t = t0 + r;
+      if (t < nr) {   // uniform
+        const int i = backward ? m - 2 - t : t;
+        const double u = (j > i && j < m) ? ring[r] : 0.0;
+        const double tau = rtau[r];
+        fetch(t + RD, ring[r], rtau[r]);
+        if (tau != 0.0) {   // uniform
+          const double s = riptrm_wave::wave_sum(u * v);
+          if (lane == 0) red[t & 1][w] = s;
+          __syncthreads();
+          double S = 0.0;
+#pragma unroll
+          for (int q = 0; q < 16; ++q) S += red[t & 1][q];
+          v = v - (tau * S) * u;
+        }
+      }
+    }
+  }
+  if (j < m) sb[ooff + j] = v;
 }
 
 }  // namespace riptrm_tri

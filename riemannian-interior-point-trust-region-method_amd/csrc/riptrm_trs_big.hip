@@ -1066,12 +1066,18 @@ __global__ void __launch_bounds__(WG) k_finish_dir(DevParams P, Bat B) {
   }
 }
 
-__global__ void k_finish_mineig(DevParams P, Bat B, int cnt) {
+// the smallest eigenvalue of the trial point's matrix -> the instance, which resumes at PH_MINEIG_END.
+// NaN (the machine stops the instance, RIPTRM_ERR_EIGEN) when the eigenvalues are not valid: a
+// non-converged rocSOLVER dsyevd (info > 0), non-finite input (1) or a timed-out exchange (3).  The
+// hand-written solvers' info 2 (Gram-Schmidt could not orthonormalise the vectors, riptrm_eig.h) leaves
+// the bisection's eigenvalues valid: vals_ok2 = 1 there.
+__device__ __forceinline__ bool eig_values_ok(int info, int vals_ok2) { return info == 0 || (info == 2 && vals_ok2); }
+__global__ void k_finish_mineig(DevParams P, Bat B, int cnt, int vals_ok2) {
   const int k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= cnt) return;
   const Slot q = slot_at(B, k);
   double* s = P.st + (int64_t)B.ids[k] * ST_N;
-  s[ST_MINEIG] = *q.info != 0 ? NAN : q.v[VS_EV][0];   // non-converged dsyevd: the machine stops the instance
+  s[ST_MINEIG] = eig_values_ok(*q.info, vals_ok2) ? q.v[VS_EV][0] : NAN;
   s[ST_PHASE] = PH_MINEIG_END;
 }
 
@@ -1091,11 +1097,11 @@ __global__ void __launch_bounds__(256) k_gep_out(Bat B, int m, int64_t ldv, doub
 
 // the smallest eigenvalue of slot k (eigenvalues ascending) -> mineig[ids[k]]; NaN when the
 // eigensolve did not converge
-__global__ void k_min_out(Bat B, int cnt, double* mineig) {
+__global__ void k_min_out(Bat B, int cnt, double* mineig, int vals_ok2) {
   const int k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= cnt) return;
   const Slot q = slot_at(B, k);
-  mineig[B.ids[k]] = *q.info != 0 ? NAN : q.v[VS_EV][0];
+  mineig[B.ids[k]] = eig_values_ok(*q.info, vals_ok2) ? q.v[VS_EV][0] : NAN;
 }
 
 // copy subproblem ids[k]'s m x m block (row-major, lda) into slot k's matrix (lda m) and a
@@ -1663,6 +1669,12 @@ static int tri_launch_el(riptrm_ctx* c, riptrm_tri::TriArgs a, int cnt, int m) {
     c->tri_grid_bytes = gbytes;
   }
   HIPCHK(c, hipMemsetAsync(a.infos, 0, (size_t)cnt * sizeof(int32_t), c->stream));
+  long long* stamps = nullptr;   // RIPTRM_TRI_STAMPS=1: phase cycles of matrix 0's workgroup 0 on stderr
+  if (getenv_is("RIPTRM_TRI_STAMPS", '1')) {
+    HIPCHK(c, hipMalloc(&stamps, 8 * sizeof(long long)));
+    HIPCHK(c, hipMemsetAsync(stamps, 0, 8 * sizeof(long long), c->stream));
+  }
+  a.stamps = stamps;
   for (int k0 = 0; k0 < cnt; k0 += per) {
     const int nk = std::min(per, cnt - k0);
     HIPCHK(c, hipMemsetAsync(c->tri_grid, 0, (size_t)riptrm_tri::tri_granules(m) * 16 * nk, c->stream));
@@ -1673,6 +1685,16 @@ static int tri_launch_el(riptrm_ctx* c, riptrm_tri::TriArgs a, int cnt, int m) {
     a.G = G;
     void* args[] = {&a};
     HIPCHK(c, hipLaunchCooperativeKernel((const void*)kern, dim3(G, nk), dim3(riptrm_tri::TT), args, 0, c->stream));
+    a.stamps = nullptr;
+  }
+  if (stamps) {
+    long long h[8];
+    HIPCHK(c, hipMemcpyAsync(h, stamps, sizeof(h), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    (void)hipFree(stamps);
+    fprintf(stderr, "[tri stamps] m=%d G=%d cnt=%d gather %lld wave0 %lld update %lld cycles (per step %.0f / %.0f / %.0f; "
+            "wave 0: p.v %.0f, w and c %.0f, reflector %.0f)\n", m, G, cnt, h[0], h[1], h[2], h[0] / (double)(m - 1),
+            h[1] / (double)(m - 1), h[2] / (double)(m - 1), h[4] / (double)(m - 2), h[5] / (double)(m - 2), h[6] / (double)(m - 2));
   }
   return RIPTRM_OK;
 }
@@ -1703,8 +1725,16 @@ static int tri_tridiag(riptrm_ctx* c, const Bat& B, int cnt, int m, int64_t aoff
   return tri_launch(c, a, cnt, m);
 }
 
+// v <- H^T v / H v for the pass's slots (the tridiagonal path's reflectors): one 1024-thread workgroup per
+// slot (k_refl_wg); RIPTRM_TRI_REFL=w: one wave with the vector in registers (k_refl_big, A/B)
 static int tri_refl(riptrm_ctx* c, const Bat& B, int cnt, int m, int64_t voff, int64_t ooff, int backward) {
   const dim3 grid(1, cnt);
+  if (!getenv_is("RIPTRM_TRI_REFL", 'w')) {
+    hipLaunchKernelGGL(riptrm_tri::k_refl_wg, grid, dim3(1024), 0, c->stream, B.base, B.sd, 0, m, off_refl(B.N), voff, ooff,
+                       backward);
+    HIPCHK(c, hipGetLastError());
+    return RIPTRM_OK;
+  }
   switch (riptrm_tri::tri_el(m)) {
     case 4: hipLaunchKernelGGL(riptrm_tri::k_refl_big<4>, grid, dim3(64), 0, c->stream, B.base, B.sd, 0, m, off_refl(B.N), voff, ooff, backward); break;
     case 8: hipLaunchKernelGGL(riptrm_tri::k_refl_big<8>, grid, dim3(64), 0, c->stream, B.base, B.sd, 0, m, off_refl(B.N), voff, ooff, backward); break;
@@ -1717,15 +1747,29 @@ static int tri_refl(riptrm_ctx* c, const Bat& B, int cnt, int m, int64_t voff, i
 template <int EL>
 static int tri_solve_el(riptrm_ctx* c, const Bat& B, int cnt, int m, const double* D, int64_t dstride, double tolhc, int mode) {
   const int64_t N = B.N;
-  const size_t shm = (size_t)8 * 64 * EL * sizeof(double);
+  const size_t shm = (size_t)riptrm_tri::TRI_SOLVE_ARRAYS * 64 * EL * sizeof(double);
   auto kern = riptrm_tri::k_tri_solve<EL>;
   HIPCHK(c, hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm));
   const riptrm_tri::TriSc S{SC_CG_OK, SC_P1OBJ, SC_KIND, SC_LAM1, SC_MINEIG, SC_INTERIOR, SC_DELTA, SC_AN, SC_ATOL, SC_IT,
-                            SC_DONE, SC_TRI_FB};
+                            SC_DONE, SC_TRI_FB, SC_RHO_PREV};   // (SC_RHO_PREV: the Newton steps, diagnostics)
+  long long* stamps = nullptr;   // RIPTRM_TRI_STAMPS=1: slot 0's phase clocks on stderr
+  if (getenv_is("RIPTRM_TRI_STAMPS", '1')) {
+    HIPCHK(c, hipMalloc(&stamps, 8 * sizeof(long long)));
+    HIPCHK(c, hipMemsetAsync(stamps, 0, 8 * sizeof(long long), c->stream));
+  }
   hipLaunchKernelGGL(kern, dim3(1, cnt), dim3(256), shm, c->stream, B.base, B.sd, B.infos, m, off_vec(N, VS_R),
                      off_vec(N, VS_P), off_vec(N, VS_G), off_vec(N, VS_A), off_vec(N, VS_PE), off_vec(N, VS_CGX),
-                     off_vec(N, VS_EV), off_sc(N), S, D, dstride, B.ids, tolhc, mode);
+                     off_vec(N, VS_EV), off_sc(N), S, D, dstride, B.ids, tolhc, mode, stamps);
   HIPCHK(c, hipGetLastError());
+  if (stamps) {
+    long long h[8];
+    HIPCHK(c, hipMemcpyAsync(h, stamps, sizeof(h), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    (void)hipFree(stamps);
+    if (h[0])
+      fprintf(stderr, "[tri_solve stamps] m=%d mode=%d eig %lld hard %lld newton %lld (%lld steps) cg %lld (%lld it) end %lld\n",
+              m, mode, h[1] - h[0], h[2] - h[1], h[3] ? h[3] - h[2] : 0, h[6], h[4] ? h[4] - h[2] : 0, h[7], h[5] - h[0]);
+  }
   return RIPTRM_OK;
 }
 
@@ -1853,10 +1897,11 @@ int riptrm_big_service(riptrm_ctx* c, int* served) {
         if (tri) {
           if (int rc = tri_tridiag(c, Bt, cnt, n - 1, aoff, n)) return rc;
           if (int rc = tri_finish(c, Bt, cnt, n - 1, P.st + ST_DELTA, ST_N, P.opt.trs_tolhardcase, 1)) return rc;
-        } else if (int rc = eig_batched(c, Bt, cnt, true, n - 1, aoff, n)) {
+        } else if (int rc = eig_batched(c, Bt, cnt, cached, n - 1, aoff, n)) {   // vectors only for the cache
           return rc;
         }
-        hipLaunchKernelGGL(k_finish_mineig, dim3(blocks_of(cnt, 64)), dim3(64), 0, c->stream, P, Bt, cnt);
+        hipLaunchKernelGGL(k_finish_mineig, dim3(blocks_of(cnt, 64)), dim3(64), 0, c->stream, P, Bt, cnt,
+                           eig_compact(n - 1) ? 1 : 0);
         if (cached)
           hipLaunchKernelGGL(k_cache_store, dim3(blocks_of((int64_t)n * n, 256), cnt), dim3(256), 0, c->stream, P, Bt, cache,
                              CN, tri ? 1 : 0);
@@ -2049,7 +2094,8 @@ int riptrm_big_gep_ids(riptrm_ctx* c, int dim, const int32_t* sel, int count, co
         return fail(c, RIPTRM_E_HIP, "Exact_RepMat: rocsolver_dsyevd did not converge (info " + std::to_string(info[k]) +
                                          ") on subproblem " + std::to_string(sel[b0 + k]));
     if (mineig_only)
-      hipLaunchKernelGGL(k_min_out, dim3(blocks_of(cnt, 64)), dim3(64), 0, c->stream, Bt, cnt, mineig);
+      hipLaunchKernelGGL(k_min_out, dim3(blocks_of(cnt, 64)), dim3(64), 0, c->stream, Bt, cnt, mineig,
+                         (eig_compact(dim) || tri_mode(dim)) ? 1 : 0);
     else
       hipLaunchKernelGGL(k_gep_out, dim3(blocks_of(dim, 256), cnt), dim3(256), 0, c->stream, Bt, dim, ldv, x, lam1, kind,
                          mineig);

@@ -46,7 +46,7 @@ ERROR_TEXT = {C["RIPTRM_ERR_NO_TCG_ITER"]: "manifold dimension 0: truncated CG c
                                           "trust-region radius or <delta, H delta>; returning the iterate the outer "
                                           "step started from (the completed iterate when the residual at the outer "
                                           "loop head is the non-finite value)"),
-              C["RIPTRM_ERR_EIGEN"]: ("Exact_RepMat: the eigendecomposition did not converge (rocSOLVER dsyevd info != 0; "
+              C["RIPTRM_ERR_EIGEN"]: ("Exact_RepMat: the eigendecomposition did not converge (eigensolver info != 0; "
                                       "scipy.linalg.eig raises LinAlgError); returning the iterate the outer step "
                                       "started from")}
 STATUS_NAMES = {0: None, 1: "initial", 2: "converged", 3: "primal_infeasible", 4: "successful",

@@ -3,8 +3,10 @@
 ``TRSgep(A, a, B, Del, tolhardcase)`` keeps the reference's signature and return value
 (src/solver/RIPTRM.py:218-299: ``(x, lam1, type)``); ``trs_gep_batched`` solves a batch of
 subproblems held as torch tensors on the GPU (dim <= RIPTRM_TRS_DIM_MAX: one launch, the matrix in
-LDS; larger: the HBM path — SciPy CG restated, batched rocSOLVER dsyevd, secular Newton — every
-subproblem of the batch in one pass when the scratch budget allows).  Only B = I is supported — the one call site passes ``np.eye(xdim)``
+LDS; larger: the HBM path — up to dim 199 the hand-written eigensolver and SciPy's CG restated in its
+eigen-coordinates, 200..1024 the cooperative tridiagonalisation and the subproblem in T's coordinates,
+rocSOLVER dsyevd above and for hard cases; the secular Newton — every subproblem of the batch in one
+pass when the scratch budget allows).  Only B = I is supported — the one call site passes ``np.eye(xdim)``
 (RIPTRM.py:441).  No CPU fallback.
 """
 from __future__ import annotations

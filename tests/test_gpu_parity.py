@@ -541,7 +541,8 @@ def test_exact_repmat_lds_and_hbm_paths_agree_near_97(monkeypatch):
     """the two Exact_RepMat paths at the size where they meet.  n = 97 (manifold.dim 96,
     the LDS solver's limit: Householder frame matrix, parallel Jacobi in LDS) solved again with
     RIPTRM_TRS_HBM=1 (the HBM service: densified frame matrix, coef = -x^T (M x) + y^T x in
-    k_repmat_vec, rocSOLVER dsyevd, the eigenpair cache) -- the same reference step (RIPTRM.py:433-444,
+    k_repmat_vec, the hand-written eigensolver of riptrm_eig.h with SciPy's CG in its eigen-coordinates
+    (k_cg_diag), the eigenpair cache) -- the same reference step (RIPTRM.py:433-444,
     599-617, TRSgep :218-299) in two arithmetics, so their trajectories must agree with the bar the
     solo Exact test uses against the oracle (parity.compare_until_flip), and both against the oracle."""
     from parity import compare_until_flip

@@ -147,8 +147,9 @@ def test_si_scaled_exact_repmat_hbm(d, sos, inner):
     """TRS_solver = 'Exact_RepMat' past d = 7 (RIPTRM.py:433-444, :599-617 with TRSgep :218-299):
     manifold.dim = 100 (d = 8) / 392 (d = 16) > RIPTRM_TRS_DIM_MAX, so each instance builds the matrix
     of HwCur (manifold.dim HVPs) in HBM and parks; riptrm_si_solve serves the parked instances in
-    batched passes of the NonnegPCA HBM path (SciPy CG, rocSOLVER dsyevd, secular solve) and
-    relaunches.  Bars: an instance's trajectory is bitwise the one it has solved alone (a slot's
+    batched passes of the NonnegPCA HBM service (d = 8: the hand-written eigensolver of riptrm_eig.h and
+    SciPy's CG in its eigen-coordinates; d = 16: the distributed tridiagonalisation of riptrm_tri.h and
+    the subproblem in T's coordinates; the secular solve) and relaunches.  Bars: an instance's trajectory is bitwise the one it has solved alone (a slot's
     arithmetic does not depend on its pass), and each instance's rows meet compare_until_flip's bar
     against the oracle (trs_oracle: the reference's 2n x 2n pencil).  One outer iteration with a
     few inner ones: the oracle's own cost at these sizes (~2 s per inner iteration at d = 8 with the

@@ -253,7 +253,9 @@ def _hard_cg_cases(m, rs):
     A = (Q * lam) @ Q.T
     A = (A + A.T) / 2
     a = rs.randn(m)
-    out.append((A, a, 1e12, "nearly singular"))
+    out.append((A, a, 1e3, "nearly singular"))
+    a0 = a - Q[:, 0] * (Q[:, 0] @ a)   # no component on the near-null direction: an interior solution
+    out.append((A, a0, 10.0 * np.linalg.norm(np.linalg.lstsq(A, -a0, rcond=1e-8)[0]), "nearly singular, interior"))
     lam = np.sort(np.abs(rs.randn(m))) + 0.5
     lam[0] = -1e-3
     A = (Q * lam) @ Q.T
@@ -306,7 +308,8 @@ def test_compact_cg_matches_dense_cg_on_delicate_subproblems(m, monkeypatch):
             print(f"[cg] m={m} {what}: scipy rr {rr:.1e} eligible {decisions} -> {ref_kind}; {mode}: {k}", flush=True)
             if k == "interior":
                 assert np.linalg.norm(Ab @ x[b] + a) / np.linalg.norm(a) < 1e-5 and x[b] @ x[b] < Del ** 2, (what, mode)
-                assert _obj(Ab, a, x[b]) <= _obj(Ab, a, xb) + 1e-10 * abs(_obj(Ab, a, xb)), (what, mode)
+                assert _obj(Ab, a, x[b]) <= _obj(Ab, a, xb) + 1e-10 * abs(_obj(Ab, a, xb)) + \
+                    10 * m * np.finfo(float).eps * np.linalg.norm(Ab, 2) * max(x[b] @ x[b], xb @ xb), (what, mode)
             else:   # the boundary solution: x within 1e-8, or (at condition numbers 1e9, where both solves
                 # of the secular equation carry ~eps cond) on the sphere with the same model value to 1e-8
                 assert np.linalg.norm(x[b] - xb) <= 1e-8 * max(np.linalg.norm(xb), 1e-300) or \
@@ -317,8 +320,10 @@ def test_compact_cg_matches_dense_cg_on_delicate_subproblems(m, monkeypatch):
                 if k == "interior":
                     # both are CG iterates at rtol 1e-5, so x moves by up to cond x 1e-5 and the model
                     # value by each iterate's own error r^T A^-1 r / 2 <= ||r||^2 / (2 lam_min)
+                    # (plus the evaluation's own rounding, ~m eps ||A|| ||x||^2)
                     lmin = max(np.linalg.eigvalsh(Ab)[0], 1e-300)
                     rx, rp = np.linalg.norm(Ab @ x[b] + a), np.linalg.norm(Ab @ p1 + a)
-                    bound = (rx * rx + rp * rp) / (2.0 * lmin) + 1e-8 * abs(_obj(Ab, a, p1))
+                    ev_err = 10 * m * np.finfo(float).eps * np.linalg.norm(Ab, 2) * max(x[b] @ x[b], p1 @ p1)
+                    bound = (rx * rx + rp * rp) / (2.0 * lmin) + 1e-8 * abs(_obj(Ab, a, p1)) + ev_err
                     assert abs(_obj(Ab, a, x[b]) - _obj(Ab, a, p1)) <= bound, (what, mode)
     assert stable >= 2 * len(cases) // 3, stable
