@@ -888,14 +888,15 @@ def si_cpu_pool(K: int, budget_s: float, procs: int, trs: str, d: int = 5, inner
 
 
 def tri_roofline(m: int, dev, reps: int = 5):
-    """The Exact_RepMat HBM service's work for one subproblem of order 200..1024 (csrc/riptrm_tri.h:
-    the cooperative tridiagonalisation k_tridiag_dist, then k_refl_big / k_tri_solve), timed live with
-    HIP events around riptrm_trs_gep on one frame-like matrix (O(1) symmetric part plus diagonal
-    barrier terms up to 1e6).  Bound: latency.  The tridiagonalisation's m - 1 columns are one all-to-all
-    exchange each (every workgroup publishes its rows' p = tau A v and polls every other's), a chain no
-    bandwidth can shorten; the floor is m - 1 hand-offs at the measured single hop
-    (MI355X_MICROARCH.md, handoff-1to1: ~1.0 us on an idle chip).  Its flops (4/3 m^3) at the FP64
-    vector peak are reported beside it (flops_frac)."""
+    """The Exact_RepMat HBM service's dominant kernel above order 199, the cooperative tridiagonalisation
+    (csrc/riptrm_tri.h k_tridiag_dist, ~m / 16 workgroups), timed live with HIP events on torch's current
+    stream (the library runs on it) around riptrm_sym_tridiag on one frame-like matrix (O(1) symmetric
+    part plus diagonal barrier terms up to 1e6): the reduction alone, as the service runs it per
+    subproblem and per trial point.  Bound: latency.  Its m - 1 columns are one all-to-all exchange each
+    (every workgroup publishes its rows' p = tau A v and polls every other's), a chain no bandwidth can
+    shorten; the floor is m - 1 hand-offs at the measured single hop (MI355X_MICROARCH.md,
+    handoff-1to1: ~1.0 us on an idle chip).  Its flops (4/3 m^3) at the FP64 vector peak are reported
+    beside it (flops_frac)."""
     import numpy as np
     import torch
     import trs
@@ -903,26 +904,25 @@ def tri_roofline(m: int, dev, reps: int = 5):
     D = rs.randn(m, m) / np.sqrt(m)
     D = D + D.T + np.diag(np.where(rs.rand(m) < 0.3, 10.0 ** rs.uniform(2, 6, m), 0.0))
     A = torch.tensor(D[None], dtype=torch.float64, device=dev)
-    a = torch.tensor(rs.randn(1, m), dtype=torch.float64, device=dev)
-    Del = torch.tensor([0.5], dtype=torch.float64, device=dev)
     for _ in range(2):
-        trs.trs_gep_batched(A, a, Del, 1e-8)
+        _, _, info = trs.sym_tridiag(A)
+    assert int(info[0]) == 0
     ts = []
     for _ in range(reps):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
-        trs.trs_gep_batched(A, a, Del, 1e-8)
+        trs.sym_tridiag(A)
         e1.record()
         torch.cuda.synchronize(dev)
         ts.append(e0.elapsed_time(e1) / 1e3)
     t = sorted(ts)[len(ts) // 2]
     hop = 1.0e-6
     ach = (m - 1) / t
+    G = (m + 15) // 16 if m > 512 else (m + 31) // 32 if m > 256 else (m + 63) // 64
     return {"bound": "latency", "achieved": ach, "peak": 1.0 / hop, "unit": "columns/s", "frac": ach / (1.0 / hop),
             "traffic": None, "avg_launch_us": t * 1e6,
-            "kernel": (f"riptrm_tri (k_tridiag_dist on {(m + 15) // 16 if m > 512 else (m + 31) // 32 if m > 256 else (m + 63) // 64} "
-                       "cooperative workgroups, k_refl_big, k_tri_solve): one TRSgep subproblem of order "
-                       f"{m} through riptrm_trs_gep"),
+            "kernel": (f"riptrm_tri::k_tridiag_dist on {G} cooperative workgroups: the tridiagonal reduction of one "
+                       f"order-{m} subproblem matrix through riptrm_sym_tridiag"),
             "flops_frac": (4.0 / 3.0 * m ** 3 / t) / 81.7e12,
             "why": ("latency-bound: one all-to-all exchange per tridiagonalisation column; floor = m - 1 hand-offs "
                     "at ~1.0 us (MI355X_MICROARCH.md handoff-1to1, idle chip)")}

@@ -456,6 +456,17 @@ int riptrm_trs_skip_stats(riptrm_ctx* ctx, int64_t* checked, int64_t* skipped);
 int riptrm_sym_eig(riptrm_ctx* ctx, int32_t dim, int32_t batch, double* A, int64_t lda, int64_t a_stride, double* w,
                    int64_t w_stride, int32_t* info, int32_t vectors);
 
+/* The tridiagonal reduction the Exact_RepMat HBM service runs above order 199 (csrc/riptrm_tri.h
+ * k_tridiag_dist: LAPACK dsytd2, lower, as scipy.linalg.lapack.dsytrd(lower=1) / the eigh inside
+ * TRSgep's pencil, RIPTRM.py:251, would start; the matrix spread over one cooperative launch of
+ * ~m / 16 workgroups, rows in registers, one all-to-all exchange per column).  batch matrices of order
+ * dim (64 <= dim <= 1024) at A + k a_stride (leading dimension lda; the lower triangle is read, A is
+ * not written): the diagonal into d + k de_stride (dim entries), the off-diagonal into e + k de_stride
+ * (dim - 1 entries).  info[k] = 0, or 3 when an exchange timed out.  Asynchronous on the context's
+ * stream; the context keeps the reflectors in a scratch (dim (dim + 1) / 2 doubles per matrix). */
+int riptrm_sym_tridiag(riptrm_ctx* ctx, int32_t dim, int32_t batch, const double* A, int64_t lda, int64_t a_stride,
+                       double* d, double* e, int64_t de_stride, int32_t* info);
+
 /* ==== Stiefel(n, p) manifold operations =========================================
  * Not in the reference (north_star / BASELINE configs[4] ask for them): pymanopt 2.x formulas,
  * oracle/stiefel_oracle.py, parity unpinned.  Batched over `batch` instances, each an n x p

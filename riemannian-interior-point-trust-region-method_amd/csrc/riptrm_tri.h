@@ -10,14 +10,16 @@
 // Exact line's GPU time: profiles/r6_exact1000_rocsolver_rocprofv3_kernel_stats.csv).  Here:
 //   1. k_tridiag_dist: dsytd2 (lower) on G = ceil(m / 8 RW) workgroups per matrix, row l on workgroup
 //      l mod G (cyclic, so the shrinking trailing matrix stays balanced), each wave holding RW rows
-//      with EL elements per lane in registers.  ONE exchange per column: every workgroup publishes
-//      p_l = tau A v for its rows and the owner of row i + 1 publishes that row; each workgroup then
-//      forms w = p - tau (p.v) v / 2, the next column c = row_{i+1} - (v w_{i+1} + w v_{i+1}) and its
+//      with EL elements per lane in registers.  ONE exchange per column: every workgroup publishes,
+//      per row l, the pair {p_l = tau A_l . v, A_{l, i+1}} (row i + 1 of the updated matrix is its
+//      column i + 1: the bitwise-symmetric update keeps it so); each workgroup then forms
+//      w = p - tau (p.v) v / 2, the next column c = col_{i+1} - (v w_{i+1} + w v_{i+1}) and its
 //      reflector redundantly (the same arithmetic everywhere: bitwise the same values), and runs the
-//      rank-two update of its rows fused with the next column's p.  The exchange is the k_persist
-//      protocol: 16-byte granules {value, tag} written by one write-through store each, polled with
-//      sc1 loads (MI355X_MICROARCH.md, persistent hand-offs), two parities, plus one arrival granule
-//      per workgroup and pass so no workgroup overwrites a parity another still reads.
+//      rank-two update of its rows fused with the next column's p.  The exchange: 16-byte granules
+//      {p_l, A_{l, i+1}} written by one write-through store each, their mantissas' last bits set to the
+//      pass's tag bit (a rounding-level change every workgroup sees alike), polled with sc1 loads
+//      (MI355X_MICROARCH.md, persistent hand-offs), two parities, plus one arrival granule {value,
+//      check, pass} per workgroup and pass so no workgroup overwrites a parity another still reads.
 //   2. k_refl_big: b = H^T a (and x = H y at the end) with the reflectors from HBM, one wave.
 //   3. k_tri_solve: the extreme eigenvalues of T by Sturm bisection (riptrm_eig.h's counts), the
 //      hard-case test on lam_min's eigenvector (a twisted factorisation), the secular Newton of
@@ -47,8 +49,8 @@ constexpr unsigned long long TRI_TIMEOUT = 200000000ull;   // 2 s of the 100 MHz
 __host__ __device__ constexpr int tri_el(int m) { return m <= 256 ? 4 : (m <= 512 ? 8 : 16); }
 __host__ __device__ constexpr int tri_rw(int m) { return 32 / tri_el(m); }
 __host__ __device__ constexpr int tri_groups(int m) { return (m + 8 * tri_rw(m) - 1) / (8 * tri_rw(m)); }
-// granules per matrix: 2 parities x [p: m][row: m][arrivals: G]
-__host__ __device__ constexpr int64_t tri_par(int m) { return 2 * (int64_t)m + tri_groups(m); }
+// granules per matrix: 2 parities x [{p, column}: m][arrivals: G]
+__host__ __device__ constexpr int64_t tri_par(int m) { return (int64_t)m + tri_groups(m); }
 __host__ __device__ constexpr int64_t tri_granules(int m) { return 2 * tri_par(m); }
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
@@ -58,6 +60,17 @@ __device__ __forceinline__ unsigned tag_check(unsigned lo, unsigned hi, unsigned
 __device__ __forceinline__ void st_gran(__amdgpu_buffer_rsrc_t rs, int64_t g, double v, unsigned pass) {
   const unsigned lo = (unsigned)__double2loint(v), hi = (unsigned)__double2hiint(v);
   const u32x4 q = {lo, hi, tag_check(lo, hi, pass), pass};
+  __builtin_amdgcn_raw_buffer_store_b128(q, rs, (int)(g * 16), 0, 16);   // aux 16: sc1 (write-through)
+}
+
+// the pair granule {a, b} of pass `pass`: both mantissas' last bits = the pass's tag bit, which
+// alternates between the passes sharing a parity (and is 1 on each parity's first pass: the grid
+// starts zeroed); a reader takes it when both bits match (a granule torn between passes mixes them)
+__device__ __forceinline__ unsigned pair_bit(unsigned pass) { return ((pass + 1) >> 1) & 1u; }
+__device__ __forceinline__ void st_pair(__amdgpu_buffer_rsrc_t rs, int64_t g, double a, double b, unsigned pass) {
+  const unsigned t = pair_bit(pass);
+  const u32x4 q = {((unsigned)__double2loint(a) & ~1u) | t, (unsigned)__double2hiint(a),
+                   ((unsigned)__double2loint(b) & ~1u) | t, (unsigned)__double2hiint(b)};
   __builtin_amdgcn_raw_buffer_store_b128(q, rs, (int)(g * 16), 0, 16);   // aux 16: sc1 (write-through)
 }
 
@@ -73,8 +86,11 @@ struct TriArgs {
   void* grid;            // granules, tri_granules(m) per launch slot (zeroed before the launch)
   int64_t grid_bytes;
   int m, G;
+  int sleep;             // s_sleep 1 rounds between polls (RIPTRM_TRI_SLEEP; default 1)
+  long long* hops;       // diagnostics (RIPTRM_TRI_STAMPS=2): matrix 0, every workgroup, steps i = 16 s: the
+                         // wall clock (100 MHz, chip-wide) at [g][s][0] its gather's start, [1] its end
   long long* stamps;     // diagnostics (RIPTRM_TRI_STAMPS=1): workgroup 0 of matrix 0 accumulates clock64
-                         // cycles in [0] the gather, [1] wave 0's section + barrier, [2] the update + publish
+                         // cycles in [0] the gather, [1] the column step, [2] the update + publish
 };
 
 // the reflector of the column c[i+1 .. m) (dlarfg: H (alpha, x) = (beta, 0), v(i+1) = 1) into vo, by
@@ -117,9 +133,11 @@ __device__ __forceinline__ void bar_lds() { asm volatile("s_waitcnt lgkmcnt(0)\n
 template <int EL, int RW>
 __global__ void __launch_bounds__(TT) k_tridiag_dist(TriArgs a) {
   __shared__ double Vbuf[2][EL * 64];   // v_i and v_{i+1} (by step parity)
-  __shared__ double GP[EL * 64];        // gathered p (written by the gather, read by wave 0 only)
-  __shared__ double W[EL * 64];         // w = p + a2 v (wave 0 -> every wave after the barrier)
-  __shared__ double C[EL * 64];         // gathered row i + 1, then the column c of step i + 1 (wave 0)
+  __shared__ double GP[EL * 64];        // gathered p (written by the gather, read by the column step)
+  __shared__ double W[EL * 64];         // w = p + a2 v (column step -> every wave's update)
+  __shared__ double C[EL * 64];         // gathered column (= row) i + 1 (column 0 of the input in the prologue)
+  __shared__ double CN[EL * 64];        // the column c of step i + 1 (column step -> every wave's update)
+  __shared__ double red[2][8];          // the column step's per-wave partial sums
   // (a wave that finishes its rows early starts the next gather while others still read W, Vbuf: the
   // gather writes only GP and C, which nobody reads after the step's barrier)
   __shared__ double scal[2];
@@ -177,7 +195,8 @@ __global__ void __launch_bounds__(TT) k_tridiag_dist(TriArgs a) {
   }
   __syncthreads();
   double tau_c = scal[0];
-  // pass 1: p^(0)_l = tau_0 A_l. v_0 for own rows l >= 1, row 1 by its owner, this workgroup's arrival
+  // pass 1: {p^(0)_l = tau_0 A_l. v_0, A_{l,1}} for own rows l >= 1 (lane 1 holds column 1), this
+  // workgroup's arrival
   {
     const int64_t pb = gbase + (int64_t)(1 & 1) * par;
     double vq[EL];
@@ -191,20 +210,13 @@ __global__ void __launch_bounds__(TT) k_tridiag_dist(TriArgs a) {
 #pragma unroll
         for (int q = 0; q < EL; ++q) acc += (lane + 64 * q >= 1) ? Ar[s][q] * vq[q] : 0.0;
         const double p = tau_c * riptrm_wave::wave_sum(acc);
-        if (lane == 0) st_gran(rs, pb + l, p, 1u);
-        if (l == 1 && m > 1) {
-#pragma unroll
-          for (int q = 0; q < EL; ++q) {
-            const int j = lane + 64 * q;
-            if (j >= 1 && j < m) st_gran(rs, pb + m + j, Ar[s][q], 1u);
-          }
-        }
+        if (lane == 1) st_pair(rs, pb + l, p, Ar[s][0], 1u);
       }
     }
-    if (tid == 0) st_gran(rs, pb + 2 * m + g, 0.0, 1u);
+    if (tid == 0) st_gran(rs, pb + m + g, 0.0, 1u);
   }
 
-  constexpr int NG = (2 * 64 * EL + 256 + TT - 1) / TT;   // granules polled per thread (upper bound)
+  constexpr int NG = (64 * EL + 64 + TT - 1) / TT;   // granules polled per thread (upper bound)
   bool failed = false;
   long long* stp = (a.stamps && g == 0 && k == 0 && tid == 0) ? a.stamps : nullptr;
   long long acc0 = 0, acc1 = 0, acc2 = 0, tq = stp ? clock64() : 0, sa = 0, sb = 0, sc = 0, sd = 0;
@@ -212,9 +224,16 @@ __global__ void __launch_bounds__(TT) k_tridiag_dist(TriArgs a) {
     const unsigned pass = (unsigned)(i + 1);
     const int64_t pb = gbase + (int64_t)(pass & 1) * par;
     const int r = m - i - 1;   // trailing indices i + 1 .. m - 1
-    const int ng = 2 * r + G;
-    // gather: p_j, row_{i+1}[j] (j > i) and every workgroup's arrival, polled until the tags say this pass
+    const int ng = r + G;
+    lds_t* Vc = (lds_t*)Vbuf[i & 1];
+    lds_t* Vn = (lds_t*)Vbuf[(i + 1) & 1];
+    long long* hp = (a.hops && k == 0 && tid == 0 && (i & 15) == 0) ? a.hops + ((int64_t)g * ((m + 15) / 16) + (i >> 4)) * 2 : nullptr;
+    if (hp) hp[0] = (long long)wall_clock64();
+    // gather: p_j, row_{i+1}[j] (j > i) and every workgroup's arrival, polled until the tags say this
+    // pass; each p_j as it lands goes into this wave's share of p . v (the column step's first sum, its
+    // wave tree and partial ahead of the gather's barrier: one barrier less per step)
     {
+      double sp = 0.0;
       int pend = 0;
       int64_t gi[NG];
 #pragma unroll
@@ -222,8 +241,7 @@ __global__ void __launch_bounds__(TT) k_tridiag_dist(TriArgs a) {
         const int t = tid + TT * u;
         int64_t gx = 0;
         if (t < r) gx = pb + i + 1 + t;
-        else if (t < 2 * r) gx = pb + m + i + 1 + (t - r);
-        else if (t < ng) gx = pb + 2 * m + (t - 2 * r);
+        else if (t < ng) gx = pb + m + (t - r);
         gi[u] = gx;
         if (t < ng) pend |= 1 << u;
       }
@@ -237,11 +255,15 @@ __global__ void __launch_bounds__(TT) k_tridiag_dist(TriArgs a) {
         for (int u = 0; u < NG; ++u)
           if (pend & (1 << u)) {
             const u32x4 q = qv[u];
-            if (q.w == pass && q.z == tag_check(q.x, q.y, pass)) {
-              const int t = tid + TT * u;
-              const double v = __hiloint2double((int)q.y, (int)q.x);
-              if (t < r) GP[i + 1 + t] = v;
-              else if (t < 2 * r) C[i + 1 + (t - r)] = v;
+            const int t = tid + TT * u;
+            const unsigned tb = pair_bit(pass);
+            if (t < r ? ((q.x & 1u) == tb && (q.z & 1u) == tb) : (q.w == pass && q.z == tag_check(q.x, q.y, pass))) {
+              if (t < r) {   // {p_j, A_{j, i+1}}, j = i + 1 + t
+                const double pv = __hiloint2double((int)q.y, (int)q.x);
+                GP[i + 1 + t] = pv;
+                C[i + 1 + t] = __hiloint2double((int)q.w, (int)q.z);
+                sp += pv * Vc[i + 1 + t];
+              }
               pend &= ~(1 << u);
             }
           }
@@ -250,8 +272,10 @@ __global__ void __launch_bounds__(TT) k_tridiag_dist(TriArgs a) {
           failed = true;
           break;
         }
-        __builtin_amdgcn_s_sleep(1);
+        for (int z = 0; z < a.sleep; ++z) __builtin_amdgcn_s_sleep(1);
       }
+      sp = riptrm_wave::wave_sum(sp);
+      if (lane == 0) red[0][w] = sp;
     }
     if (failed) failflag = 1;
     bar_lds();
@@ -259,6 +283,7 @@ __global__ void __launch_bounds__(TT) k_tridiag_dist(TriArgs a) {
       if (tid == 0) a.infos[k] = 3;
       return;
     }
+    if (hp) hp[1] = (long long)wall_clock64();
     if (stp) {
       const long long t1 = clock64();
       acc0 += t1 - tq;
@@ -267,109 +292,96 @@ __global__ void __launch_bounds__(TT) k_tridiag_dist(TriArgs a) {
     // this workgroup has read pass i + 1: the parity of pass i + 2 (= pass i's) may be reused
     const int64_t pn = gbase + (int64_t)((pass + 1) & 1) * par;
     const bool more = i + 1 <= m - 2;
-    if (tid == 0 && more) st_gran(rs, pn + 2 * m + g, 0.0, pass + 1);
-    lds_t* Vc = (lds_t*)Vbuf[i & 1];
-    lds_t* Vn = (lds_t*)Vbuf[(i + 1) & 1];
-    if (w == 0) {
-      const long long q0s = stp ? clock64() : 0;
-      // w = p + a2 v, a2 = -tau (p . v) / 2; the column i + 1 of the updated matrix; its reflector.
-      // Every operand is loaded in one batch first (loads inside the selects were issued one
-      // latency at a time: 3 us of the 7.6 us step at m = 999), the column stays in registers.
-      const int i2 = i + 2 < m ? i + 2 : i + 1;
-      const double gp1 = GP[i + 1], vi1 = Vc[i + 1], cr1 = C[i + 1];
-      const double gp2 = GP[i2], vc2 = Vc[i2], cr2 = C[i2];
-      // (chunks of four columns: every chunk's loads in flight together, few registers live beside the rows)
-      double s = 0.0;
+    if (tid == 0 && more) st_gran(rs, pn + m + g, 0.0, pass + 1);
+    // The column step, spread over the eight waves (wave w owns the columns j = lane + 64 q, q = w + 8 t):
+    // w = p + a2 v with a2 = -tau (p . v) / 2, the column i + 1 of the updated matrix, its reflector.
+    // Two block sums (p . v, its wave partials made in the gather, and the reflector's sum of squares:
+    // wave trees then eight partials in a fixed order, so every thread of every workgroup holds the
+    // same tau); the column stays in registers.  (One wave doing all of it was a 2.4 us latency chain
+    // of the 7 us step at m = 999.)
+    constexpr int QT = (EL + 7) / 8;
+    const long long q0s = stp ? clock64() : 0;
+    const int i2 = i + 2 < m ? i + 2 : i + 1;
+    const double gp1 = GP[i + 1], vi1 = Vc[i + 1], cr1 = C[i + 1];
+    const double gp2 = GP[i2], vc2 = Vc[i2], cr2 = C[i2];
+    double gq[QT], vq[QT], cq[QT];
 #pragma unroll
-      for (int q0 = 0; q0 < EL; q0 += 4) {
-        double gp[4], vc[4];
+    for (int t = 0; t < QT; ++t) {
+      const int q = w + 8 * t, j = lane + 64 * q;
+      const bool on = q < EL;   // uniform over the wave
+      gq[t] = on ? GP[j] : 0.0;
+      vq[t] = on ? Vc[j] : 0.0;
+      cq[t] = on ? C[j] : 0.0;
+    }
+    const long long q1s = stp ? clock64() : 0;
+    double s = 0.0;   // p . v from the gather's partials
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          gp[u] = GP[lane + 64 * (q0 + u)];
-          vc[u] = Vc[lane + 64 * (q0 + u)];
-        }
+    for (int u = 0; u < 8; ++u) s += red[0][u];
+    const double a2 = -0.5 * tau_c * s;
+    const double wi1 = gp1 + a2 * vi1;
+    double sn = 0.0, cn[QT];   // the reflector's sum over c_j^2, j >= i + 3
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const int j = lane + 64 * (q0 + u);
-          s += (j > i && j < m) ? gp[u] * vc[u] : 0.0;
-        }
-        __builtin_amdgcn_sched_barrier(0);
+    for (int t = 0; t < QT; ++t) {
+      const int q = w + 8 * t, j = lane + 64 * q;
+      const bool on = q < EL;
+      const double wj = (on && j > i && j < m) ? gq[t] + a2 * vq[t] : 0.0;
+      cn[t] = (on && j > i + 1 && j < m) ? cq[t] - (vq[t] * wi1 + wj * vi1) : 0.0;   // row j's update at column i + 1
+      if (on) {
+        W[j] = wj;
+        CN[j] = cn[t];
       }
-      s = riptrm_wave::wave_sum(s);
-      const double a2 = -0.5 * tau_c * s;
-      const long long q1s = stp ? clock64() : 0;
-      const double wi1 = gp1 + a2 * vi1;
-      double sn = 0.0;   // the reflector's sum over c_j^2, j >= i + 3
+      sn += j >= i + 3 ? cn[t] * cn[t] : 0.0;
+    }
+    sn = riptrm_wave::wave_sum(sn);
+    if (lane == 0) red[1][w] = sn;
+    bar_lds();
+    const long long q2s = stp ? clock64() : 0;
+    sn = 0.0;
 #pragma unroll
-      for (int q0 = 0; q0 < EL; q0 += 4) {
-        double gp[4], vc[4], cr[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          gp[u] = GP[lane + 64 * (q0 + u)];
-          vc[u] = Vc[lane + 64 * (q0 + u)];
-          cr[u] = C[lane + 64 * (q0 + u)];
-        }
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const int j = lane + 64 * (q0 + u);
-          const double wj = (j > i && j < m) ? gp[u] + a2 * vc[u] : 0.0;
-          W[j] = wj;
-          const double cj = (j > i + 1 && j < m) ? cr[u] - (vc[u] * wi1 + wj * vi1) : 0.0;   // row j's update at column i + 1
-          C[j] = cj;
-          sn += j >= i + 3 ? cj * cj : 0.0;
-        }
-        __builtin_amdgcn_sched_barrier(0);   // keep the next chunk's loads behind this one (register pressure)
+    for (int u = 0; u < 8; ++u) sn += red[1][u];
+    if (writer && tid == 0) dv[i + 1] = cr1 - (vi1 * wi1 + wi1 * vi1);
+    double tau_n = 0.0, scl = 0.0;
+    if (more) {
+      // dlarfg on c[i+2 .. m): alpha = c[i+2] by its update formula (every thread)
+      const double alpha = cr2 - (vc2 * wi1 + (gp2 + a2 * vc2) * vi1);
+      double beta = alpha;
+      if (sn != 0.0) {
+        beta = -copysign(sqrt(alpha * alpha + sn), alpha);
+        tau_n = (beta - alpha) / beta;
+        scl = 1.0 / (alpha - beta);
       }
-      const double di1 = cr1 - (vi1 * wi1 + wi1 * vi1);
-      const long long q2s = stp ? clock64() : 0;
-      if (writer && lane == 0) dv[i + 1] = di1;
-      if (more) {
-        // dlarfg on c[i+2 .. m): alpha = c[i+2] (its update formula, every lane), the sum over j >= i + 3
-        const double alpha = cr2 - (vc2 * wi1 + (gp2 + a2 * vc2) * vi1);
-        sn = riptrm_wave::wave_sum(sn);
-        double tau = 0.0, beta = alpha, scl = 0.0;
-        if (sn != 0.0) {
-          beta = -copysign(sqrt(alpha * alpha + sn), alpha);
-          tau = (beta - alpha) / beta;
-          scl = 1.0 / (alpha - beta);
-        }
+      const int64_t co = riptrm_eig::refl_col(m, i + 1) - (i + 2);
 #pragma unroll
-        for (int q = 0; q < EL; ++q) {   // (each lane reads back its own c_j)
-          const int j = lane + 64 * q;
-          Vn[j] = (j <= i + 1 || j >= m) ? 0.0 : (j == i + 2 ? 1.0 : C[j] * scl);
+      for (int t = 0; t < QT; ++t) {
+        const int q = w + 8 * t, j = lane + 64 * q;
+        if (q < EL) {
+          const double vn = (j <= i + 1 || j >= m) ? 0.0 : (j == i + 2 ? 1.0 : cn[t] * scl);
+          Vn[j] = vn;
+          if (writer && j >= i + 2 && j < m) R[co + j] = vn;
         }
-        if (lane == 0) scal[(i + 1) & 1] = tau;
-        if (stp) {
-          const long long q3s = clock64();
-          sa += q1s - q0s;
-          sb += q2s - q1s;
-          sc += q3s - q2s;
-        }
-        if (writer) {
-          if (lane == 0) {
-            ev[i + 1] = beta;
-            R[riptrm_eig::refl_tau(m) + i + 1] = tau;
-          }
-          const int64_t co = riptrm_eig::refl_col(m, i + 1) - (i + 2);
-#pragma unroll
-          for (int q = 0; q < EL; ++q) {
-            const int j = lane + 64 * q;
-            if (j >= i + 2 && j < m) R[co + j] = Vn[j];
-          }
-        }
+      }
+      if (writer && tid == 0) {
+        ev[i + 1] = beta;
+        R[riptrm_eig::refl_tau(m) + i + 1] = tau_n;
+      }
+      if (stp) {
+        const long long q3s = clock64();
+        sa += q1s - q0s;
+        sb += q2s - q1s;
+        sc += q3s - q2s;
       }
     }
-    bar_lds();
+    // (no barrier: the update below takes v_{i+1} = c scl from CN and the scalars every thread holds;
+    // Vn is next step's v, read after its gather's barrier)
     if (stp) {
       const long long t1 = clock64();
       acc1 += t1 - tq;
       tq = t1;
     }
     if (!more) break;
-    const double tau_n = scal[(i + 1) & 1];
     // rank-two update of own rows l >= i + 2 (row i + 1 is finished: its diagonal is d_{i+1}), fused
     // with p^(i+1)_l = tau_{i+1} A'_l. v_{i+1}; publish pass i + 2
-    // (v, w, v_{i+1} read from LDS per row: held in registers beside the rows they spill)
+    // (v, w, c read from LDS per row: held in registers beside the rows they spill)
 #pragma unroll
     for (int s = 0; s < RW; ++s) {
       const int l = rowid[s];
@@ -381,17 +393,15 @@ __global__ void __launch_bounds__(TT) k_tridiag_dist(TriArgs a) {
           const int j = lane + 64 * q;
           const double x = Ar[s][q] - (vl * W[j] + wl * Vc[j]);
           Ar[s][q] = x;
-          acc += (j >= i + 2) ? x * Vn[j] : 0.0;
+          acc += (j >= i + 2) ? x * (j == i + 2 ? 1.0 : CN[j] * scl) : 0.0;   // v_{i+1}[j], as Vn holds it
         }
         const double p = tau_n * riptrm_wave::wave_sum(acc);
-        if (lane == 0) st_gran(rs, pn + l, p, pass + 1);
-        if (l == i + 2) {
+        // {p_l, A_{l, i+2}}: column i + 2 sits in lane (i + 2) mod 64, register (i + 2) / 64
+        const int qc = (i + 2) >> 6;
+        double ac = Ar[s][0];
 #pragma unroll
-          for (int q = 0; q < EL; ++q) {
-            const int j = lane + 64 * q;
-            if (j >= i + 2 && j < m) st_gran(rs, pn + m + j, Ar[s][q], pass + 1);
-          }
-        }
+        for (int q = 1; q < EL; ++q) ac = q == qc ? Ar[s][q] : ac;
+        if (lane == ((i + 2) & 63)) st_pair(rs, pn + l, p, ac, pass + 1);
       }
     }
     tau_c = tau_n;
@@ -695,6 +705,98 @@ __device__ __forceinline__ void ldl_newton(const lds_t* d, const lds_t* e, const
   s3 = a3;
 }
 
+// The eigenvector of T (d, e, e2 = e^2; split where e_j = 0) for its smallest eigenvalue lt, unnormalised,
+// into Z[0 .. m) by one thread: riptrm_eig::twisted_vector for t = 0 (dlar1v's twisted factorisation of
+// T - lt I, z_r = 1 at the twist r where |gamma_r| is least, in the first block of the split T holding
+// an eigenvalue within delta of lt), restructured for one thread's latency: every pass loads four
+// steps' operands ahead, the pivots' reciprocals come off the chains (the pass that needs D+ ratios
+// reads them from DP, the last pass is one multiply per step), no divisions.  DP: scratch (D+).
+__device__ __forceinline__ void twisted_min(lds_t* Z, lds_t* DP, const lds_t* d, const lds_t* e, int m, double lt,
+                                            double delta, double pivmin) {
+  using riptrm_eig::rcp_nr;
+  const double xa = lt - delta, xb = lt + delta;
+  int blo = 0, bhi = m - 1, bs = 0, ca = 0, cb = 0;
+  bool found = false;
+  double qa = 0.0, qb = 0.0, dp = 0.0;
+  // forward: the Sturm counts at lt -+ delta (the block) and D+ (restarting at every split)
+  auto fstep = [&](int j, double dj, double ejm, double ej) {
+    const bool start = j == bs;
+    const double ej2 = start ? 0.0 : ejm * ejm;
+    qa = (dj - xa) - (start ? 0.0 : ej2 * rcp_nr(qa));
+    qb = (dj - xb) - (start ? 0.0 : ej2 * rcp_nr(qb));
+    dp = (dj - lt) - (start ? 0.0 : ej2 * rcp_nr(dp));
+    if (fabs(qa) < pivmin) qa = -pivmin;
+    if (fabs(qb) < pivmin) qb = -pivmin;
+    if (fabs(dp) < pivmin) dp = -pivmin;
+    DP[j] = dp;
+    ca += qa < 0.0;
+    cb += qb < 0.0;
+    if (j == m - 1 || ej == 0.0) {   // block bs .. j ends: the first one with an eigenvalue near lt
+      if (!found && cb - ca > 0) {
+        found = true;
+        blo = bs;
+        bhi = j;
+      }
+      ca = cb = 0;
+      bs = j + 1;
+    }
+  };
+  int j = 0;
+  for (; j + 4 <= m; j += 4) {
+    const double d0 = d[j], d1 = d[j + 1], d2 = d[j + 2], d3 = d[j + 3];
+    const double em = j > 0 ? e[j - 1] : 0.0, e0 = e[j], e1 = e[j + 1], e2v = e[j + 2], e3 = j + 3 < m - 1 ? e[j + 3] : 0.0;
+    fstep(j, d0, em, e0);
+    fstep(j + 1, d1, e0, e1);
+    fstep(j + 2, d2, e1, e2v);
+    fstep(j + 3, d3, e2v, e3);
+  }
+  for (; j < m; ++j) fstep(j, d[j], j > 0 ? e[j - 1] : 0.0, j < m - 1 ? e[j] : 0.0);
+  // backward over the block: D- and gamma_j = D+_j + D-_j - (d_j - lt) (gamma_bhi = D+_bhi); Z[j] =
+  // e_{j-1} / D-_j for the solve above the twist
+  double dm = d[bhi] - lt;
+  if (fabs(dm) < pivmin) dm = -pivmin;
+  double best = fabs(DP[bhi]);
+  int r = bhi;
+  if (bhi > blo) Z[bhi] = e[bhi - 1] * rcp_nr(dm);
+  auto bstep = [&](int i, double di, double ei, double dpi, double eim) {
+    const double dil = di - lt;
+    dm = dil - (ei * ei) * rcp_nr(dm);
+    if (fabs(dm) < pivmin) dm = -pivmin;
+    const double g = fabs(dpi + dm - dil);
+    if (g < best) {
+      best = g;
+      r = i;
+    }
+    Z[i] = eim * rcp_nr(dm);
+  };
+  int i = bhi - 1;
+  for (; i - 3 >= blo; i -= 4) {
+    const double d0 = d[i], d1 = d[i - 1], d2 = d[i - 2], d3 = d[i - 3];
+    const double e0 = e[i], e1 = e[i - 1], e2v = e[i - 2], e3 = e[i - 3];
+    const double p0 = DP[i], p1 = DP[i - 1], p2 = DP[i - 2], p3 = DP[i - 3];
+    const double e4 = i - 4 >= 0 ? e[i - 4] : 0.0;
+    bstep(i, d0, e0, p0, e1);
+    bstep(i - 1, d1, e1, p1, e2v);
+    bstep(i - 2, d2, e2v, p2, e3);
+    bstep(i - 3, d3, e3, p3, e4);
+  }
+  for (; i >= blo; --i) bstep(i, d[i], e[i], DP[i], i > 0 ? e[i - 1] : 0.0);
+  // the solve outward from the twist: z_j = -(e_{j-1} / D-_j) z_{j-1} above, -(e_j / D+_j) z_{j+1} below
+  double z = 1.0;
+  for (int k = r + 1; k <= bhi; ++k) {
+    z = -Z[k] * z;
+    Z[k] = z;
+  }
+  z = 1.0;
+  for (int k = r - 1; k >= blo; --k) {
+    z = -(e[k] * rcp_nr(DP[k])) * z;
+    Z[k] = z;
+  }
+  Z[r] = 1.0;
+  for (int k = 0; k < blo; ++k) Z[k] = 0.0;
+  for (int k = bhi + 1; k < m; ++k) Z[k] = 0.0;
+}
+
 // scalar slots this header uses (riptrm_trs_big.hip Sc)
 struct TriSc {
   int cg_ok, p1obj, kind, lam1, mineig, interior, delta, an, atol, it, done, fallback, newton;
@@ -702,20 +804,22 @@ struct TriSc {
 
 // After k_tridiag_dist (and the reflector application: b = H^T a at boff): mode 0 the subproblem, mode 1
 // the smallest eigenvalue only.  One workgroup of 256 threads per slot: waves 0 / 1 the extreme
-// eigenvalues; then, at once, wave 0 the secular Newton (lane 0), wave 1 SciPy's CG on T y = -b and
-// wave 2 the hard-case test (lam_min's multiplicity and the component of b on its twisted eigenvector;
-// a hard case discards the other two and sets the fallback flag).  Writes the boundary / interior
-// candidate in T coordinates at peoff (the host applies H), lam_min at evoff[0].
-constexpr int TRI_SOLVE_ARRAYS = 10;   // LDS vectors of 64 EL doubles
+// eigenvalues; then, at once, wave 0 the secular Newton (lane 0) and the boundary candidate's model
+// value, waves 1 and 3 the CG's certified skip test (cg_skip; k_cg_wg's bounds) and wave 2 the
+// hard-case test (lam_min's multiplicity and the component of b on its twisted eigenvector; a hard
+// case sets the fallback flag and ends there); then wave 1 SciPy's CG on T y = -b unless the skip
+// test shows that its candidate cannot win.  Writes the boundary / interior candidate in T
+// coordinates at peoff (the host applies H), lam_min at evoff[0].
+constexpr int TRI_SOLVE_ARRAYS = 13;   // LDS vectors of 64 EL doubles
 template <int EL>
 __global__ void __launch_bounds__(256) k_tri_solve(double* base, int64_t sd, int32_t* infos, int m, int64_t d_off,
                                                    int64_t e_off, int64_t boff, int64_t aoff_vec, int64_t peoff,
                                                    int64_t cgxoff, int64_t evoff, int64_t scoff, TriSc S,
                                                    const double* Dg, int64_t dstride, const int32_t* ids, double tolhc,
-                                                   int mode, long long* stamps) {
+                                                   int mode, int cg_skip, long long* stamps) {
   // stamps (diagnostics, RIPTRM_TRI_STAMPS=1; slot 0): clock64 at [0] start, [1] extreme eigenvalues,
-  // [2] hard-case test done (wave 2), [3] the Newton done (wave 0), [4] the CG done (wave 1), [5] end;
-  // [6] Newton steps, [7] CG iterations
+  // [2] hard-case test done (wave 2), [3] the Newton done (wave 0), [4] the CG done or skipped (wave 1),
+  // [5] end, [6] Newton steps, [7] CG iterations, [8] the skip test done (wave 1), [9] 1: CG skipped
   long long* stp = (stamps && blockIdx.y == 0) ? stamps : nullptr;
   if (stp && threadIdx.x == 0) stp[0] = clock64();
   extern __shared__ double smem[];
@@ -730,8 +834,14 @@ __global__ void __launch_bounds__(256) k_tri_solve(double* base, int64_t sd, int
   lds_t* rd = lf + V;
   lds_t* z = rd + V;   // the twisted eigenvector
   lds_t* cx = z + V;   // the CG's iterate
+  lds_t* pz = cx + V;  // the skip test: T^-1 b and its LDL^T factor
+  lds_t* lz = pz + V;
+  lds_t* rz = lz + V;
   __shared__ double red[8];
-  __shared__ double xs[10];   // lam_min, lam_max, multiplicity, xobj, lam1, CG ok, p1obj, Newton steps, ghard
+  // lam_min, lam_max, multiplicity, xobj, lam1, CG ok, p1obj, Newton steps, ghard, -Delta / ||y||,
+  // ||T^-1 b||, b . T^-1 b, its residual
+  __shared__ double xs[13];
+  __shared__ int ic[128];   // the skip test's Sturm counts
   const int k = blockIdx.y;
   double* sb = base + (int64_t)k * sd;
   double* sc = sb + scoff;
@@ -838,11 +948,18 @@ __global__ void __launch_bounds__(256) k_tri_solve(double* base, int64_t sd, int
   an = sqrt((red[0] + red[1]) + (red[2] + red[3]));
   const double gn = sqrt((red[4] + red[5]) + (red[6] + red[7]));
   __syncthreads();
+  const double lmx = fmax(fabs(lmin), fabs(lmaxv));
   if (w == 0) {
     // the secular Newton of k_secular: ||(T + l1 I)^-1 b|| = Delta from l1 = -lam_min + ||b|| / Delta
     if (lane == 0) {
+      // The iterates bracket the root: f > 0 right of it, f < 0 left (bl starts at the pole -lam_min).
+      // A step to or below bl bisects towards it (k_secular bisects towards the pole: the same
+      // sequence while no iterate has landed left of the root); a step past br is taken (bisecting
+      // there costs ~45 steps where f bends the wrong way: OUT=r6tri9), and a bracket shrunk to the
+      // stopping tolerance, or |f| at rounding level, ends the loop (near a hard case the LDL^T's f is
+      // rounding noise at the step tolerance: 100 steps without these)
       const double lo = -lmin;
-      double l1 = lo + gn / Delta;
+      double l1 = lo + gn / Delta, bl = lo, br = INFINITY;
       int itn = 0;
       for (; itn < 100; ++itn) {
         double s2, s3;
@@ -850,9 +967,13 @@ __global__ void __launch_bounds__(256) k_tri_solve(double* base, int64_t sd, int
         const double xn = sqrt(s2);
         const double f = 1.0 / xn - 1.0 / Delta;
         const double fp = s3 / (xn * xn * xn);
+        if (fabs(f) * Delta <= 4.0 * eps) break;   // ||y|| = Delta to rounding: no step can do better
+        if (f > 0.0) br = fmin(br, l1);
+        else bl = fmax(bl, l1);
         double nl = l1 - f / fp;
-        if (nl <= lo) nl = 0.5 * (lo + l1);
-        if (fabs(nl - l1) <= 1e-15 * fmax(1.0, fabs(l1))) {
+        if (nl <= bl) nl = 0.5 * (bl + l1);
+        const double tol = 1e-15 * fmax(1.0, fabs(l1));
+        if (fabs(nl - l1) <= tol || br - bl <= tol) {
           l1 = nl;
           break;
         }
@@ -860,23 +981,130 @@ __global__ void __launch_bounds__(256) k_tri_solve(double* base, int64_t sd, int
       }
       double s2, s3;
       ldl_newton(d, e, e2, m, l1, b, y, t2, lf, rd, false, s2, s3);
-      const double scl = Delta / sqrt(s2);
-      double o0 = 0.0, o1 = 0.0;
-      for (int j = 0; j < m; ++j) {
-        const double c = -y[j] * scl;
-        y[j] = c;
-      }
-      for (int j = 0; j < m; ++j) {   // xobj = pe^T T pe / 2 + b^T pe
-        const double tp = d[j] * y[j] + (j > 0 ? e[j - 1] * y[j - 1] : 0.0) + (j < m - 1 ? e[j] * y[j + 1] : 0.0);
-        o0 += y[j] * tp;
-        o1 += b[j] * y[j];
-      }
-      xs[3] = 0.5 * o0 + o1;
       xs[4] = l1;
       xs[7] = (double)itn;
+      xs[9] = -Delta / sqrt(s2);
+      if (stp) stp[6] = itn;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // lane 0's solve -> the wave
+    // the boundary candidate pe = -Delta y / ||y|| and xobj = pe^T T pe / 2 + b^T pe (lane-strided)
+    const double scl = xs[9];
+    double o0 = 0.0, o1 = 0.0;
+    for (int j = lane; j < m; j += 64) {
+      const double yj = y[j] * scl;
+      const double tp = d[j] * yj + (j > 0 ? e[j - 1] * (y[j - 1] * scl) : 0.0) + (j < m - 1 ? e[j] * (y[j + 1] * scl) : 0.0);
+      o0 += yj * tp;
+      o1 += b[j] * yj;
+    }
+    for (int j = lane; j < m; j += 64) y[j] *= scl;   // (after every lane's reads: one wave, in order)
+    o0 = riptrm_wave::wave_sum(o0);
+    o1 = riptrm_wave::wave_sum(o1);
+    if (lane == 0) {
+      xs[3] = 0.5 * o0 + o1;
+      if (stp) stp[3] = clock64();
+    }
+  } else if (w == 1 || w == 3) {
+    // The CG's certified skip (k_cg_wg's bounds, from T alone): lam_s <= min |lambda_i| by Sturm counts
+    // at 64 points either side of 0 (x = -+ lmx 2^(-7 l / 16), down to 2e-9 lmx; wave 1 the negative
+    // side and 0 itself, wave 3 the positive side), and p* = -T^-1 b by the LDL^T at 0 with its
+    // residual, whose error ||T^-1 res|| <= ||res|| / lam_s enters both bounds.
+    const double x = w == 1 ? (lane == 63 ? 0.0 : -lmx * exp2(-7.0 * (62 - lane) / 16.0)) : lmx * exp2(-7.0 * lane / 16.0);
+    const int cnt = (cg_skip && lmx > 0.0) ? sturm_count_df(d, e2, m, x) : 0;
+    ic[w == 1 ? lane : 64 + lane] = cnt;
+    if (w == 1 && cg_skip && lane == 0) {
+      double s2, s3;
+      ldl_newton(d, e, e2, m, 0.0, b, pz, nullptr, lz, rz, false, s2, s3);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (w == 1 && cg_skip) {   // the residual T ps - b and b . ps (ps = T^-1 b, p* = -ps)
+      double rr = 0.0, bp = 0.0, pp = 0.0;
+      for (int j = lane; j < m; j += 64) {
+        const double tp = d[j] * pz[j] + (j > 0 ? e[j - 1] * pz[j - 1] : 0.0) + (j < m - 1 ? e[j] * pz[j + 1] : 0.0);
+        rr += (tp - b[j]) * (tp - b[j]);
+        bp += b[j] * pz[j];
+        pp += pz[j] * pz[j];
+      }
+      rr = riptrm_wave::wave_sum(rr);
+      bp = riptrm_wave::wave_sum(bp);
+      pp = riptrm_wave::wave_sum(pp);
+      if (lane == 0) {
+        xs[10] = sqrt(pp);
+        xs[11] = bp;
+        xs[12] = sqrt(rr);
+        if (stp) stp[8] = clock64();
+      }
+    }
+  } else if (w == 2) {
+    // hard-case test (k_secular): the component of b on the eigenspace of lam_min (eigenvalues within
+    // 1e-12 max(1, max |lambda|)); a multiple lam_min or a hard case goes to the eigendecomposition path
+    const double hard_tol = 1e-12 * fmax(1.0, lmx);
+    if (lane == 0) {
+      xs[2] = (double)sturm_count_df(d, e2, m, lmin + hard_tol);
+      twisted_min(z, cx, d, e, m, lmin, 16.0 * eps * tnorm, pivmin);   // (cx: the CG's, free until the barrier)
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // lane 0's vector -> the wave
+    double zb = 0.0, zz = 0.0;
+    for (int j = lane; j < m; j += 64) {
+      zb += z[j] * b[j];
+      zz += z[j] * z[j];
+    }
+    zb = riptrm_wave::wave_sum(zb);
+    zz = riptrm_wave::wave_sum(zz);
+    if (lane == 0) {
+      xs[8] = fabs(zb) / sqrt(zz);
+      if (stp) stp[2] = clock64();
+    }
+  }
+  __syncthreads();
+  const bool fb = xs[2] > 1.5 || xs[8] <= tolhc * gn;
+  if (fb) {   // uniform
+    if (tid == 0) {
+      sc[S.fallback] = 1.0;
+      sb[evoff] = lmin;
+      infos[k] = 0;
+    }
+    return;
+  }
+  // the skip: no iterate with ||T p1 + b|| <= e := 1e-5 ||a|| can pass RIPTRM.py:294-298 when
+  //   ||p1|| >= ||p*|| - e / lam_s >= Delta   or   p1obj >= -b^T T^-1 b / 2 - e^2 / (2 lam_s) > xobj
+  // (k_cg_wg), with ||p*|| >= ||ps|| - ||res|| / lam_s and b^T T^-1 b <= b . ps + ||b|| ||res|| / lam_s
+  bool skip = false;
+  if (cg_skip) {
+    const int c0 = ic[63];   // eigenvalues below 0
+    // the strongest bounds: the largest |x| with every negative eigenvalue below x (count c0), the
+    // largest x > 0 with none in [0, x) (count c0); none certified: 0 (no skip)
+    double ng = 0.0, ps = 0.0;
+    for (int l = 0; l < 63; ++l)
+      if (ic[l] == c0) ng = fmax(ng, lmx * exp2(-7.0 * (62 - l) / 16.0));
+    for (int l = 0; l < 64; ++l)
+      if (ic[64 + l] == c0) ps = fmax(ps, lmx * exp2(-7.0 * l / 16.0));
+    if (c0 == 0) ng = INFINITY;
+    if (c0 == m) ps = INFINITY;
+    const double lam_s = fmin(ng, ps) * (1.0 - 1e-6) - 4.0 * m * eps * tnorm;
+    const double pn = xs[10], bp = xs[11], resn = xs[12], xobj = xs[3];
+    if (lam_s > 1e-8 * lmx && isfinite(pn) && isfinite(bp) && isfinite(resn) && isfinite(xobj)) {
+      const double e1 = 1e-5 * an;
+      const bool far = (pn - resn / lam_s) * (1.0 - 1e-6) - e1 / lam_s >= Delta;
+      const double s2u = bp + gn * resn / lam_s;
+      const double p1lo = -0.5 * s2u - 0.5 * e1 * e1 / lam_s;
+      const bool worse = p1lo - xobj > 1e-6 * (fabs(s2u) + fabs(xobj)) + 1e-10 * (e1 * 1e5) * Delta;
+      skip = far || worse;
+    }
+  }
+  if (skip) {   // uniform
+    if (tid == 0) {
+      sc[S.an] = an;
+      sc[S.atol] = 1e-5 * an;
+      sc[S.it] = 0.0;
+      sc[S.done] = 4.0;
+      sc[S.cg_ok] = 0.0;
+      sc[S.p1obj] = 0.0;
+      sc[S.delta] = Delta;
+      xs[5] = 0.0;
+      xs[6] = 0.0;
       if (stp) {
-        stp[3] = clock64();
-        stp[6] = itn;
+        stp[4] = clock64();
+        stp[9] = 1;
       }
     }
   } else if (w == 1) {
@@ -972,34 +1200,8 @@ __global__ void __launch_bounds__(256) k_tri_solve(double* base, int64_t sd, int
         stp[7] = (long long)it;
       }
     }
-  } else if (w == 2) {
-    // hard-case test (k_secular): the component of b on the eigenspace of lam_min (eigenvalues within
-    // 1e-12 max(1, max |lambda|)); a multiple lam_min or a hard case goes to the eigendecomposition path
-    const double hard_tol = 1e-12 * fmax(1.0, fmax(fabs(lmin), fabs(lmaxv)));
-    if (lane == 0) {
-      xs[2] = (double)sturm_count_df(d, e2, m, lmin + hard_tol);
-      double evl[1] = {lmin};
-      riptrm_eig::twisted_vector(z, d, e, evl, m, 0, 16.0 * eps * tnorm, pivmin);
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // lane 0's vector -> the wave
-    double zb = 0.0;
-    for (int j = lane; j < m; j += 64) zb += z[j] * b[j];
-    zb = riptrm_wave::wave_sum(zb);
-    if (lane == 0) {
-      xs[8] = fabs(zb);
-      if (stp) stp[2] = clock64();
-    }
   }
   __syncthreads();
-  const bool fb = xs[2] > 1.5 || xs[8] <= tolhc * gn;
-  if (fb) {   // uniform
-    if (tid == 0) {
-      sc[S.fallback] = 1.0;
-      sb[evoff] = lmin;
-      infos[k] = 0;
-    }
-    return;
-  }
   // the interior / boundary choice (RIPTRM.py:294-298) and the candidate in T coordinates
   const bool interior = xs[5] != 0.0 && xs[6] <= xs[3];
   if (stp && tid == 0) stp[5] = clock64();
@@ -1060,6 +1262,127 @@ __global__ void __launch_bounds__(1024) k_refl_wg(double* base, int64_t sd, int 
         }
       }
     }
+  }
+  if (j < m) sb[ooff + j] = v;
+}
+
+// ---- blocked reflector application --------------------------------------------------------------
+// RB consecutive reflections in one round: with s_a = u_a . v (v at the block's start), G_ab = u_a . u_b
+// and c_a = tau_a (s_a - sum over the block's earlier reflections b of G_ab c_b), the block maps v to
+// v - sum_a c_a u_a (the reflections' exact composition; the sums in another order).  G depends on the
+// reflectors only: k_refl_gram forms it once per tridiagonalisation, for both applications.
+constexpr int RB = 16;
+__host__ __device__ constexpr int refl_blocks(int m) { return (m - 1 + RB - 1) / RB; }
+__host__ __device__ constexpr int64_t refl_gram_doubles(int m) { return (int64_t)refl_blocks(m) * RB * RB; }
+
+// u_i[j] of reflector i (riptrm_eig refl_col layout: j = i + 1 .. m - 1, u_i[i + 1] = 1), 0 elsewhere
+__device__ __forceinline__ double refl_u(const double* R, int m, int i, int j) {
+  const bool ok = i < m - 1 && j > i && j < m;
+  return ok ? R[riptrm_eig::refl_col(m, i) - i - 1 + j] : 0.0;
+}
+
+// G of block blockIdx.x (reflectors b RB .. b RB + RB - 1; absent ones 0) of slot k0 + blockIdx.y into
+// the slot at goff + b RB^2 (row-major RB x RB, symmetric; the diagonal unused)
+__global__ void __launch_bounds__(256) k_refl_gram(double* base, int64_t sd, int k0, int m, int64_t r_off, int64_t goff) {
+  constexpr int NP = RB * (RB - 1) / 2;
+  __shared__ double part[4][NP];
+  double* sb = base + (int64_t)(k0 + blockIdx.y) * sd;
+  const double* R = sb + r_off;
+  const int b = blockIdx.x, i0 = b * RB, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  double acc[NP];
+#pragma unroll
+  for (int x = 0; x < NP; ++x) acc[x] = 0.0;
+  for (int j = i0 + 1 + tid; j < m; j += 256) {
+    double u[RB];
+#pragma unroll
+    for (int a = 0; a < RB; ++a) u[a] = refl_u(R, m, i0 + a, j);
+    int x = 0;
+#pragma unroll
+    for (int a = 0; a < RB; ++a)
+#pragma unroll
+      for (int c = a + 1; c < RB; ++c) acc[x++] += u[a] * u[c];
+  }
+#pragma unroll
+  for (int x = 0; x < NP; ++x) {
+    const double t = riptrm_wave::wave_sum(acc[x]);
+    if (lane == 0) part[w][x] = t;
+  }
+  __syncthreads();
+  if (tid < NP) {
+    int a = 0, x = tid;
+    while (x >= RB - 1 - a) {
+      x -= RB - 1 - a;
+      ++a;
+    }
+    const int c = a + 1 + x;
+    const double g = (part[0][tid] + part[1][tid]) + (part[2][tid] + part[3][tid]);
+    double* G = sb + goff + (int64_t)b * RB * RB;
+    G[a * RB + c] = g;
+    G[c * RB + a] = g;
+  }
+}
+
+// v <- H^T v (backward = 0: H_{m-2} ... H_0 v) or H v (backward = 1) for orders up to 1024 on one
+// 1024-thread workgroup (element j on thread j), RB reflections per round: the RB dot products (wave
+// trees, sixteen partials per value in a fixed order), wave 0 solves for c (lane a holds s_a and row a
+// of G; one broadcast per reflection), every thread subtracts its sum of c_a u_a[j].  The next block's
+// reflector entries are loaded during the current one.  G from k_refl_gram at goff.
+__global__ void __launch_bounds__(1024) k_refl_blk(double* base, int64_t sd, int k0, int m, int64_t r_off, int64_t goff,
+                                                   int64_t voff, int64_t ooff, int backward) {
+  __shared__ double part[16][RB];
+  __shared__ double cs[RB];
+  double* sb = base + (int64_t)(k0 + blockIdx.y) * sd;
+  const double* R = sb + r_off;
+  const double* Gall = sb + goff;
+  const int j = threadIdx.x, lane = j & 63, w = j >> 6;
+  const int nt = riptrm_eig::refl_tau(m), nb = refl_blocks(m);
+  double v = j < m ? sb[voff + j] : 0.0;
+  double un[RB];
+  auto load = [&](int bi, double (&u)[RB]) {
+    const int b = backward ? nb - 1 - bi : bi;
+#pragma unroll
+    for (int a = 0; a < RB; ++a) u[a] = bi < nb ? refl_u(R, m, b * RB + a, j) : 0.0;
+  };
+  load(0, un);
+  for (int bi = 0; bi < nb; ++bi) {
+    const int b = backward ? nb - 1 - bi : bi, i0 = b * RB;
+    double u[RB];
+#pragma unroll
+    for (int a = 0; a < RB; ++a) u[a] = un[a];
+    load(bi + 1, un);
+#pragma unroll
+    for (int a = 0; a < RB; ++a) {
+      const double t = riptrm_wave::wave_sum(u[a] * v);
+      if (lane == 0) part[w][a] = t;
+    }
+    __syncthreads();
+    if (w == 0) {
+      // lane a < RB: s_a, tau_a, G row a; the reflections in application order
+      const int a = lane < RB ? lane : 0;
+      double sa = 0.0;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) sa += part[q][a];
+      const int ia = i0 + a;
+      const double ta = (lane < RB && ia < m - 1) ? R[nt + ia] : 0.0;
+      double g[RB];
+#pragma unroll
+      for (int c = 0; c < RB; ++c) g[c] = Gall[(int64_t)b * RB * RB + a * RB + c];
+      double cmine = 0.0;
+#pragma unroll
+      for (int t = 0; t < RB; ++t) {
+        const int at = backward ? RB - 1 - t : t;   // (static per unrolled step and direction)
+        const double cl = ta * sa;                   // c of lane at, once lane at's s is final
+        const double c = __shfl(cl, at);
+        if (lane == at) cmine = c;
+        sa -= (backward ? g[RB - 1 - t] : g[t]) * c;
+      }
+      if (lane < RB) cs[lane] = cmine;
+    }
+    __syncthreads();
+    double dv = 0.0;
+#pragma unroll
+    for (int a = 0; a < RB; ++a) dv += cs[a] * u[a];
+    v -= dv;
   }
   if (j < m) sb[ooff + j] = v;
 }

@@ -30,6 +30,7 @@
 #include <dlfcn.h>
 #include <math.h>
 #include <algorithm>
+#include <climits>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -1675,6 +1676,17 @@ static int tri_launch_el(riptrm_ctx* c, riptrm_tri::TriArgs a, int cnt, int m) {
     HIPCHK(c, hipMemsetAsync(stamps, 0, 8 * sizeof(long long), c->stream));
   }
   a.stamps = stamps;
+  long long* hops = nullptr;   // RIPTRM_TRI_STAMPS=2: every workgroup's gather start / end every 16 steps
+  const int ns = (m + 15) / 16;
+  if (getenv_is("RIPTRM_TRI_STAMPS", '2')) {
+    HIPCHK(c, hipMalloc(&hops, (size_t)G * ns * 2 * sizeof(long long)));
+    HIPCHK(c, hipMemsetAsync(hops, 0, (size_t)G * ns * 2 * sizeof(long long), c->stream));
+  }
+  a.hops = hops;
+  {
+    const char* sl = getenv("RIPTRM_TRI_SLEEP");   // polling pace (A/B)
+    a.sleep = sl ? std::max(1, atoi(sl)) : 1;
+  }
   for (int k0 = 0; k0 < cnt; k0 += per) {
     const int nk = std::min(per, cnt - k0);
     HIPCHK(c, hipMemsetAsync(c->tri_grid, 0, (size_t)riptrm_tri::tri_granules(m) * 16 * nk, c->stream));
@@ -1686,14 +1698,48 @@ static int tri_launch_el(riptrm_ctx* c, riptrm_tri::TriArgs a, int cnt, int m) {
     void* args[] = {&a};
     HIPCHK(c, hipLaunchCooperativeKernel((const void*)kern, dim3(G, nk), dim3(riptrm_tri::TT), args, 0, c->stream));
     a.stamps = nullptr;
+    a.hops = nullptr;
+  }
+  if (hops) {
+    // per sampled step: the publishers' skew (last - first gather start: a workgroup starts its
+    // gather right after publishing) and each workgroup's wait past the last publisher
+    std::vector<long long> h((size_t)G * ns * 2);
+    HIPCHK(c, hipMemcpyAsync(h.data(), hops, h.size() * sizeof(long long), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    (void)hipFree(hops);
+    double skew = 0.0, lat = 0.0, own = 0.0, latmax = 0.0;
+    int cntv = 0;
+    for (int t = 1; t < ns - 1; ++t) {
+      long long lo = LLONG_MAX, hi = LLONG_MIN;
+      for (int g = 0; g < G; ++g) {
+        lo = std::min(lo, h[((size_t)g * ns + t) * 2]);
+        hi = std::max(hi, h[((size_t)g * ns + t) * 2]);
+      }
+      double lt = 0.0, lm = 0.0, ow = 0.0;
+      for (int g = 0; g < G; ++g) {
+        const long long e = h[((size_t)g * ns + t) * 2 + 1];
+        lt += (double)(e - hi);
+        lm = std::max(lm, (double)(e - hi));
+        ow += (double)(e - h[((size_t)g * ns + t) * 2]);
+      }
+      skew += (double)(hi - lo);
+      lat += lt / G;
+      latmax += lm;
+      own += ow / G;
+      ++cntv;
+    }
+    if (cntv)
+      fprintf(stderr, "[tri hops] m=%d G=%d over %d sampled steps (us): publisher skew %.2f, wait past the last publisher "
+              "mean %.2f max %.2f, gather (own start to end) %.2f\n", m, G, cntv, skew / cntv / 100.0, lat / cntv / 100.0,
+              latmax / cntv / 100.0, own / cntv / 100.0);
   }
   if (stamps) {
     long long h[8];
     HIPCHK(c, hipMemcpyAsync(h, stamps, sizeof(h), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     (void)hipFree(stamps);
-    fprintf(stderr, "[tri stamps] m=%d G=%d cnt=%d gather %lld wave0 %lld update %lld cycles (per step %.0f / %.0f / %.0f; "
-            "wave 0: p.v %.0f, w and c %.0f, reflector %.0f)\n", m, G, cnt, h[0], h[1], h[2], h[0] / (double)(m - 1),
+    fprintf(stderr, "[tri stamps] m=%d G=%d cnt=%d gather %lld column %lld update %lld cycles (per step %.0f / %.0f / %.0f; "
+            "column step: p.v %.0f, w and c %.0f, reflector %.0f)\n", m, G, cnt, h[0], h[1], h[2], h[0] / (double)(m - 1),
             h[1] / (double)(m - 1), h[2] / (double)(m - 1), h[4] / (double)(m - 2), h[5] / (double)(m - 2), h[6] / (double)(m - 2));
   }
   return RIPTRM_OK;
@@ -1726,10 +1772,18 @@ static int tri_tridiag(riptrm_ctx* c, const Bat& B, int cnt, int m, int64_t aoff
 }
 
 // v <- H^T v / H v for the pass's slots (the tridiagonal path's reflectors): one 1024-thread workgroup per
-// slot (k_refl_wg); RIPTRM_TRI_REFL=w: one wave with the vector in registers (k_refl_big, A/B)
+// slot, 16 reflections per round (k_refl_blk; the rounds' Gram blocks from k_refl_gram in the slot's
+// matrix area, dead once T is formed: tri_finish makes them); RIPTRM_TRI_REFL=s one reflection per
+// round (k_refl_wg), =w one wave with the vector in registers (k_refl_big) (A/B)
 static int tri_refl(riptrm_ctx* c, const Bat& B, int cnt, int m, int64_t voff, int64_t ooff, int backward) {
   const dim3 grid(1, cnt);
-  if (!getenv_is("RIPTRM_TRI_REFL", 'w')) {
+  if (!getenv_is("RIPTRM_TRI_REFL", 'w') && !getenv_is("RIPTRM_TRI_REFL", 's')) {
+    hipLaunchKernelGGL(riptrm_tri::k_refl_blk, grid, dim3(1024), 0, c->stream, B.base, B.sd, 0, m, off_refl(B.N),
+                       (int64_t)0, voff, ooff, backward);
+    HIPCHK(c, hipGetLastError());
+    return RIPTRM_OK;
+  }
+  if (getenv_is("RIPTRM_TRI_REFL", 's')) {
     hipLaunchKernelGGL(riptrm_tri::k_refl_wg, grid, dim3(1024), 0, c->stream, B.base, B.sd, 0, m, off_refl(B.N), voff, ooff,
                        backward);
     HIPCHK(c, hipGetLastError());
@@ -1745,7 +1799,8 @@ static int tri_refl(riptrm_ctx* c, const Bat& B, int cnt, int m, int64_t voff, i
 }
 
 template <int EL>
-static int tri_solve_el(riptrm_ctx* c, const Bat& B, int cnt, int m, const double* D, int64_t dstride, double tolhc, int mode) {
+static int tri_solve_el(riptrm_ctx* c, const Bat& B, int cnt, int m, const double* D, int64_t dstride, double tolhc, int mode,
+                        bool cg_skip) {
   const int64_t N = B.N;
   const size_t shm = (size_t)riptrm_tri::TRI_SOLVE_ARRAYS * 64 * EL * sizeof(double);
   auto kern = riptrm_tri::k_tri_solve<EL>;
@@ -1754,21 +1809,26 @@ static int tri_solve_el(riptrm_ctx* c, const Bat& B, int cnt, int m, const doubl
                             SC_DONE, SC_TRI_FB, SC_RHO_PREV};   // (SC_RHO_PREV: the Newton steps, diagnostics)
   long long* stamps = nullptr;   // RIPTRM_TRI_STAMPS=1: slot 0's phase clocks on stderr
   if (getenv_is("RIPTRM_TRI_STAMPS", '1')) {
-    HIPCHK(c, hipMalloc(&stamps, 8 * sizeof(long long)));
-    HIPCHK(c, hipMemsetAsync(stamps, 0, 8 * sizeof(long long), c->stream));
+    HIPCHK(c, hipMalloc(&stamps, 10 * sizeof(long long)));
+    HIPCHK(c, hipMemsetAsync(stamps, 0, 10 * sizeof(long long), c->stream));
   }
   hipLaunchKernelGGL(kern, dim3(1, cnt), dim3(256), shm, c->stream, B.base, B.sd, B.infos, m, off_vec(N, VS_R),
                      off_vec(N, VS_P), off_vec(N, VS_G), off_vec(N, VS_A), off_vec(N, VS_PE), off_vec(N, VS_CGX),
-                     off_vec(N, VS_EV), off_sc(N), S, D, dstride, B.ids, tolhc, mode, stamps);
+                     off_vec(N, VS_EV), off_sc(N), S, D, dstride, B.ids, tolhc, mode, cg_skip ? 1 : 0, stamps);
   HIPCHK(c, hipGetLastError());
   if (stamps) {
-    long long h[8];
+    long long h[10];
     HIPCHK(c, hipMemcpyAsync(h, stamps, sizeof(h), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     (void)hipFree(stamps);
-    if (h[0])
-      fprintf(stderr, "[tri_solve stamps] m=%d mode=%d eig %lld hard %lld newton %lld (%lld steps) cg %lld (%lld it) end %lld\n",
-              m, mode, h[1] - h[0], h[2] - h[1], h[3] ? h[3] - h[2] : 0, h[6], h[4] ? h[4] - h[2] : 0, h[7], h[5] - h[0]);
+    if (h[0] && mode == 0) {
+      const long long par = std::max(std::max(h[2], h[3]), h[8]);   // the concurrent phases' end
+      fprintf(stderr, "[tri_solve stamps] m=%d mode=0 eig %lld hard %lld newton %lld (%lld steps) skip-test %lld cg %lld "
+              "(%lld it%s) end %lld\n", m, h[1] - h[0], h[2] - h[1], h[3] - h[1], h[6], h[8] ? h[8] - h[1] : 0,
+              h[4] ? h[4] - par : 0, h[7], h[9] ? ", skipped" : "", h[5] - h[0]);
+    } else if (h[0]) {
+      fprintf(stderr, "[tri_solve stamps] m=%d mode=1 eig %lld\n", m, h[1] - h[0]);
+    }
   }
   return RIPTRM_OK;
 }
@@ -1776,15 +1836,20 @@ static int tri_solve_el(riptrm_ctx* c, const Bat& B, int cnt, int m, const doubl
 // after tri_tridiag (or a cache load of T): mode 1 the smallest eigenvalue only (-> VS_EV[0]); mode 0
 // the subproblem min x^T A x / 2 + a^T x, ||x|| <= Delta (a at VS_A): b = H^T a, k_tri_solve, x = H pe
 // -> VS_X and the result scalars.  Subproblems it cannot serve set SC_TRI_FB (tri_fallback_ids).
-static int tri_finish(riptrm_ctx* c, const Bat& B, int cnt, int m, const double* D, int64_t dstride, double tolhc, int mode) {
+static int tri_finish(riptrm_ctx* c, const Bat& B, int cnt, int m, const double* D, int64_t dstride, double tolhc, int mode,
+                      bool cg_skip = false) {
   const int64_t N = B.N;
-  if (mode == 0)
+  if (mode == 0) {
+    hipLaunchKernelGGL(riptrm_tri::k_refl_gram, dim3(riptrm_tri::refl_blocks(m), cnt), dim3(256), 0, c->stream, B.base,
+                       B.sd, 0, m, off_refl(N), (int64_t)0);
+    HIPCHK(c, hipGetLastError());
     if (int rc = tri_refl(c, B, cnt, m, off_vec(N, VS_A), off_vec(N, VS_G), 0)) return rc;
+  }
   int rc;
   switch (riptrm_tri::tri_el(m)) {
-    case 4: rc = tri_solve_el<4>(c, B, cnt, m, D, dstride, tolhc, mode); break;
-    case 8: rc = tri_solve_el<8>(c, B, cnt, m, D, dstride, tolhc, mode); break;
-    default: rc = tri_solve_el<16>(c, B, cnt, m, D, dstride, tolhc, mode); break;
+    case 4: rc = tri_solve_el<4>(c, B, cnt, m, D, dstride, tolhc, mode, cg_skip); break;
+    case 8: rc = tri_solve_el<8>(c, B, cnt, m, D, dstride, tolhc, mode, cg_skip); break;
+    default: rc = tri_solve_el<16>(c, B, cnt, m, D, dstride, tolhc, mode, cg_skip); break;
   }
   if (rc) return rc;
   if (mode == 0) return tri_refl(c, B, cnt, m, off_vec(N, VS_PE), off_vec(N, VS_X), 1);
@@ -1793,14 +1858,25 @@ static int tri_finish(riptrm_ctx* c, const Bat& B, int cnt, int m, const double*
 
 // the ids of the pass whose subproblem set SC_TRI_FB (a hard case or a multiple smallest eigenvalue).
 // Synchronises.
-static int tri_fallback_ids(riptrm_ctx* c, const Bat& B, int cnt, const int32_t* ids, std::vector<int32_t>& out) {
+// (count_skip: the pass ran k_tri_solve's CG skip test; its outcomes into riptrm_trs_skip_stats)
+static int tri_fallback_ids(riptrm_ctx* c, const Bat& B, int cnt, const int32_t* ids, std::vector<int32_t>& out,
+                            bool count_skip = false) {
   out.clear();
-  std::vector<double> fb(cnt);
+  std::vector<double> fb(cnt), done(count_skip ? cnt : 0);
   HIPCHK(c, hipMemcpy2DAsync(fb.data(), sizeof(double), B.base + off_sc(B.N) + SC_TRI_FB, (size_t)B.sd * sizeof(double),
                              sizeof(double), cnt, hipMemcpyDeviceToHost, c->stream));
+  if (count_skip)
+    HIPCHK(c, hipMemcpy2DAsync(done.data(), sizeof(double), B.base + off_sc(B.N) + SC_DONE, (size_t)B.sd * sizeof(double),
+                               sizeof(double), cnt, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
-  for (int k = 0; k < cnt; ++k)
-    if (fb[k] != 0.0) out.push_back(ids[k]);
+  for (int k = 0; k < cnt; ++k) {
+    if (fb[k] != 0.0) {
+      out.push_back(ids[k]);
+    } else if (count_skip) {   // (a hard case ends before the test)
+      c->big_cg_checked += 1;
+      c->big_cg_skipped += done[k] == 4.0;
+    }
+  }
   c->tri_fallbacks += (int64_t)out.size();
   return RIPTRM_OK;
 }
@@ -1911,10 +1987,11 @@ int riptrm_big_service(riptrm_ctx* c, int* served) {
                              CN, 1);
         else if (int rc = tri_tridiag(c, Bt, cnt, n - 1, aoff, n))
           return rc;
-        if (int rc = tri_finish(c, Bt, cnt, n - 1, P.st + ST_DELTA, ST_N, P.opt.trs_tolhardcase, 0)) return rc;
+        const bool skip = !getenv_is("RIPTRM_CG_SKIP", '0');
+        if (int rc = tri_finish(c, Bt, cnt, n - 1, P.st + ST_DELTA, ST_N, P.opt.trs_tolhardcase, 0, skip)) return rc;
         hipLaunchKernelGGL(k_finish_dir, dim3(1, cnt), dim3(WG), 0, c->stream, P, Bt);
         std::vector<int32_t> fbi;
-        if (int rc = tri_fallback_ids(c, Bt, cnt, L.data() + k0, fbi)) return rc;
+        if (int rc = tri_fallback_ids(c, Bt, cnt, L.data() + k0, fbi, skip)) return rc;
         for (size_t f0 = 0; f0 < fbi.size(); f0 += (size_t)S) {   // hard cases: the eigendecomposition path
           const int fc = (int)std::min<size_t>((size_t)S, fbi.size() - f0);
           if (int rc = put_ids(c, Bt, fbi.data() + f0, fc)) return rc;
@@ -2043,8 +2120,9 @@ int riptrm_big_gep_ids(riptrm_ctx* c, int dim, const int32_t* sel, int count, co
       }
     } else if (tri_mode(dim)) {   // T = H^T A H across the chip, the subproblem in T's coordinates
       if (int rc = tri_tridiag(c, Bt, cnt, dim, 0, dim)) return rc;
-      if (int rc = tri_finish(c, Bt, cnt, dim, Delta, 1, tolhc, 0)) return rc;
-      if (int rc = tri_fallback_ids(c, Bt, cnt, sel + b0, fb_ids)) return rc;
+      const bool skip = per_instance && !getenv_is("RIPTRM_CG_SKIP", '0');
+      if (int rc = tri_finish(c, Bt, cnt, dim, Delta, 1, tolhc, 0, skip)) return rc;
+      if (int rc = tri_fallback_ids(c, Bt, cnt, sel + b0, fb_ids, skip)) return rc;
     } else if (per_instance && cg_one_workgroup(dim, cnt) && !getenv_is("RIPTRM_CG_SKIP", '0')) {
       // eigenpairs, g = Q^T a and the boundary candidate first; the CG then reads A from the
       // caller's array and is skipped where the eigenpairs prove the interior candidate cannot win
@@ -2223,6 +2301,36 @@ int riptrm_sym_eig(riptrm_ctx* ctx, int32_t dim, int32_t batch, double* A, int64
             dim, t[1] - t[0], t[6], t[7], t[2] - t[1], t[3] - t[2], t[5] - t[4], t[5] - t[0]);
   }
   return RIPTRM_OK;
+}
+
+int riptrm_sym_tridiag(riptrm_ctx* ctx, int32_t dim, int32_t batch, const double* A, int64_t lda, int64_t a_stride,
+                       double* d, double* e, int64_t de_stride, int32_t* info) {
+  if (!ctx) return RIPTRM_E_ARG;
+  if (dim < 64 || dim > riptrm_tri::TRI_MAX || batch < 1 || !A || !d || !e || !info || lda < dim ||
+      a_stride < (int64_t)dim * lda || de_stride < dim)
+    return fail(ctx, RIPTRM_E_ARG, "sym_tridiag: need 64 <= dim <= " + std::to_string(riptrm_tri::TRI_MAX) +
+                                       ", batch >= 1, lda >= dim, a_stride >= dim * lda, de_stride >= dim");
+  HIPCHK(ctx, hipSetDevice(ctx->device));
+  const int64_t per = (int64_t)riptrm_eig::refl_doubles(dim);   // the reflectors + tau of one matrix
+  const size_t need = (size_t)per * batch * sizeof(double);
+  if (ctx->eig_scratch_bytes < need) {
+    if (ctx->eig_scratch) HIPCHK(ctx, hipFree(ctx->eig_scratch));
+    ctx->eig_scratch = nullptr;
+    ctx->eig_scratch_bytes = 0;
+    HIPCHK(ctx, hipMalloc(&ctx->eig_scratch, need));
+    ctx->eig_scratch_bytes = need;
+  }
+  riptrm_tri::TriArgs a{};
+  a.A0 = A;
+  a.a_stride = a_stride;
+  a.lda = lda;
+  a.d0 = d;
+  a.e0 = e;
+  a.de_stride = de_stride;
+  a.R0 = (double*)ctx->eig_scratch;
+  a.r_stride = per;
+  a.infos = info;
+  return tri_launch(ctx, a, batch, dim);
 }
 
 int riptrm_trs_skip_stats(riptrm_ctx* ctx, int64_t* checked, int64_t* skipped) {

@@ -495,6 +495,14 @@ class NonnegPCABatch:
         return {"ms_per_launch_tile": t.value, "ms_per_launch_super": u.value,
                 "kernel": "k_spass_sup" if k.value == 1 else "k_spass_sym"}
 
+    def trs_skip_stats(self):
+        """(Exact_RepMat subproblems whose CG went through the certified skip test, CGs skipped) since
+        the context was created (riptrm_trs_skip_stats; the tridiagonal path above order 199 counts
+        here, the eigen-coordinate path below does not)."""
+        a, b = ctypes.c_int64(0), ctypes.c_int64(0)
+        self.ctx.check(self.lib.riptrm_trs_skip_stats(self.ctx.h, ctypes.byref(a), ctypes.byref(b)), "riptrm_trs_skip_stats")
+        return int(a.value), int(b.value)
+
     def persistent_state(self) -> Dict[str, bool]:
         """riptrm_get_persistent: whether the bound shape runs k_persist on this device, and whether
         the current solve / tCG run uses it."""

@@ -83,6 +83,8 @@ SIGNATURES: Dict[str, tuple] = {
     "riptrm_trs_bind_cache": (c_int32, [c_void_p, c_void_p, ctypes.c_int64, c_int32, c_int32]),
     "riptrm_trs_cache_stats": (c_int32, [c_void_p, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64)]),
     "riptrm_trs_skip_stats": (c_int32, [c_void_p, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64)]),
+    "riptrm_sym_tridiag": (c_int32, [c_void_p, c_int32, c_int32, c_void_p, c_int64, c_int64, c_void_p, c_void_p,
+                                     c_int64, c_void_p]),
     "riptrm_sym_eig": (c_int32, [c_void_p, c_int32, c_int32, c_void_p, c_int64, c_int64, c_void_p, c_int64, c_void_p,
                                  c_int32]),
     "riptrm_trs_backend_status": (c_int32, [ctypes.c_char_p, c_int32]),

@@ -118,3 +118,24 @@ def sym_eig(A: torch.Tensor, vectors: bool = True) -> Tuple[torch.Tensor, torch.
     ctx.check(ctx.lib.riptrm_sym_eig(ctx.h, dim, B, p(V), dim, dim * dim, p(w), dim, p(info), 1 if vectors else 0),
               "riptrm_sym_eig")
     return w, (V if vectors else None), info
+
+
+def sym_tridiag(A: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+    """Batched tridiagonal reduction on the GPU (riptrm_sym_tridiag, csrc/riptrm_tri.h k_tridiag_dist: the
+    first stage of the Exact_RepMat HBM service above order 199; dsytd2 lower).  A: (batch, dim, dim)
+    symmetric float64 on one GPU, 64 <= dim <= 1024.  Returns (d (batch, dim), e (batch, dim) with
+    e[:, :dim - 1] the off-diagonal, info (batch,))."""
+    if not torch.cuda.is_available():
+        raise RuntimeError("sym_tridiag needs a ROCm GPU (gfx950); there is no CPU fallback")
+    if A.dim() != 3 or A.shape[1] != A.shape[2] or A.dtype != torch.float64 or not A.is_cuda:
+        raise ValueError("expected A (batch, dim, dim) float64 on a GPU")
+    A = A.contiguous()
+    B, dim = A.shape[0], A.shape[1]
+    d = torch.empty((B, dim), dtype=torch.float64, device=A.device)
+    e = torch.zeros((B, dim), dtype=torch.float64, device=A.device)
+    info = torch.empty(B, dtype=torch.int32, device=A.device)
+    ctx = _context(A.device)
+    p = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    ctx.check(ctx.lib.riptrm_sym_tridiag(ctx.h, dim, B, p(A), dim, dim * dim, p(d), p(e), dim, p(info)),
+              "riptrm_sym_tridiag")
+    return d, e, info

@@ -626,6 +626,38 @@ def test_exact_repmat_above_lds_size_batched(monkeypatch, n):
     compare_until_flip(base.log(0), ref.log)
 
 
+@pytest.mark.timeout(600)
+def test_exact_repmat_tri_cg_skip_is_bitwise_neutral(monkeypatch):
+    """The tridiagonal path's certified CG skip (csrc/riptrm_tri.h k_tri_solve: from Sturm counts
+    either side of 0 and the LDL^T solve T ps = b with its residual, k_cg_wg's bounds show that no CG
+    iterate passing RIPTRM.py:246-251 can have p1obj <= xobj, RIPTRM.py:294-298) must not change a
+    bit: the bench's own n = 1000 workload (bench.py defaults, instances 0..3 from seed 20251212) with
+    the class defaults over K = 5 outer iterations, default vs RIPTRM_CG_SKIP=0 (every CG run to
+    SciPy's exit, 10 m iterations where it does not converge): same logs, x and y bit for bit, and
+    some CGs really skipped (the test is not vacuous)."""
+    import engine
+    n, B, K = 1000, 4, 5
+    opt = _gpu_opt(TRS_solver="Exact_RepMat", second_order_stationarity=True, maxiter=K)
+    runs = {}
+    for flag in (None, "0"):
+        if flag:
+            monkeypatch.setenv("RIPTRM_CG_SKIP", flag)
+        else:
+            monkeypatch.delenv("RIPTRM_CG_SKIP", raising=False)
+        e = engine.NonnegPCABatch(n, B)
+        x0, y0 = e.generate_synthetic(20251212, ids=list(range(B)))
+        runs[flag] = (e.solve(x0, y0, opt), e.trs_skip_stats())
+    (r1, (checked, skipped)), (r0, st0) = runs[None], runs["0"]
+    print(f"n = 1000: {checked} subproblems through the skip test, {skipped} CGs skipped")
+    assert st0 == (0, 0) and checked > 0 and skipped > 0, (checked, skipped, st0)
+    for b in range(B):
+        assert max(r1.log(b)["iteration"]) == K
+        for key in ("cost", "residual", "normdx", "dxtype", "mineigvalHw", "inner_status", "radius_update"):
+            assert r1.log(b)[key] == r0.log(b)[key], (b, key)
+    np.testing.assert_array_equal(r1.x.cpu().numpy(), r0.x.cpu().numpy())
+    np.testing.assert_array_equal(r1.y.cpu().numpy(), r0.y.cpu().numpy())
+
+
 @pytest.mark.timeout(900)
 def test_exact_repmat_configs1_size_drop_in(monkeypatch):
     """BASELINE configs[1] size (n = 1000) with the reference's class defaults (Exact_RepMat +

@@ -262,9 +262,9 @@ def test_si_exact_cg_skip_is_bitwise_neutral(d, sos, bench_starts, monkeypatch):
     r0 = e0.solve(xs, ys, opt)
     assert e0.trs_skip_stats() == (0, 0)
     print(f"d={d} sos={sos}: {checked} subproblems decided on their eigenpairs, {skipped} CGs skipped")
-    # manifold.dim 100 (d = 8) runs the one-workgroup CG, where the skip is decided; 392 (d = 16)
-    # the grid-wide CG, which always runs
-    assert (checked > 0) == (d == 8), checked
+    # manifold.dim 100 (d = 8) runs the one-workgroup CG, where the skip is decided on the
+    # eigenpairs; 392 (d = 16) the tridiagonal path, where k_tri_solve decides it on T
+    assert checked > 0, checked
     if bench_starts:
         assert skipped > 0
     for b in range(len(xs)):

@@ -223,6 +223,48 @@ def test_sym_eig_matches_lapack(m):
     np.testing.assert_array_equal(V3.cpu().numpy()[0], V[-1])
 
 
+@pytest.mark.parametrize("m", [64, 200, 257, 513, 1000])
+def test_sym_tridiag_matches_lapack(m):
+    """The distributed tridiagonal reduction (riptrm_sym_tridiag, csrc/riptrm_tri.h k_tridiag_dist: the
+    Exact_RepMat HBM service's first stage above order 199, one cooperative launch of ~m / 16..64
+    workgroups exchanging p = tau A v per column) against LAPACK dsytrd (lower: the same dsytd2
+    reflector convention, scipy.linalg.lapack.dsytrd).  Three matrices per batch (several matrices per
+    launch): random, frame-like (O(1) part plus diagonal barrier terms up to 1e6), clustered spectrum.
+    T's eigenvalues within 1e-13 ||A|| max(1, sqrt(m) / 4) of eigvalsh(A) (the reduction is backward
+    stable), and d, e within 1e-10 ||A|| of dsytrd's on the random matrix (two stable reductions of
+    one matrix; the frame-like and clustered ones are checked through the spectrum only); a matrix
+    reduced alone gives the same bits."""
+    import scipy.linalg as sl
+    from scipy.linalg import lapack
+    import trs
+    rs = np.random.RandomState(1000 + m)
+    M0 = rs.randn(m, m)
+    mats = [M0 + M0.T]
+    D = rs.randn(m, m) / np.sqrt(m)
+    mats.append(D + D.T + np.diag(np.where(rs.rand(m) < 0.3, 10.0 ** rs.uniform(2, 6, m), 0.0)))
+    mats.append(_clustered(m, rs, (1e-4, 1e-8, 1e-12)))
+    A = torch.tensor(np.stack(mats), dtype=torch.float64, device="cuda")
+    d, e, info = trs.sym_tridiag(A)
+    torch.cuda.synchronize()
+    d, e, info = d.cpu().numpy(), e.cpu().numpy(), info.cpu().numpy()
+    assert (info == 0).all(), info
+    for k, M in enumerate(mats):
+        nrm = np.linalg.norm(M, 2)
+        wt = sl.eigvalsh_tridiagonal(d[k], e[k][:m - 1])
+        ref = np.linalg.eigvalsh(M)
+        err = np.max(np.abs(wt - ref))
+        assert err <= 1e-13 * nrm * max(1.0, np.sqrt(m) / 4), (k, err / nrm)
+    _, dl, el, _, inf = lapack.dsytrd(mats[0], lower=1)
+    assert inf == 0
+    nrm = np.linalg.norm(mats[0], 2)
+    assert np.max(np.abs(d[0] - dl)) <= 1e-10 * nrm, np.max(np.abs(d[0] - dl)) / nrm
+    assert np.max(np.abs(e[0][:m - 1] - el)) <= 1e-10 * nrm, np.max(np.abs(e[0][:m - 1] - el)) / nrm
+    d1, e1, _ = trs.sym_tridiag(A[1:2].contiguous())
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(d1.cpu().numpy()[0], d[1])
+    np.testing.assert_array_equal(e1.cpu().numpy()[0], e[1])
+
+
 def _scipy_cg_decision(A, a, Del):
     """The reference's interior candidate (RIPTRM.py:243-248): SciPy's CG on A p = -a (rtol 1e-5, at
     most 10 m iterations) and its eligibility: (eligible, p1, relative true residual)."""

@@ -108,13 +108,14 @@ def test_layout_functions(built_lib):
 def test_exact_hbm_scratch_sizes(built_lib, monkeypatch):
     """Host-side sizing of the HBM Exact_RepMat path: the per-instance eigendecomposition cache
     (n^2 + 3 vpad(n) + 8 doubles per instance, vpad = n rounded up to 64, plus the compact
-    eigenvectors' reflectors: m (m + 1) / 2 rounded up to 8, m = min(n, 199)), the engine's all-or-none cache budget, and the SI
+    eigenvectors' or the tridiagonal path's reflectors: m (m + 1) / 2 rounded up to 8, m = n up to
+    order 1024, riptrm_tri.h TRI_MAX, else 199), the engine's all-or-none cache budget, and the SI
     workspace's extra regions once manifold.dim = d(d-1)/2 + d(d+1) exceeds RIPTRM_TRS_DIM_MAX
     (d >= 8: the subproblem matrix, coordinates, service outputs and resume records)."""
     import engine
     vpad = lambda n: -(-n // 64) * 64
-    for n, B in ((98, 1), (200, 64), (1000, 3)):
-        m = min(n, 199)
+    for n, B in ((98, 1), (200, 64), (1000, 3), (1025, 2)):
+        m = n if n <= 1024 else 199
         refl = -(-(m * (m + 1) // 2) // 8) * 8
         assert built_lib.riptrm_trs_cache_bytes(n, B) == (n * n + 3 * vpad(n) + 8 + refl) * 8 * B
     assert built_lib.riptrm_trs_cache_bytes(0, 4) == 0 and built_lib.riptrm_trs_cache_bytes(4, 0) == 0
