@@ -52,26 +52,30 @@ __host__ __device__ constexpr int tri_groups(int m) { return (m + 8 * tri_rw(m) 
 // granules per matrix: 2 parities x [{p, column}: m][arrivals: G]
 __host__ __device__ constexpr int64_t tri_par(int m) { return (int64_t)m + tri_groups(m); }
 __host__ __device__ constexpr int64_t tri_granules(int m) { return 2 * tri_par(m); }
+// byte offset of granule g: eight granules (one 128-byte line) every 128 << sp bytes (sp = 0: packed;
+// larger sp spreads the lines every workgroup polls over more memory channels)
+__host__ __device__ constexpr int64_t gran_off(int64_t g, int sp) { return ((g >> 3) << (7 + sp)) + ((g & 7) << 4); }
+__host__ __device__ constexpr int64_t tri_grid_bytes(int64_t granules, int sp) { return ((granules + 7) >> 3) << (7 + sp); }
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ unsigned tag_check(unsigned lo, unsigned hi, unsigned pass) {
   return lo ^ hi ^ (pass * 0x9E3779B9u);
 }
-__device__ __forceinline__ void st_gran(__amdgpu_buffer_rsrc_t rs, int64_t g, double v, unsigned pass) {
+__device__ __forceinline__ void st_gran(__amdgpu_buffer_rsrc_t rs, int64_t g, int sp, double v, unsigned pass) {
   const unsigned lo = (unsigned)__double2loint(v), hi = (unsigned)__double2hiint(v);
   const u32x4 q = {lo, hi, tag_check(lo, hi, pass), pass};
-  __builtin_amdgcn_raw_buffer_store_b128(q, rs, (int)(g * 16), 0, 16);   // aux 16: sc1 (write-through)
+  __builtin_amdgcn_raw_buffer_store_b128(q, rs, (int)gran_off(g, sp), 0, 16);   // aux 16: sc1 (write-through)
 }
 
 // the pair granule {a, b} of pass `pass`: both mantissas' last bits = the pass's tag bit, which
 // alternates between the passes sharing a parity (and is 1 on each parity's first pass: the grid
 // starts zeroed); a reader takes it when both bits match (a granule torn between passes mixes them)
 __device__ __forceinline__ unsigned pair_bit(unsigned pass) { return ((pass + 1) >> 1) & 1u; }
-__device__ __forceinline__ void st_pair(__amdgpu_buffer_rsrc_t rs, int64_t g, double a, double b, unsigned pass) {
+__device__ __forceinline__ void st_pair(__amdgpu_buffer_rsrc_t rs, int64_t g, int sp, double a, double b, unsigned pass) {
   const unsigned t = pair_bit(pass);
   const u32x4 q = {((unsigned)__double2loint(a) & ~1u) | t, (unsigned)__double2hiint(a),
                    ((unsigned)__double2loint(b) & ~1u) | t, (unsigned)__double2hiint(b)};
-  __builtin_amdgcn_raw_buffer_store_b128(q, rs, (int)(g * 16), 0, 16);   // aux 16: sc1 (write-through)
+  __builtin_amdgcn_raw_buffer_store_b128(q, rs, (int)gran_off(g, sp), 0, 16);   // aux 16: sc1 (write-through)
 }
 
 struct TriArgs {
@@ -87,6 +91,7 @@ struct TriArgs {
   int64_t grid_bytes;
   int m, G;
   int sleep;             // s_sleep 1 rounds between polls (RIPTRM_TRI_SLEEP; default 1)
+  int spread;            // gran_off's sp (RIPTRM_TRI_SPREAD)
   long long* hops;       // diagnostics (RIPTRM_TRI_STAMPS=2): matrix 0, every workgroup, steps i = 16 s: the
                          // wall clock (100 MHz, chip-wide) at [g][s][0] its gather's start, [1] its end
   long long* stamps;     // diagnostics (RIPTRM_TRI_STAMPS=1): workgroup 0 of matrix 0 accumulates clock64
@@ -136,7 +141,6 @@ __global__ void __launch_bounds__(TT) k_tridiag_dist(TriArgs a) {
   __shared__ double GP[EL * 64];        // gathered p (written by the gather, read by the column step)
   __shared__ double W[EL * 64];         // w = p + a2 v (column step -> every wave's update)
   __shared__ double C[EL * 64];         // gathered column (= row) i + 1 (column 0 of the input in the prologue)
-  __shared__ double CN[EL * 64];        // the column c of step i + 1 (column step -> every wave's update)
   __shared__ double red[2][8];          // the column step's per-wave partial sums
   // (a wave that finishes its rows early starts the next gather while others still read W, Vbuf: the
   // gather writes only GP and C, which nobody reads after the step's barrier)
@@ -153,6 +157,7 @@ __global__ void __launch_bounds__(TT) k_tridiag_dist(TriArgs a) {
   const bool writer = g == (m - 1) % G;   // owns row m - 1, active to the last step: writes d, e, H
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(a.grid, 0, (int)a.grid_bytes, 0x00020000);
   const int64_t gbase = (int64_t)ks * tri_granules(m);
+  const int gsp = a.spread;
   const int64_t par = tri_par(m);
 
   // own rows into registers (unconditional loads of clamped addresses)
@@ -210,10 +215,10 @@ __global__ void __launch_bounds__(TT) k_tridiag_dist(TriArgs a) {
 #pragma unroll
         for (int q = 0; q < EL; ++q) acc += (lane + 64 * q >= 1) ? Ar[s][q] * vq[q] : 0.0;
         const double p = tau_c * riptrm_wave::wave_sum(acc);
-        if (lane == 1) st_pair(rs, pb + l, p, Ar[s][0], 1u);
+        if (lane == 1) st_pair(rs, pb + l, gsp, p, Ar[s][0], 1u);
       }
     }
-    if (tid == 0) st_gran(rs, pb + m + g, 0.0, 1u);
+    if (tid == 0) st_gran(rs, pb + m + g, gsp, 0.0, 1u);
   }
 
   constexpr int NG = (64 * EL + 64 + TT - 1) / TT;   // granules polled per thread (upper bound)
@@ -250,7 +255,7 @@ __global__ void __launch_bounds__(TT) k_tridiag_dist(TriArgs a) {
         u32x4 qv[NG];
 #pragma unroll
         for (int u = 0; u < NG; ++u)
-          if (pend & (1 << u)) qv[u] = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(gi[u] * 16), 0, 16);
+          if (pend & (1 << u)) qv[u] = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)gran_off(gi[u], gsp), 0, 16);
 #pragma unroll
         for (int u = 0; u < NG; ++u)
           if (pend & (1 << u)) {
@@ -292,7 +297,7 @@ __global__ void __launch_bounds__(TT) k_tridiag_dist(TriArgs a) {
     // this workgroup has read pass i + 1: the parity of pass i + 2 (= pass i's) may be reused
     const int64_t pn = gbase + (int64_t)((pass + 1) & 1) * par;
     const bool more = i + 1 <= m - 2;
-    if (tid == 0 && more) st_gran(rs, pn + m + g, 0.0, pass + 1);
+    if (tid == 0 && more) st_gran(rs, pn + m + g, gsp, 0.0, pass + 1);
     // The column step, spread over the eight waves (wave w owns the columns j = lane + 64 q, q = w + 8 t):
     // w = p + a2 v with a2 = -tau (p . v) / 2, the column i + 1 of the updated matrix, its reflector.
     // Two block sums (p . v, its wave partials made in the gather, and the reflector's sum of squares:
@@ -326,10 +331,7 @@ __global__ void __launch_bounds__(TT) k_tridiag_dist(TriArgs a) {
       const bool on = q < EL;
       const double wj = (on && j > i && j < m) ? gq[t] + a2 * vq[t] : 0.0;
       cn[t] = (on && j > i + 1 && j < m) ? cq[t] - (vq[t] * wi1 + wj * vi1) : 0.0;   // row j's update at column i + 1
-      if (on) {
-        W[j] = wj;
-        CN[j] = cn[t];
-      }
+      if (on) W[j] = wj;
       sn += j >= i + 3 ? cn[t] * cn[t] : 0.0;
     }
     sn = riptrm_wave::wave_sum(sn);
@@ -340,11 +342,11 @@ __global__ void __launch_bounds__(TT) k_tridiag_dist(TriArgs a) {
 #pragma unroll
     for (int u = 0; u < 8; ++u) sn += red[1][u];
     if (writer && tid == 0) dv[i + 1] = cr1 - (vi1 * wi1 + wi1 * vi1);
-    double tau_n = 0.0, scl = 0.0;
+    double tau_n = 0.0;
     if (more) {
       // dlarfg on c[i+2 .. m): alpha = c[i+2] by its update formula (every thread)
       const double alpha = cr2 - (vc2 * wi1 + (gp2 + a2 * vc2) * vi1);
-      double beta = alpha;
+      double beta = alpha, scl = 0.0;
       if (sn != 0.0) {
         beta = -copysign(sqrt(alpha * alpha + sn), alpha);
         tau_n = (beta - alpha) / beta;
@@ -371,8 +373,10 @@ __global__ void __launch_bounds__(TT) k_tridiag_dist(TriArgs a) {
         sc += q3s - q2s;
       }
     }
-    // (no barrier: the update below takes v_{i+1} = c scl from CN and the scalars every thread holds;
-    // Vn is next step's v, read after its gather's barrier)
+    // (v_{i+1} complete in LDS before the update's dot products.  Taking it as c scl from a copy of c
+    // instead, without this barrier, was slower: OUT=r6tri13, 14.4k vs 13.2k cycles per step -- the
+    // waves then publish and start polling at spread times)
+    bar_lds();
     if (stp) {
       const long long t1 = clock64();
       acc1 += t1 - tq;
@@ -381,7 +385,7 @@ __global__ void __launch_bounds__(TT) k_tridiag_dist(TriArgs a) {
     if (!more) break;
     // rank-two update of own rows l >= i + 2 (row i + 1 is finished: its diagonal is d_{i+1}), fused
     // with p^(i+1)_l = tau_{i+1} A'_l. v_{i+1}; publish pass i + 2
-    // (v, w, c read from LDS per row: held in registers beside the rows they spill)
+    // (v, w, v_{i+1} read from LDS per row: held in registers beside the rows they spill)
 #pragma unroll
     for (int s = 0; s < RW; ++s) {
       const int l = rowid[s];
@@ -393,7 +397,7 @@ __global__ void __launch_bounds__(TT) k_tridiag_dist(TriArgs a) {
           const int j = lane + 64 * q;
           const double x = Ar[s][q] - (vl * W[j] + wl * Vc[j]);
           Ar[s][q] = x;
-          acc += (j >= i + 2) ? x * (j == i + 2 ? 1.0 : CN[j] * scl) : 0.0;   // v_{i+1}[j], as Vn holds it
+          acc += (j >= i + 2) ? x * Vn[j] : 0.0;
         }
         const double p = tau_n * riptrm_wave::wave_sum(acc);
         // {p_l, A_{l, i+2}}: column i + 2 sits in lane (i + 2) mod 64, register (i + 2) / 64
@@ -401,7 +405,7 @@ __global__ void __launch_bounds__(TT) k_tridiag_dist(TriArgs a) {
         double ac = Ar[s][0];
 #pragma unroll
         for (int q = 1; q < EL; ++q) ac = q == qc ? Ar[s][q] : ac;
-        if (lane == ((i + 2) & 63)) st_pair(rs, pn + l, p, ac, pass + 1);
+        if (lane == ((i + 2) & 63)) st_pair(rs, pn + l, gsp, p, ac, pass + 1);
       }
     }
     tau_c = tau_n;
@@ -1323,68 +1327,106 @@ __global__ void __launch_bounds__(256) k_refl_gram(double* base, int64_t sd, int
 }
 
 // v <- H^T v (backward = 0: H_{m-2} ... H_0 v) or H v (backward = 1) for orders up to 1024 on one
-// 1024-thread workgroup (element j on thread j), RB reflections per round: the RB dot products (wave
-// trees, sixteen partials per value in a fixed order), wave 0 solves for c (lane a holds s_a and row a
-// of G; one broadcast per reflection), every thread subtracts its sum of c_a u_a[j].  The next block's
-// reflector entries are loaded during the current one.  G from k_refl_gram at goff.
-__global__ void __launch_bounds__(1024) k_refl_blk(double* base, int64_t sd, int k0, int m, int64_t r_off, int64_t goff,
-                                                   int64_t voff, int64_t ooff, int backward) {
-  __shared__ double part[16][RB];
+// 512-thread workgroup (elements j = t and t + 512 on thread t), RB reflections per round: the RB dot
+// products (one reduce-scatter per wave, eight partials per value in a fixed order), wave 0 solves for
+// c (lane a holds s_a, tau_a and row a of G; one readlane broadcast per reflection), every thread subtracts its sums of
+// c_a u_a[j].  The next round's reflector entries, Gram block and tau are loaded during the current
+// one (unconditional loads of clamped addresses, masked at use: a load under a condition made the
+// compiler wait for every outstanding load, the prefetch included, and 1024 threads left too few
+// registers to hold it: 5.8 us per round, OUT=r6tri15); thread t < RB^2 loads one Gram entry, the
+// next RB threads one tau each, staged through LDS at the round's barrier.
+constexpr int RBT = 512;
+__global__ void __launch_bounds__(RBT) k_refl_blk(double* base, int64_t sd, int k0, int m, int64_t r_off, int64_t goff,
+                                                  int64_t voff, int64_t ooff, int backward) {
+  constexpr int NW = RBT / 64;
+  __shared__ double part[NW][RB];
   __shared__ double cs[RB];
+  __shared__ double gl[RB * RB + RB];   // the round's Gram block, then its tau
   double* sb = base + (int64_t)(k0 + blockIdx.y) * sd;
   const double* R = sb + r_off;
   const double* Gall = sb + goff;
-  const int j = threadIdx.x, lane = j & 63, w = j >> 6;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int nt = riptrm_eig::refl_tau(m), nb = refl_blocks(m);
-  double v = j < m ? sb[voff + j] : 0.0;
-  double un[RB];
-  auto load = [&](int bi, double (&u)[RB]) {
-    const int b = backward ? nb - 1 - bi : bi;
+  double v[2];
 #pragma unroll
-    for (int a = 0; a < RB; ++a) u[a] = bi < nb ? refl_u(R, m, b * RB + a, j) : 0.0;
-  };
-  load(0, un);
-  for (int bi = 0; bi < nb; ++bi) {
-    const int b = backward ? nb - 1 - bi : bi, i0 = b * RB;
-    double u[RB];
+  for (int e = 0; e < 2; ++e) v[e] = t + RBT * e < m ? sb[voff + t + RBT * e] : 0.0;
+  double un[2][RB], gn;
+  unsigned okn[2];
+  bool gok;
+  auto load = [&](int bi) {
+    int b = backward ? nb - 1 - bi : bi;
+    b = b < 0 ? 0 : (b >= nb ? nb - 1 : b);
 #pragma unroll
-    for (int a = 0; a < RB; ++a) u[a] = un[a];
-    load(bi + 1, un);
+    for (int e = 0; e < 2; ++e) {
+      const int j = t + RBT * e;
+      okn[e] = 0;
 #pragma unroll
-    for (int a = 0; a < RB; ++a) {
-      const double t = riptrm_wave::wave_sum(u[a] * v);
-      if (lane == 0) part[w][a] = t;
+      for (int a = 0; a < RB; ++a) {
+        const int i = b * RB + a;
+        const bool live = bi < nb && i < m - 1 && j > i && j < m;
+        un[e][a] = R[live ? riptrm_eig::refl_col(m, i) - i - 1 + j : nt];
+        okn[e] |= (unsigned)live << a;
+      }
     }
+    const int ia = b * RB + (t - RB * RB);
+    const bool isg = t < RB * RB, ist = !isg && t < RB * RB + RB && ia < m - 1;
+    gok = bi < nb && (isg || ist);
+    gn = isg ? Gall[(int64_t)b * RB * RB + t] : R[ist ? nt + ia : nt];
+  };
+  load(0);
+  for (int bi = 0; bi < nb; ++bi) {
+    double u[2][RB];
+#pragma unroll
+    for (int e = 0; e < 2; ++e)
+#pragma unroll
+      for (int a = 0; a < RB; ++a) u[e][a] = (okn[e] >> a) & 1u ? un[e][a] : 0.0;
+    const double gc = gok ? gn : 0.0;
+    const int b = backward ? nb - 1 - bi : bi, i0 = b * RB;
+    (void)i0;
+    load(bi + 1);
+    {
+      static_assert(RB == 16, "k_refl_blk: one reduce-scatter of sixteen sums");
+      double pr[RB];
+#pragma unroll
+      for (int a = 0; a < RB; ++a) pr[a] = u[0][a] * v[0] + u[1][a] * v[1];
+      const double x = riptrm_wave::wave_sum16(pr);
+      if ((lane & 3) == 0) part[w][riptrm_wave::wave_sum16_index(lane)] = x;
+    }
+    if (t < RB * RB + RB) gl[t] = gc;
     __syncthreads();
     if (w == 0) {
       // lane a < RB: s_a, tau_a, G row a; the reflections in application order
       const int a = lane < RB ? lane : 0;
       double sa = 0.0;
 #pragma unroll
-      for (int q = 0; q < 16; ++q) sa += part[q][a];
-      const int ia = i0 + a;
-      const double ta = (lane < RB && ia < m - 1) ? R[nt + ia] : 0.0;
+      for (int q = 0; q < NW; ++q) sa += part[q][a];
+      const double ta = lane < RB ? gl[RB * RB + a] : 0.0;
       double g[RB];
 #pragma unroll
-      for (int c = 0; c < RB; ++c) g[c] = Gall[(int64_t)b * RB * RB + a * RB + c];
+      for (int c = 0; c < RB; ++c) g[c] = gl[a * RB + c];
       double cmine = 0.0;
 #pragma unroll
-      for (int t = 0; t < RB; ++t) {
-        const int at = backward ? RB - 1 - t : t;   // (static per unrolled step and direction)
+      for (int s = 0; s < RB; ++s) {
+        const int at = backward ? RB - 1 - s : s;   // (static per unrolled step and direction)
         const double cl = ta * sa;                   // c of lane at, once lane at's s is final
-        const double c = __shfl(cl, at);
+        const double c = riptrm_wave::read_lane(cl, at);
         if (lane == at) cmine = c;
-        sa -= (backward ? g[RB - 1 - t] : g[t]) * c;
+        sa -= (backward ? g[RB - 1 - s] : g[s]) * c;
       }
       if (lane < RB) cs[lane] = cmine;
     }
     __syncthreads();
-    double dv = 0.0;
 #pragma unroll
-    for (int a = 0; a < RB; ++a) dv += cs[a] * u[a];
-    v -= dv;
+    for (int e = 0; e < 2; ++e) {
+      double dv = 0.0;
+#pragma unroll
+      for (int a = 0; a < RB; ++a) dv += cs[a] * u[e][a];
+      v[e] -= dv;
+    }
   }
-  if (j < m) sb[ooff + j] = v;
+#pragma unroll
+  for (int e = 0; e < 2; ++e)
+    if (t + RBT * e < m) sb[ooff + t + RBT * e] = v[e];
 }
 
 }  // namespace riptrm_tri

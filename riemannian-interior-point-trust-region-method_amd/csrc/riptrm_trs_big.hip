@@ -1661,7 +1661,10 @@ static int tri_launch_el(riptrm_ctx* c, riptrm_tri::TriArgs a, int cnt, int m) {
   const int64_t cap = (int64_t)nb * c->ncu;
   if (nb < 1 || cap < G) return fail(c, RIPTRM_E_HIP, "tridiagonalisation: " + std::to_string(G) + " workgroups per matrix do not fit");
   const int per = (int)std::min<int64_t>(cnt, cap / G);   // matrices per cooperative launch
-  const size_t gbytes = (size_t)riptrm_tri::tri_granules(m) * 16 * per;
+  const char* spe = getenv("RIPTRM_TRI_SPREAD");   // granule lines every 128 << sp bytes (A/B)
+  a.spread = spe ? std::min(std::max(atoi(spe), 0), 8) : 0;
+  const size_t gbytes = (size_t)riptrm_tri::tri_grid_bytes(riptrm_tri::tri_granules(m) * per, a.spread);
+  if (gbytes >= (size_t)INT32_MAX) return fail(c, RIPTRM_E_HIP, "tridiagonalisation: granule grid above 2 GiB");
   if (c->tri_grid_bytes < gbytes) {
     if (c->tri_grid) HIPCHK(c, hipFree(c->tri_grid));
     c->tri_grid = nullptr;
@@ -1689,7 +1692,8 @@ static int tri_launch_el(riptrm_ctx* c, riptrm_tri::TriArgs a, int cnt, int m) {
   }
   for (int k0 = 0; k0 < cnt; k0 += per) {
     const int nk = std::min(per, cnt - k0);
-    HIPCHK(c, hipMemsetAsync(c->tri_grid, 0, (size_t)riptrm_tri::tri_granules(m) * 16 * nk, c->stream));
+    HIPCHK(c, hipMemsetAsync(c->tri_grid, 0, (size_t)riptrm_tri::tri_grid_bytes(riptrm_tri::tri_granules(m) * nk, a.spread),
+                             c->stream));
     a.k0 = k0;
     a.grid = c->tri_grid;
     a.grid_bytes = (int64_t)c->tri_grid_bytes;
@@ -1771,14 +1775,14 @@ static int tri_tridiag(riptrm_ctx* c, const Bat& B, int cnt, int m, int64_t aoff
   return tri_launch(c, a, cnt, m);
 }
 
-// v <- H^T v / H v for the pass's slots (the tridiagonal path's reflectors): one 1024-thread workgroup per
+// v <- H^T v / H v for the pass's slots (the tridiagonal path's reflectors): one 512-thread workgroup per
 // slot, 16 reflections per round (k_refl_blk; the rounds' Gram blocks from k_refl_gram in the slot's
 // matrix area, dead once T is formed: tri_finish makes them); RIPTRM_TRI_REFL=s one reflection per
 // round (k_refl_wg), =w one wave with the vector in registers (k_refl_big) (A/B)
 static int tri_refl(riptrm_ctx* c, const Bat& B, int cnt, int m, int64_t voff, int64_t ooff, int backward) {
   const dim3 grid(1, cnt);
   if (!getenv_is("RIPTRM_TRI_REFL", 'w') && !getenv_is("RIPTRM_TRI_REFL", 's')) {
-    hipLaunchKernelGGL(riptrm_tri::k_refl_blk, grid, dim3(1024), 0, c->stream, B.base, B.sd, 0, m, off_refl(B.N),
+    hipLaunchKernelGGL(riptrm_tri::k_refl_blk, grid, dim3(riptrm_tri::RBT), 0, c->stream, B.base, B.sd, 0, m, off_refl(B.N),
                        (int64_t)0, voff, ooff, backward);
     HIPCHK(c, hipGetLastError());
     return RIPTRM_OK;

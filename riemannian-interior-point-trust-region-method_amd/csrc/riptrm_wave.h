@@ -60,4 +60,46 @@ __device__ __forceinline__ double wave_sum(double v) { return wave_reduce<0>(v);
 __device__ __forceinline__ double wave_min(double v) { return wave_reduce<1>(v); }
 __device__ __forceinline__ double wave_max(double v) { return wave_reduce<2>(v); }
 
+// The wave sums of 16 values at once (reduce-scatter): every level pairs lanes by an involution that
+// flips one lane bit (permlane32 / permlane16 swaps, row mirror, half-row mirror), each lane keeps the
+// half of its values selected by that bit and adds the partner's copy of that half (the partner sends
+// the half it does not keep); then the last two bits (quad DPP) complete the single remaining value.
+// Lane L returns the wave's sum of v[idx], idx = 8 b5 + 4 b4 + 2 b3 + b2 (b = the bits of L); the four
+// lanes sharing bits 5..2 hold bitwise the same sum.  30 half-exchanges instead of 16 x 6 for sixteen
+// wave_sum calls.
+__device__ __forceinline__ double wave_sum16(const double (&v)[16]) {
+  const unsigned lane = __lane_id();
+  const bool b5 = lane & 32, b4 = lane & 16, b3 = lane & 8, b2 = lane & 4;
+  double x8[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    double h0, h1;
+    pair32(b5 ? v[k] : v[k + 8], h0, h1);   // the half the partner keeps
+    x8[k] = (b5 ? v[k + 8] : v[k]) + (b5 ? h0 : h1);
+  }
+  double x4[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    double ev, od;
+    pair16(b4 ? x8[k] : x8[k + 4], ev, od);
+    x4[k] = (b4 ? x8[k + 4] : x8[k]) + (b4 ? ev : od);
+  }
+  double x2[2];
+#pragma unroll
+  for (int k = 0; k < 2; ++k) x2[k] = (b3 ? x4[k + 2] : x4[k]) + dpp<DPP_MIRROR>(b3 ? x4[k] : x4[k + 2]);
+  double x = (b2 ? x2[1] : x2[0]) + dpp<DPP_HALF_MIRROR>(b2 ? x2[0] : x2[1]);
+  x = x + dpp<DPP_XOR2>(x);
+  return x + dpp<DPP_XOR1>(x);
+}
+__host__ __device__ constexpr int wave_sum16_index(int lane) {
+  return ((lane >> 5) & 1) * 8 + ((lane >> 4) & 1) * 4 + ((lane >> 3) & 1) * 2 + ((lane >> 2) & 1);
+}
+
+// v from lane l (uniform l): two readlanes, no LDS
+__device__ __forceinline__ double read_lane(double v, int l) {
+  const int lo = __builtin_amdgcn_readlane(__double2loint(v), l);
+  const int hi = __builtin_amdgcn_readlane(__double2hiint(v), l);
+  return __hiloint2double(hi, lo);
+}
+
 }  // namespace riptrm_wave
