@@ -594,6 +594,145 @@ __device__ __forceinline__ double extreme_eig(const lds_t* d, const lds_t* e2, i
   return 0.5 * (lo + hi);
 }
 
+// (T + lam I) y = r on ONE wave by partitioned elimination: lane k owns rows kL .. kL + L - 1 (L = EL;
+// rows past m padded as decoupled unit rows), its first L - 1 rows interior, the last a separator.
+// Each lane factors its interior block (LDL^T, pivots in registers) and solves it for the right-hand
+// side (z) and for the couplings to the separator before (u) and its own (w); the separators' 64 x 64
+// tridiagonal Schur complement is solved by lane 0 (Thomas); interiors x = z - u x_prev - w x_sep.
+// A symmetric reordering of the LDL^T the serial ldl_newton runs (stable for T + lam I positive
+// definite, what the secular Newton keeps); for an indefinite T (the CG skip test at lam = 0) a tiny
+// pivot shows up as a large residual, which that test checks.  u, w live in LDS (UT, WT: element i of
+// lane k at i 64 + k, bank-conflict free), the Schur complement's rows and factors in RS[7][64].
+template <int L>
+struct PartSolve {
+  double rpv[L - 1], lo[L - 1];   // interior pivots' reciprocals and L multipliers
+  double a_s, o_l2, o_l1;         // separator diagonal (+ lam), e at rows L - 2 and L - 1
+  lds_t *UT, *WT, *RS;
+  int lane, base, m;
+  // RS rows: 0 Lc, 1 D, 2 Uc, 3 rhs, 4 denom, 5 c', 6 x
+  __device__ __forceinline__ void factor(const lds_t* d, const lds_t* e, int m_, double lam, lds_t* ut, lds_t* wt, lds_t* rs,
+                                         int lane_) {
+    UT = ut;
+    WT = wt;
+    RS = rs;
+    lane = lane_;
+    m = m_;
+    base = lane * L;
+    double a[L], o[L];
+#pragma unroll
+    for (int i = 0; i < L; ++i) {
+      const int j = base + i;
+      a[i] = j < m ? d[j] + lam : 1.0;
+      o[i] = j < m - 1 ? e[j] : 0.0;
+    }
+    const double eprev = (base > 0 && base - 1 < m - 1) ? e[base - 1] : 0.0;
+    a_s = a[L - 1];
+    o_l2 = o[L - 2];
+    o_l1 = o[L - 1];
+    double pv = a[0];
+#pragma unroll
+    for (int i = 1; i < L - 1; ++i) {
+      rpv[i - 1] = riptrm_eig::rcp_nr(pv);
+      lo[i - 1] = o[i - 1] * rpv[i - 1];
+      pv = a[i] - lo[i - 1] * o[i - 1];
+    }
+    rpv[L - 2] = riptrm_eig::rcp_nr(pv);
+    const double* rp = rpv;
+    // u: right-hand side eprev at interior row 0
+    double g = eprev, gu[L - 1];
+    gu[0] = g;
+#pragma unroll
+    for (int i = 1; i < L - 1; ++i) gu[i] = -lo[i - 1] * gu[i - 1];
+    double u = gu[L - 2] * rp[L - 2];
+    UT[(L - 2) * 64 + lane] = u;
+    const double u_last = u;
+#pragma unroll
+    for (int i = L - 3; i >= 0; --i) {
+      u = gu[i] * rp[i] - lo[i] * u;
+      UT[i * 64 + lane] = u;
+    }
+    const double u_first = u;
+    // w: right-hand side o[L - 2] at interior row L - 2
+    double w = o_l2 * rp[L - 2];
+    WT[(L - 2) * 64 + lane] = w;
+    const double w_last = w;
+#pragma unroll
+    for (int i = L - 3; i >= 0; --i) {
+      w = -lo[i] * w;
+      WT[i * 64 + lane] = w;
+    }
+    const double w_first = w;
+    // the separators' Schur complement: row k couples x_{s_{k-1}} (Lc), x_{s_k} (D), x_{s_{k+1}} (Uc)
+    const double u_nx = __shfl(u_first, lane < 63 ? lane + 1 : 63), w_nx = __shfl(w_first, lane < 63 ? lane + 1 : 63);
+    RS[0 * 64 + lane] = -o_l2 * u_last;
+    RS[1 * 64 + lane] = (a_s - o_l2 * w_last) - (lane < 63 ? o_l1 * u_nx : 0.0);
+    RS[2 * 64 + lane] = lane < 63 ? -o_l1 * w_nx : 0.0;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (lane == 0) {   // Thomas factors: 1 / denom_k, c'_k
+      double cp = 0.0;
+#pragma unroll 8
+      for (int k = 0; k < 64; ++k) {
+        const double rden = riptrm_eig::rcp_nr(RS[1 * 64 + k] - (k > 0 ? RS[0 * 64 + k] * cp : 0.0));
+        cp = RS[2 * 64 + k] * rden;
+        RS[4 * 64 + k] = rden;
+        RS[5 * 64 + k] = cp;
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
+  // y = (T + lam I)^-1 r into y (natural order); returns the wave's sum of y_j * q_j over j < m
+  // (q = y when q is null: ||y||^2)
+  __device__ __forceinline__ double solve(const lds_t* r, lds_t* y, const lds_t* q) {
+    double rr[L];
+#pragma unroll
+    for (int i = 0; i < L; ++i) rr[i] = base + i < m ? r[base + i] : 0.0;
+    double gz[L - 1];
+    gz[0] = rr[0];
+#pragma unroll
+    for (int i = 1; i < L - 1; ++i) gz[i] = rr[i] - lo[i - 1] * gz[i - 1];
+    double z[L - 1];
+    z[L - 2] = gz[L - 2] * rpv[L - 2];
+#pragma unroll
+    for (int i = L - 3; i >= 0; --i) z[i] = gz[i] * rpv[i] - lo[i] * z[i + 1];
+    const double z_nx = __shfl(z[0], lane < 63 ? lane + 1 : 63);
+    RS[3 * 64 + lane] = (rr[L - 1] - o_l2 * z[L - 2]) - (lane < 63 ? o_l1 * z_nx : 0.0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (lane == 0) {
+      double yp = 0.0;
+#pragma unroll 8
+      for (int k = 0; k < 64; ++k) {
+        yp = (RS[3 * 64 + k] - (k > 0 ? RS[0 * 64 + k] * yp : 0.0)) * RS[4 * 64 + k];
+        RS[6 * 64 + k] = yp;
+      }
+      double x = RS[6 * 64 + 63];
+#pragma unroll 8
+      for (int k = 62; k >= 0; --k) {
+        x = RS[6 * 64 + k] - RS[5 * 64 + k] * x;
+        RS[6 * 64 + k] = x;
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    const double xs = RS[6 * 64 + lane], xp = lane > 0 ? RS[6 * 64 + lane - 1] : 0.0;
+    double acc = 0.0;
+#pragma unroll
+    for (int i = 0; i < L - 1; ++i) {
+      const double x = (z[i] - UT[i * 64 + lane] * xp) - WT[i * 64 + lane] * xs;
+      const int j = base + i;
+      if (j < m) {
+        const double qv = q ? q[j] : x;
+        y[j] = x;
+        acc += x * qv;
+      }
+    }
+    if (base + L - 1 < m) {
+      const double qv = q ? q[base + L - 1] : xs;
+      y[base + L - 1] = xs;
+      acc += xs * qv;
+    }
+    return riptrm_wave::wave_sum(acc);
+  }
+};
+
 // One Newton step's solves of the secular equation, by one thread: (T + lam I) = L D L^T (no pivoting:
 // positive definite for lam > -lam_min), y = (T + lam I)^-1 b and, with second, t = (T + lam I)^-1 y;
 // returns s2 = y . y (and s3 = y . t).  The pivots come from the leading minors P_j = (d_j + lam)
@@ -715,13 +854,43 @@ __device__ __forceinline__ void ldl_newton(const lds_t* d, const lds_t* e, const
 // an eigenvalue within delta of lt), restructured for one thread's latency: every pass loads four
 // steps' operands ahead, the pivots' reciprocals come off the chains (the pass that needs D+ ratios
 // reads them from DP, the last pass is one multiply per step), no divisions.  DP: scratch (D+).
-__device__ __forceinline__ void twisted_min(lds_t* Z, lds_t* DP, const lds_t* d, const lds_t* e, int m, double lt,
-                                            double delta, double pivmin) {
+// split: T has some e_j = 0 (j < m - 1).  Without one the block is the whole T and the forward pass is
+// the D+ chain alone (the block search's two Sturm counts, and its per-step branches, only matter
+// between splits): one dependent chain per step instead of three.
+__device__ __forceinline__ void twisted_min(lds_t* Z, lds_t* DP, const lds_t* d, const lds_t* e, const lds_t* e2, int m,
+                                            double lt, double delta, double pivmin, bool split) {
   using riptrm_eig::rcp_nr;
   const double xa = lt - delta, xb = lt + delta;
   int blo = 0, bhi = m - 1, bs = 0, ca = 0, cb = 0;
   bool found = false;
   double qa = 0.0, qb = 0.0, dp = 0.0;
+  if (!split) {
+    dp = d[0] - lt;
+    if (fabs(dp) < pivmin) dp = -pivmin;
+    DP[0] = dp;
+    int j = 1;
+    for (; j + 4 <= m; j += 4) {
+      const double d0 = d[j], d1 = d[j + 1], d2 = d[j + 2], d3 = d[j + 3];
+      const double f0 = e2[j - 1], f1 = e2[j], f2 = e2[j + 1], f3 = e2[j + 2];
+      dp = (d0 - lt) - f0 * rcp_nr(dp);
+      if (fabs(dp) < pivmin) dp = -pivmin;
+      DP[j] = dp;
+      dp = (d1 - lt) - f1 * rcp_nr(dp);
+      if (fabs(dp) < pivmin) dp = -pivmin;
+      DP[j + 1] = dp;
+      dp = (d2 - lt) - f2 * rcp_nr(dp);
+      if (fabs(dp) < pivmin) dp = -pivmin;
+      DP[j + 2] = dp;
+      dp = (d3 - lt) - f3 * rcp_nr(dp);
+      if (fabs(dp) < pivmin) dp = -pivmin;
+      DP[j + 3] = dp;
+    }
+    for (; j < m; ++j) {
+      dp = (d[j] - lt) - e2[j - 1] * rcp_nr(dp);
+      if (fabs(dp) < pivmin) dp = -pivmin;
+      DP[j] = dp;
+    }
+  }
   // forward: the Sturm counts at lt -+ delta (the block) and D+ (restarting at every split)
   auto fstep = [&](int j, double dj, double ejm, double ej) {
     const bool start = j == bs;
@@ -745,16 +914,18 @@ __device__ __forceinline__ void twisted_min(lds_t* Z, lds_t* DP, const lds_t* d,
       bs = j + 1;
     }
   };
-  int j = 0;
-  for (; j + 4 <= m; j += 4) {
-    const double d0 = d[j], d1 = d[j + 1], d2 = d[j + 2], d3 = d[j + 3];
-    const double em = j > 0 ? e[j - 1] : 0.0, e0 = e[j], e1 = e[j + 1], e2v = e[j + 2], e3 = j + 3 < m - 1 ? e[j + 3] : 0.0;
-    fstep(j, d0, em, e0);
-    fstep(j + 1, d1, e0, e1);
-    fstep(j + 2, d2, e1, e2v);
-    fstep(j + 3, d3, e2v, e3);
+  if (split) {
+    int j = 0;
+    for (; j + 4 <= m; j += 4) {
+      const double d0 = d[j], d1 = d[j + 1], d2 = d[j + 2], d3 = d[j + 3];
+      const double em = j > 0 ? e[j - 1] : 0.0, e0 = e[j], e1 = e[j + 1], e2v = e[j + 2], e3 = j + 3 < m - 1 ? e[j + 3] : 0.0;
+      fstep(j, d0, em, e0);
+      fstep(j + 1, d1, e0, e1);
+      fstep(j + 2, d2, e1, e2v);
+      fstep(j + 3, d3, e2v, e3);
+    }
+    for (; j < m; ++j) fstep(j, d[j], j > 0 ? e[j - 1] : 0.0, j < m - 1 ? e[j] : 0.0);
   }
-  for (; j < m; ++j) fstep(j, d[j], j > 0 ? e[j - 1] : 0.0, j < m - 1 ? e[j] : 0.0);
   // backward over the block: D- and gamma_j = D+_j + D-_j - (d_j - lt) (gamma_bhi = D+_bhi); Z[j] =
   // e_{j-1} / D-_j for the solve above the twist
   double dm = d[bhi] - lt;
@@ -767,10 +938,9 @@ __device__ __forceinline__ void twisted_min(lds_t* Z, lds_t* DP, const lds_t* d,
     dm = dil - (ei * ei) * rcp_nr(dm);
     if (fabs(dm) < pivmin) dm = -pivmin;
     const double g = fabs(dpi + dm - dil);
-    if (g < best) {
-      best = g;
-      r = i;
-    }
+    const bool better = g < best;
+    best = better ? g : best;
+    r = better ? i : r;
     Z[i] = eim * rcp_nr(dm);
   };
   int i = bhi - 1;
@@ -820,7 +990,7 @@ __global__ void __launch_bounds__(256) k_tri_solve(double* base, int64_t sd, int
                                                    int64_t e_off, int64_t boff, int64_t aoff_vec, int64_t peoff,
                                                    int64_t cgxoff, int64_t evoff, int64_t scoff, TriSc S,
                                                    const double* Dg, int64_t dstride, const int32_t* ids, double tolhc,
-                                                   int mode, int cg_skip, long long* stamps) {
+                                                   int mode, int cg_skip, int eig_known, int serial, long long* stamps) {
   // stamps (diagnostics, RIPTRM_TRI_STAMPS=1; slot 0): clock64 at [0] start, [1] extreme eigenvalues,
   // [2] hard-case test done (wave 2), [3] the Newton done (wave 0), [4] the CG done or skipped (wave 1),
   // [5] end, [6] Newton steps, [7] CG iterations, [8] the skip test done (wave 1), [9] 1: CG skipped
@@ -846,6 +1016,7 @@ __global__ void __launch_bounds__(256) k_tri_solve(double* base, int64_t sd, int
   // ||T^-1 b||, b . T^-1 b, its residual
   __shared__ double xs[13];
   __shared__ int ic[128];   // the skip test's Sturm counts
+  __shared__ double rs0[7 * 64], rs1[7 * 64];   // PartSolve's Schur complements (Newton, skip test)
   const int k = blockIdx.y;
   double* sb = base + (int64_t)k * sd;
   double* sc = sb + scoff;
@@ -883,13 +1054,15 @@ __global__ void __launch_bounds__(256) k_tri_solve(double* base, int64_t sd, int
   __syncthreads();
   tn0 = fmax(fmax(red[0], red[1]), fmax(red[2], red[3]));
   __syncthreads();
+  int sp0 = 0;
   for (int j = tid; j < V; j += 256) {
     double ej = e[j];
     if (j < m - 1 && fabs(ej) <= 4.0 * eps * tn0) ej = 0.0;
     e[j] = ej;
     e2[j] = ej * ej;
+    sp0 |= j < m - 1 && ej == 0.0;
   }
-  __syncthreads();
+  const bool split = __syncthreads_or(sp0);
   double glo = INFINITY, ghi = -INFINITY, tnorm = 0.0, emax2 = 0.0;
   for (int j = tid; j < m; j += 256) {
     const double r0 = j > 0 ? fabs(e[j - 1]) : 0.0, r1 = j < m - 1 ? fabs(e[j]) : 0.0;
@@ -916,9 +1089,10 @@ __global__ void __launch_bounds__(256) k_tri_solve(double* base, int64_t sd, int
   __syncthreads();
   const double pivmin = DBL_MIN * fmax(1.0, emax2);
   const double fudge = 2.0 * eps * tnorm + 2.0 * pivmin;
-  // lam_min (wave 0) and lam_max (wave 1)
+  // lam_min (wave 0) and lam_max (wave 1), or (eig_known, mode 0) the ones a mode-1 pass over the same
+  // T left at evoff[0], evoff[1] (the eigendecomposition cache hands them on with T: same bits)
   if (w < 2) {
-    const double lx = extreme_eig(d, e2, m, w == 1, glo, ghi, fudge, tnorm, lane);
+    const double lx = (eig_known && mode == 0) ? sb[evoff + w] : extreme_eig(d, e2, m, w == 1, glo, ghi, fudge, tnorm, lane);
     if (lane == 0) xs[w] = lx;
   }
   __syncthreads();
@@ -928,6 +1102,7 @@ __global__ void __launch_bounds__(256) k_tri_solve(double* base, int64_t sd, int
   if (mode == 1) {
     if (tid == 0) {
       sb[evoff] = lmin;
+      sb[evoff + 1] = lmaxv;
       sc[S.mineig] = lmin;
       infos[k] = 0;
     }
@@ -954,8 +1129,41 @@ __global__ void __launch_bounds__(256) k_tri_solve(double* base, int64_t sd, int
   __syncthreads();
   const double lmx = fmax(fabs(lmin), fabs(lmaxv));
   if (w == 0) {
-    // the secular Newton of k_secular: ||(T + l1 I)^-1 b|| = Delta from l1 = -lam_min + ||b|| / Delta
-    if (lane == 0) {
+    // the secular Newton of k_secular: ||(T + l1 I)^-1 b|| = Delta from l1 = -lam_min + ||b|| / Delta;
+    // the solves by the whole wave (PartSolve), or by lane 0 alone (ldl_newton; serial = 1, A/B)
+    if (!serial) {
+      const double lo = -lmin;
+      double l1 = lo + gn / Delta, bl = lo, br = INFINITY;
+      int itn = 0;
+      PartSolve<EL> ps;
+      for (; itn < 100; ++itn) {   // (uniform: every lane holds the same sums)
+        ps.factor(d, e, m, l1, lf, rd, (lds_t*)rs0, lane);
+        const double s2 = ps.solve(b, y, nullptr);
+        const double s3 = ps.solve(y, t2, y);
+        const double xn = sqrt(s2);
+        const double f = 1.0 / xn - 1.0 / Delta;
+        const double fp = s3 / (xn * xn * xn);
+        if (fabs(f) * Delta <= 4.0 * eps) break;
+        if (f > 0.0) br = fmin(br, l1);
+        else bl = fmax(bl, l1);
+        double nl = l1 - f / fp;
+        if (nl <= bl) nl = 0.5 * (bl + l1);
+        const double tol = 1e-15 * fmax(1.0, fabs(l1));
+        if (fabs(nl - l1) <= tol || br - bl <= tol) {
+          l1 = nl;
+          break;
+        }
+        l1 = nl;
+      }
+      ps.factor(d, e, m, l1, lf, rd, (lds_t*)rs0, lane);
+      const double s2 = ps.solve(b, y, nullptr);
+      if (lane == 0) {
+        xs[4] = l1;
+        xs[7] = (double)itn;
+        xs[9] = -Delta / sqrt(s2);
+        if (stp) stp[6] = itn;
+      }
+    } else if (lane == 0) {
       // The iterates bracket the root: f > 0 right of it, f < 0 left (bl starts at the pole -lam_min).
       // A step to or below bl bisects towards it (k_secular bisects towards the pole: the same
       // sequence while no iterate has landed left of the root); a step past br is taken (bisecting
@@ -1015,9 +1223,15 @@ __global__ void __launch_bounds__(256) k_tri_solve(double* base, int64_t sd, int
     const double x = w == 1 ? (lane == 63 ? 0.0 : -lmx * exp2(-7.0 * (62 - lane) / 16.0)) : lmx * exp2(-7.0 * lane / 16.0);
     const int cnt = (cg_skip && lmx > 0.0) ? sturm_count_df(d, e2, m, x) : 0;
     ic[w == 1 ? lane : 64 + lane] = cnt;
-    if (w == 1 && cg_skip && lane == 0) {
-      double s2, s3;
-      ldl_newton(d, e, e2, m, 0.0, b, pz, nullptr, lz, rz, false, s2, s3);
+    if (w == 1 && cg_skip) {
+      if (!serial) {
+        PartSolve<EL> ps;
+        ps.factor(d, e, m, 0.0, lz, rz, (lds_t*)rs1, lane);
+        (void)ps.solve(b, pz, nullptr);
+      } else if (lane == 0) {
+        double s2, s3;
+        ldl_newton(d, e, e2, m, 0.0, b, pz, nullptr, lz, rz, false, s2, s3);
+      }
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     if (w == 1 && cg_skip) {   // the residual T ps - b and b . ps (ps = T^-1 b, p* = -ps)
@@ -1044,7 +1258,7 @@ __global__ void __launch_bounds__(256) k_tri_solve(double* base, int64_t sd, int
     const double hard_tol = 1e-12 * fmax(1.0, lmx);
     if (lane == 0) {
       xs[2] = (double)sturm_count_df(d, e2, m, lmin + hard_tol);
-      twisted_min(z, cx, d, e, m, lmin, 16.0 * eps * tnorm, pivmin);   // (cx: the CG's, free until the barrier)
+      twisted_min(z, cx, d, e, e2, m, lmin, 16.0 * eps * tnorm, pivmin, split);   // (cx: the CG's, free until the barrier)
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // lane 0's vector -> the wave
     double zb = 0.0, zz = 0.0;

@@ -1646,9 +1646,13 @@ static int compact_trs(riptrm_ctx* c, const Bat& B, int cnt, int m, int64_t aoff
 
 // ---- the tridiagonal path (riptrm_tri.h): orders above the one-workgroup eigensolver ------------------
 // RIPTRM_BIG_EIG unset (or 'h'): orders TRI_MIN .. TRI_MAX take it; otherwise rocSOLVER (A/B)
+// the tridiagonal path from order TRI_MIN (RIPTRM_TRI_MIN=k: from k >= 64 in the NonnegPCA service, A/B;
+// riptrm_trs_gep and the StableIdentification service keep the compact eigensolver up to 199)
 static bool tri_mode(int m) {
   const char* e = getenv("RIPTRM_BIG_EIG");
-  return m >= riptrm_tri::TRI_MIN && m <= riptrm_tri::TRI_MAX && !(e && e[0] != 'h');
+  const char* t = getenv("RIPTRM_TRI_MIN");
+  const int lo = t ? std::min(std::max(atoi(t), 64), riptrm_tri::TRI_MIN) : riptrm_tri::TRI_MIN;
+  return m >= lo && m <= riptrm_tri::TRI_MAX && !(e && e[0] != 'h');
 }
 
 template <int EL>
@@ -1804,7 +1808,7 @@ static int tri_refl(riptrm_ctx* c, const Bat& B, int cnt, int m, int64_t voff, i
 
 template <int EL>
 static int tri_solve_el(riptrm_ctx* c, const Bat& B, int cnt, int m, const double* D, int64_t dstride, double tolhc, int mode,
-                        bool cg_skip) {
+                        bool cg_skip, bool eig_known) {
   const int64_t N = B.N;
   const size_t shm = (size_t)riptrm_tri::TRI_SOLVE_ARRAYS * 64 * EL * sizeof(double);
   auto kern = riptrm_tri::k_tri_solve<EL>;
@@ -1818,7 +1822,8 @@ static int tri_solve_el(riptrm_ctx* c, const Bat& B, int cnt, int m, const doubl
   }
   hipLaunchKernelGGL(kern, dim3(1, cnt), dim3(256), shm, c->stream, B.base, B.sd, B.infos, m, off_vec(N, VS_R),
                      off_vec(N, VS_P), off_vec(N, VS_G), off_vec(N, VS_A), off_vec(N, VS_PE), off_vec(N, VS_CGX),
-                     off_vec(N, VS_EV), off_sc(N), S, D, dstride, B.ids, tolhc, mode, cg_skip ? 1 : 0, stamps);
+                     off_vec(N, VS_EV), off_sc(N), S, D, dstride, B.ids, tolhc, mode, cg_skip ? 1 : 0, eig_known ? 1 : 0,
+                     getenv_is("RIPTRM_TRI_SERIAL", '1') ? 1 : 0, stamps);
   HIPCHK(c, hipGetLastError());
   if (stamps) {
     long long h[10];
@@ -1841,7 +1846,7 @@ static int tri_solve_el(riptrm_ctx* c, const Bat& B, int cnt, int m, const doubl
 // the subproblem min x^T A x / 2 + a^T x, ||x|| <= Delta (a at VS_A): b = H^T a, k_tri_solve, x = H pe
 // -> VS_X and the result scalars.  Subproblems it cannot serve set SC_TRI_FB (tri_fallback_ids).
 static int tri_finish(riptrm_ctx* c, const Bat& B, int cnt, int m, const double* D, int64_t dstride, double tolhc, int mode,
-                      bool cg_skip = false) {
+                      bool cg_skip = false, bool eig_known = false) {
   const int64_t N = B.N;
   if (mode == 0) {
     hipLaunchKernelGGL(riptrm_tri::k_refl_gram, dim3(riptrm_tri::refl_blocks(m), cnt), dim3(256), 0, c->stream, B.base,
@@ -1851,9 +1856,9 @@ static int tri_finish(riptrm_ctx* c, const Bat& B, int cnt, int m, const double*
   }
   int rc;
   switch (riptrm_tri::tri_el(m)) {
-    case 4: rc = tri_solve_el<4>(c, B, cnt, m, D, dstride, tolhc, mode, cg_skip); break;
-    case 8: rc = tri_solve_el<8>(c, B, cnt, m, D, dstride, tolhc, mode, cg_skip); break;
-    default: rc = tri_solve_el<16>(c, B, cnt, m, D, dstride, tolhc, mode, cg_skip); break;
+    case 4: rc = tri_solve_el<4>(c, B, cnt, m, D, dstride, tolhc, mode, cg_skip, eig_known); break;
+    case 8: rc = tri_solve_el<8>(c, B, cnt, m, D, dstride, tolhc, mode, cg_skip, eig_known); break;
+    default: rc = tri_solve_el<16>(c, B, cnt, m, D, dstride, tolhc, mode, cg_skip, eig_known); break;
   }
   if (rc) return rc;
   if (mode == 0) return tri_refl(c, B, cnt, m, off_vec(N, VS_PE), off_vec(N, VS_X), 1);
@@ -1992,7 +1997,8 @@ int riptrm_big_service(riptrm_ctx* c, int* served) {
         else if (int rc = tri_tridiag(c, Bt, cnt, n - 1, aoff, n))
           return rc;
         const bool skip = !getenv_is("RIPTRM_CG_SKIP", '0');
-        if (int rc = tri_finish(c, Bt, cnt, n - 1, P.st + ST_DELTA, ST_N, P.opt.trs_tolhardcase, 0, skip)) return rc;
+        // (a cache hit's T comes with the extreme eigenvalues its trial pass found: kind 1)
+        if (int rc = tri_finish(c, Bt, cnt, n - 1, P.st + ST_DELTA, ST_N, P.opt.trs_tolhardcase, 0, skip, kind == 1)) return rc;
         hipLaunchKernelGGL(k_finish_dir, dim3(1, cnt), dim3(WG), 0, c->stream, P, Bt);
         std::vector<int32_t> fbi;
         if (int rc = tri_fallback_ids(c, Bt, cnt, L.data() + k0, fbi, skip)) return rc;
