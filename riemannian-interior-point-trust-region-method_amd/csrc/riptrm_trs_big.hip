@@ -1658,8 +1658,12 @@ static bool tri_mode(int m) {
 template <int EL>
 static int tri_launch_el(riptrm_ctx* c, riptrm_tri::TriArgs a, int cnt, int m) {
   constexpr int RW = 32 / EL;
-  const int G = riptrm_tri::tri_groups(m);
+  int G = riptrm_tri::tri_groups(m);
   auto kern = riptrm_tri::k_tridiag_dist<EL, RW>;
+  if (EL == 16 && getenv_is("RIPTRM_TRI_RW", '4')) {   // twice the rows per wave, half the workgroups (A/B;
+    kern = riptrm_tri::k_tridiag_dist<16, 4>;          // the granule layout's per-parity room covers it)
+    G = (m + 31) / 32;
+  }
   int nb = 0;
   HIPCHK(c, hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kern, riptrm_tri::TT, 0));
   const int64_t cap = (int64_t)nb * c->ncu;
