@@ -596,12 +596,13 @@ def main():
                               "kernel": "k_state (tCG step, Sphere projection / retraction, trial point, acceptance; "
                                         "runs beside the other stream group's S-pass)"}
         spass_roofline = None
-        if args.trs == "Exact_RepMat" and 96 < n - 1 <= 199 and rank == 0:
+        tri_lo, tri_hi = engine.C["RIPTRM_TRS_TRI_MIN"], engine.C["RIPTRM_TRS_TRI_MAX"]
+        if args.trs == "Exact_RepMat" and 96 < n - 1 < tri_lo and rank == 0:
             # the eigensolver, not the S-pass, sets this line's time: price it, keep the S-pass in detail
             spass_roofline, roofline = roofline, eig_roofline(n - 1, B, dev)
-        elif args.trs == "Exact_RepMat" and 199 < n - 1 <= 1024 and rank == 0:
+        elif args.trs == "Exact_RepMat" and tri_lo <= n - 1 <= tri_hi and rank == 0:
             # the tridiagonal path's subproblem service (riptrm_tri.h) sets this line's time
-            spass_roofline, roofline = roofline, tri_roofline(n - 1, dev)
+            spass_roofline, roofline = roofline, tri_roofline(n - 1, dev, min(B, 64))
         cpu = None
         if args.cpu_budget > 0 and world == 1:
             positions = window_positions(W, K, args.cycle)
@@ -664,8 +665,8 @@ def main():
                        **({"exact_repmat_note": (
                            "manifold.dim > 96: the subproblems are served in batched passes between lock-step "
                            "chunks (csrc/riptrm_trs_big.hip); the pass, not the S-pass (detail.spass_roofline), sets "
-                           "this line's time: up to order 199 the hand-written eigensolver (csrc/riptrm_eig.h) with the "
-                           "CG in its eigen-coordinates; 200..1024 the cooperative tridiagonalisation and the subproblem "
+                           "this line's time: up to order 149 the hand-written eigensolver (csrc/riptrm_eig.h) with the "
+                           "CG in its eigen-coordinates; 150..1024 the cooperative tridiagonalisation and the subproblem "
                            "in T's coordinates (csrc/riptrm_tri.h); a subproblem at an accepted trial point reuses that "
                            "point's eigenpairs / tridiagonal form (riptrm_trs_bind_cache)"),
                            "trs_cache": dict(zip(("hits", "subproblems"), eng.trs_cache_stats()))}
@@ -887,12 +888,13 @@ def si_cpu_pool(K: int, budget_s: float, procs: int, trs: str, d: int = 5, inner
                        f"rate x {procs}, evaluation time excluded as RIPTRM.py:932-941")}
 
 
-def tri_roofline(m: int, dev, reps: int = 5):
-    """The Exact_RepMat HBM service's dominant kernel above order 199, the cooperative tridiagonalisation
+def tri_roofline(m: int, dev, B: int = 1, reps: int = 5):
+    """The Exact_RepMat HBM service's dominant kernel from order 150 on, the cooperative tridiagonalisation
     (csrc/riptrm_tri.h k_tridiag_dist, ~m / 16 workgroups), timed live with HIP events on torch's current
-    stream (the library runs on it) around riptrm_sym_tridiag on one frame-like matrix (O(1) symmetric
-    part plus diagonal barrier terms up to 1e6): the reduction alone, as the service runs it per
-    subproblem and per trial point.  Bound: latency.  Its m - 1 columns are one all-to-all exchange each
+    stream (the library runs on it) around riptrm_sym_tridiag on B frame-like matrices (O(1) symmetric
+    part plus diagonal barrier terms up to 1e6; B = the line's batch, several matrices per cooperative
+    launch): the reduction alone, as the service runs it per pass of subproblems and of trial points.
+    Bound: latency.  Each matrix's m - 1 columns are one all-to-all exchange each
     (every workgroup publishes its rows' p = tau A v and polls every other's), a chain no bandwidth can
     shorten; the floor is m - 1 hand-offs at the measured single hop (MI355X_MICROARCH.md,
     handoff-1to1: ~1.0 us on an idle chip).  Its flops (4/3 m^3) at the FP64 vector peak are reported
@@ -901,12 +903,14 @@ def tri_roofline(m: int, dev, reps: int = 5):
     import torch
     import trs
     rs = np.random.RandomState(m)
-    D = rs.randn(m, m) / np.sqrt(m)
-    D = D + D.T + np.diag(np.where(rs.rand(m) < 0.3, 10.0 ** rs.uniform(2, 6, m), 0.0))
-    A = torch.tensor(D[None], dtype=torch.float64, device=dev)
+    mats = []
+    for _ in range(B):
+        D = rs.randn(m, m) / np.sqrt(m)
+        mats.append(D + D.T + np.diag(np.where(rs.rand(m) < 0.3, 10.0 ** rs.uniform(2, 6, m), 0.0)))
+    A = torch.tensor(np.stack(mats), dtype=torch.float64, device=dev)
     for _ in range(2):
         _, _, info = trs.sym_tridiag(A)
-    assert int(info[0]) == 0
+    assert int(info.abs().sum()) == 0
     ts = []
     for _ in range(reps):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -917,13 +921,13 @@ def tri_roofline(m: int, dev, reps: int = 5):
         ts.append(e0.elapsed_time(e1) / 1e3)
     t = sorted(ts)[len(ts) // 2]
     hop = 1.0e-6
-    ach = (m - 1) / t
+    ach = B * (m - 1) / t
     G = (m + 15) // 16 if m > 512 else (m + 31) // 32 if m > 256 else (m + 63) // 64
-    return {"bound": "latency", "achieved": ach, "peak": 1.0 / hop, "unit": "columns/s", "frac": ach / (1.0 / hop),
+    return {"bound": "latency", "achieved": ach, "peak": B / hop, "unit": "columns/s", "frac": ach / (B / hop),
             "traffic": None, "avg_launch_us": t * 1e6,
-            "kernel": (f"riptrm_tri::k_tridiag_dist on {G} cooperative workgroups: the tridiagonal reduction of one "
-                       f"order-{m} subproblem matrix through riptrm_sym_tridiag"),
-            "flops_frac": (4.0 / 3.0 * m ** 3 / t) / 81.7e12,
+            "kernel": (f"riptrm_tri::k_tridiag_dist on {G} cooperative workgroups per matrix: the tridiagonal reduction "
+                       f"of {B} order-{m} subproblem matrices through riptrm_sym_tridiag"),
+            "flops_frac": (B * 4.0 / 3.0 * m ** 3 / t) / 81.7e12,
             "why": ("latency-bound: one all-to-all exchange per tridiagonalisation column; floor = m - 1 hand-offs "
                     "at ~1.0 us (MI355X_MICROARCH.md handoff-1to1, idle chip)")}
 
@@ -934,7 +938,7 @@ CLOCK_HZ = 2.4e9              # max engine clock
 
 def eig_roofline(m: int, B: int, dev, reps: int = 5):
     """The Exact_RepMat HBM service's dominant kernel, the hand-written eigensolver (csrc/riptrm_eig.h,
-    manifold.dim <= 199), timed live with HIP events on the library's stream: B matrices of order m
+    manifold.dim 97..149), timed live with HIP events on the library's stream: B matrices of order m
     shaped like the frame matrices (O(1) symmetric part plus diagonal barrier terms up to 1e6),
     compact eigenpairs as the service takes them.  Bound: LDS of the CUs it occupies (one workgroup
     per matrix holds it in LDS for the tridiagonalisation, its dominant phase); algorithmic bytes =
@@ -1102,7 +1106,7 @@ def bench_si(args, world, rank, dev, dist):
                    "global_batch": B * world, "parallelism": f"instance-sharded x{world}", "world_size": world},
         "roofline": si_roofline(args, d, hvps, kern_s, sec, tot("PASSES")),
         # the HBM TRS service's eigensolver at this manifold.dim (the line's other half: DESIGN 7b)
-        **({"service_eig_roofline": eig_roofline(tdim, B, dev)} if args.trs != "tCG" and 96 < tdim <= 199 else {}),
+        **({"service_eig_roofline": eig_roofline(tdim, B, dev)} if args.trs != "tCG" and 96 < tdim < engine.C["RIPTRM_TRS_TRI_MIN"] else {}),
         "cpu_baseline": cpu,
         "detail": {"inner_iterations_per_s": inner / T, "tcg_iterations_per_s": tcg / T, "hvps_per_s": hvps / T,
                    "section_fraction": secfrac, "us_per_hvp_per_instance": sec["hvp"] / max(1.0, tot("PASSES")) * 1e6,

@@ -82,6 +82,11 @@ extern "C" {
  * riptrm_solve_advance, StableIdentification d >= 8 in riptrm_si_solve) keep the matrix in HBM
  * scratch bound with riptrm_trs_bind_workspace (below) */
 #define RIPTRM_TRS_DIM_MAX 96
+/* From this manifold.dim up to RIPTRM_TRS_TRI_MAX the HBM path reduces the matrix to tridiagonal form
+ * across the chip and solves the subproblem in its coordinates (no eigenvectors; csrc/riptrm_tri.h);
+ * below it the one-workgroup batched eigensolver (csrc/riptrm_eig.h) serves it */
+#define RIPTRM_TRS_TRI_MIN 150
+#define RIPTRM_TRS_TRI_MAX 1024
 
 /* inner_status codes (RIPTRM.py:763,770,678,698,829,837); 0 = None */
 #define RIPTRM_IS_NONE 0
@@ -394,8 +399,8 @@ int riptrm_si_solve(riptrm_ctx* ctx, const riptrm_options* opt, const double* x0
  * (RIPTRM_TRS_*).  mineig (may be NULL) = the smallest eigenvalue of A (RIPTRM.py:611).
  * dim <= RIPTRM_TRS_DIM_MAX: one workgroup per instance, A staged in LDS, asynchronous.
  * dim > RIPTRM_TRS_DIM_MAX: needs riptrm_trs_bind_workspace(order >= dim); up to `slots` subproblems
- * per pass on HBM-resident matrices (dim <= 199: the hand-written eigensolver and SciPy's CG restated in
- * its eigen-coordinates; 200 <= dim <= 1024: the cooperative tridiagonalisation T = H^T A H and the
+ * per pass on HBM-resident matrices (dim < RIPTRM_TRS_TRI_MIN: the hand-written eigensolver and SciPy's CG restated in
+ * its eigen-coordinates; RIPTRM_TRS_TRI_MIN <= dim <= 1024: the cooperative tridiagonalisation T = H^T A H and the
  * subproblem in T's coordinates, riptrm_tri.h; above, or for a hard case, rocSOLVER
  * dsyevd_strided_batched and SciPy's CG on A; the secular Newton per subproblem); synchronises.  A non-converged eigensolve fails the call
  * (RIPTRM_E_HIP naming the subproblem: scipy.linalg.eig raises there). */
@@ -407,8 +412,8 @@ int riptrm_trs_gep(riptrm_ctx* ctx, int32_t dim, int32_t batch, const double* A,
  * :599-617 and TRSgep :218-299 at any size): `slots` subproblems of matrix order `order` (NonnegPCA:
  * order = n, the n x n frame matrix; riptrm_trs_gep: order = dim).  Bytes for riptrm_trs_bind_workspace,
  * caller-owned device memory (256-byte aligned).  Each subproblem of a pass takes one slot; with
- * fewer slots than subproblems the pass repeats, with bitwise the same results.  Orders <= 199
- * take the hand-written eigensolver (riptrm_eig.h), 200..1024 the tridiagonal path (riptrm_tri.h, no
+ * fewer slots than subproblems the pass repeats, with bitwise the same results.  Orders <= 149
+ * take the hand-written eigensolver (riptrm_eig.h), 150..1024 the tridiagonal path (riptrm_tri.h, no
  * eigenvectors); rocSOLVER's dsyevd_strided_batched serves larger orders and the tridiagonal path's
  * hard cases, loaded at first use (dlopen of librocsolver.so.0; it manages its own workspace).  In a NonnegPCA solve an
  * instance that reaches the subproblem (or, with the second-order test, a trial point) parks;
@@ -424,8 +429,8 @@ int riptrm_trs_bind_workspace(riptrm_ctx* ctx, void* ws, int64_t bytes, int32_t 
 /* Eigendecomposition cache of the HBM path in a NonnegPCA solve with the second-order test
  * (RIPTRM.py:599-617 computes the trial point's eigenpairs; :686-692 keeps HwNewmatrix for the next
  * subproblem when the step was accepted without dual clipping).  One entry per instance (order >= n,
- * batch >= the bound batch): the trial point's eigenvectors / eigenvalues (orders <= 199) or its
- * tridiagonal form and reflectors (200..1024) keyed by its (x, y).  A
+ * batch >= the bound batch): the trial point's eigenvectors / eigenvalues (orders <= 149) or its
+ * tridiagonal form and reflectors (150..1024) keyed by its (x, y).  A
  * subproblem whose (x, y) equals its instance's key bitwise builds the same matrix bits, so it runs
  * CG and the secular step on the cached eigenpairs without an eigensolve: results are bitwise those
  * of the uncached solve.  Caller-owned device memory, riptrm_trs_cache_bytes(order, batch) bytes,
@@ -456,7 +461,7 @@ int riptrm_trs_skip_stats(riptrm_ctx* ctx, int64_t* checked, int64_t* skipped);
 int riptrm_sym_eig(riptrm_ctx* ctx, int32_t dim, int32_t batch, double* A, int64_t lda, int64_t a_stride, double* w,
                    int64_t w_stride, int32_t* info, int32_t vectors);
 
-/* The tridiagonal reduction the Exact_RepMat HBM service runs above order 199 (csrc/riptrm_tri.h
+/* The tridiagonal reduction the Exact_RepMat HBM service runs from order RIPTRM_TRS_TRI_MIN on (csrc/riptrm_tri.h
  * k_tridiag_dist: LAPACK dsytd2, lower, as scipy.linalg.lapack.dsytrd(lower=1) / the eigh inside
  * TRSgep's pencil, RIPTRM.py:251, would start; the matrix spread over one cooperative launch of
  * ~m / 16 workgroups, rows in registers, one all-to-all exchange per column).  batch matrices of order

@@ -9,9 +9,9 @@ eqLagmult)`` whose ``log`` has the reference's columns, one row per inner iterat
 * ``TRS_solver='tCG'`` (what every shipped config selects) and ``'Exact_RepMat'`` (the class
   default, with ``second_order_stationarity``) at any size: up to ``manifold.dim = 96`` the matrix
   of HwCur lives in LDS (csrc/riptrm_trs.h), beyond that in HBM (csrc/riptrm_trs_big.hip), with the
-  hand-written batched eigensolver (csrc/riptrm_eig.h) up to order 199, the hand-written
+  hand-written batched eigensolver (csrc/riptrm_eig.h) up to order 149, the hand-written
   distributed tridiagonalisation with the subproblem solved in T's coordinates (csrc/riptrm_tri.h)
-  for orders 200..1024, and rocSOLVER's dsyevd only for that path's hard cases and above 1024;
+  for orders 150..1024, and rocSOLVER's dsyevd only for that path's hard cases and above 1024;
 * the problem is a structured descriptor (``problems.NonnegPCAProblem`` or
   ``si.SIProblem`` for StableIdentification) instead of a list of autograd closures, because
   closures cannot execute on the GPU;

@@ -33,6 +33,7 @@
 #include <math.h>
 #include "riptrm_eig.h"
 #include "riptrm_wave.h"
+#include "../../include/riptrm.h"
 
 namespace riptrm_tri {
 
@@ -41,8 +42,10 @@ namespace riptrm_tri {
 using riptrm_eig::lds_t;
 
 constexpr int TT = 512;                          // threads per tridiagonalisation workgroup
-constexpr int TRI_MIN = riptrm_eig::EIG_LDS_MAX + 1;
-constexpr int TRI_MAX = 1024;                    // (EL = 32 for 2048 spilled the rows to scratch)
+constexpr int TRI_MIN = RIPTRM_TRS_TRI_MIN;      // (m = 199 x 64: 10.0k vs 7.7k outer it/s by the
+                                                 // eigensolver path, OUT=r6e200)
+constexpr int TRI_MAX = RIPTRM_TRS_TRI_MAX;      // (EL = 32 for 2048 spilled the rows to scratch)
+static_assert(TRI_MIN > 64 && TRI_MIN <= riptrm_eig::EIG_LDS_MAX + 1 && TRI_MAX == 1024, "riptrm_tri: orders");
 constexpr unsigned long long TRI_TIMEOUT = 200000000ull;   // 2 s of the 100 MHz wall clock
 
 // elements per lane (EL) and rows per wave (RW) of order m: 32 doubles of the matrix per lane

@@ -1646,12 +1646,12 @@ static int compact_trs(riptrm_ctx* c, const Bat& B, int cnt, int m, int64_t aoff
 
 // ---- the tridiagonal path (riptrm_tri.h): orders above the one-workgroup eigensolver ------------------
 // RIPTRM_BIG_EIG unset (or 'h'): orders TRI_MIN .. TRI_MAX take it; otherwise rocSOLVER (A/B)
-// the tridiagonal path from order TRI_MIN (RIPTRM_TRI_MIN=k: from k >= 64 in the NonnegPCA service, A/B;
-// riptrm_trs_gep and the StableIdentification service keep the compact eigensolver up to 199)
+// the tridiagonal path from order TRI_MIN = RIPTRM_TRS_TRI_MIN (RIPTRM_TRI_MIN=k: from k instead, 64 <= k
+// <= 200, A/B; 200 keeps the compact eigensolver at every order it serves)
 static bool tri_mode(int m) {
   const char* e = getenv("RIPTRM_BIG_EIG");
   const char* t = getenv("RIPTRM_TRI_MIN");
-  const int lo = t ? std::min(std::max(atoi(t), 64), riptrm_tri::TRI_MIN) : riptrm_tri::TRI_MIN;
+  const int lo = t ? std::min(std::max(atoi(t), 64), riptrm_eig::EIG_LDS_MAX + 1) : riptrm_tri::TRI_MIN;
   return m >= lo && m <= riptrm_tri::TRI_MAX && !(e && e[0] != 'h');
 }
 
@@ -2062,7 +2062,7 @@ int riptrm_big_reset_cache(riptrm_ctx* c) {
 // instances (riptrm_si.hip).
 static_assert(RIPTRM_EIG_COMPACT_MAX == riptrm_eig::EIG_LDS_MAX, "riptrm_ctx.h's copy of EIG_LDS_MAX");
 int64_t riptrm_big_kcache_doubles(int dim, int klen) { return kc_doubles(dim, klen); }
-bool riptrm_big_kcache_usable(int dim) { return eig_compact(dim); }
+bool riptrm_big_kcache_usable(int dim) { return eig_compact(dim) && !tri_mode(dim); }
 
 // the instances ids whose cache entry matches their key (hit) and the others (miss).  Synchronises.
 int riptrm_big_kcache_split(riptrm_ctx* c, int dim, const std::vector<int32_t>& ids, const KeyedEigCache& kc,
@@ -2096,7 +2096,7 @@ int riptrm_big_gep_ids(riptrm_ctx* c, int dim, const int32_t* sel, int count, co
   if (!c->big_ws || c->big_order < dim || c->big_slots < 1)
     return fail(c, RIPTRM_E_STATE, "Exact_RepMat above dim 96 needs riptrm_trs_bind_workspace (order >= dim)");
   const Bat Bt = bat_of(c);
-  const int kmode = (kc && kc->cache && eig_compact(dim)) ? kc->mode : 0;
+  const int kmode = (kc && kc->cache && eig_compact(dim) && !tri_mode(dim)) ? kc->mode : 0;
   if (kmode == 1 && mineig_only) return fail(c, RIPTRM_E_STATE, "gep_ids: cached eigenpairs serve subproblems only");
   std::vector<int32_t> info(c->big_slots);
   std::vector<double> skip_done;   // SC_DONE of the pass's slots (4 = CG skipped by k_cg_wg's bound)
@@ -2117,6 +2117,11 @@ int riptrm_big_gep_ids(riptrm_ctx* c, int dim, const int32_t* sel, int count, co
       if (kmode == 2)
         hipLaunchKernelGGL(k_kc_store, dim3(blocks_of((int64_t)dim * dim, 256), cnt), dim3(256), 0, c->stream, Bt, dim,
                            kc->keys, kc->kstride, kc->klen, kc->cache, kc->cstride);
+    } else if (tri_mode(dim)) {   // T = H^T A H across the chip, the subproblem in T's coordinates
+      if (int rc = tri_tridiag(c, Bt, cnt, dim, 0, dim)) return rc;
+      const bool skip = per_instance && !getenv_is("RIPTRM_CG_SKIP", '0');
+      if (int rc = tri_finish(c, Bt, cnt, dim, Delta, 1, tolhc, 0, skip)) return rc;
+      if (int rc = tri_fallback_ids(c, Bt, cnt, sel + b0, fb_ids, skip)) return rc;
     } else if (eig_compact(dim)) {
       // eigenpairs first (or the cached ones), then the CG in eigen-coordinates (k_cg_diag), skipped
       // where the certified bound shows its candidate cannot win (per_instance; RIPTRM_CG_SKIP=0: never)
@@ -2132,11 +2137,6 @@ int riptrm_big_gep_ids(riptrm_ctx* c, int dim, const int32_t* sel, int count, co
         HIPCHK(c, hipMemcpy2DAsync(skip_done.data(), sizeof(double), Bt.base + off_sc(Bt.N) + SC_DONE,
                                    (size_t)Bt.sd * sizeof(double), sizeof(double), cnt, hipMemcpyDeviceToHost, c->stream));
       }
-    } else if (tri_mode(dim)) {   // T = H^T A H across the chip, the subproblem in T's coordinates
-      if (int rc = tri_tridiag(c, Bt, cnt, dim, 0, dim)) return rc;
-      const bool skip = per_instance && !getenv_is("RIPTRM_CG_SKIP", '0');
-      if (int rc = tri_finish(c, Bt, cnt, dim, Delta, 1, tolhc, 0, skip)) return rc;
-      if (int rc = tri_fallback_ids(c, Bt, cnt, sel + b0, fb_ids, skip)) return rc;
     } else if (per_instance && cg_one_workgroup(dim, cnt) && !getenv_is("RIPTRM_CG_SKIP", '0')) {
       // eigenpairs, g = Q^T a and the boundary candidate first; the CG then reads A from the
       // caller's array and is skipped where the eigenpairs prove the interior candidate cannot win

@@ -497,7 +497,7 @@ class NonnegPCABatch:
 
     def trs_skip_stats(self):
         """(Exact_RepMat subproblems whose CG went through the certified skip test, CGs skipped) since
-        the context was created (riptrm_trs_skip_stats; the tridiagonal path above order 199 counts
+        the context was created (riptrm_trs_skip_stats; the tridiagonal path from order 150 on counts
         here, the eigen-coordinate path below does not)."""
         a, b = ctypes.c_int64(0), ctypes.c_int64(0)
         self.ctx.check(self.lib.riptrm_trs_skip_stats(self.ctx.h, ctypes.byref(a), ctypes.byref(b)), "riptrm_trs_skip_stats")

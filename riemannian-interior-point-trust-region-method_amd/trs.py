@@ -3,8 +3,8 @@
 ``TRSgep(A, a, B, Del, tolhardcase)`` keeps the reference's signature and return value
 (src/solver/RIPTRM.py:218-299: ``(x, lam1, type)``); ``trs_gep_batched`` solves a batch of
 subproblems held as torch tensors on the GPU (dim <= RIPTRM_TRS_DIM_MAX: one launch, the matrix in
-LDS; larger: the HBM path — up to dim 199 the hand-written eigensolver and SciPy's CG restated in its
-eigen-coordinates, 200..1024 the cooperative tridiagonalisation and the subproblem in T's coordinates,
+LDS; larger: the HBM path — up to dim 149 the hand-written eigensolver and SciPy's CG restated in its
+eigen-coordinates, 150..1024 the cooperative tridiagonalisation and the subproblem in T's coordinates,
 rocSOLVER dsyevd above and for hard cases; the secular Newton — every subproblem of the batch in one
 pass when the scratch budget allows).  Only B = I is supported — the one call site passes ``np.eye(xdim)``
 (RIPTRM.py:441).  No CPU fallback.
@@ -122,7 +122,7 @@ def sym_eig(A: torch.Tensor, vectors: bool = True) -> Tuple[torch.Tensor, torch.
 
 def sym_tridiag(A: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
     """Batched tridiagonal reduction on the GPU (riptrm_sym_tridiag, csrc/riptrm_tri.h k_tridiag_dist: the
-    first stage of the Exact_RepMat HBM service above order 199; dsytd2 lower).  A: (batch, dim, dim)
+    first stage of the Exact_RepMat HBM service from order 150 on; dsytd2 lower).  A: (batch, dim, dim)
     symmetric float64 on one GPU, 64 <= dim <= 1024.  Returns (d (batch, dim), e (batch, dim) with
     e[:, :dim - 1] the off-diagonal, info (batch,))."""
     if not torch.cuda.is_available():
