@@ -104,16 +104,16 @@ def test_trs_gep_reference_signature():
 
 
 @pytest.mark.timeout(600)
-@pytest.mark.parametrize("dim", [97, 200, 392, 999])
+@pytest.mark.parametrize("dim", [97, 149, 150, 200, 392, 999])
 def test_trs_gep_above_lds_size_matches_oracle(dim):
     """dim > RIPTRM_TRS_DIM_MAX: the HBM service (csrc/riptrm_trs_big.hip) against the reference's
     pencil (dims 97, 200, 392) and, at 999, the eigh formulation trs_oracle.trs_eigh (the pencil's QZ on
     1998 x 1998 takes ~90 s per case on the CPU; measured on these cases while choosing the bar:
-    trs_eigh vs pencil 5e-14 in x, 6e-14 in lam1 at 999, <= 2e-14 at 97 / 200).  Orders <= 199 take
+    trs_eigh vs pencil 5e-14 in x, 6e-14 in lam1 at 999, <= 2e-14 at 97 / 200).  Orders <= 149 take
     the hand-written eigensolver (riptrm_eig.h) and SciPy's CG in its eigen-coordinates (k_cg_diag);
-    orders 200 .. 1024 the distributed tridiagonalisation and the subproblem in T's coordinates
-    (riptrm_tri.h: Sturm bisection, secular Newton on LDL^T solves, the CG on T).  Same bar as the LDS
-    path."""
+    orders 150 .. 1024 (RIPTRM_TRS_TRI_MIN..) the distributed tridiagonalisation and the subproblem in
+    T's coordinates (riptrm_tri.h: Sturm bisection, secular Newton on partitioned LDL^T solves, the CG
+    on T); 149 / 150 are the two sides of that boundary.  Same bar as the LDS path."""
     from trs import KIND_NAMES
     cases = _cases(dim, 4, [dim])
     if dim == 999:
@@ -134,12 +134,31 @@ def test_trs_gep_above_lds_size_matches_oracle(dim):
         assert abs(mineig[b] - ev) <= 1e-11 * max(1.0, np.abs(A).max() * dim), (b, mineig[b], ev)
 
 
-@pytest.mark.parametrize("n", [150, 250])
+@pytest.mark.parametrize("dim", [200, 999])
+def test_tri_wave_solves_match_one_lane_solves(dim, monkeypatch):
+    """The tridiagonal path's subproblem solves on the whole wave (riptrm_tri.h PartSolve: 64 interior
+    blocks eliminated in parallel, the separators' Schur complement by Thomas) against the one-lane
+    LDL^T of the same T (RIPTRM_TRI_SERIAL=1): the same secular Newton and CG-skip decisions on
+    reorderings of one factorisation, so the same kinds and, to rounding, the same steps and
+    multipliers (x within 1e-10 relative, lam1 within 1e-11 relative)."""
+    cases = _cases(dim, 4, [dim])
+    monkeypatch.delenv("RIPTRM_TRI_SERIAL", raising=False)
+    xw, lw, kw, mw = _solve(cases)
+    monkeypatch.setenv("RIPTRM_TRI_SERIAL", "1")
+    xs, ls, ks, ms = _solve(cases)
+    np.testing.assert_array_equal(kw, ks)
+    np.testing.assert_array_equal(mw, ms)   # the extreme eigenvalues do not depend on the solves
+    for b in range(len(cases)):
+        assert np.linalg.norm(xw[b] - xs[b]) <= 1e-10 * np.linalg.norm(xs[b]), (b, np.linalg.norm(xw[b] - xs[b]))
+        assert abs(lw[b] - ls[b]) <= 1e-11 * max(1.0, abs(ls[b])), (b, lw[b], ls[b])
+
+
+@pytest.mark.parametrize("n", [120, 250])
 def test_trs_gep_hard_case_above_lds_size(n):
-    """The hard case (a orthogonal to lam_min's eigenvector): at 150 the eigen-coordinates of
+    """The hard case (a orthogonal to lam_min's eigenvector): at 120 the eigen-coordinates of
     riptrm_eig.h; at 250 the tridiagonal path detects it (riptrm_tri.h k_tri_solve: the component of
     H^T a on the twisted eigenvector of lam_min) and hands the subproblem to the eigendecomposition
-    path (rocSOLVER dsyevd), which solves it as at 150."""
+    path (rocSOLVER dsyevd), which solves it as at 120."""
     rs = np.random.RandomState(8)
     cases = []
     for _ in range(2):
