@@ -1106,7 +1106,7 @@ def bench_si(args, world, rank, dev, dist):
                    "global_batch": B * world, "parallelism": f"instance-sharded x{world}", "world_size": world},
         "roofline": si_roofline(args, d, hvps, kern_s, sec, tot("PASSES")),
         # the HBM TRS service's eigensolver at this manifold.dim (the line's other half: DESIGN 7b)
-        **({"service_eig_roofline": eig_roofline(tdim, B, dev)} if args.trs != "tCG" and 96 < tdim < engine.C["RIPTRM_TRS_TRI_MIN"] else {}),
+        **({"service_eig_roofline": eig_roofline(tdim, B, dev)} if args.trs != "tCG" and 96 < tdim < si.C["RIPTRM_TRS_TRI_MIN"] else {}),
         "cpu_baseline": cpu,
         "detail": {"inner_iterations_per_s": inner / T, "tcg_iterations_per_s": tcg / T, "hvps_per_s": hvps / T,
                    "section_fraction": secfrac, "us_per_hvp_per_instance": sec["hvp"] / max(1.0, tot("PASSES")) * 1e6,

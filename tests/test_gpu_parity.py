@@ -514,12 +514,12 @@ def test_exact_repmat_reference_defaults_drop_in(fixture_n50):
 
 
 @pytest.mark.timeout(600)
-@pytest.mark.parametrize("n", [200, 260])
+@pytest.mark.parametrize("n", [130, 200, 260])
 @pytest.mark.parametrize("sos", [True, False])
 def test_exact_repmat_above_lds_size_matches_oracle(sos, n):
-    """NonnegPCA n = 200 / 260 (manifold.dim 199 / 259) with Exact_RepMat: the HBM path (frame matrix
-    densified from S; at 199 the hand-written eigensolver and the CG in its eigen-coordinates, at 259
-    the distributed tridiagonalisation and the subproblem in T's coordinates, riptrm_tri.h; the
+    """NonnegPCA n = 130 / 200 / 260 (manifold.dim 129 / 199 / 259) with Exact_RepMat: the HBM path (frame
+    matrix densified from S; at 129 the hand-written eigensolver and the CG in its eigen-coordinates, from
+    150 on (RIPTRM_TRS_TRI_MIN) the distributed tridiagonalisation and the subproblem in T's coordinates, riptrm_tri.h; the
     trial-point eigenvalue with the second-order test) against the oracle (the reference's 2n x 2n
     pencil per inner step, trs_oracle.trs_gep; its per-constraint HVPs build the matrix), with the
     Exact_RepMat trajectory bar (parity.compare_until_flip)."""
@@ -563,10 +563,10 @@ def test_exact_repmat_lds_and_hbm_paths_agree_near_97(monkeypatch):
 
 
 @pytest.mark.timeout(600)
-@pytest.mark.parametrize("n", [200, 260])
+@pytest.mark.parametrize("n", [130, 260])
 def test_exact_repmat_above_lds_size_batched(monkeypatch, n):
     """The HBM Exact_RepMat service over a batch (csrc/riptrm_trs_big.hip: every parked instance in
-    one pass, one workspace slot each; n = 200 the batched hand-written eigensolver, n = 260 the
+    one pass, one workspace slot each; n = 130 the batched hand-written eigensolver, n = 260 the
     distributed tridiagonalisation, several matrices per cooperative launch): six instances with the
     second-order test.  Each instance's trajectory is the one it has solved alone (a slot's arithmetic does not
     depend on the pass it shares), whichever CG form serves it (one workgroup per slot or the

@@ -245,7 +245,7 @@ def test_sym_eig_matches_lapack(m):
 @pytest.mark.parametrize("m", [64, 200, 257, 513, 1000])
 def test_sym_tridiag_matches_lapack(m):
     """The distributed tridiagonal reduction (riptrm_sym_tridiag, csrc/riptrm_tri.h k_tridiag_dist: the
-    Exact_RepMat HBM service's first stage above order 199, one cooperative launch of ~m / 16..64
+    Exact_RepMat HBM service's first stage from order 150 on, one cooperative launch of ~m / 16..64
     workgroups exchanging p = tau A v per column) against LAPACK dsytrd (lower: the same dsytd2
     reflector convention, scipy.linalg.lapack.dsytrd).  Three matrices per batch (several matrices per
     launch): random, frame-like (O(1) part plus diagonal barrier terms up to 1e6), clustered spectrum.
