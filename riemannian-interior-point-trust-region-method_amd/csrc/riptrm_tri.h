@@ -1612,7 +1612,7 @@ __global__ void __launch_bounds__(RBT) k_refl_blk(double* base, int64_t sd, int 
       if ((lane & 3) == 0) part[w][riptrm_wave::wave_sum16_index(lane)] = x;
     }
     if (t < RB * RB + RB) gl[t] = gc;
-    __syncthreads();
+    bar_lds();   // (not __syncthreads(): its vmcnt(0) would wait for the next round's prefetch)
     if (w == 0) {
       // lane a < RB: s_a, tau_a, G row a; the reflections in application order
       const int a = lane < RB ? lane : 0;
@@ -1634,7 +1634,7 @@ __global__ void __launch_bounds__(RBT) k_refl_blk(double* base, int64_t sd, int 
       }
       if (lane < RB) cs[lane] = cmine;
     }
-    __syncthreads();
+    bar_lds();
 #pragma unroll
     for (int e = 0; e < 2; ++e) {
       double dv = 0.0;
