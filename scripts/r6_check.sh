@@ -13,3 +13,13 @@ grep -E "passed|failed" $O/tests.log | tail -2
 [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 $B --dim 200 --batch 64 --steps 4 --warmup 1 > $O/e200.json 2> $O/e200.err && v $O/e200.json &&
 timeout -k 10 300 $B --dim 1000 --batch 1 --steps 3 --warmup 1 > $O/e1000.json 2> $O/e1000.err && v $O/e1000.json
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/p1000 -o p -- python bench.py --trs Exact_RepMat \
+  --dim 1000 --batch 1 --steps 3 --warmup 1 --cpu-budget 0 --cpu-procs 0 > $O/e1000_prof.json 2> $O/e1000_prof.err
+[ -f $O/p1000/p_kernel_stats.csv ] || exit 1
+find $O -name "*kernel_trace.csv" -delete
+python - <<PY
+import csv
+rows=list(csv.DictReader(open("$O/p1000/p_kernel_stats.csv")))
+for r in rows[:8]:
+    print(f'  {r["Name"][:50]:50s} calls {r["Calls"]:>6s} avg_us {float(r["AverageNs"])/1e3:9.1f} pct {float(r["Percentage"]):5.1f}')
+PY
