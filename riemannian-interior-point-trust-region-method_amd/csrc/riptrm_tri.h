@@ -1556,7 +1556,9 @@ __global__ void __launch_bounds__(256) k_refl_gram(double* base, int64_t sd, int
 // next RB threads one tau each, staged through LDS at the round's barrier.
 constexpr int RBT = 512;
 __global__ void __launch_bounds__(RBT) k_refl_blk(double* base, int64_t sd, int k0, int m, int64_t r_off, int64_t goff,
-                                                  int64_t voff, int64_t ooff, int backward) {
+                                                  int64_t voff, int64_t ooff, int backward, long long* stamps) {
+  // stamps (RIPTRM_TRI_STAMPS=3, slot 0, thread 0): clock64 cycles summed over the rounds in [0] the
+  // operands' arrival + the dot products to the first barrier, [1] wave 0's solve to the second, [2] the update
   constexpr int NW = RBT / 64;
   __shared__ double part[NW][RB];
   __shared__ double cs[RB];
@@ -1593,6 +1595,8 @@ __global__ void __launch_bounds__(RBT) k_refl_blk(double* base, int64_t sd, int 
     gn = isg ? Gall[(int64_t)b * RB * RB + t] : R[ist ? nt + ia : nt];
   };
   load(0);
+  long long* stp = (stamps && blockIdx.y == 0 && threadIdx.x == 0) ? stamps : nullptr;
+  long long s0 = 0, s1 = 0, s2 = 0, tq = stp ? clock64() : 0;
   for (int bi = 0; bi < nb; ++bi) {
     double u[2][RB];
 #pragma unroll
@@ -1613,6 +1617,11 @@ __global__ void __launch_bounds__(RBT) k_refl_blk(double* base, int64_t sd, int 
     }
     if (t < RB * RB + RB) gl[t] = gc;
     bar_lds();   // (not __syncthreads(): its vmcnt(0) would wait for the next round's prefetch)
+    if (stp) {
+      const long long t1 = clock64();
+      s0 += t1 - tq;
+      tq = t1;
+    }
     if (w == 0) {
       // lane a < RB: s_a, tau_a, G row a; the reflections in application order
       const int a = lane < RB ? lane : 0;
@@ -1635,6 +1644,11 @@ __global__ void __launch_bounds__(RBT) k_refl_blk(double* base, int64_t sd, int 
       if (lane < RB) cs[lane] = cmine;
     }
     bar_lds();
+    if (stp) {
+      const long long t1 = clock64();
+      s1 += t1 - tq;
+      tq = t1;
+    }
 #pragma unroll
     for (int e = 0; e < 2; ++e) {
       double dv = 0.0;
@@ -1642,10 +1656,20 @@ __global__ void __launch_bounds__(RBT) k_refl_blk(double* base, int64_t sd, int 
       for (int a = 0; a < RB; ++a) dv += cs[a] * u[e][a];
       v[e] -= dv;
     }
+    if (stp) {
+      const long long t1 = clock64();
+      s2 += t1 - tq;
+      tq = t1;
+    }
   }
 #pragma unroll
   for (int e = 0; e < 2; ++e)
     if (t + RBT * e < m) sb[ooff + t + RBT * e] = v[e];
+  if (stp) {
+    stp[0] = s0;
+    stp[1] = s1;
+    stp[2] = s2;
+  }
 }
 
 }  // namespace riptrm_tri

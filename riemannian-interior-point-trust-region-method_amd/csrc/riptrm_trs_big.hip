@@ -1790,9 +1790,23 @@ static int tri_tridiag(riptrm_ctx* c, const Bat& B, int cnt, int m, int64_t aoff
 static int tri_refl(riptrm_ctx* c, const Bat& B, int cnt, int m, int64_t voff, int64_t ooff, int backward) {
   const dim3 grid(1, cnt);
   if (!getenv_is("RIPTRM_TRI_REFL", 'w') && !getenv_is("RIPTRM_TRI_REFL", 's')) {
+    long long* stamps = nullptr;   // RIPTRM_TRI_STAMPS=3: slot 0's phase cycles on stderr
+    if (getenv_is("RIPTRM_TRI_STAMPS", '3')) {
+      HIPCHK(c, hipMalloc(&stamps, 4 * sizeof(long long)));
+      HIPCHK(c, hipMemsetAsync(stamps, 0, 4 * sizeof(long long), c->stream));
+    }
     hipLaunchKernelGGL(riptrm_tri::k_refl_blk, grid, dim3(riptrm_tri::RBT), 0, c->stream, B.base, B.sd, 0, m, off_refl(B.N),
-                       (int64_t)0, voff, ooff, backward);
+                       (int64_t)0, voff, ooff, backward, stamps);
     HIPCHK(c, hipGetLastError());
+    if (stamps) {
+      long long h[4];
+      HIPCHK(c, hipMemcpyAsync(h, stamps, sizeof(h), hipMemcpyDeviceToHost, c->stream));
+      HIPCHK(c, hipStreamSynchronize(c->stream));
+      (void)hipFree(stamps);
+      const int nb = riptrm_tri::refl_blocks(m);
+      fprintf(stderr, "[refl stamps] m=%d rounds=%d per round: operands + dots %.0f, solve %.0f, update %.0f cycles\n", m, nb,
+              h[0] / (double)nb, h[1] / (double)nb, h[2] / (double)nb);
+    }
     return RIPTRM_OK;
   }
   if (getenv_is("RIPTRM_TRI_REFL", 's')) {
