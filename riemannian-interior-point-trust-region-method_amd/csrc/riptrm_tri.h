@@ -1489,11 +1489,13 @@ __global__ void __launch_bounds__(1024) k_refl_wg(double* base, int64_t sd, int 
   if (j < m) sb[ooff + j] = v;
 }
 
-// ---- blocked reflector application --------------------------------------------------------------
-// RB consecutive reflections in one round: with s_a = u_a . v (v at the block's start), G_ab = u_a . u_b
-// and c_a = tau_a (s_a - sum over the block's earlier reflections b of G_ab c_b), the block maps v to
-// v - sum_a c_a u_a (the reflections' exact composition; the sums in another order).  G depends on the
-// reflectors only: k_refl_gram forms it once per tridiagonalisation, for both applications.
+// ---- blocked reflector application ----------------------------------------------------------------
+// RB consecutive reflections H_a = I - tau_a u_a u_a^T (a = 0 .. RB - 1) compose to H_0 ... H_{RB-1} =
+// I - U T U^T with T upper triangular (the compact WY form, LAPACK dlarft's forward columnwise recurrence:
+// T_aa = tau_a, T_{0:a, a} = -tau_a T_{0:a, 0:a} G_{0:a, a}, G_ab = u_a . u_b).  Applied first-to-last
+// (v <- H_{RB-1} ... H_0 v) the block maps v to v - U T^T s, last-to-first to v - U T s, s = U^T v: the
+// reflections' exact composition, the sums in another order.  T depends on the reflectors only:
+// k_refl_gram forms the blocks' T once per tridiagonalisation, for both applications.
 constexpr int RB = 16;
 __host__ __device__ constexpr int refl_blocks(int m) { return (m - 1 + RB - 1) / RB; }
 __host__ __device__ constexpr int64_t refl_gram_doubles(int m) { return (int64_t)refl_blocks(m) * RB * RB; }
@@ -1504,11 +1506,13 @@ __device__ __forceinline__ double refl_u(const double* R, int m, int i, int j) {
   return ok ? R[riptrm_eig::refl_col(m, i) - i - 1 + j] : 0.0;
 }
 
-// G of block blockIdx.x (reflectors b RB .. b RB + RB - 1; absent ones 0) of slot k0 + blockIdx.y into
-// the slot at goff + b RB^2 (row-major RB x RB, symmetric; the diagonal unused)
+// T of block blockIdx.x (reflectors b RB .. b RB + RB - 1; absent ones tau 0) of slot k0 + blockIdx.y into
+// the slot at goff + b RB^2 (row-major RB x RB, zero below the diagonal): G's upper triangle from 256
+// threads, then thread a < RB forms row a of T (its own earlier entries and G only: no barrier per column)
 __global__ void __launch_bounds__(256) k_refl_gram(double* base, int64_t sd, int k0, int m, int64_t r_off, int64_t goff) {
   constexpr int NP = RB * (RB - 1) / 2;
   __shared__ double part[4][NP];
+  __shared__ double gs[RB][RB];
   double* sb = base + (int64_t)(k0 + blockIdx.y) * sd;
   const double* R = sb + r_off;
   const int b = blockIdx.x, i0 = b * RB, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -1537,113 +1541,147 @@ __global__ void __launch_bounds__(256) k_refl_gram(double* base, int64_t sd, int
       x -= RB - 1 - a;
       ++a;
     }
-    const int c = a + 1 + x;
-    const double g = (part[0][tid] + part[1][tid]) + (part[2][tid] + part[3][tid]);
-    double* G = sb + goff + (int64_t)b * RB * RB;
-    G[a * RB + c] = g;
-    G[c * RB + a] = g;
+    gs[a][a + 1 + x] = (part[0][tid] + part[1][tid]) + (part[2][tid] + part[3][tid]);
+  }
+  __syncthreads();
+  if (tid < RB) {
+    const int nt = riptrm_eig::refl_tau(m);
+    double tr[RB];   // row tid of T
+#pragma unroll
+    for (int c = 0; c < RB; ++c) {
+      const double tc = i0 + c < m - 1 ? R[nt + i0 + c] : 0.0;
+      double x = c == tid ? tc : 0.0;
+      if (tid < c) {
+        double z = 0.0;
+#pragma unroll
+        for (int l = 0; l < c; ++l)
+          if (l >= tid) z += tr[l] * gs[l][c];
+        x = -tc * z;
+      }
+      tr[c] = x;
+    }
+    double* T = sb + goff + (int64_t)b * RB * RB + tid * RB;
+#pragma unroll
+    for (int c = 0; c < RB; ++c) T[c] = tr[c];
   }
 }
 
 // v <- H^T v (backward = 0: H_{m-2} ... H_0 v) or H v (backward = 1) for orders up to 1024 on one
 // 512-thread workgroup (elements j = t and t + 512 on thread t), RB reflections per round: the RB dot
-// products (one reduce-scatter per wave, eight partials per value in a fixed order), wave 0 solves for
-// c (lane a holds s_a, tau_a and row a of G; one readlane broadcast per reflection), every thread subtracts its sums of
-// c_a u_a[j].  The next round's reflector entries, Gram block and tau are loaded during the current
-// one (unconditional loads of clamped addresses, masked at use: a load under a condition made the
-// compiler wait for every outstanding load, the prefetch included, and 1024 threads left too few
-// registers to hold it: 5.8 us per round, OUT=r6tri15); thread t < RB^2 loads one Gram entry, the
-// next RB threads one tau each, staged through LDS at the round's barrier.
+// products s = U^T v (one reduce-scatter per wave, eight partials per value summed in a fixed order),
+// then every wave forms c = T^T s (T s backward) itself -- lane a < 16 one row, the s_b and then the c_a
+// broadcast by readlane -- and subtracts its sums of c_a u_a[j]: one barrier per round (the partials and
+// T double-buffered by round parity, so a wave one round ahead cannot overwrite what a slower one still
+// reads).  The next round's reflector entries and T block are loaded during the current one into the
+// other of two register sets (the round loop unrolled twice, no copies), unconditionally (a load under a
+// condition made the compiler wait for every outstanding load, the prefetch included).
+// Instruction issue, not memory, bounds the round (OUT=r6refl: 612 VALU + 325 SALU per wave per round,
+// 8.1k of 10k cycles before the first barrier, with wave 0's sequential 16-step solve 1.7k more): the
+// address of u_i[j] is the wave-uniform start of reflector i (a buffer load's soffset) plus a per-thread
+// byte offset fixed for the whole launch (j clamped into 1 .. m - 1, so every load stays inside the
+// reflector triangle), no vector instruction per load; the masks (j > i, j < m) are applied only by
+// the one or two waves whose element range straddles the round's reflectors or the order, and a wave
+// whose elements all lie at or above the block (or past m) skips its dot products and update.
+// Measured (OUT=r6chk3/r6chk4/r6help, m = 999): 255 -> 208 us per application; the first phase still
+// 5.8k cycles per round and insensitive to bytes and to where they come from -- reading only live lines
+// (no change) and 1, 2 or 4 L2-prefetch workgroups on workgroup 0's XCD (no change) -- so the floor is
+// the CU's own vector-memory return path (32 x 512 B per wave per round) and the reduction's issue.
 constexpr int RBT = 512;
 __global__ void __launch_bounds__(RBT) k_refl_blk(double* base, int64_t sd, int k0, int m, int64_t r_off, int64_t goff,
                                                   int64_t voff, int64_t ooff, int backward, long long* stamps) {
   // stamps (RIPTRM_TRI_STAMPS=3, slot 0, thread 0): clock64 cycles summed over the rounds in [0] the
-  // operands' arrival + the dot products to the first barrier, [1] wave 0's solve to the second, [2] the update
+  // operands' arrival + the dot products to the barrier, [1] c, [2] the update
   constexpr int NW = RBT / 64;
-  __shared__ double part[NW][RB];
-  __shared__ double cs[RB];
-  __shared__ double gl[RB * RB + RB];   // the round's Gram block, then its tau
+  __shared__ double part[2][NW][RB];
+  __shared__ double gl[2][RB * RB];   // the round's T (forward: gl[b RB + a] = T_ba; backward T_ab)
   double* sb = base + (int64_t)(k0 + blockIdx.y) * sd;
   const double* R = sb + r_off;
   const double* Gall = sb + goff;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  const int nt = riptrm_eig::refl_tau(m), nb = refl_blocks(m);
+  const int wu = __builtin_amdgcn_readfirstlane(w);
+  const int nb = refl_blocks(m);
   double v[2];
+  unsigned jb[2];   // bytes from u_i[0]'s position to element j (clamped into 1 .. m - 1)
 #pragma unroll
-  for (int e = 0; e < 2; ++e) v[e] = t + RBT * e < m ? sb[voff + t + RBT * e] : 0.0;
-  double un[2][RB], gn;
-  unsigned okn[2];
-  bool gok;
-  auto load = [&](int bi) {
+  for (int e = 0; e < 2; ++e) {
+    const int j = t + RBT * e;
+    v[e] = j < m ? sb[voff + j] : 0.0;
+    jb[e] = (unsigned)(j < 1 ? 1 : (j > m - 1 ? m - 1 : j)) * 8u;
+  }
+  // buffer loads: R - 1 as the base, the reflector's start (uniform) as soffset, jb as voffset
+  const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(R - 1), (short)0, 0x7fffffff, 0x00020000);
+  const int tg = t < RB * RB ? t : 0, tl = backward ? (tg & (RB - 1)) * RB + (tg >> 4) : tg;
+  auto load = [&](int bi, double (&un)[2][RB], double& gn) {
     int b = backward ? nb - 1 - bi : bi;
     b = b < 0 ? 0 : (b >= nb ? nb - 1 : b);
+    // elements at or above the block's first reflector all read its first entry's position (one line
+    // per wave, not the previous reflectors' tails: half the bytes of a full-width read)
+    const unsigned lo = (unsigned)(b * RB + 1) * 8u;
+    const unsigned jv[2] = {jb[0] > lo ? jb[0] : lo, jb[1] > lo ? jb[1] : lo};
 #pragma unroll
-    for (int e = 0; e < 2; ++e) {
-      const int j = t + RBT * e;
-      okn[e] = 0;
+    for (int a = 0; a < RB; ++a) {
+      // (reflectors past m - 2 reread m - 2's entries; their T rows and columns are 0)
+      const int i = min(b * RB + a, m - 2), d = i * (m - 2) - (i * (i - 1) >> 1);   // refl_col(m, i) - i
 #pragma unroll
-      for (int a = 0; a < RB; ++a) {
-        const int i = b * RB + a;
-        const bool live = bi < nb && i < m - 1 && j > i && j < m;
-        un[e][a] = R[live ? riptrm_eig::refl_col(m, i) - i - 1 + j : nt];
-        okn[e] |= (unsigned)live << a;
-      }
+      for (int e = 0; e < 2; ++e)
+        un[e][a] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rsrc, (int)jv[e], d * 8, 0));
     }
-    const int ia = b * RB + (t - RB * RB);
-    const bool isg = t < RB * RB, ist = !isg && t < RB * RB + RB && ia < m - 1;
-    gok = bi < nb && (isg || ist);
-    gn = isg ? Gall[(int64_t)b * RB * RB + t] : R[ist ? nt + ia : nt];
+    gn = Gall[(int64_t)b * RB * RB + tg];
   };
-  load(0);
   long long* stp = (stamps && blockIdx.y == 0 && threadIdx.x == 0) ? stamps : nullptr;
   long long s0 = 0, s1 = 0, s2 = 0, tq = stp ? clock64() : 0;
-  for (int bi = 0; bi < nb; ++bi) {
-    double u[2][RB];
+  auto round = [&](int bi, double (&u)[2][RB], double g, double (&un)[2][RB], double& gn) {
+    const int b = backward ? nb - 1 - bi : bi, i0 = b * RB, p = bi & 1;
+    bool use[2];
 #pragma unroll
-    for (int e = 0; e < 2; ++e)
+    for (int e = 0; e < 2; ++e) {
+      const int jmin = 64 * wu + RBT * e, jmax = jmin + 63;   // (uniform)
+      use[e] = jmax > i0 && jmin < m;
+      if (use[e] && (jmin <= i0 + RB - 1 || jmax >= m)) {
+        const int j = t + RBT * e;
 #pragma unroll
-      for (int a = 0; a < RB; ++a) u[e][a] = (okn[e] >> a) & 1u ? un[e][a] : 0.0;
-    const double gc = gok ? gn : 0.0;
-    const int b = backward ? nb - 1 - bi : bi, i0 = b * RB;
-    (void)i0;
-    load(bi + 1);
+        for (int a = 0; a < RB; ++a) u[e][a] = (j > i0 + a && j < m) ? u[e][a] : 0.0;
+      }
+    }
+    if (t < RB * RB) gl[p][tl] = g;
+    load(bi + 1, un, gn);
     {
       static_assert(RB == 16, "k_refl_blk: one reduce-scatter of sixteen sums");
       double pr[RB];
+      if (use[0] && use[1]) {
 #pragma unroll
-      for (int a = 0; a < RB; ++a) pr[a] = u[0][a] * v[0] + u[1][a] * v[1];
+        for (int a = 0; a < RB; ++a) pr[a] = u[0][a] * v[0] + u[1][a] * v[1];
+      } else if (use[0]) {
+#pragma unroll
+        for (int a = 0; a < RB; ++a) pr[a] = u[0][a] * v[0];
+      } else if (use[1]) {
+#pragma unroll
+        for (int a = 0; a < RB; ++a) pr[a] = u[1][a] * v[1];
+      } else {
+#pragma unroll
+        for (int a = 0; a < RB; ++a) pr[a] = 0.0;
+      }
       const double x = riptrm_wave::wave_sum16(pr);
-      if ((lane & 3) == 0) part[w][riptrm_wave::wave_sum16_index(lane)] = x;
+      if ((lane & 3) == 0) part[p][w][riptrm_wave::wave_sum16_index(lane)] = x;
     }
-    if (t < RB * RB + RB) gl[t] = gc;
     bar_lds();   // (not __syncthreads(): its vmcnt(0) would wait for the next round's prefetch)
     if (stp) {
       const long long t1 = clock64();
       s0 += t1 - tq;
       tq = t1;
     }
-    if (w == 0) {
-      // lane a < RB: s_a, tau_a, G row a; the reflections in application order
-      const int a = lane < RB ? lane : 0;
+    double cv[RB];
+    {
+      const int a = lane & (RB - 1);
       double sa = 0.0;
 #pragma unroll
-      for (int q = 0; q < NW; ++q) sa += part[q][a];
-      const double ta = lane < RB ? gl[RB * RB + a] : 0.0;
-      double g[RB];
+      for (int q = 0; q < NW; ++q) sa += part[p][q][a];
+      double ca = 0.0;
 #pragma unroll
-      for (int c = 0; c < RB; ++c) g[c] = gl[a * RB + c];
-      double cmine = 0.0;
+      for (int c = 0; c < RB; ++c) ca += gl[p][c * RB + a] * riptrm_wave::read_lane(sa, c);
 #pragma unroll
-      for (int s = 0; s < RB; ++s) {
-        const int at = backward ? RB - 1 - s : s;   // (static per unrolled step and direction)
-        const double cl = ta * sa;                   // c of lane at, once lane at's s is final
-        const double c = riptrm_wave::read_lane(cl, at);
-        if (lane == at) cmine = c;
-        sa -= (backward ? g[RB - 1 - s] : g[s]) * c;
-      }
-      if (lane < RB) cs[lane] = cmine;
+      for (int c = 0; c < RB; ++c) cv[c] = riptrm_wave::read_lane(ca, c);
     }
-    bar_lds();
     if (stp) {
       const long long t1 = clock64();
       s1 += t1 - tq;
@@ -1651,16 +1689,24 @@ __global__ void __launch_bounds__(RBT) k_refl_blk(double* base, int64_t sd, int 
     }
 #pragma unroll
     for (int e = 0; e < 2; ++e) {
-      double dv = 0.0;
+      if (use[e]) {
+        double dv = 0.0;
 #pragma unroll
-      for (int a = 0; a < RB; ++a) dv += cs[a] * u[e][a];
-      v[e] -= dv;
+        for (int a = 0; a < RB; ++a) dv += cv[a] * u[e][a];
+        v[e] -= dv;
+      }
     }
     if (stp) {
       const long long t1 = clock64();
       s2 += t1 - tq;
       tq = t1;
     }
+  };
+  double ua[2][RB], ub[2][RB], ga, gb;
+  load(0, ua, ga);
+  for (int bi = 0; bi < nb; bi += 2) {
+    round(bi, ua, ga, ub, gb);
+    if (bi + 1 < nb) round(bi + 1, ub, gb, ua, ga);
   }
 #pragma unroll
   for (int e = 0; e < 2; ++e)

@@ -1784,8 +1784,8 @@ static int tri_tridiag(riptrm_ctx* c, const Bat& B, int cnt, int m, int64_t aoff
 }
 
 // v <- H^T v / H v for the pass's slots (the tridiagonal path's reflectors): one 512-thread workgroup per
-// slot, 16 reflections per round (k_refl_blk; the rounds' Gram blocks from k_refl_gram in the slot's
-// matrix area, dead once T is formed: tri_finish makes them); RIPTRM_TRI_REFL=s one reflection per
+// slot, 16 reflections per round (k_refl_blk; the rounds' compact-WY T blocks from k_refl_gram in the
+// slot's matrix area, dead once the tridiagonal T is formed: tri_finish makes them); RIPTRM_TRI_REFL=s one reflection per
 // round (k_refl_wg), =w one wave with the vector in registers (k_refl_big) (A/B)
 static int tri_refl(riptrm_ctx* c, const Bat& B, int cnt, int m, int64_t voff, int64_t ooff, int backward) {
   const dim3 grid(1, cnt);
