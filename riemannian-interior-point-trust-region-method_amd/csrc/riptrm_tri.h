@@ -1586,12 +1586,14 @@ __global__ void __launch_bounds__(256) k_refl_gram(double* base, int64_t sd, int
 // 5.8k cycles per round and insensitive to bytes and to where they come from -- reading only live lines
 // (no change) and 1, 2 or 4 L2-prefetch workgroups on workgroup 0's XCD (no change) -- so the floor is
 // the CU's own vector-memory return path (32 x 512 B per wave per round) and the reduction's issue.
-constexpr int RBT = 512;
-__global__ void __launch_bounds__(RBT) k_refl_blk(double* base, int64_t sd, int k0, int m, int64_t r_off, int64_t goff,
+// E elements per thread (1024 / E threads): E = 2 the default, E = 1 four waves per SIMD (A/B,
+// RIPTRM_TRI_REFL_E=1)
+template <int E>
+__global__ void __launch_bounds__(1024 / E) k_refl_blk(double* base, int64_t sd, int k0, int m, int64_t r_off, int64_t goff,
                                                   int64_t voff, int64_t ooff, int backward, long long* stamps) {
   // stamps (RIPTRM_TRI_STAMPS=3, slot 0, thread 0): clock64 cycles summed over the rounds in [0] the
   // operands' arrival + the dot products to the barrier, [1] c, [2] the update
-  constexpr int NW = RBT / 64;
+  constexpr int NT = 1024 / E, NW = NT / 64;
   __shared__ double part[2][NW][RB];
   __shared__ double gl[2][RB * RB];   // the round's T (forward: gl[b RB + a] = T_ba; backward T_ab)
   double* sb = base + (int64_t)(k0 + blockIdx.y) * sd;
@@ -1600,45 +1602,47 @@ __global__ void __launch_bounds__(RBT) k_refl_blk(double* base, int64_t sd, int 
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int wu = __builtin_amdgcn_readfirstlane(w);
   const int nb = refl_blocks(m);
-  double v[2];
-  unsigned jb[2];   // bytes from u_i[0]'s position to element j (clamped into 1 .. m - 1)
+  double v[E];
+  unsigned jb[E];   // bytes from u_i[0]'s position to element j (clamped into 1 .. m - 1)
 #pragma unroll
-  for (int e = 0; e < 2; ++e) {
-    const int j = t + RBT * e;
+  for (int e = 0; e < E; ++e) {
+    const int j = t + NT * e;
     v[e] = j < m ? sb[voff + j] : 0.0;
     jb[e] = (unsigned)(j < 1 ? 1 : (j > m - 1 ? m - 1 : j)) * 8u;
   }
   // buffer loads: R - 1 as the base, the reflector's start (uniform) as soffset, jb as voffset
   const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(R - 1), (short)0, 0x7fffffff, 0x00020000);
   const int tg = t < RB * RB ? t : 0, tl = backward ? (tg & (RB - 1)) * RB + (tg >> 4) : tg;
-  auto load = [&](int bi, double (&un)[2][RB], double& gn) {
+  auto load = [&](int bi, double (&un)[E][RB], double& gn) {
     int b = backward ? nb - 1 - bi : bi;
     b = b < 0 ? 0 : (b >= nb ? nb - 1 : b);
     // elements at or above the block's first reflector all read its first entry's position (one line
     // per wave, not the previous reflectors' tails: half the bytes of a full-width read)
     const unsigned lo = (unsigned)(b * RB + 1) * 8u;
-    const unsigned jv[2] = {jb[0] > lo ? jb[0] : lo, jb[1] > lo ? jb[1] : lo};
+    unsigned jv[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) jv[e] = jb[e] > lo ? jb[e] : lo;
 #pragma unroll
     for (int a = 0; a < RB; ++a) {
       // (reflectors past m - 2 reread m - 2's entries; their T rows and columns are 0)
       const int i = min(b * RB + a, m - 2), d = i * (m - 2) - (i * (i - 1) >> 1);   // refl_col(m, i) - i
 #pragma unroll
-      for (int e = 0; e < 2; ++e)
+      for (int e = 0; e < E; ++e)
         un[e][a] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rsrc, (int)jv[e], d * 8, 0));
     }
     gn = Gall[(int64_t)b * RB * RB + tg];
   };
   long long* stp = (stamps && blockIdx.y == 0 && threadIdx.x == 0) ? stamps : nullptr;
   long long s0 = 0, s1 = 0, s2 = 0, tq = stp ? clock64() : 0;
-  auto round = [&](int bi, double (&u)[2][RB], double g, double (&un)[2][RB], double& gn) {
+  auto round = [&](int bi, double (&u)[E][RB], double g, double (&un)[E][RB], double& gn) {
     const int b = backward ? nb - 1 - bi : bi, i0 = b * RB, p = bi & 1;
-    bool use[2];
+    bool use[E];
 #pragma unroll
-    for (int e = 0; e < 2; ++e) {
-      const int jmin = 64 * wu + RBT * e, jmax = jmin + 63;   // (uniform)
+    for (int e = 0; e < E; ++e) {
+      const int jmin = 64 * wu + NT * e, jmax = jmin + 63;   // (uniform)
       use[e] = jmax > i0 && jmin < m;
       if (use[e] && (jmin <= i0 + RB - 1 || jmax >= m)) {
-        const int j = t + RBT * e;
+        const int j = t + NT * e;
 #pragma unroll
         for (int a = 0; a < RB; ++a) u[e][a] = (j > i0 + a && j < m) ? u[e][a] : 0.0;
       }
@@ -1648,7 +1652,10 @@ __global__ void __launch_bounds__(RBT) k_refl_blk(double* base, int64_t sd, int 
     {
       static_assert(RB == 16, "k_refl_blk: one reduce-scatter of sixteen sums");
       double pr[RB];
-      if (use[0] && use[1]) {
+      if constexpr (E == 1) {
+#pragma unroll
+        for (int a = 0; a < RB; ++a) pr[a] = use[0] ? u[0][a] * v[0] : 0.0;
+      } else if (use[0] && use[1]) {
 #pragma unroll
         for (int a = 0; a < RB; ++a) pr[a] = u[0][a] * v[0] + u[1][a] * v[1];
       } else if (use[0]) {
@@ -1688,7 +1695,7 @@ __global__ void __launch_bounds__(RBT) k_refl_blk(double* base, int64_t sd, int 
       tq = t1;
     }
 #pragma unroll
-    for (int e = 0; e < 2; ++e) {
+    for (int e = 0; e < E; ++e) {
       if (use[e]) {
         double dv = 0.0;
 #pragma unroll
@@ -1702,15 +1709,15 @@ __global__ void __launch_bounds__(RBT) k_refl_blk(double* base, int64_t sd, int 
       tq = t1;
     }
   };
-  double ua[2][RB], ub[2][RB], ga, gb;
+  double ua[E][RB], ub[E][RB], ga, gb;
   load(0, ua, ga);
   for (int bi = 0; bi < nb; bi += 2) {
     round(bi, ua, ga, ub, gb);
     if (bi + 1 < nb) round(bi + 1, ub, gb, ua, ga);
   }
 #pragma unroll
-  for (int e = 0; e < 2; ++e)
-    if (t + RBT * e < m) sb[ooff + t + RBT * e] = v[e];
+  for (int e = 0; e < E; ++e)
+    if (t + NT * e < m) sb[ooff + t + NT * e] = v[e];
   if (stp) {
     stp[0] = s0;
     stp[1] = s1;

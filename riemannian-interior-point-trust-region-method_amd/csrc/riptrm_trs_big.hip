@@ -1795,8 +1795,12 @@ static int tri_refl(riptrm_ctx* c, const Bat& B, int cnt, int m, int64_t voff, i
       HIPCHK(c, hipMalloc(&stamps, 4 * sizeof(long long)));
       HIPCHK(c, hipMemsetAsync(stamps, 0, 4 * sizeof(long long), c->stream));
     }
-    hipLaunchKernelGGL(riptrm_tri::k_refl_blk, grid, dim3(riptrm_tri::RBT), 0, c->stream, B.base, B.sd, 0, m, off_refl(B.N),
-                       (int64_t)0, voff, ooff, backward, stamps);
+    if (getenv_is("RIPTRM_TRI_REFL_E", '1'))
+      hipLaunchKernelGGL(riptrm_tri::k_refl_blk<1>, grid, dim3(1024), 0, c->stream, B.base, B.sd, 0, m, off_refl(B.N),
+                         (int64_t)0, voff, ooff, backward, stamps);
+    else
+      hipLaunchKernelGGL(riptrm_tri::k_refl_blk<2>, grid, dim3(512), 0, c->stream, B.base, B.sd, 0, m, off_refl(B.N),
+                         (int64_t)0, voff, ooff, backward, stamps);
     HIPCHK(c, hipGetLastError());
     if (stamps) {
       long long h[4];
