@@ -1507,42 +1507,54 @@ __device__ __forceinline__ double refl_u(const double* R, int m, int i, int j) {
 }
 
 // T of block blockIdx.x (reflectors b RB .. b RB + RB - 1; absent ones tau 0) of slot k0 + blockIdx.y into
-// the slot at goff + b RB^2 (row-major RB x RB, zero below the diagonal): G's upper triangle from 256
-// threads, then thread a < RB forms row a of T (its own earlier entries and G only: no barrier per column)
+// the slot at goff + b RB^2 (row-major RB x RB, zero below the diagonal): G's upper triangle by thread
+// (a, c) < 120 over chunks of 128 rows staged in LDS (coalesced: consecutive threads, consecutive rows of
+// one reflector), two accumulation chains; then thread a < RB forms row a of T (its own earlier entries
+// and G only: no barrier per column).  (Round 6 first form: 120 accumulators per thread and 120 wave
+// sums, 31.5 us per 13 x 64 blocks at order 199, 17.9 us at 999.)
 __global__ void __launch_bounds__(256) k_refl_gram(double* base, int64_t sd, int k0, int m, int64_t r_off, int64_t goff) {
-  constexpr int NP = RB * (RB - 1) / 2;
-  __shared__ double part[4][NP];
+  constexpr int NP = RB * (RB - 1) / 2, CH = 128;
+  __shared__ double us[CH][RB + 1];
   __shared__ double gs[RB][RB];
   double* sb = base + (int64_t)(k0 + blockIdx.y) * sd;
   const double* R = sb + r_off;
-  const int b = blockIdx.x, i0 = b * RB, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  double acc[NP];
-#pragma unroll
-  for (int x = 0; x < NP; ++x) acc[x] = 0.0;
-  for (int j = i0 + 1 + tid; j < m; j += 256) {
-    double u[RB];
-#pragma unroll
-    for (int a = 0; a < RB; ++a) u[a] = refl_u(R, m, i0 + a, j);
-    int x = 0;
-#pragma unroll
-    for (int a = 0; a < RB; ++a)
-#pragma unroll
-      for (int c = a + 1; c < RB; ++c) acc[x++] += u[a] * u[c];
-  }
-#pragma unroll
-  for (int x = 0; x < NP; ++x) {
-    const double t = riptrm_wave::wave_sum(acc[x]);
-    if (lane == 0) part[w][x] = t;
-  }
-  __syncthreads();
+  const int b = blockIdx.x, i0 = b * RB, tid = threadIdx.x;
+  int pa = 0, pc = 1;
   if (tid < NP) {
-    int a = 0, x = tid;
-    while (x >= RB - 1 - a) {
-      x -= RB - 1 - a;
-      ++a;
+    int x = tid;
+    while (x >= RB - 1 - pa) {
+      x -= RB - 1 - pa;
+      ++pa;
     }
-    gs[a][a + 1 + x] = (part[0][tid] + part[1][tid]) + (part[2][tid] + part[3][tid]);
+    pc = pa + 1 + x;
   }
+  double acc0 = 0.0, acc1 = 0.0;
+  for (int j0 = i0 + 1; j0 < m; j0 += CH) {
+    __syncthreads();   // (the previous chunk is consumed)
+    // all eight loads of a thread issued before any is used: clamped addresses, masked after (a load
+    // under the bound's condition is waited for one at a time)
+    double x[CH * RB / 256];
+#pragma unroll
+    for (int r = 0; r < CH * RB / 256; ++r) {
+      const int q = tid + 256 * r, a = q / CH, i = i0 + a, j = j0 + q % CH;
+      const bool ok = i < m - 1 && j > i && j < m;
+      x[r] = R[ok ? riptrm_eig::refl_col(m, i) - i - 1 + j : 0];
+    }
+#pragma unroll
+    for (int r = 0; r < CH * RB / 256; ++r) {
+      const int q = tid + 256 * r, a = q / CH, i = i0 + a, j = j0 + q % CH;
+      us[q % CH][a] = (i < m - 1 && j > i && j < m) ? x[r] : 0.0;
+    }
+    __syncthreads();
+    if (tid < NP) {
+#pragma unroll 8
+      for (int jj = 0; jj < CH; jj += 2) {
+        acc0 += us[jj][pa] * us[jj][pc];
+        acc1 += us[jj + 1][pa] * us[jj + 1][pc];
+      }
+    }
+  }
+  if (tid < NP) gs[pa][pc] = acc0 + acc1;
   __syncthreads();
   if (tid < RB) {
     const int nt = riptrm_eig::refl_tau(m);
